@@ -1,0 +1,104 @@
+"""Native build: compile the gfx950 HIP kernels + C++ engine + pybind11 bindings in-tree.
+
+`python -m aios_amd._build` (or `__graft_entry__.build()`) drives hipcc directly -- no hipify,
+no torch.utils.cpp_extension -- producing `aios_amd/_engine*.so` next to the package so the
+snapshot that travels to the GPU box carries it.  Objects are cached under `build/` and
+rebuilt when a source or any header is newer.
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import os
+import shutil
+import subprocess
+import sys
+import sysconfig
+from pathlib import Path
+
+PKG = Path(__file__).resolve().parent
+ROOT = PKG.parent
+CSRC = PKG / "csrc"
+BUILD = ROOT / "build" / "native"
+ARCH = os.environ.get("AIOS_OFFLOAD_ARCH", "gfx950")
+
+
+def _hipcc() -> str:
+    for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if c and os.path.exists(c):
+            return c
+    raise RuntimeError("hipcc not found (ROCm toolchain required)")
+
+
+def ext_suffix() -> str:
+    return sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+
+
+def target_path() -> Path:
+    return PKG / ("_engine" + ext_suffix())
+
+
+def _sources():
+    srcs = sorted((CSRC / "kernels").glob("*.hip")) + [CSRC / "engine.hip", CSRC / "bindings.cpp"]
+    return srcs
+
+
+def _headers():
+    return list(CSRC.rglob("*.h"))
+
+
+def _flags():
+    import pybind11
+
+    return [
+        f"--offload-arch={ARCH}",
+        "-O3",
+        "-std=c++17",
+        "-fPIC",
+        "-fvisibility=hidden",
+        "-Wno-unused-result",
+        "-Wno-pass-failed",
+        f"-I{CSRC}",
+        f"-I{pybind11.get_include()}",
+        f"-I{sysconfig.get_paths()['include']}",
+    ]
+
+
+def _compile(src: Path, flags, hipcc) -> Path:
+    obj = BUILD / (src.stem + ".o")
+    newest_dep = max([src.stat().st_mtime] + [h.stat().st_mtime for h in _headers()])
+    if obj.exists() and obj.stat().st_mtime >= newest_dep:
+        return obj
+    cmd = [hipcc, *flags, "-c", str(src), "-o", str(obj)]
+    if src.suffix == ".cpp":
+        cmd = [hipcc, *flags, "-x", "hip", "-c", str(src), "-o", str(obj)]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"hipcc failed for {src.name}:\n{r.stderr[-6000:]}")
+    return obj
+
+
+def build(verbose: bool = True, jobs: int | None = None) -> Path:
+    BUILD.mkdir(parents=True, exist_ok=True)
+    hipcc = _hipcc()
+    flags = _flags()
+    srcs = _sources()
+    jobs = jobs or min(len(srcs), max(1, (os.cpu_count() or 4)), 16)
+    with cf.ThreadPoolExecutor(jobs) as ex:
+        objs = list(ex.map(lambda s: _compile(s, flags, hipcc), srcs))
+    out = target_path()
+    newest = max(o.stat().st_mtime for o in objs)
+    if not out.exists() or out.stat().st_mtime < newest:
+        tmp = out.with_suffix(".tmp.so")
+        cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(tmp), *map(str, objs)]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed:\n{r.stderr[-6000:]}")
+        os.replace(tmp, out)
+    if verbose:
+        print(f"[aios_amd] native engine: {out} ({out.stat().st_size / 1e6:.1f} MB, {ARCH})")
+    return out
+
+
+if __name__ == "__main__":
+    build()
+    sys.exit(0)

@@ -1,0 +1,273 @@
+// pybind11 bindings: the Engine (runtime) plus raw-pointer op entry points used by the kernel
+// numerics tests (torch tensors pass data_ptr() and torch.cuda.current_stream().cuda_stream).
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <cstring>
+
+#include "engine.h"
+#include "ops.h"
+
+namespace py = pybind11;
+using namespace aios;
+
+namespace {
+
+hipStream_t S(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
+
+// Owning device matrix in the repacked layout (tests / tools)
+struct PyQMatrix {
+  QWeight w{};
+  void* buf = nullptr;
+  size_t bytes = 0;
+  PyQMatrix(int qt, int rows, int cols, py::buffer raw) {
+    py::buffer_info bi = raw.request();
+    const size_t nbytes = (size_t)bi.size * bi.itemsize;
+    // engine-less allocation mirroring Engine::alloc_qmat
+    EngineConfig cfg;
+    cfg.n_layers = 0;
+    (void)cfg;
+    const int be = (qt == QT_Q4_K || qt == QT_Q5_K || qt == QT_Q6_K) ? 256 : ((qt == QT_F16 || qt == QT_BF16) ? 1 : 32);
+    const size_t nb = (size_t)rows * (cols / be);
+    size_t s0 = 0, s1 = 0, s2 = 0, s3 = 0;
+    switch (qt) {
+      case QT_Q4_K: s0 = nb * 128; s1 = nb * 16; break;
+      case QT_Q5_K: s0 = nb * 128; s1 = nb * 16; s2 = nb * 32; break;
+      case QT_Q6_K: s0 = nb * 128; s1 = nb * 64; s2 = nb * 16; s3 = nb * 2; break;
+      case QT_Q4_0: s0 = nb * 16; s1 = nb * 2; break;
+      case QT_Q8_0: s0 = nb * 32; s1 = nb * 2; break;
+      case QT_F16:
+      case QT_BF16: s0 = nb * 2; break;
+      default: throw std::runtime_error("QMatrix: unsupported type");
+    }
+    auto al = [](size_t x) { return (x + 255) / 256 * 256; };
+    const size_t o1 = al(s0), o2 = o1 + al(s1), o3 = o2 + al(s2);
+    bytes = o3 + al(s3) + 64;
+    HIP_CHECK(hipMalloc(&buf, bytes));
+    uint8_t* base = (uint8_t*)buf;
+    w.qtype = qt;
+    w.rows = rows;
+    w.cols = cols;
+    w.p0 = base;
+    w.p1 = s1 ? base + o1 : nullptr;
+    w.p2 = s2 ? base + o2 : nullptr;
+    w.p3 = s3 ? base + o3 : nullptr;
+    void* staging = nullptr;
+    HIP_CHECK(hipMalloc(&staging, nbytes));
+    HIP_CHECK(hipMemcpy(staging, bi.ptr, nbytes, hipMemcpyHostToDevice));
+    if (qt == QT_F16 || qt == QT_BF16) HIP_CHECK(hipMemcpy(buf, staging, nbytes, hipMemcpyDeviceToDevice));
+    else launch_repack(qt, staging, nb, w, nullptr);
+    HIP_CHECK(hipDeviceSynchronize());
+    HIP_CHECK(hipFree(staging));
+  }
+  ~PyQMatrix() {
+    if (buf) hipFree(buf);
+  }
+};
+
+}  // namespace
+
+PYBIND11_MODULE(_engine, m) {
+  m.doc() = "aiOS-MI355X native inference engine (gfx950 HIP kernels + C++ runtime)";
+  m.attr("QT_F32") = (int)QT_F32;
+  m.attr("QT_F16") = (int)QT_F16;
+  m.attr("QT_BF16") = (int)QT_BF16;
+  m.attr("QT_Q4_0") = (int)QT_Q4_0;
+  m.attr("QT_Q8_0") = (int)QT_Q8_0;
+  m.attr("QT_Q4_K") = (int)QT_Q4_K;
+  m.attr("QT_Q5_K") = (int)QT_Q5_K;
+  m.attr("QT_Q6_K") = (int)QT_Q6_K;
+  m.attr("EPI_STORE") = (int)EPI_STORE;
+  m.attr("EPI_RESID") = (int)EPI_RESID;
+  m.attr("EPI_SWIGLU") = (int)EPI_SWIGLU;
+  m.attr("EPI_QKV") = (int)EPI_QKV;
+  m.attr("ATTN_CHUNK") = (int)ATTN_CHUNK;
+
+  m.def("device_count", []() {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+  });
+  m.def("device_name", [](int dev) {
+    hipDeviceProp_t p;
+    HIP_CHECK(hipGetDeviceProperties(&p, dev));
+    return std::string(p.name) + " / " + p.gcnArchName;
+  });
+  m.def("synchronize", []() { HIP_CHECK(hipDeviceSynchronize()); });
+
+  py::class_<EngineConfig>(m, "EngineConfig")
+      .def(py::init<>())
+      .def_readwrite("name", &EngineConfig::name)
+      .def_readwrite("vocab_size", &EngineConfig::vocab_size)
+      .def_readwrite("d_model", &EngineConfig::d_model)
+      .def_readwrite("n_layers", &EngineConfig::n_layers)
+      .def_readwrite("n_heads", &EngineConfig::n_heads)
+      .def_readwrite("n_kv_heads", &EngineConfig::n_kv_heads)
+      .def_readwrite("head_dim", &EngineConfig::head_dim)
+      .def_readwrite("d_ff", &EngineConfig::d_ff)
+      .def_readwrite("rope_theta", &EngineConfig::rope_theta)
+      .def_readwrite("rope_neox", &EngineConfig::rope_neox)
+      .def_readwrite("norm_eps", &EngineConfig::norm_eps)
+      .def_readwrite("max_ctx", &EngineConfig::max_ctx)
+      .def_readwrite("max_slots", &EngineConfig::max_slots)
+      .def_readwrite("max_batch", &EngineConfig::max_batch)
+      .def_readwrite("tie_embeddings", &EngineConfig::tie_embeddings)
+      .def_readwrite("qk_norm", &EngineConfig::qk_norm)
+      .def_readwrite("qkv_bias", &EngineConfig::qkv_bias)
+      .def_readwrite("tp_rank", &EngineConfig::tp_rank)
+      .def_readwrite("tp_size", &EngineConfig::tp_size)
+      .def_readwrite("device", &EngineConfig::device);
+
+  py::class_<Engine>(m, "Engine")
+      .def(py::init<const EngineConfig&>())
+      .def("set_tensor",
+           [](Engine& e, const std::string& name, int qt, int rows, int cols, py::buffer raw) {
+             py::buffer_info bi = raw.request();
+             const size_t nbytes = (size_t)bi.size * bi.itemsize;
+             py::gil_scoped_release nogil;
+             e.set_tensor(name, qt, rows, cols, bi.ptr, nbytes);
+           })
+      .def("init_random", &Engine::init_random, py::call_guard<py::gil_scoped_release>())
+      .def("finalize", &Engine::finalize, py::call_guard<py::gil_scoped_release>())
+      .def("missing_tensors", &Engine::missing_tensors)
+      .def("weight_type_summary", &Engine::weight_type_summary)
+      .def_property_readonly("ready", &Engine::ready)
+      .def_property_readonly("weight_bytes", &Engine::weight_bytes)
+      .def_property_readonly("kv_bytes", &Engine::kv_bytes)
+      .def_property_readonly("workspace_bytes", &Engine::workspace_bytes)
+      .def_property_readonly("config", &Engine::config)
+      .def("prefill",
+           [](Engine& e, int slot, const std::vector<int>& tokens, int start_pos, bool want_logits) {
+             std::vector<float> out;
+             {
+               py::gil_scoped_release nogil;
+               out = e.prefill(slot, tokens, start_pos, want_logits);
+             }
+             return py::array_t<float>(out.size(), out.data());
+           },
+           py::arg("slot"), py::arg("tokens"), py::arg("start_pos") = 0, py::arg("want_logits") = true)
+      .def("decode", &Engine::decode, py::arg("slots"), py::arg("tokens"), py::arg("pos"),
+           py::arg("temperature") = std::vector<float>{}, py::arg("top_k") = std::vector<int>{},
+           py::arg("seed") = 0, py::arg("mask") = std::vector<uint8_t>{}, py::call_guard<py::gil_scoped_release>())
+      .def("last_logits",
+           [](Engine& e, int B) {
+             std::vector<float> v;
+             {
+               py::gil_scoped_release nogil;
+               v = e.last_logits(B);
+             }
+             py::array_t<float> a({(py::ssize_t)B, (py::ssize_t)e.config().vocab_size});
+             std::memcpy(a.mutable_data(), v.data(), v.size() * 4);
+             return a;
+           })
+      .def("decode_loop_prepare", &Engine::decode_loop_prepare, py::call_guard<py::gil_scoped_release>())
+      .def("decode_loop_run", &Engine::decode_loop_run, py::arg("B"), py::arg("n_steps"), py::arg("use_graph") = true,
+           py::call_guard<py::gil_scoped_release>())
+      .def("decode_loop_history", &Engine::decode_loop_history, py::call_guard<py::gil_scoped_release>())
+      .def("synchronize", &Engine::synchronize, py::call_guard<py::gil_scoped_release>())
+      .def("reset_graphs", &Engine::reset_graphs)
+      .def("copy_slot", &Engine::copy_slot, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("stream", &Engine::stream_handle)
+      .def_property_readonly("k_cache_ptr", &Engine::kv_cache_k)
+      .def_property_readonly("v_cache_ptr", &Engine::kv_cache_v)
+      .def("set_allreduce_ptr", [](Engine& e, uintptr_t fn, uintptr_t ctx) {
+        e.set_allreduce(reinterpret_cast<AllReduceFn>(fn), reinterpret_cast<void*>(ctx));
+      });
+
+  // ------------------------------------------------------------------ raw ops (tests / tools)
+  py::class_<PyQMatrix>(m, "QMatrix")
+      .def(py::init<int, int, int, py::buffer>())
+      .def_property_readonly("qtype", [](const PyQMatrix& q) { return q.w.qtype; })
+      .def_property_readonly("rows", [](const PyQMatrix& q) { return q.w.rows; })
+      .def_property_readonly("cols", [](const PyQMatrix& q) { return q.w.cols; })
+      .def_property_readonly("nbytes", [](const PyQMatrix& q) { return q.bytes; })
+      .def("dequant_bf16", [](PyQMatrix& q, uintptr_t out, uintptr_t st) { launch_dequant_bf16(q.w, (void*)out, S(st)); })
+      .def("get_rows", [](PyQMatrix& q, uintptr_t rows, int n, uintptr_t out, int ldo, uintptr_t st) {
+        launch_get_rows(q.w, (const int*)rows, n, (float*)out, ldo, 1.f, S(st));
+      })
+      .def("fill_random", [](PyQMatrix& q, uint64_t seed, float amp) {
+        fill_random_weight(q.w, seed, amp, nullptr);
+        HIP_CHECK(hipDeviceSynchronize());
+      });
+
+  m.def("gemv",
+        [](std::vector<PyQMatrix*> segs, int B, uintptr_t x, int ldx, uintptr_t norm_w, float eps, uintptr_t y,
+           int ldy, int epi, uintptr_t st) {
+          GemvArgs a;
+          std::memset(&a, 0, sizeof(a));
+          a.nseg = (int)segs.size();
+          int r = 0;
+          for (int s = 0; s < a.nseg; ++s) { a.seg[s] = segs[s]->w; a.seg_row0[s] = r; r += segs[s]->w.rows; }
+          a.N = r; a.K = segs[0]->w.cols; a.B = B;
+          a.x = (const float*)x; a.ldx = ldx; a.norm_w = (const float*)norm_w; a.eps = eps;
+          a.y = (float*)y; a.ldy = ldy; a.epi = epi;
+          launch_gemv(a, S(st));
+        });
+  m.def("gemv_qkv",
+        [](std::vector<PyQMatrix*> segs, int B, uintptr_t x, int ldx, uintptr_t norm_w, float eps, uintptr_t q_out,
+           uintptr_t bias, int head_dim, int n_heads, int n_kv_heads, int max_ctx, int rope_neox, float rope_base,
+           uintptr_t pos, uintptr_t slot, uintptr_t k_cache, uintptr_t v_cache, uintptr_t st) {
+          GemvArgs a;
+          std::memset(&a, 0, sizeof(a));
+          a.nseg = (int)segs.size();
+          int r = 0;
+          for (int s = 0; s < a.nseg; ++s) { a.seg[s] = segs[s]->w; a.seg_row0[s] = r; r += segs[s]->w.rows; }
+          a.N = r; a.K = segs[0]->w.cols; a.B = B;
+          a.x = (const float*)x; a.ldx = ldx; a.norm_w = (const float*)norm_w; a.eps = eps;
+          a.y = (float*)q_out; a.ldy = n_heads * head_dim; a.epi = EPI_QKV;
+          a.bias = (const float*)bias; a.head_dim = head_dim; a.q_dim = n_heads * head_dim;
+          a.kv_dim = n_kv_heads * head_dim; a.n_kv_heads = n_kv_heads; a.max_ctx = max_ctx;
+          a.rope_neox = rope_neox; a.rope_base = rope_base; a.pos = (const int*)pos; a.slot = (const int*)slot;
+          a.k_cache = (bf16_t*)k_cache; a.v_cache = (bf16_t*)v_cache;
+          launch_gemv(a, S(st));
+        });
+  m.def("attn_decode",
+        [](uintptr_t q, uintptr_t k, uintptr_t v, uintptr_t seq_len, uintptr_t slot, int B, int H, int Hkv, int hd,
+           int max_ctx, int n_chunks, float scale, uintptr_t opart, uintptr_t ml, uintptr_t out, uintptr_t st) {
+          AttnDecodeArgs a;
+          a.q = (const float*)q; a.k_cache = (const bf16_t*)k; a.v_cache = (const bf16_t*)v;
+          a.seq_len = (const int*)seq_len; a.slot = (const int*)slot;
+          a.B = B; a.n_heads = H; a.n_kv_heads = Hkv; a.head_dim = hd; a.max_ctx = max_ctx; a.n_chunks = n_chunks;
+          a.scale = scale; a.o_part = (float*)opart; a.ml = (float*)ml; a.out = (float*)out;
+          launch_attn_decode(a, S(st));
+        });
+  m.def("rmsnorm", [](uintptr_t x, int ldx, uintptr_t w, uintptr_t y, int ldy, int rows, int n, float eps, uintptr_t st) {
+    launch_rmsnorm((const float*)x, ldx, (const float*)w, (float*)y, ldy, rows, n, eps, S(st));
+  });
+  m.def("rmsnorm_bf16", [](uintptr_t x, int ldx, uintptr_t w, uintptr_t y, int ldy, int rows, int n, float eps, uintptr_t st) {
+    launch_rmsnorm_bf16((const float*)x, ldx, (const float*)w, (bf16_t*)y, ldy, rows, n, eps, S(st));
+  });
+  m.def("swiglu", [](uintptr_t gu, int ldg, uintptr_t out, int ldo, int rows, int n, uintptr_t st) {
+    launch_swiglu_interleaved((const float*)gu, ldg, (float*)out, ldo, rows, n, S(st));
+  });
+  m.def("qkv_post",
+        [](uintptr_t qkv, int ldqkv, int T, int H, int Hkv, int hd, uintptr_t q_norm, uintptr_t k_norm, float eps,
+           int rope_neox, float rope_base, uintptr_t pos, uintptr_t slot, uintptr_t q_out, uintptr_t k_cache,
+           uintptr_t v_cache, int max_ctx, uintptr_t st) {
+          QkvPostArgs a;
+          a.qkv = (const float*)qkv; a.ldqkv = ldqkv; a.T = T; a.n_heads = H; a.n_kv_heads = Hkv; a.head_dim = hd;
+          a.q_norm = (const float*)q_norm; a.k_norm = (const float*)k_norm; a.eps = eps; a.rope_neox = rope_neox;
+          a.rope_base = rope_base; a.pos = (const int*)pos; a.slot = (const int*)slot; a.q_out = (float*)q_out;
+          a.k_cache = (bf16_t*)k_cache; a.v_cache = (bf16_t*)v_cache; a.max_ctx = max_ctx;
+          launch_qkv_post(a, S(st));
+        });
+  m.def("sample",
+        [](uintptr_t logits, int ldl, int B, int V, uintptr_t temperature, uintptr_t top_k, uint64_t seed,
+           uintptr_t tokens, uintptr_t pos, uintptr_t mask, uintptr_t st) {
+          SampleArgs a;
+          std::memset(&a, 0, sizeof(a));
+          a.logits = (const float*)logits; a.ldl = ldl; a.B = B; a.V = V;
+          a.temperature = (const float*)temperature; a.top_k = (const int*)top_k; a.seed = seed;
+          a.tokens = (int*)tokens; a.pos = (int*)pos; a.mask = (const uint8_t*)mask;
+          launch_sample(a, S(st));
+        });
+  m.def("gemm",
+        [](uintptr_t A, int lda, PyQMatrix* w, int M, uintptr_t C, int ldc, int accumulate, uintptr_t st) {
+          GemmArgs a;
+          a.A = (const bf16_t*)A; a.lda = lda; a.w = w->w; a.M = M; a.N = w->w.rows; a.K = w->w.cols;
+          a.C = (float*)C; a.ldc = ldc; a.accumulate = accumulate;
+          launch_gemm(a, S(st));
+        });
+  m.def("gemm_supports", &gemm_supports);
+}

@@ -1,0 +1,88 @@
+// Common device/host definitions for the aiOS-MI355X inference engine (gfx950 / CDNA4).
+//
+// Everything here is written for wave64 CDNA4: lane = threadIdx.x & 63, 64-bit ballots,
+// cross-lane reductions over 64 lanes with __shfl_xor.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <hip/hip_fp16.h>
+#include <stdint.h>
+
+#include <stdexcept>
+#include <string>
+
+#define AIOS_WAVE 64
+
+#define HIP_CHECK(expr)                                                                   \
+  do {                                                                                    \
+    hipError_t _e = (expr);                                                               \
+    if (_e != hipSuccess) {                                                               \
+      throw std::runtime_error(std::string("HIP error ") + hipGetErrorString(_e) + " at " + \
+                               __FILE__ + ":" + std::to_string(__LINE__) + " : " #expr);  \
+    }                                                                                     \
+  } while (0)
+
+namespace aios {
+
+// ggml type ids (GGUF on-disk ids)
+enum QType : int {
+  QT_F32 = 0,
+  QT_F16 = 1,
+  QT_Q4_0 = 2,
+  QT_Q4_1 = 3,
+  QT_Q5_0 = 6,
+  QT_Q5_1 = 7,
+  QT_Q8_0 = 8,
+  QT_Q4_K = 12,
+  QT_Q5_K = 13,
+  QT_Q6_K = 14,
+  QT_BF16 = 30,
+};
+
+typedef uint16_t bf16_t;
+
+__device__ __forceinline__ float bf16_to_f32(uint32_t h) { return __uint_as_float(h << 16); }
+__device__ __forceinline__ uint16_t f32_to_bf16(float f) {
+  // round-to-nearest-even; NaN stays NaN
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+__device__ __forceinline__ float h2f(uint16_t h) { return __half2float(__ushort_as_half(h)); }
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Block-wide sum over blockDim.x threads (multiple of 64, <= 1024). `red` has >= 16 floats.
+__device__ __forceinline__ float block_sum(float v, float* red) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  v = wave_sum(v);
+  __syncthreads();
+  if (lane == 0) red[wid] = v;
+  __syncthreads();
+  float t = 0.f;
+  for (int i = 0; i < nw; ++i) t += red[i];
+  return t;
+}
+
+// 6-bit (scale, min) of sub-block j (0..7) of a Q4_K/Q5_K super-block.
+__device__ __forceinline__ void kq_scale_min(int j, const uint8_t* q, int& sc, int& m) {
+  if (j < 4) {
+    sc = q[j] & 63;
+    m = q[j + 4] & 63;
+  } else {
+    sc = (q[j + 4] & 0xF) | ((q[j - 4] >> 6) << 4);
+    m = (q[j + 4] >> 4) | ((q[j] >> 6) << 4);
+  }
+}
+
+}  // namespace aios

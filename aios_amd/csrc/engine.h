@@ -1,0 +1,165 @@
+// In-process inference engine for Llama-family GGUF models on one MI355X (gfx950).
+//
+// Replaces the reference's per-model llama-server child process
+// (`runtime/src/model_manager.rs:185-204`, HTTP at `runtime/src/inference.rs:94-186`):
+// weights live in HBM in the repacked GEMV layout, the KV cache is a bf16 slab
+// [layer][slot][kv_head][max_ctx][head_dim], and the whole decode step (embed -> L x {QKV+RoPE+KV,
+// attention, O+residual, gate/up+SwiGLU, down+residual} -> norm+lm_head -> sample) is one
+// stream-ordered sequence of launches that is captured once per batch size into a hipGraph and
+// replayed (SURVEY.md §2.7 fusion targets, §7.6 hard part 2).  Sampled tokens are fed back on
+// device, so N decode steps need no host round trip.
+#pragma once
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "common.h"
+#include "ops.h"
+
+namespace aios {
+
+struct EngineConfig {
+  std::string name = "model";
+  int vocab_size = 32000;
+  int d_model = 2048;
+  int n_layers = 22;
+  int n_heads = 32;
+  int n_kv_heads = 4;
+  int head_dim = 64;
+  int d_ff = 5632;
+  float rope_theta = 10000.f;
+  int rope_neox = 0;
+  float norm_eps = 1e-5f;
+  int max_ctx = 2048;
+  int max_slots = 4;
+  int max_batch = 8;
+  int tie_embeddings = 0;
+  int qk_norm = 0;
+  int qkv_bias = 0;
+  // tensor parallel (the engine holds this rank's shard; collectives via the comm hook)
+  int tp_rank = 0;
+  int tp_size = 1;
+  int device = 0;
+};
+
+// device matrix in repacked layout (owns its buffer)
+struct QMat {
+  QWeight w{};
+  void* buf = nullptr;
+  size_t bytes = 0;
+  bool valid() const { return buf != nullptr; }
+};
+
+struct LayerW {
+  float* attn_norm = nullptr;
+  float* ffn_norm = nullptr;
+  float* q_norm = nullptr;
+  float* k_norm = nullptr;
+  float* bqkv = nullptr;  // [q_dim + 2 kv_dim]
+  QMat wq, wk, wv, wo, wgu, wdown;
+};
+
+// all-reduce hook (TP): sum `n` floats in place on `stream`; installed by parallel/comm.
+using AllReduceFn = void (*)(void* ctx, float* data, size_t n, hipStream_t stream);
+
+class Engine {
+ public:
+  explicit Engine(const EngineConfig& cfg);
+  ~Engine();
+
+  const EngineConfig& config() const { return cfg_; }
+
+  // --- weights -------------------------------------------------------------------------------
+  // raw GGUF bytes (host pointer) of a named tensor; names follow GGUF ("blk.3.attn_q.weight").
+  void set_tensor(const std::string& name, int ggml_type, int rows, int cols, const void* host, size_t nbytes);
+  // random-init synthetic weights generated in HBM (recipe: "Q4_K_M", "Q4_0", "Q8_0", "BF16", ...)
+  void init_random(const std::string& recipe, uint64_t seed);
+  void finalize();  // checks completeness, allocates KV cache + workspace
+  bool ready() const { return finalized_; }
+  size_t weight_bytes() const { return weight_bytes_; }
+  size_t kv_bytes() const { return kv_bytes_; }
+  size_t workspace_bytes() const { return ws_bytes_; }
+  std::vector<std::string> missing_tensors() const;
+  std::string weight_type_summary() const;
+
+  // --- inference -----------------------------------------------------------------------------
+  // Prefill `tokens` into `slot` starting at position `start_pos`.  Returns logits of the last
+  // token (host copy) if want_logits, and leaves the slot ready to decode.
+  std::vector<float> prefill(int slot, const std::vector<int>& tokens, int start_pos, bool want_logits);
+  // One decode step for B sequences: input token ids at positions pos[b] in slots[b].  Samples
+  // with per-row temperature/top_k (0 = greedy) and optional grammar bitmasks; returns tokens.
+  std::vector<int> decode(const std::vector<int>& slots, const std::vector<int>& tokens, const std::vector<int>& pos,
+                          const std::vector<float>& temperature, const std::vector<int>& top_k, uint64_t seed,
+                          const std::vector<uint8_t>& mask);
+  // logits of the last decode (B x V) -- host copy
+  std::vector<float> last_logits(int B);
+
+  // Device-resident greedy generation for benchmarking: runs n_steps decode steps for B
+  // sequences without host synchronisation (tokens fed back on device, graph replay when
+  // use_graph).  Sequences must already be prefilled to positions pos[b].
+  void decode_loop_prepare(const std::vector<int>& slots, const std::vector<int>& tokens, const std::vector<int>& pos);
+  void decode_loop_run(int B, int n_steps, bool use_graph);
+  std::vector<int> decode_loop_history(int B, int from_pos, int n);
+
+  void synchronize();
+  uintptr_t stream_handle() const { return (uintptr_t)stream_; }
+  void set_allreduce(AllReduceFn fn, void* ctx) { allreduce_ = fn; allreduce_ctx_ = ctx; }
+  void reset_graphs();
+  void copy_slot(int src, int dst, int n_tokens);  // prefix-cache: duplicate KV rows [0, n)
+
+  // raw device pointers for tests / custom kernels
+  uintptr_t kv_cache_k() const { return (uintptr_t)k_cache_; }
+  uintptr_t kv_cache_v() const { return (uintptr_t)v_cache_; }
+
+ private:
+  void enqueue_decode_step(int B);       // uses device arrays d_tokens_/d_pos_/d_seqlen_/d_slot_
+  void layer_decode(int l, int B);
+  void gemv(const std::vector<const QMat*>& segs, int N, int K, int B, const float* x, int ldx, const float* norm_w,
+            float* y, int ldy, int epi, int layer);
+  QMat alloc_qmat(int qt, int rows, int cols);
+  QMat upload_qmat(int qt, int rows, int cols, const void* host, size_t nbytes);
+  float* upload_f32(const void* host, size_t n, int qt);
+  QMat interleave_rows(const QMat& a, const QMat& b);
+  void* dmalloc(size_t bytes);
+  void allreduce(float* p, size_t n);
+
+  EngineConfig cfg_;
+  hipStream_t stream_ = nullptr;
+  bool finalized_ = false;
+  std::vector<void*> allocs_;
+  size_t weight_bytes_ = 0, kv_bytes_ = 0, ws_bytes_ = 0;
+
+  QMat tok_embd_, output_;
+  float* out_norm_ = nullptr;
+  std::vector<LayerW> layers_;
+  std::map<std::string, QMat> pending_;  // gate/up waiting for their partner
+
+  bf16_t* k_cache_ = nullptr;
+  bf16_t* v_cache_ = nullptr;
+  size_t layer_kv_elems_ = 0;
+
+  // workspace
+  float *x_ = nullptr, *q_ = nullptr, *attn_ = nullptr, *ff_ = nullptr, *qkv_ = nullptr;
+  float *opart_ = nullptr, *ml_ = nullptr, *logits_ = nullptr;
+  int *d_tokens_ = nullptr, *d_pos_ = nullptr, *d_seqlen_ = nullptr, *d_slot_ = nullptr, *d_history_ = nullptr;
+  int *d_topk_ = nullptr, *d_step_ = nullptr;
+  float* d_temp_ = nullptr;
+  uint8_t* d_mask_ = nullptr;
+  int n_chunks_ = 0;
+  int prefill_rows_ = 64;  // rows of the prefill workspace
+  float *pf_x_ = nullptr, *pf_q_ = nullptr, *pf_attn_ = nullptr, *pf_ff_ = nullptr, *pf_qkv_ = nullptr;
+  float *pf_opart_ = nullptr, *pf_ml_ = nullptr;
+  bf16_t* pf_a16_ = nullptr;
+  int *pf_tokens_ = nullptr, *pf_pos_ = nullptr, *pf_seqlen_ = nullptr, *pf_slot_ = nullptr;
+
+  std::map<int, hipGraphExec_t> graphs_;
+  AllReduceFn allreduce_ = nullptr;
+  void* allreduce_ctx_ = nullptr;
+  // sampling config for the enqueued step
+  bool sample_temp_ = false;
+  bool sample_mask_ = false;
+  uint64_t sample_seed_ = 0;
+};
+
+}  // namespace aios

@@ -1,0 +1,823 @@
+// Engine implementation -- see engine.h.
+#include "engine.h"
+
+#include <algorithm>
+#include <cstring>
+#include <regex>
+#include <sstream>
+
+namespace aios {
+
+static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+static bool is_kquant(int qt) { return qt == QT_Q4_K || qt == QT_Q5_K || qt == QT_Q6_K; }
+static int block_elems(int qt) {
+  if (is_kquant(qt)) return 256;
+  if (qt == QT_F32 || qt == QT_F16 || qt == QT_BF16) return 1;
+  return 32;
+}
+static int block_bytes(int qt) {
+  switch (qt) {
+    case QT_Q4_K: return 144;
+    case QT_Q5_K: return 176;
+    case QT_Q6_K: return 210;
+    case QT_Q4_0: return 18;
+    case QT_Q4_1: return 20;
+    case QT_Q5_0: return 22;
+    case QT_Q5_1: return 24;
+    case QT_Q8_0: return 34;
+    case QT_F16:
+    case QT_BF16: return 2;
+    case QT_F32: return 4;
+  }
+  throw std::runtime_error("unsupported ggml type " + std::to_string(qt));
+}
+// formats the GEMV streams natively; others are expanded to BF16 at load
+static bool native_qtype(int qt) {
+  return qt == QT_Q4_K || qt == QT_Q5_K || qt == QT_Q6_K || qt == QT_Q4_0 || qt == QT_Q8_0 || qt == QT_F16 ||
+         qt == QT_BF16;
+}
+
+Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
+  HIP_CHECK(hipSetDevice(cfg_.device));
+  HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+  layers_.resize(cfg_.n_layers);
+  if (cfg_.max_batch < 1 || cfg_.max_batch > 8) throw std::runtime_error("max_batch must be 1..8");
+  if (cfg_.max_slots < cfg_.max_batch) cfg_.max_slots = cfg_.max_batch;
+}
+
+Engine::~Engine() {
+  for (auto& kv : graphs_) hipGraphExecDestroy(kv.second);
+  for (void* p : allocs_) hipFree(p);
+  if (stream_) hipStreamDestroy(stream_);
+}
+
+void* Engine::dmalloc(size_t bytes) {
+  void* p = nullptr;
+  HIP_CHECK(hipMalloc(&p, std::max<size_t>(bytes, 16)));
+  allocs_.push_back(p);
+  return p;
+}
+
+QMat Engine::alloc_qmat(int qt, int rows, int cols) {
+  if (cols % block_elems(qt)) throw std::runtime_error("matrix cols not a multiple of the quant block");
+  QMat m;
+  m.w.qtype = qt;
+  m.w.rows = rows;
+  m.w.cols = cols;
+  const size_t nb = (size_t)rows * (cols / block_elems(qt));
+  size_t s0 = 0, s1 = 0, s2 = 0, s3 = 0;
+  switch (qt) {
+    case QT_Q4_K: s0 = nb * 128; s1 = nb * 16; break;
+    case QT_Q5_K: s0 = nb * 128; s1 = nb * 16; s2 = nb * 32; break;
+    case QT_Q6_K: s0 = nb * 128; s1 = nb * 64; s2 = nb * 16; s3 = nb * 2; break;
+    case QT_Q4_0: s0 = nb * 16; s1 = nb * 2; break;
+    case QT_Q8_0: s0 = nb * 32; s1 = nb * 2; break;
+    case QT_F16:
+    case QT_BF16: s0 = (size_t)rows * cols * 2; break;
+    default: throw std::runtime_error("alloc_qmat: non-native type");
+  }
+  const size_t a = 256;
+  const size_t o1 = align_up(s0, a), o2 = o1 + align_up(s1, a), o3 = o2 + align_up(s2, a);
+  m.bytes = o3 + align_up(s3, a) + 64;
+  m.buf = dmalloc(m.bytes);
+  uint8_t* base = (uint8_t*)m.buf;
+  m.w.p0 = base;
+  m.w.p1 = s1 ? base + o1 : nullptr;
+  m.w.p2 = s2 ? base + o2 : nullptr;
+  m.w.p3 = s3 ? base + o3 : nullptr;
+  weight_bytes_ += m.bytes;
+  return m;
+}
+
+QMat Engine::upload_qmat(int qt, int rows, int cols, const void* host, size_t nbytes) {
+  const size_t expect = (size_t)rows * (cols / block_elems(qt)) * block_bytes(qt);
+  if (nbytes != expect)
+    throw std::runtime_error("tensor byte size mismatch: got " + std::to_string(nbytes) + " expected " +
+                             std::to_string(expect));
+  void* staging = nullptr;
+  HIP_CHECK(hipMalloc(&staging, nbytes));
+  HIP_CHECK(hipMemcpyAsync(staging, host, nbytes, hipMemcpyHostToDevice, stream_));
+  QMat m;
+  if (native_qtype(qt)) {
+    m = alloc_qmat(qt, rows, cols);
+    if (qt == QT_F16 || qt == QT_BF16) {
+      HIP_CHECK(hipMemcpyAsync(m.buf, staging, nbytes, hipMemcpyDeviceToDevice, stream_));
+    } else {
+      launch_repack(qt, staging, (size_t)rows * (cols / block_elems(qt)), m.w, stream_);
+    }
+  } else {
+    m = alloc_qmat(QT_BF16, rows, cols);
+    launch_legacy_to_bf16(qt, staging, (size_t)rows * cols, m.buf, stream_);
+  }
+  HIP_CHECK(hipStreamSynchronize(stream_));
+  HIP_CHECK(hipFree(staging));
+  return m;
+}
+
+float* Engine::upload_f32(const void* host, size_t n, int qt) {
+  std::vector<float> tmp(n);
+  if (qt == QT_F32) {
+    std::memcpy(tmp.data(), host, n * 4);
+  } else if (qt == QT_F16 || qt == QT_BF16) {
+    const uint16_t* h = (const uint16_t*)host;
+    for (size_t i = 0; i < n; ++i) {
+      if (qt == QT_BF16) {
+        uint32_t u = (uint32_t)h[i] << 16;
+        std::memcpy(&tmp[i], &u, 4);
+      } else {
+        // IEEE half -> float
+        const uint32_t s = (h[i] >> 15) & 1, e = (h[i] >> 10) & 31, f = h[i] & 1023;
+        float v;
+        if (e == 0) v = std::ldexp((float)f, -24);
+        else if (e == 31) v = f ? NAN : INFINITY;
+        else v = std::ldexp((float)(f | 1024), (int)e - 25);
+        tmp[i] = s ? -v : v;
+      }
+    }
+  } else {
+    throw std::runtime_error("norm/bias tensors must be F32/F16/BF16");
+  }
+  float* d = (float*)dmalloc(n * 4);
+  HIP_CHECK(hipMemcpy(d, tmp.data(), n * 4, hipMemcpyHostToDevice));
+  weight_bytes_ += n * 4;
+  return d;
+}
+
+// rows of a and b interleaved: out row 2i = a row i, 2i+1 = b row i (gate/up -> SwiGLU pairs)
+QMat Engine::interleave_rows(const QMat& a, const QMat& b) {
+  if (a.w.qtype != b.w.qtype || a.w.rows != b.w.rows || a.w.cols != b.w.cols)
+    throw std::runtime_error("gate/up shape or format mismatch");
+  QMat m = alloc_qmat(a.w.qtype, 2 * a.w.rows, a.w.cols);
+  const int rows = a.w.rows;
+  const size_t nbr = a.w.cols / block_elems(a.w.qtype);  // blocks per row
+  auto copy_stream = [&](const uint8_t* dst, const uint8_t* sa, const uint8_t* sb, size_t row_bytes) {
+    if (!dst) return;
+    HIP_CHECK(hipMemcpy2DAsync((void*)dst, 2 * row_bytes, sa, row_bytes, row_bytes, rows, hipMemcpyDeviceToDevice,
+                               stream_));
+    HIP_CHECK(hipMemcpy2DAsync((void*)(dst + row_bytes), 2 * row_bytes, sb, row_bytes, row_bytes, rows,
+                               hipMemcpyDeviceToDevice, stream_));
+  };
+  size_t r0 = 0, r1 = 0, r2 = 0, r3 = 0;
+  switch (a.w.qtype) {
+    case QT_Q4_K: r0 = nbr * 128; r1 = nbr * 16; break;
+    case QT_Q5_K: r0 = nbr * 128; r1 = nbr * 16; r2 = nbr * 32; break;
+    case QT_Q6_K: r0 = nbr * 128; r1 = nbr * 64; r2 = nbr * 16; r3 = nbr * 2; break;
+    case QT_Q4_0: r0 = nbr * 16; r1 = nbr * 2; break;
+    case QT_Q8_0: r0 = nbr * 32; r1 = nbr * 2; break;
+    default: r0 = (size_t)a.w.cols * 2; break;
+  }
+  copy_stream(m.w.p0, a.w.p0, b.w.p0, r0);
+  if (r1) copy_stream(m.w.p1, a.w.p1, b.w.p1, r1);
+  if (r2) copy_stream(m.w.p2, a.w.p2, b.w.p2, r2);
+  if (r3) copy_stream(m.w.p3, a.w.p3, b.w.p3, r3);
+  HIP_CHECK(hipStreamSynchronize(stream_));
+  return m;
+}
+
+void Engine::set_tensor(const std::string& name, int qt, int rows, int cols, const void* host, size_t nbytes) {
+  if (finalized_) throw std::runtime_error("set_tensor after finalize");
+  HIP_CHECK(hipSetDevice(cfg_.device));
+  static const std::regex blk_re(R"(blk\.(\d+)\.(.+))");
+  std::smatch m;
+  if (name == "token_embd.weight") {
+    tok_embd_ = upload_qmat(qt, rows, cols, host, nbytes);
+    return;
+  }
+  if (name == "output.weight") {
+    output_ = upload_qmat(qt, rows, cols, host, nbytes);
+    return;
+  }
+  if (name == "output_norm.weight") {
+    out_norm_ = upload_f32(host, (size_t)rows * cols, qt);
+    return;
+  }
+  if (!std::regex_match(name, m, blk_re)) throw std::runtime_error("unknown tensor " + name);
+  const int l = std::stoi(m[1]);
+  if (l < 0 || l >= cfg_.n_layers) throw std::runtime_error("layer index out of range in " + name);
+  const std::string t = m[2];
+  LayerW& L = layers_[l];
+  const size_t n = (size_t)rows * cols;
+  if (t == "attn_norm.weight") L.attn_norm = upload_f32(host, n, qt);
+  else if (t == "ffn_norm.weight") L.ffn_norm = upload_f32(host, n, qt);
+  else if (t == "attn_q_norm.weight") L.q_norm = upload_f32(host, n, qt);
+  else if (t == "attn_k_norm.weight") L.k_norm = upload_f32(host, n, qt);
+  else if (t == "attn_q.weight") L.wq = upload_qmat(qt, rows, cols, host, nbytes);
+  else if (t == "attn_k.weight") L.wk = upload_qmat(qt, rows, cols, host, nbytes);
+  else if (t == "attn_v.weight") L.wv = upload_qmat(qt, rows, cols, host, nbytes);
+  else if (t == "attn_output.weight") L.wo = upload_qmat(qt, rows, cols, host, nbytes);
+  else if (t == "ffn_down.weight") L.wdown = upload_qmat(qt, rows, cols, host, nbytes);
+  else if (t == "ffn_gate.weight" || t == "ffn_up.weight") {
+    const std::string other = (t == "ffn_gate.weight") ? "ffn_up.weight" : "ffn_gate.weight";
+    const std::string key = "blk." + std::to_string(l) + ".";
+    QMat q = upload_qmat(qt, rows, cols, host, nbytes);
+    auto it = pending_.find(key + other);
+    if (it == pending_.end()) {
+      pending_[key + t] = q;
+    } else {
+      const QMat& g = (t == "ffn_gate.weight") ? q : it->second;
+      const QMat& u = (t == "ffn_gate.weight") ? it->second : q;
+      L.wgu = interleave_rows(g, u);
+      // the separate copies are no longer needed
+      for (const QMat* mm : {&q, &it->second}) {
+        auto pos = std::find(allocs_.begin(), allocs_.end(), mm->buf);
+        if (pos != allocs_.end()) allocs_.erase(pos);
+        weight_bytes_ -= mm->bytes;
+        HIP_CHECK(hipFree(mm->buf));
+      }
+      pending_.erase(it);
+    }
+  } else if (t == "attn_q.bias" || t == "attn_k.bias" || t == "attn_v.bias") {
+    const int qd = cfg_.n_heads * cfg_.head_dim, kvd = cfg_.n_kv_heads * cfg_.head_dim;
+    if (!L.bqkv) {
+      L.bqkv = (float*)dmalloc((size_t)(qd + 2 * kvd) * 4);
+      HIP_CHECK(hipMemset(L.bqkv, 0, (size_t)(qd + 2 * kvd) * 4));
+    }
+    const int off = t == "attn_q.bias" ? 0 : (t == "attn_k.bias" ? qd : qd + kvd);
+    float* tmp = upload_f32(host, n, qt);
+    HIP_CHECK(hipMemcpy(L.bqkv + off, tmp, n * 4, hipMemcpyDeviceToDevice));
+  } else {
+    throw std::runtime_error("unknown layer tensor " + name);
+  }
+}
+
+void Engine::init_random(const std::string& recipe_in, uint64_t seed) {
+  HIP_CHECK(hipSetDevice(cfg_.device));
+  std::string r = recipe_in;
+  std::transform(r.begin(), r.end(), r.begin(), ::toupper);
+  const int d = cfg_.d_model, qd = cfg_.n_heads * cfg_.head_dim, kvd = cfg_.n_kv_heads * cfg_.head_dim;
+  const int ff = cfg_.d_ff, V = cfg_.vocab_size, NL = cfg_.n_layers;
+  auto more_bits = [&](int i) { return i < NL / 8 || i >= 7 * NL / 8 || (i - NL / 8) % 3 == 2; };
+  auto type_for = [&](const std::string& t, int layer) -> int {
+    if (r == "Q4_K_M") {
+      if (t == "output") return QT_Q6_K;
+      if (t == "attn_v" || t == "ffn_down") return more_bits(layer) ? QT_Q6_K : QT_Q4_K;
+      return QT_Q4_K;
+    }
+    if (r == "Q5_K_M") {
+      if (t == "output") return QT_Q6_K;
+      if (t == "attn_v" || t == "ffn_down") return more_bits(layer) ? QT_Q6_K : QT_Q5_K;
+      return QT_Q5_K;
+    }
+    if (r == "Q4_K") return QT_Q4_K;
+    if (r == "Q6_K") return QT_Q6_K;
+    if (r == "Q4_0") return t == "output" ? QT_Q6_K : QT_Q4_0;
+    if (r == "Q8_0") return QT_Q8_0;
+    if (r == "F16") return QT_F16;
+    if (r == "BF16") return QT_BF16;
+    throw std::runtime_error("unknown recipe " + recipe_in);
+  };
+  uint64_t s = seed * 1000003ULL;
+  auto mk = [&](int qt, int rows, int cols, float amp) {
+    QMat m = alloc_qmat(qt, rows, cols);
+    fill_random_weight(m.w, ++s, amp, stream_);
+    return m;
+  };
+  auto vec = [&](int n, float base, float amp) {
+    float* p = (float*)dmalloc((size_t)n * 4);
+    weight_bytes_ += (size_t)n * 4;
+    fill_random_f32(p, n, ++s, base, amp, stream_);
+    return p;
+  };
+  const float amp = 0.02f;
+  tok_embd_ = mk(type_for("token_embd", 0), V, d, 1.0f);
+  if (!cfg_.tie_embeddings) output_ = mk(type_for("output", 0), V, d, amp);
+  out_norm_ = vec(d, 1.f, 0.1f);
+  for (int l = 0; l < NL; ++l) {
+    LayerW& L = layers_[l];
+    L.attn_norm = vec(d, 1.f, 0.1f);
+    L.ffn_norm = vec(d, 1.f, 0.1f);
+    if (cfg_.qk_norm) {
+      L.q_norm = vec(cfg_.head_dim, 1.f, 0.1f);
+      L.k_norm = vec(cfg_.head_dim, 1.f, 0.1f);
+    }
+    if (cfg_.qkv_bias) L.bqkv = vec(qd + 2 * kvd, 0.f, 0.02f);
+    L.wq = mk(type_for("attn_q", l), qd, d, amp);
+    L.wk = mk(type_for("attn_k", l), kvd, d, amp);
+    L.wv = mk(type_for("attn_v", l), kvd, d, amp);
+    L.wo = mk(type_for("attn_output", l), d, qd, amp);
+    L.wgu = mk(type_for("ffn_gate", l), 2 * ff, d, amp);
+    L.wdown = mk(type_for("ffn_down", l), d, ff, amp);
+  }
+  HIP_CHECK(hipStreamSynchronize(stream_));
+}
+
+std::vector<std::string> Engine::missing_tensors() const {
+  std::vector<std::string> miss;
+  if (!tok_embd_.valid()) miss.push_back("token_embd.weight");
+  if (!out_norm_) miss.push_back("output_norm.weight");
+  for (int l = 0; l < cfg_.n_layers; ++l) {
+    const LayerW& L = layers_[l];
+    const std::string p = "blk." + std::to_string(l) + ".";
+    if (!L.attn_norm) miss.push_back(p + "attn_norm.weight");
+    if (!L.ffn_norm) miss.push_back(p + "ffn_norm.weight");
+    if (!L.wq.valid()) miss.push_back(p + "attn_q.weight");
+    if (!L.wk.valid()) miss.push_back(p + "attn_k.weight");
+    if (!L.wv.valid()) miss.push_back(p + "attn_v.weight");
+    if (!L.wo.valid()) miss.push_back(p + "attn_output.weight");
+    if (!L.wgu.valid()) miss.push_back(p + "ffn_gate.weight/ffn_up.weight");
+    if (!L.wdown.valid()) miss.push_back(p + "ffn_down.weight");
+    if (cfg_.qk_norm && (!L.q_norm || !L.k_norm)) miss.push_back(p + "attn_q_norm/attn_k_norm");
+  }
+  return miss;
+}
+
+std::string Engine::weight_type_summary() const {
+  std::map<int, size_t> cnt;
+  auto add = [&](const QMat& m) { if (m.valid()) cnt[m.w.qtype] += (size_t)m.w.rows * m.w.cols; };
+  add(tok_embd_);
+  add(output_);
+  for (const LayerW& L : layers_) { add(L.wq); add(L.wk); add(L.wv); add(L.wo); add(L.wgu); add(L.wdown); }
+  std::ostringstream os;
+  for (auto& kv : cnt) os << kv.first << ":" << kv.second << " ";
+  return os.str();
+}
+
+void Engine::finalize() {
+  HIP_CHECK(hipSetDevice(cfg_.device));
+  auto miss = missing_tensors();
+  if (!miss.empty()) throw std::runtime_error("missing tensors, first: " + miss[0]);
+  if (!output_.valid()) {
+    if (!cfg_.tie_embeddings) cfg_.tie_embeddings = 1;
+    output_ = tok_embd_;  // tied embeddings (GGUF files without output.weight)
+  }
+  const int d = cfg_.d_model, hd = cfg_.head_dim, H = cfg_.n_heads, Hkv = cfg_.n_kv_heads;
+  const int qd = H * hd, kvd = Hkv * hd, V = cfg_.vocab_size, Bm = cfg_.max_batch;
+  if (cfg_.max_ctx % 64) cfg_.max_ctx = (int)align_up(cfg_.max_ctx, 64);
+  layer_kv_elems_ = (size_t)cfg_.max_slots * Hkv * cfg_.max_ctx * hd;
+  kv_bytes_ = 2 * layer_kv_elems_ * cfg_.n_layers * sizeof(bf16_t);
+  k_cache_ = (bf16_t*)dmalloc(kv_bytes_ / 2);
+  v_cache_ = (bf16_t*)dmalloc(kv_bytes_ / 2);
+  HIP_CHECK(hipMemset(k_cache_, 0, kv_bytes_ / 2));
+  HIP_CHECK(hipMemset(v_cache_, 0, kv_bytes_ / 2));
+  n_chunks_ = (cfg_.max_ctx + ATTN_CHUNK - 1) / ATTN_CHUNK;
+
+  size_t ws = 0;
+  auto fbuf = [&](size_t n) { ws += n * 4; return (float*)dmalloc(n * 4); };
+  auto ibuf = [&](size_t n) { ws += n * 4; int* p = (int*)dmalloc(n * 4); HIP_CHECK(hipMemset(p, 0, n * 4)); return p; };
+  x_ = fbuf((size_t)Bm * d);
+  q_ = fbuf((size_t)Bm * qd);
+  qkv_ = fbuf((size_t)Bm * (qd + 2 * kvd));
+  attn_ = fbuf((size_t)Bm * std::max(qd, d));
+  ff_ = fbuf((size_t)Bm * std::max(cfg_.d_ff, d));
+  opart_ = fbuf((size_t)Bm * H * n_chunks_ * hd);
+  ml_ = fbuf((size_t)Bm * H * n_chunks_ * 2);
+  logits_ = fbuf((size_t)Bm * V);
+  d_tokens_ = ibuf(Bm);
+  d_pos_ = ibuf(Bm);
+  d_seqlen_ = ibuf(Bm);
+  d_slot_ = ibuf(Bm);
+  d_topk_ = ibuf(Bm);
+  d_step_ = ibuf(4);
+  d_temp_ = fbuf(Bm);
+  HIP_CHECK(hipMemset(d_temp_, 0, Bm * 4));
+  d_history_ = ibuf((size_t)Bm * (cfg_.max_ctx + 1));
+  d_mask_ = (uint8_t*)dmalloc((size_t)Bm * ((V + 7) / 8));
+  ws += (size_t)Bm * ((V + 7) / 8);
+  const int R = prefill_rows_;
+  pf_x_ = fbuf((size_t)R * d);
+  pf_q_ = fbuf((size_t)R * qd);
+  pf_qkv_ = fbuf((size_t)R * (qd + 2 * kvd));
+  pf_attn_ = fbuf((size_t)R * std::max(qd, d));
+  pf_ff_ = fbuf((size_t)R * std::max(cfg_.d_ff, d));
+  pf_opart_ = fbuf((size_t)R * H * n_chunks_ * hd);
+  pf_ml_ = fbuf((size_t)R * H * n_chunks_ * 2);
+  pf_a16_ = (bf16_t*)dmalloc((size_t)R * std::max({d, qd, cfg_.d_ff}) * 2);
+  pf_tokens_ = ibuf(R);
+  pf_pos_ = ibuf(R);
+  pf_seqlen_ = ibuf(R);
+  pf_slot_ = ibuf(R);
+  ws_bytes_ = ws;
+  HIP_CHECK(hipDeviceSynchronize());
+  finalized_ = true;
+}
+
+void Engine::allreduce(float* p, size_t n) {
+  if (cfg_.tp_size > 1) {
+    if (!allreduce_) throw std::runtime_error("tensor-parallel engine without an all-reduce hook");
+    allreduce_(allreduce_ctx_, p, n, stream_);
+  }
+}
+
+void Engine::gemv(const std::vector<const QMat*>& segs, int N, int K, int B, const float* x, int ldx,
+                  const float* norm_w, float* y, int ldy, int epi, int layer) {
+  GemvArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.nseg = (int)segs.size();
+  int row = 0;
+  for (int s = 0; s < a.nseg; ++s) {
+    a.seg[s] = segs[s]->w;
+    a.seg_row0[s] = row;
+    row += segs[s]->w.rows;
+  }
+  a.N = N;
+  a.K = K;
+  a.B = B;
+  a.row_base = 0;
+  a.x = x;
+  a.ldx = ldx;
+  a.norm_w = norm_w;
+  a.eps = cfg_.norm_eps;
+  a.y = y;
+  a.ldy = ldy;
+  a.epi = epi;
+  if (epi == EPI_QKV) {
+    const LayerW& L = layers_[layer];
+    a.bias = L.bqkv;
+    a.head_dim = cfg_.head_dim;
+    a.q_dim = cfg_.n_heads * cfg_.head_dim;
+    a.kv_dim = cfg_.n_kv_heads * cfg_.head_dim;
+    a.n_kv_heads = cfg_.n_kv_heads;
+    a.max_ctx = cfg_.max_ctx;
+    a.rope_neox = cfg_.rope_neox;
+    a.rope_base = cfg_.rope_theta;
+    a.k_cache = k_cache_ + (size_t)layer * layer_kv_elems_;
+    a.v_cache = v_cache_ + (size_t)layer * layer_kv_elems_;
+  }
+  launch_gemv(a, stream_);
+}
+
+// QKV segments: group into launches where only the last segment may differ in format
+static std::vector<std::vector<const QMat*>> qkv_groups(const LayerW& L) {
+  const QMat* s[3] = {&L.wq, &L.wk, &L.wv};
+  if (s[0]->w.qtype == s[1]->w.qtype && gemv_supports(s[0]->w.qtype, s[2]->w.qtype)) return {{s[0], s[1], s[2]}};
+  if (s[0]->w.qtype == s[1]->w.qtype) return {{s[0], s[1]}, {s[2]}};
+  return {{s[0]}, {s[1]}, {s[2]}};
+}
+
+// one transformer block for the B rows staged in x_ (decode) -- also used by prefill with
+// pointers swapped in (see prefill()).
+void Engine::layer_decode(int l, int B) {
+  const LayerW& L = layers_[l];
+  const int d = cfg_.d_model, hd = cfg_.head_dim, qd = cfg_.n_heads * hd, kvd = cfg_.n_kv_heads * hd;
+  const bool fused_qkv = !cfg_.qk_norm && !cfg_.rope_neox;
+  // ---- QKV (+RMSNorm prologue, RoPE + KV-cache epilogue)
+  {
+    int row0 = 0;
+    for (auto& grp : qkv_groups(L)) {
+      int n = 0;
+      for (auto* m : grp) n += m->w.rows;
+      GemvArgs a;
+      std::memset(&a, 0, sizeof(a));
+      a.nseg = (int)grp.size();
+      int r = 0;
+      for (int s = 0; s < a.nseg; ++s) { a.seg[s] = grp[s]->w; a.seg_row0[s] = r; r += grp[s]->w.rows; }
+      a.N = n; a.K = d; a.B = B; a.row_base = row0;
+      a.x = x_; a.ldx = d; a.norm_w = L.attn_norm; a.eps = cfg_.norm_eps;
+      if (fused_qkv) {
+        a.epi = EPI_QKV; a.y = q_; a.ldy = qd;
+        a.bias = L.bqkv;
+        a.head_dim = hd; a.q_dim = qd; a.kv_dim = kvd; a.n_kv_heads = cfg_.n_kv_heads; a.max_ctx = cfg_.max_ctx;
+        a.rope_neox = cfg_.rope_neox; a.rope_base = cfg_.rope_theta;
+        a.pos = d_pos_; a.slot = d_slot_;
+        a.k_cache = k_cache_ + (size_t)l * layer_kv_elems_;
+        a.v_cache = v_cache_ + (size_t)l * layer_kv_elems_;
+      } else {
+        a.epi = EPI_STORE; a.y = qkv_; a.ldy = qd + 2 * kvd;
+      }
+      launch_gemv(a, stream_);
+      row0 += n;
+    }
+    if (!fused_qkv) {
+      if (L.bqkv) throw std::runtime_error("qkv bias with unfused QKV path not supported yet");
+      QkvPostArgs p;
+      p.qkv = qkv_; p.ldqkv = qd + 2 * kvd; p.T = B;
+      p.n_heads = cfg_.n_heads; p.n_kv_heads = cfg_.n_kv_heads; p.head_dim = hd;
+      p.q_norm = L.q_norm; p.k_norm = L.k_norm; p.eps = cfg_.norm_eps;
+      p.rope_neox = cfg_.rope_neox; p.rope_base = cfg_.rope_theta;
+      p.pos = d_pos_; p.slot = d_slot_; p.q_out = q_;
+      p.k_cache = k_cache_ + (size_t)l * layer_kv_elems_;
+      p.v_cache = v_cache_ + (size_t)l * layer_kv_elems_;
+      p.max_ctx = cfg_.max_ctx;
+      launch_qkv_post(p, stream_);
+    }
+  }
+  // ---- attention
+  {
+    AttnDecodeArgs a;
+    a.q = q_;
+    a.k_cache = k_cache_ + (size_t)l * layer_kv_elems_;
+    a.v_cache = v_cache_ + (size_t)l * layer_kv_elems_;
+    a.seq_len = d_seqlen_;
+    a.slot = d_slot_;
+    a.B = B; a.n_heads = cfg_.n_heads; a.n_kv_heads = cfg_.n_kv_heads; a.head_dim = hd; a.max_ctx = cfg_.max_ctx;
+    a.n_chunks = n_chunks_;
+    a.scale = 1.f / std::sqrt((float)hd);
+    a.o_part = opart_; a.ml = ml_; a.out = attn_;
+    launch_attn_decode(a, stream_);
+  }
+  // ---- O projection (+ residual; TP: partial -> all-reduce -> add)
+  if (cfg_.tp_size > 1) {
+    gemv({&L.wo}, d, qd, B, attn_, qd, nullptr, ff_, d, EPI_STORE, l);
+    allreduce(ff_, (size_t)B * d);
+    launch_add(x_, ff_, (size_t)B * d, stream_);
+  } else {
+    gemv({&L.wo}, d, qd, B, attn_, qd, nullptr, x_, d, EPI_RESID, l);
+  }
+  // ---- gate/up (+RMSNorm, SwiGLU)
+  gemv({&L.wgu}, 2 * cfg_.d_ff, d, B, x_, d, L.ffn_norm, ff_, cfg_.d_ff, EPI_SWIGLU, l);
+  // ---- down (+ residual)
+  if (cfg_.tp_size > 1) {
+    gemv({&L.wdown}, d, cfg_.d_ff, B, ff_, cfg_.d_ff, nullptr, attn_, d, EPI_STORE, l);
+    allreduce(attn_, (size_t)B * d);
+    launch_add(x_, attn_, (size_t)B * d, stream_);
+  } else {
+    gemv({&L.wdown}, d, cfg_.d_ff, B, ff_, cfg_.d_ff, nullptr, x_, d, EPI_RESID, l);
+  }
+}
+
+void Engine::enqueue_decode_step(int B) {
+  const int d = cfg_.d_model, V = cfg_.vocab_size;
+  launch_get_rows(tok_embd_.w, d_tokens_, B, x_, d, 1.f, stream_);
+  for (int l = 0; l < cfg_.n_layers; ++l) layer_decode(l, B);
+  gemv({&output_}, V, d, B, x_, d, out_norm_, logits_, V, EPI_STORE, 0);
+  SampleArgs s;
+  std::memset(&s, 0, sizeof(s));
+  s.logits = logits_; s.ldl = V; s.B = B; s.V = V;
+  s.temperature = d_temp_; s.top_k = d_topk_;
+  s.seed = sample_seed_;
+  s.tokens = d_tokens_; s.pos = d_pos_; s.seq_len = d_seqlen_;
+  s.history = d_history_; s.hist_stride = cfg_.max_ctx + 1;
+  s.advance = 1;
+  s.mask = sample_mask_ ? d_mask_ : nullptr;
+  launch_sample(s, stream_);
+}
+
+std::vector<float> Engine::prefill(int slot, const std::vector<int>& tokens, int start_pos, bool want_logits) {
+  if (!finalized_) throw std::runtime_error("engine not finalized");
+  HIP_CHECK(hipSetDevice(cfg_.device));
+  const int T = (int)tokens.size();
+  if (T == 0) throw std::runtime_error("prefill: empty prompt");
+  if (start_pos + T > cfg_.max_ctx) throw std::runtime_error("prefill: context overflow");
+  if (slot < 0 || slot >= cfg_.max_slots) throw std::runtime_error("prefill: bad slot");
+  for (int t : tokens)
+    if (t < 0 || t >= cfg_.vocab_size) throw std::runtime_error("prefill: token id out of range");
+  const int d = cfg_.d_model, V = cfg_.vocab_size;
+  const int R = prefill_rows_;
+  // swap decode workspace pointers with the prefill ones for the duration of the call
+  std::swap(x_, pf_x_); std::swap(q_, pf_q_); std::swap(qkv_, pf_qkv_); std::swap(attn_, pf_attn_);
+  std::swap(ff_, pf_ff_); std::swap(opart_, pf_opart_); std::swap(ml_, pf_ml_);
+  int* save_tok = d_tokens_; int* save_pos = d_pos_; int* save_sl = d_seqlen_; int* save_slot = d_slot_;
+  std::vector<int> hp(R), hs(R), hsl(R);
+  try {
+    for (int r0 = 0; r0 < T; r0 += R) {
+      const int n = std::min(R, T - r0);
+      for (int i = 0; i < n; ++i) { hp[i] = start_pos + r0 + i; hsl[i] = hp[i] + 1; hs[i] = slot; }
+      HIP_CHECK(hipMemcpyAsync(pf_tokens_, tokens.data() + r0, n * 4, hipMemcpyHostToDevice, stream_));
+      HIP_CHECK(hipMemcpyAsync(pf_pos_, hp.data(), n * 4, hipMemcpyHostToDevice, stream_));
+      HIP_CHECK(hipMemcpyAsync(pf_seqlen_, hsl.data(), n * 4, hipMemcpyHostToDevice, stream_));
+      HIP_CHECK(hipMemcpyAsync(pf_slot_, hs.data(), n * 4, hipMemcpyHostToDevice, stream_));
+      launch_get_rows(tok_embd_.w, pf_tokens_, n, x_, d, 1.f, stream_);
+      float* xb = x_;
+      float *qb = q_, *qkvb = qkv_, *ab = attn_, *fb = ff_;
+      for (int l = 0; l < cfg_.n_layers; ++l) {
+        // sub-batches of <= 8 rows through the GEMV path; attention over all n rows at once
+        const int nsub = (n + 7) / 8;
+        for (int sb = 0; sb < nsub; ++sb) {
+          const int o = sb * 8, bn = std::min(8, n - o);
+          x_ = xb + (size_t)o * d; q_ = qb + (size_t)o * cfg_.n_heads * cfg_.head_dim;
+          qkv_ = qkvb + (size_t)o * (cfg_.n_heads + 2 * cfg_.n_kv_heads) * cfg_.head_dim;
+          d_pos_ = pf_pos_ + o; d_slot_ = pf_slot_ + o; d_seqlen_ = pf_seqlen_ + o;
+          // QKV only (layer_decode runs the whole block; split it by temporarily faking)
+          const LayerW& L = layers_[l];
+          const int hd = cfg_.head_dim, qd = cfg_.n_heads * hd, kvd = cfg_.n_kv_heads * hd;
+          const bool fused_qkv = !cfg_.qk_norm && !cfg_.rope_neox;
+          int row0 = 0;
+          for (auto& grp : qkv_groups(L)) {
+            int nn = 0;
+            for (auto* m : grp) nn += m->w.rows;
+            GemvArgs a;
+            std::memset(&a, 0, sizeof(a));
+            a.nseg = (int)grp.size();
+            int r = 0;
+            for (int s = 0; s < a.nseg; ++s) { a.seg[s] = grp[s]->w; a.seg_row0[s] = r; r += grp[s]->w.rows; }
+            a.N = nn; a.K = d; a.B = bn; a.row_base = row0;
+            a.x = x_; a.ldx = d; a.norm_w = L.attn_norm; a.eps = cfg_.norm_eps;
+            if (fused_qkv) {
+              a.epi = EPI_QKV; a.y = q_; a.ldy = qd; a.bias = L.bqkv;
+              a.head_dim = hd; a.q_dim = qd; a.kv_dim = kvd; a.n_kv_heads = cfg_.n_kv_heads; a.max_ctx = cfg_.max_ctx;
+              a.rope_neox = cfg_.rope_neox; a.rope_base = cfg_.rope_theta;
+              a.pos = d_pos_; a.slot = d_slot_;
+              a.k_cache = k_cache_ + (size_t)l * layer_kv_elems_;
+              a.v_cache = v_cache_ + (size_t)l * layer_kv_elems_;
+            } else {
+              a.epi = EPI_STORE; a.y = qkv_; a.ldy = qd + 2 * kvd;
+            }
+            launch_gemv(a, stream_);
+            row0 += nn;
+          }
+          if (!fused_qkv) {
+            QkvPostArgs p;
+            p.qkv = qkv_; p.ldqkv = qd + 2 * kvd; p.T = bn;
+            p.n_heads = cfg_.n_heads; p.n_kv_heads = cfg_.n_kv_heads; p.head_dim = hd;
+            p.q_norm = L.q_norm; p.k_norm = L.k_norm; p.eps = cfg_.norm_eps;
+            p.rope_neox = cfg_.rope_neox; p.rope_base = cfg_.rope_theta;
+            p.pos = d_pos_; p.slot = d_slot_; p.q_out = q_;
+            p.k_cache = k_cache_ + (size_t)l * layer_kv_elems_;
+            p.v_cache = v_cache_ + (size_t)l * layer_kv_elems_;
+            p.max_ctx = cfg_.max_ctx;
+            launch_qkv_post(p, stream_);
+          }
+        }
+        // attention for all n rows (causal by per-row seq_len)
+        {
+          AttnDecodeArgs a;
+          a.q = qb;
+          a.k_cache = k_cache_ + (size_t)l * layer_kv_elems_;
+          a.v_cache = v_cache_ + (size_t)l * layer_kv_elems_;
+          a.seq_len = pf_seqlen_; a.slot = pf_slot_;
+          a.B = n; a.n_heads = cfg_.n_heads; a.n_kv_heads = cfg_.n_kv_heads; a.head_dim = cfg_.head_dim;
+          a.max_ctx = cfg_.max_ctx;
+          a.n_chunks = n_chunks_;
+          a.scale = 1.f / std::sqrt((float)cfg_.head_dim);
+          a.o_part = opart_; a.ml = ml_; a.out = ab;
+          launch_attn_decode(a, stream_);
+        }
+        for (int sb = 0; sb < nsub; ++sb) {
+          const int o = sb * 8, bn = std::min(8, n - o);
+          const LayerW& L = layers_[l];
+          const int qd = cfg_.n_heads * cfg_.head_dim;
+          float* xr = xb + (size_t)o * d;
+          if (cfg_.tp_size > 1) {
+            gemv({&L.wo}, d, qd, bn, ab + (size_t)o * qd, qd, nullptr, fb + (size_t)o * d, d, EPI_STORE, l);
+          } else {
+            gemv({&L.wo}, d, qd, bn, ab + (size_t)o * qd, qd, nullptr, xr, d, EPI_RESID, l);
+          }
+        }
+        if (cfg_.tp_size > 1) {
+          allreduce(fb, (size_t)n * d);
+          launch_add(xb, fb, (size_t)n * d, stream_);
+        }
+        for (int sb = 0; sb < nsub; ++sb) {
+          const int o = sb * 8, bn = std::min(8, n - o);
+          const LayerW& L = layers_[l];
+          gemv({&L.wgu}, 2 * cfg_.d_ff, d, bn, xb + (size_t)o * d, d, L.ffn_norm, fb + (size_t)o * cfg_.d_ff,
+               cfg_.d_ff, EPI_SWIGLU, l);
+        }
+        for (int sb = 0; sb < nsub; ++sb) {
+          const int o = sb * 8, bn = std::min(8, n - o);
+          const LayerW& L = layers_[l];
+          if (cfg_.tp_size > 1) {
+            gemv({&L.wdown}, d, cfg_.d_ff, bn, fb + (size_t)o * cfg_.d_ff, cfg_.d_ff, nullptr, ab + (size_t)o * d,
+                 d, EPI_STORE, l);
+          } else {
+            gemv({&L.wdown}, d, cfg_.d_ff, bn, fb + (size_t)o * cfg_.d_ff, cfg_.d_ff, nullptr, xb + (size_t)o * d,
+                 d, EPI_RESID, l);
+          }
+        }
+        if (cfg_.tp_size > 1) {
+          allreduce(ab, (size_t)n * d);
+          launch_add(xb, ab, (size_t)n * d, stream_);
+        }
+      }
+      x_ = xb; q_ = qb; qkv_ = qkvb; attn_ = ab; ff_ = fb;
+      if (r0 + n == T && want_logits) {
+        gemv({&output_}, V, d, 1, x_ + (size_t)(n - 1) * d, d, out_norm_, logits_, V, EPI_STORE, 0);
+      }
+    }
+  } catch (...) {
+    std::swap(x_, pf_x_); std::swap(q_, pf_q_); std::swap(qkv_, pf_qkv_); std::swap(attn_, pf_attn_);
+    std::swap(ff_, pf_ff_); std::swap(opart_, pf_opart_); std::swap(ml_, pf_ml_);
+    d_tokens_ = save_tok; d_pos_ = save_pos; d_seqlen_ = save_sl; d_slot_ = save_slot;
+    throw;
+  }
+  std::swap(x_, pf_x_); std::swap(q_, pf_q_); std::swap(qkv_, pf_qkv_); std::swap(attn_, pf_attn_);
+  std::swap(ff_, pf_ff_); std::swap(opart_, pf_opart_); std::swap(ml_, pf_ml_);
+  d_tokens_ = save_tok; d_pos_ = save_pos; d_seqlen_ = save_sl; d_slot_ = save_slot;
+  std::vector<float> out;
+  if (want_logits) {
+    out.resize(V);
+    HIP_CHECK(hipMemcpyAsync(out.data(), logits_, (size_t)V * 4, hipMemcpyDeviceToHost, stream_));
+  }
+  HIP_CHECK(hipStreamSynchronize(stream_));
+  return out;
+}
+
+std::vector<int> Engine::decode(const std::vector<int>& slots, const std::vector<int>& tokens,
+                                const std::vector<int>& pos, const std::vector<float>& temperature,
+                                const std::vector<int>& top_k, uint64_t seed, const std::vector<uint8_t>& mask) {
+  if (!finalized_) throw std::runtime_error("engine not finalized");
+  HIP_CHECK(hipSetDevice(cfg_.device));
+  const int B = (int)slots.size();
+  if (B < 1 || B > cfg_.max_batch) throw std::runtime_error("decode: batch out of range");
+  if ((int)tokens.size() != B || (int)pos.size() != B) throw std::runtime_error("decode: size mismatch");
+  std::vector<int> sl(B);
+  for (int b = 0; b < B; ++b) {
+    if (pos[b] < 0 || pos[b] >= cfg_.max_ctx) throw std::runtime_error("decode: position out of range");
+    if (slots[b] < 0 || slots[b] >= cfg_.max_slots) throw std::runtime_error("decode: bad slot");
+    if (tokens[b] < 0 || tokens[b] >= cfg_.vocab_size) throw std::runtime_error("decode: token out of range");
+    sl[b] = pos[b] + 1;
+  }
+  std::vector<float> temps(B, 0.f);
+  std::vector<int> tks(B, 0);
+  for (int b = 0; b < B && b < (int)temperature.size(); ++b) temps[b] = temperature[b];
+  for (int b = 0; b < B && b < (int)top_k.size(); ++b) tks[b] = top_k[b];
+  HIP_CHECK(hipMemcpyAsync(d_slot_, slots.data(), B * 4, hipMemcpyHostToDevice, stream_));
+  HIP_CHECK(hipMemcpyAsync(d_tokens_, tokens.data(), B * 4, hipMemcpyHostToDevice, stream_));
+  HIP_CHECK(hipMemcpyAsync(d_pos_, pos.data(), B * 4, hipMemcpyHostToDevice, stream_));
+  HIP_CHECK(hipMemcpyAsync(d_seqlen_, sl.data(), B * 4, hipMemcpyHostToDevice, stream_));
+  HIP_CHECK(hipMemcpyAsync(d_temp_, temps.data(), B * 4, hipMemcpyHostToDevice, stream_));
+  HIP_CHECK(hipMemcpyAsync(d_topk_, tks.data(), B * 4, hipMemcpyHostToDevice, stream_));
+  const size_t mbytes = (size_t)B * ((cfg_.vocab_size + 7) / 8);
+  sample_mask_ = !mask.empty();
+  if (sample_mask_) {
+    if (mask.size() != mbytes) throw std::runtime_error("decode: mask size mismatch");
+    HIP_CHECK(hipMemcpyAsync(d_mask_, mask.data(), mbytes, hipMemcpyHostToDevice, stream_));
+  }
+  sample_seed_ = seed;
+  // graphs bake the seed: only graph the greedy/unmasked common case keyed by B
+  const bool graphable = !sample_mask_ && seed == 0;
+  if (graphable) {
+    decode_loop_run(B, 1, true);
+  } else {
+    enqueue_decode_step(B);
+  }
+  std::vector<int> out(B);
+  HIP_CHECK(hipMemcpyAsync(out.data(), d_tokens_, B * 4, hipMemcpyDeviceToHost, stream_));
+  HIP_CHECK(hipStreamSynchronize(stream_));
+  sample_mask_ = false;
+  return out;
+}
+
+std::vector<float> Engine::last_logits(int B) {
+  std::vector<float> out((size_t)B * cfg_.vocab_size);
+  HIP_CHECK(hipMemcpyAsync(out.data(), logits_, out.size() * 4, hipMemcpyDeviceToHost, stream_));
+  HIP_CHECK(hipStreamSynchronize(stream_));
+  return out;
+}
+
+void Engine::decode_loop_prepare(const std::vector<int>& slots, const std::vector<int>& tokens,
+                                 const std::vector<int>& pos) {
+  const int B = (int)slots.size();
+  std::vector<int> sl(B);
+  for (int b = 0; b < B; ++b) sl[b] = pos[b] + 1;
+  std::vector<float> temps(B, 0.f);
+  std::vector<int> tks(B, 0);
+  HIP_CHECK(hipMemcpyAsync(d_slot_, slots.data(), B * 4, hipMemcpyHostToDevice, stream_));
+  HIP_CHECK(hipMemcpyAsync(d_tokens_, tokens.data(), B * 4, hipMemcpyHostToDevice, stream_));
+  HIP_CHECK(hipMemcpyAsync(d_pos_, pos.data(), B * 4, hipMemcpyHostToDevice, stream_));
+  HIP_CHECK(hipMemcpyAsync(d_seqlen_, sl.data(), B * 4, hipMemcpyHostToDevice, stream_));
+  HIP_CHECK(hipMemcpyAsync(d_temp_, temps.data(), B * 4, hipMemcpyHostToDevice, stream_));
+  HIP_CHECK(hipMemcpyAsync(d_topk_, tks.data(), B * 4, hipMemcpyHostToDevice, stream_));
+  HIP_CHECK(hipStreamSynchronize(stream_));
+  sample_seed_ = 0;
+  sample_mask_ = false;
+}
+
+void Engine::decode_loop_run(int B, int n_steps, bool use_graph) {
+  HIP_CHECK(hipSetDevice(cfg_.device));
+  if (!use_graph) {
+    for (int i = 0; i < n_steps; ++i) enqueue_decode_step(B);
+    return;
+  }
+  auto it = graphs_.find(B);
+  if (it == graphs_.end()) {
+    hipGraph_t g;
+    HIP_CHECK(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal));
+    try {
+      enqueue_decode_step(B);
+    } catch (...) {
+      hipStreamEndCapture(stream_, &g);
+      throw;
+    }
+    HIP_CHECK(hipStreamEndCapture(stream_, &g));
+    hipGraphExec_t ge;
+    HIP_CHECK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+    HIP_CHECK(hipGraphDestroy(g));
+    it = graphs_.emplace(B, ge).first;
+  }
+  for (int i = 0; i < n_steps; ++i) HIP_CHECK(hipGraphLaunch(it->second, stream_));
+}
+
+std::vector<int> Engine::decode_loop_history(int B, int from_pos, int n) {
+  std::vector<int> out((size_t)B * n);
+  for (int b = 0; b < B; ++b)
+    HIP_CHECK(hipMemcpyAsync(out.data() + (size_t)b * n, d_history_ + (size_t)b * (cfg_.max_ctx + 1) + from_pos,
+                             n * 4, hipMemcpyDeviceToHost, stream_));
+  HIP_CHECK(hipStreamSynchronize(stream_));
+  return out;
+}
+
+void Engine::synchronize() { HIP_CHECK(hipStreamSynchronize(stream_)); }
+
+void Engine::reset_graphs() {
+  for (auto& kv : graphs_) hipGraphExecDestroy(kv.second);
+  graphs_.clear();
+}
+
+void Engine::copy_slot(int src, int dst, int n) {
+  if (src == dst || n <= 0) return;
+  const int hd = cfg_.head_dim, Hkv = cfg_.n_kv_heads;
+  const size_t pitch = (size_t)cfg_.max_ctx * hd * 2;
+  for (int l = 0; l < cfg_.n_layers; ++l) {
+    for (bf16_t* base : {k_cache_, v_cache_}) {
+      bf16_t* lb = base + (size_t)l * layer_kv_elems_;
+      const bf16_t* s = lb + (size_t)src * Hkv * cfg_.max_ctx * hd;
+      bf16_t* d = lb + (size_t)dst * Hkv * cfg_.max_ctx * hd;
+      HIP_CHECK(hipMemcpy2DAsync(d, pitch, s, pitch, (size_t)n * hd * 2, Hkv, hipMemcpyDeviceToDevice, stream_));
+    }
+  }
+  HIP_CHECK(hipStreamSynchronize(stream_));
+}
+
+}  // namespace aios

@@ -1,0 +1,44 @@
+// Host-visible argument block for the fused decode GEMV (kernels/gemv.hip).
+#pragma once
+#include "common.h"
+#include "qweight.h"
+
+namespace aios {
+
+constexpr int GEMV_MAX_SEGS = 3;
+
+enum GemvEpilogue : int {
+  EPI_STORE = 0,   // y[b][n]  = acc
+  EPI_RESID = 1,   // y[b][n] += acc        (residual stream update)
+  EPI_SWIGLU = 2,  // y[b][n/2] = silu(acc[2i]) * acc[2i+1]   (rows interleaved gate/up)
+  EPI_QKV = 3,     // (+bias) RoPE on Q/K, Q -> y, K/V -> bf16 KV cache at pos[b]
+};
+
+struct GemvArgs {
+  QWeight seg[GEMV_MAX_SEGS];   // row-range segments (e.g. Q,K in Q4_K + V in Q6_K)
+  int seg_row0[GEMV_MAX_SEGS];  // first global row of each segment (multiples of 8)
+  int nseg;
+  int N, K, B;
+  int row_base;                 // global row of local row 0 (epilogue indexing)
+  int kt_max;                   // K tile held in LDS (set by launch_gemv)
+  const float* x;               // [B][ldx] fp32 input (residual stream if norm_w != null)
+  int ldx;
+  const float* norm_w;          // RMSNorm weight [K] or null
+  float eps;
+  float* y;                     // output, see epilogue
+  int ldy;
+  int epi;
+  // QKV epilogue
+  const float* bias;            // [N] or null
+  int head_dim, q_dim, kv_dim, n_kv_heads, max_ctx;
+  int rope_neox;
+  float rope_base;
+  const int* pos;               // [B] position of the token being written
+  const int* slot;              // [B] KV-cache slot (null -> b)
+  bf16_t* k_cache;              // layer base: [slots][n_kv][max_ctx][hd]
+  bf16_t* v_cache;
+};
+
+void launch_gemv(const GemvArgs& a, hipStream_t st);
+
+}  // namespace aios

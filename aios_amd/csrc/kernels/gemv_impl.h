@@ -1,0 +1,318 @@
+// Fused dequant-GEMV for decode (M = batch <= 8): y[b][n] = sum_k W[n][k] * xn[b][k]
+// (SURVEY.md §2.7 K3 "mul_mat_vec_q", fused with K2 RMSNorm prologue, K4/K5 RoPE + KV write,
+//  K7 SwiGLU and K8 residual epilogues).
+//
+// Design (gfx950, wave64):
+//  * 256-thread workgroup = 4 waves; each wave owns ROWS=2 adjacent output rows (a RoPE pair,
+//    or an interleaved (gate_i, up_i) pair) and streams them with 16-B lane chunks straight to
+//    VGPRs (decode weights are read once: the 'GEMV / M <= 16' row of the CDNA guide -- no LDS
+//    round trip for weights).  U chunks x ROWS rows of loads are issued before any decode.
+//  * x (optionally RMS-normalised) is staged once per workgroup in LDS in *chunk order* with a
+//    float4 rotation swizzle, so each lane reads its W x-values with conflict-free ds_read_b128,
+//    plus per-16-run sums of x (for the K-quant min/bias terms).  The x reads are shared by the
+//    2 rows of a wave and the B batch columns reuse the decoded weights.
+//  * One kernel per (format0, format1) pair: segment 0 (e.g. Q and K rows) and segment 1 (e.g.
+//    V rows in Q6_K) can differ, so a mixed Q4_K_M QKV projection is still one launch.
+//  * Epilogues: store / residual-add / SwiGLU / QKV(+bias, RoPE, bf16 KV-cache write).
+#pragma once
+#include <algorithm>
+
+#include "../common.h"
+#include "../gemv.h"
+#include "../qweight.h"
+
+namespace aios {
+
+constexpr int GEMV_THREADS = 256;
+constexpr int GEMV_WAVES = GEMV_THREADS / 64;
+constexpr int GEMV_ROWS = 2;  // rows per wave
+constexpr int GEMV_ROWS_PER_BLOCK = GEMV_WAVES * GEMV_ROWS;
+constexpr int GEMV_LDS_FLOATS = 16384;  // 64 KiB of x per K tile
+
+__device__ __forceinline__ int swz_pos(int c, int j, int F, int S) { return (j + (c >> S)) & (F - 1); }
+
+template <int QT>
+__device__ __forceinline__ void stage_x_tile(const float* __restrict__ x, int ldx, int B, int k0, int kt,
+                                             const float* __restrict__ inv_rms, const float* __restrict__ nw,
+                                             float* xl, float* xs) {
+  using F_ = QFmt<QT>;
+  constexpr int W = F_::W, F = W / 4, S = (F == 8 ? 1 : (F == 4 ? 2 : 3));
+  const int tile_chunks = kt / W;
+  if constexpr (W >= 16) {
+    const int runs = kt / 16;  // one thread per 16-wide run
+    for (int t = threadIdx.x; t < B * runs; t += blockDim.x) {
+      const int b = t / runs, r = t - b * runs;
+      int c, s0;
+      F_::run_pos(r, c, s0);
+      const float* src = x + (size_t)b * ldx + k0 + r * 16;
+      float v[16];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float4 f = *(const float4*)(src + 4 * i);
+        v[4 * i] = f.x; v[4 * i + 1] = f.y; v[4 * i + 2] = f.z; v[4 * i + 3] = f.w;
+      }
+      if (nw) {
+        const float ir = inv_rms[b];
+        const float* wp = nw + k0 + r * 16;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) v[i] = v[i] * ir * wp[i];
+      }
+      float s = 0.f;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) s += v[i];
+      float* dst = xl + ((size_t)b * tile_chunks + c) * W;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int jj = s0 / 4 + j;
+        *(float4*)(dst + 4 * swz_pos(c, jj, F, S)) = make_float4(v[4 * j], v[4 * j + 1], v[4 * j + 2], v[4 * j + 3]);
+      }
+      xs[(size_t)b * tile_chunks * F_::RUNS + c * F_::RUNS + (s0 >> 4)] = s;
+    }
+  } else {
+    for (int t = threadIdx.x; t < B * tile_chunks; t += blockDim.x) {
+      const int b = t / tile_chunks, c = t - b * tile_chunks;
+      const float* src = x + (size_t)b * ldx + k0 + c * W;
+      float v[W];
+#pragma unroll
+      for (int i = 0; i < W / 4; ++i) {
+        float4 f = *(const float4*)(src + 4 * i);
+        v[4 * i] = f.x; v[4 * i + 1] = f.y; v[4 * i + 2] = f.z; v[4 * i + 3] = f.w;
+      }
+      if (nw) {
+        const float ir = inv_rms[b];
+        const float* wp = nw + k0 + c * W;
+#pragma unroll
+        for (int i = 0; i < W; ++i) v[i] = v[i] * ir * wp[i];
+      }
+      float* dst = xl + ((size_t)b * tile_chunks + c) * W;
+#pragma unroll
+      for (int j = 0; j < F; ++j)
+        *(float4*)(dst + 4 * swz_pos(c, j, F, S)) = make_float4(v[4 * j], v[4 * j + 1], v[4 * j + 2], v[4 * j + 3]);
+    }
+  }
+}
+
+// rows (row0, row0+1) of w over the K-tile [k0, k0+kt)
+template <int QT, int B, int U>
+__device__ __forceinline__ void gemv_tile(const QWeight& w, int row0, int k0, int kt, const float* xl,
+                                          const float* xs, float (&acc)[GEMV_ROWS][B]) {
+  using F_ = QFmt<QT>;
+  using S_ = QStream<QT>;
+  constexpr int W = F_::W, F = W / 4, S = (F == 8 ? 1 : (F == 4 ? 2 : 3)), R = F_::RUNS;
+  const int lane = threadIdx.x & 63;
+  const int c_base = k0 / W;
+  const int tile_chunks = kt / W;
+  for (int it = 0; it < tile_chunks; it += 64 * U) {
+    RawChunk raw[U][GEMV_ROWS];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int c = it + u * 64 + lane;
+      if (c < tile_chunks) {
+#pragma unroll
+        for (int r = 0; r < GEMV_ROWS; ++r) F_::load(w, row0 + r, c_base + c, raw[u][r]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int c = it + u * 64 + lane;
+      if (c < tile_chunks) {
+        const int cg = c_base + c;
+        float sc[GEMV_ROWS][R], of[GEMV_ROWS][R];
+#pragma unroll
+        for (int r = 0; r < GEMV_ROWS; ++r) S_::scales(raw[u][r], cg, sc[r], of[r]);
+#pragma unroll
+        for (int b = 0; b < B; ++b) {
+          const float* xc = xl + ((size_t)b * tile_chunks + c) * W;
+          float part[GEMV_ROWS][R];
+#pragma unroll
+          for (int r = 0; r < GEMV_ROWS; ++r)
+#pragma unroll
+            for (int rr = 0; rr < R; ++rr) part[r][rr] = 0.f;
+#pragma unroll
+          for (int j = 0; j < F; ++j) {
+            const float4 xv = *(const float4*)(xc + 4 * swz_pos(c, j, F, S));
+            constexpr int JPR = 16 / 4;  // float4s per 16-run
+            const int rr = (R == 1) ? 0 : (j / JPR);
+#pragma unroll
+            for (int r = 0; r < GEMV_ROWS; ++r) {
+              float q[4];
+              S_::quad(raw[u][r], cg, j, q);
+              part[r][rr] = fmaf(q[0], xv.x, part[r][rr]);
+              part[r][rr] = fmaf(q[1], xv.y, part[r][rr]);
+              part[r][rr] = fmaf(q[2], xv.z, part[r][rr]);
+              part[r][rr] = fmaf(q[3], xv.w, part[r][rr]);
+            }
+          }
+          if constexpr (W >= 16) {
+            const float* xsc = xs + (size_t)b * tile_chunks * R + c * R;
+            float xsv[R];
+#pragma unroll
+            for (int rr = 0; rr < R; ++rr) xsv[rr] = xsc[rr];
+#pragma unroll
+            for (int r = 0; r < GEMV_ROWS; ++r)
+#pragma unroll
+              for (int rr = 0; rr < R; ++rr) acc[r][b] += sc[r][rr] * part[r][rr] - of[r][rr] * xsv[rr];
+          } else {
+#pragma unroll
+            for (int r = 0; r < GEMV_ROWS; ++r) acc[r][b] += part[r][0];
+          }
+        }
+      }
+    }
+  }
+}
+
+template <int QT, int B, int U>
+__device__ __forceinline__ void gemv_seg(const GemvArgs& a, const QWeight& w, int local_row, bool active,
+                                         const float* inv_rms, float* xl, float* xs, float (&acc)[GEMV_ROWS][B]) {
+  const int K = a.K, kt_max = a.kt_max;
+  for (int k0 = 0; k0 < K; k0 += kt_max) {
+    const int kt = min(kt_max, K - k0);
+    if (k0 > 0) __syncthreads();
+    stage_x_tile<QT>(a.x, a.ldx, a.B, k0, kt, inv_rms, a.norm_w, xl, xs);
+    __syncthreads();
+    if (active) gemv_tile<QT, B, U>(w, local_row, k0, kt, xl, xs, acc);
+  }
+}
+
+template <int QT0, int QT1, int B, int U>
+__global__ void __launch_bounds__(GEMV_THREADS) gemv_kernel(GemvArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* red = smem;  // 64 floats: block-reduction scratch + inv_rms[16..]
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int row_blk = blockIdx.x * GEMV_ROWS_PER_BLOCK;
+  // segments are row ranges (multiples of 8 rows) so a workgroup never straddles two
+  int sidx = 0;
+#pragma unroll
+  for (int s = 1; s < GEMV_MAX_SEGS; ++s)
+    if (s < a.nseg && row_blk >= a.seg_row0[s]) sidx = s;
+  const int seg_row0 = a.seg_row0[sidx];
+  const int K = a.K;
+  const int nb_act = a.B;  // real batch (<= B; padding columns are never stored)
+
+  float* inv_rms = red + 16;
+  if (a.norm_w) {
+    for (int b = 0; b < nb_act; ++b) {
+      float s = 0.f;
+      const float* xb = a.x + (size_t)b * a.ldx;
+      for (int k = threadIdx.x * 4; k < K; k += GEMV_THREADS * 4) {
+        const float4 v = *(const float4*)(xb + k);
+        s += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+      }
+      s = block_sum(s, red);
+      if (threadIdx.x == 0) inv_rms[b] = rsqrtf(s / (float)K + a.eps);
+      __syncthreads();
+    }
+  }
+
+  float acc[GEMV_ROWS][B];
+#pragma unroll
+  for (int r = 0; r < GEMV_ROWS; ++r)
+#pragma unroll
+    for (int b = 0; b < B; ++b) acc[r][b] = 0.f;
+  float* xl = smem + 64;
+  float* xs = xl + B * a.kt_max;
+  const int local_row = row_blk - seg_row0 + wave * GEMV_ROWS;
+  const bool active = (row_blk + wave * GEMV_ROWS) < a.N;
+  // the type-0 segment(s) come first; type-1 is only ever the last segment
+  if (QT0 == QT1 || sidx < a.nseg - 1 || a.nseg == 1)
+    gemv_seg<QT0, B, U>(a, a.seg[sidx], local_row, active, inv_rms, xl, xs, acc);
+  else
+    gemv_seg<QT1, B, U>(a, a.seg[sidx], local_row, active, inv_rms, xl, xs, acc);
+  if (!active) return;
+
+#pragma unroll
+  for (int r = 0; r < GEMV_ROWS; ++r)
+#pragma unroll
+    for (int b = 0; b < B; ++b) acc[r][b] = wave_sum(acc[r][b]);
+  if (lane >= nb_act) return;
+  float v0 = 0.f, v1 = 0.f;  // lane b handles batch column b
+#pragma unroll
+  for (int b = 0; b < B; ++b)
+    if (lane == b) { v0 = acc[0][b]; v1 = acc[1][b]; }
+  const int b = lane;
+  const int grow = a.row_base + row_blk + wave * GEMV_ROWS;
+  const int nrow = a.row_base + a.N;
+  switch (a.epi) {
+    case EPI_STORE: {
+      float* y = a.y + (size_t)b * a.ldy;
+      y[grow] = v0;
+      if (grow + 1 < nrow) y[grow + 1] = v1;
+    } break;
+    case EPI_RESID: {
+      float* y = a.y + (size_t)b * a.ldy;
+      y[grow] += v0;
+      if (grow + 1 < nrow) y[grow + 1] += v1;
+    } break;
+    case EPI_SWIGLU: {
+      const float g = v0, u = v1;  // rows (2i, 2i+1) = (gate_i, up_i)
+      a.y[(size_t)b * a.ldy + (grow >> 1)] = g / (1.f + __expf(-g)) * u;
+    } break;
+    case EPI_QKV: {
+      if (a.bias) { v0 += a.bias[grow]; v1 += a.bias[grow + 1]; }
+      const int hd = a.head_dim, qd = a.q_dim, kvd = a.kv_dim;
+      const int pos = a.pos[b];
+      const int slot = a.slot ? a.slot[b] : b;
+      int part, r;
+      if (grow < qd) { part = 0; r = grow; }
+      else if (grow < qd + kvd) { part = 1; r = grow - qd; }
+      else { part = 2; r = grow - qd - kvd; }
+      const int head = r / hd, lr = r - head * hd, p = lr >> 1;
+      int da, db;
+      if (part == 2) { da = lr; db = lr + 1; }
+      else if (a.rope_neox) { da = p; db = p + (hd >> 1); }
+      else { da = 2 * p; db = 2 * p + 1; }
+      if (part < 2) {
+        const float theta = (float)pos * powf(a.rope_base, -2.f * (float)p / (float)hd);
+        float sn, cs;
+        sincosf(theta, &sn, &cs);
+        const float o0 = v0 * cs - v1 * sn, o1 = v0 * sn + v1 * cs;
+        v0 = o0; v1 = o1;
+      }
+      if (part == 0) {
+        float* q = a.y + (size_t)b * a.ldy + head * hd;
+        q[da] = v0; q[db] = v1;
+      } else {
+        bf16_t* cache = (part == 1 ? a.k_cache : a.v_cache);
+        const size_t base = (((size_t)slot * a.n_kv_heads + head) * a.max_ctx + pos) * hd;
+        cache[base + da] = f32_to_bf16(v0);
+        cache[base + db] = f32_to_bf16(v1);
+      }
+    } break;
+  }
+}
+
+inline int qtype_block(int qt) {
+  return (qt == QT_Q4_K || qt == QT_Q5_K || qt == QT_Q6_K) ? 256 : (qt == QT_F16 || qt == QT_BF16 ? 8 : 32);
+}
+
+template <int QT0, int QT1, int B, int U>
+void launch_gemv_t(GemvArgs a, hipStream_t st) {
+  const int blocks = (a.N + GEMV_ROWS_PER_BLOCK - 1) / GEMV_ROWS_PER_BLOCK;
+  int kt = (GEMV_LDS_FLOATS / B) / 256 * 256;
+  if (kt >= a.K) kt = a.K;
+  int blk = 8;
+  for (int s = 0; s < a.nseg; ++s) blk = std::max(blk, qtype_block(a.seg[s].qtype));
+  if (kt < blk) kt = blk;
+  a.kt_max = kt;
+  const size_t lds = (64 + (size_t)B * kt + (size_t)B * kt / 16 + 4) * sizeof(float);
+  hipLaunchKernelGGL((gemv_kernel<QT0, QT1, B, U>), dim3(blocks), dim3(GEMV_THREADS), lds, st, a);
+}
+
+template <int QT0, int QT1>
+void launch_gemv_pair(const GemvArgs& a, hipStream_t st) {
+  constexpr int W = QFmt<QT0>::W;
+  const int chunks_per_lane = (a.K / W + 63) / 64;
+  if (a.B == 1) {
+    if (chunks_per_lane >= 4) launch_gemv_t<QT0, QT1, 1, 4>(a, st);
+    else launch_gemv_t<QT0, QT1, 1, 2>(a, st);
+  } else if (a.B == 2) {
+    launch_gemv_t<QT0, QT1, 2, 2>(a, st);
+  } else if (a.B <= 4) {
+    launch_gemv_t<QT0, QT1, 4, 2>(a, st);
+  } else {
+    launch_gemv_t<QT0, QT1, 8, 1>(a, st);
+  }
+}
+
+}  // namespace aios

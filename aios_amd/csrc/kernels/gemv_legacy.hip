@@ -1,0 +1,8 @@
+// GEMV instantiations: 32-block formats (Q4_0, Q8_0) and 16-bit float weights (F16, BF16).
+#include "gemv_impl.h"
+namespace aios {
+void gemv_q4_0(const GemvArgs& a, hipStream_t st) { launch_gemv_pair<QT_Q4_0, QT_Q4_0>(a, st); }
+void gemv_q8_0(const GemvArgs& a, hipStream_t st) { launch_gemv_pair<QT_Q8_0, QT_Q8_0>(a, st); }
+void gemv_f16(const GemvArgs& a, hipStream_t st) { launch_gemv_pair<QT_F16, QT_F16>(a, st); }
+void gemv_bf16(const GemvArgs& a, hipStream_t st) { launch_gemv_pair<QT_BF16, QT_BF16>(a, st); }
+}  // namespace aios

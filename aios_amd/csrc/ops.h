@@ -1,0 +1,107 @@
+// Host launchers for every device op of the engine (one header so the engine, the bindings and
+// the tests see the same signatures).  All launchers are stream-ordered and capture-safe: no
+// allocation, no synchronisation (CDNA guide §6 Guideline 9), so the decode step can be captured
+// into a hipGraph.
+#pragma once
+#include "common.h"
+#include "gemv.h"
+#include "qweight.h"
+
+namespace aios {
+
+// ---- weights -------------------------------------------------------------------------------
+void launch_repack(int qt, const void* raw, size_t nblocks, const QWeight& w, hipStream_t st);
+void launch_get_rows(const QWeight& w, const int* rows, int nrows, float* out, int ldo, float scale,
+                     hipStream_t st);
+void launch_dequant_bf16(const QWeight& w, void* out, hipStream_t st);
+void launch_legacy_to_bf16(int qt, const void* raw, size_t n, void* out, hipStream_t st);
+void fill_random_weight(const QWeight& w, uint64_t seed, float amp, hipStream_t st);
+void fill_random_f32(float* p, size_t n, uint64_t seed, float base, float amp, hipStream_t st);
+bool gemv_supports(int qt0, int qt1);
+
+// ---- elementwise / norms ---------------------------------------------------------------------
+// y[b] = x[b] * rsqrt(mean(x^2)+eps) * w     (rows of length n, row strides ldx/ldy)
+void launch_rmsnorm(const float* x, int ldx, const float* w, float* y, int ldy, int rows, int n, float eps,
+                    hipStream_t st);
+// same, bf16 output (GEMM A operand)
+void launch_rmsnorm_bf16(const float* x, int ldx, const float* w, bf16_t* y, int ldy, int rows, int n, float eps,
+                         hipStream_t st);
+void launch_f32_to_bf16(const float* x, bf16_t* y, size_t n, hipStream_t st);
+void launch_add(float* y, const float* x, size_t n, hipStream_t st);
+// out[b][i] = silu(gu[b][2i]) * gu[b][2i+1]
+void launch_swiglu_interleaved(const float* gu, int ldg, float* out, int ldo, int rows, int n, hipStream_t st);
+
+// Per-head: optional RMSNorm(q/k heads) + RoPE + Q store + K/V cache write, from a packed
+// qkv row [B][q_dim + 2 kv_dim] (used for Qwen3 QK-norm and the prefill GEMM path).
+struct QkvPostArgs {
+  const float* qkv;  // [T][ldqkv]
+  int ldqkv;
+  int T;
+  int n_heads, n_kv_heads, head_dim;
+  const float* q_norm;  // [head_dim] or null
+  const float* k_norm;
+  float eps;
+  int rope_neox;
+  float rope_base;
+  const int* pos;    // [T]
+  const int* slot;   // [T] or null (0)
+  float* q_out;      // [T][n_heads*head_dim]
+  bf16_t* k_cache;   // layer base
+  bf16_t* v_cache;
+  int max_ctx;
+};
+void launch_qkv_post(const QkvPostArgs& a, hipStream_t st);
+
+// ---- attention ---------------------------------------------------------------------------------
+struct AttnDecodeArgs {
+  const float* q;          // [B][n_heads][head_dim]
+  const bf16_t* k_cache;   // layer base [slots][n_kv][max_ctx][hd]
+  const bf16_t* v_cache;
+  const int* seq_len;      // [B] number of valid keys (pos+1)
+  const int* slot;         // [B] or null
+  int B, n_heads, n_kv_heads, head_dim, max_ctx;
+  int n_chunks;            // grid chunks (>= ceil(max_len / ATTN_CHUNK))
+  float scale;
+  float* o_part;           // [B][n_heads][n_chunks][hd]
+  float* ml;               // [B][n_heads][n_chunks][2]
+  float* out;              // [B][n_heads*hd]
+};
+constexpr int ATTN_CHUNK = 64;
+void launch_attn_decode(const AttnDecodeArgs& a, hipStream_t st);
+
+// ---- sampling ---------------------------------------------------------------------------------
+// per row b: token[b] = argmax(logits[b])   (temperature[b] > 0 -> Gumbel-max sample with
+// top-k filtering when top_k[b] > 0); then pos[b] += 1, seq_len[b] = pos[b] + 1,
+// history[b][step] = token.
+struct SampleArgs {
+  const float* logits;
+  int ldl;
+  int B, V;
+  const float* temperature;  // [B] or null (greedy)
+  const int* top_k;          // [B] or null
+  uint64_t seed;             // RNG key = (seed, row, pos[row])
+  int* tokens;               // [B] out
+  int* pos;                  // [B] in/out (incremented when advance != 0)
+  int* seq_len;              // [B] out (pos+1) or null
+  int* history;              // [B][hist_stride] or null
+  int hist_stride;
+  int advance;
+  const uint8_t* mask;       // [B][ceil(V/8)] allowed-token bitmask or null
+};
+void launch_sample(const SampleArgs& a, hipStream_t st);
+
+// ---- MFMA GEMM (prefill) ----------------------------------------------------------------------
+// C[M][N] (fp32, epilogue) = A[M][K] (bf16) x W[N][K]^T (quantized, dequantized tile-wise in LDS)
+struct GemmArgs {
+  const bf16_t* A;
+  int lda;
+  QWeight w;
+  int M, N, K;
+  float* C;
+  int ldc;
+  int accumulate;  // C += result
+};
+void launch_gemm(const GemmArgs& a, hipStream_t st);
+bool gemm_supports(int qt);
+
+}  // namespace aios

@@ -1,0 +1,426 @@
+// Device-side quantized weight descriptor + per-format chunk decoders (gfx950).
+//
+// Weights are repacked at load time (quant_pack.hip) from the GGUF array-of-blocks layout into
+// a structure-of-arrays layout per row, so that one lane loads exactly one aligned 16-byte
+// "chunk" of quant bits per global_load_dwordx4 and the per-block metadata sits in a separate,
+// separately-aligned stream:
+//
+//   Q4_K : p0 = qs   [rows][nb*128]    p1 = meta [rows][nb*16] = {f16 d, f16 dmin, u8 scales[12]}
+//   Q5_K : p0 = qs   [rows][nb*128]    p1 = meta [rows][nb*16]   p2 = qh [rows][nb*32]
+//   Q6_K : p0 = ql   [rows][nb*128]    p1 = qh   [rows][nb*64]   p2 = sc [rows][nb*16] (int8)
+//          p3 = d    [rows][nb] (f16)
+//   Q4_0 : p0 = qs   [rows][nb*16]     p1 = d    [rows][nb] (f16)             (nb = K/32)
+//   Q8_0 : p0 = qs   [rows][nb*32]     p1 = d    [rows][nb] (f16)             (nb = K/32)
+//   F16 / BF16 : p0 = [rows][K]
+//
+// A chunk covers W weights (32 for Q4_K/Q5_K/Q6_K/Q4_0, 16 for Q8_0, 8 for F16/BF16) made of
+// RUNS contiguous 16-weight runs (K index ranges).  `chunk_k0(c, run)` gives the first K index
+// of each run; the GEMV prologue lays x out in LDS in chunk order so a lane reads its W x-values
+// with W/4 conflict-free ds_read_b128.
+#pragma once
+#include "common.h"
+
+namespace aios {
+
+struct QWeight {
+  int qtype;
+  int rows;
+  int cols;
+  int pad_;
+  const uint8_t* p0;
+  const uint8_t* p1;
+  const uint8_t* p2;
+  const uint8_t* p3;
+};
+
+struct RawChunk {
+  uint4 a;      // main quant bits
+  uint4 b;      // meta / qh
+  uint4 c;      // qh / scales
+  uint32_t d;   // f16 scale (Q6_K / Q4_0 / Q8_0)
+};
+
+template <int QT>
+struct QFmt;
+
+__device__ __forceinline__ uint32_t u4_word(const uint4& v, int i) {
+  return i == 0 ? v.x : (i == 1 ? v.y : (i == 2 ? v.z : v.w));
+}
+
+// ------------------------------------------------------------------------------------ Q4_K
+template <>
+struct QFmt<QT_Q4_K> {
+  static constexpr int W = 32, RUNS = 2, CHUNKS_PER_BLOCK = 8, BLOCK = 256;
+  __device__ static int chunk_k0(int c, int run) {
+    const int b = c >> 3, l = c & 7, g = l >> 1, h = l & 1;
+    return b * 256 + 64 * g + 16 * h + 32 * run;
+  }
+  // run r (16 contiguous k) -> (chunk, slot0)
+  __device__ static void run_pos(int r, int& c, int& s0) {
+    const int b = r >> 4, rr = r & 15, g = rr >> 2, hi = (rr >> 1) & 1, h = rr & 1;
+    c = b * 8 + 2 * g + h;
+    s0 = 16 * hi;
+  }
+  __device__ static void load(const QWeight& w, int row, int c, RawChunk& r) {
+    const int nb = w.cols >> 8;
+    r.a = *(const uint4*)(w.p0 + ((size_t)row * nb * 8 + c) * 16);
+    r.b = *(const uint4*)(w.p1 + ((size_t)row * nb + (c >> 3)) * 16);
+  }
+  // q[] as raw unsigned values, run scale/offset: contribution = sc*dot(q,x) - of*sum(x)
+  __device__ static void decode(const RawChunk& r, int c, float q[32], float sc[2], float of[2]) {
+    const int l = c & 7, g = l >> 1;
+    const uint32_t dd = r.b.x;
+    const float d = __half2float(__ushort_as_half((uint16_t)(dd & 0xffff)));
+    const float dmin = __half2float(__ushort_as_half((uint16_t)(dd >> 16)));
+    const uint32_t w1 = r.b.y, w2 = r.b.z, w3 = r.b.w;  // scales[0..3], [4..7], [8..11]
+    const int sh = 16 * (g & 1);
+    uint32_t scp, mp;
+    if (g < 2) {
+      scp = (w1 >> sh) & 0x3f3f;
+      mp = (w2 >> sh) & 0x3f3f;
+    } else {
+      scp = ((w3 >> sh) & 0x0f0f) | (((w1 >> sh) >> 2) & 0x3030);
+      mp = (((w3 >> sh) >> 4) & 0x0f0f) | (((w2 >> sh) >> 2) & 0x3030);
+    }
+    sc[0] = d * (float)(scp & 0xff);
+    sc[1] = d * (float)(scp >> 8);
+    of[0] = dmin * (float)(mp & 0xff);
+    of[1] = dmin * (float)(mp >> 8);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint32_t wv = u4_word(r.a, i);
+      const uint32_t lo = wv & 0x0f0f0f0fu, hi = (wv >> 4) & 0x0f0f0f0fu;
+      q[4 * i + 0] = (float)(lo & 0xff);
+      q[4 * i + 1] = (float)((lo >> 8) & 0xff);
+      q[4 * i + 2] = (float)((lo >> 16) & 0xff);
+      q[4 * i + 3] = (float)(lo >> 24);
+      q[16 + 4 * i + 0] = (float)(hi & 0xff);
+      q[16 + 4 * i + 1] = (float)((hi >> 8) & 0xff);
+      q[16 + 4 * i + 2] = (float)((hi >> 16) & 0xff);
+      q[16 + 4 * i + 3] = (float)(hi >> 24);
+    }
+  }
+};
+
+// ------------------------------------------------------------------------------------ Q5_K
+template <>
+struct QFmt<QT_Q5_K> {
+  static constexpr int W = 32, RUNS = 2, CHUNKS_PER_BLOCK = 8, BLOCK = 256;
+  __device__ static int chunk_k0(int c, int run) { return QFmt<QT_Q4_K>::chunk_k0(c, run); }
+  __device__ static void run_pos(int r, int& c, int& s0) { QFmt<QT_Q4_K>::run_pos(r, c, s0); }
+  __device__ static void load(const QWeight& w, int row, int c, RawChunk& r) {
+    const int nb = w.cols >> 8;
+    r.a = *(const uint4*)(w.p0 + ((size_t)row * nb * 8 + c) * 16);
+    r.b = *(const uint4*)(w.p1 + ((size_t)row * nb + (c >> 3)) * 16);
+    // qh bytes [16*h, 16*h+16) of the block's 32
+    r.c = *(const uint4*)(w.p2 + ((size_t)row * nb + (c >> 3)) * 32 + 16 * (c & 1));
+  }
+  __device__ static void decode(const RawChunk& r, int c, float q[32], float sc[2], float of[2]) {
+    QFmt<QT_Q4_K>::decode(r, c, q, sc, of);
+    const int g = (c & 7) >> 1;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint32_t hv = u4_word(r.c, i);
+      const uint32_t h0 = (hv >> (2 * g)) & 0x01010101u, h1 = (hv >> (2 * g + 1)) & 0x01010101u;
+      q[4 * i + 0] += (float)((h0 & 0xff) << 4);
+      q[4 * i + 1] += (float)(((h0 >> 8) & 0xff) << 4);
+      q[4 * i + 2] += (float)(((h0 >> 16) & 0xff) << 4);
+      q[4 * i + 3] += (float)((h0 >> 24) << 4);
+      q[16 + 4 * i + 0] += (float)((h1 & 0xff) << 4);
+      q[16 + 4 * i + 1] += (float)(((h1 >> 8) & 0xff) << 4);
+      q[16 + 4 * i + 2] += (float)(((h1 >> 16) & 0xff) << 4);
+      q[16 + 4 * i + 3] += (float)((h1 >> 24) << 4);
+    }
+  }
+};
+
+// ------------------------------------------------------------------------------------ Q6_K
+// chunk p (0..7) of a block: n = p>>2 (128-half), o = 16*(p&3) ql offset inside the half.
+//   o <  32: l = o..o+15 : low nibble -> k = 128n + l      (scale is = l/16 + 0), high -> +64 (is+4)
+//   o >= 32: l = o-32..  : low nibble -> k = 128n + l + 32 (is + 2),              high -> +96 (is+6)
+template <>
+struct QFmt<QT_Q6_K> {
+  static constexpr int W = 32, RUNS = 2, CHUNKS_PER_BLOCK = 8, BLOCK = 256;
+  __device__ static int chunk_k0(int c, int run) {
+    const int b = c >> 3, p = c & 7, n = p >> 2, o = 16 * (p & 3);
+    const int l = o & 31, up = o >> 5;
+    return b * 256 + 128 * n + l + 32 * up + 64 * run;
+  }
+  __device__ static void run_pos(int r, int& c, int& s0) {
+    const int b = r >> 4, rr = r & 15, n = rr >> 3, q4 = (rr >> 1) & 3, lh = rr & 1;
+    c = b * 8 + 4 * n + 2 * (q4 & 1) + lh;
+    s0 = 16 * (q4 >> 1);
+  }
+  __device__ static void load(const QWeight& w, int row, int c, RawChunk& r) {
+    const int nb = w.cols >> 8;
+    const size_t blk = (size_t)row * nb + (c >> 3);
+    const int p = c & 7, n = p >> 2, o = 16 * (p & 3);
+    r.a = *(const uint4*)(w.p0 + ((size_t)row * nb * 8 + c) * 16);
+    r.b = *(const uint4*)(w.p1 + blk * 64 + 32 * n + (o & 31));
+    r.c = *(const uint4*)(w.p2 + blk * 16);
+    r.d = *(const uint16_t*)(w.p3 + blk * 2);
+  }
+  __device__ static void decode(const RawChunk& r, int c, float q[32], float sc[2], float of[2]) {
+    const int p = c & 7, n = p >> 2, o = 16 * (p & 3);
+    const int up = o >> 5, is = (o & 31) >> 4;
+    const float d = __half2float(__ushort_as_half((uint16_t)r.d));
+    const int s_lo = 8 * n + is + 2 * up, s_hi = s_lo + 4;
+    const int8_t sl = (int8_t)((u4_word(r.c, s_lo >> 2) >> (8 * (s_lo & 3))) & 0xff);
+    const int8_t sh = (int8_t)((u4_word(r.c, s_hi >> 2) >> (8 * (s_hi & 3))) & 0xff);
+    sc[0] = d * (float)sl;
+    sc[1] = d * (float)sh;
+    // q - 32: folded as -32*sc*sum(x)
+    of[0] = 32.f * sc[0];
+    of[1] = 32.f * sc[1];
+    const int hs = 2 * up;  // qh bit pair for low nibble: bits hs..hs+1, high nibble: hs+4..hs+5
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint32_t wv = u4_word(r.a, i), hv = u4_word(r.b, i);
+      const uint32_t lo = (wv & 0x0f0f0f0fu) | (((hv >> hs) & 0x03030303u) << 4);
+      const uint32_t hi = ((wv >> 4) & 0x0f0f0f0fu) | (((hv >> (hs + 4)) & 0x03030303u) << 4);
+      q[4 * i + 0] = (float)(lo & 0xff);
+      q[4 * i + 1] = (float)((lo >> 8) & 0xff);
+      q[4 * i + 2] = (float)((lo >> 16) & 0xff);
+      q[4 * i + 3] = (float)(lo >> 24);
+      q[16 + 4 * i + 0] = (float)(hi & 0xff);
+      q[16 + 4 * i + 1] = (float)((hi >> 8) & 0xff);
+      q[16 + 4 * i + 2] = (float)((hi >> 16) & 0xff);
+      q[16 + 4 * i + 3] = (float)(hi >> 24);
+    }
+  }
+};
+
+// ------------------------------------------------------------------------------------ Q4_0
+template <>
+struct QFmt<QT_Q4_0> {
+  static constexpr int W = 32, RUNS = 2, CHUNKS_PER_BLOCK = 1, BLOCK = 32;
+  __device__ static int chunk_k0(int c, int run) { return c * 32 + 16 * run; }
+  __device__ static void run_pos(int r, int& c, int& s0) {
+    c = r >> 1;
+    s0 = 16 * (r & 1);
+  }
+  __device__ static void load(const QWeight& w, int row, int c, RawChunk& r) {
+    const int nb = w.cols >> 5;
+    r.a = *(const uint4*)(w.p0 + ((size_t)row * nb + c) * 16);
+    r.d = *(const uint16_t*)(w.p1 + ((size_t)row * nb + c) * 2);
+  }
+  __device__ static void decode(const RawChunk& r, int c, float q[32], float sc[2], float of[2]) {
+    const float d = __half2float(__ushort_as_half((uint16_t)r.d));
+    sc[0] = sc[1] = d;
+    of[0] = of[1] = 8.f * d;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint32_t wv = u4_word(r.a, i);
+      const uint32_t lo = wv & 0x0f0f0f0fu, hi = (wv >> 4) & 0x0f0f0f0fu;
+      q[4 * i + 0] = (float)(lo & 0xff);
+      q[4 * i + 1] = (float)((lo >> 8) & 0xff);
+      q[4 * i + 2] = (float)((lo >> 16) & 0xff);
+      q[4 * i + 3] = (float)(lo >> 24);
+      q[16 + 4 * i + 0] = (float)(hi & 0xff);
+      q[16 + 4 * i + 1] = (float)((hi >> 8) & 0xff);
+      q[16 + 4 * i + 2] = (float)((hi >> 16) & 0xff);
+      q[16 + 4 * i + 3] = (float)(hi >> 24);
+    }
+  }
+};
+
+// ------------------------------------------------------------------------------------ Q8_0
+template <>
+struct QFmt<QT_Q8_0> {
+  static constexpr int W = 16, RUNS = 1, CHUNKS_PER_BLOCK = 2, BLOCK = 32;
+  __device__ static int chunk_k0(int c, int run) { return c * 16; }
+  __device__ static void run_pos(int r, int& c, int& s0) {
+    c = r;
+    s0 = 0;
+  }
+  __device__ static void load(const QWeight& w, int row, int c, RawChunk& r) {
+    const int nb = w.cols >> 5;
+    r.a = *(const uint4*)(w.p0 + (size_t)row * w.cols + c * 16);
+    r.d = *(const uint16_t*)(w.p1 + ((size_t)row * nb + (c >> 1)) * 2);
+  }
+  __device__ static void decode(const RawChunk& r, int c, float q[16], float sc[1], float of[1]) {
+    const float d = __half2float(__ushort_as_half((uint16_t)r.d));
+    sc[0] = d;
+    of[0] = 128.f * d;  // bytes re-biased to unsigned
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint32_t u = u4_word(r.a, i) ^ 0x80808080u;
+      q[4 * i + 0] = (float)(u & 0xff);
+      q[4 * i + 1] = (float)((u >> 8) & 0xff);
+      q[4 * i + 2] = (float)((u >> 16) & 0xff);
+      q[4 * i + 3] = (float)(u >> 24);
+    }
+  }
+};
+
+// ------------------------------------------------------------------------------------ F16
+template <>
+struct QFmt<QT_F16> {
+  static constexpr int W = 8, RUNS = 1, CHUNKS_PER_BLOCK = 1, BLOCK = 8;
+  __device__ static int chunk_k0(int c, int run) { return c * 8; }
+  __device__ static void load(const QWeight& w, int row, int c, RawChunk& r) {
+    r.a = *(const uint4*)(w.p0 + ((size_t)row * w.cols + c * 8) * 2);
+  }
+  __device__ static void decode(const RawChunk& r, int c, float q[8], float sc[1], float of[1]) {
+    sc[0] = 1.f;
+    of[0] = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint32_t u = u4_word(r.a, i);
+      q[2 * i] = __half2float(__ushort_as_half((uint16_t)(u & 0xffff)));
+      q[2 * i + 1] = __half2float(__ushort_as_half((uint16_t)(u >> 16)));
+    }
+  }
+};
+
+// ------------------------------------------------------------------------------------ BF16
+template <>
+struct QFmt<QT_BF16> {
+  static constexpr int W = 8, RUNS = 1, CHUNKS_PER_BLOCK = 1, BLOCK = 8;
+  __device__ static int chunk_k0(int c, int run) { return c * 8; }
+  __device__ static void load(const QWeight& w, int row, int c, RawChunk& r) {
+    r.a = *(const uint4*)(w.p0 + ((size_t)row * w.cols + c * 8) * 2);
+  }
+  __device__ static void decode(const RawChunk& r, int c, float q[8], float sc[1], float of[1]) {
+    sc[0] = 1.f;
+    of[0] = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint32_t u = u4_word(r.a, i);
+      q[2 * i] = __uint_as_float(u << 16);
+      q[2 * i + 1] = __uint_as_float(u & 0xffff0000u);
+    }
+  }
+};
+
+
+// ------------------------------------------------------------------------------------------
+// Streaming decode interface used by the GEMV: per chunk scales, then 4 weights at a time
+// (j = float4 index inside the chunk's W weights) so decoded values stay transient.
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ void ubytes4(uint32_t v, float q[4]) {
+  q[0] = (float)(v & 0xff);
+  q[1] = (float)((v >> 8) & 0xff);
+  q[2] = (float)((v >> 16) & 0xff);
+  q[3] = (float)(v >> 24);
+}
+
+template <int QT>
+struct QStream;
+
+template <>
+struct QStream<QT_Q4_K> {
+  __device__ static void scales(const RawChunk& r, int c, float* sc, float* of) {
+    const int g = (c & 7) >> 1;
+    const uint32_t dd = r.b.x;
+    const float d = __half2float(__ushort_as_half((uint16_t)(dd & 0xffff)));
+    const float dmin = __half2float(__ushort_as_half((uint16_t)(dd >> 16)));
+    const uint32_t w1 = r.b.y, w2 = r.b.z, w3 = r.b.w;
+    const int sh = 16 * (g & 1);
+    uint32_t scp, mp;
+    if (g < 2) {
+      scp = (w1 >> sh) & 0x3f3f;
+      mp = (w2 >> sh) & 0x3f3f;
+    } else {
+      scp = ((w3 >> sh) & 0x0f0f) | (((w1 >> sh) >> 2) & 0x3030);
+      mp = (((w3 >> sh) >> 4) & 0x0f0f) | (((w2 >> sh) >> 2) & 0x3030);
+    }
+    sc[0] = d * (float)(scp & 0xff);
+    sc[1] = d * (float)(scp >> 8);
+    of[0] = dmin * (float)(mp & 0xff);
+    of[1] = dmin * (float)(mp >> 8);
+  }
+  // j in 0..7: j<4 -> low nibbles of word j (run 0), j>=4 -> high nibbles of word j-4 (run 1)
+  __device__ static void quad(const RawChunk& r, int c, int j, float q[4]) {
+    const uint32_t wv = u4_word(r.a, j & 3);
+    ubytes4(j < 4 ? (wv & 0x0f0f0f0fu) : ((wv >> 4) & 0x0f0f0f0fu), q);
+  }
+};
+
+template <>
+struct QStream<QT_Q5_K> {
+  __device__ static void scales(const RawChunk& r, int c, float* sc, float* of) {
+    QStream<QT_Q4_K>::scales(r, c, sc, of);
+  }
+  __device__ static void quad(const RawChunk& r, int c, int j, float q[4]) {
+    const int g = (c & 7) >> 1;
+    const uint32_t wv = u4_word(r.a, j & 3), hv = u4_word(r.c, j & 3);
+    const uint32_t nib = j < 4 ? (wv & 0x0f0f0f0fu) : ((wv >> 4) & 0x0f0f0f0fu);
+    const uint32_t hb = (hv >> (2 * g + (j >= 4 ? 1 : 0))) & 0x01010101u;
+    ubytes4(nib | (hb << 4), q);
+  }
+};
+
+template <>
+struct QStream<QT_Q6_K> {
+  __device__ static void scales(const RawChunk& r, int c, float* sc, float* of) {
+    const int p = c & 7, n = p >> 2, o = 16 * (p & 3);
+    const int up = o >> 5, is = (o & 31) >> 4;
+    const float d = __half2float(__ushort_as_half((uint16_t)r.d));
+    const int s_lo = 8 * n + is + 2 * up, s_hi = s_lo + 4;
+    const int8_t sl = (int8_t)((u4_word(r.c, s_lo >> 2) >> (8 * (s_lo & 3))) & 0xff);
+    const int8_t shv = (int8_t)((u4_word(r.c, s_hi >> 2) >> (8 * (s_hi & 3))) & 0xff);
+    sc[0] = d * (float)sl;
+    sc[1] = d * (float)shv;
+    of[0] = 32.f * sc[0];
+    of[1] = 32.f * sc[1];
+  }
+  __device__ static void quad(const RawChunk& r, int c, int j, float q[4]) {
+    const int up = (c & 3) >> 1;   // o >= 32  <=>  (p & 3) >= 2
+    const int hs = 2 * up + (j >= 4 ? 4 : 0);
+    const uint32_t wv = u4_word(r.a, j & 3), hv = u4_word(r.b, j & 3);
+    const uint32_t nib = j < 4 ? (wv & 0x0f0f0f0fu) : ((wv >> 4) & 0x0f0f0f0fu);
+    ubytes4(nib | (((hv >> hs) & 0x03030303u) << 4), q);
+  }
+};
+
+template <>
+struct QStream<QT_Q4_0> {
+  __device__ static void scales(const RawChunk& r, int c, float* sc, float* of) {
+    const float d = __half2float(__ushort_as_half((uint16_t)r.d));
+    sc[0] = sc[1] = d;
+    of[0] = of[1] = 8.f * d;
+  }
+  __device__ static void quad(const RawChunk& r, int c, int j, float q[4]) {
+    const uint32_t wv = u4_word(r.a, j & 3);
+    ubytes4(j < 4 ? (wv & 0x0f0f0f0fu) : ((wv >> 4) & 0x0f0f0f0fu), q);
+  }
+};
+
+template <>
+struct QStream<QT_Q8_0> {
+  __device__ static void scales(const RawChunk& r, int c, float* sc, float* of) {
+    const float d = __half2float(__ushort_as_half((uint16_t)r.d));
+    sc[0] = d;
+    of[0] = 128.f * d;
+  }
+  __device__ static void quad(const RawChunk& r, int c, int j, float q[4]) {
+    ubytes4(u4_word(r.a, j) ^ 0x80808080u, q);
+  }
+};
+
+template <>
+struct QStream<QT_F16> {
+  __device__ static void scales(const RawChunk& r, int c, float* sc, float* of) { sc[0] = 1.f; of[0] = 0.f; }
+  __device__ static void quad(const RawChunk& r, int c, int j, float q[4]) {
+    const uint32_t u0 = u4_word(r.a, 2 * j), u1 = u4_word(r.a, 2 * j + 1);
+    q[0] = __half2float(__ushort_as_half((uint16_t)(u0 & 0xffff)));
+    q[1] = __half2float(__ushort_as_half((uint16_t)(u0 >> 16)));
+    q[2] = __half2float(__ushort_as_half((uint16_t)(u1 & 0xffff)));
+    q[3] = __half2float(__ushort_as_half((uint16_t)(u1 >> 16)));
+  }
+};
+
+template <>
+struct QStream<QT_BF16> {
+  __device__ static void scales(const RawChunk& r, int c, float* sc, float* of) { sc[0] = 1.f; of[0] = 0.f; }
+  __device__ static void quad(const RawChunk& r, int c, int j, float q[4]) {
+    const uint32_t u0 = u4_word(r.a, 2 * j), u1 = u4_word(r.a, 2 * j + 1);
+    q[0] = __uint_as_float(u0 << 16);
+    q[1] = __uint_as_float(u0 & 0xffff0000u);
+    q[2] = __uint_as_float(u1 << 16);
+    q[3] = __uint_as_float(u1 & 0xffff0000u);
+  }
+};
+
+}  // namespace aios

@@ -1,0 +1,387 @@
+"""GGML block-quant formats: CPU reference (numpy) dequantizers and simple quantizers.
+
+This is the bit-exact oracle the HIP dequant kernels are tested against.  The
+byte layouts are the public GGUF/ggml block formats that the reference's
+llama-server consumes (`runtime/src/model_manager.rs:187-204` spawns it on
+Q4_K_M GGUF files, `scripts/download-models.sh:70-77`).  SURVEY.md §2.7 K3/K12
+lists the formats a Q4_K_M file contains (Q4_K, Q6_K, plus Q5_K/Q8_0/Q4_0/F16/BF16).
+
+Quantizers here are deliberately simple (min/max per sub-block): they produce
+valid blocks for synthetic random-init models; only dequantization has to match
+ggml exactly.
+"""
+from __future__ import annotations
+
+import enum
+
+import numpy as np
+
+
+class GGMLType(enum.IntEnum):
+    F32 = 0
+    F16 = 1
+    Q4_0 = 2
+    Q4_1 = 3
+    Q5_0 = 6
+    Q5_1 = 7
+    Q8_0 = 8
+    Q8_1 = 9
+    Q2_K = 10
+    Q3_K = 11
+    Q4_K = 12
+    Q5_K = 13
+    Q6_K = 14
+    Q8_K = 15
+    BF16 = 30
+
+
+QK_K = 256
+
+# (elements per block, bytes per block)
+BLOCK_INFO = {
+    GGMLType.F32: (1, 4),
+    GGMLType.F16: (1, 2),
+    GGMLType.BF16: (1, 2),
+    GGMLType.Q4_0: (32, 18),
+    GGMLType.Q4_1: (32, 20),
+    GGMLType.Q5_0: (32, 22),
+    GGMLType.Q5_1: (32, 24),
+    GGMLType.Q8_0: (32, 34),
+    GGMLType.Q4_K: (256, 144),
+    GGMLType.Q5_K: (256, 176),
+    GGMLType.Q6_K: (256, 210),
+}
+
+
+def type_size(t: GGMLType, n_elements: int) -> int:
+    blk, nbytes = BLOCK_INFO[GGMLType(t)]
+    if n_elements % blk:
+        raise ValueError(f"{GGMLType(t).name}: {n_elements} not a multiple of {blk}")
+    return n_elements // blk * nbytes
+
+
+def _f16(b: np.ndarray) -> np.ndarray:
+    """View trailing 2 bytes as float16 -> float32."""
+    return np.ascontiguousarray(b).view(np.float16).astype(np.float32)
+
+
+# ----------------------------------------------------------------------------------
+# dequantizers: raw bytes [n_blocks * block_bytes] -> float32 [n_blocks * block_elems]
+# ----------------------------------------------------------------------------------
+
+def _blocks(raw: np.ndarray, t: GGMLType) -> np.ndarray:
+    _, nb = BLOCK_INFO[t]
+    raw = np.frombuffer(raw, dtype=np.uint8) if not isinstance(raw, np.ndarray) else raw.view(np.uint8)
+    assert raw.size % nb == 0, (raw.size, nb)
+    return raw.reshape(-1, nb)
+
+
+def dequant_q4_0(raw) -> np.ndarray:
+    b = _blocks(raw, GGMLType.Q4_0)
+    d = _f16(b[:, 0:2]).reshape(-1, 1)
+    qs = b[:, 2:18]
+    lo = (qs & 0x0F).astype(np.int32) - 8
+    hi = (qs >> 4).astype(np.int32) - 8
+    return (np.concatenate([lo, hi], axis=1) * d).astype(np.float32).ravel()
+
+
+def dequant_q4_1(raw) -> np.ndarray:
+    b = _blocks(raw, GGMLType.Q4_1)
+    d = _f16(b[:, 0:2]).reshape(-1, 1)
+    m = _f16(b[:, 2:4]).reshape(-1, 1)
+    qs = b[:, 4:20]
+    q = np.concatenate([qs & 0x0F, qs >> 4], axis=1).astype(np.float32)
+    return (q * d + m).astype(np.float32).ravel()
+
+
+def _q5_high(b: np.ndarray, off: int) -> np.ndarray:
+    qh = np.ascontiguousarray(b[:, off:off + 4]).view(np.uint32).reshape(-1, 1)
+    j = np.arange(16, dtype=np.uint32).reshape(1, -1)
+    h0 = ((qh >> j) << 4) & 0x10
+    h1 = (qh >> (j + 12)) & 0x10
+    return h0.astype(np.int32), h1.astype(np.int32)
+
+
+def dequant_q5_0(raw) -> np.ndarray:
+    b = _blocks(raw, GGMLType.Q5_0)
+    d = _f16(b[:, 0:2]).reshape(-1, 1)
+    h0, h1 = _q5_high(b, 2)
+    qs = b[:, 6:22].astype(np.int32)
+    x0 = ((qs & 0x0F) | h0) - 16
+    x1 = ((qs >> 4) | h1) - 16
+    return (np.concatenate([x0, x1], axis=1) * d).astype(np.float32).ravel()
+
+
+def dequant_q5_1(raw) -> np.ndarray:
+    b = _blocks(raw, GGMLType.Q5_1)
+    d = _f16(b[:, 0:2]).reshape(-1, 1)
+    m = _f16(b[:, 2:4]).reshape(-1, 1)
+    h0, h1 = _q5_high(b, 4)
+    qs = b[:, 8:24].astype(np.int32)
+    x0 = (qs & 0x0F) | h0
+    x1 = (qs >> 4) | h1
+    return (np.concatenate([x0, x1], axis=1) * d + m).astype(np.float32).ravel()
+
+
+def dequant_q8_0(raw) -> np.ndarray:
+    b = _blocks(raw, GGMLType.Q8_0)
+    d = _f16(b[:, 0:2]).reshape(-1, 1)
+    q = b[:, 2:34].view(np.int8).astype(np.float32)
+    return (q * d).astype(np.float32).ravel()
+
+
+def kquant_scale_min(scales: np.ndarray):
+    """Unpack the 12-byte 6-bit (scale, min) table of Q4_K/Q5_K -> two [nb, 8] int arrays."""
+    q = scales.astype(np.int32)
+    sc = np.empty((q.shape[0], 8), np.int32)
+    mn = np.empty((q.shape[0], 8), np.int32)
+    for j in range(8):
+        if j < 4:
+            sc[:, j] = q[:, j] & 63
+            mn[:, j] = q[:, j + 4] & 63
+        else:
+            sc[:, j] = (q[:, j + 4] & 0xF) | ((q[:, j - 4] >> 6) << 4)
+            mn[:, j] = (q[:, j + 4] >> 4) | ((q[:, j] >> 6) << 4)
+    return sc, mn
+
+
+def kquant_pack_scale_min(sc: np.ndarray, mn: np.ndarray) -> np.ndarray:
+    """Inverse of kquant_scale_min: [nb,8] 6-bit values -> [nb,12] bytes."""
+    sc = sc.astype(np.int32)
+    mn = mn.astype(np.int32)
+    out = np.zeros((sc.shape[0], 12), np.int32)
+    for j in range(8):
+        if j < 4:
+            out[:, j] |= sc[:, j] & 63
+            out[:, j + 4] |= mn[:, j] & 63
+        else:
+            out[:, j + 4] |= (sc[:, j] & 0xF) | ((mn[:, j] & 0xF) << 4)
+            out[:, j - 4] |= (sc[:, j] >> 4) << 6
+            out[:, j] |= (mn[:, j] >> 4) << 6
+    return out.astype(np.uint8)
+
+
+def dequant_q4_k(raw) -> np.ndarray:
+    b = _blocks(raw, GGMLType.Q4_K)
+    d = _f16(b[:, 0:2]).reshape(-1, 1)
+    dmin = _f16(b[:, 2:4]).reshape(-1, 1)
+    sc, mn = kquant_scale_min(b[:, 4:16])
+    qs = b[:, 16:144].reshape(-1, 4, 32)
+    out = np.empty((b.shape[0], 4, 2, 32), np.float32)
+    for g in range(4):
+        d1 = d * sc[:, 2 * g:2 * g + 1]
+        m1 = dmin * mn[:, 2 * g:2 * g + 1]
+        d2 = d * sc[:, 2 * g + 1:2 * g + 2]
+        m2 = dmin * mn[:, 2 * g + 1:2 * g + 2]
+        out[:, g, 0] = d1 * (qs[:, g] & 0xF) - m1
+        out[:, g, 1] = d2 * (qs[:, g] >> 4) - m2
+    return out.ravel()
+
+
+def dequant_q5_k(raw) -> np.ndarray:
+    b = _blocks(raw, GGMLType.Q5_K)
+    d = _f16(b[:, 0:2]).reshape(-1, 1)
+    dmin = _f16(b[:, 2:4]).reshape(-1, 1)
+    sc, mn = kquant_scale_min(b[:, 4:16])
+    qh = b[:, 16:48]
+    qs = b[:, 48:176].reshape(-1, 4, 32)
+    out = np.empty((b.shape[0], 4, 2, 32), np.float32)
+    for g in range(4):
+        d1 = d * sc[:, 2 * g:2 * g + 1]
+        m1 = dmin * mn[:, 2 * g:2 * g + 1]
+        d2 = d * sc[:, 2 * g + 1:2 * g + 2]
+        m2 = dmin * mn[:, 2 * g + 1:2 * g + 2]
+        h1 = ((qh >> (2 * g)) & 1).astype(np.int32) * 16
+        h2 = ((qh >> (2 * g + 1)) & 1).astype(np.int32) * 16
+        out[:, g, 0] = d1 * ((qs[:, g] & 0xF) + h1) - m1
+        out[:, g, 1] = d2 * ((qs[:, g] >> 4) + h2) - m2
+    return out.ravel()
+
+
+def dequant_q6_k(raw) -> np.ndarray:
+    b = _blocks(raw, GGMLType.Q6_K)
+    ql = b[:, 0:128].astype(np.int32)
+    qh = b[:, 128:192].astype(np.int32)
+    sc = b[:, 192:208].view(np.int8).astype(np.float32)
+    d = _f16(b[:, 208:210]).reshape(-1, 1)
+    out = np.empty((b.shape[0], 2, 4, 32), np.float32)
+    for n in range(2):
+        l0 = ql[:, 64 * n:64 * n + 32]
+        l1 = ql[:, 64 * n + 32:64 * n + 64]
+        h = qh[:, 32 * n:32 * n + 32]
+        s = sc[:, 8 * n:8 * n + 8]
+        q1 = ((l0 & 0xF) | (((h >> 0) & 3) << 4)) - 32
+        q2 = ((l1 & 0xF) | (((h >> 2) & 3) << 4)) - 32
+        q3 = ((l0 >> 4) | (((h >> 4) & 3) << 4)) - 32
+        q4 = ((l1 >> 4) | (((h >> 6) & 3) << 4)) - 32
+        # scale index is = l/16 (+0,+2,+4,+6)
+        for k, q in enumerate((q1, q2, q3, q4)):
+            sidx = np.repeat(np.array([0, 1]) + 2 * k, 16)
+            out[:, n, k] = d * s[:, sidx] * q
+    return out.ravel()
+
+
+def dequant_f16(raw) -> np.ndarray:
+    return np.frombuffer(raw, dtype=np.float16).astype(np.float32) if not isinstance(raw, np.ndarray) \
+        else raw.view(np.float16).astype(np.float32).ravel()
+
+
+def dequant_bf16(raw) -> np.ndarray:
+    u = (np.frombuffer(raw, dtype=np.uint16) if not isinstance(raw, np.ndarray) else raw.view(np.uint16).ravel())
+    return (u.astype(np.uint32) << 16).view(np.float32)
+
+
+def dequant_f32(raw) -> np.ndarray:
+    return (np.frombuffer(raw, dtype=np.float32) if not isinstance(raw, np.ndarray) else raw.view(np.float32).ravel()).copy()
+
+
+DEQUANT = {
+    GGMLType.F32: dequant_f32,
+    GGMLType.F16: dequant_f16,
+    GGMLType.BF16: dequant_bf16,
+    GGMLType.Q4_0: dequant_q4_0,
+    GGMLType.Q4_1: dequant_q4_1,
+    GGMLType.Q5_0: dequant_q5_0,
+    GGMLType.Q5_1: dequant_q5_1,
+    GGMLType.Q8_0: dequant_q8_0,
+    GGMLType.Q4_K: dequant_q4_k,
+    GGMLType.Q5_K: dequant_q5_k,
+    GGMLType.Q6_K: dequant_q6_k,
+}
+
+
+def dequantize(raw, t: GGMLType, shape=None) -> np.ndarray:
+    out = DEQUANT[GGMLType(t)](raw)
+    return out.reshape(shape) if shape is not None else out
+
+
+# ----------------------------------------------------------------------------------
+# quantizers (float32 [n] -> raw bytes)
+# ----------------------------------------------------------------------------------
+
+def _to_f16_bytes(x: np.ndarray) -> np.ndarray:
+    return x.astype(np.float16).reshape(-1, 1).view(np.uint8).reshape(-1, 2)
+
+
+def quant_q4_0(x: np.ndarray) -> np.ndarray:
+    x = x.astype(np.float32).reshape(-1, 32)
+    amax_idx = np.argmax(np.abs(x), axis=1)
+    mx = x[np.arange(x.shape[0]), amax_idx]
+    d = mx / -8.0
+    dh = d.astype(np.float16).astype(np.float32)
+    inv = np.where(dh != 0, 1.0 / np.where(dh == 0, 1, dh), 0.0).reshape(-1, 1)
+    q = np.clip(np.floor(x * inv + 8.5), 0, 15).astype(np.uint8)
+    qs = (q[:, :16] | (q[:, 16:] << 4)).astype(np.uint8)
+    return np.concatenate([_to_f16_bytes(dh), qs], axis=1).ravel()
+
+
+def quant_q8_0(x: np.ndarray) -> np.ndarray:
+    x = x.astype(np.float32).reshape(-1, 32)
+    amax = np.abs(x).max(axis=1)
+    d = (amax / 127.0).astype(np.float16).astype(np.float32)
+    inv = np.where(d != 0, 1.0 / np.where(d == 0, 1, d), 0.0).reshape(-1, 1)
+    q = np.clip(np.round(x * inv), -127, 127).astype(np.int8)
+    return np.concatenate([_to_f16_bytes(d), q.view(np.uint8)], axis=1).ravel()
+
+
+def _kquant_affine(x: np.ndarray, nmax: int):
+    """x [nb, 8, 32] -> (d, dmin f16-rounded [nb], sc6, mn6 [nb,8], q [nb,8,32] in 0..nmax)."""
+    lo = np.minimum(x.min(axis=2), 0.0)  # min is stored as a positive offset: y = d*sc*q - dmin*m
+    hi = x.max(axis=2)
+    scale = (hi - lo) / nmax
+    mins = -lo
+    max_scale = scale.max(axis=1)
+    max_min = mins.max(axis=1)
+    d = (max_scale / 63.0).astype(np.float16).astype(np.float32)
+    dmin = (max_min / 63.0).astype(np.float16).astype(np.float32)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        sc = np.where(d[:, None] > 0, np.round(scale / d[:, None]), 0).clip(0, 63).astype(np.int32)
+        mn = np.where(dmin[:, None] > 0, np.round(mins / dmin[:, None]), 0).clip(0, 63).astype(np.int32)
+        eff_d = d[:, None] * sc
+        eff_m = dmin[:, None] * mn
+        q = np.where(eff_d[..., None] > 0, np.round((x + eff_m[..., None]) / eff_d[..., None]), 0)
+    q = q.clip(0, nmax).astype(np.int32)
+    return d, dmin, sc, mn, q
+
+
+def quant_q4_k(x: np.ndarray) -> np.ndarray:
+    x = x.astype(np.float32).reshape(-1, 8, 32)
+    d, dmin, sc, mn, q = _kquant_affine(x, 15)
+    qs = np.empty((x.shape[0], 4, 32), np.uint8)
+    for g in range(4):
+        qs[:, g] = (q[:, 2 * g] | (q[:, 2 * g + 1] << 4)).astype(np.uint8)
+    return np.concatenate([_to_f16_bytes(d), _to_f16_bytes(dmin), kquant_pack_scale_min(sc, mn),
+                           qs.reshape(-1, 128)], axis=1).ravel()
+
+
+def quant_q5_k(x: np.ndarray) -> np.ndarray:
+    x = x.astype(np.float32).reshape(-1, 8, 32)
+    d, dmin, sc, mn, q = _kquant_affine(x, 31)
+    qs = np.empty((x.shape[0], 4, 32), np.uint8)
+    qh = np.zeros((x.shape[0], 32), np.int32)
+    for g in range(4):
+        a, b = q[:, 2 * g], q[:, 2 * g + 1]
+        qs[:, g] = ((a & 0xF) | ((b & 0xF) << 4)).astype(np.uint8)
+        qh |= ((a >> 4) & 1) << (2 * g)
+        qh |= ((b >> 4) & 1) << (2 * g + 1)
+    return np.concatenate([_to_f16_bytes(d), _to_f16_bytes(dmin), kquant_pack_scale_min(sc, mn),
+                           qh.astype(np.uint8), qs.reshape(-1, 128)], axis=1).ravel()
+
+
+def quant_q6_k(x: np.ndarray) -> np.ndarray:
+    x = x.astype(np.float32).reshape(-1, 16, 16)
+    amax_idx = np.argmax(np.abs(x), axis=2)
+    mx = np.take_along_axis(x, amax_idx[..., None], axis=2)[..., 0]
+    scale = mx / -32.0  # per 16-elem sub-block
+    amax_s_idx = np.argmax(np.abs(scale), axis=1)
+    smax = scale[np.arange(x.shape[0]), amax_s_idx]
+    d = (smax / -128.0).astype(np.float16).astype(np.float32)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        sc = np.where(d[:, None] != 0, np.round(scale / d[:, None]), 0).clip(-128, 127).astype(np.int32)
+        eff = d[:, None] * sc
+        q = np.where(eff[..., None] != 0, np.round(x / eff[..., None]), 0)
+    q = (q.clip(-32, 31) + 32).astype(np.int32).reshape(-1, 256)
+    nb = x.shape[0]
+    ql = np.zeros((nb, 128), np.int32)
+    qh = np.zeros((nb, 64), np.int32)
+    for n in range(2):
+        base = 128 * n
+        q1 = q[:, base + 0:base + 32]
+        q2 = q[:, base + 32:base + 64]
+        q3 = q[:, base + 64:base + 96]
+        q4 = q[:, base + 96:base + 128]
+        ql[:, 64 * n:64 * n + 32] = (q1 & 0xF) | ((q3 & 0xF) << 4)
+        ql[:, 64 * n + 32:64 * n + 64] = (q2 & 0xF) | ((q4 & 0xF) << 4)
+        qh[:, 32 * n:32 * n + 32] = (q1 >> 4) | ((q2 >> 4) << 2) | ((q3 >> 4) << 4) | ((q4 >> 4) << 6)
+    return np.concatenate([ql.astype(np.uint8), qh.astype(np.uint8), sc.astype(np.int8).view(np.uint8),
+                           _to_f16_bytes(d)], axis=1).ravel()
+
+
+def quant_f16(x):
+    return x.astype(np.float16).view(np.uint8).ravel()
+
+
+def quant_bf16(x):
+    u = x.astype(np.float32).view(np.uint32)
+    r = ((u + 0x7FFF + ((u >> 16) & 1)) >> 16).astype(np.uint16)
+    return r.view(np.uint8).ravel()
+
+
+def quant_f32(x):
+    return x.astype(np.float32).view(np.uint8).ravel()
+
+
+QUANT = {
+    GGMLType.F32: quant_f32,
+    GGMLType.F16: quant_f16,
+    GGMLType.BF16: quant_bf16,
+    GGMLType.Q4_0: quant_q4_0,
+    GGMLType.Q8_0: quant_q8_0,
+    GGMLType.Q4_K: quant_q4_k,
+    GGMLType.Q5_K: quant_q5_k,
+    GGMLType.Q6_K: quant_q6_k,
+}
+
+
+def quantize(x: np.ndarray, t: GGMLType) -> np.ndarray:
+    return QUANT[GGMLType(t)](np.ascontiguousarray(x, dtype=np.float32).ravel())

@@ -1,0 +1,83 @@
+"""GGUF -> native engine loader (SURVEY.md §3.4 `load`, §2.7 K12).
+
+Replaces `ModelManager::load_model` spawning llama-server (`runtime/src/model_manager.rs:149-277`):
+the file is memory-mapped, each tensor's raw block bytes are handed zero-copy to the engine,
+which uploads them to HBM and repacks them into the GEMV/MFMA layout.  Under tensor
+parallelism each rank receives only its shard: column-parallel Q/K/V/gate/up (whole heads /
+rows), row-parallel attn_output/ffn_down (whole quant blocks along K), replicated embeddings,
+norms and lm_head (SURVEY.md §2.9 TP row).
+"""
+from __future__ import annotations
+
+import time
+from typing import Optional
+
+import numpy as np
+
+from ..gguf.quants import BLOCK_INFO, GGMLType
+from ..gguf.reader import GGUFReader
+from ..models.config import ModelConfig
+from . import native
+
+COLUMN_PARALLEL = ("attn_q.weight", "attn_k.weight", "attn_v.weight", "ffn_gate.weight", "ffn_up.weight",
+                   "attn_q.bias", "attn_k.bias", "attn_v.bias")
+ROW_PARALLEL = ("attn_output.weight", "ffn_down.weight")
+
+
+def shard_tensor(name: str, raw: np.ndarray, ggml_type: int, rows: int, cols: int, rank: int, tp: int):
+    """Return (raw_shard, rows, cols) of this rank's slice of a GGUF tensor."""
+    if tp == 1:
+        return raw, rows, cols
+    short = name.split(".", 2)[-1] if name.startswith("blk.") else name
+    blk, bpb = BLOCK_INFO[GGMLType(ggml_type)]
+    if short in COLUMN_PARALLEL:
+        if short.endswith(".bias"):  # 1-D: rows == 1, cols == n
+            n = cols // tp
+            return raw.view(np.uint8).reshape(cols, -1)[rank * n:(rank + 1) * n].ravel(), 1, n
+        if rows % tp:
+            raise ValueError(f"{name}: {rows} rows not divisible by TP={tp}")
+        n = rows // tp
+        rb = raw.size // rows
+        return raw[rank * n * rb:(rank + 1) * n * rb], n, cols
+    if short in ROW_PARALLEL:
+        nblk = cols // blk
+        if nblk % tp:
+            raise ValueError(f"{name}: K={cols} not divisible into whole {blk}-blocks for TP={tp}")
+        nb = nblk // tp
+        r = raw.reshape(rows, nblk, bpb)[:, rank * nb:(rank + 1) * nb, :]
+        return np.ascontiguousarray(r).ravel(), rows, nb * blk
+    return raw, rows, cols
+
+
+def load_engine(path: str, max_ctx: Optional[int] = None, max_slots: int = 4, max_batch: int = 8, device: int = 0,
+                tp_rank: int = 0, tp_size: int = 1, name: Optional[str] = None, verbose: bool = False):
+    """Load a GGUF file into a native Engine on `device`. Returns (engine, ModelConfig, reader)."""
+    m = native.require()
+    t0 = time.time()
+    r = GGUFReader(path)
+    cfg = ModelConfig.from_gguf(r, name=name)
+    ec = native.engine_config(cfg, max_ctx=max_ctx or min(cfg.max_ctx, 4096), max_slots=max_slots,
+                              max_batch=max_batch, device=device, tp_rank=tp_rank, tp_size=tp_size)
+    eng = m.Engine(ec)
+    for tname, ti in r.tensors.items():
+        raw = r.tensor_array(tname)
+        rows, cols = ti.rows, ti.cols
+        raw, rows, cols = shard_tensor(tname, raw, int(ti.ggml_type), rows, cols, tp_rank, tp_size)
+        eng.set_tensor(tname, int(ti.ggml_type), rows, cols, raw)
+    eng.finalize()
+    if verbose:
+        print(f"[loader] {cfg.name}: {eng.weight_bytes / 1e9:.2f} GB weights, {eng.kv_bytes / 1e9:.2f} GB KV, "
+              f"{time.time() - t0:.1f}s")
+    return eng, cfg, r
+
+
+def random_engine(cfg: ModelConfig, recipe: str = "Q4_K_M", seed: int = 0, max_ctx: Optional[int] = None,
+                  max_slots: int = 4, max_batch: int = 8, device: int = 0, tp_rank: int = 0, tp_size: int = 1):
+    """Engine with random-init weights of `cfg`'s architecture generated directly in HBM."""
+    m = native.require()
+    ec = native.engine_config(cfg, max_ctx=max_ctx or min(cfg.max_ctx, 4096), max_slots=max_slots,
+                              max_batch=max_batch, device=device, tp_rank=tp_rank, tp_size=tp_size)
+    eng = m.Engine(ec)
+    eng.init_random(recipe, seed)
+    eng.finalize()
+    return eng

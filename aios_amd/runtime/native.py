@@ -1,0 +1,92 @@
+"""Loader for the native engine extension (`aios_amd/_engine*.so`).
+
+torch is imported first on purpose: torch-ROCm bundles `libamdhip64.so.7`; importing it before
+the extension makes the dynamic loader resolve our DT_NEEDED entry to that same runtime, so one
+process never holds two HIP runtimes.
+
+On a machine with a GPU the extension is mandatory: `require()` raises instead of silently
+falling back to a Python path (the round-end checks record which .so files were loaded).
+"""
+from __future__ import annotations
+
+import importlib
+import os
+from typing import Optional
+
+_mod = None
+_err: Optional[BaseException] = None
+
+
+def load(build_if_missing: bool = True):
+    global _mod, _err
+    if _mod is not None:
+        return _mod
+    try:
+        import torch  # noqa: F401  (see module docstring)
+    except Exception:  # pragma: no cover - torch is present in this image
+        pass
+    try:
+        _mod = importlib.import_module("aios_amd._engine")
+        return _mod
+    except ImportError as e:
+        _err = e
+    if build_if_missing and os.environ.get("AIOS_NO_AUTOBUILD") != "1":
+        from .. import _build
+
+        _build.build(verbose=False)
+        importlib.invalidate_caches()
+        _mod = importlib.import_module("aios_amd._engine")
+        return _mod
+    raise ImportError(f"aios_amd native engine not built: {_err}")
+
+
+def available() -> bool:
+    try:
+        load(build_if_missing=False)
+        return True
+    except Exception:
+        return False
+
+
+def gpu_available() -> bool:
+    try:
+        import torch
+
+        return torch.cuda.is_available() and torch.cuda.device_count() > 0
+    except Exception:
+        return False
+
+
+def require():
+    """The native engine, loudly: on a GPU box a missing extension is an error."""
+    return load(build_if_missing=True)
+
+
+def engine_config(cfg, max_ctx: Optional[int] = None, max_slots: int = 4, max_batch: int = 8, device: int = 0,
+                  tp_rank: int = 0, tp_size: int = 1):
+    """aios_amd.models.config.ModelConfig -> native EngineConfig (per-rank shapes under TP)."""
+    m = require()
+    ec = m.EngineConfig()
+    ec.name = cfg.name
+    ec.vocab_size = cfg.vocab_size
+    ec.d_model = cfg.d_model
+    ec.n_layers = cfg.n_layers
+    if cfg.n_heads % tp_size or cfg.n_kv_heads % tp_size or cfg.d_ff % tp_size:
+        raise ValueError(f"TP={tp_size} does not divide heads/kv_heads/d_ff of {cfg.name}")
+    ec.n_heads = cfg.n_heads // tp_size
+    ec.n_kv_heads = cfg.n_kv_heads // tp_size
+    ec.head_dim = cfg.head_dim
+    ec.d_ff = cfg.d_ff // tp_size
+    ec.rope_theta = float(cfg.rope_theta)
+    ec.rope_neox = 1 if cfg.rope_mode == 2 else 0
+    ec.norm_eps = float(cfg.norm_eps)
+    ec.max_ctx = int(max_ctx or cfg.max_ctx)
+    ec.max_slots = max_slots
+    ec.max_batch = max_batch
+    ec.tie_embeddings = int(cfg.tie_embeddings)
+    ec.qk_norm = int(cfg.qk_norm)
+    ec.qkv_bias = int(cfg.qkv_bias)
+    ec.tp_rank = tp_rank
+    ec.tp_size = tp_size
+    ec.device = device
+    return ec

@@ -1,0 +1,158 @@
+#!/usr/bin/env python3
+"""Headline benchmark: decode tokens/sec of Mistral-7B Q4_K_M on MI355X (BASELINE.json metric #1).
+
+One process per GPU (torchrun / torch.distributed, RCCL backend on ROCm).  Each rank serves its
+own co-resident replica -- the agent router's request-level data parallelism (SURVEY.md §2.9 DP
+row) -- so per-GPU work is fixed as N grows ("weak" scaling) and `value` is the whole-job
+aggregate: total decoded tokens / max-over-ranks wall time.
+
+Per rank: random-init Mistral-7B weights in the exact Q4_K_M per-tensor layout (Q6_K lm_head and
+"more bits" attn_v/ffn_down, Q4_K elsewhere; ~4.1 GB) generated directly in HBM (no network ->
+no real checkpoint), a synthetic prompt prefilled into the KV cache, W untimed warmup decode
+steps, then exactly K timed decode steps, each the full forward (embed, 32 blocks, lm_head,
+on-device greedy sampling) replayed from a captured hipGraph with the sampled token fed back on
+device.  Baseline: the reference's GPU target "<100 ms for a 50-token Mistral-7B response"
+(docs/phases/04-AI-RUNTIME.md:334) => 500 tok/s.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+BASELINE_MISTRAL_TOKS = 500.0   # Mistral-7B GPU target => >= 500 tok/s
+BASELINE_TINYLLAMA_TOKS = 250.0  # TinyLlama target  => >= 250 tok/s
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=256)
+    ap.add_argument("--warmup", type=int, default=16)
+    ap.add_argument("--batch", type=int, default=1, help="concurrent sequences per GPU (decode batch)")
+    ap.add_argument("--prompt", type=int, default=128, help="prompt tokens prefilled before decoding")
+    ap.add_argument("--model", default="mistral-7b")
+    ap.add_argument("--recipe", default="Q4_K_M")
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-secondary", action="store_true", help="skip the TinyLlama secondary measurement")
+    return ap.parse_args()
+
+
+def measure(preset: str, recipe: str, batch: int, prompt: int, steps: int, warmup: int, use_graph: bool, dist,
+            device: int):
+    import torch
+
+    from aios_amd.models.config import get_preset
+    from aios_amd.runtime.loader import random_engine
+
+    cfg = get_preset(preset)
+    max_ctx = ((prompt + warmup + steps + 2 + 63) // 64) * 64
+    eng = random_engine(cfg, recipe, seed=1234, max_ctx=max_ctx, max_slots=max(batch, 1), max_batch=batch,
+                        device=device)
+    slots = list(range(batch))
+    toks = []
+    for s in slots:
+        p = [cfg.bos_id] + [(7 * i + 13 * s) % (cfg.vocab_size - 3) + 3 for i in range(prompt - 1)]
+        toks.append(int(eng.prefill(s, p, 0, True).argmax()))
+    eng.decode_loop_prepare(slots, toks, [prompt] * batch)
+    eng.decode_loop_run(batch, warmup, use_graph)
+    eng.synchronize()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    t0 = time.perf_counter()
+    eng.decode_loop_run(batch, steps, use_graph)
+    eng.synchronize()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    hist = eng.decode_loop_history(batch, prompt + warmup + 1, steps)
+    assert all(0 <= t < cfg.vocab_size for t in hist), "invalid token ids from decode loop"
+    info = dict(weight_gb=round(eng.weight_bytes / 1e9, 3), kv_gb=round(eng.kv_bytes / 1e9, 3))
+    del eng
+    return dt, info
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+
+    dist = None
+    if world > 1:
+        import torch.distributed as td
+
+        torch.cuda.set_device(local)
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        td.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dist = td
+    else:
+        torch.cuda.set_device(local)
+
+    dt, info = measure(args.model, args.recipe, args.batch, args.prompt, args.steps, args.warmup,
+                       not args.no_graph, dist, local)
+    secondary = None
+    if not args.no_secondary:
+        dt2, _ = measure("tinyllama-1.1b", "Q4_K_M", 1, args.prompt, args.steps, args.warmup,
+                         not args.no_graph, dist, local)
+        secondary = dt2
+
+    # max over ranks
+    if dist is not None:
+        t = torch.tensor([dt, secondary or 0.0], device="cuda", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt, secondary = float(t[0]), (float(t[1]) if secondary is not None else None)
+    n = world
+    total_tokens = n * args.batch * args.steps
+    value = total_tokens / dt
+    if rank == 0:
+        out = {
+            "metric": "decode tokens/sec Mistral-7B Q4_K (aggregate over GPUs)",
+            "value": round(value, 2),
+            "unit": "tokens/s",
+            "n_gpus": n,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(dt / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": round(value / (BASELINE_MISTRAL_TOKS * 1.0), 3),
+            "dtype": "fp32",
+            "data": "synthetic (random-init Q4_K_M weights of the Mistral-7B architecture, synthetic prompt)",
+            "config": {
+                "model": "Mistral-7B-Instruct-v0.2 Q4_K_M (architecture: d4096 L32 H32/8 ff14336 V32000)",
+                "global_batch": n * args.batch,
+                "seq_len": args.prompt + args.warmup + args.steps,
+                "parallelism": f"dp{n}",
+                "weights": args.recipe,
+                "activations": "fp32 (fp32 accumulate), KV cache bf16",
+                "per_gpu_batch": args.batch,
+                "prompt_tokens": args.prompt,
+                "hipgraph": not args.no_graph,
+                **info,
+            },
+        }
+        if secondary is not None:
+            tl = n * args.steps / secondary
+            out["secondary"] = {
+                "metric": "decode tokens/sec TinyLlama-1.1B Q4_K_M (aggregate)",
+                "value": round(tl, 2),
+                "ms_per_step": round(secondary / args.steps * 1e3, 4),
+                "vs_baseline": round(tl / BASELINE_TINYLLAMA_TOKS, 3),
+            }
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

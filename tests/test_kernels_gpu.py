@@ -1,0 +1,267 @@
+"""GPU numerics: every HIP kernel against a plain PyTorch fp32 reference of the same op."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from aios_amd.gguf.quants import GGMLType, dequantize, quantize
+
+pytestmark = pytest.mark.gpu
+
+QTS = [GGMLType.Q4_K, GGMLType.Q6_K, GGMLType.Q5_K, GGMLType.Q4_0, GGMLType.Q8_0, GGMLType.F16, GGMLType.BF16]
+
+
+@pytest.fixture(scope="module")
+def E():
+    from aios_amd.runtime import native
+
+    return native.require()
+
+
+def stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def qmat(E, t, rows, cols, seed=0, std=0.05):
+    rng = np.random.default_rng(seed)
+    x = rng.standard_normal((rows, cols)).astype(np.float32) * std
+    raw = quantize(x, t)
+    ref = torch.from_numpy(dequantize(raw, t).reshape(rows, cols).copy())
+    return E.QMatrix(int(t), rows, cols, raw), ref
+
+
+@pytest.mark.parametrize("t", QTS)
+def test_dequant_exact(E, t):
+    m, ref = qmat(E, t, 16, 512, seed=1)
+    out = torch.empty(16, 512, dtype=torch.bfloat16, device="cuda")
+    m.dequant_bf16(out.data_ptr(), stream())
+    torch.cuda.synchronize()
+    assert torch.equal(out.cpu(), ref.to(torch.bfloat16))
+
+
+@pytest.mark.parametrize("t", QTS)
+def test_get_rows(E, t):
+    m, ref = qmat(E, t, 32, 256, seed=2)
+    rows = torch.tensor([3, 0, 31, 7], dtype=torch.int32, device="cuda")
+    out = torch.empty(4, 256, device="cuda")
+    m.get_rows(rows.data_ptr(), 4, out.data_ptr(), 256, stream())
+    torch.cuda.synchronize()
+    assert torch.allclose(out.cpu(), ref[rows.cpu().long()], atol=1e-6, rtol=1e-6)
+
+
+@pytest.mark.parametrize("t", QTS)
+@pytest.mark.parametrize("B", [1, 3, 8])
+@pytest.mark.parametrize("K", [512, 2304])
+def test_gemv_store(E, t, B, K):
+    if t == GGMLType.Q4_K and K == 2304:
+        pass
+    N = 264
+    m, W = qmat(E, t, N, K, seed=3)
+    x = torch.randn(B, K, device="cuda")
+    y = torch.zeros(B, N, device="cuda")
+    E.gemv([m], B, x.data_ptr(), K, 0, 1e-5, y.data_ptr(), N, E.EPI_STORE, stream())
+    torch.cuda.synchronize()
+    ref = x.cpu() @ W.T
+    assert torch.allclose(y.cpu(), ref, atol=2e-3, rtol=2e-3), (y.cpu() - ref).abs().max()
+
+
+@pytest.mark.parametrize("t", [GGMLType.Q4_K, GGMLType.Q6_K, GGMLType.BF16])
+def test_gemv_long_k_tiles(E, t):
+    # K = 14336 with B = 4 forces several LDS K-tiles
+    N, K, B = 64, 14336, 4
+    m, W = qmat(E, t, N, K, seed=4, std=0.02)
+    x = torch.randn(B, K, device="cuda")
+    y = torch.zeros(B, N, device="cuda")
+    E.gemv([m], B, x.data_ptr(), K, 0, 1e-5, y.data_ptr(), N, E.EPI_STORE, stream())
+    torch.cuda.synchronize()
+    ref = x.cpu() @ W.T
+    assert torch.allclose(y.cpu(), ref, atol=5e-3, rtol=5e-3)
+
+
+def test_gemv_norm_resid_swiglu(E):
+    K, F, B = 512, 256, 2
+    gate, Wg = qmat(E, GGMLType.Q4_K, F, K, seed=5)
+    up, Wu = qmat(E, GGMLType.Q4_K, F, K, seed=6)
+    # interleave rows on the host through raw re-quantization of the dequantized values
+    inter = torch.empty(2 * F, K)
+    inter[0::2], inter[1::2] = Wg, Wu
+    gu = E.QMatrix(int(GGMLType.BF16), 2 * F, K, inter.to(torch.bfloat16).view(torch.int16).numpy())
+    Wgu = inter.to(torch.bfloat16).float()
+    x = torch.randn(B, K, device="cuda") * 3
+    nw = torch.rand(K, device="cuda") + 0.5
+    out = torch.zeros(B, F, device="cuda")
+    E.gemv([gu], B, x.data_ptr(), K, nw.data_ptr(), 1e-5, out.data_ptr(), F, E.EPI_SWIGLU, stream())
+    torch.cuda.synchronize()
+    xc = x.cpu()
+    xn = xc * torch.rsqrt((xc * xc).mean(-1, keepdim=True) + 1e-5) * nw.cpu()
+    h = xn @ Wgu.T
+    ref = torch.nn.functional.silu(h[:, 0::2]) * h[:, 1::2]
+    assert torch.allclose(out.cpu(), ref, atol=2e-3, rtol=2e-3)
+    # residual epilogue
+    y0 = torch.randn(B, 2 * F, device="cuda")
+    y = y0.clone()
+    E.gemv([gu], B, x.data_ptr(), K, 0, 1e-5, y.data_ptr(), 2 * F, E.EPI_RESID, stream())
+    torch.cuda.synchronize()
+    assert torch.allclose(y.cpu(), y0.cpu() + xc @ Wgu.T, atol=2e-3, rtol=2e-3)
+
+
+def rope_ref(x, pos, theta, neox=False):
+    hd = x.shape[-1]
+    p = torch.arange(hd // 2, dtype=torch.float32)
+    freq = torch.pow(torch.tensor(theta), -2.0 * p / hd)
+    ang = pos.float()[:, None] * freq[None]
+    c, s = torch.cos(ang)[:, None], torch.sin(ang)[:, None]
+    out = torch.empty_like(x)
+    if neox:
+        a, b = x[..., :hd // 2], x[..., hd // 2:]
+        return torch.cat([a * c - b * s, a * s + b * c], -1)
+    a, b = x[..., 0::2], x[..., 1::2]
+    out[..., 0::2] = a * c - b * s
+    out[..., 1::2] = a * s + b * c
+    return out
+
+
+@pytest.mark.parametrize("mixed", [False, True])
+def test_gemv_qkv_rope_kv(E, mixed):
+    d, H, Hkv, hd, max_ctx, slots = 256, 4, 2, 64, 128, 3
+    B = 3
+    wq, Wq = qmat(E, GGMLType.Q4_K, H * hd, d, seed=7)
+    wk, Wk = qmat(E, GGMLType.Q4_K, Hkv * hd, d, seed=8)
+    wv, Wv = qmat(E, GGMLType.Q6_K if mixed else GGMLType.Q4_K, Hkv * hd, d, seed=9)
+    x = torch.randn(B, d, device="cuda")
+    nw = torch.rand(d, device="cuda") + 0.5
+    pos = torch.tensor([5, 17, 100], dtype=torch.int32, device="cuda")
+    slot = torch.tensor([2, 0, 1], dtype=torch.int32, device="cuda")
+    kc = torch.zeros(slots, Hkv, max_ctx, hd, dtype=torch.bfloat16, device="cuda")
+    vc = torch.zeros_like(kc)
+    q = torch.zeros(B, H * hd, device="cuda")
+    E.gemv_qkv([wq, wk, wv], B, x.data_ptr(), d, nw.data_ptr(), 1e-5, q.data_ptr(), 0, hd, H, Hkv, max_ctx, 0,
+               10000.0, pos.data_ptr(), slot.data_ptr(), kc.data_ptr(), vc.data_ptr(), stream())
+    torch.cuda.synchronize()
+    xc = x.cpu()
+    xn = xc * torch.rsqrt((xc * xc).mean(-1, keepdim=True) + 1e-5) * nw.cpu()
+    qr = rope_ref((xn @ Wq.T).view(B, H, hd), pos.cpu(), 10000.0)
+    kr = rope_ref((xn @ Wk.T).view(B, Hkv, hd), pos.cpu(), 10000.0)
+    vr = (xn @ Wv.T).view(B, Hkv, hd)
+    assert torch.allclose(q.cpu().view(B, H, hd), qr, atol=2e-3, rtol=2e-3)
+    for b in range(B):
+        s, p = int(slot[b]), int(pos[b])
+        assert torch.allclose(kc[s, :, p].float().cpu(), kr[b], atol=2e-2, rtol=1e-2)
+        assert torch.allclose(vc[s, :, p].float().cpu(), vr[b], atol=2e-2, rtol=1e-2)
+
+
+@pytest.mark.parametrize("hd,H,Hkv", [(64, 8, 1), (128, 32, 8), (64, 32, 4), (128, 40, 8)])
+@pytest.mark.parametrize("lens", [[1], [37, 200], [64, 65, 129, 1]])
+def test_attention_decode(E, hd, H, Hkv, lens):
+    B = len(lens)
+    max_ctx, slots = 256, B + 1
+    kc = (torch.randn(slots, Hkv, max_ctx, hd) * 0.5).to(torch.bfloat16).cuda()
+    vc = torch.randn(slots, Hkv, max_ctx, hd).to(torch.bfloat16).cuda()
+    q = torch.randn(B, H, hd, device="cuda")
+    seq = torch.tensor(lens, dtype=torch.int32, device="cuda")
+    slot = torch.tensor(list(range(1, B + 1)), dtype=torch.int32, device="cuda")
+    nch = max_ctx // E.ATTN_CHUNK
+    opart = torch.empty(B, H, nch, hd, device="cuda")
+    ml = torch.empty(B, H, nch, 2, device="cuda")
+    out = torch.empty(B, H * hd, device="cuda")
+    scale = 1 / math.sqrt(hd)
+    E.attn_decode(q.data_ptr(), kc.data_ptr(), vc.data_ptr(), seq.data_ptr(), slot.data_ptr(), B, H, Hkv, hd,
+                  max_ctx, nch, scale, opart.data_ptr(), ml.data_ptr(), out.data_ptr(), stream())
+    torch.cuda.synchronize()
+    G = H // Hkv
+    for b in range(B):
+        L, s = lens[b], b + 1
+        k = kc[s, :, :L].float().cpu().repeat_interleave(G, 0)
+        v = vc[s, :, :L].float().cpu().repeat_interleave(G, 0)
+        att = torch.softmax(torch.einsum("hd,hsd->hs", q[b].cpu(), k) * scale, -1)
+        ref = torch.einsum("hs,hsd->hd", att, v).reshape(-1)
+        assert torch.allclose(out[b].cpu(), ref, atol=2e-4, rtol=2e-3), (b, (out[b].cpu() - ref).abs().max())
+
+
+def test_rmsnorm(E):
+    x = torch.randn(5, 4096, device="cuda") * 2
+    w = torch.rand(4096, device="cuda")
+    y = torch.empty_like(x)
+    E.rmsnorm(x.data_ptr(), 4096, w.data_ptr(), y.data_ptr(), 4096, 5, 4096, 1e-5, stream())
+    yb = torch.empty(5, 4096, dtype=torch.bfloat16, device="cuda")
+    E.rmsnorm_bf16(x.data_ptr(), 4096, w.data_ptr(), yb.data_ptr(), 4096, 5, 4096, 1e-5, stream())
+    torch.cuda.synchronize()
+    ref = x * torch.rsqrt((x * x).mean(-1, keepdim=True) + 1e-5) * w
+    assert torch.allclose(y, ref, atol=1e-5, rtol=1e-5)
+    assert torch.allclose(yb.float(), ref, atol=2e-2, rtol=1e-2)
+
+
+@pytest.mark.parametrize("neox", [0, 1])
+def test_qkv_post_qknorm(E, neox):
+    T, H, Hkv, hd, max_ctx = 4, 4, 2, 128, 64
+    qkv = torch.randn(T, (H + 2 * Hkv) * hd, device="cuda")
+    qn = torch.rand(hd, device="cuda") + 0.5
+    kn = torch.rand(hd, device="cuda") + 0.5
+    pos = torch.tensor([0, 1, 9, 33], dtype=torch.int32, device="cuda")
+    kc = torch.zeros(1, Hkv, max_ctx, hd, dtype=torch.bfloat16, device="cuda")
+    vc = torch.zeros_like(kc)
+    q = torch.empty(T, H * hd, device="cuda")
+    E.qkv_post(qkv.data_ptr(), qkv.shape[1], T, H, Hkv, hd, qn.data_ptr(), kn.data_ptr(), 1e-6, neox, 1e6,
+               pos.data_ptr(), 0, q.data_ptr(), kc.data_ptr(), vc.data_ptr(), max_ctx, stream())
+    torch.cuda.synchronize()
+    c = qkv.cpu()
+    rms = lambda x, w: x * torch.rsqrt((x * x).mean(-1, keepdim=True) + 1e-6) * w
+    qr = rope_ref(rms(c[:, :H * hd].view(T, H, hd), qn.cpu()), pos.cpu(), 1e6, bool(neox))
+    kr = rope_ref(rms(c[:, H * hd:(H + Hkv) * hd].view(T, Hkv, hd), kn.cpu()), pos.cpu(), 1e6, bool(neox))
+    assert torch.allclose(q.cpu().view(T, H, hd), qr, atol=1e-4, rtol=1e-4)
+    for t in range(T):
+        assert torch.allclose(kc[0, :, int(pos[t])].float().cpu(), kr[t], atol=2e-2, rtol=1e-2)
+
+
+def test_sample_greedy_and_mask(E):
+    B, V = 3, 32000
+    logits = torch.randn(B, V, device="cuda")
+    tok = torch.zeros(B, dtype=torch.int32, device="cuda")
+    E.sample(logits.data_ptr(), V, B, V, 0, 0, 0, tok.data_ptr(), 0, 0, stream())
+    torch.cuda.synchronize()
+    assert torch.equal(tok.cpu().long(), logits.argmax(-1).cpu())
+    # grammar mask: allow only tokens 10..19
+    mask = np.zeros((B, V // 8), np.uint8)
+    for b in range(B):
+        for i in range(10, 20):
+            mask[b, i >> 3] |= 1 << (i & 7)
+    m = torch.from_numpy(mask).cuda()
+    E.sample(logits.data_ptr(), V, B, V, 0, 0, 0, tok.data_ptr(), 0, m.data_ptr(), stream())
+    torch.cuda.synchronize()
+    assert torch.equal(tok.cpu().long(), logits[:, 10:20].argmax(-1).cpu() + 10)
+
+
+def test_sample_temperature_topk_distribution(E):
+    V = 1000
+    logits = torch.full((1, V), -10.0, device="cuda")
+    logits[0, 3], logits[0, 7], logits[0, 11] = 2.0, 1.0, 0.0
+    temp = torch.tensor([1.0], device="cuda")
+    topk = torch.tensor([2], dtype=torch.int32, device="cuda")
+    tok = torch.zeros(1, dtype=torch.int32, device="cuda")
+    counts = {}
+    for i in range(400):
+        pos = torch.tensor([i], dtype=torch.int32, device="cuda")
+        E.sample(logits.data_ptr(), V, 1, V, temp.data_ptr(), topk.data_ptr(), 1234, tok.data_ptr(), pos.data_ptr(),
+                 0, stream())
+        counts[int(tok.item())] = counts.get(int(tok.item()), 0) + 1
+    assert set(counts) <= {3, 7}
+    p3 = counts.get(3, 0) / 400
+    assert abs(p3 - math.e / (math.e + 1)) < 0.08
+
+
+@pytest.mark.parametrize("t", QTS)
+@pytest.mark.parametrize("M", [1, 64, 100])
+def test_gemm_mfma(E, t, M):
+    N, K = 192, 512
+    m, W = qmat(E, t, N, K, seed=11)
+    A = torch.randn(M, K, device="cuda").to(torch.bfloat16)
+    C = torch.zeros(M, N, device="cuda")
+    E.gemm(A.data_ptr(), K, m, M, C.data_ptr(), N, 0, stream())
+    torch.cuda.synchronize()
+    ref = A.float().cpu() @ W.to(torch.bfloat16).float().T
+    assert torch.allclose(C.cpu(), ref, atol=2e-3, rtol=2e-3), (C.cpu() - ref).abs().max()
+    C2 = C.clone()
+    E.gemm(A.data_ptr(), K, m, M, C2.data_ptr(), N, 1, stream())
+    torch.cuda.synchronize()
+    assert torch.allclose(C2.cpu(), 2 * ref, atol=4e-3, rtol=2e-3)

@@ -1,0 +1,75 @@
+"""CPU tests: GGML block formats (bit-exact layouts the HIP kernels mirror)."""
+import numpy as np
+import pytest
+
+from aios_amd.gguf.quants import (BLOCK_INFO, GGMLType, dequantize, kquant_pack_scale_min, kquant_scale_min,
+                                  quantize, type_size)
+
+FORMATS = [GGMLType.Q4_0, GGMLType.Q8_0, GGMLType.Q4_K, GGMLType.Q5_K, GGMLType.Q6_K, GGMLType.F16, GGMLType.BF16]
+TOL = {GGMLType.Q4_0: 0.2, GGMLType.Q8_0: 0.01, GGMLType.Q4_K: 0.12, GGMLType.Q5_K: 0.06, GGMLType.Q6_K: 0.03,
+       GGMLType.F16: 1e-3, GGMLType.BF16: 1e-2}
+
+
+@pytest.mark.parametrize("t", FORMATS)
+def test_roundtrip_error(t):
+    rng = np.random.default_rng(0)
+    x = rng.standard_normal(256 * 16).astype(np.float32)
+    raw = quantize(x, t)
+    assert raw.size == type_size(t, x.size)
+    y = dequantize(raw, t)
+    rel = np.sqrt(np.mean((x - y) ** 2)) / np.sqrt(np.mean(x ** 2))
+    assert rel < TOL[t], (t, rel)
+
+
+def test_scale_min_pack_roundtrip():
+    rng = np.random.default_rng(1)
+    sc = rng.integers(0, 64, (50, 8))
+    mn = rng.integers(0, 64, (50, 8))
+    s2, m2 = kquant_scale_min(kquant_pack_scale_min(sc, mn))
+    assert (s2 == sc).all() and (m2 == mn).all()
+
+
+def test_q4k_hand_block():
+    # d=1, dmin=0.5, all scales 1, mins 2, nibble pattern known
+    d = np.array([1.0], np.float16).view(np.uint8)
+    dmin = np.array([0.5], np.float16).view(np.uint8)
+    scales = kquant_pack_scale_min(np.ones((1, 8), int), np.full((1, 8), 2))[0]
+    qs = np.arange(128, dtype=np.uint8) % 16 | ((np.arange(128, dtype=np.uint8) % 7) << 4)
+    blk = np.concatenate([d, dmin, scales, qs])
+    y = dequantize(blk, GGMLType.Q4_K)
+    # group 0 low nibbles -> elements 0..31
+    assert np.allclose(y[:32], (np.arange(32) % 16) * 1.0 - 1.0)
+    assert np.allclose(y[32:64], (np.arange(32) % 7) * 1.0 - 1.0)
+
+
+def test_q6k_matches_formula():
+    rng = np.random.default_rng(2)
+    raw = rng.integers(0, 256, 210 * 3, dtype=np.uint8)
+    raw.reshape(3, 210)[:, 208:210] = np.array([0.01], np.float16).view(np.uint8)
+    y = dequantize(raw, GGMLType.Q6_K).reshape(3, 256)
+    b = raw.reshape(3, 210)
+    # scalar reimplementation of the published reference loop
+    for i in range(3):
+        ql, qh, sc = b[i, :128].astype(int), b[i, 128:192].astype(int), b[i, 192:208].view(np.int8).astype(int)
+        d = float(b[i, 208:210].view(np.float16)[0])
+        out = np.zeros(256)
+        for n in range(2):
+            for l in range(32):
+                is_ = l // 16
+                q1 = ((ql[64 * n + l] & 0xF) | (((qh[32 * n + l] >> 0) & 3) << 4)) - 32
+                q2 = ((ql[64 * n + l + 32] & 0xF) | (((qh[32 * n + l] >> 2) & 3) << 4)) - 32
+                q3 = ((ql[64 * n + l] >> 4) | (((qh[32 * n + l] >> 4) & 3) << 4)) - 32
+                q4 = ((ql[64 * n + l + 32] >> 4) | (((qh[32 * n + l] >> 6) & 3) << 4)) - 32
+                out[128 * n + l] = d * sc[8 * n + is_] * q1
+                out[128 * n + l + 32] = d * sc[8 * n + is_ + 2] * q2
+                out[128 * n + l + 64] = d * sc[8 * n + is_ + 4] * q3
+                out[128 * n + l + 96] = d * sc[8 * n + is_ + 6] * q4
+        assert np.allclose(y[i], out, atol=1e-6)
+
+
+def test_block_info_sizes():
+    assert BLOCK_INFO[GGMLType.Q4_K] == (256, 144)
+    assert BLOCK_INFO[GGMLType.Q6_K] == (256, 210)
+    assert BLOCK_INFO[GGMLType.Q5_K] == (256, 176)
+    assert BLOCK_INFO[GGMLType.Q8_0] == (32, 34)
+    assert BLOCK_INFO[GGMLType.Q4_0] == (32, 18)
