@@ -193,7 +193,7 @@ PYBIND11_MODULE(_engine, m) {
 
   m.def("gemv",
         [](std::vector<PyQMatrix*> segs, int B, uintptr_t x, int ldx, uintptr_t norm_w, float eps, uintptr_t y,
-           int ldy, int epi, uintptr_t st) {
+           int ldy, int epi, uintptr_t st, int force_v1) {
           GemvArgs a;
           std::memset(&a, 0, sizeof(a));
           a.nseg = (int)segs.size();
@@ -201,9 +201,11 @@ PYBIND11_MODULE(_engine, m) {
           for (int s = 0; s < a.nseg; ++s) { a.seg[s] = segs[s]->w; a.seg_row0[s] = r; r += segs[s]->w.rows; }
           a.N = r; a.K = segs[0]->w.cols; a.B = B;
           a.x = (const float*)x; a.ldx = ldx; a.norm_w = (const float*)norm_w; a.eps = eps;
-          a.y = (float*)y; a.ldy = ldy; a.epi = epi;
+          a.y = (float*)y; a.ldy = ldy; a.epi = epi; a.force_v1 = force_v1;
           launch_gemv(a, S(st));
-        });
+        },
+        py::arg("segs"), py::arg("B"), py::arg("x"), py::arg("ldx"), py::arg("norm_w"), py::arg("eps"), py::arg("y"),
+        py::arg("ldy"), py::arg("epi"), py::arg("stream"), py::arg("force_v1") = 0);
   m.def("gemv_qkv",
         [](std::vector<PyQMatrix*> segs, int B, uintptr_t x, int ldx, uintptr_t norm_w, float eps, uintptr_t q_out,
            uintptr_t bias, int head_dim, int n_heads, int n_kv_heads, int max_ctx, int rope_neox, float rope_base,
@@ -218,7 +220,7 @@ PYBIND11_MODULE(_engine, m) {
           a.y = (float*)q_out; a.ldy = n_heads * head_dim; a.epi = EPI_QKV;
           a.bias = (const float*)bias; a.head_dim = head_dim; a.q_dim = n_heads * head_dim;
           a.kv_dim = n_kv_heads * head_dim; a.n_kv_heads = n_kv_heads; a.max_ctx = max_ctx;
-          a.rope_neox = rope_neox; a.rope_base = rope_base; a.pos = (const int*)pos; a.slot = (const int*)slot;
+          a.rope_neox = rope_neox; a.rope_base = rope_base; a.rope_cs = nullptr; a.pos = (const int*)pos; a.slot = (const int*)slot;
           a.k_cache = (bf16_t*)k_cache; a.v_cache = (bf16_t*)v_cache;
           launch_gemv(a, S(st));
         });
@@ -248,7 +250,7 @@ PYBIND11_MODULE(_engine, m) {
           QkvPostArgs a;
           a.qkv = (const float*)qkv; a.ldqkv = ldqkv; a.T = T; a.n_heads = H; a.n_kv_heads = Hkv; a.head_dim = hd;
           a.q_norm = (const float*)q_norm; a.k_norm = (const float*)k_norm; a.eps = eps; a.rope_neox = rope_neox;
-          a.rope_base = rope_base; a.pos = (const int*)pos; a.slot = (const int*)slot; a.q_out = (float*)q_out;
+          a.rope_base = rope_base; a.rope_cs = nullptr; a.pos = (const int*)pos; a.slot = (const int*)slot; a.q_out = (float*)q_out;
           a.k_cache = (bf16_t*)k_cache; a.v_cache = (bf16_t*)v_cache; a.max_ctx = max_ctx;
           launch_qkv_post(a, S(st));
         });

@@ -3,6 +3,7 @@
 
 #include <algorithm>
 #include <cstring>
+#include <cmath>
 #include <regex>
 #include <sstream>
 
@@ -351,6 +352,18 @@ void Engine::finalize() {
   HIP_CHECK(hipMemset(k_cache_, 0, kv_bytes_ / 2));
   HIP_CHECK(hipMemset(v_cache_, 0, kv_bytes_ / 2));
   n_chunks_ = (cfg_.max_ctx + ATTN_CHUNK - 1) / ATTN_CHUNK;
+  {
+    const int half = hd / 2;
+    std::vector<float> tab((size_t)cfg_.max_ctx * half * 2);
+    for (int pos = 0; pos < cfg_.max_ctx; ++pos)
+      for (int p = 0; p < half; ++p) {
+        const double th = (double)pos * std::pow((double)cfg_.rope_theta, -2.0 * p / (double)hd);
+        tab[((size_t)pos * half + p) * 2] = (float)std::cos(th);
+        tab[((size_t)pos * half + p) * 2 + 1] = (float)std::sin(th);
+      }
+    rope_cs_ = (float2*)dmalloc(tab.size() * 4);
+    HIP_CHECK(hipMemcpy(rope_cs_, tab.data(), tab.size() * 4, hipMemcpyHostToDevice));
+  }
 
   size_t ws = 0;
   auto fbuf = [&](size_t n) { ws += n * 4; return (float*)dmalloc(n * 4); };
@@ -431,6 +444,7 @@ void Engine::gemv(const std::vector<const QMat*>& segs, int N, int K, int B, con
     a.max_ctx = cfg_.max_ctx;
     a.rope_neox = cfg_.rope_neox;
     a.rope_base = cfg_.rope_theta;
+    a.rope_cs = rope_cs_;
     a.k_cache = k_cache_ + (size_t)layer * layer_kv_elems_;
     a.v_cache = v_cache_ + (size_t)layer * layer_kv_elems_;
   }
@@ -468,7 +482,7 @@ void Engine::layer_decode(int l, int B) {
         a.epi = EPI_QKV; a.y = q_; a.ldy = qd;
         a.bias = L.bqkv;
         a.head_dim = hd; a.q_dim = qd; a.kv_dim = kvd; a.n_kv_heads = cfg_.n_kv_heads; a.max_ctx = cfg_.max_ctx;
-        a.rope_neox = cfg_.rope_neox; a.rope_base = cfg_.rope_theta;
+        a.rope_neox = cfg_.rope_neox; a.rope_base = cfg_.rope_theta; a.rope_cs = rope_cs_;
         a.pos = d_pos_; a.slot = d_slot_;
         a.k_cache = k_cache_ + (size_t)l * layer_kv_elems_;
         a.v_cache = v_cache_ + (size_t)l * layer_kv_elems_;
@@ -484,7 +498,7 @@ void Engine::layer_decode(int l, int B) {
       p.qkv = qkv_; p.ldqkv = qd + 2 * kvd; p.T = B;
       p.n_heads = cfg_.n_heads; p.n_kv_heads = cfg_.n_kv_heads; p.head_dim = hd;
       p.q_norm = L.q_norm; p.k_norm = L.k_norm; p.eps = cfg_.norm_eps;
-      p.rope_neox = cfg_.rope_neox; p.rope_base = cfg_.rope_theta;
+      p.rope_neox = cfg_.rope_neox; p.rope_base = cfg_.rope_theta; p.rope_cs = rope_cs_;
       p.pos = d_pos_; p.slot = d_slot_; p.q_out = q_;
       p.k_cache = k_cache_ + (size_t)l * layer_kv_elems_;
       p.v_cache = v_cache_ + (size_t)l * layer_kv_elems_;
@@ -596,7 +610,7 @@ std::vector<float> Engine::prefill(int slot, const std::vector<int>& tokens, int
             if (fused_qkv) {
               a.epi = EPI_QKV; a.y = q_; a.ldy = qd; a.bias = L.bqkv;
               a.head_dim = hd; a.q_dim = qd; a.kv_dim = kvd; a.n_kv_heads = cfg_.n_kv_heads; a.max_ctx = cfg_.max_ctx;
-              a.rope_neox = cfg_.rope_neox; a.rope_base = cfg_.rope_theta;
+              a.rope_neox = cfg_.rope_neox; a.rope_base = cfg_.rope_theta; a.rope_cs = rope_cs_;
               a.pos = d_pos_; a.slot = d_slot_;
               a.k_cache = k_cache_ + (size_t)l * layer_kv_elems_;
               a.v_cache = v_cache_ + (size_t)l * layer_kv_elems_;
@@ -611,7 +625,7 @@ std::vector<float> Engine::prefill(int slot, const std::vector<int>& tokens, int
             p.qkv = qkv_; p.ldqkv = qd + 2 * kvd; p.T = bn;
             p.n_heads = cfg_.n_heads; p.n_kv_heads = cfg_.n_kv_heads; p.head_dim = hd;
             p.q_norm = L.q_norm; p.k_norm = L.k_norm; p.eps = cfg_.norm_eps;
-            p.rope_neox = cfg_.rope_neox; p.rope_base = cfg_.rope_theta;
+            p.rope_neox = cfg_.rope_neox; p.rope_base = cfg_.rope_theta; p.rope_cs = rope_cs_;
             p.pos = d_pos_; p.slot = d_slot_; p.q_out = q_;
             p.k_cache = k_cache_ + (size_t)l * layer_kv_elems_;
             p.v_cache = v_cache_ + (size_t)l * layer_kv_elems_;

@@ -21,6 +21,7 @@ struct GemvArgs {
   int N, K, B;
   int row_base;                 // global row of local row 0 (epilogue indexing)
   int kt_max;                   // K tile held in LDS (set by launch_gemv)
+  int force_v1;                 // testing: bypass the persistent kernel
   const float* x;               // [B][ldx] fp32 input (residual stream if norm_w != null)
   int ldx;
   const float* norm_w;          // RMSNorm weight [K] or null
@@ -33,6 +34,7 @@ struct GemvArgs {
   int head_dim, q_dim, kv_dim, n_kv_heads, max_ctx;
   int rope_neox;
   float rope_base;
+  const float2* rope_cs;         // [max_ctx][head_dim/2] (cos, sin) table or null
   const int* pos;               // [B] position of the token being written
   const int* slot;              // [B] KV-cache slot (null -> b)
   bf16_t* k_cache;              // layer base: [slots][n_kv][max_ctx][hd]

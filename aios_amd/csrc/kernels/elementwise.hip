@@ -111,9 +111,14 @@ __global__ void qkv_post_kernel(QkvPostArgs a) {
     float v0 = src[ia], v1 = src[ib];
     if (nw) { v0 *= inv * nw[ia]; v1 *= inv * nw[ib]; }
     if (part < 2) {
-      const float theta = (float)pos * powf(a.rope_base, -2.f * (float)p / (float)hd);
       float sn, cs;
-      sincosf(theta, &sn, &cs);
+      if (a.rope_cs) {
+        const float2 t = a.rope_cs[(size_t)pos * half + p];
+        cs = t.x; sn = t.y;
+      } else {
+        const float theta = (float)pos * powf(a.rope_base, -2.f * (float)p / (float)hd);
+        sincosf(theta, &sn, &cs);
+      }
       const float o0 = v0 * cs - v1 * sn, o1 = v0 * sn + v1 * cs;
       v0 = o0; v1 = o1;
     }

@@ -162,6 +162,62 @@ __device__ __forceinline__ void gemv_tile(const QWeight& w, int row0, int k0, in
   }
 }
 
+__device__ __forceinline__ void gemv_epilogue(const GemvArgs& a, int grow, int b, float v0, float v1) {
+  const int nrow = a.row_base + a.N;
+  switch (a.epi) {
+    case EPI_STORE: {
+      float* y = a.y + (size_t)b * a.ldy;
+      y[grow] = v0;
+      if (grow + 1 < nrow) y[grow + 1] = v1;
+    } break;
+    case EPI_RESID: {
+      float* y = a.y + (size_t)b * a.ldy;
+      y[grow] += v0;
+      if (grow + 1 < nrow) y[grow + 1] += v1;
+    } break;
+    case EPI_SWIGLU: {
+      const float g = v0, u = v1;  // rows (2i, 2i+1) = (gate_i, up_i)
+      a.y[(size_t)b * a.ldy + (grow >> 1)] = g / (1.f + __expf(-g)) * u;
+    } break;
+    case EPI_QKV: {
+      if (a.bias) { v0 += a.bias[grow]; v1 += a.bias[grow + 1]; }
+      const int hd = a.head_dim, qd = a.q_dim, kvd = a.kv_dim;
+      const int pos = a.pos[b];
+      const int slot = a.slot ? a.slot[b] : b;
+      int part, r;
+      if (grow < qd) { part = 0; r = grow; }
+      else if (grow < qd + kvd) { part = 1; r = grow - qd; }
+      else { part = 2; r = grow - qd - kvd; }
+      const int head = r / hd, lr = r - head * hd, p = lr >> 1;
+      int da, db;
+      if (part == 2) { da = lr; db = lr + 1; }
+      else if (a.rope_neox) { da = p; db = p + (hd >> 1); }
+      else { da = 2 * p; db = 2 * p + 1; }
+      if (part < 2) {
+        float sn, cs;
+        if (a.rope_cs) {
+          const float2 t = a.rope_cs[(size_t)pos * (hd >> 1) + p];
+          cs = t.x; sn = t.y;
+        } else {
+          const float theta = (float)pos * powf(a.rope_base, -2.f * (float)p / (float)hd);
+          sincosf(theta, &sn, &cs);
+        }
+        const float o0 = v0 * cs - v1 * sn, o1 = v0 * sn + v1 * cs;
+        v0 = o0; v1 = o1;
+      }
+      if (part == 0) {
+        float* q = a.y + (size_t)b * a.ldy + head * hd;
+        q[da] = v0; q[db] = v1;
+      } else {
+        bf16_t* cache = (part == 1 ? a.k_cache : a.v_cache);
+        const size_t base = (((size_t)slot * a.n_kv_heads + head) * a.max_ctx + pos) * hd;
+        cache[base + da] = f32_to_bf16(v0);
+        cache[base + db] = f32_to_bf16(v1);
+      }
+    } break;
+  }
+}
+
 template <int QT, int B, int U>
 __device__ __forceinline__ void gemv_seg(const GemvArgs& a, const QWeight& w, int local_row, bool active,
                                          const float* inv_rms, float* xl, float* xs, float (&acc)[GEMV_ROWS][B]) {
@@ -230,56 +286,231 @@ __global__ void __launch_bounds__(GEMV_THREADS) gemv_kernel(GemvArgs a) {
 #pragma unroll
   for (int b = 0; b < B; ++b)
     if (lane == b) { v0 = acc[0][b]; v1 = acc[1][b]; }
-  const int b = lane;
-  const int grow = a.row_base + row_blk + wave * GEMV_ROWS;
-  const int nrow = a.row_base + a.N;
-  switch (a.epi) {
-    case EPI_STORE: {
-      float* y = a.y + (size_t)b * a.ldy;
-      y[grow] = v0;
-      if (grow + 1 < nrow) y[grow + 1] = v1;
-    } break;
-    case EPI_RESID: {
-      float* y = a.y + (size_t)b * a.ldy;
-      y[grow] += v0;
-      if (grow + 1 < nrow) y[grow + 1] += v1;
-    } break;
-    case EPI_SWIGLU: {
-      const float g = v0, u = v1;  // rows (2i, 2i+1) = (gate_i, up_i)
-      a.y[(size_t)b * a.ldy + (grow >> 1)] = g / (1.f + __expf(-g)) * u;
-    } break;
-    case EPI_QKV: {
-      if (a.bias) { v0 += a.bias[grow]; v1 += a.bias[grow + 1]; }
-      const int hd = a.head_dim, qd = a.q_dim, kvd = a.kv_dim;
-      const int pos = a.pos[b];
-      const int slot = a.slot ? a.slot[b] : b;
-      int part, r;
-      if (grow < qd) { part = 0; r = grow; }
-      else if (grow < qd + kvd) { part = 1; r = grow - qd; }
-      else { part = 2; r = grow - qd - kvd; }
-      const int head = r / hd, lr = r - head * hd, p = lr >> 1;
-      int da, db;
-      if (part == 2) { da = lr; db = lr + 1; }
-      else if (a.rope_neox) { da = p; db = p + (hd >> 1); }
-      else { da = 2 * p; db = 2 * p + 1; }
-      if (part < 2) {
-        const float theta = (float)pos * powf(a.rope_base, -2.f * (float)p / (float)hd);
-        float sn, cs;
-        sincosf(theta, &sn, &cs);
-        const float o0 = v0 * cs - v1 * sn, o1 = v0 * sn + v1 * cs;
-        v0 = o0; v1 = o1;
-      }
-      if (part == 0) {
-        float* q = a.y + (size_t)b * a.ldy + head * hd;
-        q[da] = v0; q[db] = v1;
-      } else {
-        bf16_t* cache = (part == 1 ? a.k_cache : a.v_cache);
-        const size_t base = (((size_t)slot * a.n_kv_heads + head) * a.max_ctx + pos) * hd;
-        cache[base + da] = f32_to_bf16(v0);
-        cache[base + db] = f32_to_bf16(v1);
-      }
-    } break;
+  gemv_epilogue(a, a.row_base + row_blk + wave * GEMV_ROWS, lane, v0, v1);
+}
+
+
+// =============================================================================================
+// Persistent, software-pipelined GEMV (v2).
+//
+// The v1 kernel above gives every 8-row workgroup its own RMSNorm + x-staging prologue; for the
+// Mistral gate/up projection that is 7168 prologues re-reading 32 KB each (more L2 traffic than
+// the 132 MB of weights) and each workgroup's weight loads only start after it.  Here:
+//  * grid = min(row groups, CUs x occupancy): each workgroup stages x ONCE, then walks its
+//    row-pairs grid-stride (pair p = blk*WAVES + wave + i*grid*WAVES);
+//  * the first pair's weight loads are issued before the prologue (they do not depend on x);
+//  * work items (pair, K-iteration) are double-buffered in registers: the next item's loads are
+//    in flight while the current one is decoded (hipcc's counted vmcnt waits only for the
+//    older group), so each wave keeps two items (~2 x 8 KB for Q4_K) in flight at all times.
+// Requires B*K floats of x (+ run sums) to fit the LDS budget; the launcher falls back to v1.
+// =============================================================================================
+constexpr int GP_THREADS = 256;
+constexpr int GP_WAVES = GP_THREADS / 64;
+
+template <int QT, int U>
+__device__ __forceinline__ void gp_load(const QWeight& w, int lrow, int it, int nch, RawChunk (&r)[U][GEMV_ROWS]) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int c = (it * U + u) * 64 + lane;
+    if (c < nch) {
+#pragma unroll
+      for (int rr = 0; rr < GEMV_ROWS; ++rr) QFmt<QT>::load(w, lrow + rr, c, r[u][rr]);
+    }
   }
+}
+
+template <int QT, int B, int U>
+__device__ __forceinline__ void gp_compute(const RawChunk (&raw)[U][GEMV_ROWS], int it, int nch, const float* xl,
+                                           const float* xs, float (&acc)[GEMV_ROWS][B]) {
+  using F_ = QFmt<QT>;
+  using S_ = QStream<QT>;
+  constexpr int W = F_::W, F = W / 4, S = (F == 8 ? 1 : (F == 4 ? 2 : 3)), R = F_::RUNS;
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int c = (it * U + u) * 64 + lane;
+    if (c < nch) {
+      float sc[GEMV_ROWS][R], of[GEMV_ROWS][R];
+#pragma unroll
+      for (int r = 0; r < GEMV_ROWS; ++r) S_::scales(raw[u][r], c, sc[r], of[r]);
+#pragma unroll
+      for (int b = 0; b < B; ++b) {
+        const float* xc = xl + ((size_t)b * nch + c) * W;
+        float part[GEMV_ROWS][R];
+#pragma unroll
+        for (int r = 0; r < GEMV_ROWS; ++r)
+#pragma unroll
+          for (int rr = 0; rr < R; ++rr) part[r][rr] = 0.f;
+#pragma unroll
+        for (int j = 0; j < F; ++j) {
+          const float4 xv = *(const float4*)(xc + 4 * swz_pos(c, j, F, S));
+          const int rr = (R == 1) ? 0 : (j / 4);
+#pragma unroll
+          for (int r = 0; r < GEMV_ROWS; ++r) {
+            float q[4];
+            S_::quad(raw[u][r], c, j, q);
+            part[r][rr] = fmaf(q[0], xv.x, part[r][rr]);
+            part[r][rr] = fmaf(q[1], xv.y, part[r][rr]);
+            part[r][rr] = fmaf(q[2], xv.z, part[r][rr]);
+            part[r][rr] = fmaf(q[3], xv.w, part[r][rr]);
+          }
+        }
+        if constexpr (W >= 16) {
+          const float* xsc = xs + (size_t)b * nch * R + c * R;
+          float xsv[R];
+#pragma unroll
+          for (int rr = 0; rr < R; ++rr) xsv[rr] = xsc[rr];
+#pragma unroll
+          for (int r = 0; r < GEMV_ROWS; ++r)
+#pragma unroll
+            for (int rr = 0; rr < R; ++rr) acc[r][b] += sc[r][rr] * part[r][rr] - of[r][rr] * xsv[rr];
+        } else {
+#pragma unroll
+          for (int r = 0; r < GEMV_ROWS; ++r) acc[r][b] += part[r][0];
+        }
+      }
+    }
+  }
+}
+
+template <int QT0, int QT1, int B, int U>
+__global__ void __launch_bounds__(GP_THREADS) gemv_persistent(GemvArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* red = smem;
+  float* inv_rms = red + 16;
+  constexpr bool MIXED = QT0 != QT1;
+  constexpr int W0 = QFmt<QT0>::W, W1 = QFmt<QT1>::W;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int K = a.K;
+  const int npairs = a.N >> 1;
+  const int nch0 = K / W0, nch1 = K / W1;
+  const int nit0 = (nch0 + 64 * U - 1) / (64 * U), nit1 = (nch1 + 64 * U - 1) / (64 * U);
+  const int stride = gridDim.x * GP_WAVES;
+  // LDS: [red 64][x layout 0: B*K][sums 0: B*K/16][x layout 1][sums 1]
+  float* xl0 = smem + 64;
+  float* xs0 = xl0 + B * K;
+  float* xl1 = MIXED ? xs0 + B * K / 16 : xl0;
+  float* xs1 = MIXED ? xl1 + B * K : xs0;
+
+  auto info = [&](int p, int& lrow, bool& t1, const QWeight*& w) {
+    const int row = 2 * p;
+    int s = 0;
+#pragma unroll
+    for (int k = 1; k < GEMV_MAX_SEGS; ++k)
+      if (k < a.nseg && row >= a.seg_row0[k]) s = k;
+    lrow = row - a.seg_row0[s];
+    t1 = MIXED && (s == a.nseg - 1) && a.nseg > 1;
+    w = &a.seg[s];
+  };
+  auto load = [&](int p, int it, RawChunk (&r)[U][GEMV_ROWS]) {
+    int lrow;
+    bool t1;
+    const QWeight* w;
+    info(p, lrow, t1, w);
+    if (MIXED && t1) gp_load<QT1, U>(*w, lrow, it, nch1, r);
+    else gp_load<QT0, U>(*w, lrow, it, nch0, r);
+  };
+
+  int p = blockIdx.x * GP_WAVES + wave;
+  int it = 0;
+  RawChunk bufA[U][GEMV_ROWS], bufB[U][GEMV_ROWS];
+  if (p < npairs) load(p, 0, bufA);  // weight loads in flight during the prologue
+
+  // ---- prologue: RMSNorm statistics + x staging (once per workgroup)
+  if (a.norm_w) {
+    for (int b = 0; b < a.B; ++b) {
+      float s = 0.f;
+      const float* xb = a.x + (size_t)b * a.ldx;
+      for (int k = threadIdx.x * 4; k < K; k += GP_THREADS * 4) {
+        const float4 v = *(const float4*)(xb + k);
+        s += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+      }
+      s = block_sum(s, red);
+      if (threadIdx.x == 0) inv_rms[b] = rsqrtf(s / (float)K + a.eps);
+      __syncthreads();
+    }
+  }
+  stage_x_tile<QT0>(a.x, a.ldx, a.B, 0, K, inv_rms, a.norm_w, xl0, xs0);
+  if (MIXED) stage_x_tile<QT1>(a.x, a.ldx, a.B, 0, K, inv_rms, a.norm_w, xl1, xs1);
+  __syncthreads();
+
+  float acc[GEMV_ROWS][B];
+#pragma unroll
+  for (int r = 0; r < GEMV_ROWS; ++r)
+#pragma unroll
+    for (int b = 0; b < B; ++b) acc[r][b] = 0.f;
+
+  // one pipelined step: prefetch the item after (p,it) into `nxt`, compute `cur`
+  auto step = [&](RawChunk (&cur)[U][GEMV_ROWS], RawChunk (&nxt)[U][GEMV_ROWS]) -> bool {
+    int lrow;
+    bool t1;
+    const QWeight* w;
+    info(p, lrow, t1, w);
+    const int nit = (MIXED && t1) ? nit1 : nit0;
+    int pn = p, itn = it + 1;
+    if (itn >= nit) { pn = p + stride; itn = 0; }
+    if (pn < npairs) load(pn, itn, nxt);
+    if (MIXED && t1) gp_compute<QT1, B, U>(cur, it, nch1, xl1, xs1, acc);
+    else gp_compute<QT0, B, U>(cur, it, nch0, xl0, xs0, acc);
+    if (itn == 0) {  // pair p complete
+#pragma unroll
+      for (int r = 0; r < GEMV_ROWS; ++r)
+#pragma unroll
+        for (int b = 0; b < B; ++b) acc[r][b] = wave_sum(acc[r][b]);
+      if (lane < a.B) {
+        float v0 = 0.f, v1 = 0.f;
+#pragma unroll
+        for (int b = 0; b < B; ++b)
+          if (lane == b) { v0 = acc[0][b]; v1 = acc[1][b]; }
+        gemv_epilogue(a, a.row_base + 2 * p, lane, v0, v1);
+      }
+#pragma unroll
+      for (int r = 0; r < GEMV_ROWS; ++r)
+#pragma unroll
+        for (int b = 0; b < B; ++b) acc[r][b] = 0.f;
+    }
+    p = pn;
+    it = itn;
+    return p < npairs;
+  };
+  while (p < npairs) {
+    if (!step(bufA, bufB)) break;
+    if (!step(bufB, bufA)) break;
+  }
+}
+
+inline int device_cu_count() {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+  }
+  return cus;
+}
+
+// returns false when the shape does not fit the persistent kernel's LDS budget
+template <int QT0, int QT1, int B, int U>
+bool launch_gemv_persistent(GemvArgs a, hipStream_t st) {
+  constexpr bool MIXED = QT0 != QT1;
+  const size_t xfl = (size_t)B * a.K + (size_t)B * a.K / 16;
+  const size_t lds = (64 + xfl * (MIXED ? 2 : 1) + 4) * sizeof(float);
+  if (lds > 96 * 1024) return false;
+  static int occ = -1;  // resident workgroups per CU for this instantiation (VGPR + LDS limited)
+  if (occ < 0) {
+    int o = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, gemv_persistent<QT0, QT1, B, U>, GP_THREADS, lds) !=
+            hipSuccess || o <= 0)
+      o = 1;
+    occ = o;
+  }
+  const int per_cu = std::max(1, std::min(occ, (int)((160 * 1024) / lds)));
+  const int groups = (a.N / 2 + GP_WAVES - 1) / GP_WAVES;
+  const int blocks = std::min(groups, device_cu_count() * per_cu);
+  a.kt_max = a.K;
+  hipLaunchKernelGGL((gemv_persistent<QT0, QT1, B, U>), dim3(blocks), dim3(GP_THREADS), lds, st, a);
+  return true;
 }
 
 inline int qtype_block(int qt) {
@@ -303,6 +534,11 @@ template <int QT0, int QT1>
 void launch_gemv_pair(const GemvArgs& a, hipStream_t st) {
   constexpr int W = QFmt<QT0>::W;
   const int chunks_per_lane = (a.K / W + 63) / 64;
+  if (!a.force_v1) {
+    if (a.B == 1 && launch_gemv_persistent<QT0, QT1, 1, 2>(a, st)) return;
+    if (a.B == 2 && launch_gemv_persistent<QT0, QT1, 2, 2>(a, st)) return;
+    if (a.B > 2 && a.B <= 4 && launch_gemv_persistent<QT0, QT1, 4, 1>(a, st)) return;
+  }
   if (a.B == 1) {
     if (chunks_per_lane >= 4) launch_gemv_t<QT0, QT1, 1, 4>(a, st);
     else launch_gemv_t<QT0, QT1, 1, 2>(a, st);

@@ -43,6 +43,7 @@ struct QkvPostArgs {
   float eps;
   int rope_neox;
   float rope_base;
+  const float2* rope_cs;  // [max_ctx][head_dim/2] table or null
   const int* pos;    // [T]
   const int* slot;   // [T] or null (0)
   float* q_out;      // [T][n_heads*head_dim]

@@ -51,25 +51,25 @@ def test_get_rows(E, t):
 
 
 @pytest.mark.parametrize("t", QTS)
-@pytest.mark.parametrize("B", [1, 3, 8])
+@pytest.mark.parametrize("B", [1, 2, 3, 8])
 @pytest.mark.parametrize("K", [512, 2304])
-def test_gemv_store(E, t, B, K):
-    if t == GGMLType.Q4_K and K == 2304:
-        pass
-    N = 264
+@pytest.mark.parametrize("v1", [0, 1])
+@pytest.mark.parametrize("N", [264, 4098])
+def test_gemv_store(E, t, B, K, v1, N):
     m, W = qmat(E, t, N, K, seed=3)
     x = torch.randn(B, K, device="cuda")
     y = torch.zeros(B, N, device="cuda")
-    E.gemv([m], B, x.data_ptr(), K, 0, 1e-5, y.data_ptr(), N, E.EPI_STORE, stream())
+    E.gemv([m], B, x.data_ptr(), K, 0, 1e-5, y.data_ptr(), N, E.EPI_STORE, stream(), v1)
     torch.cuda.synchronize()
     ref = x.cpu() @ W.T
     assert torch.allclose(y.cpu(), ref, atol=2e-3, rtol=2e-3), (y.cpu() - ref).abs().max()
 
 
 @pytest.mark.parametrize("t", [GGMLType.Q4_K, GGMLType.Q6_K, GGMLType.BF16])
-def test_gemv_long_k_tiles(E, t):
-    # K = 14336 with B = 4 forces several LDS K-tiles
-    N, K, B = 64, 14336, 4
+@pytest.mark.parametrize("B", [1, 4])
+def test_gemv_long_k_tiles(E, t, B):
+    # K = 14336: B = 1 runs the persistent kernel, B = 4 forces several LDS K-tiles (v1)
+    N, K = 64, 14336
     m, W = qmat(E, t, N, K, seed=4, std=0.02)
     x = torch.randn(B, K, device="cuda")
     y = torch.zeros(B, N, device="cuda")
