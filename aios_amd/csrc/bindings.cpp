@@ -115,6 +115,7 @@ PYBIND11_MODULE(_engine, m) {
       .def_readwrite("tie_embeddings", &EngineConfig::tie_embeddings)
       .def_readwrite("qk_norm", &EngineConfig::qk_norm)
       .def_readwrite("qkv_bias", &EngineConfig::qkv_bias)
+      .def_readwrite("act_q8", &EngineConfig::act_q8)
       .def_readwrite("tp_rank", &EngineConfig::tp_rank)
       .def_readwrite("tp_size", &EngineConfig::tp_size)
       .def_readwrite("device", &EngineConfig::device);
@@ -193,7 +194,7 @@ PYBIND11_MODULE(_engine, m) {
 
   m.def("gemv",
         [](std::vector<PyQMatrix*> segs, int B, uintptr_t x, int ldx, uintptr_t norm_w, float eps, uintptr_t y,
-           int ldy, int epi, uintptr_t st, int force_v1) {
+           int ldy, int epi, uintptr_t st, int force_v1, int act_q8) {
           GemvArgs a;
           std::memset(&a, 0, sizeof(a));
           a.nseg = (int)segs.size();
@@ -201,15 +202,15 @@ PYBIND11_MODULE(_engine, m) {
           for (int s = 0; s < a.nseg; ++s) { a.seg[s] = segs[s]->w; a.seg_row0[s] = r; r += segs[s]->w.rows; }
           a.N = r; a.K = segs[0]->w.cols; a.B = B;
           a.x = (const float*)x; a.ldx = ldx; a.norm_w = (const float*)norm_w; a.eps = eps;
-          a.y = (float*)y; a.ldy = ldy; a.epi = epi; a.force_v1 = force_v1;
+          a.y = (float*)y; a.ldy = ldy; a.epi = epi; a.force_v1 = force_v1; a.act_q8 = act_q8;
           launch_gemv(a, S(st));
         },
         py::arg("segs"), py::arg("B"), py::arg("x"), py::arg("ldx"), py::arg("norm_w"), py::arg("eps"), py::arg("y"),
-        py::arg("ldy"), py::arg("epi"), py::arg("stream"), py::arg("force_v1") = 0);
+        py::arg("ldy"), py::arg("epi"), py::arg("stream"), py::arg("force_v1") = 0, py::arg("act_q8") = 0);
   m.def("gemv_qkv",
         [](std::vector<PyQMatrix*> segs, int B, uintptr_t x, int ldx, uintptr_t norm_w, float eps, uintptr_t q_out,
            uintptr_t bias, int head_dim, int n_heads, int n_kv_heads, int max_ctx, int rope_neox, float rope_base,
-           uintptr_t pos, uintptr_t slot, uintptr_t k_cache, uintptr_t v_cache, uintptr_t st) {
+           uintptr_t pos, uintptr_t slot, uintptr_t k_cache, uintptr_t v_cache, uintptr_t st, int act_q8) {
           GemvArgs a;
           std::memset(&a, 0, sizeof(a));
           a.nseg = (int)segs.size();
@@ -221,9 +222,13 @@ PYBIND11_MODULE(_engine, m) {
           a.bias = (const float*)bias; a.head_dim = head_dim; a.q_dim = n_heads * head_dim;
           a.kv_dim = n_kv_heads * head_dim; a.n_kv_heads = n_kv_heads; a.max_ctx = max_ctx;
           a.rope_neox = rope_neox; a.rope_base = rope_base; a.rope_cs = nullptr; a.pos = (const int*)pos; a.slot = (const int*)slot;
-          a.k_cache = (bf16_t*)k_cache; a.v_cache = (bf16_t*)v_cache;
+          a.k_cache = (bf16_t*)k_cache; a.v_cache = (bf16_t*)v_cache; a.act_q8 = act_q8;
           launch_gemv(a, S(st));
-        });
+        },
+        py::arg("segs"), py::arg("B"), py::arg("x"), py::arg("ldx"), py::arg("norm_w"), py::arg("eps"),
+        py::arg("q_out"), py::arg("bias"), py::arg("head_dim"), py::arg("n_heads"), py::arg("n_kv_heads"),
+        py::arg("max_ctx"), py::arg("rope_neox"), py::arg("rope_base"), py::arg("pos"), py::arg("slot"),
+        py::arg("k_cache"), py::arg("v_cache"), py::arg("stream"), py::arg("act_q8") = 0);
   m.def("attn_decode",
         [](uintptr_t q, uintptr_t k, uintptr_t v, uintptr_t seq_len, uintptr_t slot, int B, int H, int Hkv, int hd,
            int max_ctx, int n_chunks, float scale, uintptr_t opart, uintptr_t ml, uintptr_t out, uintptr_t st) {

@@ -37,6 +37,7 @@ struct EngineConfig {
   int tie_embeddings = 0;
   int qk_norm = 0;
   int qkv_bias = 0;
+  int act_q8 = 1;  // int8 activations (v_dot4) in the quantised GEMVs, as llama.cpp's q8_1 path
   // tensor parallel (the engine holds this rank's shard; collectives via the comm hook)
   int tp_rank = 0;
   int tp_size = 1;

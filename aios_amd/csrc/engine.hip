@@ -416,6 +416,7 @@ void Engine::gemv(const std::vector<const QMat*>& segs, int N, int K, int B, con
                   const float* norm_w, float* y, int ldy, int epi, int layer) {
   GemvArgs a;
   std::memset(&a, 0, sizeof(a));
+  a.act_q8 = cfg_.act_q8;
   a.nseg = (int)segs.size();
   int row = 0;
   for (int s = 0; s < a.nseg; ++s) {
@@ -473,6 +474,7 @@ void Engine::layer_decode(int l, int B) {
       for (auto* m : grp) n += m->w.rows;
       GemvArgs a;
       std::memset(&a, 0, sizeof(a));
+  a.act_q8 = cfg_.act_q8;
       a.nseg = (int)grp.size();
       int r = 0;
       for (int s = 0; s < a.nseg; ++s) { a.seg[s] = grp[s]->w; a.seg_row0[s] = r; r += grp[s]->w.rows; }
@@ -602,6 +604,7 @@ std::vector<float> Engine::prefill(int slot, const std::vector<int>& tokens, int
             for (auto* m : grp) nn += m->w.rows;
             GemvArgs a;
             std::memset(&a, 0, sizeof(a));
+  a.act_q8 = cfg_.act_q8;
             a.nseg = (int)grp.size();
             int r = 0;
             for (int s = 0; s < a.nseg; ++s) { a.seg[s] = grp[s]->w; a.seg_row0[s] = r; r += grp[s]->w.rows; }

@@ -22,6 +22,7 @@ struct GemvArgs {
   int row_base;                 // global row of local row 0 (epilogue indexing)
   int kt_max;                   // K tile held in LDS (set by launch_gemv)
   int force_v1;                 // testing: bypass the persistent kernel
+  int act_q8;                   // int8-quantised activations (v_dot4) for quantised weights
   const float* x;               // [B][ldx] fp32 input (residual stream if norm_w != null)
   int ldx;
   const float* norm_w;          // RMSNorm weight [K] or null

@@ -20,21 +20,43 @@ from .config import ROPE_NEOX, ModelConfig
 
 class ReferenceModel:
     def __init__(self, cfg: ModelConfig, weights: Dict[str, torch.Tensor], kv_bf16: bool = False,
-                 device: str = "cpu"):
+                 device: str = "cpu", act_q8: bool = False, quantized: Optional[set] = None):
         self.cfg = cfg
         self.w = weights
         self.kv_bf16 = kv_bf16
         self.device = device
+        self.act_q8 = act_q8                     # emulate the engine's int8 activation path
+        self.quantized = quantized or set()      # weight names stored in a block-quant format
 
     @classmethod
-    def from_gguf(cls, path: str, kv_bf16: bool = False, device: str = "cpu") -> "ReferenceModel":
+    def from_gguf(cls, path: str, kv_bf16: bool = False, device: str = "cpu", act_q8: bool = False) -> "ReferenceModel":
+        from ..gguf.quants import GGMLType
+
         r = GGUFReader(path)
         cfg = ModelConfig.from_gguf(r)
         w = {}
-        for name in r.tensors:
+        quant = set()
+        for name, ti in r.tensors.items():
             w[name] = torch.from_numpy(np.ascontiguousarray(r.dequantize(name))).to(device)
+            if ti.ggml_type not in (GGMLType.F32, GGMLType.F16, GGMLType.BF16):
+                quant.add(name)
         r.close()
-        return cls(cfg, w, kv_bf16=kv_bf16, device=device)
+        return cls(cfg, w, kv_bf16=kv_bf16, device=device, act_q8=act_q8, quantized=quant)
+
+    @staticmethod
+    def q8(x: torch.Tensor) -> torch.Tensor:
+        """Per-32-block int8 round trip of activations (amax/127 scale, round-half-even)."""
+        shp = x.shape
+        xb = x.reshape(-1, 32).to(torch.float32)
+        amax = xb.abs().amax(-1, keepdim=True)
+        inv = torch.where(amax > 0, 127.0 / amax, torch.zeros_like(amax))
+        q = torch.round(xb * inv).clamp(-127, 127)
+        return (q * (amax / 127.0)).reshape(shp)
+
+    def _mm(self, x: torch.Tensor, name: str) -> torch.Tensor:
+        if self.act_q8 and name in self.quantized:
+            x = self.q8(x)
+        return x @ self.w[name].T
 
     # ------------------------------------------------------------------------------------------
     def _rms(self, x, w):
@@ -75,9 +97,9 @@ class ReferenceModel:
         for l in range(cfg.n_layers):
             p = f"blk.{l}."
             h = self._rms(x, self.w[p + "attn_norm.weight"])
-            q = h @ self.w[p + "attn_q.weight"].T
-            k = h @ self.w[p + "attn_k.weight"].T
-            v = h @ self.w[p + "attn_v.weight"].T
+            q = self._mm(h, p + "attn_q.weight")
+            k = self._mm(h, p + "attn_k.weight")
+            v = self._mm(h, p + "attn_v.weight")
             if p + "attn_q.bias" in self.w:
                 q = q + self.w[p + "attn_q.bias"]
                 k = k + self.w[p + "attn_k.bias"]
@@ -106,15 +128,14 @@ class ReferenceModel:
             att = att.masked_fill((kpos > qpos)[None], float("-inf"))
             att = torch.softmax(att, dim=-1)
             o = torch.einsum("hts,shd->thd", att, vv).reshape(T, H * hd)
-            x = x + o @ self.w[p + "attn_output.weight"].T
+            x = x + self._mm(o, p + "attn_output.weight")
             h = self._rms(x, self.w[p + "ffn_norm.weight"])
-            g = h @ self.w[p + "ffn_gate.weight"].T
-            u = h @ self.w[p + "ffn_up.weight"].T
-            x = x + (torch.nn.functional.silu(g) * u) @ self.w[p + "ffn_down.weight"].T
+            g = self._mm(h, p + "ffn_gate.weight")
+            u = self._mm(h, p + "ffn_up.weight")
+            x = x + self._mm(torch.nn.functional.silu(g) * u, p + "ffn_down.weight")
         cache["len"] = start + T
         x = self._rms(x, self.w["output_norm.weight"])
-        out_w = self.w.get("output.weight", self.w["token_embd.weight"])
-        return x @ out_w.T
+        return self._mm(x, "output.weight" if "output.weight" in self.w else "token_embd.weight")
 
     @torch.no_grad()
     def greedy(self, prompt: List[int], n_new: int) -> List[int]:

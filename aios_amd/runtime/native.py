@@ -63,7 +63,7 @@ def require():
 
 
 def engine_config(cfg, max_ctx: Optional[int] = None, max_slots: int = 4, max_batch: int = 8, device: int = 0,
-                  tp_rank: int = 0, tp_size: int = 1):
+                  tp_rank: int = 0, tp_size: int = 1, act_q8: bool = True):
     """aios_amd.models.config.ModelConfig -> native EngineConfig (per-rank shapes under TP)."""
     m = require()
     ec = m.EngineConfig()
@@ -89,4 +89,5 @@ def engine_config(cfg, max_ctx: Optional[int] = None, max_slots: int = 4, max_ba
     ec.tp_rank = tp_rank
     ec.tp_size = tp_size
     ec.device = device
+    ec.act_q8 = int(act_q8)
     return ec

@@ -28,10 +28,11 @@ def _load(path, **kw):
 
 
 @pytest.mark.parametrize("recipe", ["Q4_K_M", "Q4_0", "Q8_0", "BF16", "mistral_shape"])
-def test_prefill_logits_match_reference(model_files, recipe):
+@pytest.mark.parametrize("q8", [False, True])
+def test_prefill_logits_match_reference(model_files, recipe, q8):
     path = model_files[recipe]
-    eng, cfg = _load(path)
-    ref = ReferenceModel.from_gguf(path, kv_bf16=True)
+    eng, cfg = _load(path, act_q8=q8)
+    ref = ReferenceModel.from_gguf(path, kv_bf16=True, act_q8=q8)
     prompt = [1] + list(np.random.default_rng(0).integers(3, cfg.vocab_size, 40))
     logits = torch.from_numpy(np.asarray(eng.prefill(0, prompt, 0, True)))
     rl = ref.forward(prompt)[-1]
@@ -41,10 +42,11 @@ def test_prefill_logits_match_reference(model_files, recipe):
 
 
 @pytest.mark.parametrize("recipe", ["Q4_K_M", "BF16"])
-def test_greedy_decode_token_exact(model_files, recipe):
+@pytest.mark.parametrize("q8", [False, True])
+def test_greedy_decode_token_exact(model_files, recipe, q8):
     path = model_files[recipe]
-    eng, cfg = _load(path)
-    ref = ReferenceModel.from_gguf(path, kv_bf16=True)
+    eng, cfg = _load(path, act_q8=q8)
+    ref = ReferenceModel.from_gguf(path, kv_bf16=True, act_q8=q8)
     prompt = [1, 30, 40, 50, 60, 70, 80]
     n = 12
     want = ref.greedy(prompt, n)

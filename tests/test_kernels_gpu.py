@@ -23,6 +23,12 @@ def stream():
     return torch.cuda.current_stream().cuda_stream
 
 
+def q8_ref(x):
+    from aios_amd.models.reference import ReferenceModel
+
+    return ReferenceModel.q8(x)
+
+
 def qmat(E, t, rows, cols, seed=0, std=0.05):
     rng = np.random.default_rng(seed)
     x = rng.standard_normal((rows, cols)).astype(np.float32) * std
@@ -53,15 +59,17 @@ def test_get_rows(E, t):
 @pytest.mark.parametrize("t", QTS)
 @pytest.mark.parametrize("B", [1, 2, 3, 8])
 @pytest.mark.parametrize("K", [512, 2304])
-@pytest.mark.parametrize("v1", [0, 1])
+@pytest.mark.parametrize("mode", ["v1", "v2", "q8"])
 @pytest.mark.parametrize("N", [264, 4098])
-def test_gemv_store(E, t, B, K, v1, N):
+def test_gemv_store(E, t, B, K, mode, N):
     m, W = qmat(E, t, N, K, seed=3)
     x = torch.randn(B, K, device="cuda")
     y = torch.zeros(B, N, device="cuda")
-    E.gemv([m], B, x.data_ptr(), K, 0, 1e-5, y.data_ptr(), N, E.EPI_STORE, stream(), v1)
+    q8 = mode == "q8" and t not in (GGMLType.F16, GGMLType.BF16)
+    E.gemv([m], B, x.data_ptr(), K, 0, 1e-5, y.data_ptr(), N, E.EPI_STORE, stream(), int(mode == "v1"), int(q8))
     torch.cuda.synchronize()
-    ref = x.cpu() @ W.T
+    xr = q8_ref(x.cpu()) if q8 else x.cpu()
+    ref = xr @ W.T
     assert torch.allclose(y.cpu(), ref, atol=2e-3, rtol=2e-3), (y.cpu() - ref).abs().max()
 
 
@@ -123,7 +131,8 @@ def rope_ref(x, pos, theta, neox=False):
 
 
 @pytest.mark.parametrize("mixed", [False, True])
-def test_gemv_qkv_rope_kv(E, mixed):
+@pytest.mark.parametrize("q8", [0, 1])
+def test_gemv_qkv_rope_kv(E, mixed, q8):
     d, H, Hkv, hd, max_ctx, slots = 256, 4, 2, 64, 128, 3
     B = 3
     wq, Wq = qmat(E, GGMLType.Q4_K, H * hd, d, seed=7)
@@ -137,10 +146,12 @@ def test_gemv_qkv_rope_kv(E, mixed):
     vc = torch.zeros_like(kc)
     q = torch.zeros(B, H * hd, device="cuda")
     E.gemv_qkv([wq, wk, wv], B, x.data_ptr(), d, nw.data_ptr(), 1e-5, q.data_ptr(), 0, hd, H, Hkv, max_ctx, 0,
-               10000.0, pos.data_ptr(), slot.data_ptr(), kc.data_ptr(), vc.data_ptr(), stream())
+               10000.0, pos.data_ptr(), slot.data_ptr(), kc.data_ptr(), vc.data_ptr(), stream(), q8)
     torch.cuda.synchronize()
     xc = x.cpu()
     xn = xc * torch.rsqrt((xc * xc).mean(-1, keepdim=True) + 1e-5) * nw.cpu()
+    if q8:
+        xn = q8_ref(xn)
     qr = rope_ref((xn @ Wq.T).view(B, H, hd), pos.cpu(), 10000.0)
     kr = rope_ref((xn @ Wk.T).view(B, Hkv, hd), pos.cpu(), 10000.0)
     vr = (xn @ Wv.T).view(B, Hkv, hd)
