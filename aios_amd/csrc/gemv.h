@@ -23,6 +23,9 @@ struct GemvArgs {
   int kt_max;                   // K tile held in LDS (set by launch_gemv)
   int force_v1;                 // testing: bypass the persistent kernel
   int act_q8;                   // int8-quantised activations (v_dot4) for quantised weights
+  int tune_grid;                // blocks per CU override for the persistent kernels (0 = auto)
+  int tune_u;                   // chunks per lane per work item override (0 = auto; 1, 2, 4)
+  int tune_ksplit;              // -1 disables the K-split decomposition (testing / tuning)
   const float* x;               // [B][ldx] fp32 input (residual stream if norm_w != null)
   int ldx;
   const float* norm_w;          // RMSNorm weight [K] or null

@@ -514,316 +514,7 @@ bool launch_gemv_persistent(GemvArgs a, hipStream_t st) {
 }
 
 
-// =============================================================================================
-// int8-activation path (the llama.cpp "q8_1 x quant" trick, done per workgroup in LDS):
-// x is quantised to int8 per 32-element block (scale dx = amax/127) while it is staged, and
-// each 16-B weight chunk is multiplied with v_dot4_i32_i8 (4 MACs per VALU op) straight on the
-// 4-bit / 6-bit codes: ~5x fewer VALU ops per weight than the fp32 path and 4x fewer LDS bytes.
-// Per 16-run r of a chunk: contrib = sc_r * dx_r * isum_r - of_r * sx_r, with sx_r = dx_r*sum(xq)
-// over the run (the K-quant "min" and the Q4_0/Q6_K code bias fold into of_r).
-// LDS per batch row: xq[nch][W] bytes (16-B pieces rotated by (c >> 3)) + (dx, sx)[nch][R].
-// =============================================================================================
-template <int QT>
-struct QDot {
-  // isum[r] over the chunk's runs; x = 8 (or 4) packed int8x4 words in slot order
-  __device__ static void isums(const RawChunk& r, int c, const int (&x)[8], int* is);
-};
-template <>
-struct QDot<QT_Q4_K> {
-  __device__ static void isums(const RawChunk& r, int c, const int (&x)[8], int* is) {
-    int s0 = 0, s1 = 0;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const uint32_t wv = u4_word(r.a, i);
-      s0 = __builtin_amdgcn_sdot4((int)(wv & 0x0f0f0f0fu), x[i], s0, false);
-      s1 = __builtin_amdgcn_sdot4((int)((wv >> 4) & 0x0f0f0f0fu), x[4 + i], s1, false);
-    }
-    is[0] = s0; is[1] = s1;
-  }
-};
-template <>
-struct QDot<QT_Q4_0> {
-  __device__ static void isums(const RawChunk& r, int c, const int (&x)[8], int* is) {
-    QDot<QT_Q4_K>::isums(r, c, x, is);
-  }
-};
-template <>
-struct QDot<QT_Q5_K> {
-  __device__ static void isums(const RawChunk& r, int c, const int (&x)[8], int* is) {
-    const int g = (c & 7) >> 1;
-    int s0 = 0, s1 = 0;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const uint32_t wv = u4_word(r.a, i), hv = u4_word(r.c, i);
-      const uint32_t lo = (wv & 0x0f0f0f0fu) | (((hv >> (2 * g)) & 0x01010101u) << 4);
-      const uint32_t hi = ((wv >> 4) & 0x0f0f0f0fu) | (((hv >> (2 * g + 1)) & 0x01010101u) << 4);
-      s0 = __builtin_amdgcn_sdot4((int)lo, x[i], s0, false);
-      s1 = __builtin_amdgcn_sdot4((int)hi, x[4 + i], s1, false);
-    }
-    is[0] = s0; is[1] = s1;
-  }
-};
-template <>
-struct QDot<QT_Q6_K> {
-  __device__ static void isums(const RawChunk& r, int c, const int (&x)[8], int* is) {
-    const int hs = 2 * ((c & 3) >> 1);
-    int s0 = 0, s1 = 0;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const uint32_t wv = u4_word(r.a, i), hv = u4_word(r.b, i);
-      const uint32_t lo = (wv & 0x0f0f0f0fu) | (((hv >> hs) & 0x03030303u) << 4);
-      const uint32_t hi = ((wv >> 4) & 0x0f0f0f0fu) | (((hv >> (hs + 4)) & 0x03030303u) << 4);
-      s0 = __builtin_amdgcn_sdot4((int)lo, x[i], s0, false);
-      s1 = __builtin_amdgcn_sdot4((int)hi, x[4 + i], s1, false);
-    }
-    is[0] = s0; is[1] = s1;
-  }
-};
-template <>
-struct QDot<QT_Q8_0> {
-  __device__ static void isums(const RawChunk& r, int c, const int (&x)[8], int* is) {
-    int s = 0;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) s = __builtin_amdgcn_sdot4((int)u4_word(r.a, i), x[i], s, false);
-    is[0] = s;
-  }
-};
-// signed Q8_0 codes: no bias term
-__device__ __forceinline__ void q8_scales_q80(const RawChunk& r, float* sc, float* of) {
-  sc[0] = __half2float(__ushort_as_half((uint16_t)r.d));
-  of[0] = 0.f;
-}
-
-// Stage B rows of x (optionally RMS-normalised) as int8 per 32-block in chunk order.
-template <int QT>
-__device__ __forceinline__ void stage_x_q8(const float* __restrict__ x, int ldx, int B, int K,
-                                           const float* __restrict__ inv_rms, const float* __restrict__ nw,
-                                           int8_t* xq, float2* ms) {
-  using F_ = QFmt<QT>;
-  constexpr int W = F_::W, R = F_::RUNS;
-  const int nch = K / W;
-  const int nblk = K / 32;
-  for (int t = threadIdx.x; t < B * nblk; t += blockDim.x) {
-    const int b = t / nblk, blk = t - b * nblk;
-    const float* src = x + (size_t)b * ldx + blk * 32;
-    float v[32];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const float4 f = *(const float4*)(src + 4 * i);
-      v[4 * i] = f.x; v[4 * i + 1] = f.y; v[4 * i + 2] = f.z; v[4 * i + 3] = f.w;
-    }
-    if (nw) {
-      const float ir = inv_rms[b];
-      const float* wp = nw + blk * 32;
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const float4 g = *(const float4*)(wp + 4 * i);
-        v[4 * i] *= ir * g.x; v[4 * i + 1] *= ir * g.y; v[4 * i + 2] *= ir * g.z; v[4 * i + 3] *= ir * g.w;
-      }
-    }
-    float amax = 0.f;
-#pragma unroll
-    for (int i = 0; i < 32; ++i) amax = fmaxf(amax, fabsf(v[i]));
-    const float dx = amax / 127.f;
-    const float inv = amax > 0.f ? 127.f / amax : 0.f;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {  // the block's two 16-runs
-      uint32_t wq[4];
-      int isum = 0;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        uint32_t w = 0;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int q = (int)rintf(v[16 * h + 4 * j + e] * inv);
-          isum += q;
-          w |= ((uint32_t)(q & 0xff)) << (8 * e);
-        }
-        wq[j] = w;
-      }
-      int c, s0;
-      F_::run_pos(blk * 2 + h, c, s0);
-      int piece = s0 >> 4;
-      if (W == 32) piece = (piece + (c >> 3)) & 1;
-      *(uint4*)(xq + ((size_t)b * nch + c) * W + 16 * piece) = make_uint4(wq[0], wq[1], wq[2], wq[3]);
-      ms[((size_t)b * nch + c) * R + (s0 >> 4)] = make_float2(dx, dx * (float)isum);
-    }
-  }
-}
-
-template <int QT, int B, int U>
-__device__ __forceinline__ void gp_compute_q8(const RawChunk (&raw)[U][GEMV_ROWS], int it, int nch, const int8_t* xq,
-                                              const float2* ms, float (&acc)[GEMV_ROWS][B]) {
-  using F_ = QFmt<QT>;
-  constexpr int W = F_::W, R = F_::RUNS;
-  const int lane = threadIdx.x & 63;
-#pragma unroll
-  for (int u = 0; u < U; ++u) {
-    const int c = (it * U + u) * 64 + lane;
-    if (c < nch) {
-      float sc[GEMV_ROWS][R], of[GEMV_ROWS][R];
-#pragma unroll
-      for (int r = 0; r < GEMV_ROWS; ++r) {
-        if constexpr (QT == QT_Q8_0) q8_scales_q80(raw[u][r], sc[r], of[r]);
-        else QStream<QT>::scales(raw[u][r], c, sc[r], of[r]);
-      }
-#pragma unroll
-      for (int b = 0; b < B; ++b) {
-        int xv[8];
-        const int8_t* xc = xq + ((size_t)b * nch + c) * W;
-        if constexpr (W == 32) {
-          const int rot = (c >> 3) & 1;
-          const uint4 p0 = *(const uint4*)(xc + 16 * rot);
-          const uint4 p1 = *(const uint4*)(xc + 16 * (rot ^ 1));
-          xv[0] = p0.x; xv[1] = p0.y; xv[2] = p0.z; xv[3] = p0.w;
-          xv[4] = p1.x; xv[5] = p1.y; xv[6] = p1.z; xv[7] = p1.w;
-        } else {
-          const uint4 p0 = *(const uint4*)xc;
-          xv[0] = p0.x; xv[1] = p0.y; xv[2] = p0.z; xv[3] = p0.w;
-          xv[4] = xv[5] = xv[6] = xv[7] = 0;
-        }
-        float2 m[R];
-        const float2* mp = ms + ((size_t)b * nch + c) * R;
-#pragma unroll
-        for (int rr = 0; rr < R; ++rr) m[rr] = mp[rr];
-#pragma unroll
-        for (int r = 0; r < GEMV_ROWS; ++r) {
-          int is[R];
-          QDot<QT>::isums(raw[u][r], c, xv, is);
-#pragma unroll
-          for (int rr = 0; rr < R; ++rr) acc[r][b] += sc[r][rr] * m[rr].x * (float)is[rr] - of[r][rr] * m[rr].y;
-        }
-      }
-    }
-  }
-}
-
-template <int QT0, int QT1, int B, int U>
-__global__ void __launch_bounds__(GP_THREADS) gemv_persistent_q8(GemvArgs a) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  float* red = smem;
-  float* inv_rms = red + 16;
-  constexpr bool MIXED = QT0 != QT1;
-  constexpr int W0 = QFmt<QT0>::W, W1 = QFmt<QT1>::W, R0 = QFmt<QT0>::RUNS, R1 = QFmt<QT1>::RUNS;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int K = a.K;
-  const int npairs = a.N >> 1;
-  const int nch0 = K / W0, nch1 = K / W1;
-  const int nit0 = (nch0 + 64 * U - 1) / (64 * U), nit1 = (nch1 + 64 * U - 1) / (64 * U);
-  const int stride = gridDim.x * GP_WAVES;
-  // LDS: [red 64 floats][ms0: B*nch0*R0 float2][xq0: B*K bytes][ms1][xq1]
-  float2* ms0 = (float2*)(smem + 64);
-  int8_t* xq0 = (int8_t*)(ms0 + (size_t)B * nch0 * R0);
-  float2* ms1 = MIXED ? (float2*)(xq0 + (size_t)B * K) : ms0;
-  int8_t* xq1 = MIXED ? (int8_t*)(ms1 + (size_t)B * nch1 * R1) : xq0;
-
-  auto info = [&](int p, int& lrow, bool& t1, const QWeight*& w) {
-    const int row = 2 * p;
-    int s = 0;
-#pragma unroll
-    for (int k = 1; k < GEMV_MAX_SEGS; ++k)
-      if (k < a.nseg && row >= a.seg_row0[k]) s = k;
-    lrow = row - a.seg_row0[s];
-    t1 = MIXED && (s == a.nseg - 1) && a.nseg > 1;
-    w = &a.seg[s];
-  };
-  auto load = [&](int p, int it, RawChunk (&r)[U][GEMV_ROWS]) {
-    int lrow;
-    bool t1;
-    const QWeight* w;
-    info(p, lrow, t1, w);
-    if (MIXED && t1) gp_load<QT1, U>(*w, lrow, it, nch1, r);
-    else gp_load<QT0, U>(*w, lrow, it, nch0, r);
-  };
-
-  int p = blockIdx.x * GP_WAVES + wave;
-  int it = 0;
-  RawChunk bufA[U][GEMV_ROWS], bufB[U][GEMV_ROWS];
-  if (p < npairs) load(p, 0, bufA);
-
-  if (a.norm_w) {
-    for (int b = 0; b < a.B; ++b) {
-      float s = 0.f;
-      const float* xb = a.x + (size_t)b * a.ldx;
-      for (int k = threadIdx.x * 4; k < K; k += GP_THREADS * 4) {
-        const float4 v = *(const float4*)(xb + k);
-        s += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
-      }
-      s = block_sum(s, red);
-      if (threadIdx.x == 0) inv_rms[b] = rsqrtf(s / (float)K + a.eps);
-      __syncthreads();
-    }
-  }
-  stage_x_q8<QT0>(a.x, a.ldx, a.B, K, inv_rms, a.norm_w, xq0, ms0);
-  if (MIXED) stage_x_q8<QT1>(a.x, a.ldx, a.B, K, inv_rms, a.norm_w, xq1, ms1);
-  __syncthreads();
-
-  float acc[GEMV_ROWS][B];
-#pragma unroll
-  for (int r = 0; r < GEMV_ROWS; ++r)
-#pragma unroll
-    for (int b = 0; b < B; ++b) acc[r][b] = 0.f;
-
-  auto step = [&](RawChunk (&cur)[U][GEMV_ROWS], RawChunk (&nxt)[U][GEMV_ROWS]) -> bool {
-    int lrow;
-    bool t1;
-    const QWeight* w;
-    info(p, lrow, t1, w);
-    const int nit = (MIXED && t1) ? nit1 : nit0;
-    int pn = p, itn = it + 1;
-    if (itn >= nit) { pn = p + stride; itn = 0; }
-    if (pn < npairs) load(pn, itn, nxt);
-    if (MIXED && t1) gp_compute_q8<QT1, B, U>(cur, it, nch1, xq1, ms1, acc);
-    else gp_compute_q8<QT0, B, U>(cur, it, nch0, xq0, ms0, acc);
-    if (itn == 0) {
-#pragma unroll
-      for (int r = 0; r < GEMV_ROWS; ++r)
-#pragma unroll
-        for (int b = 0; b < B; ++b) acc[r][b] = wave_sum(acc[r][b]);
-      if (lane < a.B) {
-        float v0 = 0.f, v1 = 0.f;
-#pragma unroll
-        for (int b = 0; b < B; ++b)
-          if (lane == b) { v0 = acc[0][b]; v1 = acc[1][b]; }
-        gemv_epilogue(a, a.row_base + 2 * p, lane, v0, v1);
-      }
-#pragma unroll
-      for (int r = 0; r < GEMV_ROWS; ++r)
-#pragma unroll
-        for (int b = 0; b < B; ++b) acc[r][b] = 0.f;
-    }
-    p = pn;
-    it = itn;
-    return p < npairs;
-  };
-  while (p < npairs) {
-    if (!step(bufA, bufB)) break;
-    if (!step(bufB, bufA)) break;
-  }
-}
-
-template <int QT0, int QT1, int B, int U>
-bool launch_gemv_q8(GemvArgs a, hipStream_t st) {
-  constexpr bool MIXED = QT0 != QT1;
-  auto bytes_for = [&](int W, int R) { return (size_t)B * a.K + (size_t)B * (a.K / W) * R * 8; };
-  const size_t lds = 64 * 4 + bytes_for(QFmt<QT0>::W, QFmt<QT0>::RUNS) +
-                     (MIXED ? bytes_for(QFmt<QT1>::W, QFmt<QT1>::RUNS) : 0) + 64;
-  if (lds > 96 * 1024) return false;
-  static int occ = -1;
-  if (occ < 0) {
-    int o = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, gemv_persistent_q8<QT0, QT1, B, U>, GP_THREADS, lds) !=
-            hipSuccess || o <= 0)
-      o = 1;
-    occ = o;
-  }
-  const int per_cu = std::max(1, std::min(occ, (int)((160 * 1024) / lds)));
-  const int groups = (a.N / 2 + GP_WAVES - 1) / GP_WAVES;
-  const int blocks = std::min(groups, device_cu_count() * per_cu);
-  a.kt_max = a.K;
-  hipLaunchKernelGGL((gemv_persistent_q8<QT0, QT1, B, U>), dim3(blocks), dim3(GP_THREADS), lds, st, a);
-  return true;
-}
+#include "gemv_q8.h"
 
 inline int qtype_block(int qt) {
   return (qt == QT_Q4_K || qt == QT_Q5_K || qt == QT_Q6_K) ? 256 : (qt == QT_F16 || qt == QT_BF16 ? 8 : 32);
@@ -849,7 +540,12 @@ void launch_gemv_pair(const GemvArgs& a, hipStream_t st) {
   constexpr bool Q8OK = QT0 != QT_F16 && QT0 != QT_BF16;
   if constexpr (Q8OK) {
     if (!a.force_v1 && a.act_q8) {
-      if (a.B == 1 && launch_gemv_q8<QT0, QT1, 1, 2>(a, st)) return;
+      if (a.B == 1) {
+        const int u = a.tune_u ? a.tune_u : 2;
+        if (u == 1 && launch_gemv_q8<QT0, QT1, 1, 1>(a, st)) return;
+        if (u == 4 && launch_gemv_q8<QT0, QT1, 1, 4>(a, st)) return;
+        if (u == 2 && launch_gemv_q8<QT0, QT1, 1, 2>(a, st)) return;
+      }
       if (a.B == 2 && launch_gemv_q8<QT0, QT1, 2, 2>(a, st)) return;
       if (a.B > 2 && a.B <= 4 && launch_gemv_q8<QT0, QT1, 4, 2>(a, st)) return;
       if (a.B > 4 && launch_gemv_q8<QT0, QT1, 8, 1>(a, st)) return;

@@ -73,17 +73,25 @@ def test_gemv_store(E, t, B, K, mode, N):
     assert torch.allclose(y.cpu(), ref, atol=2e-3, rtol=2e-3), (y.cpu() - ref).abs().max()
 
 
-@pytest.mark.parametrize("t", [GGMLType.Q4_K, GGMLType.Q6_K, GGMLType.BF16])
-@pytest.mark.parametrize("B", [1, 4])
-def test_gemv_long_k_tiles(E, t, B):
-    # K = 14336: B = 1 runs the persistent kernel, B = 4 forces several LDS K-tiles (v1)
-    N, K = 64, 14336
+@pytest.mark.parametrize("t", [GGMLType.Q4_K, GGMLType.Q6_K, GGMLType.Q8_0, GGMLType.BF16])
+@pytest.mark.parametrize("B", [1, 2, 4])
+@pytest.mark.parametrize("q8", [0, 1])
+@pytest.mark.parametrize("ksplit", [0, -1])
+def test_gemv_long_k(E, t, B, q8, ksplit):
+    # K = 14336: fp32 persistent kernel / int8 k-split / int8 row kernels / v1 K-tiles (B = 4, fp32)
+    N, K = 200, 14336
     m, W = qmat(E, t, N, K, seed=4, std=0.02)
     x = torch.randn(B, K, device="cuda")
+    nw = torch.rand(K, device="cuda") + 0.5
     y = torch.zeros(B, N, device="cuda")
-    E.gemv([m], B, x.data_ptr(), K, 0, 1e-5, y.data_ptr(), N, E.EPI_STORE, stream())
+    q8 = q8 and t != GGMLType.BF16
+    E.gemv([m], B, x.data_ptr(), K, nw.data_ptr(), 1e-5, y.data_ptr(), N, E.EPI_STORE, stream(), 0, q8, 0, 0, ksplit)
     torch.cuda.synchronize()
-    ref = x.cpu() @ W.T
+    xc = x.cpu()
+    xn = xc * torch.rsqrt((xc * xc).mean(-1, keepdim=True) + 1e-5) * nw.cpu()
+    if q8:
+        xn = q8_ref(xc * nw.cpu()) * torch.rsqrt((xc * xc).mean(-1, keepdim=True) + 1e-5)
+    ref = xn @ W.T
     assert torch.allclose(y.cpu(), ref, atol=5e-3, rtol=5e-3)
 
 
