@@ -148,6 +148,7 @@ class Engine {
   float* d_temp_ = nullptr;
   uint8_t* d_mask_ = nullptr;
   int n_chunks_ = 0;
+  int* attn_cnt_ = nullptr;  // [max(prefill_rows, max_batch)][n_kv_heads] combine tickets
   float2* rope_cs_ = nullptr;  // [max_ctx][head_dim/2] cos/sin computed in double on the host
   int prefill_rows_ = 64;  // rows of the prefill workspace
   float *pf_x_ = nullptr, *pf_q_ = nullptr, *pf_attn_ = nullptr, *pf_ff_ = nullptr, *pf_qkv_ = nullptr;

@@ -353,6 +353,11 @@ void Engine::finalize() {
   HIP_CHECK(hipMemset(v_cache_, 0, kv_bytes_ / 2));
   n_chunks_ = (cfg_.max_ctx + ATTN_CHUNK - 1) / ATTN_CHUNK;
   {
+    const size_t nc = (size_t)std::max(prefill_rows_, Bm) * Hkv;
+    attn_cnt_ = (int*)dmalloc(nc * 4);
+    HIP_CHECK(hipMemset(attn_cnt_, 0, nc * 4));
+  }
+  {
     const int half = hd / 2;
     std::vector<float> tab((size_t)cfg_.max_ctx * half * 2);
     for (int pos = 0; pos < cfg_.max_ctx; ++pos)
@@ -519,7 +524,7 @@ void Engine::layer_decode(int l, int B) {
     a.B = B; a.n_heads = cfg_.n_heads; a.n_kv_heads = cfg_.n_kv_heads; a.head_dim = hd; a.max_ctx = cfg_.max_ctx;
     a.n_chunks = n_chunks_;
     a.scale = 1.f / std::sqrt((float)hd);
-    a.o_part = opart_; a.ml = ml_; a.out = attn_;
+    a.o_part = opart_; a.ml = ml_; a.out = attn_; a.counters = attn_cnt_;
     launch_attn_decode(a, stream_);
   }
   // ---- O projection (+ residual; TP: partial -> all-reduce -> add)
@@ -647,7 +652,7 @@ std::vector<float> Engine::prefill(int slot, const std::vector<int>& tokens, int
           a.max_ctx = cfg_.max_ctx;
           a.n_chunks = n_chunks_;
           a.scale = 1.f / std::sqrt((float)cfg_.head_dim);
-          a.o_part = opart_; a.ml = ml_; a.out = ab;
+          a.o_part = opart_; a.ml = ml_; a.out = ab; a.counters = attn_cnt_;
           launch_attn_decode(a, stream_);
         }
         for (int sb = 0; sb < nsub; ++sb) {

@@ -1,25 +1,51 @@
-// Split-K flash-decode GQA attention over the bf16 KV cache (decode shape).
+// Split-K flash-decode GQA attention over the bf16 KV cache (decode shape),
+// with the log-sum-exp combine fused in (last-arriving workgroup per (row, kv-head)).
 //
 // grid = (n_chunks, n_kv_heads, B); a 256-thread workgroup handles one KV head x one chunk of
 // ATTN_CHUNK keys for all G = n_heads/n_kv_heads query heads of the group, so each K/V byte is
-// read once per group (GQA reuse).  K/V rows go straight to VGPRs (16 B per lane, LPK = hd/8
-// lanes per key -- the 'attention decode' row of the CDNA guide's Appendix B); scores and the
-// chunk softmax live in LDS; each chunk emits an unnormalised partial (o, m, l) that a tiny
-// combine kernel merges (log-sum-exp).  Chunks past seq_len exit immediately, so the grid can be
-// sized for max_ctx and captured once in a hipGraph while the context grows.
+// read once per group (GQA reuse).  Latency is what matters at decode sizes, so every global load
+// a lane needs (its q slice, and its K and V rows) is issued up front: K/V rows below max_ctx are
+// always valid memory, so the loads do not wait for seq_len -- keys past it are masked after.
+// K/V go straight to VGPRs (16 B per lane, LPK = hd/8 lanes per key: the 'attention decode' row
+// of the CDNA guide's Appendix B); scores and the chunk softmax live in LDS.
+//
+// Combine: each chunk writes its unnormalised partial (o, m, l) with write-through (sc1, agent
+// scope) stores, drains them (s_waitcnt vmcnt(0)), and after a workgroup barrier one lane bumps
+// an agent-scope counter for (row, kv head).  The workgroup that draws the last ticket reads all
+// partials with sc1 loads and writes the normalised output, then re-arms the counter -- the
+// write-through hand-off of CDNA guide §6 Guideline 16 / split-K item 2 (no release/acquire
+// fences, placement independent).  Chunks past seq_len exit before arriving; the expected
+// arrivals are ceil(seq_len / ATTN_CHUNK).
 #include "../common.h"
 #include "../ops.h"
 
 namespace aios {
+
+__device__ __forceinline__ void st_wt(float* p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ld_wt(const float* p) {
+  return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ void bf16x8_to_f32(const uint4& v, float f[8]) {
+  f[0] = bf16_to_f32(v.x & 0xffff); f[1] = bf16_to_f32(v.x >> 16);
+  f[2] = bf16_to_f32(v.y & 0xffff); f[3] = bf16_to_f32(v.y >> 16);
+  f[4] = bf16_to_f32(v.z & 0xffff); f[5] = bf16_to_f32(v.z >> 16);
+  f[6] = bf16_to_f32(v.w & 0xffff); f[7] = bf16_to_f32(v.w >> 16);
+}
 
 template <int HD, int G>
 __global__ void __launch_bounds__(256) attn_decode_kernel(AttnDecodeArgs a) {
   constexpr int LPK = HD / 8;        // lanes per key (8 dims per lane)
   constexpr int KPS = 64 / LPK;      // keys per wave step
   constexpr int CH = ATTN_CHUNK;
+  constexpr int KPW = CH / 4;        // keys per wave
+  constexpr int STEPS = KPW / KPS;
   __shared__ float s_p[G][CH];
   __shared__ float s_o[4][G][HD];
   __shared__ float s_m[G], s_l[G];
+  __shared__ int s_last;
 
   const int ch = blockIdx.x, kvh = blockIdx.y, b = blockIdx.z;
   const int len = a.seq_len[b];
@@ -33,49 +59,50 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(AttnDecodeArgs a) {
   const bf16_t* kc = a.k_cache + kv_base;
   const bf16_t* vc = a.v_cache + kv_base;
 
-  // q slice for the group's G heads: 8 dims per lane
+  // ---- every global load up front
+  uint4 kraw[STEPS], vraw[STEPS];
+#pragma unroll
+  for (int s = 0; s < STEPS; ++s) {
+    const int key = start + wave * KPW + s * KPS + ksub;  // < start + CH <= max_ctx
+    kraw[s] = *(const uint4*)(kc + (size_t)key * HD + dsl * 8);
+  }
   float q[G][8];
 #pragma unroll
   for (int g = 0; g < G; ++g) {
     const float* qp = a.q + ((size_t)b * a.n_heads + kvh * G + g) * HD + dsl * 8;
     const float4 q0 = *(const float4*)qp, q1 = *(const float4*)(qp + 4);
-    q[g][0] = q0.x * a.scale; q[g][1] = q0.y * a.scale; q[g][2] = q0.z * a.scale; q[g][3] = q0.w * a.scale;
-    q[g][4] = q1.x * a.scale; q[g][5] = q1.y * a.scale; q[g][6] = q1.z * a.scale; q[g][7] = q1.w * a.scale;
+    q[g][0] = q0.x; q[g][1] = q0.y; q[g][2] = q0.z; q[g][3] = q0.w;
+    q[g][4] = q1.x; q[g][5] = q1.y; q[g][6] = q1.z; q[g][7] = q1.w;
+  }
+#pragma unroll
+  for (int s = 0; s < STEPS; ++s) {
+    const int key = start + wave * KPW + s * KPS + ksub;
+    vraw[s] = *(const uint4*)(vc + (size_t)key * HD + dsl * 8);
   }
 
-  // ---- scores: wave w handles keys [w*CH/4, (w+1)*CH/4) of the chunk
-  constexpr int KPW = CH / 4;
+  // ---- scores
 #pragma unroll
-  for (int s = 0; s < KPW / KPS; ++s) {
+  for (int s = 0; s < STEPS; ++s) {
     const int kl = wave * KPW + s * KPS + ksub;
+    float kf[8];
+    bf16x8_to_f32(kraw[s], kf);
     float dot[G];
 #pragma unroll
-    for (int g = 0; g < G; ++g) dot[g] = 0.f;
-    if (kl < n) {
-      const uint4 kv = *(const uint4*)(kc + (size_t)(start + kl) * HD + dsl * 8);
-      float kf[8];
-      kf[0] = bf16_to_f32(kv.x & 0xffff); kf[1] = bf16_to_f32(kv.x >> 16);
-      kf[2] = bf16_to_f32(kv.y & 0xffff); kf[3] = bf16_to_f32(kv.y >> 16);
-      kf[4] = bf16_to_f32(kv.z & 0xffff); kf[5] = bf16_to_f32(kv.z >> 16);
-      kf[6] = bf16_to_f32(kv.w & 0xffff); kf[7] = bf16_to_f32(kv.w >> 16);
-#pragma unroll
-      for (int g = 0; g < G; ++g)
-#pragma unroll
-        for (int i = 0; i < 8; ++i) dot[g] = fmaf(q[g][i], kf[i], dot[g]);
-    }
-#pragma unroll
     for (int g = 0; g < G; ++g) {
+      dot[g] = 0.f;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) dot[g] = fmaf(q[g][i], kf[i], dot[g]);
 #pragma unroll
       for (int o = LPK / 2; o > 0; o >>= 1) dot[g] += __shfl_xor(dot[g], o, 64);
     }
     if (dsl == 0) {
 #pragma unroll
-      for (int g = 0; g < G; ++g) s_p[g][kl] = kl < n ? dot[g] : -INFINITY;
+      for (int g = 0; g < G; ++g) s_p[g][kl] = kl < n ? dot[g] * a.scale : -INFINITY;
     }
   }
   __syncthreads();
 
-  // ---- chunk softmax: wave w handles heads w, w+4, ...  (CH = 64 keys = one per lane)
+  // ---- chunk softmax: wave w handles heads w, w+4, ... (CH = 64 keys = one per lane)
   for (int g = wave; g < G; g += 4) {
     const float v = s_p[g][lane];
     const float m = wave_max(v);
@@ -93,24 +120,17 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(AttnDecodeArgs a) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) o[g][i] = 0.f;
 #pragma unroll
-  for (int s = 0; s < KPW / KPS; ++s) {
+  for (int s = 0; s < STEPS; ++s) {
     const int kl = wave * KPW + s * KPS + ksub;
-    if (kl < n) {
-      const uint4 vv = *(const uint4*)(vc + (size_t)(start + kl) * HD + dsl * 8);
-      float vf[8];
-      vf[0] = bf16_to_f32(vv.x & 0xffff); vf[1] = bf16_to_f32(vv.x >> 16);
-      vf[2] = bf16_to_f32(vv.y & 0xffff); vf[3] = bf16_to_f32(vv.y >> 16);
-      vf[4] = bf16_to_f32(vv.z & 0xffff); vf[5] = bf16_to_f32(vv.z >> 16);
-      vf[6] = bf16_to_f32(vv.w & 0xffff); vf[7] = bf16_to_f32(vv.w >> 16);
+    float vf[8];
+    bf16x8_to_f32(vraw[s], vf);
 #pragma unroll
-      for (int g = 0; g < G; ++g) {
-        const float p = s_p[g][kl];
+    for (int g = 0; g < G; ++g) {
+      const float p = s_p[g][kl];  // 0 for masked keys
 #pragma unroll
-        for (int i = 0; i < 8; ++i) o[g][i] = fmaf(p, vf[i], o[g][i]);
-      }
+      for (int i = 0; i < 8; ++i) o[g][i] = fmaf(p, vf[i], o[g][i]);
     }
   }
-  // reduce over the KPS key-lanes of the wave (lanes with equal dsl)
 #pragma unroll
   for (int g = 0; g < G; ++g)
 #pragma unroll
@@ -124,37 +144,54 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(AttnDecodeArgs a) {
       for (int i = 0; i < 8; ++i) s_o[wave][g][dsl * 8 + i] = o[g][i];
   }
   __syncthreads();
-  // across the 4 waves, write the partial
+
+  const int nact = (len + CH - 1) / CH;  // chunks that arrive
+  if (nact == 1) {  // single chunk: normalise directly, no hand-off
+    for (int idx = threadIdx.x; idx < G * HD; idx += 256) {
+      const int g = idx / HD, d = idx - g * HD;
+      const float v = s_o[0][g][d] + s_o[1][g][d] + s_o[2][g][d] + s_o[3][g][d];
+      a.out[((size_t)b * a.n_heads + kvh * G + g) * HD + d] = v / s_l[g];
+    }
+    return;
+  }
+  // ---- publish this chunk's partial (write-through), then take a ticket
   for (int idx = threadIdx.x; idx < G * HD; idx += 256) {
     const int g = idx / HD, d = idx - g * HD;
     const float v = s_o[0][g][d] + s_o[1][g][d] + s_o[2][g][d] + s_o[3][g][d];
     const int h = kvh * G + g;
-    a.o_part[(((size_t)b * a.n_heads + h) * a.n_chunks + ch) * HD + d] = v;
+    st_wt(a.o_part + (((size_t)b * a.n_heads + h) * a.n_chunks + ch) * HD + d, v);
     if (d == 0) {
       float* ml = a.ml + (((size_t)b * a.n_heads + h) * a.n_chunks + ch) * 2;
-      ml[0] = s_m[g];
-      ml[1] = s_l[g];
+      st_wt(ml, s_m[g]);
+      st_wt(ml + 1, s_l[g]);
     }
   }
-}
-
-// grid (n_heads, B), block = hd threads
-__global__ void attn_combine_kernel(AttnDecodeArgs a) {
-  const int h = blockIdx.x, b = blockIdx.y, d = threadIdx.x;
-  const int HD = a.head_dim;
-  const int len = a.seq_len[b];
-  const int nch = min(a.n_chunks, (len + ATTN_CHUNK - 1) / ATTN_CHUNK);
-  const float* ml = a.ml + ((size_t)b * a.n_heads + h) * a.n_chunks * 2;
-  float M = -INFINITY;
-  for (int c = 0; c < nch; ++c) M = fmaxf(M, ml[2 * c]);
-  float L = 0.f, acc = 0.f;
-  const float* op = a.o_part + ((size_t)b * a.n_heads + h) * a.n_chunks * HD;
-  for (int c = 0; c < nch; ++c) {
-    const float w = __expf(ml[2 * c] - M);
-    L += w * ml[2 * c + 1];
-    acc += w * op[(size_t)c * HD + d];
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
+  __syncthreads();
+  int* cnt = a.counters + (size_t)b * a.n_kv_heads + kvh;
+  if (threadIdx.x == 0) {
+    const int t = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = (t == nact - 1);
   }
-  a.out[((size_t)b * a.n_heads + h) * HD + d] = nch > 0 ? acc / L : 0.f;
+  __syncthreads();
+  if (!s_last) return;
+  // ---- last arriver: log-sum-exp combine over the nact chunks (sc1 loads of every partial)
+  for (int idx = threadIdx.x; idx < G * HD; idx += 256) {
+    const int g = idx / HD, d = idx - g * HD;
+    const int h = kvh * G + g;
+    const float* ml = a.ml + ((size_t)b * a.n_heads + h) * a.n_chunks * 2;
+    const float* op = a.o_part + ((size_t)b * a.n_heads + h) * a.n_chunks * HD;
+    float M = -INFINITY;
+    for (int c = 0; c < nact; ++c) M = fmaxf(M, ld_wt(ml + 2 * c));
+    float L = 0.f, acc = 0.f;
+    for (int c = 0; c < nact; ++c) {
+      const float w = __expf(ld_wt(ml + 2 * c) - M);
+      L += w * ld_wt(ml + 2 * c + 1);
+      acc += w * ld_wt(op + (size_t)c * HD + d);
+    }
+    a.out[((size_t)b * a.n_heads + h) * HD + d] = acc / L;
+  }
+  if (threadIdx.x == 0) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
 }
 
 template <int HD>
@@ -172,11 +209,12 @@ static void launch_hd(const AttnDecodeArgs& a, int G, hipStream_t st) {
 
 void launch_attn_decode(const AttnDecodeArgs& a, hipStream_t st) {
   if (a.n_heads % a.n_kv_heads) throw std::runtime_error("attn_decode: n_heads % n_kv_heads != 0");
+  if (!a.counters) throw std::runtime_error("attn_decode: counters buffer required");
+  if (a.max_ctx % ATTN_CHUNK) throw std::runtime_error("attn_decode: max_ctx must be a multiple of ATTN_CHUNK");
   const int G = a.n_heads / a.n_kv_heads;
   if (a.head_dim == 128) launch_hd<128>(a, G, st);
   else if (a.head_dim == 64) launch_hd<64>(a, G, st);
   else throw std::runtime_error("attn_decode: head_dim must be 64 or 128");
-  hipLaunchKernelGGL(attn_combine_kernel, dim3(a.n_heads, a.B), dim3(a.head_dim), 0, st, a);
 }
 
 }  // namespace aios

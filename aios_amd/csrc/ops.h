@@ -66,6 +66,7 @@ struct AttnDecodeArgs {
   float* o_part;           // [B][n_heads][n_chunks][hd]
   float* ml;               // [B][n_heads][n_chunks][2]
   float* out;              // [B][n_heads*hd]
+  int* counters;           // [B][n_kv_heads] arrival tickets, zero-initialised, self re-arming
 };
 constexpr int ATTN_CHUNK = 64;
 void launch_attn_decode(const AttnDecodeArgs& a, hipStream_t st);

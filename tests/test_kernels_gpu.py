@@ -171,7 +171,7 @@ def test_gemv_qkv_rope_kv(E, mixed, q8):
 
 
 @pytest.mark.parametrize("hd,H,Hkv", [(64, 8, 1), (128, 32, 8), (64, 32, 4), (128, 40, 8)])
-@pytest.mark.parametrize("lens", [[1], [37, 200], [64, 65, 129, 1]])
+@pytest.mark.parametrize("lens", [[1], [37, 200], [64, 65, 129, 1], [256, 255, 192]])
 def test_attention_decode(E, hd, H, Hkv, lens):
     B = len(lens)
     max_ctx, slots = 256, B + 1
@@ -184,10 +184,14 @@ def test_attention_decode(E, hd, H, Hkv, lens):
     opart = torch.empty(B, H, nch, hd, device="cuda")
     ml = torch.empty(B, H, nch, 2, device="cuda")
     out = torch.empty(B, H * hd, device="cuda")
+    cnt = torch.zeros(B, Hkv, dtype=torch.int32, device="cuda")
     scale = 1 / math.sqrt(hd)
-    E.attn_decode(q.data_ptr(), kc.data_ptr(), vc.data_ptr(), seq.data_ptr(), slot.data_ptr(), B, H, Hkv, hd,
-                  max_ctx, nch, scale, opart.data_ptr(), ml.data_ptr(), out.data_ptr(), stream())
+    for _ in range(2):  # second launch checks the counters re-armed themselves
+        out.zero_()
+        E.attn_decode(q.data_ptr(), kc.data_ptr(), vc.data_ptr(), seq.data_ptr(), slot.data_ptr(), B, H, Hkv, hd,
+                      max_ctx, nch, scale, opart.data_ptr(), ml.data_ptr(), out.data_ptr(), cnt.data_ptr(), stream())
     torch.cuda.synchronize()
+    assert int(cnt.abs().sum()) == 0
     G = H // Hkv
     for b in range(B):
         L, s = lens[b], b + 1
