@@ -48,10 +48,7 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(AttnDecodeArgs a) {
   __shared__ int s_last;
 
   const int ch = blockIdx.x, kvh = blockIdx.y, b = blockIdx.z;
-  const int len = a.seq_len[b];
   const int start = ch * CH;
-  if (start >= len) return;
-  const int n = min(CH, len - start);
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int ksub = lane / LPK, dsl = lane % LPK;
   const int slot = a.slot ? a.slot[b] : b;
@@ -79,6 +76,10 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(AttnDecodeArgs a) {
     const int key = start + wave * KPW + s * KPS + ksub;
     vraw[s] = *(const uint4*)(vc + (size_t)key * HD + dsl * 8);
   }
+  // seq_len is only needed now: its load overlaps the K/V/q loads above
+  const int len = a.seq_len[b];
+  if (start >= len) return;
+  const int n = min(CH, len - start);
 
   // ---- scores
 #pragma unroll

@@ -425,7 +425,8 @@ bool launch_gemv_q8(GemvArgs a, hipStream_t st) {
   constexpr int W0 = QFmt<QT0>::W;
   const int nit = (a.K / W0 + 64 * U - 1) / (64 * U);
   const int npairs = a.N / 2;
-  const bool ksplit = (QT0 == QT1) && nit >= 3 && a.tune_ksplit >= 0;
+  // K-split measured slower than row pairs on MI355X (down-proj 15.6 vs 13.6 us): opt-in only
+  const bool ksplit = (QT0 == QT1) && nit >= 3 && a.tune_ksplit > 0;
   a.kt_max = a.K;
   if (ksplit) {
     static int occ = -1;

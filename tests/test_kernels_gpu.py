@@ -76,7 +76,7 @@ def test_gemv_store(E, t, B, K, mode, N):
 @pytest.mark.parametrize("t", [GGMLType.Q4_K, GGMLType.Q6_K, GGMLType.Q8_0, GGMLType.BF16])
 @pytest.mark.parametrize("B", [1, 2, 4])
 @pytest.mark.parametrize("q8", [0, 1])
-@pytest.mark.parametrize("ksplit", [0, -1])
+@pytest.mark.parametrize("ksplit", [0, 1])
 def test_gemv_long_k(E, t, B, q8, ksplit):
     # K = 14336: fp32 persistent kernel / int8 k-split / int8 row kernels / v1 K-tiles (B = 4, fp32)
     N, K = 200, 14336
