@@ -38,7 +38,7 @@ def target_path() -> Path:
 
 
 def _sources():
-    srcs = sorted((CSRC / "kernels").glob("*.hip")) + [CSRC / "engine.hip", CSRC / "bindings.cpp"]
+    srcs = sorted((CSRC / "kernels").glob("*.hip")) + [CSRC / "engine.hip", CSRC / "grammar.cpp", CSRC / "bindings.cpp"]
     return srcs
 
 

@@ -7,6 +7,7 @@
 #include <cstring>
 
 #include "engine.h"
+#include "grammar.h"
 #include "ops.h"
 
 namespace py = pybind11;
@@ -152,9 +153,26 @@ PYBIND11_MODULE(_engine, m) {
              return py::array_t<float>(out.size(), out.data());
            },
            py::arg("slot"), py::arg("tokens"), py::arg("start_pos") = 0, py::arg("want_logits") = true)
-      .def("decode", &Engine::decode, py::arg("slots"), py::arg("tokens"), py::arg("pos"),
-           py::arg("temperature") = std::vector<float>{}, py::arg("top_k") = std::vector<int>{},
-           py::arg("seed") = 0, py::arg("mask") = std::vector<uint8_t>{}, py::call_guard<py::gil_scoped_release>())
+      .def("decode",
+           [](Engine& e, const std::vector<int>& slots, const std::vector<int>& tokens, const std::vector<int>& pos,
+              const std::vector<float>& temperature, const std::vector<int>& top_k, uint64_t seed, py::bytes mask) {
+             std::string m = mask;  // packed allowed-token bitmask, B rows of ceil(V/8) bytes (or empty)
+             std::vector<uint8_t> mv(m.begin(), m.end());
+             py::gil_scoped_release nogil;
+             return e.decode(slots, tokens, pos, temperature, top_k, seed, mv);
+           },
+           py::arg("slots"), py::arg("tokens"), py::arg("pos"), py::arg("temperature") = std::vector<float>{},
+           py::arg("top_k") = std::vector<int>{}, py::arg("seed") = 0, py::arg("mask") = py::bytes())
+      .def("resample",
+           [](Engine& e, int B, const std::vector<float>& temperature, const std::vector<int>& top_k, uint64_t seed,
+              py::bytes mask) {
+             std::string m = mask;
+             std::vector<uint8_t> mv(m.begin(), m.end());
+             py::gil_scoped_release nogil;
+             return e.resample(B, temperature, top_k, seed, mv);
+           },
+           py::arg("B"), py::arg("temperature") = std::vector<float>{}, py::arg("top_k") = std::vector<int>{},
+           py::arg("seed") = 0, py::arg("mask") = py::bytes())
       .def("last_logits",
            [](Engine& e, int B) {
              std::vector<float> v;
@@ -285,6 +303,36 @@ PYBIND11_MODULE(_engine, m) {
           launch_gemm(a, S(st));
         });
   m.def("gemm_supports", &gemm_supports);
+
+  // ------------------------------------------------------------------ JSON-mode grammar (K10)
+  py::class_<JsonState>(m, "JsonState")
+      .def(py::init<>())
+      .def("copy", [](const JsonState& s) { return JsonState(s); })
+      .def_property_readonly("depth", [](const JsonState& s) { return (int)s.depth; })
+      .def_property_readonly("mode", [](const JsonState& s) { return (int)s.mode; });
+  py::class_<JsonGrammar>(m, "JsonGrammar")
+      .def(py::init([](const std::vector<py::bytes>& toks, int eos, int max_ws, bool require_object) {
+             std::vector<std::string> t;
+             t.reserve(toks.size());
+             for (auto& b : toks) t.push_back(std::string(b));
+             return new JsonGrammar(t, eos, max_ws, require_object);
+           }),
+           py::arg("tokens"), py::arg("eos_id"), py::arg("max_ws") = 20, py::arg("require_object") = true)
+      .def("initial", &JsonGrammar::initial)
+      .def("accept_token", &JsonGrammar::accept_token)
+      .def("accept_bytes", [](const JsonGrammar& g, JsonState& s, py::bytes b) { return g.accept_bytes(s, std::string(b)); })
+      .def("complete", &JsonGrammar::complete)
+      .def("mask",
+           [](JsonGrammar& g, const JsonState& s) {
+             const std::vector<uint8_t>* m;
+             {
+               py::gil_scoped_release nogil;
+               m = &g.mask(s);
+             }
+             return py::bytes((const char*)m->data(), m->size());
+           })
+      .def_property_readonly("vocab_size", &JsonGrammar::vocab_size)
+      .def_property_readonly("cache_size", &JsonGrammar::cache_size);
   m.def("bench_launch_chain", &aios::bench_launch_chain, py::arg("n_kernels"), py::arg("blocks"), py::arg("use_graph"),
         py::arg("reps"), py::call_guard<py::gil_scoped_release>());
 }

@@ -93,6 +93,9 @@ class Engine {
   std::vector<int> decode(const std::vector<int>& slots, const std::vector<int>& tokens, const std::vector<int>& pos,
                           const std::vector<float>& temperature, const std::vector<int>& top_k, uint64_t seed,
                           const std::vector<uint8_t>& mask);
+  // re-sample the last step's logits (no state advance), e.g. with a grammar mask
+  std::vector<int> resample(int B, const std::vector<float>& temperature, const std::vector<int>& top_k, uint64_t seed,
+                            const std::vector<uint8_t>& mask);
   // logits of the last decode (B x V) -- host copy
   std::vector<float> last_logits(int B);
 
@@ -146,6 +149,7 @@ class Engine {
   int *d_tokens_ = nullptr, *d_pos_ = nullptr, *d_seqlen_ = nullptr, *d_slot_ = nullptr, *d_history_ = nullptr;
   int *d_topk_ = nullptr, *d_step_ = nullptr;
   float* d_temp_ = nullptr;
+  uint64_t* d_seed_ = nullptr;
   uint8_t* d_mask_ = nullptr;
   int n_chunks_ = 0;
   int* attn_cnt_ = nullptr;  // [max(prefill_rows, max_batch)][n_kv_heads] combine tickets

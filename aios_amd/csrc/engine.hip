@@ -387,6 +387,7 @@ void Engine::finalize() {
   d_slot_ = ibuf(Bm);
   d_topk_ = ibuf(Bm);
   d_step_ = ibuf(4);
+  d_seed_ = (uint64_t*)ibuf(2);
   d_temp_ = fbuf(Bm);
   HIP_CHECK(hipMemset(d_temp_, 0, Bm * 4));
   d_history_ = ibuf((size_t)Bm * (cfg_.max_ctx + 1));
@@ -557,6 +558,7 @@ void Engine::enqueue_decode_step(int B) {
   s.logits = logits_; s.ldl = V; s.B = B; s.V = V;
   s.temperature = d_temp_; s.top_k = d_topk_;
   s.seed = sample_seed_;
+  s.seed_dev = d_seed_;
   s.tokens = d_tokens_; s.pos = d_pos_; s.seq_len = d_seqlen_;
   s.history = d_history_; s.hist_stride = cfg_.max_ctx + 1;
   s.advance = 1;
@@ -746,18 +748,44 @@ std::vector<int> Engine::decode(const std::vector<int>& slots, const std::vector
     if (mask.size() != mbytes) throw std::runtime_error("decode: mask size mismatch");
     HIP_CHECK(hipMemcpyAsync(d_mask_, mask.data(), mbytes, hipMemcpyHostToDevice, stream_));
   }
-  sample_seed_ = seed;
-  // graphs bake the seed: only graph the greedy/unmasked common case keyed by B
-  const bool graphable = !sample_mask_ && seed == 0;
-  if (graphable) {
-    decode_loop_run(B, 1, true);
-  } else {
-    enqueue_decode_step(B);
-  }
+  // the seed lives in device memory, so one captured graph per (B, masked) serves every request
+  HIP_CHECK(hipMemcpyAsync(d_seed_, &seed, 8, hipMemcpyHostToDevice, stream_));
+  decode_loop_run(B, 1, true);
   std::vector<int> out(B);
   HIP_CHECK(hipMemcpyAsync(out.data(), d_tokens_, B * 4, hipMemcpyDeviceToHost, stream_));
   HIP_CHECK(hipStreamSynchronize(stream_));
   sample_mask_ = false;
+  return out;
+}
+
+std::vector<int> Engine::resample(int B, const std::vector<float>& temperature, const std::vector<int>& top_k,
+                                  uint64_t seed, const std::vector<uint8_t>& mask) {
+  // re-run only the sampler on the logits of the last step (grammar fast path: the unmasked
+  // sample was rejected on the host)
+  HIP_CHECK(hipSetDevice(cfg_.device));
+  std::vector<float> temps(B, 0.f);
+  std::vector<int> tks(B, 0);
+  for (int b = 0; b < B && b < (int)temperature.size(); ++b) temps[b] = temperature[b];
+  for (int b = 0; b < B && b < (int)top_k.size(); ++b) tks[b] = top_k[b];
+  HIP_CHECK(hipMemcpyAsync(d_temp_, temps.data(), B * 4, hipMemcpyHostToDevice, stream_));
+  HIP_CHECK(hipMemcpyAsync(d_topk_, tks.data(), B * 4, hipMemcpyHostToDevice, stream_));
+  HIP_CHECK(hipMemcpyAsync(d_seed_, &seed, 8, hipMemcpyHostToDevice, stream_));
+  const size_t mbytes = (size_t)B * ((cfg_.vocab_size + 7) / 8);
+  if (!mask.empty()) {
+    if (mask.size() != mbytes) throw std::runtime_error("resample: mask size mismatch");
+    HIP_CHECK(hipMemcpyAsync(d_mask_, mask.data(), mbytes, hipMemcpyHostToDevice, stream_));
+  }
+  SampleArgs s;
+  std::memset(&s, 0, sizeof(s));
+  s.logits = logits_; s.ldl = cfg_.vocab_size; s.B = B; s.V = cfg_.vocab_size;
+  s.temperature = d_temp_; s.top_k = d_topk_; s.seed_dev = d_seed_;
+  s.tokens = d_tokens_; s.pos = d_pos_; s.advance = 0;
+  s.mask = mask.empty() ? nullptr : d_mask_;
+  // pos was advanced by the step: RNG key uses pos[b] (a different stream than the first sample)
+  launch_sample(s, stream_);
+  std::vector<int> out(B);
+  HIP_CHECK(hipMemcpyAsync(out.data(), d_tokens_, B * 4, hipMemcpyDeviceToHost, stream_));
+  HIP_CHECK(hipStreamSynchronize(stream_));
   return out;
 }
 
@@ -781,6 +809,8 @@ void Engine::decode_loop_prepare(const std::vector<int>& slots, const std::vecto
   HIP_CHECK(hipMemcpyAsync(d_seqlen_, sl.data(), B * 4, hipMemcpyHostToDevice, stream_));
   HIP_CHECK(hipMemcpyAsync(d_temp_, temps.data(), B * 4, hipMemcpyHostToDevice, stream_));
   HIP_CHECK(hipMemcpyAsync(d_topk_, tks.data(), B * 4, hipMemcpyHostToDevice, stream_));
+  const uint64_t zero = 0;
+  HIP_CHECK(hipMemcpyAsync(d_seed_, &zero, 8, hipMemcpyHostToDevice, stream_));
   HIP_CHECK(hipStreamSynchronize(stream_));
   sample_seed_ = 0;
   sample_mask_ = false;
@@ -792,7 +822,8 @@ void Engine::decode_loop_run(int B, int n_steps, bool use_graph) {
     for (int i = 0; i < n_steps; ++i) enqueue_decode_step(B);
     return;
   }
-  auto it = graphs_.find(B);
+  const int key = B * 2 + (sample_mask_ ? 1 : 0);
+  auto it = graphs_.find(key);
   if (it == graphs_.end()) {
     hipGraph_t g;
     HIP_CHECK(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal));
@@ -806,7 +837,7 @@ void Engine::decode_loop_run(int B, int n_steps, bool use_graph) {
     hipGraphExec_t ge;
     HIP_CHECK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
     HIP_CHECK(hipGraphDestroy(g));
-    it = graphs_.emplace(B, ge).first;
+    it = graphs_.emplace(key, ge).first;
   }
   for (int i = 0; i < n_steps; ++i) HIP_CHECK(hipGraphLaunch(it->second, stream_));
 }

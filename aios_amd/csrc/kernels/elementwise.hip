@@ -219,7 +219,8 @@ __global__ void __launch_bounds__(1024) sample_kernel(SampleArgs a, float top_p_
     for (int i = threadIdx.x; i < a.V; i += blockDim.x) {
       if (mask && !((mask[i >> 3] >> (i & 7)) & 1)) continue;
       if (l[i] < thr) continue;
-      const uint32_t h = mix32(a.seed * 0x9E3779B97F4A7C15ULL + ((uint64_t)step << 40) + ((uint64_t)b << 32) + i);
+      const uint64_t seed = a.seed_dev ? *a.seed_dev : a.seed;
+      const uint32_t h = mix32(seed * 0x9E3779B97F4A7C15ULL + ((uint64_t)step << 40) + ((uint64_t)b << 32) + i);
       const float u = ((h >> 8) + 0.5f) * (1.f / 16777216.f);
       const float gum = -__logf(-__logf(u));
       g = am_better(g, ArgMax{l[i] * it_ + gum, i});

@@ -82,6 +82,7 @@ struct SampleArgs {
   const float* temperature;  // [B] or null (greedy)
   const int* top_k;          // [B] or null
   uint64_t seed;             // RNG key = (seed, row, pos[row])
+  const uint64_t* seed_dev;  // if non-null, the seed is read from device memory (graph-replay safe)
   int* tokens;               // [B] out
   int* pos;                  // [B] in/out (incremented when advance != 0)
   int* seq_len;              // [B] out (pos+1) or null

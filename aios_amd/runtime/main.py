@@ -1,0 +1,86 @@
+"""aios-runtime daemon (`runtime/src/main.rs` equivalent).
+
+* builds the ModelManager on the local MI355X,
+* auto-loads every `*.gguf` in $AIOS_MODEL_DIR (default /var/lib/aios/models/) with the
+  reference's size-based context heuristic, plus `AIOS_SYNTHETIC_MODELS` entries
+  (`name=synthetic:preset[:recipe]`, comma separated),
+* serves aios.runtime.AIRuntime on [::]:50055 (AIOS_RUNTIME_ADDR), with a 10 s health loop
+  that marks models whose engine died as errored.
+"""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import logging
+import os
+import signal
+from pathlib import Path
+
+from ..rpc.server import RpcServer
+from .model_manager import ModelManager
+from .service import AIRuntimeService
+
+log = logging.getLogger("aios.runtime")
+HEALTH_CHECK_INTERVAL = 10.0
+
+
+async def auto_load(svc: AIRuntimeService, model_dir: str):
+    d = Path(model_dir)
+    if d.is_dir():
+        for f in sorted(d.glob("*.gguf")):
+            req_name = f.stem
+            log.info("auto-loading %s", f)
+            m = await svc.mgr.load_model(req_name, str(f))
+            if m.status == "ready" and svc.http:
+                await svc.start_http(m)
+    for spec in filter(None, os.environ.get("AIOS_SYNTHETIC_MODELS", "").split(",")):
+        name, _, path = spec.partition("=")
+        m = await svc.mgr.load_model(name.strip(), path.strip())
+        if m.status == "ready" and svc.http:
+            await svc.start_http(m)
+
+
+async def health_loop(mgr: ModelManager, stop: asyncio.Event):
+    while not stop.is_set():
+        for m in mgr.list_models():
+            if m.status == "ready" and m.scheduler is not None and not m.scheduler.thread.is_alive():
+                m.status, m.error = "error", "scheduler thread died"
+        try:
+            await asyncio.wait_for(stop.wait(), HEALTH_CHECK_INTERVAL)
+        except asyncio.TimeoutError:
+            pass
+
+
+async def amain(args):
+    mgr = ModelManager(device=args.device, max_batch=args.max_batch, max_slots=args.max_slots)
+    svc = AIRuntimeService(mgr, http=not args.no_http)
+    server = RpcServer(args.addr, {"aios.runtime.AIRuntime": svc})
+    await server.start()
+    stop = asyncio.Event()
+    loop = asyncio.get_running_loop()
+    for sig in (signal.SIGINT, signal.SIGTERM):
+        try:
+            loop.add_signal_handler(sig, stop.set)
+        except NotImplementedError:
+            pass
+    asyncio.ensure_future(auto_load(svc, args.model_dir))
+    await health_loop(mgr, stop)
+    await server.stop()
+    await svc.close()
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(description="aiOS MI355X AI runtime")
+    ap.add_argument("--addr", default=os.environ.get("AIOS_RUNTIME_ADDR", "[::]:50055"))
+    ap.add_argument("--model-dir", default=os.environ.get("AIOS_MODEL_DIR", "/var/lib/aios/models/"))
+    ap.add_argument("--device", type=int, default=int(os.environ.get("AIOS_DEVICE", "0")))
+    ap.add_argument("--max-batch", type=int, default=8)
+    ap.add_argument("--max-slots", type=int, default=16)
+    ap.add_argument("--no-http", action="store_true")
+    args = ap.parse_args(argv)
+    logging.basicConfig(level=os.environ.get("AIOS_LOG", "INFO"), format="%(asctime)s %(levelname)s %(name)s %(message)s")
+    asyncio.run(amain(args))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,263 @@
+"""Continuous-batching generation scheduler for one model.
+
+Replaces the per-request HTTP round trip to llama-server (`runtime/src/inference.rs:94-186`)
+with an in-process worker per model that owns the native Engine:
+
+* admission: a waiting request takes a free KV slot; the slot whose cached tokens share the
+  longest prefix with the prompt is preferred and only the remainder is prefilled (prefix KV
+  reuse -- the autonomy loop's tool catalogue and format rules repeat on every round, §6.1);
+* each iteration runs ONE batched decode step (hipGraph replay) for every active sequence, so
+  concurrent agents/reasoning loops share each weight pass;
+* JSON mode (the reference's `response_format: json_object`) builds the allowed-token mask per
+  row with the native JsonGrammar and the device sampler applies it; generation stops as soon as
+  the top-level object is complete;
+* true token streaming: every step pushes text deltas to the request's callback (the reference
+  buffered the whole SSE body, App. A #2).
+
+The worker is a thread: engine calls release the GIL, asyncio callers get results through
+thread-safe callbacks.
+"""
+from __future__ import annotations
+
+import collections
+import dataclasses
+import logging
+import threading
+import time
+from typing import Callable, Deque, Dict, List, Optional
+
+import numpy as np
+
+from . import sampler as host_sampler
+
+log = logging.getLogger("aios.runtime.scheduler")
+
+
+@dataclasses.dataclass
+class GenRequest:
+    prompt_ids: List[int]
+    max_tokens: int = 512
+    temperature: float = 0.0
+    top_k: int = 40
+    top_p: float = 0.95
+    json_mode: bool = False
+    seed: int = 0
+    stop_ids: Optional[List[int]] = None
+    on_delta: Optional[Callable[[str], None]] = None
+    on_done: Optional[Callable[["GenResult"], None]] = None
+    deadline: float = 0.0             # absolute time.time(); 0 = none
+    cancelled: bool = False
+    submitted_at: float = dataclasses.field(default_factory=time.time)
+
+
+@dataclasses.dataclass
+class GenResult:
+    text: str
+    token_ids: List[int]
+    prompt_tokens: int
+    completion_tokens: int
+    finish_reason: str                # stop | length | grammar | cancelled | error | deadline
+    ttft_ms: float = 0.0
+    latency_ms: float = 0.0
+    cached_prompt_tokens: int = 0
+    error: str = ""
+
+
+class _Seq:
+    __slots__ = ("req", "slot", "pos", "last", "out", "grammar_state", "emitted", "t_first", "cached")
+
+    def __init__(self, req, slot):
+        self.req, self.slot = req, slot
+        self.pos = 0
+        self.last = 0
+        self.out: List[int] = []
+        self.grammar_state = None
+        self.emitted = ""
+        self.t_first = 0.0
+        self.cached = 0
+
+
+class Scheduler:
+    def __init__(self, engine, tokenizer, max_batch: int, max_slots: int, max_ctx: int, grammar=None,
+                 name: str = "model"):
+        self.engine = engine
+        self.tok = tokenizer
+        self.max_batch = max_batch
+        self.max_ctx = max_ctx
+        self.grammar = grammar
+        self.name = name
+        self.vocab = tokenizer.vocab_size
+        self.eos = {tokenizer.eos_id}
+        for extra in ("<|eot_id|>", "<|im_end|>", "<|end|>"):
+            if extra in tokenizer.vocab:
+                self.eos.add(tokenizer.vocab[extra])
+        self.slot_cache: Dict[int, List[int]] = {s: [] for s in range(max_slots)}
+        self.free_slots = list(range(max_slots))
+        self.queue: Deque[GenRequest] = collections.deque()
+        self.active: List[_Seq] = []
+        self.cv = threading.Condition()
+        self.stop_flag = False
+        self.stats = dict(requests=0, tokens=0, prefill_tokens=0, cached_tokens=0, steps=0, batch_sum=0)
+        self.thread = threading.Thread(target=self._run, name=f"sched-{name}", daemon=True)
+        self.thread.start()
+
+    # ------------------------------------------------------------------ public
+    def submit(self, req: GenRequest):
+        with self.cv:
+            self.queue.append(req)
+            self.stats["requests"] += 1
+            self.cv.notify()
+
+    def close(self):
+        with self.cv:
+            self.stop_flag = True
+            self.cv.notify()
+        self.thread.join(timeout=10)
+
+    @property
+    def load(self) -> int:
+        return len(self.queue) + len(self.active)
+
+    # ------------------------------------------------------------------ worker
+    def _run(self):
+        while True:
+            with self.cv:
+                while not self.stop_flag and not self.queue and not self.active:
+                    self.cv.wait(timeout=1.0)
+                if self.stop_flag:
+                    for s in self.active:
+                        self._finish(s, "cancelled")
+                    while self.queue:
+                        r = self.queue.popleft()
+                        self._done(r, GenResult("", [], len(r.prompt_ids), 0, "cancelled"))
+                    return
+                admit = []
+                while self.queue and self.free_slots and len(self.active) + len(admit) < self.max_batch:
+                    admit.append(self.queue.popleft())
+            for r in admit:
+                try:
+                    self._admit(r)
+                except Exception as e:  # noqa: BLE001 - reported to the caller
+                    log.exception("admission failed")
+                    self._done(r, GenResult("", [], len(r.prompt_ids), 0, "error", error=str(e)))
+            if self.active:
+                try:
+                    self._step()
+                except Exception as e:  # noqa: BLE001
+                    log.exception("decode step failed")
+                    for s in list(self.active):
+                        self._finish(s, "error", str(e))
+
+    def _pick_slot(self, ids: List[int]):
+        best, best_len = None, -1
+        for s in self.free_slots:
+            c = self.slot_cache[s]
+            n = 0
+            lim = min(len(c), len(ids) - 1)
+            while n < lim and c[n] == ids[n]:
+                n += 1
+            if n > best_len:
+                best, best_len = s, n
+        return best, max(best_len, 0)
+
+    def _admit(self, r: GenRequest):
+        ids = r.prompt_ids
+        if len(ids) >= self.max_ctx:
+            raise ValueError(f"prompt of {len(ids)} tokens exceeds the context window ({self.max_ctx})")
+        r.max_tokens = max(1, min(r.max_tokens, self.max_ctx - len(ids)))
+        slot, common = self._pick_slot(ids)
+        self.free_slots.remove(slot)
+        seq = _Seq(r, slot)
+        seq.cached = common
+        self.slot_cache[slot] = list(ids[:common])
+        logits = self.engine.prefill(slot, ids[common:], common, True)
+        self.stats["prefill_tokens"] += len(ids) - common
+        self.stats["cached_tokens"] += common
+        self.slot_cache[slot] = list(ids)
+        seq.pos = len(ids)
+        mask = None
+        if r.json_mode and self.grammar is not None:
+            seq.grammar_state = self.grammar.initial()
+            mask = self.grammar.mask(seq.grammar_state)
+        rng = np.random.default_rng(r.seed or None)
+        tok = host_sampler.sample(logits, r.temperature, r.top_k, r.top_p, mask, rng)
+        seq.t_first = time.time()
+        self.active.append(seq)
+        self._accept(seq, tok)
+
+    def _accept(self, seq: _Seq, tok: int) -> bool:
+        """Record a sampled token; returns False when the sequence finished."""
+        r = seq.req
+        if r.cancelled:
+            self._finish(seq, "cancelled")
+            return False
+        if tok in self.eos or (r.stop_ids and tok in r.stop_ids):
+            self._finish(seq, "stop")
+            return False
+        if seq.grammar_state is not None:
+            if not self.grammar.accept_token(seq.grammar_state, tok):
+                self._finish(seq, "stop")
+                return False
+        seq.out.append(tok)
+        seq.last = tok
+        self.stats["tokens"] += 1
+        if r.on_delta is not None:
+            text = self.tok.decode(seq.out)
+            if not text.endswith("�"):
+                delta = text[len(seq.emitted):]
+                if delta:
+                    seq.emitted = text
+                    r.on_delta(delta)
+        if seq.grammar_state is not None and self.grammar.complete(seq.grammar_state):
+            self._finish(seq, "grammar")
+            return False
+        if len(seq.out) >= r.max_tokens or seq.pos + 1 >= self.max_ctx:
+            self._finish(seq, "length")
+            return False
+        if r.deadline and time.time() > r.deadline:
+            self._finish(seq, "deadline")
+            return False
+        return True
+
+    def _step(self):
+        B = len(self.active)
+        slots = [s.slot for s in self.active]
+        toks = [s.last for s in self.active]
+        pos = [s.pos for s in self.active]
+        temps = [float(s.req.temperature) for s in self.active]
+        topk = [int(s.req.top_k) if s.req.temperature > 0 else 0 for s in self.active]
+        seed = int(self.active[0].req.seed) & 0xFFFFFFFF
+        mask = b""
+        if any(s.grammar_state is not None for s in self.active):
+            full = host_sampler.all_allowed(self.vocab)
+            mask = b"".join(self.grammar.mask(s.grammar_state) if s.grammar_state is not None else full
+                            for s in self.active)
+        out = self.engine.decode(slots, toks, pos, temps, topk, seed, mask)
+        self.stats["steps"] += 1
+        self.stats["batch_sum"] += B
+        for s, t in zip(list(self.active), out):
+            s.pos += 1
+            self.slot_cache[s.slot].append(s.last)
+            self._accept(s, int(t))
+
+    def _finish(self, seq: _Seq, reason: str, error: str = ""):
+        if seq in self.active:
+            self.active.remove(seq)
+        self.free_slots.append(seq.slot)
+        r = seq.req
+        text = self.tok.decode(seq.out)
+        if r.on_delta is not None and len(text) > len(seq.emitted):
+            r.on_delta(text[len(seq.emitted):])
+        now = time.time()
+        self._done(r, GenResult(
+            text=text, token_ids=list(seq.out), prompt_tokens=len(r.prompt_ids), completion_tokens=len(seq.out),
+            finish_reason=reason, ttft_ms=(seq.t_first - r.submitted_at) * 1e3 if seq.t_first else 0.0,
+            latency_ms=(now - r.submitted_at) * 1e3, cached_prompt_tokens=seq.cached, error=error))
+
+    @staticmethod
+    def _done(r: GenRequest, res: GenResult):
+        if r.on_done is not None:
+            try:
+                r.on_done(res)
+            except Exception:  # noqa: BLE001
+                log.exception("on_done callback failed")

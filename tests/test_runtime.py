@@ -1,0 +1,299 @@
+"""CPU tests of the AI runtime: tokenizer, chat templates, JSON grammar, scheduler, gRPC + HTTP.
+
+The scheduler and services run against `FakeEngine` (same Python surface as the native Engine:
+prefill/decode with per-row masks) so the control flow -- batching, prefix-KV reuse, JSON mode,
+streaming, routing errors -- is pinned without a GPU.  GPU end-to-end runs of the same paths on
+the native engine live in test_runtime_gpu.py.
+"""
+import asyncio
+import json
+
+import grpc
+import numpy as np
+import pytest
+
+from aios_amd.models.config import get_preset
+from aios_amd.models.synthetic import synthetic_vocab
+from aios_amd.runtime import chat_template, native
+from aios_amd.runtime.sampler import all_allowed, mask_to_bool, sample
+from aios_amd.runtime.tokenizer import SpmTokenizer
+
+E = native.load()
+needs_native = pytest.mark.skipif(E is None, reason="native extension not built")
+
+
+@pytest.fixture(scope="module")
+def tok():
+    t, s, ty = synthetic_vocab(1024)
+    return SpmTokenizer(t, s, ty, 1, 2)
+
+
+# ---------------------------------------------------------------------------- tokenizer / template
+def test_tokenizer_roundtrip(tok):
+    for text in ["hello world", '{"goal": "list files", "n": 3}', "tab\tand\nnewline", "ünïcødé ✓ 日本"]:
+        ids = tok.encode(text, add_bos=False)
+        assert tok.decode(ids) == text
+    ids = tok.encode("hi", add_bos=True)
+    assert ids[0] == tok.bos_id
+
+
+def test_chat_templates_render(tok):
+    msgs = chat_template.build_messages("do X", "you are aiOS")
+    assert msgs[0]["role"] == "system" and msgs[1]["content"] == "do X"
+    z = chat_template.for_model("zephyr", tok).render(msgs)
+    assert "<|system|>" in z and z.rstrip().endswith("<|assistant|>")
+    m = chat_template.for_model("mistral", tok).render(msgs)
+    assert "[INST]" in m and "you are aiOS" in m
+    l3 = chat_template.for_model("llama3", tok).render(msgs)
+    assert "<|start_header_id|>assistant<|end_header_id|>" in l3
+    c = chat_template.for_model("chatml", tok).render(msgs)
+    assert c.endswith("<|im_start|>assistant\n")
+
+
+# ---------------------------------------------------------------------------- sampler
+def test_host_sampler():
+    logits = np.array([0.0, 5.0, 1.0, 4.0], np.float32)
+    assert sample(logits) == 1
+    mask = bytes([0b1101])  # tokens 0,2,3 allowed
+    assert sample(logits, mask=mask) == 3
+    assert list(mask_to_bool(all_allowed(4), 4)) == [True] * 4
+    rng = np.random.default_rng(0)
+    draws = [sample(logits, 1.0, top_k=2, rng=rng) for _ in range(400)]
+    assert set(draws) <= {1, 3}
+    frac = draws.count(1) / len(draws)
+    assert abs(frac - 1 / (1 + np.exp(-1))) < 0.08
+
+
+# ---------------------------------------------------------------------------- grammar
+@needs_native
+def test_json_grammar_accepts_and_masks(tok):
+    g = E.JsonGrammar(tok.all_token_bytes(), tok.eos_id)
+    st = g.initial()
+    for t in tok.encode('{"a": [1, 2.5e3, "x\\n", true, null], "b": {}}', add_bos=False):
+        assert g.accept_token(st, t)
+    assert g.complete(st)
+    # the object is closed: nothing but eos may follow
+    allowed = np.flatnonzero(mask_to_bool(g.mask(st), tok.vocab_size))
+    assert list(allowed) == [tok.eos_id]
+    # the first token of a JSON-mode reply must open an object (require_object)
+    st0 = g.initial()
+    allowed0 = mask_to_bool(g.mask(st0), tok.vocab_size)
+    for t in np.flatnonzero(allowed0):
+        assert tok.token_bytes(int(t)).lstrip(b" \t\n\r")[:1] in (b"{", b"")
+    bad = g.initial()
+    assert not g.accept_bytes(bad, b'{"a" 1}')
+
+
+@needs_native
+def test_json_grammar_rejects_structural_errors(tok):
+    g = E.JsonGrammar(tok.all_token_bytes(), tok.eos_id)
+    for s in [b'{"a":}', b'{"a":1,}', b'{a:1}', b'{"a":[1,]}', b'{"a":01}', b'[]']:
+        assert not g.accept_bytes(g.initial(), s), s
+    for s in [b'{}', b'{"k": -0.5E-2}', b'{"u": "\\u00e9"}', b'{"n": [[], {}, [1]]}']:
+        st = g.initial()
+        assert g.accept_bytes(st, s) and g.complete(st), s
+
+
+# ---------------------------------------------------------------------------- fake engine
+class FakeEngine:
+    """Deterministic stand-in for the native Engine: the next token is a function of the last one,
+    or the next byte-compatible token of a scripted JSON answer when a mask is in force."""
+
+    def __init__(self, tokenizer, script='{"ok": true}'):
+        self.tok = tokenizer
+        self.V = tokenizer.vocab_size
+        self.script = tokenizer.encode(script, add_bos=False)
+        self.prefills = []
+        self.batches = []
+        self.progress = {}
+        self.weight_bytes = 1 << 20
+        self.kv_bytes = 1 << 20
+
+    def _logits(self, last):
+        l = np.zeros(self.V, np.float32)
+        l[(last * 7 + 3) % self.V] = 10.0
+        l[self.tok.eos_id] = -10.0
+        return l
+
+    def prefill(self, slot, ids, start, want_logits=True):
+        self.prefills.append((slot, len(ids), start))
+        self.progress[slot] = 1
+        l = self._logits(ids[-1] if ids else 0)
+        l[self.script[0]] = 5.0   # wins only when a grammar mask removes the free-running token
+        return l
+
+    def decode(self, slots, toks, pos, temps, topk, seed, mask):
+        self.batches.append(len(slots))
+        out = []
+        row = (self.V + 7) // 8
+        for b, (slot, t) in enumerate(zip(slots, toks)):
+            if mask:
+                allowed = mask_to_bool(mask[b * row:(b + 1) * row], self.V)
+                k = self.progress.get(slot, 0)
+                nxt = self.script[k] if k < len(self.script) else self.tok.eos_id
+                self.progress[slot] = k + 1
+                out.append(nxt if allowed[nxt] else int(np.flatnonzero(allowed)[0]))
+            else:
+                out.append(int(np.argmax(self._logits(t))))
+        return out
+
+
+@needs_native
+def test_scheduler_batches_streams_and_reuses_prefix(tok):
+    from aios_amd.runtime.scheduler import GenRequest, Scheduler
+
+    eng = FakeEngine(tok)
+    g = E.JsonGrammar(tok.all_token_bytes(), tok.eos_id)
+    sched = Scheduler(eng, tok, max_batch=4, max_slots=4, max_ctx=256, grammar=g)
+    try:
+        import threading
+
+        done = {}
+        evs = [threading.Event() for _ in range(4)]
+        deltas = {i: [] for i in range(4)}
+        prompt = tok.encode("shared system prompt with tool catalogue " * 3)
+
+        def mk(i, json_mode=False, max_tokens=6):
+            def on_done(r):
+                done[i] = r
+                evs[i].set()
+            return GenRequest(prompt_ids=prompt + [100 + i], max_tokens=max_tokens, json_mode=json_mode,
+                              on_delta=deltas[i].append, on_done=on_done)
+
+        for i in range(3):
+            sched.submit(mk(i))
+        for e in evs[:3]:
+            assert e.wait(10)
+        for i in range(3):
+            r = done[i]
+            assert r.completion_tokens == 6 and r.finish_reason == "length"
+            assert "".join(deltas[i]) == r.text
+        assert max(eng.batches) >= 2            # continuous batching shared decode steps
+        # a 4th request sharing the prompt prefix reuses a finished slot's KV
+        sched.submit(mk(3, json_mode=True, max_tokens=64))
+        assert evs[3].wait(10)
+        r = done[3]
+        assert r.cached_prompt_tokens == len(prompt)
+        assert eng.prefills[-1][2] == len(prompt) and eng.prefills[-1][1] == 1
+        assert r.finish_reason == "grammar"
+        assert json.loads(r.text) == {"ok": True}
+    finally:
+        sched.close()
+
+
+# ---------------------------------------------------------------------------- services
+def _fake_manager(tok):
+    from aios_amd.runtime import model_manager as mm
+    from aios_amd.runtime.scheduler import Scheduler
+
+    class Mgr(mm.ModelManager):
+        def _load_blocking(self, m, context_length):
+            if "missing" in m.path:
+                raise FileNotFoundError(m.path)
+            m.engine = FakeEngine(tok)
+            m.tokenizer = tok
+            m.template = chat_template.for_model("zephyr", tok)
+            m.grammar = E.JsonGrammar(tok.all_token_bytes(), tok.eos_id)
+            m.context_length = context_length or 512
+            m.scheduler = Scheduler(m.engine, tok, self.max_batch, self.max_slots, m.context_length, m.grammar, m.name)
+
+    return Mgr(base_port=18080)
+
+
+@needs_native
+def test_runtime_grpc_service_end_to_end(tok):
+    from aios_amd.rpc.client import Stub, channel
+    from aios_amd.rpc.schema import pb
+    from aios_amd.rpc.server import RpcServer
+    from aios_amd.runtime.service import AIRuntimeService
+
+    async def run():
+        svc = AIRuntimeService(_fake_manager(tok), http=False)
+        srv = RpcServer("127.0.0.1:0", {"aios.runtime.AIRuntime": svc})
+        await srv.start()
+        ch = channel(f"127.0.0.1:{srv.port}", fresh=True)
+        stub = Stub(ch, "aios.runtime.AIRuntime")
+        try:
+            # no model loaded -> UNAVAILABLE (grpc_service.rs)
+            with pytest.raises(grpc.aio.AioRpcError) as ei:
+                await stub.Infer(pb.runtime.InferRequest(prompt="x"))
+            assert ei.value.code() == grpc.StatusCode.UNAVAILABLE
+            st = await stub.LoadModel(pb.runtime.LoadModelRequest(model_name="tinyllama-1.1b", model_path="fake.gguf"))
+            assert st.status == "ready" and st.port == 18080
+            bad = await stub.LoadModel(pb.runtime.LoadModelRequest(model_name="x", model_path="missing.gguf"))
+            assert bad.status.startswith("error:")
+            lst = await stub.ListModels(pb.common.Empty())
+            assert {m.model_name for m in lst.models} == {"tinyllama-1.1b", "x"}
+            r = await stub.Infer(pb.runtime.InferRequest(prompt="plan", intelligence_level="operational", max_tokens=0))
+            assert json.loads(r.text) == {"ok": True}          # Infer always runs JSON mode
+            assert r.model_used == "tinyllama-1.1b" and r.tokens_used > 0
+            with pytest.raises(grpc.aio.AioRpcError) as ei:
+                await stub.Infer(pb.runtime.InferRequest(prompt="x", intelligence_level="reactive"))
+            assert ei.value.code() == grpc.StatusCode.INVALID_ARGUMENT
+            with pytest.raises(grpc.aio.AioRpcError) as ei:
+                await stub.Infer(pb.runtime.InferRequest(prompt="x", intelligence_level="strategic"))
+            assert ei.value.code() == grpc.StatusCode.FAILED_PRECONDITION
+            chunks = [c async for c in stub.StreamInfer(pb.runtime.InferRequest(prompt="s", max_tokens=5,
+                                                                                 temperature=-1))]
+            assert chunks[-1].done and len(chunks) >= 3
+            assert all(not c.done for c in chunks[:-1])
+            h = await stub.HealthCheck(pb.common.Empty())
+            assert h.healthy and "model:tinyllama-1.1b" in h.details
+            u = await stub.UnloadModel(pb.runtime.UnloadModelRequest(model_name="tinyllama-1.1b"))
+            assert u.success
+        finally:
+            await ch.close()
+            await srv.stop()
+            await svc.close()
+
+    asyncio.run(run())
+
+
+@needs_native
+def test_openai_http_endpoint(tok):
+    import aiohttp
+
+    from aios_amd.runtime.service import AIRuntimeService
+
+    async def run():
+        mgr = _fake_manager(tok)
+        svc = AIRuntimeService(mgr, http=True)
+        m = await mgr.load_model("tiny", "fake.gguf", port=18931)
+        await svc.start_http(m)
+        try:
+            async with aiohttp.ClientSession() as s:
+                async with s.get("http://127.0.0.1:18931/health") as r:
+                    assert (await r.json())["status"] == "ok"
+                body = {"messages": [{"role": "user", "content": "hi"}], "max_tokens": 64,
+                        "response_format": {"type": "json_object"}}
+                async with s.post("http://127.0.0.1:18931/v1/chat/completions", json=body) as r:
+                    js = await r.json()
+                assert json.loads(js["choices"][0]["message"]["content"]) == {"ok": True}
+                assert js["usage"]["completion_tokens"] > 0
+                body = {"messages": [{"role": "user", "content": "hi"}], "max_tokens": 4, "stream": True}
+                async with s.post("http://127.0.0.1:18931/v1/chat/completions", json=body) as r:
+                    raw = (await r.read()).decode()
+                events = [l[6:] for l in raw.split("\n") if l.startswith("data: ")]
+                assert events[-1] == "[DONE]"
+                text = "".join(json.loads(e)["choices"][0]["delta"].get("content", "") for e in events[:-1])
+                assert len(text) > 0
+        finally:
+            await svc.close()
+
+    asyncio.run(run())
+
+
+def test_level_routing_table():
+    from aios_amd.runtime.model_manager import LEVEL_CANDIDATES, ManagedModel, ModelManager, RoutingError
+
+    mgr = ModelManager()
+    mgr.models["mistral-7b-instruct"] = ManagedModel("mistral-7b-instruct", "p", status="ready", port=8080)
+    mgr.models["tinyllama-1.1b-chat"] = ManagedModel("tinyllama-1.1b-chat", "p", status="ready", port=8081)
+    assert mgr.resolve("", "operational").name == "tinyllama-1.1b-chat"
+    assert mgr.resolve("", "tactical").name == "mistral-7b-instruct"
+    assert mgr.resolve("", "strategic").name == "mistral-7b-instruct"   # mistral is a strategic fallback
+    with pytest.raises(RoutingError):
+        mgr.resolve("", "reactive")
+    assert mgr.resolve("tinyllama-1.1b-chat", "").request_count >= 1
+    assert LEVEL_CANDIDATES["strategic"][0] == "llama3-70b"
+    assert mgr.allocate_port() == 8082
