@@ -216,7 +216,7 @@ PYBIND11_MODULE(_engine, m) {
 
   m.def("gemv",
         [](std::vector<PyQMatrix*> segs, int B, uintptr_t x, int ldx, uintptr_t norm_w, float eps, uintptr_t y,
-           int ldy, int epi, uintptr_t st, int force_v1, int act_q8, int tune_grid, int tune_u, int tune_ksplit) {
+           int ldy, int epi, uintptr_t st, int force_v1, int act_q8, int tune_grid, int tune_u, int tune_ksplit, int tune_dbg) {
           GemvArgs a;
           std::memset(&a, 0, sizeof(a));
           a.nseg = (int)segs.size();
@@ -225,12 +225,12 @@ PYBIND11_MODULE(_engine, m) {
           a.N = r; a.K = segs[0]->w.cols; a.B = B;
           a.x = (const float*)x; a.ldx = ldx; a.norm_w = (const float*)norm_w; a.eps = eps;
           a.y = (float*)y; a.ldy = ldy; a.epi = epi; a.force_v1 = force_v1; a.act_q8 = act_q8;
-          a.tune_grid = tune_grid; a.tune_u = tune_u; a.tune_ksplit = tune_ksplit;
+          a.tune_grid = tune_grid; a.tune_u = tune_u; a.tune_ksplit = tune_ksplit; a.tune_dbg = tune_dbg;
           launch_gemv(a, S(st));
         },
         py::arg("segs"), py::arg("B"), py::arg("x"), py::arg("ldx"), py::arg("norm_w"), py::arg("eps"), py::arg("y"),
         py::arg("ldy"), py::arg("epi"), py::arg("stream"), py::arg("force_v1") = 0, py::arg("act_q8") = 0,
-        py::arg("tune_grid") = 0, py::arg("tune_u") = 0, py::arg("tune_ksplit") = 0);
+        py::arg("tune_grid") = 0, py::arg("tune_u") = 0, py::arg("tune_ksplit") = 0, py::arg("tune_dbg") = 0);
   m.def("gemv_qkv",
         [](std::vector<PyQMatrix*> segs, int B, uintptr_t x, int ldx, uintptr_t norm_w, float eps, uintptr_t q_out,
            uintptr_t bias, int head_dim, int n_heads, int n_kv_heads, int max_ctx, int rope_neox, float rope_base,

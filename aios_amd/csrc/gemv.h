@@ -26,6 +26,7 @@ struct GemvArgs {
   int tune_grid;                // blocks per CU override for the persistent kernels (0 = auto)
   int tune_u;                   // chunks per lane per work item override (0 = auto; 1, 2, 4)
   int tune_ksplit;              // -1 disables the K-split decomposition (testing / tuning)
+  int tune_dbg;                 // microbenchmarks only: bit0 skip x staging, bit1 skip dot compute
   const float* x;               // [B][ldx] fp32 input (residual stream if norm_w != null)
   int ldx;
   const float* norm_w;          // RMSNorm weight [K] or null

@@ -57,18 +57,19 @@ __device__ __forceinline__ void dequant16(const QWeight& w, int row, int k0, uin
         for (int e = 0; e < 4; ++e) v[4 * j + e] = ds * (float)((qq >> (8 * e)) & 0xff) - dm;
       }
     } break;
-    case QT_Q6_K: {
-      const int nb = w.cols >> 8, b = k0 >> 8, kk = k0 & 255, n = kk >> 7, r = kk & 127, q4 = r >> 5, l0 = r & 31;
+    case QT_Q6_K: {  // Q4_K-order repack (qweight.h)
+      const int nb = w.cols >> 8, b = k0 >> 8, kk = k0 & 255, g = kk >> 6, hi = (kk >> 5) & 1, i0 = kk & 31;
       const size_t blk = (size_t)row * nb + b;
-      const uint4 ql = *(const uint4*)(w.p0 + blk * 128 + 64 * n + ((q4 & 1) ? 32 : 0) + l0);
-      const uint4 qh = *(const uint4*)(w.p1 + blk * 64 + 32 * n + l0);
-      const int8_t s = *(const int8_t*)(w.p2 + blk * 16 + 8 * n + l0 / 16 + 2 * q4);
+      const int l = 2 * g + (i0 >> 4);
+      const uint4 q = *(const uint4*)(w.p0 + blk * 128 + 32 * g + i0);
+      const uint32_t hv = *(const uint32_t*)(w.p1 + blk * 64 + l * 8 + 4 * hi);
+      const int8_t s = *(const int8_t*)(w.p2 + blk * 16 + (kk >> 4));
       const float d = __half2float(__ushort_as_half(*(const uint16_t*)(w.p3 + blk * 2))) * (float)s;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const uint32_t wv = u4_word(ql, j), hv = u4_word(qh, j);
-        const uint32_t nib = (q4 >> 1) ? ((wv >> 4) & 0x0f0f0f0fu) : (wv & 0x0f0f0f0fu);
-        const uint32_t qq = nib | (((hv >> (2 * q4)) & 0x03030303u) << 4);
+        const uint32_t wv = u4_word(q, j);
+        const uint32_t nib = hi ? ((wv >> 4) & 0x0f0f0f0fu) : (wv & 0x0f0f0f0fu);
+        const uint32_t qq = nib | (((hv >> (2 * j)) & 0x03030303u) << 4);
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[4 * j + e] = d * (float)((int)((qq >> (8 * e)) & 0xff) - 32);
       }

@@ -390,8 +390,9 @@ __global__ void __launch_bounds__(GP_THREADS) gemv_persistent(GemvArgs a) {
   // LDS: [red 64][x layout 0: B*K][sums 0: B*K/16][x layout 1][sums 1]
   float* xl0 = smem + 64;
   float* xs0 = xl0 + B * K;
-  float* xl1 = MIXED ? xs0 + B * K / 16 : xl0;
-  float* xs1 = MIXED ? xl1 + B * K : xs0;
+  constexpr bool SEP = !same_xlayout<QT0, QT1>;
+  float* xl1 = SEP ? xs0 + B * K / 16 : xl0;
+  float* xs1 = SEP ? xl1 + B * K : xs0;
 
   auto info = [&](int p, int& lrow, bool& t1, const QWeight*& w) {
     const int row = 2 * p;
@@ -432,7 +433,7 @@ __global__ void __launch_bounds__(GP_THREADS) gemv_persistent(GemvArgs a) {
     }
   }
   stage_x_tile<QT0>(a.x, a.ldx, a.B, 0, K, inv_rms, a.norm_w, xl0, xs0);
-  if (MIXED) stage_x_tile<QT1>(a.x, a.ldx, a.B, 0, K, inv_rms, a.norm_w, xl1, xs1);
+  if constexpr (SEP) stage_x_tile<QT1>(a.x, a.ldx, a.B, 0, K, inv_rms, a.norm_w, xl1, xs1);
   __syncthreads();
 
   float acc[GEMV_ROWS][B];
@@ -493,9 +494,9 @@ inline int device_cu_count() {
 // returns false when the shape does not fit the persistent kernel's LDS budget
 template <int QT0, int QT1, int B, int U>
 bool launch_gemv_persistent(GemvArgs a, hipStream_t st) {
-  constexpr bool MIXED = QT0 != QT1;
+  constexpr bool SEP = !same_xlayout<QT0, QT1>;
   const size_t xfl = (size_t)B * a.K + (size_t)B * a.K / 16;
-  const size_t lds = (64 + xfl * (MIXED ? 2 : 1) + 4) * sizeof(float);
+  const size_t lds = (64 + xfl * (SEP ? 2 : 1) + 4) * sizeof(float);
   if (lds > 96 * 1024) return false;
   static int occ = -1;  // resident workgroups per CU for this instantiation (VGPR + LDS limited)
   if (occ < 0) {
@@ -540,15 +541,10 @@ void launch_gemv_pair(const GemvArgs& a, hipStream_t st) {
   constexpr bool Q8OK = QT0 != QT_F16 && QT0 != QT_BF16;
   if constexpr (Q8OK) {
     if (!a.force_v1 && a.act_q8) {
-      if (a.B == 1) {
-        const int u = a.tune_u ? a.tune_u : 2;
-        if (u == 1 && launch_gemv_q8<QT0, QT1, 1, 1>(a, st)) return;
-        if (u == 4 && launch_gemv_q8<QT0, QT1, 1, 4>(a, st)) return;
-        if (u == 2 && launch_gemv_q8<QT0, QT1, 1, 2>(a, st)) return;
-      }
-      if (a.B == 2 && launch_gemv_q8<QT0, QT1, 2, 2>(a, st)) return;
-      if (a.B > 2 && a.B <= 4 && launch_gemv_q8<QT0, QT1, 4, 2>(a, st)) return;
-      if (a.B > 4 && launch_gemv_q8<QT0, QT1, 8, 1>(a, st)) return;
+      if (a.B == 1 && launch_gemv_q8<QT0, QT1, 1>(a, st)) return;
+      if (a.B == 2 && launch_gemv_q8<QT0, QT1, 2>(a, st)) return;
+      if (a.B > 2 && a.B <= 4 && launch_gemv_q8<QT0, QT1, 4>(a, st)) return;
+      if (a.B > 4 && launch_gemv_q8<QT0, QT1, 8>(a, st)) return;
     }
   }
   if (!a.force_v1) {

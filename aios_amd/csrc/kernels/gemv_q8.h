@@ -2,21 +2,20 @@
 //
 // The llama.cpp "q8_1 x" trick, done per workgroup in LDS: x is quantised to int8 per 32-element
 // block (dx = amax/127) while it is staged, and every 16-B weight chunk is multiplied with
-// v_dot4_i32_i8 (4 MACs per VALU op) directly on the 4-/5-/6-bit codes -- ~5x fewer VALU ops per
-// weight than the fp32 path and 4x fewer LDS bytes.  Per 16-run r of a chunk:
+// v_dot4_i32_i8 (4 MACs per VALU op) directly on the 4-/5-/6-bit codes.  Per 16-run r of a chunk:
 //     contrib = sc_r * dx_r * isum_r - of_r * sx_r,    sx_r = dx_r * sum(xq over the run)
 // (the K-quant "min" and the Q4_0 / Q6_K code bias fold into of_r).
 //
-// Single-pass prologue: the RMSNorm statistic and the int8 staging come from ONE global read of
-// x.  Block quantisation is scale-invariant, so x*w is quantised un-normalised and 1/rms is
-// applied to the finished dot product in the epilogue (y = inv_rms * W (x*w)).
+// Block quantisation is scale-invariant, so x*w is quantised un-normalised and 1/rms is applied
+// to the finished dot product in the epilogue (y = inv_rms * W (x*w)) -- the RMSNorm statistic
+// and the int8 staging come from ONE read of x.
 //
-// Two work decompositions:
-//  * gemv_q8_rows  : one wave owns a row-pair (grid-stride, 2-deep register pipeline) -- for
-//                    short K where a pair is 1-2 work items;
-//  * gemv_q8_ksplit: the 4 waves of a workgroup split the K items of the same row-pair and
-//                    combine through LDS every G pairs -- for long K (down-proj), where one
-//                    wave per pair would be a 4-7 item dependent chain.
+// Measured on MI355X (tools/gemv_probe.py): with 256-thread workgroups x 4 per CU the per-WG
+// staging cost 1.5-4 us of a 6-20 us GEMV; this version stages once per 512-thread workgroup
+// with every thread quantising one octet (DPP quad reductions), streams weights with
+// non-temporal loads, and sizes the per-lane chunk count U so a row pair's whole K slice is in
+// flight at once.  Q4_K / Q5_K / Q6_K share one chunk order (qweight.h), so a mixed Q4_K_M QKV
+// segment list stages x once.
 #pragma once
 // (included inside namespace aios by gemv_impl.h)
 
@@ -62,15 +61,11 @@ struct QDot<QT_Q5_K> {
 template <>
 struct QDot<QT_Q6_K> {
   __device__ static void isums(const RawChunk& r, int c, const int (&x)[8], int* is) {
-    const int hs = 2 * ((c & 3) >> 1);
     int s0 = 0, s1 = 0;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const uint32_t wv = u4_word(r.a, i), hv = u4_word(r.b, i);
-      const uint32_t lo = (wv & 0x0f0f0f0fu) | (((hv >> hs) & 0x03030303u) << 4);
-      const uint32_t hi = ((wv >> 4) & 0x0f0f0f0fu) | (((hv >> (hs + 4)) & 0x03030303u) << 4);
-      s0 = __builtin_amdgcn_sdot4((int)lo, x[i], s0, false);
-      s1 = __builtin_amdgcn_sdot4((int)hi, x[4 + i], s1, false);
+      s0 = __builtin_amdgcn_sdot4((int)QFmt<QT_Q6_K>::code_lo(r, i), x[i], s0, false);
+      s1 = __builtin_amdgcn_sdot4((int)QFmt<QT_Q6_K>::code_hi(r, i), x[4 + i], s1, false);
     }
     is[0] = s0;
     is[1] = s1;
@@ -96,67 +91,221 @@ __device__ __forceinline__ void q8_scales(const RawChunk& r, int c, float* sc, f
   }
 }
 
-// Stage B rows of x (times the RMSNorm weight when nw != null, NOT normalised) as int8 per
-// 32-block in QT's chunk order; returns per-thread partial sum of squares of x in ssq[b].
+// ---------------------------------------------------------------------------------------------
+// weight loads: non-temporal (each weight byte is read exactly once per decode step; keeping it
+// out of L2/MALL leaves those for x, the KV cache and the residual stream)
+// ---------------------------------------------------------------------------------------------
+typedef unsigned int q8_u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int q8_u32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint4 ldnt16(const uint8_t* p) {
+  const q8_u32x4 v = __builtin_nontemporal_load((const q8_u32x4*)p);
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ uint2 ldnt8(const uint8_t* p) {
+  const q8_u32x2 v = __builtin_nontemporal_load((const q8_u32x2*)p);
+  return make_uint2(v.x, v.y);
+}
+__device__ __forceinline__ uint32_t ldnt2(const uint8_t* p) {
+  return (uint32_t)__builtin_nontemporal_load((const uint16_t*)p);
+}
+
+// One wave-uniform weight segment as buffer descriptors: every weight load is a
+// buffer_load with the row's byte offset in an SGPR (soffset) and only the lane's chunk offset in
+// a VGPR -- no 64-bit address arithmetic per load, and (p made uniform with readfirstlane) no
+// per-item reload of the segment table from the kernarg segment.
+struct SegRs {
+  __amdgpu_buffer_rsrc_t r0, r1, r2, r3;
+  int cols;
+};
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t mk_rsrc(const uint8_t* p) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, 0x7fffffff, 0x00020000);
+}
+__device__ __forceinline__ SegRs seg_rsrc(const GemvArgs& a, int s) {
+  const uint8_t* p0 = a.seg[0].p0;
+  const uint8_t* p1 = a.seg[0].p1;
+  const uint8_t* p2 = a.seg[0].p2;
+  const uint8_t* p3 = a.seg[0].p3;
+  int cols = a.seg[0].cols;
+  if (s == 1) { p0 = a.seg[1].p0; p1 = a.seg[1].p1; p2 = a.seg[1].p2; p3 = a.seg[1].p3; }
+  if (s == 2) { p0 = a.seg[2].p0; p1 = a.seg[2].p1; p2 = a.seg[2].p2; p3 = a.seg[2].p3; }
+  SegRs r;
+  r.r0 = mk_rsrc(p0);
+  r.r1 = mk_rsrc(p1);
+  r.r2 = mk_rsrc(p2);
+  r.r3 = mk_rsrc(p3);
+  r.cols = cols;
+  return r;
+}
+constexpr int LD_NT = 2;  // cache policy: non-temporal (each weight byte is read once per step)
+__device__ __forceinline__ uint4 bl16(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+  const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, LD_NT);
+  return make_uint4(v[0], v[1], v[2], v[3]);
+}
+
+// chunk c (lane-varying) of local row `row` (wave-uniform) of a segment
+template <int QT>
+__device__ __forceinline__ void q8_load(const SegRs& w, int row, int c, RawChunk& r) {
+  if constexpr (QT == QT_Q4_K || QT == QT_Q5_K || QT == QT_Q6_K) {
+    const int nb = w.cols >> 8;
+    const int blk0 = row * nb;  // first block of the row
+    r.a = bl16(w.r0, c * 16, blk0 * 128);
+    if constexpr (QT == QT_Q6_K) {
+      const auto h = __builtin_amdgcn_raw_buffer_load_b64(w.r1, c * 8, blk0 * 64, LD_NT);
+      r.b.x = h[0];
+      r.b.y = h[1];
+      r.c = bl16(w.r2, (c >> 3) * 16, blk0 * 16);
+      r.d = __builtin_amdgcn_raw_buffer_load_b16(w.r3, (c >> 3) * 2, blk0 * 2, LD_NT);
+    } else {
+      r.b = bl16(w.r1, (c >> 3) * 16, blk0 * 16);
+      if constexpr (QT == QT_Q5_K) r.c = bl16(w.r2, (c >> 3) * 32 + 16 * (c & 1), blk0 * 32);
+    }
+  } else if constexpr (QT == QT_Q4_0) {
+    const int blk0 = row * (w.cols >> 5);
+    r.a = bl16(w.r0, c * 16, blk0 * 16);
+    r.d = __builtin_amdgcn_raw_buffer_load_b16(w.r1, c * 2, blk0 * 2, LD_NT);
+  } else {  // Q8_0
+    r.a = bl16(w.r0, c * 16, row * w.cols);
+    r.d = __builtin_amdgcn_raw_buffer_load_b16(w.r1, (c >> 1) * 2, row * (w.cols >> 5) * 2, LD_NT);
+  }
+}
+
+// all U chunks of work item `it` for both rows; lanes past the row end re-load the last chunk
+// (cheap, in-bounds) and are zeroed in q8_compute instead of branching
+template <int QT, int U>
+__device__ __forceinline__ void q8_load_item(const SegRs& w, int lrow, int it, int nch, RawChunk (&r)[U][GEMV_ROWS]) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int c = min((it * U + u) * 64 + lane, nch - 1);
+#pragma unroll
+    for (int rr = 0; rr < GEMV_ROWS; ++rr) q8_load<QT>(w, lrow + rr, c, r[u][rr]);
+  }
+}
+
+__device__ __forceinline__ float dpp_xor1(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));  // quad_perm 1,0,3,2
+}
+__device__ __forceinline__ float dpp_xor2(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4E, 0xF, 0xF, false));  // quad_perm 2,3,0,1
+}
+__device__ __forceinline__ int dpp_xor1_i(int v) { return __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, false); }
+
+// ---------------------------------------------------------------------------------------------
+// Prologue: every thread quantises one 8-element octet of x (times the RMSNorm weight, NOT
+// normalised) per pass; the 4 lanes of a 32-block share amax through DPP quad permutes and the
+// two octets of a 16-run their code sums.  Writes int8 codes in QT's chunk order and per run
+// {dx, dx*sum(codes)}; per-wave partial sums of squares go to red[wave][b].
+// ---------------------------------------------------------------------------------------------
+struct StagePre {  // x (and norm weight) of a thread's first octet, loaded before the weights
+  float4 x0, x1, g0, g1;
+};
+__device__ __forceinline__ void q8_stage_prefetch(const GemvArgs& a, StagePre& pf) {
+  const int noct = a.K >> 3, t = threadIdx.x;
+  if (t < a.B * noct) {
+    const int b = t / noct, o = t - b * noct;
+    const float* src = a.x + (size_t)b * a.ldx + 8 * o;
+    pf.x0 = *(const float4*)src;
+    pf.x1 = *(const float4*)(src + 4);
+    if (a.norm_w) {
+      pf.g0 = *(const float4*)(a.norm_w + 8 * o);
+      pf.g1 = *(const float4*)(a.norm_w + 8 * o + 4);
+    }
+  }
+}
+
 template <int QT, int B>
-__device__ __forceinline__ void stage_q8(const float* __restrict__ x, int ldx, int nb, int K,
-                                         const float* __restrict__ nw, int8_t* xq, float2* ms, float (&ssq)[B]) {
+__device__ __forceinline__ void q8_stage(const GemvArgs& a, int8_t* xq, float2* ms, float* red, const StagePre& pf) {
   using F_ = QFmt<QT>;
   constexpr int W = F_::W, R = F_::RUNS;
-  const int nch = K / W, nblk = K / 32;
+  const int nch = a.K / W, noct = a.K >> 3, total = a.B * noct;
+  float ssq[B];
 #pragma unroll
   for (int b = 0; b < B; ++b) ssq[b] = 0.f;
-  for (int t = threadIdx.x; t < nb * nblk; t += blockDim.x) {
-    const int b = t / nblk, blk = t - b * nblk;
-    const float* src = x + (size_t)b * ldx + blk * 32;
-    float v[32];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const float4 f = *(const float4*)(src + 4 * i);
-      v[4 * i] = f.x; v[4 * i + 1] = f.y; v[4 * i + 2] = f.z; v[4 * i + 3] = f.w;
+  for (int t = threadIdx.x; t < total; t += blockDim.x) {
+    const int b = t / noct, o = t - b * noct;
+    float4 f0, f1, g0, g1;
+    if (t == (int)threadIdx.x) {
+      f0 = pf.x0; f1 = pf.x1; g0 = pf.g0; g1 = pf.g1;
+    } else {
+      const float* src = a.x + (size_t)b * a.ldx + 8 * o;
+      f0 = *(const float4*)src;
+      f1 = *(const float4*)(src + 4);
+      if (a.norm_w) {
+        g0 = *(const float4*)(a.norm_w + 8 * o);
+        g1 = *(const float4*)(a.norm_w + 8 * o + 4);
+      }
     }
+    float v[8] = {f0.x, f0.y, f0.z, f0.w, f1.x, f1.y, f1.z, f1.w};
     float s2 = 0.f;
 #pragma unroll
-    for (int i = 0; i < 32; ++i) s2 = fmaf(v[i], v[i], s2);
+    for (int i = 0; i < 8; ++i) s2 = fmaf(v[i], v[i], s2);
 #pragma unroll
     for (int bb = 0; bb < B; ++bb)
       if (bb == b) ssq[bb] += s2;
-    if (nw) {
-      const float* wp = nw + blk * 32;
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const float4 g = *(const float4*)(wp + 4 * i);
-        v[4 * i] *= g.x; v[4 * i + 1] *= g.y; v[4 * i + 2] *= g.z; v[4 * i + 3] *= g.w;
-      }
+    if (a.norm_w) {
+      v[0] *= g0.x; v[1] *= g0.y; v[2] *= g0.z; v[3] *= g0.w;
+      v[4] *= g1.x; v[5] *= g1.y; v[6] *= g1.z; v[7] *= g1.w;
     }
-    float amax = 0.f;
+    float am = 0.f;
 #pragma unroll
-    for (int i = 0; i < 32; ++i) amax = fmaxf(amax, fabsf(v[i]));
-    const float dx = amax / 127.f;
-    const float inv = amax > 0.f ? 127.f / amax : 0.f;
+    for (int i = 0; i < 8; ++i) am = fmaxf(am, fabsf(v[i]));
+    am = fmaxf(am, dpp_xor1(am));
+    am = fmaxf(am, dpp_xor2(am));
+    const float dx = am * (1.f / 127.f);
+    const float inv = am > 0.f ? 127.f / am : 0.f;
+    uint32_t wq[2];
+    int isum = 0;
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      uint32_t wq[4];
-      int isum = 0;
+    for (int j = 0; j < 2; ++j) {
+      uint32_t wv = 0;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        uint32_t w = 0;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int q = (int)rintf(v[16 * h + 4 * j + e] * inv);
-          isum += q;
-          w |= ((uint32_t)(q & 0xff)) << (8 * e);
-        }
-        wq[j] = w;
+      for (int e = 0; e < 4; ++e) {
+        const int q = (int)rintf(v[4 * j + e] * inv);
+        isum += q;
+        wv |= ((uint32_t)(q & 0xff)) << (8 * e);
       }
-      int c, s0;
-      F_::run_pos(blk * 2 + h, c, s0);
-      int piece = s0 >> 4;
-      if (W == 32) piece = (piece + (c >> 3)) & 1;
-      *(uint4*)(xq + ((size_t)b * nch + c) * W + 16 * piece) = make_uint4(wq[0], wq[1], wq[2], wq[3]);
-      ms[((size_t)b * nch + c) * R + (s0 >> 4)] = make_float2(dx, dx * (float)isum);
+      wq[j] = wv;
+    }
+    isum += dpp_xor1_i(isum);  // the other octet of this 16-run
+    const int quarter = o & 3;
+    int c, s0;
+    F_::run_pos(2 * (o >> 2) + (quarter >> 1), c, s0);
+    int piece = s0 >> 4;
+    if (W == 32) piece = (piece + (c >> 3)) & 1;
+    *(uint2*)(xq + ((size_t)b * nch + c) * W + 16 * piece + 8 * (quarter & 1)) = make_uint2(wq[0], wq[1]);
+    if (!(quarter & 1)) ms[((size_t)b * nch + c) * R + (s0 >> 4)] = make_float2(dx, dx * (float)isum);
+  }
+  if (a.norm_w) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+    for (int b = 0; b < B; ++b) {
+      const float s = wave_sum(ssq[b]);
+      if (lane == 0) red[wave * B + b] = s;
     }
   }
+}
+
+// branch-free Q4_K/Q5_K 6-bit scale/min decode for the chunk's sub-block pair (g = (c&7)>>1)
+__device__ __forceinline__ void kq_scales_bf(const RawChunk& r, int c, float* sc, float* of) {
+  const int g = (c & 7) >> 1, sh = 16 * (g & 1);
+  const uint32_t dd = r.b.x;
+  const float d = __half2float(__ushort_as_half((uint16_t)(dd & 0xffff)));
+  const float dmin = __half2float(__ushort_as_half((uint16_t)(dd >> 16)));
+  const uint32_t w1 = r.b.y >> sh, w2 = r.b.z >> sh, w3 = r.b.w >> sh;
+  const uint32_t sc_lo = w1 & 0x3f3f, m_lo = w2 & 0x3f3f;
+  const uint32_t sc_hi = (w3 & 0x0f0f) | ((w1 >> 2) & 0x3030);
+  const uint32_t m_hi = ((w3 >> 4) & 0x0f0f) | ((w2 >> 2) & 0x3030);
+  const uint32_t scp = g < 2 ? sc_lo : sc_hi, mp = g < 2 ? m_lo : m_hi;
+  sc[0] = d * (float)(scp & 0xff);
+  sc[1] = d * (float)(scp >> 8);
+  of[0] = dmin * (float)(mp & 0xff);
+  of[1] = dmin * (float)(mp >> 8);
+}
+
+template <int QT>
+__device__ __forceinline__ void q8_scales_bf(const RawChunk& r, int c, float* sc, float* of) {
+  if constexpr (QT == QT_Q4_K || QT == QT_Q5_K) kq_scales_bf(r, c, sc, of);
+  else q8_scales<QT>(r, c, sc, of);
 }
 
 template <int QT, int B, int U>
@@ -167,294 +316,359 @@ __device__ __forceinline__ void q8_compute(const RawChunk (&raw)[U][GEMV_ROWS], 
   const int lane = threadIdx.x & 63;
 #pragma unroll
   for (int u = 0; u < U; ++u) {
-    const int c = (it * U + u) * 64 + lane;
-    if (c < nch) {
-      float sc[GEMV_ROWS][R], of[GEMV_ROWS][R];
+    const int c0 = (it * U + u) * 64 + lane;
+    const bool valid = c0 < nch;
+    const int c = valid ? c0 : nch - 1;
+    float sc[GEMV_ROWS][R], of[GEMV_ROWS][R];
 #pragma unroll
-      for (int r = 0; r < GEMV_ROWS; ++r) q8_scales<QT>(raw[u][r], c, sc[r], of[r]);
-#pragma unroll
-      for (int b = 0; b < B; ++b) {
-        int xv[8];
-        const int8_t* xc = xq + ((size_t)b * nch + c) * W;
-        if constexpr (W == 32) {
-          const int rot = (c >> 3) & 1;
-          const uint4 p0 = *(const uint4*)(xc + 16 * rot);
-          const uint4 p1 = *(const uint4*)(xc + 16 * (rot ^ 1));
-          xv[0] = p0.x; xv[1] = p0.y; xv[2] = p0.z; xv[3] = p0.w;
-          xv[4] = p1.x; xv[5] = p1.y; xv[6] = p1.z; xv[7] = p1.w;
-        } else {
-          const uint4 p0 = *(const uint4*)xc;
-          xv[0] = p0.x; xv[1] = p0.y; xv[2] = p0.z; xv[3] = p0.w;
-          xv[4] = xv[5] = xv[6] = xv[7] = 0;
-        }
-        float2 m[R];
-        const float2* mp = ms + ((size_t)b * nch + c) * R;
-#pragma unroll
-        for (int rr = 0; rr < R; ++rr) m[rr] = mp[rr];
-#pragma unroll
-        for (int r = 0; r < GEMV_ROWS; ++r) {
-          int is[R];
-          QDot<QT>::isums(raw[u][r], c, xv, is);
-#pragma unroll
-          for (int rr = 0; rr < R; ++rr) acc[r][b] += sc[r][rr] * m[rr].x * (float)is[rr] - of[r][rr] * m[rr].y;
-        }
-      }
-    }
-  }
-}
-
-// shared prologue: issue nothing, stage x for one or two layouts, produce inv_rms[b] in LDS
-template <int QT0, int QT1, int B>
-__device__ __forceinline__ void q8_prologue(const GemvArgs& a, float* red, float* inv_rms, int8_t* xq0, float2* ms0,
-                                            int8_t* xq1, float2* ms1) {
-  float ssq[B];
-  stage_q8<QT0, B>(a.x, a.ldx, a.B, a.K, a.norm_w, xq0, ms0, ssq);
-  if (QT0 != QT1) {
-    float dummy[B];
-    stage_q8<QT1, B>(a.x, a.ldx, a.B, a.K, a.norm_w, xq1, ms1, dummy);
-  }
-  if (a.norm_w) {
+    for (int r = 0; r < GEMV_ROWS; ++r) q8_scales_bf<QT>(raw[u][r], c, sc[r], of[r]);
 #pragma unroll
     for (int b = 0; b < B; ++b) {
-      if (b < a.B) {
-        const float s = block_sum(ssq[b], red);
-        if (threadIdx.x == 0) inv_rms[b] = rsqrtf(s / (float)a.K + a.eps);
+      int xv[8];
+      const int8_t* xc = xq + ((size_t)b * nch + c) * W;
+      if constexpr (W == 32) {
+        const int rot = (c >> 3) & 1;
+        const uint4 p0 = *(const uint4*)(xc + 16 * rot);
+        const uint4 p1 = *(const uint4*)(xc + 16 * (rot ^ 1));
+        xv[0] = p0.x; xv[1] = p0.y; xv[2] = p0.z; xv[3] = p0.w;
+        xv[4] = p1.x; xv[5] = p1.y; xv[6] = p1.z; xv[7] = p1.w;
+      } else {
+        const uint4 p0 = *(const uint4*)xc;
+        xv[0] = p0.x; xv[1] = p0.y; xv[2] = p0.z; xv[3] = p0.w;
+        xv[4] = xv[5] = xv[6] = xv[7] = 0;
+      }
+      float2 m[R];
+      const float2* mp = ms + ((size_t)b * nch + c) * R;
+#pragma unroll
+      for (int rr = 0; rr < R; ++rr) {
+        m[rr] = mp[rr];
+        if (!valid) m[rr] = make_float2(0.f, 0.f);
+      }
+#pragma unroll
+      for (int r = 0; r < GEMV_ROWS; ++r) {
+        int is[R];
+        QDot<QT>::isums(raw[u][r], c, xv, is);
+#pragma unroll
+        for (int rr = 0; rr < R; ++rr) acc[r][b] += sc[r][rr] * m[rr].x * (float)is[rr] - of[r][rr] * m[rr].y;
       }
     }
   }
-  __syncthreads();
 }
 
-template <int QT0, int QT1, int B>
-struct Q8Lds {
-  float* red;
-  float* inv_rms;
-  float2* ms0;
-  int8_t* xq0;
-  float2* ms1;
-  int8_t* xq1;
-  float* part;  // k-split partials
-  __device__ Q8Lds(float* smem, int K) {
-    constexpr int W0 = QFmt<QT0>::W, W1 = QFmt<QT1>::W, R0 = QFmt<QT0>::RUNS, R1 = QFmt<QT1>::RUNS;
-    red = smem;
-    inv_rms = smem + 16;
-    part = smem + 64;                       // 512 floats
-    ms0 = (float2*)(smem + 64 + 512);
-    xq0 = (int8_t*)(ms0 + (size_t)B * (K / W0) * R0);
-    ms1 = (QT0 != QT1) ? (float2*)(xq0 + (size_t)B * K) : ms0;
-    xq1 = (QT0 != QT1) ? (int8_t*)(ms1 + (size_t)B * (K / W1) * R1) : xq0;
+// ---------------------------------------------------------------------------------------------
+// B = 1 epilogue that issues no global LOAD: vmcnt drains in issue order, so a load here would
+// wait for the next item's whole weight prefetch.  The residual add is a no-return atomic add
+// (each element has exactly one writer, so the result is deterministic), the RoPE (cos, sin) row
+// of this step's position sits in LDS (staged in the prologue), pos/slot are read once up front.
+// Only the rare QKV-bias models load in the epilogue.
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ void qkv_part(const GemvArgs& a, int grow, int& part, int& head, int& lr) {
+  const int hd = a.head_dim, qd = a.q_dim, kvd = a.kv_dim;
+  int r;
+  if (grow < qd) { part = 0; r = grow; }
+  else if (grow < qd + kvd) { part = 1; r = grow - qd; }
+  else { part = 2; r = grow - qd - kvd; }
+  head = r / hd;
+  lr = r - head * hd;
+}
+__device__ __forceinline__ void gemv_epilogue1(const GemvArgs& a, int grow, float v0, float v1, const float2* rope_l,
+                                               int pos0, int slot0) {
+  const int nrow = a.row_base + a.N;
+  switch (a.epi) {
+    case EPI_STORE:
+      a.y[grow] = v0;
+      if (grow + 1 < nrow) a.y[grow + 1] = v1;
+      break;
+    case EPI_RESID:
+      unsafeAtomicAdd(a.y + grow, v0);
+      if (grow + 1 < nrow) unsafeAtomicAdd(a.y + grow + 1, v1);
+      break;
+    case EPI_SWIGLU:
+      a.y[grow >> 1] = v0 / (1.f + __expf(-v0)) * v1;
+      break;
+    case EPI_QKV: {
+      if (a.bias) {
+        v0 += a.bias[grow];
+        v1 += a.bias[grow + 1];
+      }
+      const int hd = a.head_dim;
+      int part, head, lr;
+      qkv_part(a, grow, part, head, lr);
+      const int pp = lr >> 1;
+      int da, db;
+      if (part == 2) { da = lr; db = lr + 1; }
+      else if (a.rope_neox) { da = pp; db = pp + (hd >> 1); }
+      else { da = 2 * pp; db = 2 * pp + 1; }
+      if (part < 2) {
+        const float2 t = rope_l[pp];
+        const float o0 = v0 * t.x - v1 * t.y, o1 = v0 * t.y + v1 * t.x;
+        v0 = o0;
+        v1 = o1;
+      }
+      if (part == 0) {
+        float* q = a.y + head * hd;
+        q[da] = v0;
+        q[db] = v1;
+      } else {
+        bf16_t* cache = (part == 1 ? a.k_cache : a.v_cache);
+        const size_t base = (((size_t)slot0 * a.n_kv_heads + head) * a.max_ctx + pos0) * hd;
+        cache[base + da] = f32_to_bf16(v0);
+        cache[base + db] = f32_to_bf16(v1);
+      }
+    } break;
   }
-  static size_t bytes(int K) {
-    constexpr int W0 = QFmt<QT0>::W, W1 = QFmt<QT1>::W, R0 = QFmt<QT0>::RUNS, R1 = QFmt<QT1>::RUNS;
-    size_t b = (64 + 512) * 4 + (size_t)B * K + (size_t)B * (K / W0) * R0 * 8;
-    if (QT0 != QT1) b += (size_t)B * K + (size_t)B * (K / W1) * R1 * 8;
-    return b + 64;
-  }
+}
+
+// sum of two per-lane values over the wave with 7 cross-lane steps instead of 12:
+// returns (row-0 total, row-1 total) in every lane
+__device__ __forceinline__ float2 wave_sum_pair(float a0, float a1) {
+  const int lane = threadIdx.x & 63;
+  float keep = (lane & 32) ? a1 : a0;
+  const float send = (lane & 32) ? a0 : a1;
+  keep += __shfl_xor(send, 32, 64);
+#pragma unroll
+  for (int o = 16; o > 0; o >>= 1) keep += __shfl_xor(keep, o, 64);
+  const float other = __shfl_xor(keep, 32, 64);
+  return (lane & 32) ? make_float2(other, keep) : make_float2(keep, other);
+}
+
+// ---------------------------------------------------------------------------------------------
+// One wave owns a row pair; a workgroup of Q8_WAVES waves stages x once and walks row pairs
+// grid-stride.  U = 16-B chunks per lane per work item (U*64*W weights of K); host picks U so one
+// item spans all of K where it fits (the row pair's whole weight slice in flight at once).
+// PIPE = 2 double-buffers across items/pairs (short K), 1 = single buffer (large U).
+// ---------------------------------------------------------------------------------------------
+constexpr int Q8_WAVES = 8;
+
+template <int QT>
+struct FmtTag {
+  static constexpr int value = QT;
 };
 
-__device__ __forceinline__ float q8_rms_scale(const GemvArgs& a, const float* inv_rms, int b) {
-  return a.norm_w ? inv_rms[b] : 1.f;
-}
-
-// ---------------------------------------------------------------------------------------------
-// one wave per row-pair
-// ---------------------------------------------------------------------------------------------
-template <int QT0, int QT1, int B, int U>
-__global__ void __launch_bounds__(GP_THREADS) gemv_q8_rows(GemvArgs a) {
+template <int QT0, int QT1, int B, int U, int PIPE>
+__global__ void __launch_bounds__(Q8_WAVES * 64) gemv_q8_rows(GemvArgs a) {
+  static_assert(same_xlayout<QT0, QT1>, "mixed segments must share the activation layout");
   extern __shared__ __attribute__((aligned(16))) float smem[];
   constexpr bool MIXED = QT0 != QT1;
-  constexpr int W0 = QFmt<QT0>::W, W1 = QFmt<QT1>::W;
-  Q8Lds<QT0, QT1, B> L(smem, a.K);
+  constexpr int W = QFmt<QT0>::W, R = QFmt<QT0>::RUNS;
+  const int nch = a.K / W;
+  float* red = smem;                                   // [Q8_WAVES][B]
+  float2* ms = (float2*)(smem + 64);                   // [B][nch][R]
+  int8_t* xq = (int8_t*)(ms + (size_t)B * nch * R);    // [B][nch][W]
+  float2* rope_l = (float2*)(xq + (size_t)B * a.K);    // [head_dim/2] (cos, sin) at pos0 (B = 1, QKV)
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int npairs = a.N >> 1;
-  const int nch0 = a.K / W0, nch1 = a.K / W1;
-  const int nit0 = (nch0 + 64 * U - 1) / (64 * U), nit1 = (nch1 + 64 * U - 1) / (64 * U);
-  const int stride = gridDim.x * GP_WAVES;
+  // pairs [0, np0) use QT0, [np0, npairs) the last segment's QT1: one loop per format, so every
+  // loop issues a fixed load sequence and the compiler's vmcnt waits stay exact
+  const int np0 = (MIXED && a.nseg > 1) ? (a.nseg == 2 ? a.seg_row0[1] : a.seg_row0[2]) >> 1 : npairs;
+  const int nit = (nch + 64 * U - 1) / (64 * U);
+  const int stride = gridDim.x * Q8_WAVES;
+  const int wid = __builtin_amdgcn_readfirstlane(blockIdx.x * Q8_WAVES + wave);  // wave-uniform -> SGPR
 
-  auto info = [&](int p, int& lrow, bool& t1, const QWeight*& w) {
+  auto seg_idx = [&](int p, int& lrow) -> int {
     const int row = 2 * p;
     int s = 0;
 #pragma unroll
     for (int k = 1; k < GEMV_MAX_SEGS; ++k)
       if (k < a.nseg && row >= a.seg_row0[k]) s = k;
-    lrow = row - a.seg_row0[s];
-    t1 = MIXED && (s == a.nseg - 1) && a.nseg > 1;
-    w = &a.seg[s];
+    lrow = row - (s == 0 ? 0 : (s == 1 ? a.seg_row0[1] : a.seg_row0[2]));
+    return s;
   };
-  auto load = [&](int p, int it, RawChunk (&r)[U][GEMV_ROWS]) {
+  // Loads are issued unconditionally: past the range end they read x (L2-resident, in bounds for
+  // every stream's small offsets) instead of branching -- a conditional load makes the
+  // outstanding-load count path dependent and the compiler then drains with vmcnt(0).
+  auto load = [&](auto tag, int p, int pend, int it, RawChunk (&r)[U][GEMV_ROWS]) {
+    constexpr int QT = decltype(tag)::value;
+    const bool live = p < pend;
     int lrow;
-    bool t1;
-    const QWeight* w;
-    info(p, lrow, t1, w);
-    if (MIXED && t1) gp_load<QT1, U>(*w, lrow, it, nch1, r);
-    else gp_load<QT0, U>(*w, lrow, it, nch0, r);
+    const int s = seg_idx(live ? p : pend - 1, lrow);
+    SegRs w = seg_rsrc(a, s);
+    if (!live) {
+      const __amdgpu_buffer_rsrc_t rx = mk_rsrc((const uint8_t*)a.x);
+      w.r0 = w.r1 = w.r2 = w.r3 = rx;
+      lrow = 0;
+    }
+    q8_load_item<QT, U>(w, lrow, it, nch, r);
   };
 
-  int p = blockIdx.x * GP_WAVES + wave;
-  int it = 0;
-  RawChunk bufA[U][GEMV_ROWS], bufB[U][GEMV_ROWS];
-  if (p < npairs) load(p, 0, bufA);  // weight loads in flight during the prologue
-  q8_prologue<QT0, QT1, B>(a, L.red, L.inv_rms, L.xq0, L.ms0, L.xq1, L.ms1);
+  int pos0 = 0, slot0 = 0;
+  if constexpr (B == 1) {
+    if (a.epi == EPI_QKV) {
+      pos0 = a.pos[0];
+      slot0 = a.slot ? a.slot[0] : 0;
+      for (int i = threadIdx.x; i < (a.head_dim >> 1); i += blockDim.x) {
+        float2 t;
+        if (a.rope_cs) {
+          t = a.rope_cs[(size_t)pos0 * (a.head_dim >> 1) + i];
+        } else {
+          float sn, cs;
+          sincosf((float)pos0 * powf(a.rope_base, -2.f * (float)i / (float)a.head_dim), &sn, &cs);
+          t = make_float2(cs, sn);
+        }
+        rope_l[i] = t;
+      }
+    }
+  }
 
   float acc[GEMV_ROWS][B];
 #pragma unroll
   for (int r = 0; r < GEMV_ROWS; ++r)
 #pragma unroll
     for (int b = 0; b < B; ++b) acc[r][b] = 0.f;
-
-  auto step = [&](RawChunk (&cur)[U][GEMV_ROWS], RawChunk (&nxt)[U][GEMV_ROWS]) -> bool {
-    int lrow;
-    bool t1;
-    const QWeight* w;
-    info(p, lrow, t1, w);
-    const int nit = (MIXED && t1) ? nit1 : nit0;
-    int pn = p, itn = it + 1;
-    if (itn >= nit) { pn = p + stride; itn = 0; }
-    if (pn < npairs) load(pn, itn, nxt);
-    if (MIXED && t1) q8_compute<QT1, B, U>(cur, it, nch1, L.xq1, L.ms1, acc);
-    else q8_compute<QT0, B, U>(cur, it, nch0, L.xq0, L.ms0, acc);
-    if (itn == 0) {
+  auto compute = [&](auto tag, int it, const RawChunk (&cur)[U][GEMV_ROWS]) {
+    constexpr int QT = decltype(tag)::value;
+    if (a.tune_dbg & 2) {
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int r = 0; r < GEMV_ROWS; ++r) {
+          const RawChunk& q = cur[u][r];
+          acc[r][0] += (float)((q.a.x ^ q.a.y ^ q.a.z ^ q.a.w ^ q.b.x ^ q.b.y ^ q.b.z ^ q.b.w ^ q.c.x ^ q.c.w ^ q.d) & 0xff);
+        }
+      return;
+    }
+    q8_compute<QT, B, U>(cur, it, nch, xq, ms, acc);
+  };
+  auto finish = [&](int p) {
+    float s[B];
+#pragma unroll
+    for (int b = 0; b < B; ++b) {
+      s[b] = 1.f;
+      if (a.norm_w) {
+        float t = 0.f;
+#pragma unroll
+        for (int w = 0; w < Q8_WAVES; ++w) t += red[w * B + b];
+        s[b] = rsqrtf(t / (float)a.K + a.eps);
+      }
+    }
+    if constexpr (B == 1) {
+      const float2 v = wave_sum_pair(acc[0][0], acc[1][0]);
+      if (lane == 0) gemv_epilogue1(a, a.row_base + 2 * p, v.x * s[0], v.y * s[0], rope_l, pos0, slot0);
+    } else {
 #pragma unroll
       for (int r = 0; r < GEMV_ROWS; ++r)
 #pragma unroll
         for (int b = 0; b < B; ++b) acc[r][b] = wave_sum(acc[r][b]);
       if (lane < a.B) {
-        float v0 = 0.f, v1 = 0.f;
+        float v0 = 0.f, v1 = 0.f, sc = 1.f;
 #pragma unroll
         for (int b = 0; b < B; ++b)
-          if (lane == b) { v0 = acc[0][b]; v1 = acc[1][b]; }
-        const float s = q8_rms_scale(a, L.inv_rms, lane);
-        gemv_epilogue(a, a.row_base + 2 * p, lane, v0 * s, v1 * s);
+          if (lane == b) { v0 = acc[0][b]; v1 = acc[1][b]; sc = s[b]; }
+        gemv_epilogue(a, a.row_base + 2 * p, lane, v0 * sc, v1 * sc);
       }
-#pragma unroll
-      for (int r = 0; r < GEMV_ROWS; ++r)
-#pragma unroll
-        for (int b = 0; b < B; ++b) acc[r][b] = 0.f;
     }
-    p = pn;
-    it = itn;
-    return p < npairs;
+#pragma unroll
+    for (int r = 0; r < GEMV_ROWS; ++r)
+#pragma unroll
+      for (int b = 0; b < B; ++b) acc[r][b] = 0.f;
   };
-  while (p < npairs) {
-    if (!step(bufA, bufB)) break;
-    if (!step(bufB, bufA)) break;
-  }
-}
 
-// ---------------------------------------------------------------------------------------------
-// K split over the 4 waves of a workgroup (single format).  Pair j of the workgroup is
-// p = blockIdx.x + j*gridDim.x; wave w handles items it = w, w+4, ... of every pair; partials go
-// to LDS part[g][w][2][B] and every KS_G pairs one barrier + a 4-way sum runs the epilogues.
-// ---------------------------------------------------------------------------------------------
-constexpr int KS_G = 8;
-
-template <int QT, int B, int U>
-__global__ void __launch_bounds__(GP_THREADS) gemv_q8_ksplit(GemvArgs a) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  constexpr int W = QFmt<QT>::W;
-  Q8Lds<QT, QT, B> L(smem, a.K);
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int npairs = a.N >> 1;
-  const int nch = a.K / W;
-  const int nit = (nch + 64 * U - 1) / (64 * U);
-  const QWeight& w = a.seg[0];
-  const int npb = blockIdx.x < npairs ? (npairs - 1 - blockIdx.x) / gridDim.x + 1 : 0;  // pairs of this WG
-  const int ni = wave < nit ? (nit - wave + GP_WAVES - 1) / GP_WAVES : 0;                // items per pair
-  const int total = npb * ni;
-
-  auto load_f = [&](int f, RawChunk (&r)[U][GEMV_ROWS]) {
-    const int j = f / ni, i = f - j * ni;
-    const int p = blockIdx.x + j * gridDim.x;
-    gp_load<QT, U>(w, 2 * p, wave + GP_WAVES * i, nch, r);
-  };
-  RawChunk bufA[U][GEMV_ROWS], bufB[U][GEMV_ROWS];
-  if (total > 0) load_f(0, bufA);
-  q8_prologue<QT, QT, B>(a, L.red, L.inv_rms, L.xq0, L.ms0, L.xq0, L.ms0);
-
-  float acc[GEMV_ROWS][B];
-#pragma unroll
-  for (int r = 0; r < GEMV_ROWS; ++r)
-#pragma unroll
-    for (int b = 0; b < B; ++b) acc[r][b] = 0.f;
-
-  int f = 0;  // this wave's flattened item cursor
-  for (int j0 = 0; j0 < npb; j0 += KS_G) {
-    const int jn = min(j0 + KS_G, npb);
-    for (int j = j0; j < jn; ++j) {
-      for (int i = 0; i < ni; ++i) {
-        if (f + 1 < total) load_f(f + 1, bufB);  // next item in flight while this one computes
-        q8_compute<QT, B, U>(bufA, wave + GP_WAVES * i, nch, L.xq0, L.ms0, acc);
-        ++f;
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-#pragma unroll
-          for (int r = 0; r < GEMV_ROWS; ++r) bufA[u][r] = bufB[u][r];
+  RawChunk bufA[U][GEMV_ROWS];
+  // walk pairs [p, pend) grid-stride; bufA already holds item (p, 0)
+  auto run = [&](auto tag, int p, int pend) {
+    if (p >= pend) return;
+    if constexpr (PIPE == 2) {
+      // two register buffers, each reloaded right after it was consumed: while one item
+      // computes, the next one's loads (other buffer) stay in flight
+      RawChunk bufB[U][GEMV_ROWS];
+      auto advance = [&](int& pp, int& ii) {
+        if (++ii >= nit) { ii = 0; pp += stride; }
+      };
+      int pA = p, iA = 0, pB = p, iB = 0;
+      advance(pB, iB);
+      load(tag, pB, pend, iB, bufB);
+      while (true) {
+        compute(tag, iA, bufA);
+        if (iA == nit - 1) finish(pA);
+        pA = pB; iA = iB;
+        advance(pA, iA);
+        load(tag, pA, pend, iA, bufA);
+        if (pB >= pend) break;
+        compute(tag, iB, bufB);
+        if (iB == nit - 1) finish(pB);
+        pB = pA; iB = iA;
+        advance(pB, iB);
+        load(tag, pB, pend, iB, bufB);
+        if (pA >= pend) break;
       }
-      // this wave's partial of pair j -> LDS
-#pragma unroll
-      for (int r = 0; r < GEMV_ROWS; ++r)
-#pragma unroll
-        for (int b = 0; b < B; ++b) {
-          const float v = wave_sum(acc[r][b]);
-          if (lane == 0) L.part[(((j - j0) * GP_WAVES + wave) * GEMV_ROWS + r) * B + b] = v;
-          acc[r][b] = 0.f;
+    } else {
+      int it = 0;
+      while (true) {
+        compute(tag, it, bufA);
+        if (++it >= nit) {
+          finish(p);
+          it = 0;
+          p += stride;
+          if (p >= pend) break;
         }
-    }
-    __syncthreads();
-    for (int t = threadIdx.x; t < (jn - j0) * B; t += GP_THREADS) {
-      const int g = t / B, b = t - g * B;
-      if (b < a.B) {
-        float v[GEMV_ROWS] = {0.f, 0.f};
-#pragma unroll
-        for (int ww = 0; ww < GP_WAVES; ++ww)
-#pragma unroll
-          for (int r = 0; r < GEMV_ROWS; ++r) v[r] += L.part[((g * GP_WAVES + ww) * GEMV_ROWS + r) * B + b];
-        const float s = q8_rms_scale(a, L.inv_rms, b);
-        const int p = blockIdx.x + (j0 + g) * gridDim.x;
-        gemv_epilogue(a, a.row_base + 2 * p, b, v[0] * s, v[1] * s);
+        load(tag, p, pend, it, bufA);
       }
     }
-    __syncthreads();
+  };
+
+  StagePre pf{};
+  q8_stage_prefetch(a, pf);                                // x first: its wait then does not cover the weights
+  load(FmtTag<QT0>{}, wid, np0, 0, bufA);                  // weight loads in flight during the prologue
+  if (!(a.tune_dbg & 1)) q8_stage<QT0, B>(a, xq, ms, red, pf);
+  __syncthreads();
+  run(FmtTag<QT0>{}, wid, np0);
+  if constexpr (MIXED) {
+    load(FmtTag<QT1>{}, np0 + wid, npairs, 0, bufA);
+    run(FmtTag<QT1>{}, np0 + wid, npairs);
   }
 }
 
-template <int QT0, int QT1, int B, int U>
-bool launch_gemv_q8(GemvArgs a, hipStream_t st) {
-  const size_t lds = Q8Lds<QT0, QT1, B>::bytes(a.K);
-  if (lds > 96 * 1024) return false;
-  constexpr int W0 = QFmt<QT0>::W;
-  const int nit = (a.K / W0 + 64 * U - 1) / (64 * U);
-  const int npairs = a.N / 2;
-  // K-split measured slower than row pairs on MI355X (down-proj 15.6 vs 13.6 us): opt-in only
-  const bool ksplit = (QT0 == QT1) && nit >= 3 && a.tune_ksplit > 0;
-  a.kt_max = a.K;
-  if (ksplit) {
-    static int occ = -1;
-    if (occ < 0) {
-      int o = 0;
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, gemv_q8_ksplit<QT0, B, U>, GP_THREADS, lds) != hipSuccess ||
-          o <= 0)
-        o = 1;
-      occ = o;
-    }
-    int per_cu = std::max(1, std::min(occ, (int)((160 * 1024) / lds)));
-    if (a.tune_grid > 0) per_cu = a.tune_grid;
-    const int blocks = std::min(npairs, device_cu_count() * per_cu);
-    hipLaunchKernelGGL((gemv_q8_ksplit<QT0, B, U>), dim3(blocks), dim3(GP_THREADS), lds, st, a);
-    return true;
-  }
+template <int QT0, int QT1, int B>
+inline size_t q8_lds_bytes(int K) {
+  constexpr int W = QFmt<QT0>::W, R = QFmt<QT0>::RUNS;
+  return 64 * 4 + (size_t)B * (K / W) * R * 8 + (size_t)B * K + 2048 + 16;
+}
+
+template <int QT0, int QT1, int B, int U, int PIPE>
+void launch_q8_rows(const GemvArgs& a, size_t lds, hipStream_t st) {
   static int occ = -1;
   if (occ < 0) {
     int o = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, gemv_q8_rows<QT0, QT1, B, U>, GP_THREADS, lds) !=
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, gemv_q8_rows<QT0, QT1, B, U, PIPE>, Q8_WAVES * 64, lds) !=
             hipSuccess || o <= 0)
       o = 1;
     occ = o;
   }
-  int per_cu = std::max(1, std::min(occ, (int)((160 * 1024) / lds)));
+  int per_cu = std::min(occ, 2);
   if (a.tune_grid > 0) per_cu = a.tune_grid;
-  const int groups = (npairs + GP_WAVES - 1) / GP_WAVES;
+  const int npairs = a.N / 2;
+  const int groups = (npairs + Q8_WAVES - 1) / Q8_WAVES;
   const int blocks = std::min(groups, device_cu_count() * per_cu);
-  hipLaunchKernelGGL((gemv_q8_rows<QT0, QT1, B, U>), dim3(blocks), dim3(GP_THREADS), lds, st, a);
-  return true;
+  hipLaunchKernelGGL((gemv_q8_rows<QT0, QT1, B, U, PIPE>), dim3(blocks), dim3(Q8_WAVES * 64), lds, st, a);
+}
+
+template <int QT0, int QT1, int B>
+bool launch_gemv_q8(GemvArgs a, hipStream_t st) {
+  if constexpr (!same_xlayout<QT0, QT1>) {
+    return false;
+  } else {
+    const size_t lds = q8_lds_bytes<QT0, QT1, B>(a.K);
+    if (lds > 128 * 1024) return false;
+    a.kt_max = a.K;
+    if constexpr (B == 1) {
+      const int nch = a.K / QFmt<QT0>::W;
+      int u = a.tune_u;
+      if (u <= 0 || u > 8) u = nch <= 512 ? (nch + 63) / 64 : 2;
+      switch (u) {
+        case 1: launch_q8_rows<QT0, QT1, 1, 1, 2>(a, lds, st); break;
+        case 2: launch_q8_rows<QT0, QT1, 1, 2, 2>(a, lds, st); break;
+        case 3: launch_q8_rows<QT0, QT1, 1, 3, 1>(a, lds, st); break;
+        case 4: launch_q8_rows<QT0, QT1, 1, 4, 1>(a, lds, st); break;
+        case 5: launch_q8_rows<QT0, QT1, 1, 5, 1>(a, lds, st); break;
+        case 6: launch_q8_rows<QT0, QT1, 1, 6, 1>(a, lds, st); break;
+        case 7: launch_q8_rows<QT0, QT1, 1, 7, 1>(a, lds, st); break;
+        default: launch_q8_rows<QT0, QT1, 1, 8, 1>(a, lds, st); break;
+      }
+    } else if constexpr (B == 8) {
+      launch_q8_rows<QT0, QT1, 8, 1, 2>(a, lds, st);
+    } else {
+      launch_q8_rows<QT0, QT1, B, 2, 2>(a, lds, st);
+    }
+    return true;
+  }
 }

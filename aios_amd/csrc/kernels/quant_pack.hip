@@ -29,10 +29,32 @@ __global__ void repack_kernel(int qt, const uint8_t* __restrict__ raw, size_t nb
       for (int k = 0; k < 128; ++k) p0[i * 128 + k] = s[48 + k];
     } break;
     case QT_Q6_K: {
+      // re-ordered into the Q4_K chunk order (see qweight.h): 6-bit code q[k] -> low nibble in
+      // the Q4_K qs position of k, high 2 bits in a per-chunk {h0, h1} word pair.
       const uint8_t* s = raw + i * 210;
-      for (int k = 0; k < 128; ++k) p0[i * 128 + k] = s[k];
-      for (int k = 0; k < 64; ++k) p1[i * 64 + k] = s[128 + k];
-      for (int k = 0; k < 16; ++k) p2[i * 16 + k] = s[192 + k];
+      const uint8_t* ql = s;
+      const uint8_t* qh = s + 128;
+      uint8_t q[256];
+      for (int k = 0; k < 256; ++k) {
+        const int n = k >> 7, r = k & 127, q4 = r >> 5, l = r & 31;
+        const uint8_t lb = ql[64 * n + 32 * (q4 & 1) + l];
+        const int nib = (q4 >> 1) ? (lb >> 4) : (lb & 0xF);
+        q[k] = (uint8_t)(nib | (((qh[32 * n + l] >> (2 * q4)) & 3) << 4));
+      }
+      for (int j = 0; j < 128; ++j) {
+        const int g = j >> 5, t = j & 31;
+        p0[i * 128 + j] = (uint8_t)((q[64 * g + t] & 0xF) | ((q[64 * g + 32 + t] & 0xF) << 4));
+      }
+      for (int l = 0; l < 8; ++l) {
+        const int k0 = 64 * (l >> 1) + 16 * (l & 1);
+        for (int half = 0; half < 2; ++half) {
+          uint32_t hw = 0;
+          for (int j = 0; j < 4; ++j)
+            for (int e = 0; e < 4; ++e) hw |= (uint32_t)((q[k0 + 32 * half + 4 * j + e] >> 4) & 3) << (8 * e + 2 * j);
+          for (int bb = 0; bb < 4; ++bb) p1[i * 64 + l * 8 + 4 * half + bb] = (uint8_t)(hw >> (8 * bb));
+        }
+      }
+      for (int k = 0; k < 16; ++k) p2[i * 16 + k] = s[192 + k];  // int8 scale of k/16
       p3[i * 2] = s[208];
       p3[i * 2 + 1] = s[209];
     } break;
@@ -79,17 +101,16 @@ __device__ float dq_elem(const QWeight& w, int row, int k) {
       return d * sc * q - dmin * m;
     }
     case QT_Q6_K: {
-      const int nb = w.cols >> 8, b = k >> 8, kk = k & 255, n = kk >> 7, r = kk & 127, q4 = r >> 5, l = r & 31;
+      const int nb = w.cols >> 8, b = k >> 8, kk = k & 255, g = kk >> 6, hi = (kk >> 5) & 1, i = kk & 31;
       const size_t blk = (size_t)row * nb + b;
-      const uint8_t* ql = w.p0 + blk * 128 + 64 * n;
-      const uint8_t* qh = w.p1 + blk * 64 + 32 * n;
-      const int8_t* sc = (const int8_t*)(w.p2 + blk * 16) + 8 * n;
+      const uint8_t byte = w.p0[blk * 128 + 32 * g + i];
+      const int nib = hi ? (byte >> 4) : (byte & 0xF);
+      const int l = 2 * g + (i >> 4), j = (i & 15) >> 2, e = i & 3;
+      const uint8_t* hp = w.p1 + blk * 64 + l * 8 + 4 * hi;
+      const uint32_t hw = hp[0] | (hp[1] << 8) | (hp[2] << 16) | ((uint32_t)hp[3] << 24);
+      const int q = (nib | (((hw >> (8 * e + 2 * j)) & 3) << 4)) - 32;
       const float d = h2f(*(const uint16_t*)(w.p3 + blk * 2));
-      const int lb = (q4 & 1) ? ql[l + 32] : ql[l];
-      const int nib = (q4 >> 1) ? (lb >> 4) : (lb & 0xF);
-      const int h = (qh[l] >> (2 * q4)) & 3;
-      const int q = (nib | (h << 4)) - 32;
-      return d * sc[l / 16 + 2 * q4] * q;
+      return d * (float)((const int8_t*)(w.p2 + blk * 16))[kk >> 4] * q;
     }
     case QT_Q4_0: {
       const int nb = w.cols >> 5, b = k >> 5, j = k & 31;

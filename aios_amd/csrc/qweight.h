@@ -7,8 +7,8 @@
 //
 //   Q4_K : p0 = qs   [rows][nb*128]    p1 = meta [rows][nb*16] = {f16 d, f16 dmin, u8 scales[12]}
 //   Q5_K : p0 = qs   [rows][nb*128]    p1 = meta [rows][nb*16]   p2 = qh [rows][nb*32]
-//   Q6_K : p0 = ql   [rows][nb*128]    p1 = qh   [rows][nb*64]   p2 = sc [rows][nb*16] (int8)
-//          p3 = d    [rows][nb] (f16)
+//   Q6_K : p0 = lo4  [rows][nb*128]    p1 = hi2  [rows][nb*64]   p2 = sc [rows][nb*16] (int8)
+//          p3 = d    [rows][nb] (f16)         (re-ordered into the Q4_K chunk order, see below)
 //   Q4_0 : p0 = qs   [rows][nb*16]     p1 = d    [rows][nb] (f16)             (nb = K/32)
 //   Q8_0 : p0 = qs   [rows][nb*32]     p1 = d    [rows][nb] (f16)             (nb = K/32)
 //   F16 / BF16 : p0 = [rows][K]
@@ -42,6 +42,11 @@ struct RawChunk {
 
 template <int QT>
 struct QFmt;
+
+// formats whose chunk -> k mapping is identical share one staged activation layout
+__host__ __device__ constexpr bool kq_layout(int q) { return q == QT_Q4_K || q == QT_Q5_K || q == QT_Q6_K; }
+template <int A, int B>
+constexpr bool same_xlayout = A == B || (kq_layout(A) && kq_layout(B));
 
 __device__ __forceinline__ uint32_t u4_word(const uint4& v, int i) {
   return i == 0 ? v.x : (i == 1 ? v.y : (i == 2 ? v.z : v.w));
@@ -135,49 +140,49 @@ struct QFmt<QT_Q5_K> {
 };
 
 // ------------------------------------------------------------------------------------ Q6_K
-// chunk p (0..7) of a block: n = p>>2 (128-half), o = 16*(p&3) ql offset inside the half.
-//   o <  32: l = o..o+15 : low nibble -> k = 128n + l      (scale is = l/16 + 0), high -> +64 (is+4)
-//   o >= 32: l = o-32..  : low nibble -> k = 128n + l + 32 (is + 2),              high -> +96 (is+6)
+// Repacked into the Q4_K chunk order (quant_pack.hip), so x staging is shared with Q4_K/Q5_K and a
+// mixed Q4_K_M QKV segment list (V in Q6_K) needs ONE activation layout:
+//   p0 = low nibbles exactly where Q4_K keeps its 4-bit codes,
+//   p1 = 8 B per chunk {h0, h1}: bits (8e + 2j)..+1 of h_run = high 2 bits of weight 4j+e of the run,
+//   p2 = the 16 int8 scales (scale of k is sc[k/16]),  p3 = f16 d.
 template <>
 struct QFmt<QT_Q6_K> {
   static constexpr int W = 32, RUNS = 2, CHUNKS_PER_BLOCK = 8, BLOCK = 256;
-  __device__ static int chunk_k0(int c, int run) {
-    const int b = c >> 3, p = c & 7, n = p >> 2, o = 16 * (p & 3);
-    const int l = o & 31, up = o >> 5;
-    return b * 256 + 128 * n + l + 32 * up + 64 * run;
-  }
-  __device__ static void run_pos(int r, int& c, int& s0) {
-    const int b = r >> 4, rr = r & 15, n = rr >> 3, q4 = (rr >> 1) & 3, lh = rr & 1;
-    c = b * 8 + 4 * n + 2 * (q4 & 1) + lh;
-    s0 = 16 * (q4 >> 1);
-  }
+  __device__ static int chunk_k0(int c, int run) { return QFmt<QT_Q4_K>::chunk_k0(c, run); }
+  __device__ static void run_pos(int r, int& c, int& s0) { QFmt<QT_Q4_K>::run_pos(r, c, s0); }
   __device__ static void load(const QWeight& w, int row, int c, RawChunk& r) {
     const int nb = w.cols >> 8;
     const size_t blk = (size_t)row * nb + (c >> 3);
-    const int p = c & 7, n = p >> 2, o = 16 * (p & 3);
-    r.a = *(const uint4*)(w.p0 + ((size_t)row * nb * 8 + c) * 16);
-    r.b = *(const uint4*)(w.p1 + blk * 64 + 32 * n + (o & 31));
+    const size_t ch = (size_t)row * nb * 8 + c;
+    r.a = *(const uint4*)(w.p0 + ch * 16);
+    const uint2 h = *(const uint2*)(w.p1 + ch * 8);
+    r.b.x = h.x;
+    r.b.y = h.y;
     r.c = *(const uint4*)(w.p2 + blk * 16);
     r.d = *(const uint16_t*)(w.p3 + blk * 2);
   }
+  __device__ static void sc_idx(int c, int& s_lo, int& s_hi) {
+    const int l = c & 7;
+    s_lo = 4 * (l >> 1) + (l & 1);
+    s_hi = s_lo + 2;
+  }
+  __device__ static uint32_t code_lo(const RawChunk& r, int i) {
+    return (u4_word(r.a, i) & 0x0f0f0f0fu) | (((r.b.x >> (2 * i)) & 0x03030303u) << 4);
+  }
+  __device__ static uint32_t code_hi(const RawChunk& r, int i) {
+    return ((u4_word(r.a, i) >> 4) & 0x0f0f0f0fu) | (((r.b.y >> (2 * i)) & 0x03030303u) << 4);
+  }
   __device__ static void decode(const RawChunk& r, int c, float q[32], float sc[2], float of[2]) {
-    const int p = c & 7, n = p >> 2, o = 16 * (p & 3);
-    const int up = o >> 5, is = (o & 31) >> 4;
+    int s_lo, s_hi;
+    sc_idx(c, s_lo, s_hi);
     const float d = __half2float(__ushort_as_half((uint16_t)r.d));
-    const int s_lo = 8 * n + is + 2 * up, s_hi = s_lo + 4;
-    const int8_t sl = (int8_t)((u4_word(r.c, s_lo >> 2) >> (8 * (s_lo & 3))) & 0xff);
-    const int8_t sh = (int8_t)((u4_word(r.c, s_hi >> 2) >> (8 * (s_hi & 3))) & 0xff);
-    sc[0] = d * (float)sl;
-    sc[1] = d * (float)sh;
-    // q - 32: folded as -32*sc*sum(x)
-    of[0] = 32.f * sc[0];
+    sc[0] = d * (float)(int8_t)((u4_word(r.c, s_lo >> 2) >> (8 * (s_lo & 3))) & 0xff);
+    sc[1] = d * (float)(int8_t)((u4_word(r.c, s_hi >> 2) >> (8 * (s_hi & 3))) & 0xff);
+    of[0] = 32.f * sc[0];  // q - 32 folded as -32*sc*sum(x)
     of[1] = 32.f * sc[1];
-    const int hs = 2 * up;  // qh bit pair for low nibble: bits hs..hs+1, high nibble: hs+4..hs+5
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const uint32_t wv = u4_word(r.a, i), hv = u4_word(r.b, i);
-      const uint32_t lo = (wv & 0x0f0f0f0fu) | (((hv >> hs) & 0x03030303u) << 4);
-      const uint32_t hi = ((wv >> 4) & 0x0f0f0f0fu) | (((hv >> (hs + 4)) & 0x03030303u) << 4);
+      const uint32_t lo = code_lo(r, i), hi = code_hi(r, i);
       q[4 * i + 0] = (float)(lo & 0xff);
       q[4 * i + 1] = (float)((lo >> 8) & 0xff);
       q[4 * i + 2] = (float)((lo >> 16) & 0xff);
@@ -354,23 +359,16 @@ struct QStream<QT_Q5_K> {
 template <>
 struct QStream<QT_Q6_K> {
   __device__ static void scales(const RawChunk& r, int c, float* sc, float* of) {
-    const int p = c & 7, n = p >> 2, o = 16 * (p & 3);
-    const int up = o >> 5, is = (o & 31) >> 4;
+    int s_lo, s_hi;
+    QFmt<QT_Q6_K>::sc_idx(c, s_lo, s_hi);
     const float d = __half2float(__ushort_as_half((uint16_t)r.d));
-    const int s_lo = 8 * n + is + 2 * up, s_hi = s_lo + 4;
-    const int8_t sl = (int8_t)((u4_word(r.c, s_lo >> 2) >> (8 * (s_lo & 3))) & 0xff);
-    const int8_t shv = (int8_t)((u4_word(r.c, s_hi >> 2) >> (8 * (s_hi & 3))) & 0xff);
-    sc[0] = d * (float)sl;
-    sc[1] = d * (float)shv;
+    sc[0] = d * (float)(int8_t)((u4_word(r.c, s_lo >> 2) >> (8 * (s_lo & 3))) & 0xff);
+    sc[1] = d * (float)(int8_t)((u4_word(r.c, s_hi >> 2) >> (8 * (s_hi & 3))) & 0xff);
     of[0] = 32.f * sc[0];
     of[1] = 32.f * sc[1];
   }
   __device__ static void quad(const RawChunk& r, int c, int j, float q[4]) {
-    const int up = (c & 3) >> 1;   // o >= 32  <=>  (p & 3) >= 2
-    const int hs = 2 * up + (j >= 4 ? 4 : 0);
-    const uint32_t wv = u4_word(r.a, j & 3), hv = u4_word(r.b, j & 3);
-    const uint32_t nib = j < 4 ? (wv & 0x0f0f0f0fu) : ((wv >> 4) & 0x0f0f0f0fu);
-    ubytes4(nib | (((hv >> hs) & 0x03030303u) << 4), q);
+    ubytes4(j < 4 ? QFmt<QT_Q6_K>::code_lo(r, j) : QFmt<QT_Q6_K>::code_hi(r, j & 3), q);
   }
 };
 
