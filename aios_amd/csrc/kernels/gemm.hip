@@ -36,12 +36,8 @@ __device__ __forceinline__ void dequant16(const QWeight& w, int row, int k0, uin
       const uint4 meta = *(const uint4*)(w.p1 + blk * 16);
       const float d = __half2float(__ushort_as_half((uint16_t)(meta.x & 0xffff)));
       const float dmin = __half2float(__ushort_as_half((uint16_t)(meta.x >> 16)));
-      uint8_t sc8[12];
-      *(uint32_t*)&sc8[0] = meta.y;
-      *(uint32_t*)&sc8[4] = meta.z;
-      *(uint32_t*)&sc8[8] = meta.w;
-      int sc, m;
-      kq_scale_min(2 * g + hi, sc8, sc, m);
+      const uint32_t f = kq_field(meta.y, meta.z, meta.w, g);
+      const int sc = (f >> (6 * hi)) & 63, m = (f >> (12 + 6 * hi)) & 63;
       const float ds = d * sc, dm = dmin * m;
       const uint4 q = *(const uint4*)(w.p0 + blk * 128 + 32 * g + i0);
       uint4 qh = make_uint4(0, 0, 0, 0);
@@ -63,7 +59,7 @@ __device__ __forceinline__ void dequant16(const QWeight& w, int row, int k0, uin
       const int l = 2 * g + (i0 >> 4);
       const uint4 q = *(const uint4*)(w.p0 + blk * 128 + 32 * g + i0);
       const uint32_t hv = *(const uint32_t*)(w.p1 + blk * 64 + l * 8 + 4 * hi);
-      const int8_t s = *(const int8_t*)(w.p2 + blk * 16 + (kk >> 4));
+      const int8_t s = *(const int8_t*)(w.p2 + blk * 16 + 2 * l + hi);
       const float d = __half2float(__ushort_as_half(*(const uint16_t*)(w.p3 + blk * 2))) * (float)s;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {

@@ -153,7 +153,7 @@ __device__ __forceinline__ void q8_load(const SegRs& w, int row, int c, RawChunk
       const auto h = __builtin_amdgcn_raw_buffer_load_b64(w.r1, c * 8, blk0 * 64, LD_NT);
       r.b.x = h[0];
       r.b.y = h[1];
-      r.c = bl16(w.r2, (c >> 3) * 16, blk0 * 16);
+      r.c.x = __builtin_amdgcn_raw_buffer_load_b16(w.r2, c * 2, blk0 * 16, LD_NT);  // chunk's scale pair
       r.d = __builtin_amdgcn_raw_buffer_load_b16(w.r3, (c >> 3) * 2, blk0 * 2, LD_NT);
     } else {
       r.b = bl16(w.r1, (c >> 3) * 16, blk0 * 16);
@@ -196,84 +196,111 @@ __device__ __forceinline__ int dpp_xor1_i(int v) { return __builtin_amdgcn_mov_d
 // two octets of a 16-run their code sums.  Writes int8 codes in QT's chunk order and per run
 // {dx, dx*sum(codes)}; per-wave partial sums of squares go to red[wave][b].
 // ---------------------------------------------------------------------------------------------
-struct StagePre {  // x (and norm weight) of a thread's first octet, loaded before the weights
-  float4 x0, x1, g0, g1;
+// x passes loaded ahead of the weights: NPF = ceil(B*K/8 / 512) for the shapes a kernel serves
+// (1 for K <= 4096 at B = 1; 4 for the long-K down projection, K <= 16384)
+template <int NPF>
+struct StagePre {
+  float4 x0[NPF], x1[NPF], g0, g1;
 };
-__device__ __forceinline__ void q8_stage_prefetch(const GemvArgs& a, StagePre& pf) {
-  const int noct = a.K >> 3, t = threadIdx.x;
-  if (t < a.B * noct) {
-    const int b = t / noct, o = t - b * noct;
+template <int NPF>
+__device__ __forceinline__ void q8_stage_prefetch(const GemvArgs& a, StagePre<NPF>& pf) {
+  const int noct = a.K >> 3, total = a.B * noct;
+#pragma unroll
+  for (int i = 0; i < NPF; ++i) {
+    const int t = threadIdx.x + i * blockDim.x;
+    // past the end: re-read octet 0 (in bounds, unused) -- no branch around the load
+    const int tt = t < total ? t : 0;
+    const int b = tt / noct, o = tt - b * noct;
     const float* src = a.x + (size_t)b * a.ldx + 8 * o;
-    pf.x0 = *(const float4*)src;
-    pf.x1 = *(const float4*)(src + 4);
-    if (a.norm_w) {
-      pf.g0 = *(const float4*)(a.norm_w + 8 * o);
-      pf.g1 = *(const float4*)(a.norm_w + 8 * o + 4);
+    pf.x0[i] = *(const float4*)src;
+    pf.x1[i] = *(const float4*)(src + 4);
+    if (i == 0) {
+      const float* g = a.norm_w ? a.norm_w + 8 * o : src;
+      pf.g0 = *(const float4*)g;
+      pf.g1 = *(const float4*)(g + 4);
     }
   }
 }
 
+// quantise one octet (t -> row b, octet o) of x (times the norm weight) into the staging layout
 template <int QT, int B>
-__device__ __forceinline__ void q8_stage(const GemvArgs& a, int8_t* xq, float2* ms, float* red, const StagePre& pf) {
+__device__ __forceinline__ void q8_octet(const GemvArgs& a, int b, int o, float4 f0, float4 f1, float4 g0, float4 g1,
+                                         int8_t* xq, float2* ms, float (&ssq)[B]) {
   using F_ = QFmt<QT>;
   constexpr int W = F_::W, R = F_::RUNS;
-  const int nch = a.K / W, noct = a.K >> 3, total = a.B * noct;
+  const int nch = a.K / W;
+  float v[8] = {f0.x, f0.y, f0.z, f0.w, f1.x, f1.y, f1.z, f1.w};
+  float s2 = 0.f;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) s2 = fmaf(v[i], v[i], s2);
+#pragma unroll
+  for (int bb = 0; bb < B; ++bb)
+    if (bb == b) ssq[bb] += s2;
+  if (a.norm_w) {
+    v[0] *= g0.x; v[1] *= g0.y; v[2] *= g0.z; v[3] *= g0.w;
+    v[4] *= g1.x; v[5] *= g1.y; v[6] *= g1.z; v[7] *= g1.w;
+  }
+  float am = 0.f;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) am = fmaxf(am, fabsf(v[i]));
+  am = fmaxf(am, dpp_xor1(am));
+  am = fmaxf(am, dpp_xor2(am));
+  const float dx = am * (1.f / 127.f);
+  const float inv = am > 0.f ? 127.f / am : 0.f;
+  uint32_t wq[2];
+  int isum = 0;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    uint32_t wv = 0;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int q = (int)rintf(v[4 * j + e] * inv);
+      isum += q;
+      wv |= ((uint32_t)(q & 0xff)) << (8 * e);
+    }
+    wq[j] = wv;
+  }
+  isum += dpp_xor1_i(isum);  // the other octet of this 16-run
+  const int quarter = o & 3;
+  int c, s0;
+  F_::run_pos(2 * (o >> 2) + (quarter >> 1), c, s0);
+  int piece = s0 >> 4;
+  if (W == 32) piece = (piece + (c >> 3)) & 1;
+  *(uint2*)(xq + ((size_t)b * nch + c) * W + 16 * piece + 8 * (quarter & 1)) = make_uint2(wq[0], wq[1]);
+  if (!(quarter & 1)) ms[((size_t)b * nch + c) * R + (s0 >> 4)] = make_float2(dx, dx * (float)isum);
+}
+
+template <int QT, int B, int NPF>
+__device__ __forceinline__ void q8_stage(const GemvArgs& a, int8_t* xq, float2* ms, float* red,
+                                         const StagePre<NPF>& pf) {
+  const int noct = a.K >> 3, total = a.B * noct;
   float ssq[B];
 #pragma unroll
   for (int b = 0; b < B; ++b) ssq[b] = 0.f;
-  for (int t = threadIdx.x; t < total; t += blockDim.x) {
-    const int b = t / noct, o = t - b * noct;
-    float4 f0, f1, g0, g1;
-    if (t == (int)threadIdx.x) {
-      f0 = pf.x0; f1 = pf.x1; g0 = pf.g0; g1 = pf.g1;
-    } else {
-      const float* src = a.x + (size_t)b * a.ldx + 8 * o;
-      f0 = *(const float4*)src;
-      f1 = *(const float4*)(src + 4);
-      if (a.norm_w) {
+  // the prefetched passes, fully unrolled so the prefetch registers never become an indexed array
+#pragma unroll
+  for (int i = 0; i < NPF; ++i) {
+    const int t = threadIdx.x + i * blockDim.x;
+    if (t < total) {
+      const int b = t / noct, o = t - b * noct;
+      float4 g0 = pf.g0, g1 = pf.g1;
+      if (i > 0 && a.norm_w) {
         g0 = *(const float4*)(a.norm_w + 8 * o);
         g1 = *(const float4*)(a.norm_w + 8 * o + 4);
       }
+      q8_octet<QT, B>(a, b, o, pf.x0[i], pf.x1[i], g0, g1, xq, ms, ssq);
     }
-    float v[8] = {f0.x, f0.y, f0.z, f0.w, f1.x, f1.y, f1.z, f1.w};
-    float s2 = 0.f;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) s2 = fmaf(v[i], v[i], s2);
-#pragma unroll
-    for (int bb = 0; bb < B; ++bb)
-      if (bb == b) ssq[bb] += s2;
+  }
+  for (int t = threadIdx.x + NPF * blockDim.x; t < total; t += blockDim.x) {
+    const int b = t / noct, o = t - b * noct;
+    const float* src = a.x + (size_t)b * a.ldx + 8 * o;
+    const float4 f0 = *(const float4*)src, f1 = *(const float4*)(src + 4);
+    float4 g0 = f0, g1 = f1;
     if (a.norm_w) {
-      v[0] *= g0.x; v[1] *= g0.y; v[2] *= g0.z; v[3] *= g0.w;
-      v[4] *= g1.x; v[5] *= g1.y; v[6] *= g1.z; v[7] *= g1.w;
+      g0 = *(const float4*)(a.norm_w + 8 * o);
+      g1 = *(const float4*)(a.norm_w + 8 * o + 4);
     }
-    float am = 0.f;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) am = fmaxf(am, fabsf(v[i]));
-    am = fmaxf(am, dpp_xor1(am));
-    am = fmaxf(am, dpp_xor2(am));
-    const float dx = am * (1.f / 127.f);
-    const float inv = am > 0.f ? 127.f / am : 0.f;
-    uint32_t wq[2];
-    int isum = 0;
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      uint32_t wv = 0;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int q = (int)rintf(v[4 * j + e] * inv);
-        isum += q;
-        wv |= ((uint32_t)(q & 0xff)) << (8 * e);
-      }
-      wq[j] = wv;
-    }
-    isum += dpp_xor1_i(isum);  // the other octet of this 16-run
-    const int quarter = o & 3;
-    int c, s0;
-    F_::run_pos(2 * (o >> 2) + (quarter >> 1), c, s0);
-    int piece = s0 >> 4;
-    if (W == 32) piece = (piece + (c >> 3)) & 1;
-    *(uint2*)(xq + ((size_t)b * nch + c) * W + 16 * piece + 8 * (quarter & 1)) = make_uint2(wq[0], wq[1]);
-    if (!(quarter & 1)) ms[((size_t)b * nch + c) * R + (s0 >> 4)] = make_float2(dx, dx * (float)isum);
+    q8_octet<QT, B>(a, b, o, f0, f1, g0, g1, xq, ms, ssq);
   }
   if (a.norm_w) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -285,21 +312,18 @@ __device__ __forceinline__ void q8_stage(const GemvArgs& a, int8_t* xq, float2* 
   }
 }
 
-// branch-free Q4_K/Q5_K 6-bit scale/min decode for the chunk's sub-block pair (g = (c&7)>>1)
+// Q4_K/Q5_K scale/min decode for the chunk's sub-block pair (g = (c&7)>>1): one funnel shift of
+// the repacked meta (qweight.h kq_field), four bit-field extracts
 __device__ __forceinline__ void kq_scales_bf(const RawChunk& r, int c, float* sc, float* of) {
-  const int g = (c & 7) >> 1, sh = 16 * (g & 1);
+  const int g = (c & 7) >> 1;
   const uint32_t dd = r.b.x;
   const float d = __half2float(__ushort_as_half((uint16_t)(dd & 0xffff)));
   const float dmin = __half2float(__ushort_as_half((uint16_t)(dd >> 16)));
-  const uint32_t w1 = r.b.y >> sh, w2 = r.b.z >> sh, w3 = r.b.w >> sh;
-  const uint32_t sc_lo = w1 & 0x3f3f, m_lo = w2 & 0x3f3f;
-  const uint32_t sc_hi = (w3 & 0x0f0f) | ((w1 >> 2) & 0x3030);
-  const uint32_t m_hi = ((w3 >> 4) & 0x0f0f) | ((w2 >> 2) & 0x3030);
-  const uint32_t scp = g < 2 ? sc_lo : sc_hi, mp = g < 2 ? m_lo : m_hi;
-  sc[0] = d * (float)(scp & 0xff);
-  sc[1] = d * (float)(scp >> 8);
-  of[0] = dmin * (float)(mp & 0xff);
-  of[1] = dmin * (float)(mp >> 8);
+  const uint32_t f = kq_field(r.b.y, r.b.z, r.b.w, g);
+  sc[0] = d * (float)(f & 63);
+  sc[1] = d * (float)((f >> 6) & 63);
+  of[0] = dmin * (float)((f >> 12) & 63);
+  of[1] = dmin * (float)((f >> 18) & 63);
 }
 
 template <int QT>
@@ -310,7 +334,7 @@ __device__ __forceinline__ void q8_scales_bf(const RawChunk& r, int c, float* sc
 
 template <int QT, int B, int U>
 __device__ __forceinline__ void q8_compute(const RawChunk (&raw)[U][GEMV_ROWS], int it, int nch, const int8_t* xq,
-                                           const float2* ms, float (&acc)[GEMV_ROWS][B]) {
+                                           const float2* ms, float (&acc)[GEMV_ROWS][B], int dbg = 0) {
   using F_ = QFmt<QT>;
   constexpr int W = F_::W, R = F_::RUNS;
   const int lane = threadIdx.x & 63;
@@ -321,12 +345,22 @@ __device__ __forceinline__ void q8_compute(const RawChunk (&raw)[U][GEMV_ROWS], 
     const int c = valid ? c0 : nch - 1;
     float sc[GEMV_ROWS][R], of[GEMV_ROWS][R];
 #pragma unroll
-    for (int r = 0; r < GEMV_ROWS; ++r) q8_scales_bf<QT>(raw[u][r], c, sc[r], of[r]);
+    for (int r = 0; r < GEMV_ROWS; ++r) {
+      if (dbg & 8) {  // microbenchmark: scale decode skipped
+#pragma unroll
+        for (int rr = 0; rr < R; ++rr) { sc[r][rr] = __int_as_float(raw[u][r].b.y | 0x3f000000); of[r][rr] = 0.5f; }
+      } else {
+        q8_scales_bf<QT>(raw[u][r], c, sc[r], of[r]);
+      }
+    }
 #pragma unroll
     for (int b = 0; b < B; ++b) {
       int xv[8];
       const int8_t* xc = xq + ((size_t)b * nch + c) * W;
-      if constexpr (W == 32) {
+      if (dbg & 4) {  // microbenchmark: x LDS reads skipped
+#pragma unroll
+        for (int i = 0; i < 8; ++i) xv[i] = c * 0x01010101 + i;
+      } else if constexpr (W == 32) {
         const int rot = (c >> 3) & 1;
         const uint4 p0 = *(const uint4*)(xc + 16 * rot);
         const uint4 p1 = *(const uint4*)(xc + 16 * (rot ^ 1));
@@ -341,7 +375,7 @@ __device__ __forceinline__ void q8_compute(const RawChunk (&raw)[U][GEMV_ROWS], 
       const float2* mp = ms + ((size_t)b * nch + c) * R;
 #pragma unroll
       for (int rr = 0; rr < R; ++rr) {
-        m[rr] = mp[rr];
+        m[rr] = (dbg & 4) ? make_float2(1.f, (float)c) : mp[rr];
         if (!valid) m[rr] = make_float2(0.f, 0.f);
       }
 #pragma unroll
@@ -527,7 +561,7 @@ __global__ void __launch_bounds__(Q8_WAVES * 64) gemv_q8_rows(GemvArgs a) {
         }
       return;
     }
-    q8_compute<QT, B, U>(cur, it, nch, xq, ms, acc);
+    q8_compute<QT, B, U>(cur, it, nch, xq, ms, acc, a.tune_dbg);
   };
   auto finish = [&](int p) {
     float s[B];
@@ -563,33 +597,42 @@ __global__ void __launch_bounds__(Q8_WAVES * 64) gemv_q8_rows(GemvArgs a) {
       for (int b = 0; b < B; ++b) acc[r][b] = 0.f;
   };
 
-  RawChunk bufA[U][GEMV_ROWS];
-  // walk pairs [p, pend) grid-stride; bufA already holds item (p, 0)
-  auto run = [&](auto tag, int p, int pend) {
+  RawChunk buf[PIPE][U][GEMV_ROWS];
+  auto& bufA = buf[0];
+  // walk pairs [p, pend) grid-stride; buf[0] already holds item (p, 0)
+  auto run = [&](auto tag, int p, int pend, int stride) {
     if (p >= pend) return;
-    if constexpr (PIPE == 2) {
-      // two register buffers, each reloaded right after it was consumed: while one item
-      // computes, the next one's loads (other buffer) stay in flight
-      RawChunk bufB[U][GEMV_ROWS];
-      auto advance = [&](int& pp, int& ii) {
-        if (++ii >= nit) { ii = 0; pp += stride; }
-      };
-      int pA = p, iA = 0, pB = p, iB = 0;
-      advance(pB, iB);
-      load(tag, pB, pend, iB, bufB);
-      while (true) {
-        compute(tag, iA, bufA);
-        if (iA == nit - 1) finish(pA);
-        pA = pB; iA = iB;
-        advance(pA, iA);
-        load(tag, pA, pend, iA, bufA);
-        if (pB >= pend) break;
-        compute(tag, iB, bufB);
-        if (iB == nit - 1) finish(pB);
-        pB = pA; iB = iA;
-        advance(pB, iB);
-        load(tag, pB, pend, iB, bufB);
-        if (pA >= pend) break;
+    if constexpr (PIPE >= 2) {
+      // PIPE register buffers in rotation, each reloaded right after it was consumed with the item
+      // PIPE-1 ahead of the one computing next: PIPE-1 items stay in flight during every compute
+      int pk[PIPE], ik[PIPE];
+      pk[0] = p;
+      ik[0] = 0;
+      int tp = p, ti = 0;  // most recently scheduled item
+#pragma unroll
+      for (int k = 1; k < PIPE; ++k) {
+        if (++ti >= nit) { ti = 0; tp += stride; }
+        pk[k] = tp;
+        ik[k] = ti;
+        load(tag, tp, pend, ti, buf[k]);
+      }
+      bool done = false;
+      while (!done) {
+#pragma unroll
+        for (int k = 0; k < PIPE; ++k) {
+          if (!done) {
+            if (pk[k] >= pend) {
+              done = true;
+            } else {
+              compute(tag, ik[k], buf[k]);
+              if (ik[k] == nit - 1) finish(pk[k]);
+              if (++ti >= nit) { ti = 0; tp += stride; }
+              pk[k] = tp;
+              ik[k] = ti;
+              load(tag, tp, pend, ti, buf[k]);
+            }
+          }
+        }
       }
     } else {
       int it = 0;
@@ -606,15 +649,23 @@ __global__ void __launch_bounds__(Q8_WAVES * 64) gemv_q8_rows(GemvArgs a) {
     }
   };
 
-  StagePre pf{};
-  q8_stage_prefetch(a, pf);                                // x first: its wait then does not cover the weights
-  load(FmtTag<QT0>{}, wid, np0, 0, bufA);                  // weight loads in flight during the prologue
-  if (!(a.tune_dbg & 1)) q8_stage<QT0, B>(a, xq, ms, red, pf);
-  __syncthreads();
-  run(FmtTag<QT0>{}, wid, np0);
-  if constexpr (MIXED) {
+  constexpr int NPF = (B == 1 && U >= 3) ? 4 : 1;
+  StagePre<NPF> pf{};
+  q8_stage_prefetch(a, pf);  // x first: its wait then does not cover the weights
+  if constexpr (!MIXED) {
+    load(FmtTag<QT0>{}, wid, npairs, 0, bufA);  // weight loads in flight during the prologue
+    if (!(a.tune_dbg & 1)) q8_stage<QT0, B, NPF>(a, xq, ms, red, pf);
+    __syncthreads();
+    run(FmtTag<QT0>{}, wid, npairs, stride);
+  } else {
+    // one loop per format (QT0 pairs, then the last segment's QT1 pairs): a wave-split version
+    // kept both formats' buffers live and spilled to scratch
+    load(FmtTag<QT0>{}, wid, np0, 0, bufA);
+    if (!(a.tune_dbg & 1)) q8_stage<QT0, B, NPF>(a, xq, ms, red, pf);
+    __syncthreads();
+    run(FmtTag<QT0>{}, wid, np0, stride);
     load(FmtTag<QT1>{}, np0 + wid, npairs, 0, bufA);
-    run(FmtTag<QT1>{}, np0 + wid, npairs);
+    run(FmtTag<QT1>{}, np0 + wid, npairs, stride);
   }
 }
 
@@ -653,8 +704,19 @@ bool launch_gemv_q8(GemvArgs a, hipStream_t st) {
     if constexpr (B == 1) {
       const int nch = a.K / QFmt<QT0>::W;
       int u = a.tune_u;
-      if (u <= 0 || u > 8) u = nch <= 512 ? (nch + 63) / 64 : 2;
+      if (u <= 0 || (u > 8 && u != 13 && u != 14 && u != 21 && u != 22 && u != 31)) {
+        // MI355X sweep (tools/gemv_probe.py --sweep): one chunk per lane per item for short K,
+        // except the mid-sized Q4_K/Q5_K projections; the whole K slice in flight for long K
+        // (U = 1 for the small/huge-N shapes won in the eager sweep but lost 2-3 % inside the
+        // captured decode step, so the whole-K-slice rule stays)
+        u = nch <= 512 ? (nch + 63) / 64 : 2;
+      }
       switch (u) {
+        case 13: launch_q8_rows<QT0, QT1, 1, 3, 2>(a, lds, st); break;  // tuning: U = 3/4 double-buffered
+        case 14: launch_q8_rows<QT0, QT1, 1, 4, 2>(a, lds, st); break;
+        case 21: launch_q8_rows<QT0, QT1, 1, 1, 3>(a, lds, st); break;  // tuning: triple / quad buffers
+        case 22: launch_q8_rows<QT0, QT1, 1, 2, 3>(a, lds, st); break;
+        case 31: launch_q8_rows<QT0, QT1, 1, 1, 4>(a, lds, st); break;
         case 1: launch_q8_rows<QT0, QT1, 1, 1, 2>(a, lds, st); break;
         case 2: launch_q8_rows<QT0, QT1, 1, 2, 2>(a, lds, st); break;
         case 3: launch_q8_rows<QT0, QT1, 1, 3, 1>(a, lds, st); break;

@@ -8,25 +8,34 @@
 
 namespace aios {
 
+// GGUF Q4_K/Q5_K {d, dmin, scales[12]} -> repacked meta (qweight.h kq_field)
+__device__ void write_kq_meta(const uint8_t* s, uint8_t* out) {
+  uint32_t f[4];
+  for (int g = 0; g < 4; ++g) {
+    int sc0, m0, sc1, m1;
+    kq_scale_min(2 * g, s + 4, sc0, m0);
+    kq_scale_min(2 * g + 1, s + 4, sc1, m1);
+    f[g] = (uint32_t)sc0 | ((uint32_t)sc1 << 6) | ((uint32_t)m0 << 12) | ((uint32_t)m1 << 18);
+  }
+  const uint32_t w[4] = {(uint32_t)s[0] | ((uint32_t)s[1] << 8) | ((uint32_t)s[2] << 16) | ((uint32_t)s[3] << 24),
+                         f[0] | (f[1] << 24), (f[1] >> 8) | (f[2] << 16), (f[2] >> 16) | (f[3] << 8)};
+  for (int k = 0; k < 16; ++k) out[k] = (uint8_t)(w[k >> 2] >> (8 * (k & 3)));
+}
+
 // one thread per block; byte-wise copies (load time only)
 __global__ void repack_kernel(int qt, const uint8_t* __restrict__ raw, size_t nblocks, uint8_t* p0, uint8_t* p1,
                               uint8_t* p2, uint8_t* p3) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nblocks) return;
   switch (qt) {
-    case QT_Q4_K: {
-      const uint8_t* s = raw + i * 144;
-      uint4* m = (uint4*)(p1 + i * 16);
-      uint32_t w[4];
-      for (int k = 0; k < 4; ++k) w[k] = s[4 * k] | (s[4 * k + 1] << 8) | (s[4 * k + 2] << 16) | ((uint32_t)s[4 * k + 3] << 24);
-      *m = make_uint4(w[0], w[1], w[2], w[3]);
-      for (int k = 0; k < 128; ++k) p0[i * 128 + k] = s[16 + k];
-    } break;
+    case QT_Q4_K:
     case QT_Q5_K: {
-      const uint8_t* s = raw + i * 176;
-      for (int k = 0; k < 16; ++k) p1[i * 16 + k] = s[k];
-      for (int k = 0; k < 32; ++k) p2[i * 32 + k] = s[16 + k];
-      for (int k = 0; k < 128; ++k) p0[i * 128 + k] = s[48 + k];
+      const bool q5 = qt == QT_Q5_K;
+      const uint8_t* s = raw + i * (q5 ? 176 : 144);
+      write_kq_meta(s, p1 + i * 16);
+      if (q5)
+        for (int k = 0; k < 32; ++k) p2[i * 32 + k] = s[16 + k];
+      for (int k = 0; k < 128; ++k) p0[i * 128 + k] = s[(q5 ? 48 : 16) + k];
     } break;
     case QT_Q6_K: {
       // re-ordered into the Q4_K chunk order (see qweight.h): 6-bit code q[k] -> low nibble in
@@ -54,7 +63,11 @@ __global__ void repack_kernel(int qt, const uint8_t* __restrict__ raw, size_t nb
           for (int bb = 0; bb < 4; ++bb) p1[i * 64 + l * 8 + 4 * half + bb] = (uint8_t)(hw >> (8 * bb));
         }
       }
-      for (int k = 0; k < 16; ++k) p2[i * 16 + k] = s[192 + k];  // int8 scale of k/16
+      for (int l = 0; l < 8; ++l) {  // chunk l = 2g+h: (run 0, run 1) scales = sc[4g+h], sc[4g+2+h]
+        const int g = l >> 1, h = l & 1;
+        p2[i * 16 + 2 * l] = s[192 + 4 * g + h];
+        p2[i * 16 + 2 * l + 1] = s[192 + 4 * g + 2 + h];
+      }
       p3[i * 2] = s[208];
       p3[i * 2 + 1] = s[209];
     } break;
@@ -93,8 +106,9 @@ __device__ float dq_elem(const QWeight& w, int row, int k) {
       const size_t blk = (size_t)row * nb + b;
       const uint8_t* meta = w.p1 + blk * 16;
       const float d = h2f(*(const uint16_t*)meta), dmin = h2f(*(const uint16_t*)(meta + 2));
-      int sc, m;
-      kq_scale_min(2 * g + hi, meta + 4, sc, m);
+      const uint32_t* mw = (const uint32_t*)meta;
+      const uint32_t f = kq_field(mw[1], mw[2], mw[3], g);
+      const int sc = (f >> (6 * hi)) & 63, m = (f >> (12 + 6 * hi)) & 63;
       const uint8_t byte = w.p0[blk * 128 + 32 * g + i];
       int q = hi ? (byte >> 4) : (byte & 0xF);
       if (w.qtype == QT_Q5_K) q += ((w.p2[blk * 32 + i] >> (2 * g + hi)) & 1) << 4;
@@ -110,7 +124,7 @@ __device__ float dq_elem(const QWeight& w, int row, int k) {
       const uint32_t hw = hp[0] | (hp[1] << 8) | (hp[2] << 16) | ((uint32_t)hp[3] << 24);
       const int q = (nib | (((hw >> (8 * e + 2 * j)) & 3) << 4)) - 32;
       const float d = h2f(*(const uint16_t*)(w.p3 + blk * 2));
-      return d * (float)((const int8_t*)(w.p2 + blk * 16))[kk >> 4] * q;
+      return d * (float)((const int8_t*)(w.p2 + blk * 16))[2 * l + hi] * q;
     }
     case QT_Q4_0: {
       const int nb = w.cols >> 5, b = k >> 5, j = k & 31;

@@ -48,6 +48,16 @@ __host__ __device__ constexpr bool kq_layout(int q) { return q == QT_Q4_K || q =
 template <int A, int B>
 constexpr bool same_xlayout = A == B || (kq_layout(A) && kq_layout(B));
 
+// Q4_K / Q5_K repacked block meta (16 B): word0 = {f16 d, f16 dmin}; words 1..3 hold a 96-bit
+// string of four 24-bit fields, field g = sc[2g] | sc[2g+1] << 6 | m[2g] << 12 | m[2g+1] << 18
+// (the 6-bit sub-block scales / mins of the 64-weight group g).  One funnel shift extracts the
+// four values a chunk needs -- the GGUF 12-byte packing needs a g-dependent bit shuffle instead.
+__device__ __forceinline__ uint32_t kq_field(uint32_t w1, uint32_t w2, uint32_t w3, int g) {
+  const uint32_t lo = g < 2 ? w1 : (g == 2 ? w2 : w3);
+  const uint32_t hi = g < 2 ? w2 : w3;
+  return __builtin_amdgcn_alignbit(hi, lo, (24 * g) & 31);
+}
+
 __device__ __forceinline__ uint32_t u4_word(const uint4& v, int i) {
   return i == 0 ? v.x : (i == 1 ? v.y : (i == 2 ? v.z : v.w));
 }
@@ -77,16 +87,8 @@ struct QFmt<QT_Q4_K> {
     const uint32_t dd = r.b.x;
     const float d = __half2float(__ushort_as_half((uint16_t)(dd & 0xffff)));
     const float dmin = __half2float(__ushort_as_half((uint16_t)(dd >> 16)));
-    const uint32_t w1 = r.b.y, w2 = r.b.z, w3 = r.b.w;  // scales[0..3], [4..7], [8..11]
-    const int sh = 16 * (g & 1);
-    uint32_t scp, mp;
-    if (g < 2) {
-      scp = (w1 >> sh) & 0x3f3f;
-      mp = (w2 >> sh) & 0x3f3f;
-    } else {
-      scp = ((w3 >> sh) & 0x0f0f) | (((w1 >> sh) >> 2) & 0x3030);
-      mp = (((w3 >> sh) >> 4) & 0x0f0f) | (((w2 >> sh) >> 2) & 0x3030);
-    }
+    const uint32_t f = kq_field(r.b.y, r.b.z, r.b.w, g);
+    const uint32_t scp = (f & 63) | (((f >> 6) & 63) << 8), mp = ((f >> 12) & 63) | (((f >> 18) & 63) << 8);
     sc[0] = d * (float)(scp & 0xff);
     sc[1] = d * (float)(scp >> 8);
     of[0] = dmin * (float)(mp & 0xff);
@@ -144,7 +146,7 @@ struct QFmt<QT_Q5_K> {
 // mixed Q4_K_M QKV segment list (V in Q6_K) needs ONE activation layout:
 //   p0 = low nibbles exactly where Q4_K keeps its 4-bit codes,
 //   p1 = 8 B per chunk {h0, h1}: bits (8e + 2j)..+1 of h_run = high 2 bits of weight 4j+e of the run,
-//   p2 = the 16 int8 scales (scale of k is sc[k/16]),  p3 = f16 d.
+//   p2 = the 16 int8 scales re-ordered so chunk l's pair is bytes (2l, 2l+1),  p3 = f16 d.
 template <>
 struct QFmt<QT_Q6_K> {
   static constexpr int W = 32, RUNS = 2, CHUNKS_PER_BLOCK = 8, BLOCK = 256;
@@ -158,14 +160,11 @@ struct QFmt<QT_Q6_K> {
     const uint2 h = *(const uint2*)(w.p1 + ch * 8);
     r.b.x = h.x;
     r.b.y = h.y;
-    r.c = *(const uint4*)(w.p2 + blk * 16);
+    r.c.x = *(const uint16_t*)(w.p2 + ch * 2);  // this chunk's (run 0, run 1) int8 scale pair
     r.d = *(const uint16_t*)(w.p3 + blk * 2);
   }
-  __device__ static void sc_idx(int c, int& s_lo, int& s_hi) {
-    const int l = c & 7;
-    s_lo = 4 * (l >> 1) + (l & 1);
-    s_hi = s_lo + 2;
-  }
+  __device__ static float sc_lo(const RawChunk& r) { return (float)(int8_t)(r.c.x & 0xff); }
+  __device__ static float sc_hi(const RawChunk& r) { return (float)(int8_t)((r.c.x >> 8) & 0xff); }
   __device__ static uint32_t code_lo(const RawChunk& r, int i) {
     return (u4_word(r.a, i) & 0x0f0f0f0fu) | (((r.b.x >> (2 * i)) & 0x03030303u) << 4);
   }
@@ -173,11 +172,9 @@ struct QFmt<QT_Q6_K> {
     return ((u4_word(r.a, i) >> 4) & 0x0f0f0f0fu) | (((r.b.y >> (2 * i)) & 0x03030303u) << 4);
   }
   __device__ static void decode(const RawChunk& r, int c, float q[32], float sc[2], float of[2]) {
-    int s_lo, s_hi;
-    sc_idx(c, s_lo, s_hi);
     const float d = __half2float(__ushort_as_half((uint16_t)r.d));
-    sc[0] = d * (float)(int8_t)((u4_word(r.c, s_lo >> 2) >> (8 * (s_lo & 3))) & 0xff);
-    sc[1] = d * (float)(int8_t)((u4_word(r.c, s_hi >> 2) >> (8 * (s_hi & 3))) & 0xff);
+    sc[0] = d * sc_lo(r);
+    sc[1] = d * sc_hi(r);
     of[0] = 32.f * sc[0];  // q - 32 folded as -32*sc*sum(x)
     of[1] = 32.f * sc[1];
 #pragma unroll
@@ -320,20 +317,11 @@ struct QStream<QT_Q4_K> {
     const uint32_t dd = r.b.x;
     const float d = __half2float(__ushort_as_half((uint16_t)(dd & 0xffff)));
     const float dmin = __half2float(__ushort_as_half((uint16_t)(dd >> 16)));
-    const uint32_t w1 = r.b.y, w2 = r.b.z, w3 = r.b.w;
-    const int sh = 16 * (g & 1);
-    uint32_t scp, mp;
-    if (g < 2) {
-      scp = (w1 >> sh) & 0x3f3f;
-      mp = (w2 >> sh) & 0x3f3f;
-    } else {
-      scp = ((w3 >> sh) & 0x0f0f) | (((w1 >> sh) >> 2) & 0x3030);
-      mp = (((w3 >> sh) >> 4) & 0x0f0f) | (((w2 >> sh) >> 2) & 0x3030);
-    }
-    sc[0] = d * (float)(scp & 0xff);
-    sc[1] = d * (float)(scp >> 8);
-    of[0] = dmin * (float)(mp & 0xff);
-    of[1] = dmin * (float)(mp >> 8);
+    const uint32_t f = kq_field(r.b.y, r.b.z, r.b.w, g);
+    sc[0] = d * (float)(f & 63);
+    sc[1] = d * (float)((f >> 6) & 63);
+    of[0] = dmin * (float)((f >> 12) & 63);
+    of[1] = dmin * (float)((f >> 18) & 63);
   }
   // j in 0..7: j<4 -> low nibbles of word j (run 0), j>=4 -> high nibbles of word j-4 (run 1)
   __device__ static void quad(const RawChunk& r, int c, int j, float q[4]) {
@@ -359,11 +347,9 @@ struct QStream<QT_Q5_K> {
 template <>
 struct QStream<QT_Q6_K> {
   __device__ static void scales(const RawChunk& r, int c, float* sc, float* of) {
-    int s_lo, s_hi;
-    QFmt<QT_Q6_K>::sc_idx(c, s_lo, s_hi);
     const float d = __half2float(__ushort_as_half((uint16_t)r.d));
-    sc[0] = d * (float)(int8_t)((u4_word(r.c, s_lo >> 2) >> (8 * (s_lo & 3))) & 0xff);
-    sc[1] = d * (float)(int8_t)((u4_word(r.c, s_hi >> 2) >> (8 * (s_hi & 3))) & 0xff);
+    sc[0] = d * QFmt<QT_Q6_K>::sc_lo(r);
+    sc[1] = d * QFmt<QT_Q6_K>::sc_hi(r);
     of[0] = 32.f * sc[0];
     of[1] = 32.f * sc[1];
   }

@@ -22,6 +22,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--json", default=None)
     ap.add_argument("--u", type=int, default=0)
+    ap.add_argument("--sweep", action="store_true", help="U x blocks-per-CU sweep per shape")
     args = ap.parse_args()
     E = native.require()
     st = torch.cuda.current_stream().cuda_stream
@@ -38,7 +39,7 @@ def main():
             y = torch.zeros(1, N, device="cuda")
             nbytes = N * K // 256 * BLOCK_INFO[t][1]
             line = []
-            for dbg in (0, 1, 2, 3):
+            for dbg in (0, 1, 2, 3, 4, 8, 12):
                 us = time_fn(lambda: E.gemv([m], 1, x.data_ptr(), K, nw.data_ptr() if norm else 0, 1e-5, y.data_ptr(),
                                             N, E.EPI_STORE, st, 0, 1, 0, args.u, 0, dbg), reps=100)
                 res.append(dict(fmt=t.name, shape=name, dbg=dbg, us=round(us, 2), tb_s=round(nbytes / us / 1e6, 2)))
@@ -61,6 +62,29 @@ def main():
         res.append(dict(fmt="Q4_K+Q6_K", shape="qkv_mixed", dbg=dbg, us=round(us, 2)))
         line.append(f"dbg{dbg} {us:6.2f}us {nbytes / us / 1e6:4.2f}TB/s")
     print(f"Q4K+Q6K qkv_mix N=  6144 K=  4096 {nbytes / 1e6:6.1f}MB | " + " | ".join(line), flush=True)
+    if args.sweep:
+        for t in (GGMLType.Q4_K, GGMLType.Q6_K):
+            for name, N, K, norm in shapes:
+                raw = np.zeros(BLOCK_INFO[t][1] * N * K // 256, dtype=np.uint8)
+                m = E.QMatrix(int(t), N, K, raw)
+                m.fill_random(1, 0.02)
+                x = torch.randn(1, K, device="cuda")
+                nw = torch.ones(K, device="cuda")
+                y = torch.zeros(1, N, device="cuda")
+                cells = []
+                for u in list(range(1, 9)) + [13, 14, 21, 22, 31]:
+                    uu = {13: 3, 14: 4, 21: 1, 22: 2, 31: 1}.get(u, u)
+                    if (K // 32 + 64 * uu - 1) // (64 * uu) > 4:
+                        continue
+                    for g in (1, 2, 3, 4):
+                        us = time_fn(lambda: E.gemv([m], 1, x.data_ptr(), K, nw.data_ptr() if norm else 0, 1e-5,
+                                                    y.data_ptr(), N, E.EPI_STORE, st, 0, 1, g, u, 0, 0), reps=60)
+                        cells.append((us, u, g))
+                        res.append(dict(fmt=t.name, shape=name, sweep_u=u, sweep_grid=g, us=round(us, 2)))
+                cells.sort()
+                print(f"sweep {t.name} {name}: best " + ", ".join(f"u{u}/g{g} {us:.2f}us" for us, u, g in cells[:4]),
+                      flush=True)
+                del m
     # pure launch/boundary floor for reference
     for blocks in (256, 1024):
         print(f"empty-chain eager blocks={blocks}: {E.bench_launch_chain(200, blocks, 0, 20):.2f} us/kernel")
