@@ -99,6 +99,63 @@ def build(verbose: bool = True, jobs: int | None = None) -> Path:
     return out
 
 
+# ------------------------------------------------------------------------------ control-plane core
+NATIVE = PKG / "native"
+
+
+def core_target_path() -> Path:
+    return PKG / ("_core" + ext_suffix())
+
+
+def _sqlite_lib() -> str:
+    for c in ("/lib/x86_64-linux-gnu/libsqlite3.so.0", "/usr/lib/x86_64-linux-gnu/libsqlite3.so.0",
+              "/usr/lib64/libsqlite3.so.0"):
+        if os.path.exists(c):
+            return c
+    raise RuntimeError("libsqlite3.so.0 not found")
+
+
+def build_core(verbose: bool = True, jobs: int | None = None) -> Path:
+    """Host-only C++17 build of aios_amd/native (tools / memory / orchestrator cores + bindings)
+    into `aios_amd/_core*.so`, linked against the system libsqlite3 and OpenSSL libcrypto."""
+    import pybind11
+
+    cxx = os.environ.get("CXX") or shutil.which("g++") or "g++"
+    out_dir = ROOT / "build" / "core"
+    out_dir.mkdir(parents=True, exist_ok=True)
+    flags = ["-std=c++17", "-O2", "-fPIC", "-fvisibility=hidden", "-Wall", "-Wno-unused-function",
+             f"-I{NATIVE}", f"-I{pybind11.get_include()}", f"-I{sysconfig.get_paths()['include']}"]
+    srcs = sorted(NATIVE.glob("*.cpp"))
+    hdrs = list(NATIVE.glob("*.h"))
+
+    def comp(src: Path) -> Path:
+        obj = out_dir / (src.stem + ".o")
+        newest = max([src.stat().st_mtime] + [h.stat().st_mtime for h in hdrs])
+        if obj.exists() and obj.stat().st_mtime >= newest:
+            return obj
+        r = subprocess.run([cxx, *flags, "-c", str(src), "-o", str(obj)], capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"c++ failed for {src.name}:\n{r.stderr[-6000:]}")
+        return obj
+
+    jobs = jobs or min(len(srcs), max(1, (os.cpu_count() or 4)), 16)
+    with cf.ThreadPoolExecutor(jobs) as ex:
+        objs = list(ex.map(comp, srcs))
+    out = core_target_path()
+    newest = max(o.stat().st_mtime for o in objs)
+    if not out.exists() or out.stat().st_mtime < newest:
+        tmp = out.with_suffix(".tmp.so")
+        cmd = [cxx, "-shared", "-fPIC", "-o", str(tmp), *map(str, objs), _sqlite_lib(), "-lcrypto", "-lpthread"]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"core link failed:\n{r.stderr[-6000:]}")
+        os.replace(tmp, out)
+    if verbose:
+        print(f"[aios_amd] control-plane core: {out} ({out.stat().st_size / 1e6:.1f} MB)")
+    return out
+
+
 if __name__ == "__main__":
     build()
+    build_core()
     sys.exit(0)
