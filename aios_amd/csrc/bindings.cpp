@@ -6,6 +6,7 @@
 
 #include <cstring>
 
+#include "comm.h"
 #include "engine.h"
 #include "grammar.h"
 #include "ops.h"
@@ -196,7 +197,31 @@ PYBIND11_MODULE(_engine, m) {
       .def_property_readonly("v_cache_ptr", &Engine::kv_cache_v)
       .def("set_allreduce_ptr", [](Engine& e, uintptr_t fn, uintptr_t ctx) {
         e.set_allreduce(reinterpret_cast<AllReduceFn>(fn), reinterpret_cast<void*>(ctx));
+      })
+      .def("set_comm", [](Engine& e, XgmiComm& c) {
+        // the comm must outlive the engine's use of it (the Python wrapper keeps a reference)
+        e.set_allreduce(&XgmiComm::hook, &c);
       });
+
+  // ------------------------------------------------------------------ TP collectives (xGMI)
+  py::class_<XgmiComm>(m, "XgmiComm")
+      .def(py::init<int, int, int, size_t>(), py::arg("rank"), py::arg("world"), py::arg("device"),
+           py::arg("cap_floats"))
+      .def("ipc_handle", [](const XgmiComm& c) { return py::bytes(c.ipc_handle()); })
+      .def("connect", [](XgmiComm& c, const std::vector<py::bytes>& hs) {
+        std::vector<std::string> v;
+        for (auto& h : hs) v.push_back(std::string(h));
+        c.connect(v);
+      })
+      .def("allreduce", [](XgmiComm& c, uintptr_t data, size_t n, uintptr_t residual, uintptr_t st) {
+        c.allreduce((float*)data, n, (float*)residual, S(st));
+      }, py::arg("data"), py::arg("n"), py::arg("residual") = 0, py::arg("stream") = 0)
+      .def("error", &XgmiComm::error)
+      .def("reset_error", &XgmiComm::reset_error)
+      .def_property_readonly("rank", &XgmiComm::rank)
+      .def_property_readonly("world", &XgmiComm::world)
+      .def_property_readonly("capacity", &XgmiComm::capacity)
+      .def_property_readonly("connected", &XgmiComm::connected);
 
   // ------------------------------------------------------------------ raw ops (tests / tools)
   py::class_<PyQMatrix>(m, "QMatrix")

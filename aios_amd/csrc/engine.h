@@ -61,8 +61,9 @@ struct LayerW {
   QMat wq, wk, wv, wo, wgu, wdown;
 };
 
-// all-reduce hook (TP): sum `n` floats in place on `stream`; installed by parallel/comm.
-using AllReduceFn = void (*)(void* ctx, float* data, size_t n, hipStream_t stream);
+// all-reduce hook (TP): sum `n` floats of `data` over the TP ranks on `stream` and add the
+// total into `residual` (or into `data` when residual is null); installed by aios_amd/parallel.
+using AllReduceFn = void (*)(void* ctx, float* data, size_t n, float* residual, hipStream_t stream);
 
 class Engine {
  public:
@@ -126,7 +127,7 @@ class Engine {
   float* upload_f32(const void* host, size_t n, int qt);
   QMat interleave_rows(const QMat& a, const QMat& b);
   void* dmalloc(size_t bytes);
-  void allreduce(float* p, size_t n);
+  void allreduce(float* p, size_t n, float* residual);
 
   EngineConfig cfg_;
   hipStream_t stream_ = nullptr;

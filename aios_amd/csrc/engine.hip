@@ -411,10 +411,12 @@ void Engine::finalize() {
   finalized_ = true;
 }
 
-void Engine::allreduce(float* p, size_t n) {
+// TP: sum the row-parallel partials in `p` over the ranks and add the total into `residual`
+// (one fused launch: xGMI one-shot all-reduce + residual add, aios_amd/csrc/comm.h)
+void Engine::allreduce(float* p, size_t n, float* residual) {
   if (cfg_.tp_size > 1) {
     if (!allreduce_) throw std::runtime_error("tensor-parallel engine without an all-reduce hook");
-    allreduce_(allreduce_ctx_, p, n, stream_);
+    allreduce_(allreduce_ctx_, p, n, residual, stream_);
   }
 }
 
@@ -531,8 +533,7 @@ void Engine::layer_decode(int l, int B) {
   // ---- O projection (+ residual; TP: partial -> all-reduce -> add)
   if (cfg_.tp_size > 1) {
     gemv({&L.wo}, d, qd, B, attn_, qd, nullptr, ff_, d, EPI_STORE, l);
-    allreduce(ff_, (size_t)B * d);
-    launch_add(x_, ff_, (size_t)B * d, stream_);
+    allreduce(ff_, (size_t)B * d, x_);
   } else {
     gemv({&L.wo}, d, qd, B, attn_, qd, nullptr, x_, d, EPI_RESID, l);
   }
@@ -541,8 +542,7 @@ void Engine::layer_decode(int l, int B) {
   // ---- down (+ residual)
   if (cfg_.tp_size > 1) {
     gemv({&L.wdown}, d, cfg_.d_ff, B, ff_, cfg_.d_ff, nullptr, attn_, d, EPI_STORE, l);
-    allreduce(attn_, (size_t)B * d);
-    launch_add(x_, attn_, (size_t)B * d, stream_);
+    allreduce(attn_, (size_t)B * d, x_);
   } else {
     gemv({&L.wdown}, d, cfg_.d_ff, B, ff_, cfg_.d_ff, nullptr, x_, d, EPI_RESID, l);
   }
@@ -669,8 +669,7 @@ std::vector<float> Engine::prefill(int slot, const std::vector<int>& tokens, int
           }
         }
         if (cfg_.tp_size > 1) {
-          allreduce(fb, (size_t)n * d);
-          launch_add(xb, fb, (size_t)n * d, stream_);
+          allreduce(fb, (size_t)n * d, xb);
         }
         for (int sb = 0; sb < nsub; ++sb) {
           const int o = sb * 8, bn = std::min(8, n - o);
@@ -690,8 +689,7 @@ std::vector<float> Engine::prefill(int slot, const std::vector<int>& tokens, int
           }
         }
         if (cfg_.tp_size > 1) {
-          allreduce(ab, (size_t)n * d);
-          launch_add(xb, ab, (size_t)n * d, stream_);
+          allreduce(ab, (size_t)n * d, xb);
         }
       }
       x_ = xb; q_ = qb; qkv_ = qkvb; attn_ = ab; ff_ = fb;

@@ -133,6 +133,11 @@ PRESETS: Dict[str, ModelConfig] = {
     "test-small": ModelConfig(
         name="test-small", vocab_size=1024, d_model=512, n_layers=3, n_heads=8, n_kv_heads=2,
         head_dim=64, d_ff=1536, rope_theta=10000.0, max_ctx=512),
+    # smallest llama-3-style shape that shards over TP=2/4/8 in whole Q4_K blocks (8 KV heads,
+    # q_dim/8 and d_ff/8 multiples of 256) -- the TP tests' stand-in for Llama-3-70B
+    "test-tp8-shape": ModelConfig(
+        name="test-tp8-shape", vocab_size=1024, d_model=2048, n_layers=2, n_heads=16, n_kv_heads=8,
+        head_dim=128, d_ff=4096, rope_theta=5e5, max_ctx=512),
     "test-mistral-shape": ModelConfig(
         name="test-mistral-shape", vocab_size=1024, d_model=1024, n_layers=2, n_heads=8, n_kv_heads=2,
         head_dim=128, d_ff=2048, rope_theta=1e6, max_ctx=512, chat_template="mistral"),
