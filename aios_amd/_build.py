@@ -155,7 +155,31 @@ def build_core(verbose: bool = True, jobs: int | None = None) -> Path:
     return out
 
 
+def initd_target_path() -> Path:
+    return PKG / "bin" / "aios-init"
+
+
+def build_initd(verbose: bool = True) -> Path:
+    """Static-ish C++17 build of the init / supervisor daemon (aios_amd/native/initd)."""
+    cxx = os.environ.get("CXX") or shutil.which("g++") or "g++"
+    out = initd_target_path()
+    out.parent.mkdir(parents=True, exist_ok=True)
+    srcs = [NATIVE / "initd" / "initd.cpp", NATIVE / "json.cpp"]
+    deps = srcs + [NATIVE / "json.h"]
+    if not out.exists() or out.stat().st_mtime < max(d.stat().st_mtime for d in deps):
+        tmp = out.with_suffix(".tmp")
+        r = subprocess.run([cxx, "-std=c++17", "-O2", "-Wall", f"-I{NATIVE}", "-o", str(tmp), *map(str, srcs),
+                            "-lpthread"], capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"aios-init build failed:\n{r.stderr[-6000:]}")
+        os.replace(tmp, out)
+    if verbose:
+        print(f"[aios_amd] init daemon: {out}")
+    return out
+
+
 if __name__ == "__main__":
     build()
     build_core()
+    build_initd()
     sys.exit(0)
