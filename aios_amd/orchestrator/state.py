@@ -25,6 +25,8 @@ core = load_core()
 
 LEVEL_ROUNDS = {"reactive": 1, "operational": 1, "tactical": 3, "strategic": 5}
 LEVEL_TOKENS = {"reactive": 2048, "operational": 2048, "tactical": 8192, "strategic": 16384}
+# token cap of the one decomposition call (task_planner.rs:163-218 asks for <= 1024)
+PLAN_MAX_TOKENS = int(os.environ.get("AIOS_PLAN_MAX_TOKENS", "1024"))
 
 
 class OrchestratorState:
@@ -64,7 +66,7 @@ class OrchestratorState:
         tasks: List[dict] = []
         if level in ("tactical", "strategic"):
             r = await self.clients.infer_any(core.planner.ai_decomposition_prompt(description),
-                                             core.planner.DECOMPOSE_SYSTEM_PROMPT, 1024, level="tactical",
+                                             core.planner.DECOMPOSE_SYSTEM_PROMPT, PLAN_MAX_TOKENS, level="tactical",
                                              task_id=goal_id)
             if r is not None and r.success:
                 tasks = core.planner.parse_ai_decomposition(r.text, goal_id, level)

@@ -50,32 +50,29 @@ def create_comm(rank: int, world: int, device: int, cap_floats: int, group=None)
 class TPEngine:
     """Leader-side proxy: forwards each engine call to the workers, then runs it locally.
 
-    Workers block in `worker_loop`; `close()` releases them.  Attribute reads (config,
-    weight_bytes, ...) are served from the local shard."""
+    `send` broadcasts one command tuple to every worker: a gloo group (torchrun tools / tests) or
+    the loopback LeaderChannel (runtime daemon, channel.py).  Workers block in `worker_loop`;
+    `close()` releases them.  Attribute reads (config, weight_bytes, ...) come from the local
+    shard."""
 
-    _FORWARD = {"prefill", "decode", "resample", "last_logits", "decode_loop_prepare", "decode_loop_run",
-                "decode_loop_history", "synchronize", "reset_graphs", "copy_slot"}
+    _FORWARD = frozenset({"prefill", "decode", "resample", "last_logits", "decode_loop_prepare",
+                          "decode_loop_run", "decode_loop_history", "synchronize", "reset_graphs", "copy_slot"})
 
-    def __init__(self, engine, comm, group=None):
+    def __init__(self, engine, comm, group=None, send=None, on_close=None):
         self._eng = engine
         self._comm = comm
-        self._group = group
+        self._send = send or (lambda msg: _dist_bcast(msg, group))
+        self._on_close = on_close
         self._closed = False
-
-    def _bcast(self, msg):
-        import torch.distributed as dist
-
-        obj = [msg]
-        dist.broadcast_object_list(obj, src=0, group=self._group)
 
     def __getattr__(self, name):
         attr = getattr(self._eng, name)
         if name not in self._FORWARD or not callable(attr):
             return attr
 
-        def call(*args, **kw):
-            self._bcast((name, args, kw))
-            out = attr(*args, **kw)
+        def call(*args):
+            self._send([name, list(args)])
+            out = attr(*args)
             if self._comm.error():
                 raise RuntimeError("TP all-reduce timed out (a rank stopped participating)")
             return out
@@ -84,20 +81,37 @@ class TPEngine:
     def close(self):
         if not self._closed:
             self._closed = True
-            self._bcast(("__exit__", (), {}))
+            self._send(["__exit__", []])
+            if self._on_close:
+                self._on_close()
 
 
-def worker_loop(engine, comm, group=None):
-    """Ranks 1..N-1: execute the leader's engine calls until it sends __exit__."""
+def _dist_bcast(msg, group):
     import torch.distributed as dist
 
+    obj = [msg]
+    dist.broadcast_object_list(obj, src=0, group=group)
+
+
+def _dist_recv(group):
+    import torch.distributed as dist
+
+    obj = [None]
+    dist.broadcast_object_list(obj, src=0, group=group)
+    return obj[0]
+
+
+def worker_loop(engine, comm, group=None, recv=None):
+    """Ranks 1..N-1: execute the leader's engine calls (whitelisted) until it sends __exit__."""
+    recv = recv or (lambda: _dist_recv(group))
     while True:
-        obj = [None]
-        dist.broadcast_object_list(obj, src=0, group=group)
-        name, args, kw = obj[0]
+        name, args = recv()
         if name == "__exit__":
             return
-        getattr(engine, name)(*args, **kw)
+        if name not in TPEngine._FORWARD:
+            log.error("TP worker: refusing unknown command %r", name)
+            continue
+        getattr(engine, name)(*args)
         if comm.error():
             log.error("TP all-reduce timed out on this worker")
 
@@ -130,3 +144,83 @@ def local_device(local_rank: int) -> int:
 def env_rank_world():
     return int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1")), \
         int(os.environ.get("LOCAL_RANK", "0"))
+
+
+# ------------------------------------------------------------------------------ runtime launcher
+def parse_spec(path: str):
+    """'synthetic:<preset>[:<recipe>]#tp=N&q8=0' or '<file.gguf>#tp=N' -> (base, tp, act_q8).
+    q8=0 selects fp32 activations in the GEMVs (int8 activations are the default)."""
+    base, _, frag = path.partition("#")
+    tp, q8 = 1, True
+    for kv in filter(None, frag.split("&")):
+        k, _, v = kv.partition("=")
+        if k == "tp":
+            tp = int(v)
+        elif k == "q8":
+            q8 = v not in ("0", "false", "no")
+    return base, tp, q8
+
+
+def _shard(spec: str, rank: int, world: int, device: int, max_ctx: int, max_slots: int, max_batch: int, seed: int,
+           act_q8: bool = True):
+    from ..models.config import get_preset
+    from ..runtime.loader import load_engine, random_engine
+
+    if spec.startswith("synthetic:"):
+        parts = spec.split(":")
+        cfg = get_preset(parts[1])
+        eng = random_engine(cfg, parts[2] if len(parts) > 2 else "Q4_K_M", seed=seed, max_ctx=max_ctx,
+                            max_slots=max_slots, max_batch=max_batch, device=device, tp_rank=rank, tp_size=world,
+                            act_q8=act_q8)
+        return eng, cfg
+    eng, cfg, _ = load_engine(spec, max_ctx=max_ctx, max_slots=max_slots, max_batch=max_batch, device=device,
+                              tp_rank=rank, tp_size=world, act_q8=act_q8)
+    return eng, cfg
+
+
+def launch_tp(spec: str, world: int, devices, max_ctx: int, max_slots: int, max_batch: int, seed: int = 0,
+              act_q8: bool = True):
+    """Runtime-side TP model: spawn ranks 1..N-1 as worker processes (python -m
+    aios_amd.parallel.worker), build rank 0 here, exchange IPC handles over the channel.
+    Returns (TPEngine, cfg)."""
+    import subprocess
+    import sys
+
+    from ..runtime import native
+    from .channel import LeaderChannel
+
+    devices = list(devices) or [0]
+    ch = LeaderChannel(world)
+    procs = []
+    for r in range(1, world):
+        env = dict(os.environ, AIOS_TP_TOKEN=ch.token)
+        procs.append(subprocess.Popen([sys.executable, "-m", "aios_amd.parallel.worker", "--leader", ch.address,
+                                       "--rank", str(r), "--world", str(world), "--device",
+                                       str(devices[r % len(devices)]), "--spec", spec, "--max-ctx", str(max_ctx),
+                                       "--max-slots", str(max_slots), "--max-batch", str(max_batch),
+                                       "--seed", str(seed), "--q8", "1" if act_q8 else "0"], env=env))
+    try:
+        ch.accept_all()
+        eng, cfg = _shard(spec, 0, world, devices[0], max_ctx, max_slots, max_batch, seed, act_q8)
+        comm = native.require().XgmiComm(0, world, devices[0], comm_capacity(cfg.d_model, max_batch))
+        handles = ch.gather(comm.ipc_handle())
+        ch.broadcast(handles)
+        comm.connect(handles)
+        eng.set_comm(comm)
+    except Exception:
+        for p in procs:
+            p.kill()
+        ch.close()
+        raise
+
+    def shutdown():
+        for p in procs:
+            try:
+                p.wait(30)
+            except subprocess.TimeoutExpired:
+                p.kill()
+        ch.close()
+
+    tp = TPEngine(eng, comm, send=ch.broadcast, on_close=shutdown)
+    tp._keep = (comm, ch, procs)
+    return tp, cfg

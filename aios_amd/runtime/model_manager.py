@@ -85,6 +85,18 @@ class ModelManager:
         self._lock = threading.Lock()
         self.started = time.time()
 
+    def tp_devices(self) -> List[int]:
+        env = os.environ.get("AIOS_TP_DEVICES", "")
+        if env:
+            return [int(x) for x in env.split(",") if x.strip()]
+        try:
+            import torch
+
+            n = torch.cuda.device_count()
+        except Exception:
+            n = 0
+        return list(range(n)) if n > 1 else [self.device]
+
     # ------------------------------------------------------------------ lifecycle
     def allocate_port(self, requested: int = 0) -> int:
         used = {m.port for m in self.models.values()}
@@ -120,23 +132,41 @@ class ModelManager:
         from .tokenizer import SpmTokenizer, from_gguf
 
         E = native.require()
-        if m.path.startswith("synthetic:"):
-            parts = m.path.split(":")
+        from ..parallel.tp import launch_tp, parse_spec
+
+        base, tp, act_q8 = parse_spec(m.path)
+        if tp > 1:
+            # strategic tier: tensor parallel over the node's GPUs (ranks 1..tp-1 are worker
+            # processes; the xGMI all-reduce runs inside each rank's captured decode graph)
+            ctx = context_length or 4096
+            eng, cfg = launch_tp(base, tp, self.tp_devices(), ctx, self.max_slots, self.max_batch,
+                                 seed=abs(hash(m.name)) % 1000, act_q8=act_q8)
+            if base.startswith("synthetic:"):
+                toks, scores, types = synthetic_vocab(cfg.vocab_size)
+                tok = SpmTokenizer(toks, scores, types, cfg.bos_id, cfg.eos_id)
+                tmpl = chat_template.for_model(cfg.chat_template if cfg.chat_template in chat_template.BUILTIN
+                                               else "zephyr", tok)
+            else:
+                reader = GGUFReader(base)
+                tok = from_gguf(reader)
+                tmpl = chat_template.for_model(reader, tok)
+        elif base.startswith("synthetic:"):
+            parts = base.split(":")
             cfg = get_preset(parts[1])
             recipe = parts[2] if len(parts) > 2 else "Q4_K_M"
             ctx = context_length or min(cfg.max_ctx, 4096)
             eng = random_engine(cfg, recipe, seed=abs(hash(m.name)) % 1000, max_ctx=ctx, max_slots=self.max_slots,
-                                max_batch=self.max_batch, device=self.device)
+                                max_batch=self.max_batch, device=self.device, act_q8=act_q8)
             toks, scores, types = synthetic_vocab(cfg.vocab_size)
             tok = SpmTokenizer(toks, scores, types, cfg.bos_id, cfg.eos_id)
             tmpl = chat_template.for_model(cfg.chat_template if cfg.chat_template in chat_template.BUILTIN else "zephyr",
                                            tok)
         else:
-            if not os.path.exists(m.path):
-                raise FileNotFoundError(m.path)
-            ctx = context_length or context_for_size(os.path.getsize(m.path))
-            eng, cfg, reader = load_engine(m.path, max_ctx=ctx, max_slots=self.max_slots, max_batch=self.max_batch,
-                                           device=self.device, name=m.name)
+            if not os.path.exists(base):
+                raise FileNotFoundError(base)
+            ctx = context_length or context_for_size(os.path.getsize(base))
+            eng, cfg, reader = load_engine(base, max_ctx=ctx, max_slots=self.max_slots, max_batch=self.max_batch,
+                                           device=self.device, name=m.name, act_q8=act_q8)
             tok = from_gguf(reader)
             tmpl = chat_template.for_model(reader, tok)
         m.engine, m.config, m.tokenizer, m.template = eng, cfg, tok, tmpl
@@ -154,6 +184,8 @@ class ModelManager:
         m.status = "unloading"
         if m.scheduler is not None:
             await asyncio.to_thread(m.scheduler.close)
+        if hasattr(m.engine, "close"):
+            await asyncio.to_thread(m.engine.close)
         m.engine = None
         m.scheduler = None
         self.models.pop(name, None)

@@ -101,3 +101,48 @@ def test_tp_xgmi_allreduce_and_sharded_model(tmp_path, world):
     assert m["prefill_logit_max_abs_diff"] < 1e-3 * max(1.0, m["logit_scale"])
     assert max(m["decode_logit_max_abs_diff_per_step"]) < 1e-3 * max(1.0, m["logit_scale"])
     assert m["graph_tokens_match"]
+
+
+@pytest.mark.gpu
+def test_runtime_serves_tp_model(tmp_path):
+    """ModelManager hosts a TP=2 strategic model (worker process + xGMI all-reduce) and its
+    greedy generations through the continuous-batching scheduler equal the TP=1 model's."""
+    import asyncio
+    import threading
+
+    from aios_amd.models.config import get_preset
+    from aios_amd.models.synthetic import write_synthetic_gguf
+    from aios_amd.runtime.model_manager import ModelManager
+    from aios_amd.runtime.scheduler import GenRequest
+
+    path = str(tmp_path / "m.gguf")
+    write_synthetic_gguf(path, get_preset("test-tp8-shape"), "Q4_K_M", seed=3)
+    mgr = ModelManager(max_batch=4, max_slots=4)
+
+    def gen(m, prompts):
+        outs, evs = [None] * len(prompts), [threading.Event() for _ in prompts]
+        for i, p in enumerate(prompts):
+            def done(r, i=i):
+                outs[i] = r
+                evs[i].set()
+            m.scheduler.submit(GenRequest(prompt_ids=m.tokenizer.encode(p), on_done=done, max_tokens=10))
+        for e in evs:
+            assert e.wait(120)
+        return [o.token_ids for o in outs]
+
+    async def load(name, spec):
+        m = await mgr.load_model(name, spec, context_length=256)
+        assert m.status == "ready", m.error
+        return m
+
+    prompts = ["alpha beta gamma", "the strategic tier", "json { }"]
+    m1 = asyncio.run(load("ref", path + "#q8=0"))
+    ref = gen(m1, prompts)
+    asyncio.run(mgr.unload_model("ref"))
+    m2 = asyncio.run(load("llama3-70b", path + "#tp=2&q8=0"))
+    try:
+        assert type(m2.engine).__name__ == "TPEngine"
+        assert mgr.select_model_for_level("strategic") == "llama3-70b"
+        assert gen(m2, prompts) == ref
+    finally:
+        asyncio.run(mgr.unload_model("llama3-70b"))

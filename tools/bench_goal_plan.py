@@ -1,0 +1,122 @@
+#!/usr/bin/env python3
+"""p50 agent goal -> plan latency (BASELINE.json metric #3; bar: tactical tier ~200-500 ms,
+docs/VISION.md:45 of the reference).
+
+The full control path runs in one process on one MI355X: the AIRuntime service (native engine,
+Mistral-7B Q4_K_M tactical model, random-init weights of that architecture), the tool and memory
+services, and the Orchestrator service -- all over real gRPC on loopback.  Each measured goal is
+a tactical/strategic description; latency = the SubmitGoal RPC round trip, which includes
+classification, the decomposition LLM call (gateway attempt -> runtime JSON-mode generation),
+parsing, and persisting the tasks (exactly the reference's SubmitGoal path, main.rs:142-175).
+
+Random weights never stop on their own, so the decomposition output length is fixed by the token
+cap: --plan-tokens (default 160 ~ a 2-5 step JSON plan; the reference's cap is 1024, which a real
+model does not reach).  Reported alongside: the same measurement for reactive/operational goals
+(planned heuristically, no LLM).
+"""
+import argparse
+import asyncio
+import json
+import os
+import statistics
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+TACTICAL = [
+    "install nginx and then configure the firewall to allow https",
+    "design a backup plan for the model directory and verify it",
+    "analyze why the disk filled up last night and clean it",
+    "set up monitoring for the gpu temperature and alert on spikes",
+    "update all packages, then restart the web services safely",
+    "plan a rollout of the new tool plugin to the cluster nodes",
+    "investigate the failed login attempts and harden ssh",
+    "create a python project that summarises system logs daily",
+]
+REACTIVE = ["check nginx status", "report cpu usage status", "ping 1.1.1.1 health", "check disk usage"]
+
+
+async def main_async(args):
+    os.environ["AIOS_PLAN_MAX_TOKENS"] = str(args.plan_tokens)
+    from aios_amd.memory.service import MemoryServiceImpl
+    from aios_amd.orchestrator.clients import ServiceClients
+    from aios_amd.orchestrator.service import OrchestratorService
+    from aios_amd.orchestrator.state import OrchestratorState
+    from aios_amd.rpc.client import Stub, channel, close_all
+    from aios_amd.rpc.schema import pb
+    from aios_amd.rpc.server import RpcServer
+    from aios_amd.runtime.model_manager import ModelManager
+    from aios_amd.runtime.service import AIRuntimeService
+    from aios_amd.tools.service import ToolRegistryService
+
+    tmp = tempfile.mkdtemp(prefix="aios_bench_")
+    mgr = ModelManager(max_batch=8, max_slots=8)
+    t0 = time.time()
+    m = await mgr.load_model("mistral-7b", f"synthetic:{args.model}:Q4_K_M", context_length=2048)
+    assert m.status == "ready", m.error
+    load_s = time.time() - t0
+    servers = {
+        "runtime": await RpcServer("127.0.0.1:0", {"aios.runtime.AIRuntime": AIRuntimeService(mgr, http=False)}).start(),
+        "tools": await RpcServer("127.0.0.1:0", {"aios.tools.ToolRegistry": ToolRegistryService(tmp)}).start(),
+        "memory": await RpcServer("127.0.0.1:0", {"aios.memory.MemoryService": MemoryServiceImpl(
+            f"{tmp}/w.db", f"{tmp}/l.db", f"{tmp}/k.db")}).start(),
+    }
+    addrs = {k: f"127.0.0.1:{s.port}" for k, s in servers.items()}
+    addrs["api-gateway"] = "127.0.0.1:1"  # no gateway on this node: planner falls back to the runtime
+    clients = ServiceClients(timeout=60)
+    clients.address = lambda n: addrs[n]
+    st = OrchestratorState(f"{tmp}/orch", clients=clients)
+    servers["orchestrator"] = await RpcServer("127.0.0.1:0", {"aios.orchestrator.Orchestrator":
+                                                             OrchestratorService(st)}).start()
+    orch = Stub(channel(f"127.0.0.1:{servers['orchestrator'].port}"), "aios.orchestrator.Orchestrator", timeout=120)
+
+    async def submit(desc):
+        t = time.perf_counter()
+        gid = (await orch.SubmitGoal(pb.orchestrator.SubmitGoalRequest(description=desc, priority=5))).id
+        ms = (time.perf_counter() - t) * 1000
+        s = await orch.GetGoalStatus(pb.common.GoalId(id=gid))
+        return ms, len(s.tasks), s.tasks[0].intelligence_level if s.tasks else ""
+
+    for d in TACTICAL[:args.warmup]:
+        await submit(d)
+    tac = [await submit(TACTICAL[i % len(TACTICAL)] + f" #{i}") for i in range(args.goals)]
+    rea = [await submit(REACTIVE[i % len(REACTIVE)]) for i in range(args.goals)]
+    # concurrent burst: the runtime batches the decomposition calls
+    t = time.perf_counter()
+    burst = await asyncio.gather(*(submit(TACTICAL[i % len(TACTICAL)] + f" burst {i}") for i in range(args.burst)))
+    burst_s = time.perf_counter() - t
+    lat = sorted(x[0] for x in tac)
+    rlat = sorted(x[0] for x in rea)
+    blat = sorted(x[0] for x in burst)
+    q = lambda v, p: v[min(len(v) - 1, int(p * len(v)))]
+    out = {"metric": "p50 agent goal->plan latency (tactical goals, LLM decomposition)",
+           "value": round(statistics.median(lat), 1), "unit": "ms", "higher_is_better": False,
+           "p90_ms": round(q(lat, 0.9), 1), "mean_ms": round(statistics.mean(lat), 1), "goals": len(lat),
+           "tasks_per_goal": round(statistics.mean(x[1] for x in tac), 2),
+           "reactive_p50_ms": round(statistics.median(rlat), 2),
+           "burst": {"concurrent_goals": args.burst, "wall_s": round(burst_s, 3), "p50_ms": round(statistics.median(blat), 1)},
+           "plan_tokens_cap": args.plan_tokens, "model": f"{args.model} Q4_K_M (random-init, synthetic vocab)",
+           "baseline_ms": "200-500 (tactical tier, docs/VISION.md:45)", "model_load_s": round(load_s, 1),
+           "data": "synthetic goals; decomposition output length fixed by plan_tokens_cap (random weights)"}
+    print(json.dumps(out), flush=True)
+    for s in servers.values():
+        await s.stop(0)
+    await close_all()
+    await mgr.unload_model("mistral-7b")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="mistral-7b")
+    ap.add_argument("--goals", type=int, default=24)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--burst", type=int, default=8)
+    ap.add_argument("--plan-tokens", type=int, default=160)
+    asyncio.run(main_async(ap.parse_args()))
+
+
+if __name__ == "__main__":
+    main()
