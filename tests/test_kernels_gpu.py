@@ -173,10 +173,13 @@ def test_gemv_qkv_rope_kv(E, mixed, q8):
 
 
 @pytest.mark.parametrize("hd,H,Hkv", [(64, 8, 1), (128, 32, 8), (64, 32, 4), (128, 40, 8)])
-@pytest.mark.parametrize("lens", [[1], [37, 200], [64, 65, 129, 1], [256, 255, 192]])
-def test_attention_decode(E, hd, H, Hkv, lens):
+@pytest.mark.parametrize("lens,max_ctx", [([1], 256), ([37, 200], 256), ([64, 65, 129, 1], 256),
+                                          ([256, 255, 192], 256),
+                                          # several 512-key splits: exercises the cross-workgroup combine
+                                          ([1500, 513, 512, 2048], 2048), ([1025, 3], 1280)])
+def test_attention_decode(E, hd, H, Hkv, lens, max_ctx):
     B = len(lens)
-    max_ctx, slots = 256, B + 1
+    slots = B + 1
     kc = (torch.randn(slots, Hkv, max_ctx, hd) * 0.5).to(torch.bfloat16).cuda()
     vc = torch.randn(slots, Hkv, max_ctx, hd).to(torch.bfloat16).cuda()
     q = torch.randn(B, H, hd, device="cuda")
