@@ -519,6 +519,7 @@ void Engine::layer_decode(int l, int B) {
   // ---- attention
   {
     AttnDecodeArgs a;
+    a.split = 0;
     a.q = q_;
     a.k_cache = k_cache_ + (size_t)l * layer_kv_elems_;
     a.v_cache = v_cache_ + (size_t)l * layer_kv_elems_;
@@ -646,6 +647,7 @@ std::vector<float> Engine::prefill(int slot, const std::vector<int>& tokens, int
         // attention for all n rows (causal by per-row seq_len)
         {
           AttnDecodeArgs a;
+          a.split = 0;
           a.q = qb;
           a.k_cache = k_cache_ + (size_t)l * layer_kv_elems_;
           a.v_cache = v_cache_ + (size_t)l * layer_kv_elems_;

@@ -62,6 +62,7 @@ struct AttnDecodeArgs {
   const int* slot;         // [B] or null
   int B, n_heads, n_kv_heads, head_dim, max_ctx;
   int n_chunks;            // grid chunks (>= ceil(max_len / ATTN_CHUNK))
+  int split;               // keys per workgroup (multiple of ATTN_CHUNK); 0 -> chosen by the launcher
   float scale;
   float* o_part;           // [B][n_heads][n_chunks][hd]
   float* ml;               // [B][n_heads][n_chunks][2]
@@ -70,6 +71,7 @@ struct AttnDecodeArgs {
 };
 constexpr int ATTN_CHUNK = 64;
 void launch_attn_decode(const AttnDecodeArgs& a, hipStream_t st);
+int attn_decode_split(int max_ctx, int B, int n_kv_heads);  // keys per workgroup the launcher picks
 
 // ---- sampling ---------------------------------------------------------------------------------
 // per row b: token[b] = argmax(logits[b])   (temperature[b] > 0 -> Gumbel-max sample with

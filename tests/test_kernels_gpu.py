@@ -177,7 +177,8 @@ def test_gemv_qkv_rope_kv(E, mixed, q8):
                                           ([256, 255, 192], 256),
                                           # several 512-key splits: exercises the cross-workgroup combine
                                           ([1500, 513, 512, 2048], 2048), ([1025, 3], 1280)])
-def test_attention_decode(E, hd, H, Hkv, lens, max_ctx):
+@pytest.mark.parametrize("split", [0, 64, 192])  # 0 = the launcher's choice
+def test_attention_decode(E, hd, H, Hkv, lens, max_ctx, split):
     B = len(lens)
     slots = B + 1
     kc = (torch.randn(slots, Hkv, max_ctx, hd) * 0.5).to(torch.bfloat16).cuda()
@@ -194,7 +195,8 @@ def test_attention_decode(E, hd, H, Hkv, lens, max_ctx):
     for _ in range(2):  # second launch checks the counters re-armed themselves
         out.zero_()
         E.attn_decode(q.data_ptr(), kc.data_ptr(), vc.data_ptr(), seq.data_ptr(), slot.data_ptr(), B, H, Hkv, hd,
-                      max_ctx, nch, scale, opart.data_ptr(), ml.data_ptr(), out.data_ptr(), cnt.data_ptr(), stream())
+                      max_ctx, nch, scale, opart.data_ptr(), ml.data_ptr(), out.data_ptr(), cnt.data_ptr(), stream(),
+                      split)
     torch.cuda.synchronize()
     assert int(cnt.abs().sum()) == 0
     G = H // Hkv

@@ -1,0 +1,66 @@
+"""Decode-attention microbenchmark on the GPU: per-launch time (hipGraph of back-to-back launches)
+of attn_decode over context lengths x split sizes.  python tools/attn_probe.py"""
+import math
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch
+
+from aios_amd.runtime import native
+
+
+def graph_time(fn, n=64, reps=20):
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        fn()
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            for _ in range(n):
+                fn()
+    torch.cuda.synchronize()
+    g.replay()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        g.replay()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) * 1e3 / (reps * n)
+
+
+def main():
+    E = native.require()
+    H, Hkv, hd = 32, 8, 128
+    for max_ctx in (512, 4096):
+        kc = (torch.randn(1, Hkv, max_ctx, hd) * 0.5).to(torch.bfloat16).cuda()
+        vc = torch.randn(1, Hkv, max_ctx, hd).to(torch.bfloat16).cuda()
+        q = torch.randn(1, H, hd, device="cuda")
+        slot = torch.zeros(1, dtype=torch.int32, device="cuda")
+        nch = max_ctx // E.ATTN_CHUNK
+        opart = torch.empty(1, H, nch, hd, device="cuda")
+        ml = torch.empty(1, H, nch, 2, device="cuda")
+        out = torch.empty(1, H * hd, device="cuda")
+        cnt = torch.zeros(1, Hkv, dtype=torch.int32, device="cuda")
+        for L in (64, 130, 400, 1000, 2000, 4000):
+            if L > max_ctx:
+                continue
+            seq = torch.tensor([L], dtype=torch.int32, device="cuda")
+            row = []
+            for P in (0, 1, 4, 8, 16, 32, 64):
+                if P > nch:
+                    continue
+                split = P * E.ATTN_CHUNK
+                fn = lambda: E.attn_decode(q.data_ptr(), kc.data_ptr(), vc.data_ptr(), seq.data_ptr(), slot.data_ptr(),
+                                           1, H, Hkv, hd, max_ctx, nch, 1 / math.sqrt(hd), opart.data_ptr(),
+                                           ml.data_ptr(), out.data_ptr(), cnt.data_ptr(),
+                                           torch.cuda.current_stream().cuda_stream, split)
+                row.append(f"P{P}={graph_time(fn):6.2f}")
+            print(f"max_ctx={max_ctx:5d} len={L:5d}  " + "  ".join(row), flush=True)
+    print("launch chain graph (256 blocks): %.2f us/kernel" % E.bench_launch_chain(200, 256, 1, 20))
+
+
+if __name__ == "__main__":
+    main()
