@@ -333,6 +333,36 @@ PYBIND11_MODULE(_engine, m) {
           launch_gemm(a, S(st));
         });
   m.def("gemm_supports", &gemm_supports);
+  m.def(
+      "gemm_q",
+      [](uintptr_t A, int lda, std::vector<PyQMatrix*> segs, int M, uintptr_t C, uintptr_t C16, int ldc, int epi,
+         uintptr_t st) {
+        GemmQArgs a;
+        std::memset(&a, 0, sizeof(a));
+        if (segs.empty() || segs.size() > 3) throw std::runtime_error("gemm_q: 1..3 segments");
+        a.A = (const bf16_t*)A; a.lda = lda; a.nseg = (int)segs.size();
+        int n0 = 0;
+        for (int s = 0; s < a.nseg; ++s) { a.seg[s] = segs[s]->w; a.seg_n0[s] = n0; n0 += segs[s]->w.rows; }
+        a.M = M; a.N = n0; a.K = segs[0]->w.cols;
+        a.C = (float*)C; a.C16 = (bf16_t*)C16; a.ldc = ldc; a.epi = epi;
+        launch_gemm_q(a, S(st));
+      },
+      py::arg("A"), py::arg("lda"), py::arg("segs"), py::arg("M"), py::arg("C"), py::arg("C16"), py::arg("ldc"),
+      py::arg("epi"), py::arg("stream"));
+  m.attr("GEPI_STORE") = (int)GEPI_STORE;
+  m.attr("GEPI_ACCUM") = (int)GEPI_ACCUM;
+  m.attr("GEPI_SWIGLU_BF16") = (int)GEPI_SWIGLU_BF16;
+  m.def(
+      "attn_prefill",
+      [](uintptr_t q, uintptr_t k, uintptr_t v, int slot, int start, int T, int H, int Hkv, int hd, int max_ctx,
+         float scale, uintptr_t out, int ldo, uintptr_t st) {
+        AttnPrefillArgs a;
+        a.q = (const float*)q; a.k_cache = (const bf16_t*)k; a.v_cache = (const bf16_t*)v;
+        a.slot = slot; a.start = start; a.T = T; a.n_heads = H; a.n_kv_heads = Hkv; a.head_dim = hd;
+        a.max_ctx = max_ctx; a.scale = scale; a.out = (bf16_t*)out; a.ldo = ldo;
+        launch_attn_prefill(a, S(st));
+      });
+  m.def("attn_prefill_supports", &attn_prefill_supports);
 
   // ------------------------------------------------------------------ JSON-mode grammar (K10)
   py::class_<JsonState>(m, "JsonState")

@@ -7,6 +7,8 @@
 #include <hip/hip_runtime.h>
 #include <hip/hip_fp16.h>
 #include <stdint.h>
+#include <cstring>
+#include <type_traits>
 
 #include <stdexcept>
 #include <string>
@@ -83,6 +85,28 @@ __device__ __forceinline__ void kq_scale_min(int j, const uint8_t* q, int& sc, i
     sc = (q[j + 4] & 0xF) | ((q[j - 4] >> 6) << 4);
     m = (q[j + 4] >> 4) | ((q[j] >> 6) << 4);
   }
+}
+
+// compile-time loop: f(std::integral_constant<int, I>{}) for I in [0, N) -- register arrays
+// indexed by I stay in VGPRs even where the unroller would keep a runtime loop (and put the
+// array in scratch)
+template <int N, int I = 0, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for<N, I + 1>(f);
+  }
+}
+
+// CUs of the current device (host; cached per process)
+inline int device_cu_count() {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+  }
+  return cus;
 }
 
 }  // namespace aios

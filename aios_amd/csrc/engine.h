@@ -119,6 +119,8 @@ class Engine {
 
  private:
   void enqueue_decode_step(int B);       // uses device arrays d_tokens_/d_pos_/d_seqlen_/d_slot_
+  bool gemm_prefill_ok(int T) const;
+  void prefill_gemm(int slot, const std::vector<int>& tokens, int start_pos, bool want_logits);
   void layer_decode(int l, int B);
   void gemv(const std::vector<const QMat*>& segs, int N, int K, int B, const float* x, int ldx, const float* norm_w,
             float* y, int ldy, int epi, int layer);
@@ -159,6 +161,13 @@ class Engine {
   float *pf_x_ = nullptr, *pf_q_ = nullptr, *pf_attn_ = nullptr, *pf_ff_ = nullptr, *pf_qkv_ = nullptr;
   float *pf_opart_ = nullptr, *pf_ml_ = nullptr;
   bf16_t* pf_a16_ = nullptr;
+  // GEMM prefill workspace (chunks of gm_rows_ tokens through MFMA GEMMs + flash attention)
+  int gm_rows_ = 512;
+  int gm_min_rows_ = 16;  // prompts shorter than this take the GEMV path
+  bool gm_ok_ = false;    // every layer's weights / head shape supported
+  float *gm_x_ = nullptr, *gm_qkv_ = nullptr, *gm_q_ = nullptr, *gm_part_ = nullptr;
+  bf16_t *gm_a16_ = nullptr, *gm_ff16_ = nullptr, *gm_attn16_ = nullptr;
+  int *gm_tokens_ = nullptr, *gm_pos_ = nullptr, *gm_slot_ = nullptr;
   int *pf_tokens_ = nullptr, *pf_pos_ = nullptr, *pf_seqlen_ = nullptr, *pf_slot_ = nullptr;
 
   std::map<int, hipGraphExec_t> graphs_;

@@ -1,5 +1,6 @@
 // Engine implementation -- see engine.h.
 #include "engine.h"
+#include <cstdlib>
 
 #include <algorithm>
 #include <cstring>
@@ -406,6 +407,34 @@ void Engine::finalize() {
   pf_pos_ = ibuf(R);
   pf_seqlen_ = ibuf(R);
   pf_slot_ = ibuf(R);
+  // GEMM prefill path: supported when every projection is a GEMM format with 64-aligned shapes
+  // and the head layout has a flash-attention instantiation
+  {
+    if (const char* e = std::getenv("AIOS_PREFILL_GEMM_MIN")) gm_min_rows_ = std::max(1, std::atoi(e));
+    if (const char* e = std::getenv("AIOS_PREFILL_GEMM_ROWS")) gm_rows_ = std::max(64, std::atoi(e));
+    bool ok = attn_prefill_supports(H, Hkv, hd) && d % 64 == 0 && cfg_.d_ff % 64 == 0 && qd % 64 == 0 && kvd % 64 == 0;
+    for (const auto& L : layers_) {
+      for (const QMat* m : {&L.wq, &L.wk, &L.wv, &L.wo, &L.wgu, &L.wdown})
+        if (!gemm_supports(m->w.qtype) || m->w.rows % 64 || m->w.cols % 64) ok = false;
+    }
+    if (const char* e = std::getenv("AIOS_PREFILL_GEMM"))
+      if (std::atoi(e) == 0) ok = false;
+    gm_ok_ = ok;
+    if (ok) {
+      const int G = gm_rows_;
+      gm_x_ = fbuf((size_t)G * d);
+      gm_qkv_ = fbuf((size_t)G * (qd + 2 * kvd));
+      gm_q_ = fbuf((size_t)G * qd);
+      gm_part_ = fbuf((size_t)G * d);
+      gm_a16_ = (bf16_t*)dmalloc((size_t)G * d * 2);
+      gm_ff16_ = (bf16_t*)dmalloc((size_t)G * cfg_.d_ff * 2);
+      gm_attn16_ = (bf16_t*)dmalloc((size_t)G * qd * 2);
+      ws += (size_t)G * (d + cfg_.d_ff + qd) * 2;
+      gm_tokens_ = ibuf(G);
+      gm_pos_ = ibuf(G);
+      gm_slot_ = ibuf(G);
+    }
+  }
   ws_bytes_ = ws;
   HIP_CHECK(hipDeviceSynchronize());
   finalized_ = true;
@@ -567,6 +596,78 @@ void Engine::enqueue_decode_step(int B) {
   launch_sample(s, stream_);
 }
 
+bool Engine::gemm_prefill_ok(int T) const { return gm_ok_ && T >= gm_min_rows_; }
+
+// Prefill through the matrix cores: per chunk of <= gm_rows_ tokens and per layer
+//   RMSNorm -> bf16 | QKV GEMM (Q4_K/Q6_K dequant fused, one launch per format run) | RoPE + KV
+//   write | causal flash attention (MFMA) -> bf16 | O GEMM (+= residual) | RMSNorm -> bf16 |
+//   gate/up GEMM with the SwiGLU epilogue -> bf16 | down GEMM (+= residual)
+// so every weight byte is dequantised once per chunk (not once per 8 rows as on the GEMV path).
+// TP: the row-parallel O / down outputs go through the all-reduce hook into the residual.
+void Engine::prefill_gemm(int slot, const std::vector<int>& tokens, int start_pos, bool want_logits) {
+  const int T = (int)tokens.size();
+  const int d = cfg_.d_model, hd = cfg_.head_dim, H = cfg_.n_heads, Hkv = cfg_.n_kv_heads, ff = cfg_.d_ff;
+  const int qd = H * hd, kvd = Hkv * hd, ldqkv = qd + 2 * kvd, V = cfg_.vocab_size;
+  const bool tp = cfg_.tp_size > 1;
+  std::vector<int> hp(gm_rows_), hs(gm_rows_, slot);
+  for (int r0 = 0; r0 < T; r0 += gm_rows_) {
+    const int n = std::min(gm_rows_, T - r0);
+    for (int i = 0; i < n; ++i) hp[i] = start_pos + r0 + i;
+    HIP_CHECK(hipMemcpyAsync(gm_tokens_, tokens.data() + r0, n * 4, hipMemcpyHostToDevice, stream_));
+    HIP_CHECK(hipMemcpyAsync(gm_pos_, hp.data(), n * 4, hipMemcpyHostToDevice, stream_));
+    HIP_CHECK(hipMemcpyAsync(gm_slot_, hs.data(), n * 4, hipMemcpyHostToDevice, stream_));
+    launch_get_rows(tok_embd_.w, gm_tokens_, n, gm_x_, d, 1.f, stream_);
+    for (int l = 0; l < cfg_.n_layers; ++l) {
+      const LayerW& L = layers_[l];
+      bf16_t* kc = k_cache_ + (size_t)l * layer_kv_elems_;
+      bf16_t* vc = v_cache_ + (size_t)l * layer_kv_elems_;
+      launch_rmsnorm_bf16(gm_x_, d, L.attn_norm, gm_a16_, d, n, d, cfg_.norm_eps, stream_);
+      GemmQArgs g;
+      std::memset(&g, 0, sizeof(g));
+      g.A = gm_a16_; g.lda = d; g.M = n; g.K = d;
+      g.nseg = 3;
+      g.seg[0] = L.wq.w; g.seg[1] = L.wk.w; g.seg[2] = L.wv.w;
+      g.seg_n0[0] = 0; g.seg_n0[1] = qd; g.seg_n0[2] = qd + kvd;
+      g.N = ldqkv; g.C = gm_qkv_; g.ldc = ldqkv; g.epi = GEPI_STORE;
+      launch_gemm_q(g, stream_);
+      QkvPostArgs p;
+      p.qkv = gm_qkv_; p.ldqkv = ldqkv; p.T = n;
+      p.n_heads = H; p.n_kv_heads = Hkv; p.head_dim = hd;
+      p.bias = L.bqkv; p.q_norm = L.q_norm; p.k_norm = L.k_norm; p.eps = cfg_.norm_eps;
+      p.rope_neox = cfg_.rope_neox; p.rope_base = cfg_.rope_theta; p.rope_cs = rope_cs_;
+      p.pos = gm_pos_; p.slot = gm_slot_; p.q_out = gm_q_;
+      p.k_cache = kc; p.v_cache = vc; p.max_ctx = cfg_.max_ctx;
+      launch_qkv_post(p, stream_);
+      AttnPrefillArgs at;
+      at.q = gm_q_; at.k_cache = kc; at.v_cache = vc;
+      at.slot = slot; at.start = start_pos + r0; at.T = n;
+      at.n_heads = H; at.n_kv_heads = Hkv; at.head_dim = hd; at.max_ctx = cfg_.max_ctx;
+      at.scale = 1.f / std::sqrt((float)hd);
+      at.out = gm_attn16_; at.ldo = qd;
+      launch_attn_prefill(at, stream_);
+      // O projection (+ residual)
+      std::memset(&g, 0, sizeof(g));
+      g.A = gm_attn16_; g.lda = qd; g.M = n; g.K = qd; g.nseg = 1; g.seg[0] = L.wo.w; g.N = d; g.ldc = d;
+      if (tp) { g.C = gm_part_; g.epi = GEPI_STORE; } else { g.C = gm_x_; g.epi = GEPI_ACCUM; }
+      launch_gemm_q(g, stream_);
+      if (tp) allreduce(gm_part_, (size_t)n * d, gm_x_);
+      // FFN
+      launch_rmsnorm_bf16(gm_x_, d, L.ffn_norm, gm_a16_, d, n, d, cfg_.norm_eps, stream_);
+      std::memset(&g, 0, sizeof(g));
+      g.A = gm_a16_; g.lda = d; g.M = n; g.K = d; g.nseg = 1; g.seg[0] = L.wgu.w; g.N = 2 * ff;
+      g.C16 = gm_ff16_; g.ldc = ff; g.epi = GEPI_SWIGLU_BF16;
+      launch_gemm_q(g, stream_);
+      std::memset(&g, 0, sizeof(g));
+      g.A = gm_ff16_; g.lda = ff; g.M = n; g.K = ff; g.nseg = 1; g.seg[0] = L.wdown.w; g.N = d; g.ldc = d;
+      if (tp) { g.C = gm_part_; g.epi = GEPI_STORE; } else { g.C = gm_x_; g.epi = GEPI_ACCUM; }
+      launch_gemm_q(g, stream_);
+      if (tp) allreduce(gm_part_, (size_t)n * d, gm_x_);
+    }
+    if (r0 + n == T && want_logits)
+      gemv({&output_}, V, d, 1, gm_x_ + (size_t)(n - 1) * d, d, out_norm_, logits_, V, EPI_STORE, 0);
+  }
+}
+
 std::vector<float> Engine::prefill(int slot, const std::vector<int>& tokens, int start_pos, bool want_logits) {
   if (!finalized_) throw std::runtime_error("engine not finalized");
   HIP_CHECK(hipSetDevice(cfg_.device));
@@ -576,6 +677,16 @@ std::vector<float> Engine::prefill(int slot, const std::vector<int>& tokens, int
   if (slot < 0 || slot >= cfg_.max_slots) throw std::runtime_error("prefill: bad slot");
   for (int t : tokens)
     if (t < 0 || t >= cfg_.vocab_size) throw std::runtime_error("prefill: token id out of range");
+  if (gemm_prefill_ok(T)) {
+    prefill_gemm(slot, tokens, start_pos, want_logits);
+    std::vector<float> out;
+    if (want_logits) {
+      out.resize(cfg_.vocab_size);
+      HIP_CHECK(hipMemcpyAsync(out.data(), logits_, (size_t)cfg_.vocab_size * 4, hipMemcpyDeviceToHost, stream_));
+    }
+    HIP_CHECK(hipStreamSynchronize(stream_));
+    return out;
+  }
   const int d = cfg_.d_model, V = cfg_.vocab_size;
   const int R = prefill_rows_;
   // swap decode workspace pointers with the prefill ones for the duration of the call

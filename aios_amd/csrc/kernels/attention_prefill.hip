@@ -1,0 +1,229 @@
+// Causal flash attention for prefill (prefill column: "[T,H,hd]^2 causal
+// flash-attention (MFMA)"), reading K/V from the bf16 KV cache the QKV epilogue just wrote, so a
+// chunk of T new tokens attends over every cached position [0, start + T) of its slot.
+//
+// GQA packing: a workgroup owns one KV head and BQ = 128 / G query positions x all G query heads
+// of that group = 128 query rows, so every K/V tile staged in LDS is used by 4x32 rows.  Wave w
+// owns rows [32w, 32w + 32) (row = position * G + head).  Per 64-key tile:
+//   S^T[key][row] = K Q^T   -- v_mfma_f32_32x32x16_bf16, K rows straight from LDS (A operand),
+//                              Q^T from registers (B operand, loaded once, pre-scaled by
+//                              scale*log2 e): the lane then holds one query row's 32 keys, so
+//                              the row max / sum need one cross-half shuffle, not a 32-lane tree.
+//   O^T[dim][row] += V^T P^T -- P^T is taken straight from the S^T accumulator registers: the key
+//                              order of the k-dimension is permuted (rho below) to match the
+//                              accumulator layout, and V is staged transposed in LDS in natural
+//                              key order, so the V^T fragment is two 8-byte LDS reads at rho.
+// Online softmax per row in the log2 domain; fully masked rows cannot occur (key 0 <= pos).
+// Output: bf16 [T][n_heads * hd] (the O-projection GEMM's A operand).
+#include "../common.h"
+#include "../ops.h"
+
+namespace aios {
+
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef float f32x16_t __attribute__((ext_vector_type(16)));
+// native vector type for register arrays (HIP's uint4 is a struct; arrays of it copied with
+// memcpy defeat SROA and land in scratch)
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint32_t pk_bf16(float a, float b) {
+  return (uint32_t)f32_to_bf16(a) | ((uint32_t)f32_to_bf16(b) << 16);
+}
+
+constexpr int FP_KT = 64;  // keys per tile
+
+template <int HD, int G>
+__global__ void __launch_bounds__(256) attn_prefill_kernel(AttnPrefillArgs a) {
+  constexpr int BQ = 128 / G;          // query positions per workgroup
+  constexpr int KS = HD / 16;          // k-steps of the S MFMA
+  constexpr int OT = HD / 32;          // O^T accumulator tiles (32 dims each)
+  constexpr int KROW = HD + 8;         // padded LDS row (bf16) of the K tile
+  constexpr int VROW = FP_KT + 4;      // padded LDS row (bf16) of the transposed V tile
+  __shared__ __attribute__((aligned(16))) bf16_t sK[FP_KT * KROW];
+  __shared__ __attribute__((aligned(16))) bf16_t sV[HD * VROW];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int l32 = lane & 31, half = lane >> 5;
+  // heaviest (latest) query blocks first
+  const int qb = gridDim.x - 1 - blockIdx.x, kvh = blockIdx.y;
+  const int T = a.T, start = a.start;
+  const int t0 = qb * BQ;
+  // this lane's query row (column of S^T / O^T)
+  const int row = wave * 32 + l32;
+  const int tq = t0 + row / G, g = row % G;
+  const bool qvalid = tq < T;
+  const int tql = qvalid ? tq : T - 1;
+  const int qpos = start + tql;  // absolute position: keys <= qpos are visible
+  const int h = kvh * G + g;
+
+  // Q^T fragments (B operand): lane holds Q[row][16s + 8*half + 0..7] for s = 0..KS-1
+  bf16x8_t qf[KS];
+  {
+    const float* qp = a.q + ((size_t)tql * a.n_heads + h) * HD + 8 * half;
+    const float sc = a.scale * 1.4426950408889634f;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const float4 x0 = *(const float4*)(qp + 16 * s), x1 = *(const float4*)(qp + 16 * s + 4);
+      const uint4 u = make_uint4(pk_bf16(x0.x * sc, x0.y * sc), pk_bf16(x0.z * sc, x0.w * sc),
+                                 pk_bf16(x1.x * sc, x1.y * sc), pk_bf16(x1.z * sc, x1.w * sc));
+      __builtin_memcpy(&qf[s], &u, 16);
+    }
+  }
+
+  f32x16_t o[OT];
+#pragma unroll
+  for (int i = 0; i < OT; ++i)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) o[i][e] = 0.f;
+  float m_run = -INFINITY, l_run = 0.f;
+
+  const size_t kv_base = (((size_t)a.slot * a.n_kv_heads + kvh) * a.max_ctx) * HD;
+  const bf16_t* kc = a.k_cache + kv_base;
+  const bf16_t* vc = a.v_cache + kv_base;
+  const int last_pos = start + min(T, t0 + BQ) - 1;  // highest query position of the block
+  const int ntiles = last_pos / FP_KT + 1;
+
+  // tile loader: 64 keys x HD dims of K and of V, 16 B per piece
+  constexpr int PIECES = FP_KT * HD / 8;  // 16-B pieces per tensor per tile
+  constexpr int PPT = PIECES / 256;        // per thread
+  u32x4_t kreg[PPT], vreg[PPT];
+  auto load = [&](int kt) {
+    static_for<PPT>([&](auto I) {
+      constexpr int i = decltype(I)::value;
+      const int idx = tid + 256 * i, key = idx / (HD / 8), c = idx % (HD / 8);
+      const size_t off = (size_t)(kt * FP_KT + key) * HD + c * 8;  // < max_ctx rows: valid
+      kreg[i] = *(const u32x4_t*)(kc + off);
+      vreg[i] = *(const u32x4_t*)(vc + off);
+    });
+  };
+  auto stage = [&]() {
+    static_for<PPT>([&](auto I) {
+      constexpr int i = decltype(I)::value;
+      const int idx = tid + 256 * i, key = idx / (HD / 8), c = idx % (HD / 8);
+      *(u32x4_t*)(sK + key * KROW + c * 8) = kreg[i];
+      const uint32_t w[4] = {vreg[i][0], vreg[i][1], vreg[i][2], vreg[i][3]};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        sV[(c * 8 + 2 * j) * VROW + key] = (bf16_t)(w[j] & 0xffff);
+        sV[(c * 8 + 2 * j + 1) * VROW + key] = (bf16_t)(w[j] >> 16);
+      }
+    });
+  };
+
+  load(0);
+  for (int kt = 0; kt < ntiles; ++kt) {
+    __syncthreads();  // previous tile's LDS reads done
+    stage();
+    __syncthreads();
+    if (kt + 1 < ntiles) load(kt + 1);  // next tile in flight during this tile's math
+    // ---- S^T = K Q^T for the tile's two 32-key halves
+    f32x16_t st[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) st[t][e] = 0.f;
+      const bf16_t* kr = sK + (t * 32 + l32) * KROW + 8 * half;
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        const uint4 u = *(const uint4*)(kr + 16 * s);
+        bf16x8_t kf;
+        __builtin_memcpy(&kf, &u, 16);
+        st[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[s], st[t], 0, 0, 0);
+      }
+    }
+    // ---- causal mask + online softmax for this lane's row (32 of the 64 keys; partner lane^32)
+    const int kbase = kt * FP_KT;
+    const bool full = kbase + FP_KT - 1 <= qpos;
+    float mx = -INFINITY;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int key = kbase + t * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
+        if (!full && key > qpos) st[t][r] = -INFINITY;
+        mx = fmaxf(mx, st[t][r]);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float mn = fmaxf(m_run, mx);  // finite: key 0 of tile 0 is always visible
+    const float alpha = exp2f(m_run - mn);
+    float ps = 0.f;
+    uint32_t pb[2][8];  // P^T as packed bf16 pairs, accumulator order
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; r += 2) {
+        const float p0 = exp2f(st[t][r] - mn), p1 = exp2f(st[t][r + 1] - mn);
+        ps += p0 + p1;
+        pb[t][r >> 1] = pk_bf16(p0, p1);
+      }
+    ps += __shfl_xor(ps, 32, 64);
+    l_run = l_run * alpha + ps;
+    m_run = mn;
+#pragma unroll
+    for (int i = 0; i < OT; ++i)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) o[i][e] *= alpha;
+    // ---- O^T += V^T P^T over 4 k-steps of 16 keys: step s uses accumulator half t = s/2,
+    //      registers 8*(s%2) .. +7, i.e. keys rho = 16s + 4*half + {0..3} and 16s + 8 + 4*half + {0..3}
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int t = s >> 1, rb = (s & 1) * 4;
+      const uint4 pu = make_uint4(pb[t][rb], pb[t][rb + 1], pb[t][rb + 2], pb[t][rb + 3]);
+      bf16x8_t pf;
+      __builtin_memcpy(&pf, &pu, 16);
+#pragma unroll
+      for (int i = 0; i < OT; ++i) {
+        const bf16_t* vr = sV + (i * 32 + l32) * VROW + 16 * s + 4 * half;
+        const uint2 v0 = *(const uint2*)vr, v1 = *(const uint2*)(vr + 8);
+        const uint4 vu = make_uint4(v0.x, v0.y, v1.x, v1.y);
+        bf16x8_t vf;
+        __builtin_memcpy(&vf, &vu, 16);
+        o[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf, o[i], 0, 0, 0);
+      }
+    }
+  }
+  // ---- normalise and store bf16: O^T[dim][row], dim = 32 i + (r&3) + 8 (r>>2) + 4 half
+  if (qvalid) {
+    const float inv = 1.f / l_run;
+    bf16_t* op = a.out + (size_t)tq * a.ldo + (size_t)h * HD;
+#pragma unroll
+    for (int i = 0; i < OT; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; r += 4) {
+        const int d = i * 32 + 8 * (r >> 2) + 4 * half;
+        const uint2 u = make_uint2(pk_bf16(o[i][r] * inv, o[i][r + 1] * inv), pk_bf16(o[i][r + 2] * inv, o[i][r + 3] * inv));
+        *(uint2*)(op + d) = u;
+      }
+  }
+}
+
+bool attn_prefill_supports(int n_heads, int n_kv_heads, int head_dim) {
+  if (n_kv_heads <= 0 || n_heads % n_kv_heads) return false;
+  const int G = n_heads / n_kv_heads;
+  return (head_dim == 64 || head_dim == 128) && (G == 1 || G == 2 || G == 4 || G == 8);
+}
+
+template <int HD>
+static void prefill_hd(const AttnPrefillArgs& a, int G, hipStream_t st) {
+  const int BQ = 128 / G;
+  dim3 grid((a.T + BQ - 1) / BQ, a.n_kv_heads);
+  switch (G) {
+    case 1: hipLaunchKernelGGL((attn_prefill_kernel<HD, 1>), grid, dim3(256), 0, st, a); break;
+    case 2: hipLaunchKernelGGL((attn_prefill_kernel<HD, 2>), grid, dim3(256), 0, st, a); break;
+    case 4: hipLaunchKernelGGL((attn_prefill_kernel<HD, 4>), grid, dim3(256), 0, st, a); break;
+    case 8: hipLaunchKernelGGL((attn_prefill_kernel<HD, 8>), grid, dim3(256), 0, st, a); break;
+    default: throw std::runtime_error("attn_prefill: unsupported GQA group size");
+  }
+}
+
+void launch_attn_prefill(const AttnPrefillArgs& a, hipStream_t st) {
+  if (!attn_prefill_supports(a.n_heads, a.n_kv_heads, a.head_dim))
+    throw std::runtime_error("attn_prefill: unsupported head configuration");
+  if (a.T <= 0) return;
+  if (a.start + a.T > a.max_ctx) throw std::runtime_error("attn_prefill: context overflow");
+  const int G = a.n_heads / a.n_kv_heads;
+  if (a.head_dim == 128) prefill_hd<128>(a, G, st);
+  else prefill_hd<64>(a, G, st);
+}
+
+}  // namespace aios

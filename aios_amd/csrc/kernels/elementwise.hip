@@ -92,14 +92,17 @@ __global__ void qkv_post_kernel(QkvPostArgs a) {
   if (h < a.n_heads) { part = 0; head = h; }
   else if (h < a.n_heads + a.n_kv_heads) { part = 1; head = h - a.n_heads; }
   else { part = 2; head = h - a.n_heads - a.n_kv_heads; }
-  const float* src = a.qkv + (size_t)t * a.ldqkv + (part == 0 ? 0 : (part == 1 ? qd : qd + kvd)) + head * hd;
+  const int col0 = (part == 0 ? 0 : (part == 1 ? qd : qd + kvd)) + head * hd;
+  const float* src = a.qkv + (size_t)t * a.ldqkv + col0;
+  const float* bias = a.bias ? a.bias + col0 : nullptr;  // QKV bias (Qwen2-style), before norm/RoPE
+  auto val = [&](int i) { return bias ? src[i] + bias[i] : src[i]; };
   const int pos = a.pos[t];
   const int slot = a.slot ? a.slot[t] : 0;
   float inv = 1.f;
   const float* nw = part == 0 ? a.q_norm : (part == 1 ? a.k_norm : nullptr);
   if (nw) {
     float s = 0.f;
-    for (int i = lane; i < hd; i += 64) s += src[i] * src[i];
+    for (int i = lane; i < hd; i += 64) s += val(i) * val(i);
     s = wave_sum(s);
     inv = rsqrtf(s / (float)hd + a.eps);
   }
@@ -108,7 +111,7 @@ __global__ void qkv_post_kernel(QkvPostArgs a) {
     if (part == 2) { ia = 2 * p; ib = 2 * p + 1; }
     else if (a.rope_neox) { ia = p; ib = p + half; }
     else { ia = 2 * p; ib = 2 * p + 1; }
-    float v0 = src[ia], v1 = src[ib];
+    float v0 = val(ia), v1 = val(ib);
     if (nw) { v0 *= inv * nw[ia]; v1 *= inv * nw[ib]; }
     if (part < 2) {
       float sn, cs;

@@ -481,15 +481,6 @@ __global__ void __launch_bounds__(GP_THREADS) gemv_persistent(GemvArgs a) {
   }
 }
 
-inline int device_cu_count() {
-  static int cus = 0;
-  if (!cus) {
-    int dev = 0;
-    hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
-  }
-  return cus;
-}
 
 // returns false when the shape does not fit the persistent kernel's LDS budget
 template <int QT0, int QT1, int B, int U>

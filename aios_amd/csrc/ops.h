@@ -38,6 +38,7 @@ struct QkvPostArgs {
   int ldqkv;
   int T;
   int n_heads, n_kv_heads, head_dim;
+  const float* bias = nullptr;  // [q_dim + 2 kv_dim] or null (added before norm / RoPE)
   const float* q_norm;  // [head_dim] or null
   const float* k_norm;
   float eps;
@@ -71,7 +72,22 @@ struct AttnDecodeArgs {
 };
 constexpr int ATTN_CHUNK = 64;
 void launch_attn_decode(const AttnDecodeArgs& a, hipStream_t st);
-int attn_decode_split(int max_ctx, int B, int n_kv_heads);  // keys per workgroup the launcher picks
+int attn_decode_split(int max_ctx, int B, int n_kv_heads);
+
+// causal flash attention for a prefill chunk of T tokens at positions [start, start+T) of one
+// slot, over the cached keys [0, start+T) (MFMA; kernels/attention_prefill.hip)
+struct AttnPrefillArgs {
+  const float* q;          // [T][n_heads][head_dim] (RoPE applied)
+  const bf16_t* k_cache;   // layer base [slots][n_kv][max_ctx][hd]
+  const bf16_t* v_cache;
+  int slot, start, T;
+  int n_heads, n_kv_heads, head_dim, max_ctx;
+  float scale;
+  bf16_t* out;             // [T][ldo] bf16
+  int ldo;
+};
+void launch_attn_prefill(const AttnPrefillArgs& a, hipStream_t st);
+bool attn_prefill_supports(int n_heads, int n_kv_heads, int head_dim);  // keys per workgroup the launcher picks
 
 // ---- sampling ---------------------------------------------------------------------------------
 // per row b: token[b] = argmax(logits[b])   (temperature[b] > 0 -> Gumbel-max sample with
@@ -108,5 +124,21 @@ struct GemmArgs {
 };
 void launch_gemm(const GemmArgs& a, hipStream_t st);
 bool gemm_supports(int qt);
+
+// multi-segment GEMM with fused epilogues (the prefill path): C = A x [W0; W1; W2]^T
+enum GemmEpi { GEPI_STORE = 0, GEPI_ACCUM = 1, GEPI_SWIGLU_BF16 = 2 };
+struct GemmQArgs {
+  const bf16_t* A;   // [M][lda] bf16
+  int lda;
+  QWeight seg[3];    // weight segments stacked along N (rows of each a multiple of 64)
+  int seg_n0[3];     // first output column of each segment
+  int nseg;
+  int M, N, K;
+  float* C;          // [M][ldc] fp32 (STORE / ACCUM)
+  bf16_t* C16;       // [M][ldc] bf16 (SWIGLU_BF16: column n/2 = silu(col n) * col n+1)
+  int ldc;
+  int epi;
+};
+void launch_gemm_q(const GemmQArgs& a, hipStream_t st);
 
 }  // namespace aios

@@ -105,3 +105,34 @@ def test_random_init_engine_runs():
     eng.synchronize()
     h = eng.decode_loop_history(1, 5, 8)
     assert all(0 <= t < 1024 for t in h)
+
+
+@pytest.mark.parametrize("recipe", ["Q4_K_M", "mistral_shape"])
+def test_prefill_gemm_chunks_match_reference(model_files, recipe, monkeypatch):
+    # 64-row GEMM chunks: a 150-token prompt crosses two chunk boundaries (flash attention over
+    # the previous chunks' cached keys), and a prefill continued at start_pos > 0 matches too
+    monkeypatch.setenv("AIOS_PREFILL_GEMM_ROWS", "64")
+    path = model_files[recipe]
+    eng, cfg = _load(path)
+    ref = ReferenceModel.from_gguf(path, kv_bf16=True)
+    prompt = [1] + list(np.random.default_rng(3).integers(3, cfg.vocab_size, 149))
+    rl = ref.forward(prompt)[-1]
+    logits = torch.from_numpy(np.asarray(eng.prefill(0, prompt, 0, True)))
+    scale = max(rl.abs().max().item(), 1.0)
+    assert (logits - rl).abs().max().item() < 2e-2 * scale
+    eng.prefill(1, prompt[:100], 0, False)
+    logits2 = torch.from_numpy(np.asarray(eng.prefill(1, prompt[100:], 100, True)))
+    assert (logits2 - rl).abs().max().item() < 2e-2 * scale
+
+
+def test_prefill_gemm_vs_gemv_path(model_files, monkeypatch):
+    path = model_files["Q4_K_M"]
+    prompt = [1] + list(np.random.default_rng(4).integers(3, 200, 60))
+    monkeypatch.setenv("AIOS_PREFILL_GEMM", "0")
+    e1, _ = _load(path)
+    l1 = np.asarray(e1.prefill(0, prompt, 0, True))
+    del e1
+    monkeypatch.setenv("AIOS_PREFILL_GEMM", "1")
+    e2, _ = _load(path)
+    l2 = np.asarray(e2.prefill(0, prompt, 0, True))
+    assert np.abs(l1 - l2).max() < 2e-2 * max(np.abs(l1).max(), 1.0)

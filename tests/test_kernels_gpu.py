@@ -295,3 +295,75 @@ def test_gemm_mfma(E, t, M):
     E.gemm(A.data_ptr(), K, m, M, C2.data_ptr(), N, 1, stream())
     torch.cuda.synchronize()
     assert torch.allclose(C2.cpu(), 2 * ref, atol=4e-3, rtol=2e-3)
+
+
+# ---- prefill path: multi-segment MFMA GEMM with fused epilogues + causal flash attention ----------
+@pytest.mark.parametrize("segs", [[(GGMLType.Q4_K, 128), (GGMLType.Q4_K, 64), (GGMLType.Q6_K, 64)],
+                                  [(GGMLType.Q8_0, 64)], [(GGMLType.BF16, 192), (GGMLType.Q5_K, 64)],
+                                  [(GGMLType.Q4_0, 128), (GGMLType.F16, 128)]])
+@pytest.mark.parametrize("M", [1, 100, 300])
+def test_gemm_q_segments(E, segs, M):
+    K = 512
+    mats, refs = zip(*[qmat(E, t, n, K, seed=20 + i) for i, (t, n) in enumerate(segs)])
+    W = torch.cat(refs, 0)
+    N = W.shape[0]
+    A = torch.randn(M, K, device="cuda").to(torch.bfloat16)
+    C = torch.zeros(M, N, device="cuda")
+    E.gemm_q(A.data_ptr(), K, list(mats), M, C.data_ptr(), 0, N, E.GEPI_STORE, stream())
+    torch.cuda.synchronize()
+    ref = A.float().cpu() @ W.to(torch.bfloat16).float().T
+    assert torch.allclose(C.cpu(), ref, atol=2e-3, rtol=2e-3), (C.cpu() - ref).abs().max()
+    E.gemm_q(A.data_ptr(), K, list(mats), M, C.data_ptr(), 0, N, E.GEPI_ACCUM, stream())
+    torch.cuda.synchronize()
+    assert torch.allclose(C.cpu(), 2 * ref, atol=4e-3, rtol=2e-3)
+
+
+@pytest.mark.parametrize("M,N,K", [(1024, 4096, 256), (200, 2048, 1024)])
+def test_gemm_q_large_tiles(E, M, N, K):
+    # shapes that select the 128x128 and 64x128 workgroup tiles (XCD-remapped grid)
+    m, W = qmat(E, GGMLType.Q4_K, N, K, seed=5)
+    A = torch.randn(M, K, device="cuda").to(torch.bfloat16)
+    C = torch.zeros(M, N, device="cuda")
+    E.gemm_q(A.data_ptr(), K, [m], M, C.data_ptr(), 0, N, E.GEPI_STORE, stream())
+    torch.cuda.synchronize()
+    ref = A.float().cpu() @ W.to(torch.bfloat16).float().T
+    assert torch.allclose(C.cpu(), ref, atol=3e-3, rtol=3e-3), (C.cpu() - ref).abs().max()
+
+
+@pytest.mark.parametrize("M", [7, 130])
+def test_gemm_q_swiglu_epilogue(E, M):
+    K, F = 256, 192  # interleaved gate/up rows: 2F weight rows -> F bf16 outputs
+    m, W = qmat(E, GGMLType.Q4_K, 2 * F, K, seed=8, std=0.2)
+    A = torch.randn(M, K, device="cuda").to(torch.bfloat16)
+    out = torch.zeros(M, F, dtype=torch.bfloat16, device="cuda")
+    E.gemm_q(A.data_ptr(), K, [m], M, 0, out.data_ptr(), F, E.GEPI_SWIGLU_BF16, stream())
+    torch.cuda.synchronize()
+    y = A.float().cpu() @ W.to(torch.bfloat16).float().T
+    ref = torch.nn.functional.silu(y[:, 0::2]) * y[:, 1::2]
+    assert torch.allclose(out.float().cpu(), ref, atol=2e-2, rtol=2e-2), (out.float().cpu() - ref).abs().max()
+
+
+@pytest.mark.parametrize("H,Hkv,hd", [(32, 8, 128), (32, 4, 64), (8, 8, 64), (16, 8, 128), (64, 8, 128)])
+@pytest.mark.parametrize("start,T", [(0, 1), (0, 37), (70, 130), (0, 300)])
+def test_attention_prefill_causal(E, H, Hkv, hd, start, T):
+    max_ctx = 512
+    slot, slots = 1, 2
+    G = H // Hkv
+    kc = (torch.randn(slots, Hkv, max_ctx, hd) * 0.5).to(torch.bfloat16).cuda()
+    vc = torch.randn(slots, Hkv, max_ctx, hd).to(torch.bfloat16).cuda()
+    q = torch.randn(T, H, hd, device="cuda")
+    out = torch.zeros(T, H * hd, dtype=torch.bfloat16, device="cuda")
+    scale = 1 / math.sqrt(hd)
+    E.attn_prefill(q.data_ptr(), kc.data_ptr(), vc.data_ptr(), slot, start, T, H, Hkv, hd, max_ctx, scale,
+                   out.data_ptr(), H * hd, stream())
+    torch.cuda.synchronize()
+    L = start + T
+    k = kc[slot, :, :L].float().cpu().repeat_interleave(G, 0)  # [H, L, hd]
+    v = vc[slot, :, :L].float().cpu().repeat_interleave(G, 0)
+    qq = q.cpu().to(torch.bfloat16).float()
+    s = torch.einsum("thd,hld->htl", qq, k) * scale
+    pos = torch.arange(start, L)[:, None]
+    s = s.masked_fill(torch.arange(L)[None, :] > pos, float("-inf"))
+    ref = torch.einsum("htl,hld->thd", torch.softmax(s, -1), v).reshape(T, H * hd)
+    err = (out.float().cpu() - ref).abs().max().item()
+    assert err < 3e-2, err
