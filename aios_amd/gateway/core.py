@@ -288,13 +288,34 @@ class LocalRuntime(OpenAICompatible):
                 break
 
 
+def secret_keys(path: str = "") -> Dict[str, str]:
+    """Provider keys from the secrets file (`$AIOS_SECRETS` or /etc/aios/secrets.toml, TTL cache +
+    0600 check in the native SecretManager -- tools/src/secrets.rs, unwired in the reference)."""
+    path = path or os.environ.get("AIOS_SECRETS", "/etc/aios/secrets.toml")
+    if not os.path.exists(path):
+        return {}
+    try:
+        from ..core import load as load_core
+
+        sm = load_core().SecretManager(path)
+        sm.load()
+        for w in sm.warnings():
+            log.warning("secrets: %s", w)
+        return {k: v for k, v in sm.api_keys().items() if v}
+    except Exception as e:  # pragma: no cover - native core missing
+        log.warning("secrets file %s not read: %s", path, e)
+        return {}
+
+
 def providers_from_env(env=os.environ) -> Dict[str, Provider]:
+    keys = secret_keys(env.get("AIOS_SECRETS", ""))
     return {
-        "claude": Claude(env.get("CLAUDE_API_KEY", ""), env.get("CLAUDE_MODEL", "claude-sonnet-4-20250514")),
-        "openai": OpenAICompatible("openai", env.get("OPENAI_API_KEY", ""),
+        "claude": Claude(env.get("CLAUDE_API_KEY", "") or keys.get("claude", ""),
+                         env.get("CLAUDE_MODEL", "claude-sonnet-4-20250514")),
+        "openai": OpenAICompatible("openai", env.get("OPENAI_API_KEY", "") or keys.get("openai", ""),
                                    env.get("OPENAI_BASE_URL", "https://api.openai.com"),
                                    env.get("OPENAI_MODEL", "gpt-5"), 2.5, 10.0),
-        "qwen3": OpenAICompatible("qwen3", env.get("QWEN3_API_KEY", ""),
+        "qwen3": OpenAICompatible("qwen3", env.get("QWEN3_API_KEY", "") or keys.get("qwen3", ""),
                                   env.get("QWEN3_BASE_URL", "https://api.viwoapp.net"),
                                   env.get("QWEN3_MODEL", "qwen3:30b-128k")),
         "local": LocalRuntime(env.get("LOCAL_LLM_URL", "http://127.0.0.1:8082"), env.get("LOCAL_LLM_MODEL", "local"),

@@ -9,6 +9,7 @@
 #include "json.h"
 #include "memory.h"
 #include "orchestrator.h"
+#include "security.h"
 #include "tools.h"
 #include "util.h"
 
@@ -79,6 +80,7 @@ py::dict tooldef_py(const ToolDef& d) {
   o["timeout_ms"] = d.timeout_ms;
   o["rollback_tool"] = d.rollback_tool;
   o["handler_address"] = d.handler_address;
+  o["input_schema"] = d.input_schema;
   return o;
 }
 
@@ -94,6 +96,7 @@ ToolDef tooldef_from(const py::dict& o) {
   s("risk_level", d.risk_level);
   s("rollback_tool", d.rollback_tool);
   s("handler_address", d.handler_address);
+  s("input_schema", d.input_schema);
   if (o.contains("required_capabilities")) d.required_caps = o["required_capabilities"].cast<std::vector<std::string>>();
   if (o.contains("requires_confirmation")) d.requires_confirmation = o["requires_confirmation"].cast<bool>();
   if (o.contains("idempotent")) d.idempotent = o["idempotent"].cast<bool>();
@@ -450,6 +453,85 @@ PYBIND11_MODULE(_core, m) {
       .def("list", [](ScheduleStore& s) { return to_py(s.list()); })
       .def("remove", &ScheduleStore::remove)
       .def("due", [](ScheduleStore& s, int64_t now) { return to_py(s.due(now)); });
+
+  // ---------------------------------------------------------------- security / plugin runtime
+  m.def("toml_parse", [](const std::string& t) { return to_py(toml_parse(t)); });
+  m.def("schema_validate", [](py::object v, py::object schema) { return schema_validate(to_json(v), to_json(schema)); });
+  m.def("trigger_check_cron", &trigger_check_cron);
+  m.def("trigger_check_file_watch", &trigger_check_file_watch);
+  m.def("trigger_check_metric", &trigger_check_metric);
+  m.def("trigger_check_log_pattern", &trigger_check_log_pattern);
+  py::class_<SecretManager>(m, "SecretManager")
+      .def(py::init<const std::string&, int>(), py::arg("path"), py::arg("ttl_s") = 3600)
+      .def("load", &SecretManager::load)
+      .def("get", [](const SecretManager& s, const std::string& k) -> py::object {
+        std::string v;
+        if (s.get(k, v)) return py::str(v);
+        return py::none();
+      })
+      .def("get_or_reload", &SecretManager::get_or_reload)
+      .def("set", &SecretManager::set)
+      .def("wipe", &SecretManager::wipe)
+      .def("api_keys", [](SecretManager& s) { return to_py(s.api_keys()); })
+      .def("warnings", &SecretManager::warnings)
+      .def("__len__", &SecretManager::count);
+  auto rule_py = [](const FirewallRule& r) {
+    py::dict d;
+    d["name"] = r.name; d["action"] = r.action; d["direction"] = r.direction; d["protocol"] = r.protocol;
+    d["source"] = r.source; d["destination"] = r.destination; d["interface"] = r.interface;
+    d["comment"] = r.comment; d["port"] = r.port; d["port_range"] = py::make_tuple(r.port_lo, r.port_hi);
+    d["state"] = r.state;
+    return d;
+  };
+  py::class_<FirewallApplicator>(m, "FirewallApplicator")
+      .def(py::init<const std::string&, const std::string&>(), py::arg("config_path"), py::arg("backend") = "auto")
+      .def("load_config", [rule_py](const FirewallApplicator& f) {
+        std::map<std::string, std::string> pol;
+        py::list rules;
+        for (auto& r : f.load_config(&pol)) rules.append(rule_py(r));
+        return py::make_tuple(rules, pol);
+      })
+      .def("dry_run", &FirewallApplicator::dry_run)
+      .def("setup_commands", &FirewallApplicator::setup_commands)
+      .def("apply", [](FirewallApplicator& f, bool dry) { return to_py(f.apply(dry)); }, py::arg("dry_run") = true)
+      .def("record_all_applied", [](FirewallApplicator& f) {
+        for (auto& r : f.load_config()) f.record_applied(r);
+      })
+      .def("rollback_commands", &FirewallApplicator::rollback_commands)
+      .def("applied_count", &FirewallApplicator::applied_count)
+      .def_property_readonly("uses_nftables", &FirewallApplicator::uses_nftables);
+  auto trig_py = [](const PluginTrigger& t) {
+    py::dict d;
+    d["id"] = t.id; d["plugin"] = t.plugin; d["type"] = t.type; d["config"] = to_py(t.config);
+    d["enabled"] = t.enabled; d["last_fired"] = t.last_fired;
+    return d;
+  };
+  py::class_<TriggerStore>(m, "TriggerStore")
+      .def(py::init<const std::string&>())
+      .def("add", [](TriggerStore& s, const std::string& p, const std::string& t, py::object c) { return s.add(p, t, to_json(c)); })
+      .def("remove", &TriggerStore::remove)
+      .def("set_enabled", &TriggerStore::set_enabled)
+      .def("list", [trig_py](const TriggerStore& s) {
+        py::list l;
+        for (auto& t : s.list()) l.append(trig_py(t));
+        return l;
+      })
+      .def("due", [trig_py](TriggerStore& s, int64_t now, py::object metrics, py::object logs) {
+        py::list l;
+        for (auto& t : s.due(now, to_json(metrics), to_json(logs))) l.append(trig_py(t));
+        return l;
+      }, py::arg("now"), py::arg("metrics") = py::dict(), py::arg("log_lines") = py::dict());
+  py::class_<PluginWatcher>(m, "PluginWatcher")
+      .def(py::init<const std::string&>())
+      .def("poll", [](PluginWatcher& w) { return to_py(w.poll()); });
+  py::class_<TlsManager>(m, "TlsManager")
+      .def(py::init<const std::string&>())
+      .def("certs_exist", &TlsManager::certs_exist)
+      .def("generate_self_signed", [](TlsManager& t, const std::string& svc, int days) {
+        return to_py(t.generate_self_signed(svc, days));
+      }, py::arg("service") = "", py::arg("days") = 365)
+      .def("verify", [](const TlsManager& t) { return to_py(t.verify()); })
+      .def("paths", [](const TlsManager& t) { return to_py(t.paths()); });
 
   py::class_<EventBus>(m, "EventBus")
       .def(py::init<>())

@@ -29,6 +29,7 @@ struct ToolDef {
   int timeout_ms = 5000;
   std::string rollback_tool;
   std::string handler_address;             // externally registered tools (Register RPC)
+  std::string input_schema;                // JSON schema of the input ("" = unchecked); see security.h
 };
 
 struct CapCheck {

@@ -9,6 +9,7 @@
 #include <fstream>
 
 #include "tools.h"
+#include "security.h"
 
 namespace aiosn {
 
@@ -447,6 +448,7 @@ int ToolService::scan_plugins() {
     def.risk_level = "medium";
     def.timeout_ms = (int)meta.get_int("timeout_ms", 30000);
     for (auto& c : meta["capabilities"].as_arr()) def.required_caps.push_back(c.as_str());
+    if (meta["input_schema"].is_obj()) def.input_schema = meta["input_schema"].dump();
     std::lock_guard<std::mutex> g(mu_);
     if (!tools_.count(def.name)) ++n;
     tools_[def.name] = def;
@@ -466,6 +468,21 @@ ExecResult ToolService::run_pipeline(const std::string& tool, const std::string&
     r.error = "Unknown tool: " + tool;
     r.duration_ms = now_ms() - t0;
     return r;
+  }
+  // 1b. input schema (tools/src/schema.rs, unwired in the reference): a tool that declares a
+  //     schema rejects malformed input before any capability or side effect
+  if (!def.input_schema.empty()) {
+    Json schema, in = Json::object();
+    if (Json::try_parse(def.input_schema, schema) && (input_json.empty() || Json::try_parse(input_json, in))) {
+      auto errs = schema_validate(in, schema);
+      if (!errs.empty()) {
+        std::string msg;
+        for (size_t i = 0; i < errs.size() && i < 5; ++i) msg += (i ? "; " : "") + errs[i];
+        r.error = "Input validation failed: " + msg;
+        r.duration_ms = now_ms() - t0;
+        return r;
+      }
+    }
   }
   // 2. capability check (denials are audited)
   CapCheck cc = caps_.check(agent, tool);

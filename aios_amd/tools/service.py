@@ -22,6 +22,7 @@ import json
 import logging
 import os
 import signal
+import time
 from typing import Optional
 
 import grpc
@@ -41,7 +42,64 @@ def tooldef_to_pb(d: dict):
         name=d["name"], namespace=d["namespace"], version=d["version"], description=d["description"],
         required_capabilities=d["required_capabilities"], risk_level=d["risk_level"],
         requires_confirmation=d["requires_confirmation"], idempotent=d["idempotent"],
-        reversible=d["reversible"], timeout_ms=d["timeout_ms"], rollback_tool=d["rollback_tool"])
+        reversible=d["reversible"], timeout_ms=d["timeout_ms"], rollback_tool=d["rollback_tool"],
+        input_schema=d.get("input_schema", "").encode())
+
+
+class PluginRuntime:
+    """Hot reload + trigger dispatch for AI-authored plugins (one `tick()` per scan interval)."""
+
+    def __init__(self, core_svc, data: str, triggers_db: Optional[str] = None):
+        core = load_core()
+        self.svc = core_svc
+        self.plugin_dir = os.path.join(data, "plugins")
+        os.makedirs(self.plugin_dir, exist_ok=True)
+        self.watcher = core.PluginWatcher(self.plugin_dir)
+        self.triggers = core.TriggerStore(triggers_db or os.path.join(data, "data", "plugin_triggers.db"))
+        self.log_offsets: dict = {}
+        self.fired: list = []
+
+    def _metrics(self) -> dict:
+        from ..utils import sysinfo
+
+        try:
+            return sysinfo.metric_snapshot()
+        except Exception:  # pragma: no cover - platform specific
+            return {}
+
+    def _new_log_lines(self, path: str) -> list:
+        try:
+            size = os.path.getsize(path)
+        except OSError:
+            return []
+        off = self.log_offsets.get(path)
+        if off is None or off > size:  # first look: start at the end (only new lines fire)
+            self.log_offsets[path] = size
+            return []
+        with open(path, "rb") as f:
+            f.seek(off)
+            data = f.read(min(size - off, 1 << 20))
+        self.log_offsets[path] = off + len(data)
+        return data.decode(errors="replace").splitlines()
+
+    def tick(self, now: Optional[int] = None) -> dict:
+        changes = self.watcher.poll()
+        if changes["added"] or changes["changed"]:
+            self.svc.scan_plugins()
+        for name in changes["removed"]:
+            self.svc.deregister_tool(f"plugin.{name}")
+        trig = self.triggers.list()
+        logs = {t["config"]["log_path"]: self._new_log_lines(t["config"]["log_path"])
+                for t in trig if t["type"] == "log_pattern" and t["enabled"]}
+        metrics = self._metrics() if any(t["type"] == "metric_threshold" for t in trig) else {}
+        due = self.triggers.due(int(now if now is not None else time.time()), metrics, logs)
+        for t in due:
+            tool = t["plugin"] if t["plugin"].startswith("plugin.") else f"plugin.{t['plugin']}"
+            payload = json.dumps({"trigger": {"id": t["id"], "type": t["type"], "config": t["config"]}})
+            r = self.svc.execute(tool, "autonomy-loop", f"trigger-{t['id']}", payload.encode(), f"{t['type']} trigger")
+            self.fired.append({"trigger": t["id"], "tool": tool, "success": r["success"]})
+            log.info("trigger %s (%s) fired %s: %s", t["id"], t["type"], tool, "ok" if r["success"] else r["error"])
+        return {"changes": changes, "fired": [t["id"] for t in due]}
 
 
 class ToolRegistryService:
@@ -101,7 +159,8 @@ class ToolRegistryService:
             "description": t.description, "required_capabilities": list(t.required_capabilities),
             "risk_level": t.risk_level or "medium", "requires_confirmation": t.requires_confirmation,
             "idempotent": t.idempotent, "reversible": t.reversible, "timeout_ms": t.timeout_ms or 30000,
-            "rollback_tool": t.rollback_tool, "handler_address": req.handler_address})
+            "rollback_tool": t.rollback_tool, "handler_address": req.handler_address,
+            "input_schema": t.input_schema.decode(errors="replace") if t.input_schema else ""})
         log.info("register %s -> %s (%s)", t.name, req.handler_address or "local", "ok" if ok else err)
         return pb.tools.RegisterToolResponse(accepted=ok, error=err)
 
@@ -111,13 +170,17 @@ class ToolRegistryService:
 
     # ---------------------------------------------------------------- background
     async def plugin_scan_loop(self, stop: asyncio.Event):
+        """Plugin runtime (tools/src/plugin/mod.rs:107-219, events.rs, triggers.rs -- defined but
+        never started in the reference): hot reload from the plugin directory (new / changed
+        plugins are (re)registered, deleted ones deregistered) and trigger dispatch (cron,
+        file_watch, log_pattern, metric_threshold) executing the plugin through the normal
+        capability / audit pipeline as `autonomy-loop`."""
+        runtime = PluginRuntime(self.core, self.data_dir)
         while not stop.is_set():
             try:
-                n = await self._run(self.core.scan_plugins)
-                if n:
-                    log.info("plugin scan registered %d new plugin tools", n)
+                await self._run(runtime.tick)
             except Exception as e:  # pragma: no cover - defensive
-                log.warning("plugin scan failed: %s", e)
+                log.warning("plugin runtime tick failed: %s", e)
             try:
                 await asyncio.wait_for(stop.wait(), PLUGIN_SCAN_INTERVAL)
             except asyncio.TimeoutError:

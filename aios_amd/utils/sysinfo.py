@@ -110,3 +110,16 @@ def snapshot() -> dict:
     return {"cpu_percent": cpu_percent(), "memory_used_mb": used, "memory_total_mb": total,
             "disk_used_gb": du, "disk_total_gb": dt, "gpu_utilization": gpu_utilization(),
             "load_avg": load_avg(), "uptime_s": uptime_s(), "timestamp": int(time.time())}
+
+
+def metric_snapshot() -> dict:
+    """Flat metric map for plugin metric_threshold triggers (operational-memory metric keys)."""
+    used, total = memory_mb()
+    out = {"cpu.usage": cpu_percent(), "memory.used_mb": used, "memory.total_mb": total,
+           "memory.percent": 100.0 * used / total if total else 0.0, "disk.percent": disk_percent("/"),
+           "load.1m": (load_avg() or [0.0])[0], "uptime.seconds": uptime_s()}
+    try:
+        out["gpu.utilization"] = gpu_utilization()
+    except Exception:  # pragma: no cover - no GPU sysfs
+        pass
+    return out
