@@ -133,6 +133,7 @@ class Engine {
 
   EngineConfig cfg_;
   hipStream_t stream_ = nullptr;
+
   bool finalized_ = false;
   std::vector<void*> allocs_;
   size_t weight_bytes_ = 0, kv_bytes_ = 0, ws_bytes_ = 0;

@@ -1,6 +1,7 @@
 // Engine implementation -- see engine.h.
 #include "engine.h"
 #include <cstdlib>
+#include <map>
 
 #include <algorithm>
 #include <cstring>
@@ -43,6 +44,7 @@ static bool native_qtype(int qt) {
 Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
   HIP_CHECK(hipSetDevice(cfg_.device));
   HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+
   layers_.resize(cfg_.n_layers);
   if (cfg_.max_batch < 1 || cfg_.max_batch > 8) throw std::runtime_error("max_batch must be 1..8");
   if (cfg_.max_slots < cfg_.max_batch) cfg_.max_slots = cfg_.max_batch;
@@ -449,6 +451,24 @@ void Engine::allreduce(float* p, size_t n, float* residual) {
   }
 }
 
+// decode GEMV tuning knobs from the environment (read once): AIOS_GEMV_{U,GRID,KSPLIT}_{QKV,O,GU,DOWN,LM}
+// -- in-situ sweeps of the captured decode step (tools/gemv_knob_sweep.sh); 0 = the launcher's choice
+static int gemv_knob(const char* what, const char* kind) {
+  static std::map<std::string, int> cache;
+  const std::string key = std::string("AIOS_GEMV_") + what + "_" + kind;
+  auto it = cache.find(key);
+  if (it != cache.end()) return it->second;
+  const char* e = std::getenv(key.c_str());
+  const int v = e ? std::atoi(e) : 0;
+  cache[key] = v;
+  return v;
+}
+static void apply_knobs(GemvArgs& a, const char* kind) {
+  a.tune_u = gemv_knob("U", kind);
+  a.tune_grid = gemv_knob("GRID", kind);
+  a.tune_ksplit = gemv_knob("KSPLIT", kind);
+}
+
 void Engine::gemv(const std::vector<const QMat*>& segs, int N, int K, int B, const float* x, int ldx,
                   const float* norm_w, float* y, int ldy, int epi, int layer) {
   GemvArgs a;
@@ -486,6 +506,7 @@ void Engine::gemv(const std::vector<const QMat*>& segs, int N, int K, int B, con
     a.k_cache = k_cache_ + (size_t)layer * layer_kv_elems_;
     a.v_cache = v_cache_ + (size_t)layer * layer_kv_elems_;
   }
+  apply_knobs(a, K == cfg_.d_ff ? "DOWN" : (N == 2 * cfg_.d_ff ? "GU" : (N == cfg_.vocab_size ? "LM" : "O")));
   launch_gemv(a, stream_);
 }
 
@@ -528,6 +549,7 @@ void Engine::layer_decode(int l, int B) {
       } else {
         a.epi = EPI_STORE; a.y = qkv_; a.ldy = qd + 2 * kvd;
       }
+      apply_knobs(a, "QKV");
       launch_gemv(a, stream_);
       row0 += n;
     }

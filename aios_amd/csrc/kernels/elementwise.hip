@@ -248,3 +248,4 @@ void launch_sample(const SampleArgs& a, hipStream_t st) {
 }
 
 }  // namespace aios
+

@@ -709,7 +709,9 @@ bool launch_gemv_q8(GemvArgs a, hipStream_t st) {
         // except the mid-sized Q4_K/Q5_K projections; the whole K slice in flight for long K
         // (U = 1 for the small/huge-N shapes won in the eager sweep but lost 2-3 % inside the
         // captured decode step, so the whole-K-slice rule stays)
-        u = nch <= 512 ? (nch + 63) / 64 : 2;
+        // (re-swept in the captured step, tools/gemv_knob_sweep.sh: U = 1 for K = 4096 gate/up
+        // +1.8 %, QKV +1 %, O / lm_head neutral)
+        u = nch <= 128 ? 1 : (nch <= 512 ? (nch + 63) / 64 : 2);
       }
       switch (u) {
         case 13: launch_q8_rows<QT0, QT1, 1, 3, 2>(a, lds, st); break;  // tuning: U = 3/4 double-buffered

@@ -28,6 +28,7 @@ void launch_rmsnorm_bf16(const float* x, int ldx, const float* w, bf16_t* y, int
                          hipStream_t st);
 void launch_f32_to_bf16(const float* x, bf16_t* y, size_t n, hipStream_t st);
 void launch_add(float* y, const float* x, size_t n, hipStream_t st);
+
 // out[b][i] = silu(gu[b][2i]) * gu[b][2i+1]
 void launch_swiglu_interleaved(const float* gu, int ldg, float* out, int ldo, int rows, int n, hipStream_t st);
 

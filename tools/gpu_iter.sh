@@ -1,12 +1,11 @@
-# one GPU iteration (used through gpurun): kernel tests, engine tests, probes, bench, profile
+# one GPU iteration (used through gpurun): kernel tests, engine tests, bench, profile
 set -u
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 run() { local name=$1 t=$2; shift 2; timeout -k 10 $t "$@" > gpurun_out/$name.log 2>&1; local rc=$?; grep -v amdgpu.ids gpurun_out/$name.log | tail -${TAILN:-3}; [ $rc -eq 0 ] || { echo "[$name] rc=$rc"; tail -40 gpurun_out/$name.log; exit 1; }; }
-run t_new 500 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "attention"
+run t_kern 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py
 run t_eng 500 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_engine_gpu.py
-TAILN=12 run probe 200 python tools/attn_probe.py
-run bench 300 python bench.py --steps 128 --warmup 16
+run bench 300 python bench.py
 timeout -k 10 400 bash tools/prof_decode.sh > /dev/null 2>&1 || exit 1
-head -10 gpurun_out/prof_summary.txt
+head -12 gpurun_out/prof_summary.txt
