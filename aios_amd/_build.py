@@ -115,16 +115,25 @@ def _sqlite_lib() -> str:
     raise RuntimeError("libsqlite3.so.0 not found")
 
 
-def build_core(verbose: bool = True, jobs: int | None = None) -> Path:
+def core_sanitized_path(sanitize: str) -> Path:
+    return ROOT / "build" / ("core-" + sanitize.replace(",", "-")) / ("_core" + ext_suffix())
+
+
+def build_core(verbose: bool = True, jobs: int | None = None, sanitize: str = "") -> Path:
     """Host-only C++17 build of aios_amd/native (tools / memory / orchestrator cores + bindings)
-    into `aios_amd/_core*.so`, linked against the system libsqlite3 and OpenSSL libcrypto."""
+    into `aios_amd/_core*.so`, linked against the system libsqlite3 and OpenSSL libcrypto.
+
+    sanitize="address,undefined" builds an instrumented copy under build/core-address-undefined/
+    instead (loaded by aios_amd.core when AIOS_CORE_SO points at it; scripts/sanitize.sh)."""
     import pybind11
 
     cxx = os.environ.get("CXX") or shutil.which("g++") or "g++"
-    out_dir = ROOT / "build" / "core"
+    out_dir = ROOT / "build" / ("core" + ("-san-" + sanitize.replace(",", "-") if sanitize else ""))
     out_dir.mkdir(parents=True, exist_ok=True)
     flags = ["-std=c++17", "-O2", "-fPIC", "-fvisibility=hidden", "-Wall", "-Wno-unused-function",
              f"-I{NATIVE}", f"-I{pybind11.get_include()}", f"-I{sysconfig.get_paths()['include']}"]
+    san = [f"-fsanitize={sanitize}", "-fno-omit-frame-pointer", "-g"] if sanitize else []
+    flags += san
     srcs = sorted(NATIVE.glob("*.cpp"))
     hdrs = list(NATIVE.glob("*.h"))
 
@@ -141,11 +150,12 @@ def build_core(verbose: bool = True, jobs: int | None = None) -> Path:
     jobs = jobs or min(len(srcs), max(1, (os.cpu_count() or 4)), 16)
     with cf.ThreadPoolExecutor(jobs) as ex:
         objs = list(ex.map(comp, srcs))
-    out = core_target_path()
+    out = core_sanitized_path(sanitize) if sanitize else core_target_path()
+    out.parent.mkdir(parents=True, exist_ok=True)
     newest = max(o.stat().st_mtime for o in objs)
     if not out.exists() or out.stat().st_mtime < newest:
         tmp = out.with_suffix(".tmp.so")
-        cmd = [cxx, "-shared", "-fPIC", "-o", str(tmp), *map(str, objs), _sqlite_lib(), "-lcrypto", "-lpthread"]
+        cmd = [cxx, "-shared", "-fPIC", *san, "-o", str(tmp), *map(str, objs), _sqlite_lib(), "-lcrypto", "-lpthread"]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"core link failed:\n{r.stderr[-6000:]}")

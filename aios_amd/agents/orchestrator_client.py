@@ -24,7 +24,16 @@ class OrchestratorClient:
     def __init__(self, address: Optional[str] = None, timeout: float = 30.0):
         self.address = (address or os.getenv("AIOS_ORCHESTRATOR_ADDR", "127.0.0.1:50051")).replace(
             "localhost", "127.0.0.1")
-        self.stub = Stub(channel(self.address), "aios.orchestrator.Orchestrator", timeout=timeout)
+        self.timeout = timeout
+        self._stub = None
+
+    @property
+    def stub(self) -> Stub:
+        # grpc.aio channels bind to the running event loop: create lazily on first use, so a client
+        # can be constructed outside a loop (agents are built before asyncio.run)
+        if self._stub is None:
+            self._stub = Stub(channel(self.address), "aios.orchestrator.Orchestrator", timeout=self.timeout)
+        return self._stub
 
     async def submit_goal(self, description: str, priority: int = 5, source: str = "agent",
                           tags: Optional[List[str]] = None, metadata: Optional[Dict[str, Any]] = None) -> str:

@@ -6,7 +6,9 @@ import on a fresh checkout compiles it in-tree (≈20 s) unless AIOS_NO_AUTOBUIL
 from __future__ import annotations
 
 import importlib
+import importlib.util
 import os
+import sys
 
 _mod = None
 
@@ -14,6 +16,13 @@ _mod = None
 def load(build_if_missing: bool = True):
     global _mod
     if _mod is not None:
+        return _mod
+    so = os.environ.get("AIOS_CORE_SO")  # e.g. the sanitizer build (scripts/sanitize.sh)
+    if so:
+        spec = importlib.util.spec_from_file_location("aios_amd._core", so)
+        _mod = importlib.util.module_from_spec(spec)
+        sys.modules["aios_amd._core"] = _mod
+        spec.loader.exec_module(_mod)
         return _mod
     try:
         _mod = importlib.import_module("aios_amd._core")

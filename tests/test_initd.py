@@ -16,6 +16,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def initd():
     from aios_amd import _build
 
+    if os.environ.get("AIOS_INIT_BIN"):  # e.g. the ASan/UBSan build from scripts/sanitize.sh
+        return os.environ["AIOS_INIT_BIN"]
     return str(_build.build_initd(verbose=False))
 
 
