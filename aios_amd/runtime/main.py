@@ -16,6 +16,8 @@ import os
 import signal
 from pathlib import Path
 
+from ..rpc.client import Stub, channel
+from ..rpc.schema import pb
 from ..rpc.server import RpcServer
 from .model_manager import ModelManager
 from .service import AIRuntimeService
@@ -40,11 +42,27 @@ async def auto_load(svc: AIRuntimeService, model_dir: str):
             await svc.start_http(m)
 
 
-async def health_loop(mgr: ModelManager, stop: asyncio.Event):
+async def publish_metrics(mgr: ModelManager, addr: str):
+    """Best effort: runtime metrics -> MemoryService.UpdateMetric (the reference's operational
+    store has a `gpu.utilization` key that no producer ever writes)."""
+    try:
+        stub = Stub(channel(addr), "aios.memory.MemoryService", timeout=2.0)
+        for k, v in mgr.metrics().items():
+            await stub.UpdateMetric(pb.memory.MetricUpdate(key=k, value=float(v)))
+    except Exception as e:  # noqa: BLE001 - memory service not up
+        log.debug("metric publish skipped: %s", e)
+
+
+async def health_loop(mgr: ModelManager, stop: asyncio.Event, memory_addr: str = ""):
+    """10 s health pass (runtime/src/main.rs:55-63): supervision (dead scheduler / engine error /
+    decode stall -> error -> bounded auto-reload) and metric publication."""
+    memory_addr = memory_addr or os.environ.get("AIOS_MEMORY_ADDR", "127.0.0.1:50053")
     while not stop.is_set():
-        for m in mgr.list_models():
-            if m.status == "ready" and m.scheduler is not None and not m.scheduler.thread.is_alive():
-                m.status, m.error = "error", "scheduler thread died"
+        try:
+            await mgr.supervise()
+        except Exception:  # noqa: BLE001
+            log.exception("supervision pass failed")
+        await publish_metrics(mgr, memory_addr)
         try:
             await asyncio.wait_for(stop.wait(), HEALTH_CHECK_INTERVAL)
         except asyncio.TimeoutError:
@@ -67,6 +85,9 @@ async def amain(args):
     await health_loop(mgr, stop)
     await server.stop()
     await svc.close()
+    stuck = mgr.join_abandoned(5.0)
+    if stuck:
+        log.warning("%d stalled engine thread(s) still blocked at shutdown", stuck)
 
 
 def main(argv=None):

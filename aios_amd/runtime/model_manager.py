@@ -21,6 +21,8 @@ import threading
 import time
 from typing import Dict, List, Optional
 
+from .faults import FaultSpec, FaultyEngine
+
 log = logging.getLogger("aios.runtime.models")
 
 BASE_PORT = 8080  # runtime/src/model_manager.rs:70
@@ -60,6 +62,9 @@ class ManagedModel:
     config: object = None
     weight_bytes: int = 0
     kv_bytes: int = 0
+    backend: str = "gpu"
+    requested_ctx: int = 0
+    restarts: list = dataclasses.field(default_factory=list)  # reload timestamps (restart window)
 
     def status_string(self) -> str:
         return f"error: {self.error}" if self.status == "error" else self.status
@@ -82,6 +87,7 @@ class ModelManager:
         self.max_slots = max_slots
         self.base_port = base_port
         self.models: Dict[str, ManagedModel] = {}
+        self.abandoned: list = []  # schedulers of stalled engines (their threads may still be stuck)
         self._lock = threading.Lock()
         self.started = time.time()
 
@@ -112,7 +118,12 @@ class ModelManager:
             m = self.models.get(name)
             if m is not None and m.status in ("ready", "loading"):
                 return m  # idempotent (model_manager.rs:152-157)
-            m = ManagedModel(name=name, path=path, status="loading", port=self.allocate_port(port))
+            restarts = m.restarts if m is not None else []
+            keep_port = m.port if m is not None and not port else port
+            if m is not None:  # reload of an errored / unloading model: its port is free again
+                self.models.pop(name, None)
+            m = ManagedModel(name=name, path=path, status="loading", port=self.allocate_port(keep_port),
+                             requested_ctx=context_length, restarts=restarts)
             self.models[name] = m
         try:
             await asyncio.to_thread(self._load_blocking, m, context_length)
@@ -135,7 +146,13 @@ class ModelManager:
         from ..parallel.tp import launch_tp, parse_spec
 
         base, tp, act_q8 = parse_spec(m.path)
-        if tp > 1:
+        faults = FaultSpec.from_env(m.name)
+        if faults is not None:
+            faults.check("load")
+        base, cpu = self._backend(base, "cpu" in m.path.partition("#")[2].split("&"))
+        if cpu:
+            self._load_cpu(m, base, context_length)
+        elif tp > 1:
             # strategic tier: tensor parallel over the node's GPUs (ranks 1..tp-1 are worker
             # processes; the xGMI all-reduce runs inside each rank's captured decode graph)
             ctx = context_length or 4096
@@ -169,13 +186,136 @@ class ModelManager:
                                            device=self.device, name=m.name, act_q8=act_q8)
             tok = from_gguf(reader)
             tmpl = chat_template.for_model(reader, tok)
-        m.engine, m.config, m.tokenizer, m.template = eng, cfg, tok, tmpl
+        if not cpu:
+            m.engine, m.config, m.tokenizer, m.template = eng, cfg, tok, tmpl
+        if faults is not None:
+            m.engine = FaultyEngine(m.engine, faults)
+        eng, tok = m.engine, m.tokenizer
         m.context_length = eng.config.max_ctx
         m.grammar = E.JsonGrammar(tok.all_token_bytes(), tok.eos_id)
         from .scheduler import Scheduler
 
-        m.scheduler = Scheduler(eng, tok, self.max_batch, self.max_slots, m.context_length, m.grammar, name=m.name)
+        slots = getattr(eng.config, "max_slots", self.max_slots)
+        batch = getattr(eng.config, "max_batch", self.max_batch)
+        m.scheduler = Scheduler(eng, tok, min(batch, self.max_batch), min(slots, self.max_slots), m.context_length,
+                                m.grammar, name=m.name)
         m.weight_bytes, m.kv_bytes = eng.weight_bytes, eng.kv_bytes
+
+    # ------------------------------------------------------------------ CPU backend
+    @staticmethod
+    def _backend(base: str, cpu_flag: bool = False):
+        """'<path>#cpu' / AIOS_RUNTIME_DEVICE=cpu / no GPU -> the CPU engine (reference default:
+        llama-server with gpu_layers 0)."""
+        cpu = cpu_flag or os.environ.get("AIOS_RUNTIME_DEVICE", "") == "cpu"
+        if not cpu:
+            from . import native
+
+            cpu = not native.gpu_available()
+        return base, cpu
+
+    def _load_cpu(self, m: ManagedModel, base: str, context_length: int):
+        from ..gguf.reader import GGUFReader
+        from ..models.config import get_preset
+        from ..models.synthetic import synthetic_vocab, write_synthetic_gguf
+        from . import chat_template
+        from .cpu_engine import CpuEngine
+        from .tokenizer import SpmTokenizer, from_gguf
+
+        slots = min(self.max_slots, 4)
+        if base.startswith("synthetic:"):
+            parts = base.split(":")
+            cfg = get_preset(parts[1])
+            recipe = parts[2] if len(parts) > 2 else "Q4_0"
+            import tempfile
+
+            path = os.path.join(tempfile.gettempdir(), f"aios-cpu-{parts[1]}-{recipe}.gguf")
+            if not os.path.exists(path):
+                write_synthetic_gguf(path, cfg, recipe, seed=abs(hash(m.name)) % 1000)
+            ctx = context_length or min(cfg.max_ctx, 2048)
+            eng = CpuEngine.from_gguf(path, max_ctx=ctx, max_slots=slots, max_batch=min(self.max_batch, slots))
+            toks, scores, types = synthetic_vocab(cfg.vocab_size)
+            tok = SpmTokenizer(toks, scores, types, cfg.bos_id, cfg.eos_id)
+            tmpl = chat_template.for_model(cfg.chat_template if cfg.chat_template in chat_template.BUILTIN
+                                           else "zephyr", tok)
+        else:
+            if not os.path.exists(base):
+                raise FileNotFoundError(base)
+            ctx = context_length or context_for_size(os.path.getsize(base))
+            eng = CpuEngine.from_gguf(base, max_ctx=ctx, max_slots=slots, max_batch=min(self.max_batch, slots))
+            reader = GGUFReader(base)
+            tok = from_gguf(reader)
+            tmpl = chat_template.for_model(reader, tok)
+            cfg = eng.cfg
+        m.engine, m.config, m.tokenizer, m.template = eng, cfg, tok, tmpl
+        m.backend = "cpu"
+
+    # ------------------------------------------------------------------ supervision
+    async def supervise(self, stall_timeout_s: float = 0.0, auto_recover: Optional[bool] = None,
+                        max_restarts: int = 3, window_s: float = 300.0) -> List[str]:
+        """Health pass (the reference's 10 s loop, `model_manager.rs:393-447`): a dead scheduler
+        thread, an engine error or a stalled decode (no progress for stall_timeout_s with work
+        pending) marks the model `error`.  Unlike the reference, an errored model is reloaded
+        (AIOS_RUNTIME_AUTORECOVER, default on) at most max_restarts times per window_s; a stalled
+        engine's thread is abandoned (a hung device call cannot be interrupted) and its pending
+        requests are failed.  Returns the names of models reloaded in this pass."""
+        if auto_recover is None:
+            auto_recover = os.environ.get("AIOS_RUNTIME_AUTORECOVER", "1") != "0"
+        stall_timeout_s = stall_timeout_s or float(os.environ.get("AIOS_DECODE_STALL_S", "120"))
+        recovered = []
+        for m in list(self.models.values()):
+            if m.status == "ready" and m.scheduler is not None:
+                sch = m.scheduler
+                reason = ""
+                if not sch.thread.is_alive():
+                    reason = "scheduler thread died"
+                elif sch.failed:
+                    reason = f"engine failure: {sch.failed}"
+                elif sch.stalled(stall_timeout_s):
+                    reason = f"decode stalled for more than {stall_timeout_s:.0f} s"
+                if reason:
+                    log.error("model %s -> error: %s", m.name, reason)
+                    m.status, m.error = "error", reason
+                    self._abandon(m, stalled="stalled" in reason)
+            if m.status == "error" and auto_recover:
+                now = time.time()
+                m.restarts[:] = [t for t in m.restarts if now - t < window_s]
+                if len(m.restarts) >= max_restarts:
+                    continue
+                m.restarts.append(now)
+                log.warning("reloading model %s (restart %d in window)", m.name, len(m.restarts))
+                nm = await self.load_model(m.name, m.path, m.requested_ctx, m.port)
+                if nm.status == "ready":
+                    recovered.append(m.name)
+        return recovered
+
+    def _abandon(self, m: ManagedModel, stalled: bool):
+        sch = m.scheduler
+        m.scheduler = None
+        if sch is None:
+            return
+        self.abandoned.append(sch)
+        from .scheduler import GenResult
+
+        with sch.cv:
+            sch.stop_flag = True
+            pending = list(sch.queue)
+            sch.queue.clear()
+            active = list(sch.active) if stalled else []
+            sch.cv.notify()
+        for r in pending:
+            sch._done(r, GenResult("", [], len(r.prompt_ids), 0, "error", error=m.error))
+        for seq in active:  # the stuck thread never returns to finish them
+            sch._done(seq.req, GenResult("", list(seq.out), len(seq.req.prompt_ids), len(seq.out), "error",
+                                         error=m.error))
+        m.engine = None
+
+    def join_abandoned(self, timeout_s: float = 10.0) -> int:
+        """Wait (bounded) for abandoned scheduler threads to exit; returns how many are still stuck."""
+        deadline = time.time() + timeout_s
+        for sch in self.abandoned:
+            sch.thread.join(max(0.0, deadline - time.time()))
+        self.abandoned = [s for s in self.abandoned if s.thread.is_alive()]
+        return len(self.abandoned)
 
     async def unload_model(self, name: str) -> bool:
         m = self.models.get(name)
@@ -249,9 +389,33 @@ class ModelManager:
             extra = ""
             if m.scheduler is not None:
                 st = m.scheduler.stats
-                avg_b = st["batch_sum"] / st["steps"] if st["steps"] else 0.0
-                extra = (f",queue={len(m.scheduler.queue)},active={len(m.scheduler.active)},tokens={st['tokens']}"
-                         f",avg_batch={avg_b:.2f},prefix_hit_tokens={st['cached_tokens']}")
+                mt = m.scheduler.metrics()
+                extra = (f",backend={m.backend},queue={mt['queued']},active={mt['active']},tokens={st['tokens']}"
+                         f",avg_batch={mt['avg_batch']:.2f},prefix_hit_tokens={mt['prefix_hit_tokens']}"
+                         f",tok_s={mt['tokens_per_s']:.1f},ttft_p50_ms={mt['ttft_p50_ms']:.1f}"
+                         f",itl_ms={mt['itl_ms']:.2f},kv_slot_util={mt['kv_slot_util']:.2f},errors={mt['errors']}")
+            if m.restarts:
+                extra += f",restarts={len(m.restarts)}"
             details[f"model:{name}"] = (f"{m.status_string()},port={m.port},hbm_gb={(m.weight_bytes + m.kv_bytes) / 1e9:.2f}"
                                         + extra)
         return details
+
+    def metrics(self) -> Dict[str, float]:
+        """Aggregate runtime metrics for MemoryService.UpdateMetric (operational memory keys)."""
+        out = {"runtime.models_ready": float(sum(m.status == "ready" for m in self.models.values())),
+               "runtime.tokens_per_s": 0.0, "runtime.active_requests": 0.0,
+               "runtime.hbm_gb": sum((m.weight_bytes + m.kv_bytes) for m in self.models.values()) / 1e9}
+        for m in self.models.values():
+            if m.scheduler is not None:
+                mt = m.scheduler.metrics()
+                out["runtime.tokens_per_s"] += mt["tokens_per_s"]
+                out["runtime.active_requests"] += mt["active"]
+                out[f"runtime.{m.name}.ttft_p50_ms"] = mt["ttft_p50_ms"]
+                out[f"runtime.{m.name}.itl_ms"] = mt["itl_ms"]
+        try:
+            from ..utils import sysinfo
+
+            out["gpu.utilization"] = sysinfo.gpu_utilization()
+        except Exception:  # pragma: no cover
+            pass
+        return out

@@ -97,7 +97,14 @@ class Scheduler:
         self.active: List[_Seq] = []
         self.cv = threading.Condition()
         self.stop_flag = False
-        self.stats = dict(requests=0, tokens=0, prefill_tokens=0, cached_tokens=0, steps=0, batch_sum=0)
+        self.stats = dict(requests=0, tokens=0, prefill_tokens=0, cached_tokens=0, steps=0, batch_sum=0, errors=0)
+        # health / metrics (ModelManager.supervise and HealthCheck details)
+        self.max_slots = max_slots
+        self.last_progress = time.time()   # last completed admission or decode step
+        self.failed = ""                   # last engine error (a device fault leaves the engine unusable)
+        self._ttft = collections.deque(maxlen=256)
+        self._step_ms = collections.deque(maxlen=256)
+        self._tok_times = collections.deque(maxlen=4096)
         self.thread = threading.Thread(target=self._run, name=f"sched-{name}", daemon=True)
         self.thread.start()
 
@@ -137,14 +144,22 @@ class Scheduler:
             for r in admit:
                 try:
                     self._admit(r)
-                except Exception as e:  # noqa: BLE001 - reported to the caller
+                    self.last_progress = time.time()
+                except ValueError as e:  # request error (e.g. prompt too long): the engine is fine
+                    self._done(r, GenResult("", [], len(r.prompt_ids), 0, "error", error=str(e)))
+                except Exception as e:  # noqa: BLE001 - engine failure: reported to the caller
                     log.exception("admission failed")
+                    self._engine_failed(e)
                     self._done(r, GenResult("", [], len(r.prompt_ids), 0, "error", error=str(e)))
             if self.active:
                 try:
+                    t0 = time.time()
                     self._step()
+                    self.last_progress = time.time()
+                    self._step_ms.append((self.last_progress - t0) * 1e3)
                 except Exception as e:  # noqa: BLE001
                     log.exception("decode step failed")
+                    self._engine_failed(e)
                     for s in list(self.active):
                         self._finish(s, "error", str(e))
 
@@ -201,6 +216,7 @@ class Scheduler:
         seq.out.append(tok)
         seq.last = tok
         self.stats["tokens"] += 1
+        self._tok_times.append(time.time())
         if r.on_delta is not None:
             text = self.tok.decode(seq.out)
             if not text.endswith("�"):
@@ -218,6 +234,28 @@ class Scheduler:
             self._finish(seq, "deadline")
             return False
         return True
+
+    def _engine_failed(self, e: BaseException):
+        self.stats["errors"] += 1
+        self.failed = f"{type(e).__name__}: {e}"
+
+    def stalled(self, timeout_s: float) -> bool:
+        """Work is pending but nothing completed for timeout_s (a hung device call)."""
+        return bool(self.active or self.queue) and time.time() - self.last_progress > timeout_s
+
+    def metrics(self) -> dict:
+        now = time.time()
+        while self._tok_times and now - self._tok_times[0] > 10.0:
+            self._tok_times.popleft()
+        ttft = sorted(self._ttft)
+        st = self.stats
+        return {"tokens_per_s": len(self._tok_times) / 10.0,
+                "ttft_p50_ms": ttft[len(ttft) // 2] if ttft else 0.0,
+                "itl_ms": sum(self._step_ms) / len(self._step_ms) if self._step_ms else 0.0,
+                "active": len(self.active), "queued": len(self.queue),
+                "kv_slot_util": len(self.active) / max(1, self.max_slots),
+                "avg_batch": st["batch_sum"] / st["steps"] if st["steps"] else 0.0,
+                "prefix_hit_tokens": st["cached_tokens"], "errors": st["errors"]}
 
     def _step(self):
         B = len(self.active)
@@ -249,6 +287,8 @@ class Scheduler:
         if r.on_delta is not None and len(text) > len(seq.emitted):
             r.on_delta(text[len(seq.emitted):])
         now = time.time()
+        if seq.t_first:
+            self._ttft.append((seq.t_first - r.submitted_at) * 1e3)
         self._done(r, GenResult(
             text=text, token_ids=list(seq.out), prompt_tokens=len(r.prompt_ids), completion_tokens=len(seq.out),
             finish_reason=reason, ttft_ms=(seq.t_first - r.submitted_at) * 1e3 if seq.t_first else 0.0,
