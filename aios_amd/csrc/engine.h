@@ -169,6 +169,11 @@ class Engine {
   float *gm_x_ = nullptr, *gm_qkv_ = nullptr, *gm_q_ = nullptr, *gm_part_ = nullptr;
   bf16_t *gm_a16_ = nullptr, *gm_ff16_ = nullptr, *gm_attn16_ = nullptr;
   int *gm_tokens_ = nullptr, *gm_pos_ = nullptr, *gm_slot_ = nullptr;
+  // batched decode through the MFMA GEMM (B >= dec_gemm_min_b_): bf16 activation buffers
+  int dec_gemm_min_b_ = 8;
+  bf16_t *dec_a16_ = nullptr, *dec_ff16_ = nullptr;
+  float* dec_gu_ = nullptr;  // [max_batch][2 d_ff] fp32 gate/up (split-K GEMM, then SwiGLU -> bf16)
+  void layer_decode_gemm(int l, int B);
   int *pf_tokens_ = nullptr, *pf_pos_ = nullptr, *pf_seqlen_ = nullptr, *pf_slot_ = nullptr;
 
   std::map<int, hipGraphExec_t> graphs_;

@@ -46,7 +46,8 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
   HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
 
   layers_.resize(cfg_.n_layers);
-  if (cfg_.max_batch < 1 || cfg_.max_batch > 8) throw std::runtime_error("max_batch must be 1..8");
+  // B <= 8 decodes through the fused GEMVs; larger batches (up to 64) through the MFMA GEMM path
+  if (cfg_.max_batch < 1 || cfg_.max_batch > 64) throw std::runtime_error("max_batch must be 1..64");
   if (cfg_.max_slots < cfg_.max_batch) cfg_.max_slots = cfg_.max_batch;
 }
 
@@ -435,6 +436,12 @@ void Engine::finalize() {
       gm_tokens_ = ibuf(G);
       gm_pos_ = ibuf(G);
       gm_slot_ = ibuf(G);
+      if (const char* e = std::getenv("AIOS_DECODE_GEMM_MIN_B")) dec_gemm_min_b_ = std::atoi(e);
+      if (Bm >= 2) {
+        dec_a16_ = (bf16_t*)dmalloc((size_t)Bm * std::max(d, qd) * 2);
+        dec_ff16_ = (bf16_t*)dmalloc((size_t)Bm * cfg_.d_ff * 2);
+        dec_gu_ = fbuf((size_t)Bm * 2 * cfg_.d_ff);
+      }
     }
   }
   ws_bytes_ = ws;
@@ -520,7 +527,68 @@ static std::vector<std::vector<const QMat*>> qkv_groups(const LayerW& L) {
 
 // one transformer block for the B rows staged in x_ (decode) -- also used by prefill with
 // pointers swapped in (see prefill()).
+// Batched decode (B >= dec_gemm_min_b_): the GEMV kernels' VALU dot work grows with B while the
+// weight stream does not, so for several concurrent sequences the projections go through the
+// prefill MFMA GEMM instead (split-K for the small-N ones), with explicit RMSNorm -> bf16 and
+// RoPE/KV-write launches in place of the GEMV prologue / epilogue fusions.
+void Engine::layer_decode_gemm(int l, int B) {
+  const LayerW& L = layers_[l];
+  const int d = cfg_.d_model, hd = cfg_.head_dim, H = cfg_.n_heads, Hkv = cfg_.n_kv_heads, ff = cfg_.d_ff;
+  const int qd = H * hd, kvd = Hkv * hd, ldqkv = qd + 2 * kvd;
+  const bool tp = cfg_.tp_size > 1;
+  bf16_t* kc = k_cache_ + (size_t)l * layer_kv_elems_;
+  bf16_t* vc = v_cache_ + (size_t)l * layer_kv_elems_;
+  launch_rmsnorm_bf16(x_, d, L.attn_norm, dec_a16_, d, B, d, cfg_.norm_eps, stream_);
+  GemmQArgs g;
+  std::memset(&g, 0, sizeof(g));
+  g.A = dec_a16_; g.lda = d; g.M = B; g.K = d; g.nseg = 3;
+  g.seg[0] = L.wq.w; g.seg[1] = L.wk.w; g.seg[2] = L.wv.w;
+  g.seg_n0[0] = 0; g.seg_n0[1] = qd; g.seg_n0[2] = qd + kvd;
+  g.N = ldqkv; g.C = qkv_; g.ldc = ldqkv; g.epi = GEPI_STORE;
+  launch_gemm_q(g, stream_);
+  QkvPostArgs p;
+  p.qkv = qkv_; p.ldqkv = ldqkv; p.T = B;
+  p.n_heads = H; p.n_kv_heads = Hkv; p.head_dim = hd;
+  p.bias = L.bqkv; p.q_norm = L.q_norm; p.k_norm = L.k_norm; p.eps = cfg_.norm_eps;
+  p.rope_neox = cfg_.rope_neox; p.rope_base = cfg_.rope_theta; p.rope_cs = rope_cs_;
+  p.pos = d_pos_; p.slot = d_slot_; p.q_out = q_;
+  p.k_cache = kc; p.v_cache = vc; p.max_ctx = cfg_.max_ctx;
+  launch_qkv_post(p, stream_);
+  {
+    AttnDecodeArgs a;
+    a.split = 0;
+    a.q = q_; a.k_cache = kc; a.v_cache = vc; a.seq_len = d_seqlen_; a.slot = d_slot_;
+    a.B = B; a.n_heads = H; a.n_kv_heads = Hkv; a.head_dim = hd; a.max_ctx = cfg_.max_ctx;
+    a.n_chunks = n_chunks_; a.scale = 1.f / std::sqrt((float)hd);
+    a.o_part = opart_; a.ml = ml_; a.out = attn_; a.counters = attn_cnt_;
+    launch_attn_decode(a, stream_);
+  }
+  launch_f32_to_bf16(attn_, dec_a16_, (size_t)B * qd, stream_);
+  std::memset(&g, 0, sizeof(g));
+  g.A = dec_a16_; g.lda = qd; g.M = B; g.K = qd; g.nseg = 1; g.seg[0] = L.wo.w; g.N = d; g.ldc = d;
+  if (tp) { g.C = ff_; g.epi = GEPI_STORE; } else { g.C = x_; g.epi = GEPI_ACCUM; }
+  launch_gemm_q(g, stream_);
+  if (tp) allreduce(ff_, (size_t)B * d, x_);
+  launch_rmsnorm_bf16(x_, d, L.ffn_norm, dec_a16_, d, B, d, cfg_.norm_eps, stream_);
+  std::memset(&g, 0, sizeof(g));
+  g.A = dec_a16_; g.lda = d; g.M = B; g.K = d; g.nseg = 1; g.seg[0] = L.wgu.w; g.N = 2 * ff;
+  // split-K needs the full gate/up sums before the nonlinearity: fp32 out, then SwiGLU -> bf16
+  g.C = dec_gu_; g.ldc = 2 * ff; g.epi = GEPI_STORE;
+  launch_gemm_q(g, stream_);
+  launch_swiglu_interleaved_bf16(dec_gu_, 2 * ff, dec_ff16_, ff, B, ff, stream_);
+  std::memset(&g, 0, sizeof(g));
+  g.A = dec_ff16_; g.lda = ff; g.M = B; g.K = ff; g.nseg = 1; g.seg[0] = L.wdown.w; g.N = d; g.ldc = d;
+  if (tp) { g.C = attn_; g.epi = GEPI_STORE; } else { g.C = x_; g.epi = GEPI_ACCUM; }
+  launch_gemm_q(g, stream_);
+  if (tp) allreduce(attn_, (size_t)B * d, x_);
+}
+
 void Engine::layer_decode(int l, int B) {
+  if (dec_a16_ && ((dec_gemm_min_b_ > 0 && B >= dec_gemm_min_b_) || B > 8)) {
+    layer_decode_gemm(l, B);
+    return;
+  }
+  if (B > 8) throw std::runtime_error("decode: batches above 8 need the GEMM path (GEMM-capable weights)");
   const LayerW& L = layers_[l];
   const int d = cfg_.d_model, hd = cfg_.head_dim, qd = cfg_.n_heads * hd, kvd = cfg_.n_kv_heads * hd;
   const bool fused_qkv = !cfg_.qk_norm && !cfg_.rope_neox;
@@ -604,7 +672,17 @@ void Engine::enqueue_decode_step(int B) {
   const int d = cfg_.d_model, V = cfg_.vocab_size;
   launch_get_rows(tok_embd_.w, d_tokens_, B, x_, d, 1.f, stream_);
   for (int l = 0; l < cfg_.n_layers; ++l) layer_decode(l, B);
-  gemv({&output_}, V, d, B, x_, d, out_norm_, logits_, V, EPI_STORE, 0);
+  if (dec_a16_ && ((dec_gemm_min_b_ > 0 && B >= dec_gemm_min_b_) || B > 8) && V % 64 == 0 &&
+      gemm_supports(output_.w.qtype)) {
+    launch_rmsnorm_bf16(x_, d, out_norm_, dec_a16_, d, B, d, cfg_.norm_eps, stream_);
+    GemmQArgs g;
+    std::memset(&g, 0, sizeof(g));
+    g.A = dec_a16_; g.lda = d; g.M = B; g.K = d; g.nseg = 1; g.seg[0] = output_.w; g.N = V;
+    g.C = logits_; g.ldc = V; g.epi = GEPI_STORE;
+    launch_gemm_q(g, stream_);
+  } else {
+    gemv({&output_}, V, d, B, x_, d, out_norm_, logits_, V, EPI_STORE, 0);
+  }
   SampleArgs s;
   std::memset(&s, 0, sizeof(s));
   s.logits = logits_; s.ldl = V; s.B = B; s.V = V;

@@ -78,6 +78,18 @@ __global__ void swiglu_kernel(const float* __restrict__ gu, int ldg, float* __re
     o[i] = v.x / (1.f + __expf(-v.x)) * v.y;
   }
 }
+__global__ void swiglu_bf16_kernel(const float* __restrict__ gu, int ldg, bf16_t* __restrict__ out, int ldo, int n) {
+  const float* g = gu + (size_t)blockIdx.y * ldg;
+  bf16_t* o = out + (size_t)blockIdx.y * ldo;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const float2 v = *(const float2*)(g + 2 * i);
+    o[i] = f32_to_bf16(v.x / (1.f + __expf(-v.x)) * v.y);
+  }
+}
+void launch_swiglu_interleaved_bf16(const float* gu, int ldg, bf16_t* out, int ldo, int rows, int n, hipStream_t st) {
+  const int gx = std::min(64, (n + 255) / 256);
+  hipLaunchKernelGGL(swiglu_bf16_kernel, dim3(gx, rows), dim3(256), 0, st, gu, ldg, out, ldo, n);
+}
 void launch_swiglu_interleaved(const float* gu, int ldg, float* out, int ldo, int rows, int n, hipStream_t st) {
   const int gx = std::min(64, (n + 255) / 256);
   hipLaunchKernelGGL(swiglu_kernel, dim3(gx, rows), dim3(256), 0, st, gu, ldg, out, ldo, n);

@@ -286,32 +286,38 @@ __global__ void __launch_bounds__(256) gemm_q_kernel(GemmQArgs a) {
   w.p2 = s == 0 ? a.seg[0].p2 : (s == 1 ? a.seg[1].p2 : a.seg[2].p2);
   w.p3 = s == 0 ? a.seg[0].p3 : (s == 1 ? a.seg[1].p3 : a.seg[2].p3);
   const int wrow0 = n0 - (s == 0 ? a.seg_n0[0] : (s == 1 ? a.seg_n0[1] : a.seg_n0[2]));
-  const int nk = a.K / 64;
+  // split-K (blockIdx.y of gridDim.y): this workgroup's K-steps [kt0, kt1); partial sums are
+  // added atomically (the launcher zeroes C first for STORE)
+  const int nk_all = a.K / 64, S = gridDim.y;
+  const int kt0 = (int)((long)blockIdx.y * nk_all / S), kt1 = (int)((long)(blockIdx.y + 1) * nk_all / S);
 
-  u32x4 ra[AU];  // native vectors: arrays of HIP's uint4 struct are memcpy'd and end up in scratch
-  RawB rb[BU];
-#define GEMM_LOAD(kt_)                                                                  \
+  // three register stages of raw tiles: tile t lives in stage (t - kt0) % 3 and is converted into
+  // LDS two K-steps after its loads were issued (one K-step of MFMAs hides too little latency at
+  // decode-sized M: each step then waited a full memory round trip)
+  u32x4 ra0[AU], ra1[AU], ra2[AU];  // native vectors: arrays of HIP's uint4 struct end up in scratch
+  RawB rb0[BU], rb1[BU], rb2[BU];
+#define GEMM_LOAD(kt_, RA, RB)                                                          \
   {                                                                                     \
     _Pragma("unroll") for (int i = 0; i < AU; ++i) {                                    \
       const int idx = tid + 256 * i, r = idx >> 3, c = idx & 7;                         \
       const int m = min(m0 + r, a.M - 1); /* rows past M re-read the last row */        \
-      ra[i] = *(const u32x4*)(a.A + (size_t)m * a.lda + (kt_) * 64 + c * 8);            \
+      RA[i] = *(const u32x4*)(a.A + (size_t)m * a.lda + (kt_) * 64 + c * 8);            \
     }                                                                                   \
     _Pragma("unroll") for (int i = 0; i < BU; ++i) {                                    \
       const int idx = tid + 256 * i, r = idx >> 2, p = idx & 3;                         \
-      load_raw16<QT>(w, wrow0 + r, (kt_) * 64 + 16 * p, rb[i]);                        \
+      load_raw16<QT>(w, wrow0 + r, (kt_) * 64 + 16 * p, RB[i]);                        \
     }                                                                                   \
   }
-#define GEMM_STORE(buf_, kt_)                                                           \
+#define GEMM_STORE(buf_, kt_, RA, RB)                                                   \
   {                                                                                     \
     _Pragma("unroll") for (int i = 0; i < AU; ++i) {                                    \
       const int idx = tid + 256 * i, r = idx >> 3, c = idx & 7;                         \
-      *(u32x4*)&sA[buf_][r * 8 + (c ^ (r & 7))] = ra[i];                                \
+      *(u32x4*)&sA[buf_][r * 8 + (c ^ (r & 7))] = RA[i];                                \
     }                                                                                   \
     _Pragma("unroll") for (int i = 0; i < BU; ++i) {                                    \
       const int idx = tid + 256 * i, r = idx >> 2, p = idx & 3;                         \
       uint32_t o[8];                                                                    \
-      convert16<QT>(rb[i], (kt_) * 64 + 16 * p, o);                                     \
+      convert16<QT>(RB[i], (kt_) * 64 + 16 * p, o);                                     \
       sB[buf_][r * 8 + ((2 * p) ^ (r & 7))] = make_uint4(o[0], o[1], o[2], o[3]);       \
       sB[buf_][r * 8 + ((2 * p + 1) ^ (r & 7))] = make_uint4(o[4], o[5], o[6], o[7]);   \
     }                                                                                   \
@@ -325,13 +331,8 @@ __global__ void __launch_bounds__(256) gemm_q_kernel(GemmQArgs a) {
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
 
-  GEMM_LOAD(0);
-  GEMM_STORE(0, 0);
-  __syncthreads();
   const int half = lane >> 5, l32 = lane & 31;
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) GEMM_LOAD(kt + 1);
+  auto mfma_step = [&](int cur) __attribute__((always_inline)) {
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
       bf16x8 af[TM], bfr[TN];
@@ -352,9 +353,36 @@ __global__ void __launch_bounds__(256) gemm_q_kernel(GemmQArgs a) {
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
-    if (kt + 1 < nk) GEMM_STORE(cur ^ 1, kt + 1);
-    __syncthreads();
+  };
+  // Loads are issued unconditionally (tile index clamped into [kt0, kt1): a re-read of the last
+  // tile instead of a branch) -- a conditional load makes the outstanding-load count path
+  // dependent and the compiler then drains everything with vmcnt(0) before each conversion,
+  // which serialised every K-step on a full memory round trip (measured: 1.6 us per step).
+  const int klast = kt1 - 1;
+  GEMM_LOAD(kt0, ra0, rb0);
+  GEMM_LOAD(min(kt0 + 1, klast), ra1, rb1);
+  GEMM_LOAD(min(kt0 + 2, klast), ra2, rb2);
+  GEMM_STORE(0, kt0, ra0, rb0);
+  __syncthreads();
+  // one K-step: MFMAs on the LDS tile k, convert tile k+1 (stage RC) into the other LDS buffer,
+  // then reuse tile k's stage (RL) for the loads of tile k+3
+#define GEMM_STEP(k_, RC_A, RC_B, RL_A, RL_B)                                           \
+  {                                                                                     \
+    const int cur = ((k_) - kt0) & 1;                                                   \
+    mfma_step(cur);                                                                     \
+    if ((k_) + 1 < kt1) GEMM_STORE(cur ^ 1, (k_) + 1, RC_A, RC_B);                      \
+    GEMM_LOAD(min((k_) + 3, klast), RL_A, RL_B);                                        \
+    __syncthreads();                                                                    \
   }
+  int kt = kt0;
+  for (; kt + 3 <= kt1; kt += 3) {
+    GEMM_STEP(kt, ra1, rb1, ra0, rb0);
+    GEMM_STEP(kt + 1, ra2, rb2, ra1, rb1);
+    GEMM_STEP(kt + 2, ra0, rb0, ra2, rb2);
+  }
+  if (kt < kt1) GEMM_STEP(kt, ra1, rb1, ra0, rb0);
+  if (kt + 1 < kt1) GEMM_STEP(kt + 1, ra2, rb2, ra1, rb1);
+#undef GEMM_STEP
   // C/D map of the 32x32 accumulator: col = lane & 31, row = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
@@ -371,7 +399,8 @@ __global__ void __launch_bounds__(256) gemm_q_kernel(GemmQArgs a) {
           if (m < a.M && !(l32 & 1)) a.C16[(size_t)m * a.ldc + (n >> 1)] = f32_to_bf16(v / (1.f + __expf(-v)) * up);
         } else if (m < a.M) {
           float* c = a.C + (size_t)m * a.ldc + n;
-          if constexpr (EPI == GEPI_ACCUM) *c += v;
+          if (S > 1) unsafeAtomicAdd(c, v);
+          else if constexpr (EPI == GEPI_ACCUM) *c += v;
           else *c = v;
         }
       }
@@ -389,12 +418,25 @@ bool gemm_supports(int qt) {
 
 template <int QT, int BM, int BN>
 static void launch_tiles(const GemmQArgs& a, hipStream_t st) {
-  const int total = (a.N / BN) * ((a.M + BM - 1) / BM);
+  const int tiles = (a.N / BN) * ((a.M + BM - 1) / BM);
+  // split-K for grids below ~2 workgroups per CU (decode-sized M, short prefill chunks)
+  int S = a.ksplit;
+  if (S <= 0) {
+    const int cus = device_cu_count(), nk = a.K / 64;
+    // up to ~4 workgroups per CU (one wave per SIMD leaves every LDS / MFMA / VALU latency
+    // exposed at decode-sized M), >= 4 K-steps per workgroup
+    S = tiles >= 2 * cus ? 1 : std::max(1, std::min(nk / 4, (4 * cus + tiles - 1) / tiles));
+  }
+  if (a.epi == GEPI_SWIGLU_BF16) S = 1;  // nonlinear epilogue needs the full sum
+  S = std::max(1, std::min(S, a.K / 64));
+  if (S > 1 && a.epi == GEPI_STORE)
+    HIP_CHECK(hipMemset2DAsync(a.C, (size_t)a.ldc * 4, 0, (size_t)a.N * 4, a.M, st));
+  const dim3 grid(tiles, S);
   switch (a.epi) {
-    case GEPI_STORE: hipLaunchKernelGGL((gemm_q_kernel<QT, BM, BN, GEPI_STORE>), dim3(total), dim3(256), 0, st, a); break;
-    case GEPI_ACCUM: hipLaunchKernelGGL((gemm_q_kernel<QT, BM, BN, GEPI_ACCUM>), dim3(total), dim3(256), 0, st, a); break;
+    case GEPI_STORE: hipLaunchKernelGGL((gemm_q_kernel<QT, BM, BN, GEPI_STORE>), grid, dim3(256), 0, st, a); break;
+    case GEPI_ACCUM: hipLaunchKernelGGL((gemm_q_kernel<QT, BM, BN, GEPI_ACCUM>), grid, dim3(256), 0, st, a); break;
     case GEPI_SWIGLU_BF16:
-      hipLaunchKernelGGL((gemm_q_kernel<QT, BM, BN, GEPI_SWIGLU_BF16>), dim3(total), dim3(256), 0, st, a);
+      hipLaunchKernelGGL((gemm_q_kernel<QT, BM, BN, GEPI_SWIGLU_BF16>), grid, dim3(256), 0, st, a);
       break;
     default: throw std::runtime_error("gemm: bad epilogue");
   }

@@ -31,6 +31,7 @@ void launch_add(float* y, const float* x, size_t n, hipStream_t st);
 
 // out[b][i] = silu(gu[b][2i]) * gu[b][2i+1]
 void launch_swiglu_interleaved(const float* gu, int ldg, float* out, int ldo, int rows, int n, hipStream_t st);
+void launch_swiglu_interleaved_bf16(const float* gu, int ldg, bf16_t* out, int ldo, int rows, int n, hipStream_t st);
 
 // Per-head: optional RMSNorm(q/k heads) + RoPE + Q store + K/V cache write, from a packed
 // qkv row [B][q_dim + 2 kv_dim] (used for Qwen3 QK-norm and the prefill GEMM path).
@@ -139,6 +140,7 @@ struct GemmQArgs {
   bf16_t* C16;       // [M][ldc] bf16 (SWIGLU_BF16: column n/2 = silu(col n) * col n+1)
   int ldc;
   int epi;
+  int ksplit;        // K split over workgroups (atomic partial sums): 0 = auto, 1 = off
 };
 void launch_gemm_q(const GemmQArgs& a, hipStream_t st);
 

@@ -95,7 +95,7 @@ def main(argv=None):
     ap.add_argument("--addr", default=os.environ.get("AIOS_RUNTIME_ADDR", "[::]:50055"))
     ap.add_argument("--model-dir", default=os.environ.get("AIOS_MODEL_DIR", "/var/lib/aios/models/"))
     ap.add_argument("--device", type=int, default=int(os.environ.get("AIOS_DEVICE", "0")))
-    ap.add_argument("--max-batch", type=int, default=8)
+    ap.add_argument("--max-batch", type=int, default=16)
     ap.add_argument("--max-slots", type=int, default=16)
     ap.add_argument("--no-http", action="store_true")
     args = ap.parse_args(argv)

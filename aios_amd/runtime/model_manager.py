@@ -81,7 +81,7 @@ def context_for_size(nbytes: int) -> int:
 
 
 class ModelManager:
-    def __init__(self, device: int = 0, max_batch: int = 8, max_slots: int = 16, base_port: int = BASE_PORT):
+    def __init__(self, device: int = 0, max_batch: int = 16, max_slots: int = 16, base_port: int = BASE_PORT):
         self.device = device
         self.max_batch = max_batch
         self.max_slots = max_slots

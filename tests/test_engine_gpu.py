@@ -136,3 +136,21 @@ def test_prefill_gemm_vs_gemv_path(model_files, monkeypatch):
     e2, _ = _load(path)
     l2 = np.asarray(e2.prefill(0, prompt, 0, True))
     assert np.abs(l1 - l2).max() < 2e-2 * max(np.abs(l1).max(), 1.0)
+
+
+def test_batched_decode_gemm_path_matches_gemv_path(model_files, monkeypatch):
+    """B >= AIOS_DECODE_GEMM_MIN_B runs the projections through the MFMA GEMM (split-K for small
+    N); its logits must match the GEMV path's for the same batch."""
+    path = model_files["Q4_K_M"]
+    prompts = [[1, 5, 6, 7], [1, 9, 10, 11, 12, 13], [1, 100, 200], [1, 3, 4]]
+    outs = {}
+    for mode, min_b in (("gemv", "0"), ("gemm", "2")):
+        monkeypatch.setenv("AIOS_DECODE_GEMM_MIN_B", min_b)
+        eng, cfg = _load(path, max_slots=4, max_batch=4, act_q8=False)
+        firsts = [int(np.argmax(eng.prefill(s, p, 0, True))) for s, p in enumerate(prompts)]
+        toks = eng.decode([0, 1, 2, 3], firsts, [len(p) for p in prompts])
+        outs[mode] = (toks, np.asarray(eng.last_logits(4)).reshape(4, -1))
+        del eng
+    l0, l1 = outs["gemv"][1], outs["gemm"][1]
+    scale = max(np.abs(l0).max(), 1.0)
+    assert np.abs(l0 - l1).max() < 2e-2 * scale

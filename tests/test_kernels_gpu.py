@@ -302,18 +302,20 @@ def test_gemm_mfma(E, t, M):
                                   [(GGMLType.Q8_0, 64)], [(GGMLType.BF16, 192), (GGMLType.Q5_K, 64)],
                                   [(GGMLType.Q4_0, 128), (GGMLType.F16, 128)]])
 @pytest.mark.parametrize("M", [1, 100, 300])
-def test_gemm_q_segments(E, segs, M):
+@pytest.mark.parametrize("ksplit", [0, 1, 3])
+def test_gemm_q_segments(E, segs, M, ksplit):
     K = 512
     mats, refs = zip(*[qmat(E, t, n, K, seed=20 + i) for i, (t, n) in enumerate(segs)])
     W = torch.cat(refs, 0)
     N = W.shape[0]
     A = torch.randn(M, K, device="cuda").to(torch.bfloat16)
     C = torch.zeros(M, N, device="cuda")
-    E.gemm_q(A.data_ptr(), K, list(mats), M, C.data_ptr(), 0, N, E.GEPI_STORE, stream())
+    C.fill_(7.0)  # STORE must overwrite (split-K zeroes first)
+    E.gemm_q(A.data_ptr(), K, list(mats), M, C.data_ptr(), 0, N, E.GEPI_STORE, stream(), ksplit)
     torch.cuda.synchronize()
     ref = A.float().cpu() @ W.to(torch.bfloat16).float().T
     assert torch.allclose(C.cpu(), ref, atol=2e-3, rtol=2e-3), (C.cpu() - ref).abs().max()
-    E.gemm_q(A.data_ptr(), K, list(mats), M, C.data_ptr(), 0, N, E.GEPI_ACCUM, stream())
+    E.gemm_q(A.data_ptr(), K, list(mats), M, C.data_ptr(), 0, N, E.GEPI_ACCUM, stream(), ksplit)
     torch.cuda.synchronize()
     assert torch.allclose(C.cpu(), 2 * ref, atol=4e-3, rtol=2e-3)
 

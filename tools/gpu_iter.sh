@@ -1,11 +1,10 @@
-# one GPU iteration (used through gpurun): kernel tests, engine tests, bench, profile
+# one GPU iteration (used through gpurun): kernel + engine tests, batched decode bench
 set -u
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 export HSA_ENABLE_IPC_MODE_LEGACY=0
-run() { local name=$1 t=$2; shift 2; timeout -k 10 $t "$@" > gpurun_out/$name.log 2>&1; local rc=$?; grep -v amdgpu.ids gpurun_out/$name.log | tail -${TAILN:-3}; [ $rc -eq 0 ] || { echo "[$name] rc=$rc"; tail -40 gpurun_out/$name.log; exit 1; }; }
-run t_kern 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py
-run t_eng 500 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_engine_gpu.py
-run bench 300 python bench.py
-timeout -k 10 400 bash tools/prof_decode.sh > /dev/null 2>&1 || exit 1
-head -12 gpurun_out/prof_summary.txt
+run() { local name=$1 t=$2; shift 2; timeout -k 10 $t "$@" > gpurun_out/$name.log 2>&1; local rc=$?; grep -v amdgpu.ids gpurun_out/$name.log | tail -${TAILN:-2}; [ $rc -eq 0 ] || { echo "[$name] rc=$rc"; tail -40 gpurun_out/$name.log; exit 1; }; }
+run t_eng 500 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_engine_gpu.py tests/test_runtime_gpu.py
+for b in 1 2 4 8 16 32; do
+  TAILN=1 run b$b 200 python bench.py --batch $b --steps 64 --warmup 8 --no-secondary
+done
