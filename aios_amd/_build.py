@@ -89,7 +89,8 @@ def build(verbose: bool = True, jobs: int | None = None) -> Path:
     newest = max(o.stat().st_mtime for o in objs)
     if not out.exists() or out.stat().st_mtime < newest:
         tmp = out.with_suffix(".tmp.so")
-        cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(tmp), *map(str, objs)]
+        cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(tmp), *map(str, objs),
+               "-L/opt/rocm/lib", "-lrocprofiler-sdk-roctx", "-Wl,-rpath,/opt/rocm/lib"]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stderr[-6000:]}")

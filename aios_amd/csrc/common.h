@@ -98,6 +98,15 @@ __device__ __forceinline__ void static_for(F&& f) {
   }
 }
 
+// roctx ranges around the engine's host-side phases (load, prefill chunk, decode step / graph
+// replay, sampling): visible with `rocprofv3 --marker-trace` next to the kernel trace; ~free
+// when no profiler is attached.  AIOS_TRACE=0 turns them off.
+struct TraceRange {
+  explicit TraceRange(const char* name);
+  ~TraceRange();
+  bool on;
+};
+
 // CUs of the current device (host; cached per process)
 inline int device_cu_count() {
   static int cus = 0;

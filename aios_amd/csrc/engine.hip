@@ -9,7 +9,23 @@
 #include <regex>
 #include <sstream>
 
+#include <rocprofiler-sdk-roctx/roctx.h>
+
 namespace aios {
+
+static bool trace_enabled() {
+  static const int on = [] {
+    const char* e = std::getenv("AIOS_TRACE");
+    return e && std::atoi(e) == 0 ? 0 : 1;
+  }();
+  return on != 0;
+}
+TraceRange::TraceRange(const char* name) : on(trace_enabled()) {
+  if (on) roctxRangePushA(name);
+}
+TraceRange::~TraceRange() {
+  if (on) roctxRangePop();
+}
 
 static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
@@ -247,6 +263,7 @@ void Engine::set_tensor(const std::string& name, int qt, int rows, int cols, con
 }
 
 void Engine::init_random(const std::string& recipe_in, uint64_t seed) {
+  TraceRange tr("aios.init_random");
   HIP_CHECK(hipSetDevice(cfg_.device));
   std::string r = recipe_in;
   std::transform(r.begin(), r.end(), r.begin(), ::toupper);
@@ -339,6 +356,7 @@ std::string Engine::weight_type_summary() const {
 }
 
 void Engine::finalize() {
+  TraceRange tr("aios.finalize");
   HIP_CHECK(hipSetDevice(cfg_.device));
   auto miss = missing_tensors();
   if (!miss.empty()) throw std::runtime_error("missing tensors, first: " + miss[0]);
@@ -705,6 +723,7 @@ bool Engine::gemm_prefill_ok(int T) const { return gm_ok_ && T >= gm_min_rows_; 
 // so every weight byte is dequantised once per chunk (not once per 8 rows as on the GEMV path).
 // TP: the row-parallel O / down outputs go through the all-reduce hook into the residual.
 void Engine::prefill_gemm(int slot, const std::vector<int>& tokens, int start_pos, bool want_logits) {
+  TraceRange tr("aios.prefill_gemm");
   const int T = (int)tokens.size();
   const int d = cfg_.d_model, hd = cfg_.head_dim, H = cfg_.n_heads, Hkv = cfg_.n_kv_heads, ff = cfg_.d_ff;
   const int qd = H * hd, kvd = Hkv * hd, ldqkv = qd + 2 * kvd, V = cfg_.vocab_size;
@@ -769,6 +788,7 @@ void Engine::prefill_gemm(int slot, const std::vector<int>& tokens, int start_po
 }
 
 std::vector<float> Engine::prefill(int slot, const std::vector<int>& tokens, int start_pos, bool want_logits) {
+  TraceRange tr("aios.prefill");
   if (!finalized_) throw std::runtime_error("engine not finalized");
   HIP_CHECK(hipSetDevice(cfg_.device));
   const int T = (int)tokens.size();
@@ -1028,6 +1048,7 @@ void Engine::decode_loop_prepare(const std::vector<int>& slots, const std::vecto
 }
 
 void Engine::decode_loop_run(int B, int n_steps, bool use_graph) {
+  TraceRange tr(use_graph ? "aios.decode_graph_replay" : "aios.decode_eager");
   HIP_CHECK(hipSetDevice(cfg_.device));
   if (!use_graph) {
     for (int i = 0; i < n_steps; ++i) enqueue_decode_step(B);
