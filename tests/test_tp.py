@@ -85,22 +85,29 @@ def test_tp_command_channel_gloo(tmp_path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world", [2, 4])
-def test_tp_xgmi_allreduce_and_sharded_model(tmp_path, world):
+@pytest.mark.parametrize("world,gemm_prefill", [(2, 0), (4, 0), (2, 1)])
+def test_tp_xgmi_allreduce_and_sharded_model(tmp_path, world, gemm_prefill):
+    """TP=N vs TP=1 on the same weights.  With the fp32-activation GEMV prefill (gemm_prefill=0)
+    the only differences are fp32 summation order: 1e-3 of the logit scale.  The MFMA prefill
+    path rounds activations to bf16 (and sums split-K partials atomically), so a rounding flip
+    between the two shardings propagates: 1e-2 there -- a sharding bug is O(1)."""
     out = tmp_path / f"tp{world}.json"
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(world),
-           "--master-addr", "127.0.0.1", "--master-port", str(29600 + world), os.path.join(ROOT, "tools", "tp_check.py"),
-           "--out", str(out), "--model", "test-tp8-shape"]
-    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=600)
+           "--master-addr", "127.0.0.1", "--master-port", str(29600 + world + 10 * gemm_prefill),
+           os.path.join(ROOT, "tools", "tp_check.py"), "--out", str(out), "--model", "test-tp8-shape"]
+    env = dict(os.environ, AIOS_PREFILL_GEMM=str(gemm_prefill))
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=600, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     res = json.loads(out.read_text())
     assert not res["comm_error_flag"] and not res["comm_error_flag_model"]
     for e in res["allreduce"]:
         assert e["inplace_err"] < 1e-4 and e["fused_resid_err"] < 1e-4, e
     m = res["model"]
-    assert m["prefill_logit_max_abs_diff"] < 1e-3 * max(1.0, m["logit_scale"])
-    assert max(m["decode_logit_max_abs_diff_per_step"]) < 1e-3 * max(1.0, m["logit_scale"])
-    assert m["graph_tokens_match"]
+    tol = (1e-2 if gemm_prefill else 1e-3) * max(1.0, m["logit_scale"])
+    assert m["prefill_logit_max_abs_diff"] < tol
+    assert max(m["decode_logit_max_abs_diff_per_step"]) < tol
+    if not gemm_prefill:
+        assert m["graph_tokens_match"]
 
 
 @pytest.mark.gpu
