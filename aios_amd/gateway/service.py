@@ -30,12 +30,18 @@ class ApiGatewayService:
 
     @classmethod
     def from_env(cls, db_path: str = ""):
-        budget = BudgetManager(float(os.environ.get("AIOS_CLAUDE_BUDGET_USD", "100")),
-                               float(os.environ.get("AIOS_OPENAI_BUDGET_USD", "50")),
+        from ..utils import config as node_config
+
+        cfg = node_config.load()  # [api] budgets / cache; env vars still win (reference names)
+        budget = BudgetManager(float(os.environ.get("AIOS_CLAUDE_BUDGET_USD", cfg.api.claude_monthly_budget_usd)),
+                               float(os.environ.get("AIOS_OPENAI_BUDGET_USD", cfg.api.openai_monthly_budget_usd)),
                                db_path or os.path.join(data_dir(), "data", "gateway_usage.db"))
-        provs = providers_from_env()
+        env = dict(os.environ)
+        env.setdefault("AIOS_SECRETS", cfg.security.secrets_file)
+        provs = providers_from_env(env)
         log.info("available providers: %s", ", ".join(n for n, p in provs.items() if p.available()))
-        return cls(RequestRouter(provs, budget))
+        return cls(RequestRouter(provs, budget, ttl=float(cfg.api.cache_ttl_seconds),
+                                 max_entries=int(cfg.api.cache_max_entries)))
 
     async def Infer(self, req, ctx):
         log.info("inference request: provider=%s agent=%s task=%s", req.preferred_provider, req.requesting_agent,

@@ -42,7 +42,12 @@ async def amain(args):
     tasks = [AutonomyLoop(st, args.tick_ms / 1000.0).run(stop), st.health.run(stop),
              scheduler_loop(st, stop), st.event_queue.run(stop), maintenance_loop(st, stop)]
     if not args.no_proactive:
-        tasks.append(proactive_loop(st, stop, ProactiveConfig()))
+        from ..utils import config as node_config
+
+        mon = node_config.load().monitoring  # [monitoring] thresholds of the node config
+        tasks.append(proactive_loop(st, stop, ProactiveConfig(cpu_threshold=mon.cpu_threshold,
+                                                              memory_threshold=mon.memory_threshold,
+                                                              disk_threshold=mon.disk_threshold)))
     console = None
     if args.console_port > 0:
         console = ManagementConsole(st, port=args.console_port)

@@ -26,10 +26,25 @@ log = logging.getLogger("aios.runtime")
 HEALTH_CHECK_INTERVAL = 10.0
 
 
-async def auto_load(svc: AIRuntimeService, model_dir: str):
+async def auto_load(svc: AIRuntimeService, model_dir: str, cfg=None):
+    """Start-up model pool: the node config's always-loaded tiers first (context length, TP degree
+    and device from [models.<tier>] -- the reference runtime ignored that section, App. A #27),
+    then every other *.gguf in the model directory (reference auto-load, runtime/src/main.rs:65-132),
+    then AIOS_SYNTHETIC_MODELS specs."""
+    loaded = set()
+    for tier, spec, ctx in (cfg.model_specs() if cfg is not None else []):
+        base = spec.partition("#")[0]
+        name = tier if base.startswith("synthetic:") else Path(base).stem
+        log.info("loading %s tier %s from %s (ctx %s)", tier, name, spec, ctx or "auto")
+        m = await svc.mgr.load_model(name, spec, ctx)
+        loaded.add(base)
+        if m.status == "ready" and svc.http:
+            await svc.start_http(m)
     d = Path(model_dir)
     if d.is_dir():
         for f in sorted(d.glob("*.gguf")):
+            if str(f) in loaded:
+                continue
             req_name = f.stem
             log.info("auto-loading %s", f)
             m = await svc.mgr.load_model(req_name, str(f))
@@ -70,7 +85,16 @@ async def health_loop(mgr: ModelManager, stop: asyncio.Event, memory_addr: str =
 
 
 async def amain(args):
-    mgr = ModelManager(device=args.device, max_batch=args.max_batch, max_slots=args.max_slots)
+    from ..utils import config as node_config
+
+    cfg = node_config.load()
+    for w in cfg.warnings:
+        log.warning("config: %s", w)
+    max_batch = args.max_batch or cfg.models.max_batch
+    max_slots = args.max_slots or cfg.models.max_slots
+    if cfg.models.devices and "AIOS_TP_DEVICES" not in os.environ:
+        os.environ["AIOS_TP_DEVICES"] = ",".join(str(d) for d in cfg.models.devices)
+    mgr = ModelManager(device=args.device, max_batch=max_batch, max_slots=max_slots)
     svc = AIRuntimeService(mgr, http=not args.no_http)
     server = RpcServer(args.addr, {"aios.runtime.AIRuntime": svc})
     await server.start()
@@ -81,7 +105,7 @@ async def amain(args):
             loop.add_signal_handler(sig, stop.set)
         except NotImplementedError:
             pass
-    asyncio.ensure_future(auto_load(svc, args.model_dir))
+    asyncio.ensure_future(auto_load(svc, args.model_dir, cfg))
     await health_loop(mgr, stop)
     await server.stop()
     await svc.close()
@@ -95,8 +119,8 @@ def main(argv=None):
     ap.add_argument("--addr", default=os.environ.get("AIOS_RUNTIME_ADDR", "[::]:50055"))
     ap.add_argument("--model-dir", default=os.environ.get("AIOS_MODEL_DIR", "/var/lib/aios/models/"))
     ap.add_argument("--device", type=int, default=int(os.environ.get("AIOS_DEVICE", "0")))
-    ap.add_argument("--max-batch", type=int, default=16)
-    ap.add_argument("--max-slots", type=int, default=16)
+    ap.add_argument("--max-batch", type=int, default=0, help="0 = [models] max_batch of the node config")
+    ap.add_argument("--max-slots", type=int, default=0, help="0 = [models] max_slots of the node config")
     ap.add_argument("--no-http", action="store_true")
     args = ap.parse_args(argv)
     logging.basicConfig(level=os.environ.get("AIOS_LOG", "INFO"), format="%(asctime)s %(levelname)s %(name)s %(message)s")
