@@ -141,6 +141,8 @@ PYBIND11_MODULE(_engine, m) {
       .def("weight_type_summary", &Engine::weight_type_summary)
       .def_property_readonly("ready", &Engine::ready)
       .def_property_readonly("weight_bytes", &Engine::weight_bytes)
+      .def_property_readonly("blas_prefill", &Engine::blas_prefill)
+      .def_property_readonly("bf16_copy_bytes", &Engine::bf16_copy_bytes)
       .def_property_readonly("kv_bytes", &Engine::kv_bytes)
       .def_property_readonly("workspace_bytes", &Engine::workspace_bytes)
       .def_property_readonly("config", &Engine::config)

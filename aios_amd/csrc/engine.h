@@ -173,6 +173,18 @@ class Engine {
   int dec_gemm_min_b_ = 8;
   bf16_t *dec_a16_ = nullptr, *dec_ff16_ = nullptr;
   float* dec_gu_ = nullptr;  // [max_batch][2 d_ff] fp32 gate/up (split-K GEMM, then SwiGLU -> bf16)
+  // resident bf16 weight copies for hipBLASLt prefill (AIOS_BLAS, on when they fit in free HBM)
+  struct Layer16 {
+    bf16_t *qkv = nullptr, *o = nullptr, *gu = nullptr, *down = nullptr;
+  };
+  std::vector<Layer16> l16_;
+  std::unique_ptr<class BlasGemm> blas_;
+  float* gm_gu_ = nullptr;  // [gm_rows][2 d_ff] fp32 gate/up of the BLAS prefill path
+  size_t bf16_copy_bytes_ = 0;
+ public:
+  bool blas_prefill() const { return !l16_.empty(); }
+  size_t bf16_copy_bytes() const { return bf16_copy_bytes_; }
+ private:
   void layer_decode_gemm(int l, int B);
   int *pf_tokens_ = nullptr, *pf_pos_ = nullptr, *pf_seqlen_ = nullptr, *pf_slot_ = nullptr;
 

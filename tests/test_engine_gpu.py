@@ -154,3 +154,23 @@ def test_batched_decode_gemm_path_matches_gemv_path(model_files, monkeypatch):
     l0, l1 = outs["gemv"][1], outs["gemm"][1]
     scale = max(np.abs(l0).max(), 1.0)
     assert np.abs(l0 - l1).max() < 2e-2 * scale
+
+
+@pytest.mark.parametrize("recipe", ["Q4_K_M", "mistral_shape"])
+def test_prefill_blas_path_matches_reference(model_files, recipe, monkeypatch):
+    """Long prompts go through hipBLASLt on the resident bf16 weight copies; same tolerance as the
+    fused-dequant MFMA path, and both paths agree."""
+    path = model_files[recipe]
+    ref = ReferenceModel.from_gguf(path, kv_bf16=True)
+    prompt = [1] + list(np.random.default_rng(5).integers(3, 200, 140))
+    rl = ref.forward(prompt)[-1]
+    scale = max(rl.abs().max().item(), 1.0)
+    got = {}
+    for blas in ("1", "0"):
+        monkeypatch.setenv("AIOS_BLAS", blas)
+        eng, cfg = _load(path)
+        assert eng.blas_prefill == (blas == "1")
+        got[blas] = torch.from_numpy(np.asarray(eng.prefill(0, prompt, 0, True)))
+        del eng
+    assert (got["1"] - rl).abs().max().item() < 2e-2 * scale
+    assert (got["1"] - got["0"]).abs().max().item() < 2e-2 * scale
