@@ -8,6 +8,7 @@ channels are created on first use, with keepalive, and calls default to a 300 s 
 """
 from __future__ import annotations
 
+import os
 from typing import Dict, Optional
 
 import grpc
@@ -18,13 +19,31 @@ DEFAULT_TIMEOUT = 300.0
 _channels: Dict[str, grpc.aio.Channel] = {}
 
 
-def channel(address: str, fresh: bool = False) -> grpc.aio.Channel:
+def channel_credentials(tls_dir: Optional[str] = None):
+    """Client side of the node mTLS (see rpc.server.server_credentials): CA + this node's cert."""
+    d = tls_dir if tls_dir is not None else os.environ.get("AIOS_TLS_DIR", "")
+    if not d:
+        return None
+    p = {k: os.path.join(d, f) for k, f in (("ca", "ca.crt"), ("cert", "server.crt"), ("key", "server.key"))}
+    read = lambda k: open(p[k], "rb").read()  # noqa: E731
+    return grpc.ssl_channel_credentials(root_certificates=read("ca"), private_key=read("key"),
+                                        certificate_chain=read("cert"))
+
+
+def channel(address: str, fresh: bool = False, tls_dir: Optional[str] = None) -> grpc.aio.Channel:
     if fresh or address not in _channels:
-        ch = grpc.aio.insecure_channel(address, options=[
+        opts = [
             ("grpc.keepalive_time_ms", 10_000),
             ("grpc.keepalive_timeout_ms", 5_000),
             ("grpc.max_receive_message_length", 64 * 1024 * 1024),
-        ])
+        ]
+        creds = channel_credentials(tls_dir)
+        if creds is not None:
+            # certificates carry SAN localhost / 127.0.0.1 / the service name
+            opts.append(("grpc.ssl_target_name_override", os.environ.get("AIOS_TLS_SERVICE", "aios")))
+            ch = grpc.aio.secure_channel(address, creds, options=opts)
+        else:
+            ch = grpc.aio.insecure_channel(address, options=opts)
         if fresh:
             return ch
         _channels[address] = ch

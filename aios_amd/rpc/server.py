@@ -50,10 +50,31 @@ def generic_handler(full_service_name: str, impl) -> grpc.GenericRpcHandler:
     return grpc.method_handlers_generic_handler(full_service_name, handlers)
 
 
+def server_credentials(tls_dir: Optional[str] = None):
+    """mTLS for every service when AIOS_TLS_DIR (or tls_dir) holds the node certificates made by the
+    native TlsManager (agent-core/src/tls.rs -- generated but never used in the reference, whose
+    gRPC is plaintext everywhere).  Clients must present a certificate signed by the node CA
+    unless AIOS_TLS_CLIENT_AUTH=0.  Returns None for plaintext."""
+    import os
+
+    d = tls_dir if tls_dir is not None else os.environ.get("AIOS_TLS_DIR", "")
+    if not d:
+        return None
+    from ..core import load as load_core
+
+    mgr = load_core().TlsManager(d)
+    mgr.generate_self_signed(os.environ.get("AIOS_TLS_SERVICE", "aios"))  # idempotent
+    p = mgr.paths()
+    read = lambda k: open(p[k], "rb").read()  # noqa: E731
+    return grpc.ssl_server_credentials([(read("server_key"), read("server_cert"))], root_certificates=read("ca_cert"),
+                                       require_client_auth=os.environ.get("AIOS_TLS_CLIENT_AUTH", "1") != "0")
+
+
 class RpcServer:
     """grpc.aio server hosting one or more aiOS services on one address."""
 
-    def __init__(self, address: str, services: Dict[str, object], options: Optional[Iterable] = None):
+    def __init__(self, address: str, services: Dict[str, object], options: Optional[Iterable] = None,
+                 tls_dir: Optional[str] = None):
         self.address = address
         self.services = services
         self.server = grpc.aio.server(options=list(options or [
@@ -62,7 +83,9 @@ class RpcServer:
         ]))
         for name, impl in services.items():
             self.server.add_generic_rpc_handlers((generic_handler(name, impl),))
-        self.port = self.server.add_insecure_port(address)
+        creds = server_credentials(tls_dir)
+        self.tls = creds is not None
+        self.port = self.server.add_secure_port(address, creds) if creds else self.server.add_insecure_port(address)
         if self.port == 0:
             raise RuntimeError(f"could not bind {address}")
 
