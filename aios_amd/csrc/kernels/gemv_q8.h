@@ -120,14 +120,28 @@ struct SegRs {
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t mk_rsrc(const uint8_t* p) {
   return __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, 0x7fffffff, 0x00020000);
 }
+// Wave-uniform copy of a kernarg pointer.  Reading every segment's fields into SGPRs first and
+// selecting VALUES (not addresses into the kernarg struct) keeps the struct out of scratch.
+__device__ __forceinline__ const uint8_t* sgpr_ptr(const uint8_t* p) {
+  const uint64_t v = (uint64_t)p;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return (const uint8_t*)(((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ const uint8_t* sel3(int s, const uint8_t* a, const uint8_t* b, const uint8_t* c) {
+  a = sgpr_ptr(a);
+  b = sgpr_ptr(b);
+  c = sgpr_ptr(c);
+  return s == 0 ? a : (s == 1 ? b : c);
+}
 __device__ __forceinline__ SegRs seg_rsrc(const GemvArgs& a, int s) {
-  const uint8_t* p0 = a.seg[0].p0;
-  const uint8_t* p1 = a.seg[0].p1;
-  const uint8_t* p2 = a.seg[0].p2;
-  const uint8_t* p3 = a.seg[0].p3;
-  int cols = a.seg[0].cols;
-  if (s == 1) { p0 = a.seg[1].p0; p1 = a.seg[1].p1; p2 = a.seg[1].p2; p3 = a.seg[1].p3; }
-  if (s == 2) { p0 = a.seg[2].p0; p1 = a.seg[2].p1; p2 = a.seg[2].p2; p3 = a.seg[2].p3; }
+  const uint8_t* p0 = sel3(s, a.seg[0].p0, a.seg[1].p0, a.seg[2].p0);
+  const uint8_t* p1 = sel3(s, a.seg[0].p1, a.seg[1].p1, a.seg[2].p1);
+  const uint8_t* p2 = sel3(s, a.seg[0].p2, a.seg[1].p2, a.seg[2].p2);
+  const uint8_t* p3 = sel3(s, a.seg[0].p3, a.seg[1].p3, a.seg[2].p3);
+  const int c0 = __builtin_amdgcn_readfirstlane(a.seg[0].cols), c1 = __builtin_amdgcn_readfirstlane(a.seg[1].cols),
+            c2 = __builtin_amdgcn_readfirstlane(a.seg[2].cols);
+  int cols = s == 0 ? c0 : (s == 1 ? c1 : c2);
   SegRs r;
   r.r0 = mk_rsrc(p0);
   r.r1 = mk_rsrc(p1);
@@ -494,7 +508,9 @@ __global__ void __launch_bounds__(Q8_WAVES * 64) gemv_q8_rows(GemvArgs a) {
   const int npairs = a.N >> 1;
   // pairs [0, np0) use QT0, [np0, npairs) the last segment's QT1: one loop per format, so every
   // loop issues a fixed load sequence and the compiler's vmcnt waits stay exact
-  const int np0 = (MIXED && a.nseg > 1) ? (a.nseg == 2 ? a.seg_row0[1] : a.seg_row0[2]) >> 1 : npairs;
+  const int srow1 = __builtin_amdgcn_readfirstlane(a.seg_row0[1]);
+  const int srow2 = __builtin_amdgcn_readfirstlane(a.seg_row0[2]);
+  const int np0 = (MIXED && a.nseg > 1) ? (a.nseg == 2 ? srow1 : srow2) >> 1 : npairs;
   const int nit = (nch + 64 * U - 1) / (64 * U);
   const int stride = gridDim.x * Q8_WAVES;
   const int wid = __builtin_amdgcn_readfirstlane(blockIdx.x * Q8_WAVES + wave);  // wave-uniform -> SGPR
@@ -511,7 +527,7 @@ __global__ void __launch_bounds__(Q8_WAVES * 64) gemv_q8_rows(GemvArgs a) {
   // Loads are issued unconditionally: past the range end they read x (L2-resident, in bounds for
   // every stream's small offsets) instead of branching -- a conditional load makes the
   // outstanding-load count path dependent and the compiler then drains with vmcnt(0).
-  auto load = [&](auto tag, int p, int pend, int it, RawChunk (&r)[U][GEMV_ROWS]) {
+  auto load = [&](auto tag, int p, int pend, int it, RawChunk (&r)[U][GEMV_ROWS]) __attribute__((always_inline)) {
     constexpr int QT = decltype(tag)::value;
     const bool live = p < pend;
     int lrow;
@@ -549,7 +565,7 @@ __global__ void __launch_bounds__(Q8_WAVES * 64) gemv_q8_rows(GemvArgs a) {
   for (int r = 0; r < GEMV_ROWS; ++r)
 #pragma unroll
     for (int b = 0; b < B; ++b) acc[r][b] = 0.f;
-  auto compute = [&](auto tag, int it, const RawChunk (&cur)[U][GEMV_ROWS]) {
+  auto compute = [&](auto tag, int it, const RawChunk (&cur)[U][GEMV_ROWS]) __attribute__((always_inline)) {
     constexpr int QT = decltype(tag)::value;
     if (a.tune_dbg & 2) {
 #pragma unroll
@@ -563,7 +579,7 @@ __global__ void __launch_bounds__(Q8_WAVES * 64) gemv_q8_rows(GemvArgs a) {
     }
     q8_compute<QT, B, U>(cur, it, nch, xq, ms, acc, a.tune_dbg);
   };
-  auto finish = [&](int p) {
+  auto finish = [&](int p) __attribute__((always_inline)) {
     float s[B];
 #pragma unroll
     for (int b = 0; b < B; ++b) {
@@ -599,8 +615,11 @@ __global__ void __launch_bounds__(Q8_WAVES * 64) gemv_q8_rows(GemvArgs a) {
 
   RawChunk buf[PIPE][U][GEMV_ROWS];
   auto& bufA = buf[0];
-  // walk pairs [p, pend) grid-stride; buf[0] already holds item (p, 0)
-  auto run = [&](auto tag, int p, int pend, int stride) {
+  // walk pairs [p, pend) grid-stride; B[0] already holds item (p, 0).  The register buffer is a
+  // parameter so the two formats of a mixed launch each get their own (one shared array written
+  // through two different load sequences defeats SROA and lands in scratch)
+  auto run = [&](auto tag, int p, int pend, int stride, RawChunk (&buf)[PIPE][U][GEMV_ROWS]) __attribute__((always_inline)) {
+    auto& bufA = buf[0];
     if (p >= pend) return;
     if constexpr (PIPE >= 2) {
       // PIPE register buffers in rotation, each reloaded right after it was consumed with the item
@@ -656,16 +675,36 @@ __global__ void __launch_bounds__(Q8_WAVES * 64) gemv_q8_rows(GemvArgs a) {
     load(FmtTag<QT0>{}, wid, npairs, 0, bufA);  // weight loads in flight during the prologue
     if (!(a.tune_dbg & 1)) q8_stage<QT0, B, NPF>(a, xq, ms, red, pf);
     __syncthreads();
-    run(FmtTag<QT0>{}, wid, npairs, stride);
+    run(FmtTag<QT0>{}, wid, npairs, stride, buf);
   } else {
-    // one loop per format (QT0 pairs, then the last segment's QT1 pairs): a wave-split version
-    // kept both formats' buffers live and spilled to scratch
-    load(FmtTag<QT0>{}, wid, np0, 0, bufA);
-    if (!(a.tune_dbg & 1)) q8_stage<QT0, B, NPF>(a, xq, ms, red, pf);
-    __syncthreads();
-    run(FmtTag<QT0>{}, wid, np0, stride);
-    load(FmtTag<QT1>{}, np0 + wid, npairs, 0, bufA);
-    run(FmtTag<QT1>{}, np0 + wid, npairs, stride);
+    // Mixed formats (Q4_K q/k + Q6_K v of a Q4_K_M QKV): the waves are split in proportion to the
+    // pair counts, whole workgroups per format, so both formats stream concurrently instead of a
+    // Q6_K phase after the Q4_K one (which added a full memory round trip: 11.6 vs 8.3 us per QKV).
+    // W0 is a multiple of the workgroup's wave count, so every workgroup takes one branch (its
+    // barrier stays uniform); the x staging is the same for both formats (same_xlayout).
+    const int W = stride;
+    int W0 = (int)((long)W * np0 / npairs);
+    W0 = (W0 + Q8_WAVES / 2) / Q8_WAVES * Q8_WAVES;
+    W0 = max(Q8_WAVES, min(W - Q8_WAVES, W0));
+    if (W < 2 * Q8_WAVES) {  // tiny grid: the sequential schedule
+      load(FmtTag<QT0>{}, wid, np0, 0, bufA);
+      if (!(a.tune_dbg & 1)) q8_stage<QT0, B, NPF>(a, xq, ms, red, pf);
+      __syncthreads();
+      run(FmtTag<QT0>{}, wid, np0, stride, buf);
+      load(FmtTag<QT1>{}, np0 + wid, npairs, 0, bufA);
+      run(FmtTag<QT1>{}, np0 + wid, npairs, stride, buf);
+    } else if (wid < W0) {
+      load(FmtTag<QT0>{}, wid, np0, 0, bufA);
+      if (!(a.tune_dbg & 1)) q8_stage<QT0, B, NPF>(a, xq, ms, red, pf);
+      __syncthreads();
+      run(FmtTag<QT0>{}, wid, np0, W0, buf);
+    } else {
+      RawChunk buf1[PIPE][U][GEMV_ROWS];
+      load(FmtTag<QT1>{}, np0 + (wid - W0), npairs, 0, buf1[0]);
+      if (!(a.tune_dbg & 1)) q8_stage<QT0, B, NPF>(a, xq, ms, red, pf);
+      __syncthreads();
+      run(FmtTag<QT1>{}, np0 + (wid - W0), npairs, W - W0, buf1);
+    }
   }
 }
 
