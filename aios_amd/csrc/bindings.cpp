@@ -22,6 +22,34 @@ namespace {
 
 hipStream_t S(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
 
+// split-K workspace for GEMM calls from Python (tests / tools): grown on demand, never freed;
+// tickets zeroed once (the kernel's last arriver re-arms them)
+struct GemmWs {
+  float* ws = nullptr;
+  size_t bytes = 0;
+  int* cnt = nullptr;
+  int cnt_len = 0;
+};
+GemmWs& gemm_ws(int M, int N) {
+  static GemmWs g;
+  const size_t need = gemm_skinny_ws_bytes(std::min(M, 64), N);
+  const int need_cnt = gemm_skinny_cnt_len(N);
+  if (need > g.bytes) {
+    HIP_CHECK(hipDeviceSynchronize());
+    if (g.ws) HIP_CHECK(hipFree(g.ws));
+    HIP_CHECK(hipMalloc(&g.ws, need));
+    g.bytes = need;
+  }
+  if (need_cnt > g.cnt_len) {
+    HIP_CHECK(hipDeviceSynchronize());
+    if (g.cnt) HIP_CHECK(hipFree(g.cnt));
+    HIP_CHECK(hipMalloc(&g.cnt, need_cnt * 4));
+    HIP_CHECK(hipMemset(g.cnt, 0, need_cnt * 4));
+    g.cnt_len = need_cnt;
+  }
+  return g;
+}
+
 // Owning device matrix in the repacked layout (tests / tools)
 struct PyQMatrix {
   QWeight w{};
@@ -141,8 +169,6 @@ PYBIND11_MODULE(_engine, m) {
       .def("weight_type_summary", &Engine::weight_type_summary)
       .def_property_readonly("ready", &Engine::ready)
       .def_property_readonly("weight_bytes", &Engine::weight_bytes)
-      .def_property_readonly("blas_prefill", &Engine::blas_prefill)
-      .def_property_readonly("bf16_copy_bytes", &Engine::bf16_copy_bytes)
       .def_property_readonly("kv_bytes", &Engine::kv_bytes)
       .def_property_readonly("workspace_bytes", &Engine::workspace_bytes)
       .def_property_readonly("config", &Engine::config)
@@ -332,6 +358,8 @@ PYBIND11_MODULE(_engine, m) {
           GemmArgs a;
           a.A = (const bf16_t*)A; a.lda = lda; a.w = w->w; a.M = M; a.N = w->w.rows; a.K = w->w.cols;
           a.C = (float*)C; a.ldc = ldc; a.accumulate = accumulate;
+          GemmWs& g = gemm_ws(M, a.N);
+          a.ws = g.ws; a.ws_bytes = g.bytes; a.cnt = g.cnt; a.cnt_len = g.cnt_len;
           launch_gemm(a, S(st));
         });
   m.def("gemm_supports", &gemm_supports);
@@ -347,6 +375,8 @@ PYBIND11_MODULE(_engine, m) {
         for (int s = 0; s < a.nseg; ++s) { a.seg[s] = segs[s]->w; a.seg_n0[s] = n0; n0 += segs[s]->w.rows; }
         a.M = M; a.N = n0; a.K = segs[0]->w.cols;
         a.C = (float*)C; a.C16 = (bf16_t*)C16; a.ldc = ldc; a.epi = epi; a.ksplit = ksplit;
+        GemmWs& g = gemm_ws(M, a.N);
+        a.ws = g.ws; a.ws_bytes = g.bytes; a.cnt = g.cnt; a.cnt_len = g.cnt_len;
         launch_gemm_q(a, S(st));
       },
       py::arg("A"), py::arg("lda"), py::arg("segs"), py::arg("M"), py::arg("C"), py::arg("C16"), py::arg("ldc"),

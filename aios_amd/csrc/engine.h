@@ -169,21 +169,15 @@ class Engine {
   float *gm_x_ = nullptr, *gm_qkv_ = nullptr, *gm_q_ = nullptr, *gm_part_ = nullptr;
   bf16_t *gm_a16_ = nullptr, *gm_ff16_ = nullptr, *gm_attn16_ = nullptr;
   int *gm_tokens_ = nullptr, *gm_pos_ = nullptr, *gm_slot_ = nullptr;
-  // batched decode through the MFMA GEMM (B >= dec_gemm_min_b_): bf16 activation buffers
-  int dec_gemm_min_b_ = 8;
+  // batched decode through the skinny MFMA GEMM (B >= dec_gemm_min_b_): bf16 activation buffers
+  int dec_gemm_min_b_ = 2;
   bf16_t *dec_a16_ = nullptr, *dec_ff16_ = nullptr;
-  float* dec_gu_ = nullptr;  // [max_batch][2 d_ff] fp32 gate/up (split-K GEMM, then SwiGLU -> bf16)
-  // resident bf16 weight copies for hipBLASLt prefill (AIOS_BLAS, on when they fit in free HBM)
-  struct Layer16 {
-    bf16_t *qkv = nullptr, *o = nullptr, *gu = nullptr, *down = nullptr;
-  };
-  std::vector<Layer16> l16_;
-  std::unique_ptr<class BlasGemm> blas_;
-  float* gm_gu_ = nullptr;  // [gm_rows][2 d_ff] fp32 gate/up of the BLAS prefill path
-  size_t bf16_copy_bytes_ = 0;
- public:
-  bool blas_prefill() const { return !l16_.empty(); }
-  size_t bf16_copy_bytes() const { return bf16_copy_bytes_; }
+  // split-K slabs + arrival tickets of the skinny GEMM (shared by every decode GEMM of a step)
+  float* gk_ws_ = nullptr;
+  size_t gk_ws_bytes_ = 0;
+  int* gk_cnt_ = nullptr;
+  int gk_cnt_len_ = 0;
+  void gemm(GemmQArgs& g);  // launch_gemm_q with the engine's split-K workspace
  private:
   void layer_decode_gemm(int l, int B);
   int *pf_tokens_ = nullptr, *pf_pos_ = nullptr, *pf_seqlen_ = nullptr, *pf_slot_ = nullptr;

@@ -1,6 +1,5 @@
 // Engine implementation -- see engine.h.
 #include "engine.h"
-#include "blas.h"
 #include <cstdlib>
 #include <map>
 
@@ -433,6 +432,8 @@ void Engine::finalize() {
   // and the head layout has a flash-attention instantiation
   {
     if (const char* e = std::getenv("AIOS_PREFILL_GEMM_MIN")) gm_min_rows_ = std::max(1, std::atoi(e));
+    // one chunk per prompt up to 2048 tokens: the M tile count, not the chunk count, fills the chip
+    gm_rows_ = std::min(cfg_.max_ctx, 2048);
     if (const char* e = std::getenv("AIOS_PREFILL_GEMM_ROWS")) gm_rows_ = std::max(64, std::atoi(e));
     bool ok = attn_prefill_supports(H, Hkv, hd) && d % 64 == 0 && cfg_.d_ff % 64 == 0 && qd % 64 == 0 && kvd % 64 == 0;
     for (const auto& L : layers_) {
@@ -456,43 +457,16 @@ void Engine::finalize() {
       gm_pos_ = ibuf(G);
       gm_slot_ = ibuf(G);
       if (const char* e = std::getenv("AIOS_DECODE_GEMM_MIN_B")) dec_gemm_min_b_ = std::atoi(e);
-      // bf16 weight copies for the hipBLASLt prefill path, when they fit in half the free HBM
-      const char* eb = std::getenv("AIOS_BLAS");
-      if (!eb || std::atoi(eb) != 0) {
-        const size_t per_layer = ((size_t)(qd + 2 * kvd) * d + (size_t)d * qd + (size_t)2 * cfg_.d_ff * d +
-                                  (size_t)d * cfg_.d_ff) * 2;
-        const size_t need = per_layer * cfg_.n_layers;
-        size_t free_b = 0, total_b = 0;
-        HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
-        if (need < free_b / 2) {
-          blas_.reset(new BlasGemm());
-          if (blas_->ok()) {
-            l16_.resize(cfg_.n_layers);
-            for (int l = 0; l < cfg_.n_layers; ++l) {
-              const LayerW& L = layers_[l];
-              Layer16& w = l16_[l];
-              w.qkv = (bf16_t*)dmalloc((size_t)(qd + 2 * kvd) * d * 2);
-              launch_dequant_bf16(L.wq.w, w.qkv, stream_);
-              launch_dequant_bf16(L.wk.w, w.qkv + (size_t)qd * d, stream_);
-              launch_dequant_bf16(L.wv.w, w.qkv + (size_t)(qd + kvd) * d, stream_);
-              w.o = (bf16_t*)dmalloc((size_t)d * qd * 2);
-              launch_dequant_bf16(L.wo.w, w.o, stream_);
-              w.gu = (bf16_t*)dmalloc((size_t)2 * cfg_.d_ff * d * 2);
-              launch_dequant_bf16(L.wgu.w, w.gu, stream_);
-              w.down = (bf16_t*)dmalloc((size_t)d * cfg_.d_ff * 2);
-              launch_dequant_bf16(L.wdown.w, w.down, stream_);
-            }
-            gm_gu_ = fbuf((size_t)gm_rows_ * 2 * cfg_.d_ff);
-            bf16_copy_bytes_ = need;
-          } else {
-            blas_.reset();
-          }
-        }
-      }
       if (Bm >= 2) {
         dec_a16_ = (bf16_t*)dmalloc((size_t)Bm * std::max(d, qd) * 2);
         dec_ff16_ = (bf16_t*)dmalloc((size_t)Bm * cfg_.d_ff * 2);
-        dec_gu_ = fbuf((size_t)Bm * 2 * cfg_.d_ff);
+        ws += (size_t)Bm * (std::max(d, qd) + cfg_.d_ff) * 2;
+        const int maxN = std::max({qd + 2 * kvd, d, 2 * cfg_.d_ff, V});
+        gk_ws_bytes_ = gemm_skinny_ws_bytes(Bm, maxN);
+        gk_ws_ = (float*)dmalloc(gk_ws_bytes_);
+        ws += gk_ws_bytes_;
+        gk_cnt_len_ = gemm_skinny_cnt_len(maxN);
+        gk_cnt_ = ibuf(gk_cnt_len_);
       }
     }
   }
@@ -577,24 +551,26 @@ static std::vector<std::vector<const QMat*>> qkv_groups(const LayerW& L) {
   return {{s[0]}, {s[1]}, {s[2]}};
 }
 
+void Engine::gemm(GemmQArgs& g) {
+  g.ws = gk_ws_;
+  g.ws_bytes = gk_ws_bytes_;
+  g.cnt = gk_cnt_;
+  g.cnt_len = gk_cnt_len_;
+  launch_gemm_q(g, stream_);
+}
+
 // one transformer block for the B rows staged in x_ (decode) -- also used by prefill with
 // pointers swapped in (see prefill()).
-// Batched decode (B >= dec_gemm_min_b_): the GEMV kernels' VALU dot work grows with B while the
-// weight stream does not, so for several concurrent sequences the projections go through the
-// prefill MFMA GEMM instead (split-K for the small-N ones), with explicit RMSNorm -> bf16 and
-// RoPE/KV-write launches in place of the GEMV prologue / epilogue fusions.
+// Batched decode (B >= dec_gemm_min_b_): the int8 GEMV's dot work grows with B while the weight
+// stream does not, so from two concurrent sequences on the projections go through the skinny
+// MFMA GEMM (weights dequantised once per step into MFMA operands, split-K reduced in-launch),
+// with explicit RMSNorm -> bf16 and RoPE/KV-write launches in place of the GEMV prologue /
+// epilogue fusions.  SwiGLU runs in the gate/up GEMM's epilogue (bf16 out for the down GEMM).
 void Engine::layer_decode_gemm(int l, int B) {
   const LayerW& L = layers_[l];
   const int d = cfg_.d_model, hd = cfg_.head_dim, H = cfg_.n_heads, Hkv = cfg_.n_kv_heads, ff = cfg_.d_ff;
   const int qd = H * hd, kvd = Hkv * hd, ldqkv = qd + 2 * kvd;
   const bool tp = cfg_.tp_size > 1;
-  // from 8 rows the bf16 stream through hipBLASLt beats dequantising Q4_K tiles per workgroup
-  // (Mistral B=8: 1798 vs 1542 tok/s; B=32: 7260 vs 5762)
-  static const int blas_min_b = [] {
-    const char* e = std::getenv("AIOS_BLAS_DECODE_MIN_B");
-    return e ? std::atoi(e) : 8;
-  }();
-  const bool blas = blas_prefill() && blas_min_b > 0 && B >= blas_min_b;
   bf16_t* kc = k_cache_ + (size_t)l * layer_kv_elems_;
   bf16_t* vc = v_cache_ + (size_t)l * layer_kv_elems_;
   launch_rmsnorm_bf16(x_, d, L.attn_norm, dec_a16_, d, B, d, cfg_.norm_eps, stream_);
@@ -604,8 +580,7 @@ void Engine::layer_decode_gemm(int l, int B) {
   g.seg[0] = L.wq.w; g.seg[1] = L.wk.w; g.seg[2] = L.wv.w;
   g.seg_n0[0] = 0; g.seg_n0[1] = qd; g.seg_n0[2] = qd + kvd;
   g.N = ldqkv; g.C = qkv_; g.ldc = ldqkv; g.epi = GEPI_STORE;
-  if (blas) blas_->gemm(dec_a16_, d, l16_[l].qkv, d, qkv_, ldqkv, B, ldqkv, d, 0.f, stream_);
-  else launch_gemm_q(g, stream_);
+  gemm(g);
   QkvPostArgs p;
   p.qkv = qkv_; p.ldqkv = ldqkv; p.T = B;
   p.n_heads = H; p.n_kv_heads = Hkv; p.head_dim = hd;
@@ -627,22 +602,17 @@ void Engine::layer_decode_gemm(int l, int B) {
   std::memset(&g, 0, sizeof(g));
   g.A = dec_a16_; g.lda = qd; g.M = B; g.K = qd; g.nseg = 1; g.seg[0] = L.wo.w; g.N = d; g.ldc = d;
   if (tp) { g.C = ff_; g.epi = GEPI_STORE; } else { g.C = x_; g.epi = GEPI_ACCUM; }
-  if (blas) blas_->gemm(dec_a16_, qd, l16_[l].o, qd, g.C, d, B, d, qd, tp ? 0.f : 1.f, stream_);
-  else launch_gemm_q(g, stream_);
+  gemm(g);
   if (tp) allreduce(ff_, (size_t)B * d, x_);
   launch_rmsnorm_bf16(x_, d, L.ffn_norm, dec_a16_, d, B, d, cfg_.norm_eps, stream_);
   std::memset(&g, 0, sizeof(g));
   g.A = dec_a16_; g.lda = d; g.M = B; g.K = d; g.nseg = 1; g.seg[0] = L.wgu.w; g.N = 2 * ff;
-  // split-K needs the full gate/up sums before the nonlinearity: fp32 out, then SwiGLU -> bf16
-  g.C = dec_gu_; g.ldc = 2 * ff; g.epi = GEPI_STORE;
-  if (blas) blas_->gemm(dec_a16_, d, l16_[l].gu, d, dec_gu_, 2 * ff, B, 2 * ff, d, 0.f, stream_);
-  else launch_gemm_q(g, stream_);
-  launch_swiglu_interleaved_bf16(dec_gu_, 2 * ff, dec_ff16_, ff, B, ff, stream_);
+  g.C16 = dec_ff16_; g.ldc = ff; g.epi = GEPI_SWIGLU_BF16;
+  gemm(g);
   std::memset(&g, 0, sizeof(g));
   g.A = dec_ff16_; g.lda = ff; g.M = B; g.K = ff; g.nseg = 1; g.seg[0] = L.wdown.w; g.N = d; g.ldc = d;
   if (tp) { g.C = attn_; g.epi = GEPI_STORE; } else { g.C = x_; g.epi = GEPI_ACCUM; }
-  if (blas) blas_->gemm(dec_ff16_, ff, l16_[l].down, ff, g.C, d, B, d, ff, tp ? 0.f : 1.f, stream_);
-  else launch_gemm_q(g, stream_);
+  gemm(g);
   if (tp) allreduce(attn_, (size_t)B * d, x_);
 }
 
@@ -742,7 +712,7 @@ void Engine::enqueue_decode_step(int B) {
     std::memset(&g, 0, sizeof(g));
     g.A = dec_a16_; g.lda = d; g.M = B; g.K = d; g.nseg = 1; g.seg[0] = output_.w; g.N = V;
     g.C = logits_; g.ldc = V; g.epi = GEPI_STORE;
-    launch_gemm_q(g, stream_);
+    gemm(g);
   } else {
     gemv({&output_}, V, d, B, x_, d, out_norm_, logits_, V, EPI_STORE, 0);
   }
@@ -773,12 +743,6 @@ void Engine::prefill_gemm(int slot, const std::vector<int>& tokens, int start_po
   const int d = cfg_.d_model, hd = cfg_.head_dim, H = cfg_.n_heads, Hkv = cfg_.n_kv_heads, ff = cfg_.d_ff;
   const int qd = H * hd, kvd = Hkv * hd, ldqkv = qd + 2 * kvd, V = cfg_.vocab_size;
   const bool tp = cfg_.tp_size > 1;
-  // hipBLASLt on the resident bf16 copies for chunks worth a library GEMM (AIOS_BLAS_MIN_ROWS)
-  static const int blas_min = [] {
-    const char* e = std::getenv("AIOS_BLAS_MIN_ROWS");
-    return e ? std::atoi(e) : 64;
-  }();
-  const bool blas = blas_prefill() && T >= blas_min;
   std::vector<int> hp(gm_rows_), hs(gm_rows_, slot);
   for (int r0 = 0; r0 < T; r0 += gm_rows_) {
     const int n = std::min(gm_rows_, T - r0);
@@ -799,8 +763,7 @@ void Engine::prefill_gemm(int slot, const std::vector<int>& tokens, int start_po
       g.seg[0] = L.wq.w; g.seg[1] = L.wk.w; g.seg[2] = L.wv.w;
       g.seg_n0[0] = 0; g.seg_n0[1] = qd; g.seg_n0[2] = qd + kvd;
       g.N = ldqkv; g.C = gm_qkv_; g.ldc = ldqkv; g.epi = GEPI_STORE;
-      if (blas) blas_->gemm(gm_a16_, d, l16_[l].qkv, d, gm_qkv_, ldqkv, n, ldqkv, d, 0.f, stream_);
-      else launch_gemm_q(g, stream_);
+      gemm(g);
       QkvPostArgs p;
       p.qkv = gm_qkv_; p.ldqkv = ldqkv; p.T = n;
       p.n_heads = H; p.n_kv_heads = Hkv; p.head_dim = hd;
@@ -820,25 +783,18 @@ void Engine::prefill_gemm(int slot, const std::vector<int>& tokens, int start_po
       std::memset(&g, 0, sizeof(g));
       g.A = gm_attn16_; g.lda = qd; g.M = n; g.K = qd; g.nseg = 1; g.seg[0] = L.wo.w; g.N = d; g.ldc = d;
       if (tp) { g.C = gm_part_; g.epi = GEPI_STORE; } else { g.C = gm_x_; g.epi = GEPI_ACCUM; }
-      if (blas) blas_->gemm(gm_attn16_, qd, l16_[l].o, qd, g.C, d, n, d, qd, tp ? 0.f : 1.f, stream_);
-      else launch_gemm_q(g, stream_);
+      gemm(g);
       if (tp) allreduce(gm_part_, (size_t)n * d, gm_x_);
       // FFN
       launch_rmsnorm_bf16(gm_x_, d, L.ffn_norm, gm_a16_, d, n, d, cfg_.norm_eps, stream_);
       std::memset(&g, 0, sizeof(g));
       g.A = gm_a16_; g.lda = d; g.M = n; g.K = d; g.nseg = 1; g.seg[0] = L.wgu.w; g.N = 2 * ff;
       g.C16 = gm_ff16_; g.ldc = ff; g.epi = GEPI_SWIGLU_BF16;
-      if (blas) {
-        blas_->gemm(gm_a16_, d, l16_[l].gu, d, gm_gu_, 2 * ff, n, 2 * ff, d, 0.f, stream_);
-        launch_swiglu_interleaved_bf16(gm_gu_, 2 * ff, gm_ff16_, ff, n, ff, stream_);
-      } else {
-        launch_gemm_q(g, stream_);
-      }
+      gemm(g);
       std::memset(&g, 0, sizeof(g));
       g.A = gm_ff16_; g.lda = ff; g.M = n; g.K = ff; g.nseg = 1; g.seg[0] = L.wdown.w; g.N = d; g.ldc = d;
       if (tp) { g.C = gm_part_; g.epi = GEPI_STORE; } else { g.C = gm_x_; g.epi = GEPI_ACCUM; }
-      if (blas) blas_->gemm(gm_ff16_, ff, l16_[l].down, ff, g.C, d, n, d, ff, tp ? 0.f : 1.f, stream_);
-      else launch_gemm_q(g, stream_);
+      gemm(g);
       if (tp) allreduce(gm_part_, (size_t)n * d, gm_x_);
     }
     if (r0 + n == T && want_logits)

@@ -1,0 +1,332 @@
+// Batched-decode GEMM (M <= 64 rows of activations): C[M][N] = X[M][K] (bf16) x W[N][K]^T with
+// W streamed from its repacked quantised layout straight into MFMA operand registers.
+//
+// SURVEY.md §2.7 K3 decode column at B > 1 (llama.cpp's mul_mat_q / mmvq for small batches inside
+// llama-server, /root/reference/runtime/src/model_manager.rs:187-204): the weights are the only
+// large operand, read once per step, so the kernel is shaped like a GEMV that happens to finish
+// on the matrix cores:
+//   * transposed product D[n][m] = W[n][:] . X[m][:] on v_mfma_f32_16x16x32_bf16 with the weight
+//     rows as the A operand: lane (n = l & 15, q = l >> 4) loads one 16-B quant chunk (32 weights)
+//     per step, dequantises it in registers into four 8-weight fragments and never touches LDS
+//     with weight data (CDNA guide §5 "GEMV / M <= 16 decode weights": straight to VGPRs);
+//   * the k-slots of a fragment are whatever k the chunk holds -- the activation fragment of lane
+//     (m, q) is read from the same k set, so no weight repack for MFMA is needed;
+//   * X (bf16, the small operand) is staged through LDS in 4-step chunks, double-buffered and
+//     register-prefetched one chunk ahead, so its loads are always OLDER than the weight loads in
+//     flight and no vmcnt wait ever drains the weight ring;
+//   * weights are ring-buffered NL = 4 steps ahead per lane (the whole 16-row x 512-k slice of a
+//     wave in flight for Q4_K), 8 (or 4) waves per workgroup each on their own 16 rows;
+//   * K is split over S workgroups when the row tiles alone do not fill the chip; partial tiles
+//     go to write-through (sc1) fp32 slabs and the LAST arriving workgroup of a tile (relaxed
+//     agent ticket, one agent-scope acquire; CDNA guide §5 "In-launch split-K reduction") sums
+//     them and runs the epilogue -- no float atomics, deterministic result, one launch.
+// The B = 1 step keeps the int8-activation GEMV (gemv_q8.h, 4 MACs per VALU op); from B = 2 the
+// dequant-once MFMA form is cheaper than B passes of v_dot4.
+#include "gemm_common.h"
+
+namespace aios {
+
+constexpr int SK_NL = 4;    // weight ring depth = steps per X chunk
+constexpr int SK_SMAX = 8;  // K splits at most (slab workspace: gemm_skinny_ws_bytes)
+
+template <int QT>
+struct SkFmt {
+  static constexpr int W = QFmt<QT>::W;   // weights per 16-B chunk
+  static constexpr int NP = W / 8;         // 8-weight MFMA k-slots per chunk
+  static constexpr int STEPK = 4 * W;      // k covered by one load step (4 lanes per row)
+  static constexpr int KC = SK_NL * STEPK; // k per staged X chunk
+  // first k of part i of chunk c
+  __device__ static int part_k(int c, int i) {
+    if constexpr (NP == 4) return QFmt<QT>::chunk_k0(c, i >> 1) + 8 * (i & 1);
+    else if constexpr (NP == 2) return QFmt<QT>::chunk_k0(c, 0) + 8 * i;
+    else return QFmt<QT>::chunk_k0(c, 0);
+  }
+};
+
+template <int QT, int RB, int MT, int EPI>
+__global__ void __launch_bounds__(RB * 64) gemm_skinny_kernel(GemmQArgs a, int S) {
+  using F = SkFmt<QT>;
+  constexpr int NT = RB * 64, ROWS = 16 * RB, MP = 16 * MT;
+  constexpr int KC = F::KC, XROW = KC + 8;  // bf16 per LDS row (+16 B pad: conflict-free column reads)
+  constexpr int XU = MP * KC / 8;           // 16-B units of one X chunk
+  constexpr int XPT = (XU + NT - 1) / NT;   // per thread
+  __shared__ __attribute__((aligned(16))) bf16_t Xs[2][MP * XROW];
+  __shared__ int last_flag;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int rr = lane & 15, q = lane >> 4;
+  const int ntile = a.N / ROWS, total = ntile * S;
+  const int L = xcd_remap(blockIdx.x, total);
+  const int rg = L / S, sp = L % S;  // a tile's slices are consecutive: one XCD, same-L2 slabs
+  const int n0 = rg * ROWS;
+  int s = 0;
+  if (a.nseg > 1 && n0 >= a.seg_n0[1]) s = 1;
+  if (a.nseg > 2 && n0 >= a.seg_n0[2]) s = 2;
+  QWeight w;
+  w.qtype = QT;
+  w.rows = s == 0 ? a.seg[0].rows : (s == 1 ? a.seg[1].rows : a.seg[2].rows);
+  w.cols = a.K;
+  w.pad_ = 0;
+  w.p0 = s == 0 ? a.seg[0].p0 : (s == 1 ? a.seg[1].p0 : a.seg[2].p0);
+  w.p1 = s == 0 ? a.seg[0].p1 : (s == 1 ? a.seg[1].p1 : a.seg[2].p1);
+  w.p2 = s == 0 ? a.seg[0].p2 : (s == 1 ? a.seg[1].p2 : a.seg[2].p2);
+  w.p3 = s == 0 ? a.seg[0].p3 : (s == 1 ? a.seg[1].p3 : a.seg[2].p3);
+  const int lrow = n0 - (s == 0 ? a.seg_n0[0] : (s == 1 ? a.seg_n0[1] : a.seg_n0[2])) + 16 * wave + rr;
+  const int nch = a.K / F::W;                       // chunks per weight row
+  const int nsteps = (nch + 3) / 4;                 // load steps per row
+  const int nchunk = (nsteps + SK_NL - 1) / SK_NL;  // X chunks over K
+  const int c0 = (int)((long)sp * nchunk / S), c1 = (int)((long)(sp + 1) * nchunk / S);
+  const int tb = c0 * SK_NL, te = min(c1 * SK_NL, nsteps);  // this workgroup's steps [tb, te)
+
+  // ---- X chunk staging (register prefetch one chunk ahead, zero past M / K)
+  gu32x4 xr[XPT];
+  auto x_load = [&](int c) __attribute__((always_inline)) {
+    const int kc0 = c * KC;
+#pragma unroll
+    for (int i = 0; i < XPT; ++i) {
+      const int u = tid + NT * i;
+      const int m = u / (KC / 8), k = kc0 + 8 * (u % (KC / 8));
+      const int mm = min(m, a.M - 1), kk = min(k, a.K - 8);
+      xr[i] = *(const gu32x4*)(a.A + (size_t)mm * a.lda + kk);  // unconditional (clamped) load
+    }
+  };
+  auto x_store = [&](int buf, int c) __attribute__((always_inline)) {
+    const int kc0 = c * KC;
+#pragma unroll
+    for (int i = 0; i < XPT; ++i) {
+      const int u = tid + NT * i;
+      if (XU % NT == 0 || u < XU) {
+        const int m = u / (KC / 8), kl = 8 * (u % (KC / 8));
+        gu32x4 v = xr[i];
+        if (m >= a.M || kc0 + kl >= a.K) v = gu32x4{0u, 0u, 0u, 0u};
+        *(gu32x4*)&Xs[buf][m * XROW + kl] = v;
+      }
+    }
+  };
+
+  // ---- weight ring: step t -> chunk 4t + q of this lane's row (clamped in-bounds load).  Q4_K /
+  // Q5_K keep one 16-B scale/min record per 256-block = per two steps: only even steps load it
+  // and the odd step re-uses it (meta_cur), halving the load instructions.
+  constexpr bool MB = QT == QT_Q4_K || QT == QT_Q5_K;
+  RawChunk ring[SK_NL];
+  uint4 meta_cur = make_uint4(0, 0, 0, 0);
+  const int nbk = a.K >> 8;
+  auto w_load = [&](int t, RawChunk& r, bool with_meta) __attribute__((always_inline)) {
+    const int c = min(4 * min(t, te - 1) + q, nch - 1);
+    if constexpr (MB) {
+      r.a = *(const uint4*)(w.p0 + ((size_t)lrow * nbk * 8 + c) * 16);
+      if (with_meta) r.b = *(const uint4*)(w.p1 + ((size_t)lrow * nbk + (c >> 3)) * 16);
+      if constexpr (QT == QT_Q5_K) r.c = *(const uint4*)(w.p2 + ((size_t)lrow * nbk + (c >> 3)) * 32 + 16 * (c & 1));
+    } else {
+      QFmt<QT>::load(w, lrow, c, r);
+    }
+  };
+
+  gf32x4 acc[MT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) acc[mt] = gf32x4{0.f, 0.f, 0.f, 0.f};
+
+  constexpr bool BYTES = QT != QT_F16 && QT != QT_BF16;
+  auto compute = [&](const RawChunk& r, const uint4& meta, int t, int buf, int kc0) __attribute__((always_inline)) {
+    const int c = 4 * t + q;
+    const bool valid = c < nch;
+    float sc[2], of[2];
+    if constexpr (MB) {
+      RawChunk rm = r;
+      rm.b = meta;
+      QStream<QT>::scales(rm, c, sc, of);
+    } else {
+      QStream<QT>::scales(r, c, sc, of);
+    }
+    if (!valid) sc[0] = sc[1] = of[0] = of[1] = 0.f;
+    if constexpr (QFmt<QT>::RUNS == 1) { sc[1] = sc[0]; of[1] = of[0]; }
+#pragma unroll
+    for (int i = 0; i < F::NP; ++i) {
+      float qv[8];
+      if constexpr (BYTES) {
+        // raw codes as byte words made opaque, so every byte converts with one v_cvt_f32_ubyteN
+        uint32_t w0 = QStream<QT>::word(r, c, 2 * i), w1 = QStream<QT>::word(r, c, 2 * i + 1);
+        asm volatile("" : "+v"(w0), "+v"(w1));
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          qv[e] = (float)((w0 >> (8 * e)) & 0xff);
+          qv[4 + e] = (float)((w1 >> (8 * e)) & 0xff);
+        }
+      } else {
+        QStream<QT>::quad(r, c, 2 * i, qv);
+        QStream<QT>::quad(r, c, 2 * i + 1, qv + 4);
+      }
+      const int run = F::NP == 4 ? (i >> 1) : 0;
+      const float s_ = sc[run], o_ = of[run];
+      uint32_t p[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) p[e] = pk_bf16(fmaf(s_, qv[2 * e], -o_), fmaf(s_, qv[2 * e + 1], -o_));
+      gbf16x8 wf;
+      __builtin_memcpy(&wf, p, 16);
+      const int kl = F::part_k(c, i) - kc0;
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const uint4 xv = *(const uint4*)&Xs[buf][(16 * mt + rr) * XROW + kl];
+        gbf16x8 xf;
+        __builtin_memcpy(&xf, &xv, 16);
+        acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, xf, acc[mt], 0, 0, 0);
+      }
+    }
+  };
+
+  // prologue: X chunk c0 first (oldest loads), then the weight ring, then X chunk c0+1
+  x_load(c0);
+#pragma unroll
+  for (int u = 0; u < SK_NL; ++u) w_load(tb + u, ring[u], !MB || (u & 1) == 0);
+  x_store(0, c0);
+  x_load(min(c0 + 1, c1 - 1));
+  __syncthreads();
+  for (int c = c0; c < c1; ++c) {
+    const int buf = (c - c0) & 1, kc0 = c * KC;
+#pragma unroll
+    for (int u = 0; u < SK_NL; ++u) {
+      const int t = c * SK_NL + u;
+      if (t < te) compute(ring[u], (u & 1) ? meta_cur : ring[u].b, t, buf, kc0);
+      if (MB && (u & 1) == 0) meta_cur = ring[u].b;
+      w_load(t + SK_NL, ring[u], !MB || (u & 1) == 0);
+    }
+    if (c + 1 < c1) x_store(buf ^ 1, c + 1);
+    x_load(min(c + 2, c1 - 1));
+    __syncthreads();
+  }
+
+  // ---- epilogue.  lane holds D[n = 4q + j][m = 16 mt + rr], j = 0..3
+  const int nl = 16 * wave + 4 * q;  // tile-local first row of this lane's 4 outputs
+  auto finish = [&](int m, int n, gf32x4 v) __attribute__((always_inline)) {
+    if (m >= a.M) return;
+    if constexpr (EPI == GEPI_SWIGLU_BF16) {
+      const uint32_t pk = pk_bf16(v[0] / (1.f + __expf(-v[0])) * v[1], v[2] / (1.f + __expf(-v[2])) * v[3]);
+      *(uint32_t*)(a.C16 + (size_t)m * a.ldc + (n >> 1)) = pk;
+    } else {
+      float4* c = (float4*)(a.C + (size_t)m * a.ldc + n);
+      if constexpr (EPI == GEPI_ACCUM) {
+        const float4 o = *c;
+        *c = make_float4(o.x + v[0], o.y + v[1], o.z + v[2], o.w + v[3]);
+      } else {
+        *c = make_float4(v[0], v[1], v[2], v[3]);
+      }
+    }
+  };
+  if (S == 1) {
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) finish(16 * mt + rr, n0 + nl, acc[mt]);
+    return;
+  }
+  // split-K: slab [sp][rg][MP][ROWS] written through (sc1: no release fence needed), then the
+  // last arriver of the tile (relaxed agent ticket) acquires and reduces (CDNA guide §5 item 2)
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)a.ws, (short)0, 0x7fffffff, 0x00020000);
+  const int sbase = (int)(((size_t)sp * ntile + rg) * MP * ROWS * 4);
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(gu32x4, acc[mt]), rs,
+                                           sbase + ((16 * mt + rr) * ROWS + nl) * 4, 0, 16 /* sc1 */);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its slab stores
+  __syncthreads();
+  if (tid == 0) {
+    const int t = __hip_atomic_fetch_add(a.cnt + rg, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = t == S - 1;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(a.cnt + rg, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
+    }
+    last_flag = last;
+  }
+  __syncthreads();
+  if (!last_flag) return;
+  const size_t sstride = (size_t)ntile * MP * ROWS;
+  const float* base = a.ws + (size_t)rg * MP * ROWS;
+  for (int u = tid; u < MP * ROWS / 4; u += NT) {
+    const int m = u / (ROWS / 4), n4 = 4 * (u % (ROWS / 4));
+    // all slices' loads in flight at once (S <= SK_SMAX; clamped re-reads weighted by zero)
+    gf32x4 part[SK_SMAX];
+#pragma unroll
+    for (int k = 0; k < SK_SMAX; ++k)
+      part[k] = *(const gf32x4*)(base + min(k, S - 1) * sstride + (size_t)m * ROWS + n4);
+    gf32x4 v = part[0];
+#pragma unroll
+    for (int k = 1; k < SK_SMAX; ++k)
+      if (k < S) v += part[k];
+    finish(m, n0 + n4, v);
+  }
+}
+
+size_t gemm_skinny_ws_bytes(int M, int N) { return (size_t)8 * 16 * ((M + 15) / 16) * N * 4; }
+int gemm_skinny_cnt_len(int N) { return N / 64 + 1; }
+
+static int sk_env(const char* name, int dflt) {
+  const char* e = std::getenv(name);
+  return e ? std::atoi(e) : dflt;
+}
+
+template <int QT, int RB, int MT>
+static void sk_launch(const GemmQArgs& a, int S, hipStream_t st) {
+  const int grid = (a.N / (16 * RB)) * S;
+  switch (a.epi) {
+    case GEPI_STORE:
+      hipLaunchKernelGGL((gemm_skinny_kernel<QT, RB, MT, GEPI_STORE>), dim3(grid), dim3(RB * 64), 0, st, a, S);
+      break;
+    case GEPI_ACCUM:
+      hipLaunchKernelGGL((gemm_skinny_kernel<QT, RB, MT, GEPI_ACCUM>), dim3(grid), dim3(RB * 64), 0, st, a, S);
+      break;
+    default:
+      hipLaunchKernelGGL((gemm_skinny_kernel<QT, RB, MT, GEPI_SWIGLU_BF16>), dim3(grid), dim3(RB * 64), 0, st, a, S);
+      break;
+  }
+}
+
+template <int QT, int RB>
+static void sk_mt(const GemmQArgs& a, int S, hipStream_t st) {
+  if (a.M <= 16) sk_launch<QT, RB, 1>(a, S, st);
+  else if (a.M <= 32) sk_launch<QT, RB, 2>(a, S, st);
+  else sk_launch<QT, RB, 4>(a, S, st);
+}
+
+template <int QT>
+static bool sk_qt(const GemmQArgs& a, hipStream_t st) {
+  using F = SkFmt<QT>;
+  bool rows128 = a.N % 128 == 0;
+  for (int s = 0; s < a.nseg; ++s)
+    if (a.seg_n0[s] % 128 || a.seg[s].rows % 128) rows128 = false;
+  const int force_rb = sk_env("AIOS_SKINNY_RB", 0);
+  const int RB = force_rb == 4 ? 4 : (force_rb == 8 ? (rows128 ? 8 : 4) : (rows128 ? 8 : 4));
+  const int ntile = a.N / (16 * RB);
+  const int nsteps = (a.K / F::W + 3) / 4, nchunk = (nsteps + SK_NL - 1) / SK_NL;
+  const int MP = 16 * (a.M <= 16 ? 1 : (a.M <= 32 ? 2 : 4));
+  // LDS per workgroup: two X chunks; resident workgroups per CU bounded by LDS and by 2048 threads
+  const int lds = 2 * MP * (F::KC + 8) * 2;
+  const int per_cu = std::max(1, std::min(163840 / lds, 2048 / (RB * 64)));
+  int S = a.ksplit > 0 ? a.ksplit : sk_env("AIOS_SKINNY_S", 0);
+  if (S <= 0) {
+    const int target = device_cu_count() * std::min(per_cu, 2);
+    S = ntile >= target ? 1 : (target + ntile - 1) / ntile;
+  }
+  S = std::max(1, std::min({S, nchunk, SK_SMAX}));
+  // split-K needs the slab workspace and tickets; without them, one workgroup per tile
+  if (S > 1 && (!a.ws || !a.cnt || a.cnt_len < ntile || a.ws_bytes < (size_t)S * MP * a.N * 4)) S = 1;
+  if (RB == 8) sk_mt<QT, 8>(a, S, st);
+  else sk_mt<QT, 4>(a, S, st);
+  return true;
+}
+
+bool launch_gemm_skinny(const GemmQArgs& a, hipStream_t st) {
+  if (a.M > 64 || a.N % 64) return false;
+  if (a.epi == GEPI_SWIGLU_BF16 && a.ldc % 2) return false;
+  if ((a.epi != GEPI_SWIGLU_BF16 && a.ldc % 4) || a.lda % 8) return false;
+  switch (a.seg[0].qtype) {
+    case QT_Q4_K: return sk_qt<QT_Q4_K>(a, st);
+    case QT_Q5_K: return sk_qt<QT_Q5_K>(a, st);
+    case QT_Q6_K: return sk_qt<QT_Q6_K>(a, st);
+    case QT_Q4_0: return sk_qt<QT_Q4_0>(a, st);
+    case QT_Q8_0: return sk_qt<QT_Q8_0>(a, st);
+    case QT_F16: return sk_qt<QT_F16>(a, st);
+    case QT_BF16: return sk_qt<QT_BF16>(a, st);
+    default: return false;
+  }
+}
+
+}  // namespace aios

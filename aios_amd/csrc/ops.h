@@ -123,6 +123,10 @@ struct GemmArgs {
   float* C;
   int ldc;
   int accumulate;  // C += result
+  float* ws = nullptr;  // split-K workspace of the skinny (M <= 64) kernel, see GemmQArgs
+  size_t ws_bytes = 0;
+  int* cnt = nullptr;
+  int cnt_len = 0;
 };
 void launch_gemm(const GemmArgs& a, hipStream_t st);
 bool gemm_supports(int qt);
@@ -140,8 +144,17 @@ struct GemmQArgs {
   bf16_t* C16;       // [M][ldc] bf16 (SWIGLU_BF16: column n/2 = silu(col n) * col n+1)
   int ldc;
   int epi;
-  int ksplit;        // K split over workgroups (atomic partial sums): 0 = auto, 1 = off
+  int ksplit;        // K split over workgroups: 0 = auto, 1 = off
+  // skinny (M <= 64) split-K: fp32 partial slabs [S][tiles][16*Mt][rows] + per-tile arrival
+  // tickets (zero-initialised, re-armed by each tile's last arriver).  Null -> no split.
+  float* ws;
+  size_t ws_bytes;
+  int* cnt;
+  int cnt_len;
 };
+// bytes of split-K workspace / ticket count the skinny GEMM may use for an M x N output
+size_t gemm_skinny_ws_bytes(int M, int N);
+int gemm_skinny_cnt_len(int N);
 void launch_gemm_q(const GemmQArgs& a, hipStream_t st);
 
 }  // namespace aios

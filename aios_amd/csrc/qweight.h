@@ -328,6 +328,11 @@ struct QStream<QT_Q4_K> {
     const uint32_t wv = u4_word(r.a, j & 3);
     ubytes4(j < 4 ? (wv & 0x0f0f0f0fu) : ((wv >> 4) & 0x0f0f0f0fu), q);
   }
+  // the 4 raw codes of quad j as the 4 bytes of one word
+  __device__ static uint32_t word(const RawChunk& r, int c, int j) {
+    const uint32_t wv = u4_word(r.a, j & 3);
+    return j < 4 ? (wv & 0x0f0f0f0fu) : ((wv >> 4) & 0x0f0f0f0fu);
+  }
 };
 
 template <>
@@ -341,6 +346,12 @@ struct QStream<QT_Q5_K> {
     const uint32_t nib = j < 4 ? (wv & 0x0f0f0f0fu) : ((wv >> 4) & 0x0f0f0f0fu);
     const uint32_t hb = (hv >> (2 * g + (j >= 4 ? 1 : 0))) & 0x01010101u;
     ubytes4(nib | (hb << 4), q);
+  }
+  __device__ static uint32_t word(const RawChunk& r, int c, int j) {
+    const int g = (c & 7) >> 1;
+    const uint32_t wv = u4_word(r.a, j & 3), hv = u4_word(r.c, j & 3);
+    const uint32_t nib = j < 4 ? (wv & 0x0f0f0f0fu) : ((wv >> 4) & 0x0f0f0f0fu);
+    return nib | (((hv >> (2 * g + (j >= 4 ? 1 : 0))) & 0x01010101u) << 4);
   }
 };
 
@@ -356,6 +367,9 @@ struct QStream<QT_Q6_K> {
   __device__ static void quad(const RawChunk& r, int c, int j, float q[4]) {
     ubytes4(j < 4 ? QFmt<QT_Q6_K>::code_lo(r, j) : QFmt<QT_Q6_K>::code_hi(r, j & 3), q);
   }
+  __device__ static uint32_t word(const RawChunk& r, int c, int j) {
+    return j < 4 ? QFmt<QT_Q6_K>::code_lo(r, j) : QFmt<QT_Q6_K>::code_hi(r, j & 3);
+  }
 };
 
 template <>
@@ -369,6 +383,10 @@ struct QStream<QT_Q4_0> {
     const uint32_t wv = u4_word(r.a, j & 3);
     ubytes4(j < 4 ? (wv & 0x0f0f0f0fu) : ((wv >> 4) & 0x0f0f0f0fu), q);
   }
+  __device__ static uint32_t word(const RawChunk& r, int c, int j) {
+    const uint32_t wv = u4_word(r.a, j & 3);
+    return j < 4 ? (wv & 0x0f0f0f0fu) : ((wv >> 4) & 0x0f0f0f0fu);
+  }
 };
 
 template <>
@@ -381,6 +399,7 @@ struct QStream<QT_Q8_0> {
   __device__ static void quad(const RawChunk& r, int c, int j, float q[4]) {
     ubytes4(u4_word(r.a, j) ^ 0x80808080u, q);
   }
+  __device__ static uint32_t word(const RawChunk& r, int c, int j) { return u4_word(r.a, j) ^ 0x80808080u; }
 };
 
 template <>

@@ -138,18 +138,27 @@ def test_prefill_gemm_vs_gemv_path(model_files, monkeypatch):
     assert np.abs(l1 - l2).max() < 2e-2 * max(np.abs(l1).max(), 1.0)
 
 
-def test_batched_decode_gemm_path_matches_gemv_path(model_files, monkeypatch):
-    """B >= AIOS_DECODE_GEMM_MIN_B runs the projections through the MFMA GEMM (split-K for small
-    N); its logits must match the GEMV path's for the same batch."""
+@pytest.mark.parametrize("B", [2, 3, 4])
+@pytest.mark.parametrize("graph", [False, True])
+def test_batched_decode_gemm_path_matches_gemv_path(model_files, monkeypatch, B, graph):
+    """B >= AIOS_DECODE_GEMM_MIN_B runs the projections through the skinny MFMA GEMM (split-K
+    slabs reduced in-launch, SwiGLU in the gate/up epilogue, residual accumulate in O/down); its
+    logits must match the fp32-activation GEMV path's for the same batch, eager and replayed from
+    the captured decode graph."""
     path = model_files["Q4_K_M"]
-    prompts = [[1, 5, 6, 7], [1, 9, 10, 11, 12, 13], [1, 100, 200], [1, 3, 4]]
+    prompts = [[1, 5, 6, 7], [1, 9, 10, 11, 12, 13], [1, 100, 200], [1, 3, 4]][:B]
     outs = {}
     for mode, min_b in (("gemv", "0"), ("gemm", "2")):
         monkeypatch.setenv("AIOS_DECODE_GEMM_MIN_B", min_b)
         eng, cfg = _load(path, max_slots=4, max_batch=4, act_q8=False)
         firsts = [int(np.argmax(eng.prefill(s, p, 0, True))) for s, p in enumerate(prompts)]
-        toks = eng.decode([0, 1, 2, 3], firsts, [len(p) for p in prompts])
-        outs[mode] = (toks, np.asarray(eng.last_logits(4)).reshape(4, -1))
+        if graph:
+            eng.decode_loop_prepare(list(range(B)), firsts, [len(p) for p in prompts])
+            eng.decode_loop_run(B, 3, True)
+            toks = None
+        else:
+            toks = eng.decode(list(range(B)), firsts, [len(p) for p in prompts])
+        outs[mode] = (toks, np.asarray(eng.last_logits(B)).reshape(B, -1))
         del eng
     l0, l1 = outs["gemv"][1], outs["gemm"][1]
     scale = max(np.abs(l0).max(), 1.0)
@@ -157,20 +166,14 @@ def test_batched_decode_gemm_path_matches_gemv_path(model_files, monkeypatch):
 
 
 @pytest.mark.parametrize("recipe", ["Q4_K_M", "mistral_shape"])
-def test_prefill_blas_path_matches_reference(model_files, recipe, monkeypatch):
-    """Long prompts go through hipBLASLt on the resident bf16 weight copies; same tolerance as the
-    fused-dequant MFMA path, and both paths agree."""
+def test_prefill_one_chunk_matches_reference(model_files, recipe):
+    """A 140-token prompt prefills as ONE GEMM chunk (big-M MFMA kernel, dequant fused; no bf16
+    weight copy exists) and matches the fp32 reference."""
     path = model_files[recipe]
     ref = ReferenceModel.from_gguf(path, kv_bf16=True)
     prompt = [1] + list(np.random.default_rng(5).integers(3, 200, 140))
     rl = ref.forward(prompt)[-1]
     scale = max(rl.abs().max().item(), 1.0)
-    got = {}
-    for blas in ("1", "0"):
-        monkeypatch.setenv("AIOS_BLAS", blas)
-        eng, cfg = _load(path)
-        assert eng.blas_prefill == (blas == "1")
-        got[blas] = torch.from_numpy(np.asarray(eng.prefill(0, prompt, 0, True)))
-        del eng
-    assert (got["1"] - rl).abs().max().item() < 2e-2 * scale
-    assert (got["1"] - got["0"]).abs().max().item() < 2e-2 * scale
+    eng, cfg = _load(path)
+    got = torch.from_numpy(np.asarray(eng.prefill(0, prompt, 0, True)))
+    assert (got - rl).abs().max().item() < 2e-2 * scale

@@ -369,3 +369,65 @@ def test_attention_prefill_causal(E, H, Hkv, hd, start, T):
     ref = torch.einsum("htl,hld->thd", torch.softmax(s, -1), v).reshape(T, H * hd)
     err = (out.float().cpu() - ref).abs().max().item()
     assert err < 3e-2, err
+
+
+# ---- skinny (M <= 64) batched-decode GEMM: weights streamed into MFMA operands ---------------------
+@pytest.mark.parametrize("t", QTS)
+@pytest.mark.parametrize("M", [2, 16, 33, 64])
+@pytest.mark.parametrize("ksplit", [1, 3])
+@pytest.mark.parametrize("epi", ["store", "accum", "swiglu"])
+def test_gemm_skinny(E, t, M, ksplit, epi):
+    N, K = 256, 2048
+    m, W = qmat(E, t, N, K, seed=31, std=0.05)
+    A = torch.randn(M, K, device="cuda").to(torch.bfloat16)
+    y = A.float().cpu() @ W.to(torch.bfloat16).float().T
+    if epi == "swiglu":
+        out = torch.zeros(M, N // 2, dtype=torch.bfloat16, device="cuda")
+        E.gemm_q(A.data_ptr(), K, [m], M, 0, out.data_ptr(), N // 2, E.GEPI_SWIGLU_BF16, stream(), ksplit)
+        torch.cuda.synchronize()
+        ref = torch.nn.functional.silu(y[:, 0::2]) * y[:, 1::2]
+        assert torch.allclose(out.float().cpu(), ref, atol=2e-2, rtol=2e-2), (out.float().cpu() - ref).abs().max()
+        return
+    C = torch.full((M, N), 3.0, device="cuda")
+    E.gemm_q(A.data_ptr(), K, [m], M, C.data_ptr(), 0, N,
+             E.GEPI_STORE if epi == "store" else E.GEPI_ACCUM, stream(), ksplit)
+    torch.cuda.synchronize()
+    ref = y if epi == "store" else y + 3.0
+    assert torch.allclose(C.cpu(), ref, atol=3e-3, rtol=3e-3), (C.cpu() - ref).abs().max()
+
+
+@pytest.mark.parametrize("M", [4, 32])
+def test_gemm_skinny_mixed_segments_long_k(E, M):
+    # Q4_K_M-style QKV (Q4_K q/k + Q6_K v, two launches) and a K = 14336 down projection with the
+    # automatic split: every tile's last arriver reduces the slabs (tickets re-armed per launch)
+    K = 4096
+    segs = [(GGMLType.Q4_K, 512), (GGMLType.Q4_K, 128), (GGMLType.Q6_K, 128)]
+    mats, refs = zip(*[qmat(E, t, n, K, seed=40 + i, std=0.02) for i, (t, n) in enumerate(segs)])
+    W = torch.cat(refs, 0)
+    A = torch.randn(M, K, device="cuda").to(torch.bfloat16)
+    C = torch.zeros(M, W.shape[0], device="cuda")
+    for _ in range(2):  # second call re-uses the re-armed tickets
+        E.gemm_q(A.data_ptr(), K, list(mats), M, C.data_ptr(), 0, W.shape[0], E.GEPI_STORE, stream())
+    torch.cuda.synchronize()
+    ref = A.float().cpu() @ W.to(torch.bfloat16).float().T
+    assert torch.allclose(C.cpu(), ref, atol=3e-3, rtol=3e-3), (C.cpu() - ref).abs().max()
+    m, Wd = qmat(E, GGMLType.Q6_K, 256, 14336, seed=50, std=0.01)
+    X = torch.randn(M, 14336, device="cuda").to(torch.bfloat16)
+    D = torch.ones(M, 256, device="cuda")
+    E.gemm_q(X.data_ptr(), 14336, [m], M, D.data_ptr(), 0, 256, E.GEPI_ACCUM, stream())
+    torch.cuda.synchronize()
+    refd = X.float().cpu() @ Wd.to(torch.bfloat16).float().T + 1.0
+    assert torch.allclose(D.cpu(), refd, atol=4e-3, rtol=4e-3), (D.cpu() - refd).abs().max()
+
+
+@pytest.mark.parametrize("M,N,K", [(512, 1024, 4096), (2048, 512, 1024), (300, 384, 2048)])
+@pytest.mark.parametrize("t", [GGMLType.Q4_K, GGMLType.Q6_K])
+def test_gemm_big_tiles_match(E, M, N, K, t):
+    # 256-row and 128-row workgroup tiles (AIOS_GEMM_BM picks by grid size), partial last M tile
+    m, W = qmat(E, t, N, K, seed=60, std=0.02)
+    A = torch.randn(M, K, device="cuda").to(torch.bfloat16)
+    C = torch.zeros(M, N, device="cuda")
+    E.gemm_q(A.data_ptr(), K, [m], M, C.data_ptr(), 0, N, E.GEPI_STORE, stream())
+    torch.cuda.synchronize()
+    ref = A.float() @ W.to(torch.bfloat16).float().cuda().T
+    assert torch.allclose(C, ref, atol=3e-3, rtol=3e-3), (C - ref).abs().max()
