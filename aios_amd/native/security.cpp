@@ -2,6 +2,8 @@
 #include "security.h"
 
 #include <dirent.h>
+#include <fcntl.h>
+#include <sys/file.h>
 #include <openssl/evp.h>
 #include <openssl/pem.h>
 #include <openssl/x509.h>
@@ -827,20 +829,61 @@ X509Ptr make_cert(EVP_PKEY* key, const std::string& cn, X509* issuer, EVP_PKEY* 
   return c;
 }
 
-void write_pem_key(const std::string& path, EVP_PKEY* k) {
-  FILE* f = fopen(path.c_str(), "wb");
-  if (!f) throw std::runtime_error("tls: cannot write " + path);
-  PEM_write_PrivateKey(f, k, nullptr, nullptr, 0, nullptr, nullptr);
+// PEM files are written to a private temp file (created O_EXCL with the final mode, so a key is
+// never world-readable, not even briefly) and rename()d into place: a concurrent reader sees the
+// old file or the complete new one, never a half-written one.
+FILE* open_private_tmp(const std::string& path, mode_t mode, std::string& tmp) {
+  tmp = path + ".tmp." + std::to_string(::getpid());
+  ::unlink(tmp.c_str());
+  const int fd = ::open(tmp.c_str(), O_WRONLY | O_CREAT | O_EXCL | O_CLOEXEC, mode);
+  if (fd < 0) throw std::runtime_error("tls: cannot create " + tmp);
+  FILE* f = ::fdopen(fd, "wb");
+  if (!f) {
+    ::close(fd);
+    throw std::runtime_error("tls: cannot open " + tmp);
+  }
+  return f;
+}
+
+void commit_tmp(FILE* f, const std::string& tmp, const std::string& path) {
+  fflush(f);
+  ::fsync(fileno(f));
   fclose(f);
-  ::chmod(path.c_str(), 0600);
+  if (::rename(tmp.c_str(), path.c_str()) != 0) {
+    ::unlink(tmp.c_str());
+    throw std::runtime_error("tls: cannot install " + path);
+  }
+}
+
+void write_pem_key(const std::string& path, EVP_PKEY* k) {
+  std::string tmp;
+  FILE* f = open_private_tmp(path, 0600, tmp);
+  PEM_write_PrivateKey(f, k, nullptr, nullptr, 0, nullptr, nullptr);
+  commit_tmp(f, tmp, path);
 }
 
 void write_pem_cert(const std::string& path, X509* c) {
-  FILE* f = fopen(path.c_str(), "wb");
-  if (!f) throw std::runtime_error("tls: cannot write " + path);
+  std::string tmp;
+  FILE* f = open_private_tmp(path, 0644, tmp);
   PEM_write_X509(f, c);
-  fclose(f);
+  commit_tmp(f, tmp, path);
 }
+
+// exclusive advisory lock on <dir>/.lock for the lifetime of the object: services started
+// together by aios-init serialise their "generate if missing" so exactly one CA is created
+struct DirLock {
+  int fd = -1;
+  explicit DirLock(const std::string& dir) {
+    fd = ::open((dir + "/.lock").c_str(), O_RDWR | O_CREAT | O_CLOEXEC, 0600);
+    if (fd >= 0) ::flock(fd, LOCK_EX);
+  }
+  ~DirLock() {
+    if (fd >= 0) {
+      ::flock(fd, LOCK_UN);
+      ::close(fd);
+    }
+  }
+};
 
 X509Ptr read_cert(const std::string& path) {
   FILE* f = fopen(path.c_str(), "rb");
@@ -876,6 +919,11 @@ Json TlsManager::generate_self_signed(const std::string& service, int days) {
     return p;
   }
   mkdirs(dir_);
+  DirLock lock(dir_);
+  if (certs_exist()) {  // another service generated them while we waited for the lock
+    p.set("generated", false);
+    return p;
+  }
   PkeyPtr ca_key = ec_key();
   X509Ptr ca = make_cert(ca_key.get(), "aiOS Root CA", nullptr, nullptr, 3650, true, "");
   PkeyPtr srv_key = ec_key();

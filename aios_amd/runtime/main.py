@@ -32,14 +32,20 @@ async def auto_load(svc: AIRuntimeService, model_dir: str, cfg=None):
     then every other *.gguf in the model directory (reference auto-load, runtime/src/main.rs:65-132),
     then AIOS_SYNTHETIC_MODELS specs."""
     loaded = set()
-    for tier, spec, ctx in (cfg.model_specs() if cfg is not None else []):
+    for t in (cfg.tier_plan() if cfg is not None else []):
+        spec, ctx = t["spec"], t["ctx"]
         base = spec.partition("#")[0]
-        name = tier if base.startswith("synthetic:") else Path(base).stem
-        log.info("loading %s tier %s from %s (ctx %s)", tier, name, spec, ctx or "auto")
-        m = await svc.mgr.load_model(name, spec, ctx)
+        name = t["name"] if base.startswith("synthetic:") else Path(base).stem
         loaded.add(base)
-        if m.status == "ready" and svc.http:
-            await svc.start_http(m)
+        if t["on_demand"]:
+            log.info("tier %s (%s) registered for on-demand load", t["name"], spec)
+            svc.mgr.register_on_demand(name, spec, ctx, t["devices"], t["idle_unload_s"])
+            continue
+        log.info("loading %s tier %s from %s (ctx %s, devices %s)", t["name"], name, spec, ctx or "auto",
+                 t["devices"] or "default")
+        for m in await svc.mgr.load_replicas(name, spec, ctx, t["devices"], t["idle_unload_s"]):
+            if m.status == "ready" and svc.http:
+                await svc.start_http(m)
     d = Path(model_dir)
     if d.is_dir():
         for f in sorted(d.glob("*.gguf")):
@@ -92,8 +98,9 @@ async def amain(args):
         log.warning("config: %s", w)
     max_batch = args.max_batch or cfg.models.max_batch
     max_slots = args.max_slots or cfg.models.max_slots
-    if cfg.models.devices and "AIOS_TP_DEVICES" not in os.environ:
-        os.environ["AIOS_TP_DEVICES"] = ",".join(str(d) for d in cfg.models.devices)
+    tp_env = cfg.tp_devices_env()
+    if tp_env and "AIOS_TP_DEVICES" not in os.environ:
+        os.environ["AIOS_TP_DEVICES"] = tp_env
     mgr = ModelManager(device=args.device, max_batch=max_batch, max_slots=max_slots)
     svc = AIRuntimeService(mgr, http=not args.no_http)
     server = RpcServer(args.addr, {"aios.runtime.AIRuntime": svc})

@@ -6,7 +6,13 @@ processes: each model is an in-process native Engine + tokenizer + chat template
   * loads run in a worker thread, so a 30-120 s load never blocks routing/inference (#14);
   * the `strategic` level first tries a local strategic model (the TP tier, e.g. llama3-70b)
     before reproducing the reference's FailedPrecondition "route via api-gateway" (§7.1);
-  * `ModelStatus.port` is a real per-model OpenAI-compatible HTTP endpoint (service.py).
+  * `ModelStatus.port` is a real per-model OpenAI-compatible HTTP endpoint (service.py);
+  * tier lifecycle (the reference's `load_on_demand` / `unload_after_idle_minutes`,
+    `initd/src/config.rs:108-109`, which its runtime never acted on): a registered on-demand
+    tier is loaded by the first request its level routes to (`resolve_async`), any model with an
+    idle limit is unloaded by the health pass once idle and re-registered for on-demand load;
+  * replicas: one tier may run as several engines on different GPUs of the node (request-level
+    data parallelism, SURVEY §2.9 DP row); routing picks the least-loaded ready replica.
 
 Model paths: a GGUF file, or `synthetic:<preset>[:<recipe>]` for a random-init model of a named
 architecture (tests/benchmarks without network access).
@@ -65,6 +71,9 @@ class ManagedModel:
     backend: str = "gpu"
     requested_ctx: int = 0
     restarts: list = dataclasses.field(default_factory=list)  # reload timestamps (restart window)
+    device: int = -1                  # GPU of this engine (-1: the manager's default device)
+    group: str = ""                   # replica group (tier name); "" = the model's own name
+    idle_unload_s: float = 0.0        # unload after this long without a request (0 = never)
 
     def status_string(self) -> str:
         return f"error: {self.error}" if self.status == "error" else self.status
@@ -87,6 +96,10 @@ class ModelManager:
         self.max_slots = max_slots
         self.base_port = base_port
         self.models: Dict[str, ManagedModel] = {}
+        # on-demand tiers not resident yet: name -> (path, ctx, devices, idle_unload_s)
+        self.deferred: Dict[str, tuple] = {}
+        self._ondemand_locks: Dict[str, asyncio.Lock] = {}
+        self.unload_hooks: list = []  # async callables(name) run after a model is unloaded
         self.abandoned: list = []  # schedulers of stalled engines (their threads may still be stuck)
         self._lock = threading.Lock()
         self.started = time.time()
@@ -113,7 +126,8 @@ class ModelManager:
             p += 1
         return p
 
-    async def load_model(self, name: str, path: str, context_length: int = 0, port: int = 0) -> ManagedModel:
+    async def load_model(self, name: str, path: str, context_length: int = 0, port: int = 0, device: int = -1,
+                         group: str = "", idle_unload_s: float = 0.0) -> ManagedModel:
         with self._lock:
             m = self.models.get(name)
             if m is not None and m.status in ("ready", "loading"):
@@ -121,10 +135,15 @@ class ModelManager:
             restarts = m.restarts if m is not None else []
             keep_port = m.port if m is not None and not port else port
             if m is not None:  # reload of an errored / unloading model: its port is free again
+                device = m.device if device < 0 else device
+                group = group or m.group
+                idle_unload_s = idle_unload_s or m.idle_unload_s
                 self.models.pop(name, None)
             m = ManagedModel(name=name, path=path, status="loading", port=self.allocate_port(keep_port),
-                             requested_ctx=context_length, restarts=restarts)
+                             requested_ctx=context_length, restarts=restarts, device=device, group=group,
+                             idle_unload_s=idle_unload_s)
             self.models[name] = m
+            self.deferred.pop(name, None)
         try:
             await asyncio.to_thread(self._load_blocking, m, context_length)
             m.status = "ready"
@@ -144,6 +163,8 @@ class ModelManager:
 
         E = native.require()
         from ..parallel.tp import launch_tp, parse_spec
+
+        device = self.device if m.device < 0 else m.device
 
         base, tp, act_q8 = parse_spec(m.path)
         faults = FaultSpec.from_env(m.name)
@@ -172,8 +193,8 @@ class ModelManager:
             cfg = get_preset(parts[1])
             recipe = parts[2] if len(parts) > 2 else "Q4_K_M"
             ctx = context_length or min(cfg.max_ctx, 4096)
-            eng = random_engine(cfg, recipe, seed=abs(hash(m.name)) % 1000, max_ctx=ctx, max_slots=self.max_slots,
-                                max_batch=self.max_batch, device=self.device, act_q8=act_q8)
+            eng = random_engine(cfg, recipe, seed=abs(hash(m.group or m.name)) % 1000, max_ctx=ctx,
+                                max_slots=self.max_slots, max_batch=self.max_batch, device=device, act_q8=act_q8)
             toks, scores, types = synthetic_vocab(cfg.vocab_size)
             tok = SpmTokenizer(toks, scores, types, cfg.bos_id, cfg.eos_id)
             tmpl = chat_template.for_model(cfg.chat_template if cfg.chat_template in chat_template.BUILTIN else "zephyr",
@@ -183,7 +204,7 @@ class ModelManager:
                 raise FileNotFoundError(base)
             ctx = context_length or context_for_size(os.path.getsize(base))
             eng, cfg, reader = load_engine(base, max_ctx=ctx, max_slots=self.max_slots, max_batch=self.max_batch,
-                                           device=self.device, name=m.name, act_q8=act_q8)
+                                           device=device, name=m.name, act_q8=act_q8)
             tok = from_gguf(reader)
             tmpl = chat_template.for_model(reader, tok)
         if not cpu:
@@ -200,6 +221,89 @@ class ModelManager:
         m.scheduler = Scheduler(eng, tok, min(batch, self.max_batch), min(slots, self.max_slots), m.context_length,
                                 m.grammar, name=m.name)
         m.weight_bytes, m.kv_bytes = eng.weight_bytes, eng.kv_bytes
+
+    # ------------------------------------------------------------------ tier lifecycle
+    def register_on_demand(self, name: str, path: str, context_length: int = 0, devices: Optional[List[int]] = None,
+                           idle_unload_s: float = 0.0):
+        """A tier that is not loaded at start: the first request its level (or name) routes to
+        loads it (resolve_async).  `devices` > 1 entry -> one replica per device."""
+        if name not in self.models:
+            self.deferred[name] = (path, context_length, list(devices or []), idle_unload_s)
+
+    async def load_replicas(self, name: str, path: str, context_length: int = 0,
+                            devices: Optional[List[int]] = None, idle_unload_s: float = 0.0) -> List[ManagedModel]:
+        """Load one engine per device (`name` on the first, `name@<dev>` on the others); routing
+        spreads requests over the group by load.  Replicas load concurrently (one thread each)."""
+        devs = list(devices or []) or [self.device]
+        names = [name if i == 0 else f"{name}@{d}" for i, d in enumerate(devs)]
+        res = await asyncio.gather(*[self.load_model(n, path, context_length, device=d,
+                                                     group=name if len(devs) > 1 else "",
+                                                     idle_unload_s=idle_unload_s)
+                                     for n, d in zip(names, devs)])
+        return list(res)
+
+    def _deferred_for(self, model: str, level: str) -> Optional[str]:
+        if not self.deferred:
+            return None
+        if model and model in self.deferred:
+            return model
+        for c in LEVEL_CANDIDATES.get(level, []):
+            cl = c.lower()
+            for name, (path, _, _, _) in self.deferred.items():
+                if cl in name.lower() or cl in os.path.basename(path.partition("#")[0]).lower():
+                    return name
+        return None
+
+    async def resolve_async(self, model: str, level: str) -> ManagedModel:
+        """resolve() plus on-demand loading: when nothing resident serves the request but a
+        registered on-demand tier does, load it (once, concurrent requests wait on the same load)
+        and route to it.  Falls back to resolve()'s reference error codes when the load fails."""
+        try:
+            return self.resolve(model, level)
+        except RoutingError as err:
+            name = self._deferred_for(model, level)
+            if name is None:
+                raise
+            lock = self._ondemand_locks.setdefault(name, asyncio.Lock())
+            async with lock:
+                if name in self.deferred:
+                    path, ctx, devs, idle = self.deferred[name]
+                    log.info("on-demand load of tier %s (%s) for level=%r model=%r", name, path, level, model)
+                    ms = await self.load_replicas(name, path, ctx, devs, idle)
+                    if not any(m.status == "ready" for m in ms):
+                        self.deferred[name] = (path, ctx, devs, idle)  # keep it registered for a retry
+                        raise RoutingError("UNAVAILABLE", f"on-demand load of {name} failed: {ms[0].error}") from err
+            return self.resolve(model or name, level)
+
+    def _busy(self, m: ManagedModel) -> bool:
+        if m.scheduler is None:
+            return False
+        mt = m.scheduler.metrics()
+        return mt.get("queued", 0) > 0 or mt.get("active", 0) > 0
+
+    async def unload_idle(self, now: Optional[float] = None) -> List[str]:
+        """Unload every ready model whose idle limit has passed (no request for idle_unload_s and
+        nothing queued or decoding); each goes back to the on-demand registry so the next request
+        reloads it.  A replica group unloads together."""
+        now = time.time() if now is None else now
+        out = []
+        for m in list(self.models.values()):
+            if m.status != "ready" or m.idle_unload_s <= 0:
+                continue
+            last = max(m.last_used, m.loaded_at)
+            if now - last < m.idle_unload_s or self._busy(m):
+                continue
+            group = m.group or m.name
+            members = [x for x in self.models.values() if (x.group or x.name) == group]
+            if any(self._busy(x) or now - max(x.last_used, x.loaded_at) < x.idle_unload_s for x in members):
+                continue
+            devs = sorted({x.device for x in members if x.device >= 0})
+            log.info("unloading idle tier %s (%d engine(s), idle %.0f s)", group, len(members), now - last)
+            for x in members:
+                await self.unload_model(x.name)
+                out.append(x.name)
+            self.deferred[group] = (m.path, m.requested_ctx, devs, m.idle_unload_s)
+        return out
 
     # ------------------------------------------------------------------ CPU backend
     @staticmethod
@@ -286,6 +390,7 @@ class ModelManager:
                 nm = await self.load_model(m.name, m.path, m.requested_ctx, m.port)
                 if nm.status == "ready":
                     recovered.append(m.name)
+        await self.unload_idle()
         return recovered
 
     def _abandon(self, m: ManagedModel, stalled: bool):
@@ -329,24 +434,46 @@ class ModelManager:
         m.engine = None
         m.scheduler = None
         self.models.pop(name, None)
+        for hook in self.unload_hooks:
+            try:
+                await hook(name)
+            except Exception:  # noqa: BLE001
+                log.exception("unload hook failed for %s", name)
         return True
 
     def list_models(self) -> List[ManagedModel]:
         return list(self.models.values())
 
     # ------------------------------------------------------------------ routing
+    def _load_of(self, m: ManagedModel) -> float:
+        if m.scheduler is None:
+            return 0.0
+        mt = m.scheduler.metrics()
+        return float(mt.get("queued", 0) + mt.get("active", 0))
+
+    def _pick_replica(self, name: str) -> str:
+        """Least-loaded ready member of `name`'s replica group (ties: fewest requests served)."""
+        m = self.models[name]
+        if not m.group:
+            return name
+        members = [x for x in self.models.values() if x.group == m.group and x.status == "ready"]
+        if not members:
+            return name
+        best = min(members, key=lambda x: (self._load_of(x), x.request_count))
+        return best.name
+
     def _first_ready_from(self, candidates) -> Optional[str]:
         for c in candidates:
             cl = c.lower()
             for name, m in self.models.items():
                 if m.status == "ready" and cl in name.lower():
-                    return name
+                    return self._pick_replica(name)
         return None
 
     def first_ready(self) -> Optional[str]:
         for name, m in self.models.items():
             if m.status == "ready":
-                return name
+                return self._pick_replica(name)
         return None
 
     def select_model_for_level(self, level: str) -> Optional[str]:
@@ -361,7 +488,7 @@ class ModelManager:
         if model:
             m = self.models.get(model)
             if m is not None and m.status == "ready":
-                return self._touch(m)
+                return self._touch(self.models[self._pick_replica(model)])
         if level:
             name = self.select_model_for_level(level)
             if name is not None:

@@ -67,6 +67,20 @@ class AIRuntimeService:
         self.mgr = manager
         self.http = http
         self._http_runners: Dict[str, object] = {}
+        manager.unload_hooks.append(self._drop_http)
+
+    async def _drop_http(self, name: str):
+        runner = self._http_runners.pop(name, None)
+        if runner is not None:
+            await runner.cleanup()
+
+    async def _route(self, request):
+        """Resolve (loading an on-demand tier when needed) and expose a freshly loaded model's
+        OpenAI-compatible endpoint."""
+        m = await self.mgr.resolve_async(request.model, request.intelligence_level)
+        if self.http and m.name not in self._http_runners:
+            await self.start_http(m)
+        return m
 
     async def _abort(self, context, e: RoutingError):
         await context.abort(getattr(grpc.StatusCode, e.code), str(e))
@@ -86,9 +100,6 @@ class AIRuntimeService:
         return self._status(m)
 
     async def UnloadModel(self, request, context):
-        runner = self._http_runners.pop(request.model_name, None)
-        if runner is not None:
-            await runner.cleanup()
         ok = await self.mgr.unload_model(request.model_name)
         return pb.common.Status(success=ok, message="unloaded" if ok else f"model {request.model_name} not found")
 
@@ -97,7 +108,7 @@ class AIRuntimeService:
 
     async def Infer(self, request, context):
         try:
-            m = self.mgr.resolve(request.model, request.intelligence_level)
+            m = await self._route(request)
         except RoutingError as e:
             await self._abort(context, e)
         temperature, max_tokens = _gen_params(request.temperature, request.max_tokens)
@@ -111,7 +122,7 @@ class AIRuntimeService:
 
     async def StreamInfer(self, request, context):
         try:
-            m = self.mgr.resolve(request.model, request.intelligence_level)
+            m = await self._route(request)
         except RoutingError as e:
             await self._abort(context, e)
             return

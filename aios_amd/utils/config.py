@@ -43,12 +43,16 @@ class ModelTier:
     tensor_parallel: int = 1
     unload_after_idle_minutes: int = 0
     device: str = ""            # "" = GPU when present, "cpu" = the CPU engine
+    replicas: int = 1           # engines of this tier, one per GPU (request-level data parallelism)
+    devices: List[int] = dataclasses.field(default_factory=list)  # GPUs of the replicas ([] = first `replicas` of models.devices)
 
 
 @dataclasses.dataclass
 class ModelsConfig:
     model_dir: str = "/var/lib/aios/models"
-    devices: List[int] = dataclasses.field(default_factory=lambda: [0])
+    # GPUs the runtime may use; [] = every GPU the node has (TP tiers then take the first
+    # tensor_parallel of them).  Exported to the TP launcher only when it lists enough devices.
+    devices: List[int] = dataclasses.field(default_factory=list)
     max_batch: int = 16
     max_slots: int = 16
     tiers: Dict[str, ModelTier] = dataclasses.field(default_factory=dict)
@@ -108,6 +112,41 @@ class NodeConfig:
     source: str = ""            # the file read ("" = defaults only)
     warnings: List[str] = dataclasses.field(default_factory=list)
 
+    def tier_plan(self) -> List[dict]:
+        """Every configured tier with a usable file: name, runtime path spec ('#tp=N' / '#cpu'),
+        context length, whether to load it at start or on first request, replica devices and the
+        idle-unload limit in seconds (reference `initd/src/config.rs:108-109`)."""
+        out = []
+        for name, t in self.models.tiers.items():
+            if not t.file:
+                continue
+            path = t.file if (t.file.startswith("synthetic:") or os.path.isabs(t.file)) else os.path.join(
+                self.models.model_dir, t.file)
+            if not path.startswith("synthetic:") and not os.path.exists(path):
+                continue
+            frag = []
+            if t.tensor_parallel > 1:
+                frag.append(f"tp={t.tensor_parallel}")
+            if t.device == "cpu":
+                frag.append("cpu")
+            devs = list(t.devices)
+            if not devs and t.replicas > 1:
+                devs = list(self.models.devices[:t.replicas]) or list(range(t.replicas))
+            out.append(dict(name=name, spec=path + ("#" + "&".join(frag) if frag else ""),
+                            ctx=t.context_length, on_demand=bool(t.load_on_demand and not t.always_loaded),
+                            devices=devs if t.tensor_parallel <= 1 else [],
+                            idle_unload_s=60.0 * max(0, t.unload_after_idle_minutes)))
+        return out
+
+    def tp_devices_env(self) -> str:
+        """AIOS_TP_DEVICES for the runtime, or "" to let it detect every GPU: only an explicit
+        models.devices list long enough for the widest TP tier is exported (a short default list
+        would pin every rank of an 8-way tier to one GPU)."""
+        need = max([t.tensor_parallel for t in self.models.tiers.values()] + [1])
+        if self.models.devices and len(self.models.devices) >= need:
+            return ",".join(str(d) for d in self.models.devices)
+        return ""
+
     def model_specs(self) -> List[tuple]:
         """(name, runtime path spec, context_length) of the tiers to load at start: always_loaded
         tiers whose GGUF exists (absolute or under model_dir), with '#tp=N' / '#cpu' suffixes."""
@@ -134,6 +173,13 @@ def _coerce(cls, raw: Dict[str, Any], warnings: List[str], where: str):
     for k, v in raw.items():
         f = fields.get(k)
         if f is None or k == "tiers":
+            continue
+        if k == "devices":
+            if isinstance(v, list):
+                try:
+                    kw[k] = [int(x) for x in v]
+                except (TypeError, ValueError):
+                    warnings.append(f"{where}.{k}: cannot use {v!r}; default kept")
             continue
         want = f.type if isinstance(f.type, type) else None
         try:

@@ -42,3 +42,37 @@ def test_mtls_tool_registry(tmp_path):
             svc.close()
 
     asyncio.run(run())
+
+
+def _gen(d, q):
+    from aios_amd.core import load as load_core
+
+    mgr = load_core().TlsManager(d)
+    q.put(bool(mgr.generate_self_signed("aios")["generated"]))
+
+
+def test_concurrent_service_starts_share_one_ca(tmp_path):
+    """services started together each ran generate_self_signed; without a lock they
+    could create different CAs and overwrite each other's files.  Now exactly one process
+    generates, the others find a complete, consistent set, and the keys are 0600."""
+    import multiprocessing as mp
+    import os
+    import stat
+
+    from aios_amd.core import load as load_core
+
+    d = str(tmp_path / "certs")
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_gen, args=(d, q)) for _ in range(6)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(60)
+    gens = [q.get(timeout=5) for _ in procs]
+    assert sum(gens) == 1, gens
+    v = load_core().TlsManager(d).verify()
+    assert v["ok"], v
+    for k in ("ca.key", "server.key"):
+        assert stat.S_IMODE(os.stat(os.path.join(d, k)).st_mode) == 0o600
+    assert not [f for f in os.listdir(d) if ".tmp." in f]
