@@ -152,6 +152,7 @@ PYBIND11_MODULE(_engine, m) {
       .def_readwrite("act_q8", &EngineConfig::act_q8)
       .def_readwrite("tp_rank", &EngineConfig::tp_rank)
       .def_readwrite("tp_size", &EngineConfig::tp_size)
+      .def_readwrite("vocab_parallel", &EngineConfig::vocab_parallel)
       .def_readwrite("device", &EngineConfig::device);
 
   py::class_<Engine>(m, "Engine")
@@ -229,7 +230,9 @@ PYBIND11_MODULE(_engine, m) {
       .def("set_comm", [](Engine& e, XgmiComm& c) {
         // the comm must outlive the engine's use of it (the Python wrapper keeps a reference)
         e.set_allreduce(&XgmiComm::hook, &c);
-      });
+        e.set_allgather(&XgmiComm::gather_hook, &c);
+      })
+      .def_property_readonly("vocab_parallel", &Engine::vocab_parallel);
 
   // ------------------------------------------------------------------ TP collectives (xGMI)
   py::class_<XgmiComm>(m, "XgmiComm")
@@ -244,6 +247,11 @@ PYBIND11_MODULE(_engine, m) {
       .def("allreduce", [](XgmiComm& c, uintptr_t data, size_t n, uintptr_t residual, uintptr_t st) {
         c.allreduce((float*)data, n, (float*)residual, S(st));
       }, py::arg("data"), py::arg("n"), py::arg("residual") = 0, py::arg("stream") = 0)
+      .def("allgather_cols", [](XgmiComm& c, uintptr_t data, int rows, int slice, int ld, uintptr_t st) {
+        c.allgather_cols((float*)data, rows, slice, ld, S(st));
+      }, py::arg("data"), py::arg("rows"), py::arg("slice"), py::arg("ld"), py::arg("stream") = 0)
+      .def_property("two_shot_min", &XgmiComm::two_shot_min, &XgmiComm::set_two_shot_min)
+      .def_property("bf16_payload", &XgmiComm::bf16_payload, &XgmiComm::set_bf16_payload)
       .def("error", &XgmiComm::error)
       .def("reset_error", &XgmiComm::reset_error)
       .def_property_readonly("rank", &XgmiComm::rank)

@@ -1,22 +1,34 @@
-// Tensor-parallel collectives for one MI355X node: a one-shot all-reduce over IPC-mapped peer
-// buffers (each GPU reads its <=7 peers directly over the point-to-point xGMI links), used for the
-// row-parallel o_proj / down_proj partial sums of the TP "strategic" tier.
+// Tensor-parallel collectives for one MI355X node over IPC-mapped peer buffers: every GPU reads
+// its <= 7 peers directly over the point-to-point xGMI links.
 //
-// Why not a ring: a decode all-reduce is 16-64 KB; a ring pays 2(N-1) latency hops and is
-// bound by one link, while the one-shot pull reads all peers in parallel across the 7 links and
-// finishes in ~one xGMI round trip.  Prefill chunks (<= 64 rows x d) fit the same buffers.
+//  * one-shot all-reduce (decode-size messages, 16-256 KB): stage my partial, flag, pull every
+//    peer's partial and sum -- ~one xGMI round trip, all 7 links in parallel; fp32 payload;
+//  * two-shot all-reduce = reduce-scatter + all-gather (prefill-size messages, MBs): each rank
+//    reduces only its 1/world sub-shard of every workgroup chunk (pulling 7 peers' staged
+//    partials, optionally bf16 to halve the link bytes), publishes it, and all ranks gather the
+//    reduced sub-shards: 2(W-1)/W of the message crosses each GPU's links instead of (W-1)x,
+//    a mesh (all links at once), not a per-link-bound ring;
+//  * all-gather of per-rank column slices of a [rows][ld] fp32 matrix (the vocab-parallel
+//    lm_head: each rank computes V/world logits, every rank needs all of them for the identical
+//    on-device sampler and the JSON-grammar mask).
+// All three are fused with their consumer where it is an elementwise op (residual add).
 //
-// Protocol (per workgroup g, epoch e = this WG's launch counter, identical on every rank because
-// every rank issues the same sequence of collectives):
-//   1. copy my chunk of the input into my IPC buffer half  e & 1
-//   2. release fence (system scope), then store e into flag[g][my_rank] of every peer
-//   3. wait until my own flag[g][p] >= e for every peer p (bounded spin -> error flag, never hangs)
-//   4. out = sum over ranks of buf_p[e & 1][chunk]   (+ residual when fused)
-// Double buffering is safe: a rank can only reuse half e&1 at epoch e+2, which needs every peer's
-// epoch-(e+1) flag, which a peer sets only after it finished reading epoch e.
+// Why not a ring: a ring pays 2(W-1) latency hops and is bound by one link.
+//
+// Protocol (per workgroup g; epoch e = this WG's call counter, identical on every rank because
+// every rank issues the same sequence of collectives with the same sizes):
+//   1. copy my part of chunk g into my stage buffer half e & 1
+//   2. release fence (system scope), store e into flag[phase][g][my_rank] of every peer
+//   3. wait until my own flag[phase][g][p] >= e for every peer (bounded spin -> error flag)
+//   4. consume the peers' half e & 1 (two-shot: reduce, publish result, flag phase 2, wait, gather)
+// Buffer position j is always owned by workgroup j / AR_CHUNK in every kernel (each call moves
+// at most AR_MAX_WG * AR_CHUNK elements; larger messages are split into several calls), so the
+// per-workgroup epochs stay consistent across calls of different sizes and kinds.  Double
+// buffering is safe: a rank reuses half e&1 at epoch e+2, which needs every peer's epoch-(e+1)
+// phase-1 flag, which a peer sets only after it finished all its reads of epoch e.
 // Flags / buffers are uncached device memory (hipDeviceMallocUncached), so remote stores and
-// loads bypass the caches of both GPUs; works both across GPUs (xGMI) and between processes that
-// share one GPU (how the TP path is tested on a single-GPU box).
+// loads bypass the caches of both GPUs; works across GPUs (xGMI) and between processes that share
+// one GPU (how the TP path is tested on a single-GPU box).
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -28,35 +40,48 @@ namespace aios {
 
 constexpr int AR_MAX_RANKS = 8;
 constexpr int AR_MAX_WG = 512;
+constexpr int AR_THREADS = 256;
+constexpr int AR_CHUNK = AR_THREADS * 4;              // elements per workgroup per call
+constexpr size_t AR_MAX_CALL = (size_t)AR_MAX_WG * AR_CHUNK;  // elements per kernel call
 
 struct ArDevCtx {
-  float* buf[AR_MAX_RANKS];         // rank r's data buffer (mapped into this process): [2][cap]
-  uint32_t* flags[AR_MAX_RANKS];    // rank r's flag array: [AR_MAX_WG][AR_MAX_RANKS]
+  float* buf[AR_MAX_RANKS];         // rank r's shared region: stage f32 [2][cap] | result f32 [2][cap] | stage bf16 [2][cap]
+  uint32_t* flags[AR_MAX_RANKS];    // rank r's flags: [2 phases][AR_MAX_WG][AR_MAX_RANKS]
   uint32_t* epoch;                  // my per-WG epoch counters [AR_MAX_WG] (local)
   uint32_t* error;                  // set to 1 when a wait timed out
   int rank, world;
-  size_t cap;                       // floats per half-buffer
+  size_t cap;                       // elements per half-buffer (<= AR_MAX_CALL)
 };
 
 class XgmiComm {
  public:
   XgmiComm(int rank, int world, int device, size_t cap_floats);
   ~XgmiComm();
-  // opaque IPC handles of my data + flag buffers (hipIpcMemHandle_t x 2)
+  // opaque IPC handles of my shared region + flag buffer (hipIpcMemHandle_t x 2)
   std::string ipc_handle() const;
   // map every peer's buffers (handles indexed by rank; my own entry is ignored)
   void connect(const std::vector<std::string>& handles);
   bool connected() const { return connected_; }
   // sum `n` floats of `data` over all ranks; result into `data`, or added into `residual`
   // (data left as my partial) when residual != nullptr.  Stream-ordered, graph-capturable.
+  // Messages above two_shot_min() floats use reduce-scatter + all-gather; messages above the
+  // capacity are split into several calls.
   void allreduce(float* data, size_t n, float* residual, hipStream_t st);
+  // every rank owns columns [r*slice, (r+1)*slice) of the rows x ld fp32 matrix `data`;
+  // afterwards every rank holds all columns
+  void allgather_cols(float* data, int rows, int slice, int ld, hipStream_t st);
   bool error() const;
   void reset_error();
   int rank() const { return h_.rank; }
   int world() const { return h_.world; }
   size_t capacity() const { return h_.cap; }
-  // Engine hook (AllReduceFn-compatible trampoline)
+  size_t two_shot_min() const { return two_shot_min_; }
+  void set_two_shot_min(size_t n) { two_shot_min_ = n; }
+  bool bf16_payload() const { return bf16_; }
+  void set_bf16_payload(bool on) { bf16_ = on; }
+  // Engine hooks (AllReduceFn / AllGatherFn-compatible trampolines)
   static void hook(void* self, float* data, size_t n, float* residual, hipStream_t st);
+  static void gather_hook(void* self, float* data, int rows, int slice, int ld, hipStream_t st);
 
  private:
   ArDevCtx h_{};
@@ -66,6 +91,8 @@ class XgmiComm {
   std::vector<void*> opened_;
   int device_ = 0;
   bool connected_ = false;
+  size_t two_shot_min_ = 64 * 1024;  // floats (256 KB)
+  bool bf16_ = true;                 // bf16 staging for the two-shot (prefill) path
 };
 
 void launch_allreduce(const ArDevCtx* ctx, int world, float* data, size_t n, float* residual, hipStream_t st);

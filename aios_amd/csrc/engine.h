@@ -41,6 +41,9 @@ struct EngineConfig {
   // tensor parallel (the engine holds this rank's shard; collectives via the comm hook)
   int tp_rank = 0;
   int tp_size = 1;
+  // vocab-parallel lm_head under TP: output.weight holds rows [rank*V/tp, (rank+1)*V/tp) and the
+  // logits are completed by the all-gather hook (ignored for tp_size 1 / tied embeddings)
+  int vocab_parallel = 0;
   int device = 0;
 };
 
@@ -64,6 +67,9 @@ struct LayerW {
 // all-reduce hook (TP): sum `n` floats of `data` over the TP ranks on `stream` and add the
 // total into `residual` (or into `data` when residual is null); installed by aios_amd/parallel.
 using AllReduceFn = void (*)(void* ctx, float* data, size_t n, float* residual, hipStream_t stream);
+// all-gather hook (vocab-parallel lm_head): rank r owns columns [r*slice, (r+1)*slice) of the
+// rows x ld fp32 matrix `data`; afterwards every rank holds all of them
+using AllGatherFn = void (*)(void* ctx, float* data, int rows, int slice, int ld, hipStream_t stream);
 
 class Engine {
  public:
@@ -110,6 +116,8 @@ class Engine {
   void synchronize();
   uintptr_t stream_handle() const { return (uintptr_t)stream_; }
   void set_allreduce(AllReduceFn fn, void* ctx) { allreduce_ = fn; allreduce_ctx_ = ctx; }
+  void set_allgather(AllGatherFn fn, void* ctx) { allgather_ = fn; allgather_ctx_ = ctx; }
+  bool vocab_parallel() const { return cfg_.vocab_parallel != 0; }
   void reset_graphs();
   void copy_slot(int src, int dst, int n_tokens);  // prefix-cache: duplicate KV rows [0, n)
 
@@ -130,6 +138,7 @@ class Engine {
   QMat interleave_rows(const QMat& a, const QMat& b);
   void* dmalloc(size_t bytes);
   void allreduce(float* p, size_t n, float* residual);
+  void lm_head(int B, const float* x, int ldx);  // logits_[B][V] (vocab-parallel aware)
 
   EngineConfig cfg_;
   hipStream_t stream_ = nullptr;
@@ -185,6 +194,8 @@ class Engine {
   std::map<int, hipGraphExec_t> graphs_;
   AllReduceFn allreduce_ = nullptr;
   void* allreduce_ctx_ = nullptr;
+  AllGatherFn allgather_ = nullptr;
+  void* allgather_ctx_ = nullptr;
   // sampling config for the enqueued step
   bool sample_temp_ = false;
   bool sample_mask_ = false;

@@ -65,6 +65,9 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
   // B <= 8 decodes through the fused GEMVs; larger batches (up to 64) through the MFMA GEMM path
   if (cfg_.max_batch < 1 || cfg_.max_batch > 64) throw std::runtime_error("max_batch must be 1..64");
   if (cfg_.max_slots < cfg_.max_batch) cfg_.max_slots = cfg_.max_batch;
+  if (cfg_.tp_size <= 1 || cfg_.tie_embeddings) cfg_.vocab_parallel = 0;
+  if (cfg_.vocab_parallel && cfg_.vocab_size % cfg_.tp_size)
+    throw std::runtime_error("vocab_parallel: vocab_size not divisible by tp_size");
 }
 
 Engine::~Engine() {
@@ -206,6 +209,9 @@ void Engine::set_tensor(const std::string& name, int qt, int rows, int cols, con
     return;
   }
   if (name == "output.weight") {
+    if (cfg_.vocab_parallel && rows != cfg_.vocab_size / cfg_.tp_size)
+      throw std::runtime_error("vocab-parallel output.weight: expected " +
+                               std::to_string(cfg_.vocab_size / cfg_.tp_size) + " rows (this rank's shard)");
     output_ = upload_qmat(qt, rows, cols, host, nbytes);
     return;
   }
@@ -303,7 +309,7 @@ void Engine::init_random(const std::string& recipe_in, uint64_t seed) {
   };
   const float amp = 0.02f;
   tok_embd_ = mk(type_for("token_embd", 0), V, d, 1.0f);
-  if (!cfg_.tie_embeddings) output_ = mk(type_for("output", 0), V, d, amp);
+  if (!cfg_.tie_embeddings) output_ = mk(type_for("output", 0), cfg_.vocab_parallel ? V / cfg_.tp_size : V, d, amp);
   out_norm_ = vec(d, 1.f, 0.1f);
   for (int l = 0; l < NL; ++l) {
     LayerW& L = layers_[l];
@@ -362,11 +368,12 @@ void Engine::finalize() {
   if (!miss.empty()) throw std::runtime_error("missing tensors, first: " + miss[0]);
   if (!output_.valid()) {
     if (!cfg_.tie_embeddings) cfg_.tie_embeddings = 1;
+    cfg_.vocab_parallel = 0;  // the tied table is the full vocabulary
     output_ = tok_embd_;  // tied embeddings (GGUF files without output.weight)
   }
   const int d = cfg_.d_model, hd = cfg_.head_dim, H = cfg_.n_heads, Hkv = cfg_.n_kv_heads;
   const int qd = H * hd, kvd = Hkv * hd, V = cfg_.vocab_size, Bm = cfg_.max_batch;
-  if (cfg_.max_ctx % 64) cfg_.max_ctx = (int)align_up(cfg_.max_ctx, 64);
+  if (cfg_.max_ctx % 128) cfg_.max_ctx = (int)align_up(cfg_.max_ctx, 128);  // decode attention passes
   layer_kv_elems_ = (size_t)cfg_.max_slots * Hkv * cfg_.max_ctx * hd;
   kv_bytes_ = 2 * layer_kv_elems_ * cfg_.n_layers * sizeof(bf16_t);
   k_cache_ = (bf16_t*)dmalloc(kv_bytes_ / 2);
@@ -375,7 +382,7 @@ void Engine::finalize() {
   HIP_CHECK(hipMemset(v_cache_, 0, kv_bytes_ / 2));
   n_chunks_ = (cfg_.max_ctx + ATTN_CHUNK - 1) / ATTN_CHUNK;
   {
-    const size_t nc = (size_t)std::max(prefill_rows_, Bm) * Hkv;
+    const size_t nc = (size_t)std::max(prefill_rows_, Bm) * H;  // decode attention tickets [row][head]
     attn_cnt_ = (int*)dmalloc(nc * 4);
     HIP_CHECK(hipMemset(attn_cnt_, 0, nc * 4));
   }
@@ -701,21 +708,37 @@ void Engine::layer_decode(int l, int B) {
   }
 }
 
+// logits_[B][V] = rmsnorm(x) . output^T.  Vocab-parallel TP: this rank holds V/tp rows of
+// output.weight, writes its column slice of every logits row, and the xGMI all-gather completes the
+// rows on every rank, so the sampler and the grammar mask run identically everywhere -- 1/tp of
+// the largest single matrix per GPU instead of a replica (Llama-3 70B: 128256 x 8192 Q6_K).
+void Engine::lm_head(int B, const float* x, int ldx) {
+  const int d = cfg_.d_model, V = cfg_.vocab_size;
+  const bool vp = cfg_.vocab_parallel != 0;
+  const int Vl = vp ? V / cfg_.tp_size : V;
+  float* y = logits_ + (vp ? (size_t)cfg_.tp_rank * Vl : 0);
+  if (dec_a16_ && ((dec_gemm_min_b_ > 0 && B >= dec_gemm_min_b_) || B > 8) && Vl % 64 == 0 &&
+      gemm_supports(output_.w.qtype)) {
+    launch_rmsnorm_bf16(x, ldx, out_norm_, dec_a16_, d, B, d, cfg_.norm_eps, stream_);
+    GemmQArgs g;
+    std::memset(&g, 0, sizeof(g));
+    g.A = dec_a16_; g.lda = d; g.M = B; g.K = d; g.nseg = 1; g.seg[0] = output_.w; g.N = Vl;
+    g.C = y; g.ldc = V; g.epi = GEPI_STORE;
+    gemm(g);
+  } else {
+    gemv({&output_}, Vl, d, B, x, ldx, out_norm_, y, V, EPI_STORE, 0);
+  }
+  if (vp) {
+    if (!allgather_) throw std::runtime_error("vocab-parallel engine without an all-gather hook");
+    allgather_(allgather_ctx_, logits_, B, Vl, V, stream_);
+  }
+}
+
 void Engine::enqueue_decode_step(int B) {
   const int d = cfg_.d_model, V = cfg_.vocab_size;
   launch_get_rows(tok_embd_.w, d_tokens_, B, x_, d, 1.f, stream_);
   for (int l = 0; l < cfg_.n_layers; ++l) layer_decode(l, B);
-  if (dec_a16_ && ((dec_gemm_min_b_ > 0 && B >= dec_gemm_min_b_) || B > 8) && V % 64 == 0 &&
-      gemm_supports(output_.w.qtype)) {
-    launch_rmsnorm_bf16(x_, d, out_norm_, dec_a16_, d, B, d, cfg_.norm_eps, stream_);
-    GemmQArgs g;
-    std::memset(&g, 0, sizeof(g));
-    g.A = dec_a16_; g.lda = d; g.M = B; g.K = d; g.nseg = 1; g.seg[0] = output_.w; g.N = V;
-    g.C = logits_; g.ldc = V; g.epi = GEPI_STORE;
-    gemm(g);
-  } else {
-    gemv({&output_}, V, d, B, x_, d, out_norm_, logits_, V, EPI_STORE, 0);
-  }
+  lm_head(B, x_, d);
   SampleArgs s;
   std::memset(&s, 0, sizeof(s));
   s.logits = logits_; s.ldl = V; s.B = B; s.V = V;
@@ -797,8 +820,7 @@ void Engine::prefill_gemm(int slot, const std::vector<int>& tokens, int start_po
       gemm(g);
       if (tp) allreduce(gm_part_, (size_t)n * d, gm_x_);
     }
-    if (r0 + n == T && want_logits)
-      gemv({&output_}, V, d, 1, gm_x_ + (size_t)(n - 1) * d, d, out_norm_, logits_, V, EPI_STORE, 0);
+    if (r0 + n == T && want_logits) lm_head(1, gm_x_ + (size_t)(n - 1) * d, d);
   }
 }
 
@@ -941,9 +963,7 @@ std::vector<float> Engine::prefill(int slot, const std::vector<int>& tokens, int
         }
       }
       x_ = xb; q_ = qb; qkv_ = qkvb; attn_ = ab; ff_ = fb;
-      if (r0 + n == T && want_logits) {
-        gemv({&output_}, V, d, 1, x_ + (size_t)(n - 1) * d, d, out_norm_, logits_, V, EPI_STORE, 0);
-      }
+      if (r0 + n == T && want_logits) lm_head(1, x_ + (size_t)(n - 1) * d, d);
     }
   } catch (...) {
     std::swap(x_, pf_x_); std::swap(q_, pf_q_); std::swap(qkv_, pf_qkv_); std::swap(attn_, pf_attn_);

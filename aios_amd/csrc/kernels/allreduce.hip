@@ -1,4 +1,7 @@
-// One-shot xGMI all-reduce for tensor parallelism (protocol in comm.h).
+// xGMI collectives for tensor parallelism: one-shot and two-shot (reduce-scatter + all-gather)
+// all-reduce, column all-gather.  Protocol and buffer ownership in comm.h.
+#include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <stdexcept>
 
@@ -10,8 +13,6 @@ namespace aios {
 
 namespace {
 
-constexpr int AR_THREADS = 256;
-constexpr int AR_CHUNK = AR_THREADS * 4;                    // floats per WG iteration
 constexpr uint64_t AR_TIMEOUT_TICKS = 100ull * 1000 * 1000 * 3;  // 3 s of the 100 MHz wall clock
 
 __device__ __forceinline__ float4 ld_peer(const float* p) {
@@ -23,37 +24,35 @@ __device__ __forceinline__ float4 ld_peer(const float* p) {
   return v;
 }
 
-__global__ __launch_bounds__(AR_THREADS) void allreduce_oneshot(const ArDevCtx* __restrict__ c, float* __restrict__ data,
-                                                                 size_t n, float* __restrict__ residual) {
-  const int g = blockIdx.x, G = gridDim.x, t = threadIdx.x;
-  const int rank = c->rank, world = c->world;
-  __shared__ uint32_t s_e;
-  if (t == 0) {
+__device__ __forceinline__ uint32_t flag_idx(int phase, int g, int r) {
+  return ((uint32_t)phase * AR_MAX_WG + g) * AR_MAX_RANKS + r;
+}
+
+// this WG's epoch (one increment per call), broadcast through LDS
+__device__ __forceinline__ uint32_t next_epoch(const ArDevCtx* c, int g, uint32_t* s_e) {
+  if (threadIdx.x == 0) {
     const uint32_t e = c->epoch[g] + 1;  // only this WG touches epoch[g]
     c->epoch[g] = e;
-    s_e = e;
+    *s_e = e;
   }
   __syncthreads();
-  const uint32_t e = s_e;
-  const size_t half = (size_t)(e & 1u) * c->cap;
-  float* mine = c->buf[rank] + half;
-  const size_t stride = (size_t)G * AR_CHUNK;
-  // 1. stage my partial into my IPC buffer
-  for (size_t i = ((size_t)g * AR_THREADS + t) * 4; i < n; i += stride) {
-    if (i + 4 <= n) {
-      *(float4*)(mine + i) = *(const float4*)(data + i);
-    } else {
-      for (size_t k = i; k < n; ++k) mine[k] = data[k];
-    }
-  }
-  // 2. publish: every thread's stores are ordered before the flags
+  return *s_e;
+}
+
+// every thread's stores are ordered before the flags; one lane per peer raises its flag
+__device__ __forceinline__ void publish(const ArDevCtx* c, int phase, int g, uint32_t e) {
   __threadfence_system();
   __syncthreads();
-  if (t < world && t != rank)
-    __hip_atomic_store(c->flags[t] + g * AR_MAX_RANKS + rank, e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-  // 3. wait for every peer's epoch-e flag (bounded: an exit every wave reaches)
-  if (t < world && t != rank) {
-    uint32_t* f = c->flags[rank] + g * AR_MAX_RANKS + t;
+  const int t = threadIdx.x;
+  if (t < c->world && t != c->rank)
+    __hip_atomic_store(c->flags[t] + flag_idx(phase, g, c->rank), e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// wait for every peer's epoch-e flag of `phase` (bounded: an exit every wave reaches)
+__device__ __forceinline__ void wait_peers(const ArDevCtx* c, int phase, int g, uint32_t e) {
+  const int t = threadIdx.x;
+  if (t < c->world && t != c->rank) {
+    uint32_t* f = c->flags[c->rank] + flag_idx(phase, g, t);
     const uint64_t t0 = wall_clock64();
     while ((int)(__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - e) < 0) {
       __builtin_amdgcn_s_sleep(2);
@@ -65,31 +64,150 @@ __global__ __launch_bounds__(AR_THREADS) void allreduce_oneshot(const ArDevCtx* 
   }
   __syncthreads();
   __threadfence_system();
-  // 4. reduce: my partial (local) + every peer's staged partial (remote, over xGMI)
-  for (size_t i = ((size_t)g * AR_THREADS + t) * 4; i < n; i += stride) {
-    if (i + 4 <= n) {
-      float4 acc = *(const float4*)(data + i);
+}
+
+__device__ __forceinline__ void put(float* data, float* residual, size_t i, float4 v) {
+  if (residual) {
+    float4 r = *(float4*)(residual + i);
+    r.x += v.x; r.y += v.y; r.z += v.z; r.w += v.w;
+    *(float4*)(residual + i) = r;
+  } else {
+    *(float4*)(data + i) = v;
+  }
+}
+
+// ---- one-shot: every rank pulls every peer's whole partial (decode-size messages).  The sum runs
+// in rank order on every rank (own partial at its rank's position), so all ranks produce the
+// bit-identical result and their on-device samplers stay in lock step.
+__global__ __launch_bounds__(AR_THREADS) void allreduce_oneshot(const ArDevCtx* __restrict__ c, float* __restrict__ data,
+                                                                 size_t n, float* __restrict__ residual) {
+  __shared__ uint32_t s_e;
+  const int g = blockIdx.x, t = threadIdx.x;
+  const int rank = c->rank, world = c->world;
+  const uint32_t e = next_epoch(c, g, &s_e);
+  const size_t half = (size_t)(e & 1u) * c->cap;
+  float* mine = c->buf[rank] + half;
+  const size_t i = (size_t)g * AR_CHUNK + 4 * t;
+  const bool full = i + 4 <= n;
+  if (full) *(float4*)(mine + i) = *(const float4*)(data + i);
+  else for (size_t k = i; k < n; ++k) mine[k] = data[k];
+  publish(c, 0, g, e);
+  wait_peers(c, 0, g, e);
+  if (full) {
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-      for (int p = 0; p < AR_MAX_RANKS; ++p) {
-        if (p < world && p != rank) {
-          const float4 v = ld_peer(c->buf[p] + half + i);
-          acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
-        }
+    for (int p = 0; p < AR_MAX_RANKS; ++p) {
+      if (p < world) {
+        const float4 v = p == rank ? *(const float4*)(data + i) : ld_peer(c->buf[p] + half + i);
+        acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
       }
-      if (residual) {
-        float4 r = *(float4*)(residual + i);
-        r.x += acc.x; r.y += acc.y; r.z += acc.z; r.w += acc.w;
-        *(float4*)(residual + i) = r;
+    }
+    put(data, residual, i, acc);
+  } else {
+    for (size_t k = i; k < n; ++k) {
+      float acc = 0.f;
+      for (int p = 0; p < world; ++p) acc += p == rank ? data[k] : __builtin_nontemporal_load(c->buf[p] + half + k);
+      if (residual) residual[k] += acc; else data[k] = acc;
+    }
+  }
+}
+
+// ---- two-shot: reduce-scatter (each rank sums its 1/world sub-shard of the chunk, pulling the
+// peers' staged partials -- bf16 when BF16, halving the link bytes) then all-gather of the reduced
+// sub-shards.  Each element is reduced once, by its owner, so every rank gets identical bits.
+// The host launches it only for n % 4 == 0.
+template <bool BF16>
+__global__ __launch_bounds__(AR_THREADS) void allreduce_twoshot(const ArDevCtx* __restrict__ c, float* __restrict__ data,
+                                                                 size_t n, float* __restrict__ residual) {
+  __shared__ uint32_t s_e;
+  const int g = blockIdx.x, t = threadIdx.x;
+  const int rank = c->rank, world = c->world;
+  const uint32_t e = next_epoch(c, g, &s_e);
+  const size_t half = (size_t)(e & 1u) * c->cap;
+  const size_t base = (size_t)g * AR_CHUNK;
+  // 1. stage my partial of the chunk (bf16: rounded once here, summed in fp32 by the owner)
+  {
+    const size_t i = base + 4 * t;
+    if (i + 4 <= n) {
+      const float4 v = *(const float4*)(data + i);
+      if constexpr (BF16) {
+        uint16_t* s16 = (uint16_t*)(c->buf[rank] + 4 * c->cap);
+        *(uint2*)(s16 + half + i) = make_uint2((uint32_t)f32_to_bf16(v.x) | ((uint32_t)f32_to_bf16(v.y) << 16),
+                                               (uint32_t)f32_to_bf16(v.z) | ((uint32_t)f32_to_bf16(v.w) << 16));
       } else {
-        *(float4*)(data + i) = acc;
+        *(float4*)(c->buf[rank] + half + i) = v;
       }
-    } else {
-      for (size_t k = i; k < n; ++k) {
-        float acc = data[k];
-        for (int p = 0; p < world; ++p)
-          if (p != rank) acc += __builtin_nontemporal_load(c->buf[p] + half + k);
-        if (residual) residual[k] += acc; else data[k] = acc;
+    }
+  }
+  publish(c, 0, g, e);
+  wait_peers(c, 0, g, e);
+  // 2. reduce-scatter: float4 groups [lo, hi) of the chunk belong to this rank
+  const int nq = AR_CHUNK / 4;
+  const int lo = rank * nq / world, hi = (rank + 1) * nq / world;
+  for (int f = lo + t; f < hi; f += AR_THREADS) {
+    const size_t i = base + 4 * (size_t)f;
+    if (i + 4 > n) continue;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int p = 0; p < world; ++p) {
+      float4 v;
+      if (p == rank) {
+        v = *(const float4*)(data + i);
+      } else if constexpr (BF16) {
+        const uint16_t* s16 = (const uint16_t*)(c->buf[p] + 4 * c->cap);
+        typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
+        const u32x2_t u = __builtin_nontemporal_load((const u32x2_t*)(s16 + half + i));
+        v = make_float4(bf16_to_f32(u.x & 0xffff), bf16_to_f32(u.x >> 16), bf16_to_f32(u.y & 0xffff),
+                        bf16_to_f32(u.y >> 16));
+      } else {
+        v = ld_peer(c->buf[p] + half + i);
       }
+      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+    *(float4*)(c->buf[rank] + 2 * c->cap + half + i) = acc;  // my reduced sub-shard
+    put(data, residual, i, acc);
+  }
+  publish(c, 1, g, e);
+  wait_peers(c, 1, g, e);
+  // 3. all-gather the other ranks' reduced sub-shards
+  for (int p = 0; p < world; ++p) {
+    if (p == rank) continue;
+    const int plo = p * nq / world, phi = (p + 1) * nq / world;
+    for (int f = plo + t; f < phi; f += AR_THREADS) {
+      const size_t i = base + 4 * (size_t)f;
+      if (i + 4 > n) continue;
+      put(data, residual, i, ld_peer(c->buf[p] + 2 * c->cap + half + i));
+    }
+  }
+}
+
+// ---- column all-gather: position j = r*rows*slice + b*slice + col is owned by rank r
+__global__ __launch_bounds__(AR_THREADS) void allgather_cols_kernel(const ArDevCtx* __restrict__ c,
+                                                                    float* __restrict__ data, int rows, int slice,
+                                                                    int ld) {
+  __shared__ uint32_t s_e;
+  const int g = blockIdx.x, t = threadIdx.x;
+  const int rank = c->rank;
+  const uint32_t e = next_epoch(c, g, &s_e);
+  const size_t half = (size_t)(e & 1u) * c->cap;
+  const size_t per = (size_t)rows * slice, total = per * c->world;
+  float* mine = c->buf[rank] + half;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const size_t j = (size_t)g * AR_CHUNK + k * AR_THREADS + t;
+    if (j < total && (int)(j / per) == rank) {
+      const size_t w = j % per;
+      mine[j] = data[(w / slice) * (size_t)ld + (size_t)rank * slice + w % slice];
+    }
+  }
+  publish(c, 0, g, e);
+  wait_peers(c, 0, g, e);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const size_t j = (size_t)g * AR_CHUNK + k * AR_THREADS + t;
+    const int r = (int)(j / per);
+    if (j < total && r != rank) {
+      const size_t w = j % per;
+      data[(w / slice) * (size_t)ld + (size_t)r * slice + w % slice] = __builtin_nontemporal_load(c->buf[r] + half + j);
     }
   }
 }
@@ -105,14 +223,15 @@ void* alloc_shared(size_t bytes) {
   return p;
 }
 
+int grid_for(size_t n) { return (int)std::max<size_t>(1, (n + AR_CHUNK - 1) / AR_CHUNK); }
+
 }  // namespace
 
 void launch_allreduce(const ArDevCtx* ctx, int world, float* data, size_t n, float* residual, hipStream_t st) {
   (void)world;
   if (n == 0) return;
-  const size_t chunks = (n + AR_CHUNK - 1) / AR_CHUNK;
-  const int grid = (int)std::min<size_t>(chunks, AR_MAX_WG);
-  hipLaunchKernelGGL(allreduce_oneshot, dim3(grid), dim3(AR_THREADS), 0, st, ctx, data, n, residual);
+  if (n > AR_MAX_CALL) throw std::runtime_error("launch_allreduce: call above AR_MAX_CALL elements");
+  hipLaunchKernelGGL(allreduce_oneshot, dim3(grid_for(n)), dim3(AR_THREADS), 0, st, ctx, data, n, residual);
 }
 
 XgmiComm::XgmiComm(int rank, int world, int device, size_t cap_floats) : device_(device) {
@@ -120,10 +239,13 @@ XgmiComm::XgmiComm(int rank, int world, int device, size_t cap_floats) : device_
   HIP_CHECK(hipSetDevice(device));
   h_.rank = rank;
   h_.world = world;
-  h_.cap = (cap_floats + 3) & ~size_t(3);
-  mybuf_ = (float*)alloc_shared(2 * h_.cap * sizeof(float));
-  myflags_ = (uint32_t*)alloc_shared(AR_MAX_WG * AR_MAX_RANKS * sizeof(uint32_t));
-  HIP_CHECK(hipMemset(myflags_, 0, AR_MAX_WG * AR_MAX_RANKS * sizeof(uint32_t)));
+  // every call moves at most AR_MAX_CALL elements (larger messages are split), so the buffers
+  // are sized for that regardless of the requested capacity: 5 x 2 MB per rank
+  (void)cap_floats;
+  h_.cap = AR_MAX_CALL;
+  mybuf_ = (float*)alloc_shared(5 * h_.cap * sizeof(float));
+  myflags_ = (uint32_t*)alloc_shared(2 * AR_MAX_WG * AR_MAX_RANKS * sizeof(uint32_t));
+  HIP_CHECK(hipMemset(myflags_, 0, 2 * AR_MAX_WG * AR_MAX_RANKS * sizeof(uint32_t)));
   HIP_CHECK(hipMalloc(&h_.epoch, AR_MAX_WG * sizeof(uint32_t)));
   HIP_CHECK(hipMemset(h_.epoch, 0, AR_MAX_WG * sizeof(uint32_t)));
   h_.error = (uint32_t*)alloc_shared(64);
@@ -133,6 +255,8 @@ XgmiComm::XgmiComm(int rank, int world, int device, size_t cap_floats) : device_
   HIP_CHECK(hipMalloc(&d_, sizeof(ArDevCtx)));
   HIP_CHECK(hipMemcpy(d_, &h_, sizeof(ArDevCtx), hipMemcpyHostToDevice));
   HIP_CHECK(hipDeviceSynchronize());
+  if (const char* e = std::getenv("AIOS_TP_TWO_SHOT_MIN")) two_shot_min_ = (size_t)std::atoll(e);
+  if (const char* e = std::getenv("AIOS_TP_BF16")) bf16_ = std::atoi(e) != 0;
   if (world == 1) connected_ = true;
 }
 
@@ -182,13 +306,36 @@ void XgmiComm::connect(const std::vector<std::string>& handles) {
 
 void XgmiComm::allreduce(float* data, size_t n, float* residual, hipStream_t st) {
   if (!connected_) throw std::runtime_error("XgmiComm: allreduce before connect()");
-  if (n > h_.cap) throw std::runtime_error("XgmiComm: message of " + std::to_string(n) + " floats exceeds capacity " +
-                                           std::to_string(h_.cap));
   if (h_.world == 1) {
     if (residual) launch_add(residual, data, n, st);
     return;
   }
-  launch_allreduce(d_, h_.world, data, n, residual, st);
+  for (size_t off = 0; off < n; off += h_.cap) {
+    const size_t m = std::min(h_.cap, n - off);
+    float* d = data + off;
+    float* r = residual ? residual + off : nullptr;
+    if (m >= two_shot_min_ && m % 4 == 0) {
+      if (bf16_)
+        hipLaunchKernelGGL((allreduce_twoshot<true>), dim3(grid_for(m)), dim3(AR_THREADS), 0, st, d_, d, m, r);
+      else
+        hipLaunchKernelGGL((allreduce_twoshot<false>), dim3(grid_for(m)), dim3(AR_THREADS), 0, st, d_, d, m, r);
+    } else {
+      launch_allreduce(d_, h_.world, d, m, r, st);
+    }
+  }
+}
+
+void XgmiComm::allgather_cols(float* data, int rows, int slice, int ld, hipStream_t st) {
+  if (!connected_) throw std::runtime_error("XgmiComm: allgather before connect()");
+  if (h_.world == 1 || rows <= 0) return;
+  if ((size_t)h_.world * slice > h_.cap) throw std::runtime_error("XgmiComm: all-gather slice above capacity");
+  const int rows_per = (int)std::max<size_t>(1, h_.cap / ((size_t)h_.world * slice));
+  for (int r0 = 0; r0 < rows; r0 += rows_per) {
+    const int nr = std::min(rows_per, rows - r0);
+    const size_t total = (size_t)h_.world * nr * slice;
+    hipLaunchKernelGGL(allgather_cols_kernel, dim3(grid_for(total)), dim3(AR_THREADS), 0, st, d_,
+                       data + (size_t)r0 * ld, nr, slice, ld);
+  }
 }
 
 bool XgmiComm::error() const {
@@ -201,6 +348,10 @@ void XgmiComm::reset_error() { HIP_CHECK(hipMemset(h_.error, 0, 4)); }
 
 void XgmiComm::hook(void* self, float* data, size_t n, float* residual, hipStream_t st) {
   static_cast<XgmiComm*>(self)->allreduce(data, n, residual, st);
+}
+
+void XgmiComm::gather_hook(void* self, float* data, int rows, int slice, int ld, hipStream_t st) {
+  static_cast<XgmiComm*>(self)->allgather_cols(data, rows, slice, ld, st);
 }
 
 }  // namespace aios

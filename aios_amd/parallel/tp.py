@@ -1,13 +1,16 @@
 """Tensor parallelism for the local "strategic" tier (BASELINE config 5).
 
 One process per GPU.  Every rank holds a shard of the model (column-parallel Q/K/V and gate/up,
-row-parallel attn_output / ffn_down, replicated embeddings / norms / lm_head; see
-`aios_amd/runtime/loader.py:shard_tensor`) and an `XgmiComm` whose one-shot all-reduce (HIP,
-`aios_amd/csrc/kernels/allreduce.hip`) is fused with the residual add and runs inside the
-engine's captured hipGraph -- 2 collectives per layer, no host involvement per collective.
+row-parallel attn_output / ffn_down, vocab-parallel lm_head, replicated embeddings / norms; see
+`aios_amd/runtime/loader.py:shard_tensor`) and an `XgmiComm` whose all-reduce (HIP,
+`aios_amd/csrc/kernels/allreduce.hip`: one-shot for decode-size messages, reduce-scatter +
+all-gather with bf16 staging for prefill chunks) is fused with the residual add and runs inside
+the engine's captured hipGraph -- 2 collectives per layer plus one logits all-gather per step, no
+host involvement per collective.
 
-After each all-reduce every rank holds the identical residual stream, so the replicated lm_head
-and the on-device sampler produce identical tokens on every rank: no token broadcast is needed,
+After each all-reduce every rank holds the identical residual stream and, after the logits
+all-gather, the identical logits, so the on-device sampler produces identical tokens on every
+rank: no token broadcast is needed,
 only the *commands* (prefill / decode / decode_loop ...) that rank 0 -- the serving leader --
 issues.  `TPEngine` is a drop-in for the native Engine on the leader (the runtime scheduler
 drives it unchanged); `worker_loop` executes the same calls on ranks 1..N-1.

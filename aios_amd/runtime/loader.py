@@ -4,8 +4,9 @@ Replaces `ModelManager::load_model` spawning llama-server (`runtime/src/model_ma
 the file is memory-mapped, each tensor's raw block bytes are handed zero-copy to the engine,
 which uploads them to HBM and repacks them into the GEMV/MFMA layout.  Under tensor
 parallelism each rank receives only its shard: column-parallel Q/K/V/gate/up (whole heads /
-rows), row-parallel attn_output/ffn_down (whole quant blocks along K), replicated embeddings,
-norms and lm_head (SURVEY.md §2.9 TP row).
+rows), row-parallel attn_output/ffn_down (whole quant blocks along K), vocab-parallel lm_head
+(output.weight rows, the logits completed by an xGMI all-gather), replicated embeddings and norms
+(SURVEY.md §2.9 TP row).
 """
 from __future__ import annotations
 
@@ -24,13 +25,14 @@ COLUMN_PARALLEL = ("attn_q.weight", "attn_k.weight", "attn_v.weight", "ffn_gate.
 ROW_PARALLEL = ("attn_output.weight", "ffn_down.weight")
 
 
-def shard_tensor(name: str, raw: np.ndarray, ggml_type: int, rows: int, cols: int, rank: int, tp: int):
+def shard_tensor(name: str, raw: np.ndarray, ggml_type: int, rows: int, cols: int, rank: int, tp: int,
+                 vocab_parallel: bool = False):
     """Return (raw_shard, rows, cols) of this rank's slice of a GGUF tensor."""
     if tp == 1:
         return raw, rows, cols
     short = name.split(".", 2)[-1] if name.startswith("blk.") else name
     blk, bpb = BLOCK_INFO[GGMLType(ggml_type)]
-    if short in COLUMN_PARALLEL:
+    if short in COLUMN_PARALLEL or (vocab_parallel and name == "output.weight"):
         if short.endswith(".bias"):  # 1-D: rows == 1, cols == n
             n = cols // tp
             return raw.view(np.uint8).reshape(cols, -1)[rank * n:(rank + 1) * n].ravel(), 1, n
@@ -61,10 +63,11 @@ def load_engine(path: str, max_ctx: Optional[int] = None, max_slots: int = 4, ma
                               max_batch=max_batch, device=device, tp_rank=tp_rank, tp_size=tp_size,
                               act_q8=act_q8)
     eng = m.Engine(ec)
+    vp = bool(ec.vocab_parallel)
     for tname, ti in r.tensors.items():
         raw = r.tensor_array(tname)
         rows, cols = ti.rows, ti.cols
-        raw, rows, cols = shard_tensor(tname, raw, int(ti.ggml_type), rows, cols, tp_rank, tp_size)
+        raw, rows, cols = shard_tensor(tname, raw, int(ti.ggml_type), rows, cols, tp_rank, tp_size, vp)
         eng.set_tensor(tname, int(ti.ggml_type), rows, cols, raw)
     eng.finalize()
     if verbose:

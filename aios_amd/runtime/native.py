@@ -63,8 +63,10 @@ def require():
 
 
 def engine_config(cfg, max_ctx: Optional[int] = None, max_slots: int = 4, max_batch: int = 8, device: int = 0,
-                  tp_rank: int = 0, tp_size: int = 1, act_q8: bool = True):
-    """aios_amd.models.config.ModelConfig -> native EngineConfig (per-rank shapes under TP)."""
+                  tp_rank: int = 0, tp_size: int = 1, act_q8: bool = True, vocab_parallel: bool = True):
+    """aios_amd.models.config.ModelConfig -> native EngineConfig (per-rank shapes under TP).
+    Under TP the lm_head is vocab-parallel (V/tp rows per rank + logits all-gather) unless the
+    embeddings are tied or V is not divisible by tp."""
     m = require()
     ec = m.EngineConfig()
     ec.name = cfg.name
@@ -88,6 +90,8 @@ def engine_config(cfg, max_ctx: Optional[int] = None, max_slots: int = 4, max_ba
     ec.qkv_bias = int(cfg.qkv_bias)
     ec.tp_rank = tp_rank
     ec.tp_size = tp_size
+    ec.vocab_parallel = int(bool(vocab_parallel) and tp_size > 1 and not cfg.tie_embeddings
+                            and cfg.vocab_size % tp_size == 0)
     ec.device = device
     ec.act_q8 = int(act_q8)
     return ec

@@ -190,7 +190,7 @@ def test_attention_decode(E, hd, H, Hkv, lens, max_ctx, split):
     opart = torch.empty(B, H, nch, hd, device="cuda")
     ml = torch.empty(B, H, nch, 2, device="cuda")
     out = torch.empty(B, H * hd, device="cuda")
-    cnt = torch.zeros(B, Hkv, dtype=torch.int32, device="cuda")
+    cnt = torch.zeros(B, H, dtype=torch.int32, device="cuda")
     scale = 1 / math.sqrt(hd)
     for _ in range(2):  # second launch checks the counters re-armed themselves
         out.zero_()

@@ -84,24 +84,62 @@ def test_tp_command_channel_gloo(tmp_path):
     assert c0 == c1 and [c[0] for c in c0] == ["prefill", "decode", "decode_loop_run"]
 
 
+def test_shard_tensor_vocab_parallel_output():
+    from aios_amd.gguf.quants import BLOCK_INFO, GGMLType
+    from aios_amd.runtime.loader import shard_tensor
+
+    blk, bpb = BLOCK_INFO[GGMLType.Q6_K]
+    rows, cols = 64, 512
+    raw = np.arange(rows * (cols // blk) * bpb, dtype=np.uint64).astype(np.uint8)
+    assert shard_tensor("output.weight", raw, int(GGMLType.Q6_K), rows, cols, 1, 2)[0] is raw  # replicated
+    parts = [shard_tensor("output.weight", raw, int(GGMLType.Q6_K), rows, cols, r, 2, True) for r in range(2)]
+    assert all(p[1] == rows // 2 and p[2] == cols for p in parts)
+    assert np.array_equal(np.concatenate([p[0] for p in parts]), raw)
+
+
+def test_engine_config_vocab_parallel_rules():
+    from aios_amd.models.config import get_preset
+    from aios_amd.runtime import native
+
+    if native.load(build_if_missing=False) is None:
+        pytest.skip("native engine not built")
+    cfg = get_preset("test-tp8-shape")
+    assert native.engine_config(cfg, tp_size=2).vocab_parallel == 1
+    assert native.engine_config(cfg, tp_size=1).vocab_parallel == 0
+    assert native.engine_config(cfg, tp_size=2, vocab_parallel=False).vocab_parallel == 0
+    import dataclasses
+    tied = dataclasses.replace(cfg, tie_embeddings=True)
+    assert native.engine_config(tied, tp_size=2).vocab_parallel == 0
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("world,gemm_prefill", [(2, 0), (4, 0), (2, 1)])
-def test_tp_xgmi_allreduce_and_sharded_model(tmp_path, world, gemm_prefill):
+@pytest.mark.parametrize("world,gemm_prefill,prompt_len", [(2, 0, 21), (4, 0, 21), (2, 1, 21), (2, 1, 640)])
+def test_tp_xgmi_allreduce_and_sharded_model(tmp_path, world, gemm_prefill, prompt_len):
     """TP=N vs TP=1 on the same weights.  With the fp32-activation GEMV prefill (gemm_prefill=0)
     the only differences are fp32 summation order: 1e-3 of the logit scale.  The MFMA prefill
     path rounds activations to bf16 (and sums split-K partials atomically), so a rounding flip
-    between the two shardings propagates: 1e-2 there -- a sharding bug is O(1)."""
+    between the two shardings propagates: 1e-2 there -- a sharding bug is O(1).  The 640-token
+    prompt runs the MFMA prefill in one chunk whose all-reduces (640 x d_model) take the two-shot
+    path with bf16 staging, split over several calls."""
     out = tmp_path / f"tp{world}.json"
+    port = 29600 + world + 10 * gemm_prefill + (20 if prompt_len > 100 else 0)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(world),
-           "--master-addr", "127.0.0.1", "--master-port", str(29600 + world + 10 * gemm_prefill),
-           os.path.join(ROOT, "tools", "tp_check.py"), "--out", str(out), "--model", "test-tp8-shape"]
+           "--master-addr", "127.0.0.1", "--master-port", str(port),
+           os.path.join(ROOT, "tools", "tp_check.py"), "--out", str(out), "--model", "test-tp8-shape",
+           "--prompt-len", str(prompt_len)]
     env = dict(os.environ, AIOS_PREFILL_GEMM=str(gemm_prefill))
     r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=600, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     res = json.loads(out.read_text())
     assert not res["comm_error_flag"] and not res["comm_error_flag_model"]
+    assert res["vocab_parallel"]
     for e in res["allreduce"]:
-        assert e["inplace_err"] < 1e-4 and e["fused_resid_err"] < 1e-4, e
+        # fp32 staging: summation order only; bf16 two-shot staging: one bf16 rounding per partial
+        tol = world * e["scale"] * 2.0 ** -8 if (e["bf16"] and e["two_shot"]) else 1e-4
+        assert e["inplace_err"] < tol and e["fused_resid_err"] < tol + 1e-4, e
+    assert any(e["two_shot"] for e in res["allreduce"])
+    for e in res["allgather"]:
+        assert e["err"] == 0.0, e
     m = res["model"]
     tol = (1e-2 if gemm_prefill else 1e-3) * max(1.0, m["logit_scale"])
     assert m["prefill_logit_max_abs_diff"] < tol

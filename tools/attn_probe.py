@@ -43,8 +43,8 @@ def main():
         opart = torch.empty(1, H, nch, hd, device="cuda")
         ml = torch.empty(1, H, nch, 2, device="cuda")
         out = torch.empty(1, H * hd, device="cuda")
-        cnt = torch.zeros(1, Hkv, dtype=torch.int32, device="cuda")
-        for L in (64, 130, 400, 1000, 2000, 4000):
+        cnt = torch.zeros(1, H, dtype=torch.int32, device="cuda")
+        for L in (64, 130, 153, 256, 400, 1000, 2000, 4000):
             if L > max_ctx:
                 continue
             seq = torch.tensor([L], dtype=torch.int32, device="cuda")

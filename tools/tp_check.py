@@ -4,12 +4,15 @@
   python -m torch.distributed.run --nproc-per-node 2 --master-addr 127.0.0.1 tools/tp_check.py \
       --out gpurun_out/tp.json [--model test-mistral-shape] [--gguf path]
 
-1. all-reduce numerics: random fp32 vectors of several sizes (decode 1x d ... prefill 64x d), with
-   and without the fused residual, against torch's sum of every rank's input (gathered via gloo);
-2. model: a synthetic GGUF (written by rank 0) is loaded sharded on every rank and greedily
-   decoded through prefill + per-step decode + graph decode loop; rank 0 also loads it unsharded
-   (TP=1) and compares the token streams and the final logits;
-3. timing of the one-shot all-reduce at decode size (us per call, graph-free).
+1. all-reduce numerics: random fp32 vectors of several sizes (decode 1x d ... prefill chunks of
+   600 x d, which take the two-shot reduce-scatter + all-gather path and are split into several
+   calls), with and without the fused residual, fp32 and bf16 two-shot staging, against torch's
+   sum of every rank's input (gathered via gloo); the column all-gather of the vocab-parallel
+   lm_head on a rows x (world * slice) matrix;
+2. model: a synthetic GGUF (written by rank 0) is loaded sharded on every rank (vocab-parallel
+   lm_head) and greedily decoded through prefill (--prompt-len tokens) + per-step decode + graph
+   decode loop; rank 0 also loads it unsharded (TP=1) and compares the token streams and logits;
+3. timing of the one-shot all-reduce at decode size and of the two-shot at prefill size.
 Writes one JSON summary (rank 0).
 """
 import argparse
@@ -28,6 +31,7 @@ def main():
     ap.add_argument("--model", default="test-mistral-shape")
     ap.add_argument("--recipe", default="Q4_K_M")
     ap.add_argument("--steps", type=int, default=12)
+    ap.add_argument("--prompt-len", type=int, default=21)
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -46,37 +50,55 @@ def main():
     comm = create_comm(rank, world, dev, 64 * 8192)
     g = torch.Generator().manual_seed(1234 + rank)
     errs = []
-    for n in (4096, 8192, 8 * 8192, 64 * 8192, 1000, 3):
-        x = torch.randn(n, generator=g)
-        resid = torch.randn(n, generator=g)
-        allx = [torch.zeros(n) for _ in range(world)]
-        dist.all_gather(allx, x)
-        want = torch.stack(allx).sum(0)
-        xd = x.cuda()
-        comm.allreduce(xd.data_ptr(), n, 0, torch.cuda.current_stream().cuda_stream)
-        torch.cuda.synchronize()
-        e1 = float((xd.cpu() - want).abs().max())
-        xd = x.cuda()
-        rd = resid.cuda()
-        comm.allreduce(xd.data_ptr(), n, rd.data_ptr(), torch.cuda.current_stream().cuda_stream)
-        torch.cuda.synchronize()
-        e2 = float((rd.cpu() - (resid + want)).abs().max())
-        errs.append({"n": n, "inplace_err": e1, "fused_resid_err": e2})
+    st = torch.cuda.current_stream().cuda_stream
+    for bf16 in (False, True):
+        comm.bf16_payload = bf16
+        for n in (4096, 8192, 8 * 8192, 64 * 8192, 600 * 2048, 1000, 3):
+            x = torch.randn(n, generator=g)
+            resid = torch.randn(n, generator=g)
+            allx = [torch.zeros(n) for _ in range(world)]
+            dist.all_gather(allx, x)
+            want = torch.stack(allx).sum(0)
+            xd = x.cuda()
+            comm.allreduce(xd.data_ptr(), n, 0, st)
+            torch.cuda.synchronize()
+            e1 = float((xd.cpu() - want).abs().max())
+            xd = x.cuda()
+            rd = resid.cuda()
+            comm.allreduce(xd.data_ptr(), n, rd.data_ptr(), st)
+            torch.cuda.synchronize()
+            e2 = float((rd.cpu() - (resid + want)).abs().max())
+            two_shot = world > 1 and n >= comm.two_shot_min and n % 4 == 0
+            errs.append({"n": n, "bf16": bf16, "two_shot": two_shot, "inplace_err": e1, "fused_resid_err": e2,
+                         "scale": float(torch.stack(allx).abs().max())})
+    comm.bf16_payload = True
     res["allreduce"] = errs
+    # column all-gather (vocab-parallel logits): rank r fills its slice, every rank gets all
+    gerr = []
+    for rows, slice_ in ((1, 512), (3, 4000), (8, 64)):
+        ld = slice_ * world
+        full = torch.arange(rows * ld, dtype=torch.float32).reshape(rows, ld) * 0.5 - 7
+        mine = torch.full((rows, ld), float("nan"))
+        mine[:, rank * slice_:(rank + 1) * slice_] = full[:, rank * slice_:(rank + 1) * slice_]
+        md = mine.cuda()
+        comm.allgather_cols(md.data_ptr(), rows, slice_, ld, st)
+        torch.cuda.synchronize()
+        gerr.append({"rows": rows, "slice": slice_, "err": float((md.cpu() - full).abs().max())})
+    res["allgather"] = gerr
     res["comm_error_flag"] = bool(comm.error())
 
-    # timing at decode size (B=1, d=8192)
-    x = torch.randn(8192, device="cuda")
-    st = torch.cuda.current_stream().cuda_stream
-    for _ in range(20):
-        comm.allreduce(x.data_ptr(), 8192, 0, st)
-    torch.cuda.synchronize()
-    dist.barrier()
-    t0 = time.perf_counter()
-    for _ in range(500):
-        comm.allreduce(x.data_ptr(), 8192, 0, st)
-    torch.cuda.synchronize()
-    res["allreduce_us_8192"] = (time.perf_counter() - t0) / 500 * 1e6
+    # timing at decode size (B=1, d=8192): one-shot; at prefill size (512 x 8192): two-shot
+    for n, key, reps in ((8192, "allreduce_us_8192", 500), (512 * 8192, "allreduce_us_512x8192", 20)):
+        x = torch.randn(n, device="cuda")
+        for _ in range(5):
+            comm.allreduce(x.data_ptr(), n, 0, st)
+        torch.cuda.synchronize()
+        dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            comm.allreduce(x.data_ptr(), n, 0, st)
+        torch.cuda.synchronize()
+        res[key] = (time.perf_counter() - t0) / reps * 1e6
     del comm
 
     # ---- 2. sharded model vs unsharded
@@ -90,9 +112,11 @@ def main():
     # fp32 activations on both sides (the int8-activation path quantises per shard, so its
     # rounding differs from TP=1 by design); greedy stream from TP, then TP=1 teacher-forced on
     # the same tokens, comparing logits at every step
-    eng, comm = build_tp_engine(cfg, rank, world, dev, path=path, max_ctx=256, max_slots=2, max_batch=2,
+    max_ctx = (args.prompt_len + args.steps + 64 + 127) // 128 * 128
+    eng, comm = build_tp_engine(cfg, rank, world, dev, path=path, max_ctx=max_ctx, max_slots=2, max_batch=2,
                                 act_q8=False)
-    prompt = [cfg.bos_id] + [(11 * i + 5) % (cfg.vocab_size - 3) + 3 for i in range(20)]
+    res["vocab_parallel"] = bool(eng.vocab_parallel)
+    prompt = [cfg.bos_id] + [(11 * i + 5) % (cfg.vocab_size - 3) + 3 for i in range(args.prompt_len - 1)]
     if rank == 0:
         tp = TPEngine(eng, comm)
         logits = np.asarray(tp.prefill(0, prompt, 0, True))
@@ -112,7 +136,7 @@ def main():
         tp.close()
         from aios_amd.runtime.loader import load_engine
 
-        ref, _, _ = load_engine(path, max_ctx=256, max_slots=2, max_batch=2, device=dev, act_q8=False)
+        ref, _, _ = load_engine(path, max_ctx=max_ctx, max_slots=2, max_batch=2, device=dev, act_q8=False)
         rl = np.asarray(ref.prefill(0, prompt, 0, True))
         pos = len(prompt)
         diffs = []
