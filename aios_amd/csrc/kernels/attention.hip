@@ -23,6 +23,7 @@
 // CDNA guide §6 Guideline 16 / split-K item 2 -- and re-arms the counter.
 #include "../common.h"
 #include "../ops.h"
+#include "gemm_common.h"
 
 namespace aios {
 
@@ -31,13 +32,6 @@ __device__ __forceinline__ void st_wt(float* p, float v) {
 }
 __device__ __forceinline__ float ld_wt(const float* p) {
   return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-__device__ __forceinline__ void bf16x8_to_f32(const uint4& v, float f[8]) {
-  f[0] = bf16_to_f32(v.x & 0xffff); f[1] = bf16_to_f32(v.x >> 16);
-  f[2] = bf16_to_f32(v.y & 0xffff); f[3] = bf16_to_f32(v.y >> 16);
-  f[4] = bf16_to_f32(v.z & 0xffff); f[5] = bf16_to_f32(v.z >> 16);
-  f[6] = bf16_to_f32(v.w & 0xffff); f[7] = bf16_to_f32(v.w >> 16);
 }
 
 template <int CTRL>
@@ -53,41 +47,59 @@ __device__ __forceinline__ float group_sum(float v) {
   if constexpr (N == 16) v += dpp<0x140>(v);  // row_mirror: lane i <-> 15-i within 16
   return v;
 }
-// value of lane ^ OFF (OFF = 8, 16, 32) without the LDS crossbar: DPP row rotate for 8, the
-// gfx950 v_permlane16/32_swap VALU exchanges for 16 / 32
-template <int OFF>
-__device__ __forceinline__ float xlane(float v) {
-  const int lane = threadIdx.x & 63;
+// op(v[lane], v[lane ^ OFF]) for OFF = 8, 16, 32 without the LDS crossbar: DPP row rotate for 8;
+// for 16 / 32 the gfx950 v_permlane16/32_swap of v with itself returns the lower and the upper
+// row of every pair in r[0] / r[1] on all lanes, so op(r[0], r[1]) needs no lane select
+template <int OFF, typename Op>
+__device__ __forceinline__ float xlane_op(float v, Op op) {
   if constexpr (OFF == 8) {
-    return dpp<0x128>(v);  // row_ror:8 within 16 lanes = lane ^ 8
+    return op(v, dpp<0x128>(v));  // row_ror:8 within 16 lanes = lane ^ 8
   } else if constexpr (OFF == 16) {
     const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-    return __uint_as_float((lane & 16) ? r[0] : r[1]);
+    return op(__uint_as_float(r[0]), __uint_as_float(r[1]));
   } else {
     const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-    return __uint_as_float((lane & 32) ? r[0] : r[1]);
+    return op(__uint_as_float(r[0]), __uint_as_float(r[1]));
   }
 }
+struct OpMax { __device__ float operator()(float a, float b) const { return fmaxf(a, b); } };
+struct OpAdd { __device__ float operator()(float a, float b) const { return a + b; } };
 // max / sum over the lanes that share (lane % LPK), i.e. across the 64/LPK key groups of a wave
 template <int LPK>
 __device__ __forceinline__ float keys_max(float v) {
-  if constexpr (LPK <= 8) v = fmaxf(v, xlane<8>(v));
-  if constexpr (LPK <= 16) v = fmaxf(v, xlane<16>(v));
-  return fmaxf(v, xlane<32>(v));
+  if constexpr (LPK <= 8) v = xlane_op<8>(v, OpMax{});
+  if constexpr (LPK <= 16) v = xlane_op<16>(v, OpMax{});
+  return xlane_op<32>(v, OpMax{});
 }
 template <int LPK>
 __device__ __forceinline__ float keys_sum(float v) {
-  if constexpr (LPK <= 8) v += xlane<8>(v);
-  if constexpr (LPK <= 16) v += xlane<16>(v);
-  return v + xlane<32>(v);
+  if constexpr (LPK <= 8) v = xlane_op<8>(v, OpAdd{});
+  if constexpr (LPK <= 16) v = xlane_op<16>(v, OpAdd{});
+  return xlane_op<32>(v, OpAdd{});
 }
 
 constexpr float kLog2e = 1.4426950408889634f;
+// masked-key score / empty-state max: finite, so exp2(kNeg - m) underflows to 0 and
+// exp2(kNeg - kNeg) = 1 without -inf compares on the hot path
+constexpr float kNeg = -1e30f;
+// raw v_exp_f32 (denormal results flush to 0, which is all a softmax weight needs); ocml's exp2f
+// adds a range-scaling compare + 2 selects per call
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+__device__ __forceinline__ float dot2_bf16(uint32_t a, uint32_t b, float c) {
+  return __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(gbf16x2, a), __builtin_bit_cast(gbf16x2, b), c, false);
+}
 
 // One workgroup's share: heads [h0, h0 + G) of KV head kvh, keys of the passes sp, sp + P, ...
-// (P active workgroups per (row, head set); counters indexed by `ci`).
+// (P active workgroups per (row, head set); counters indexed by `ci`).  `ppw` = passes per
+// workgroup the split aims for (1: more workgroups, each one 128-key pass; 2: both buffers).
+//
+// VALU diet (the kernel is VALU-bound per CU once its loads are in flight): q . k runs on
+// v_dot2_f32_bf16 against q pre-rounded to bf16 pairs (4 instructions per 8 dims and head, as the
+// MFMA prefill path rounds q), P . V on packed v_pk_fma_f32 with the probabilities in fp32.
 template <int HD, int G>
-__device__ __forceinline__ void attn_core(const AttnDecodeArgs& a, int sp, int kvh, int h0, int ci, int P_max) {
+__device__ __forceinline__ void attn_core(const AttnDecodeArgs& a, int sp, int kvh, int h0, int ci, int P_max,
+                                          int ppw) {
   constexpr int NW = 8;                // waves per workgroup
   constexpr int LPK = HD / 8;          // lanes per key (8 dims per lane)
   constexpr int KPS = 64 / LPK;        // keys per wave-instruction
@@ -109,6 +121,11 @@ __device__ __forceinline__ void attn_core(const AttnDecodeArgs& a, int sp, int k
   const int koff = wave * KPW + ksub;  // this lane's key within a pass (+ s * KPS)
   const int cmax = a.max_ctx / CH - 1; // last chunk with valid memory
 
+  const int len = a.seq_len[b];
+  const int nchunk = (len + CH - 1) / CH;
+  const int P = max(1, min((nchunk + ppw - 1) / ppw, P_max));
+  if (sp >= P) return;  // uniform: this workgroup has no chunk, issues no K/V traffic
+
   // two passes in flight per workgroup: buffers A and B (static, so they stay in VGPRs)
   uint4 kA[STEPS], vA[STEPS], kB[STEPS], vB[STEPS];
   auto issue = [&](uint4 (&kr)[STEPS], uint4 (&vr)[STEPS], int chunk) __attribute__((always_inline)) {
@@ -118,46 +135,42 @@ __device__ __forceinline__ void attn_core(const AttnDecodeArgs& a, int sp, int k
 #pragma unroll
     for (int s = 0; s < STEPS; ++s) vr[s] = *(const uint4*)(vc + (size_t)(k0 + s * KPS) * HD);
   };
-  const int len = a.seq_len[b];
-  const int nchunk = (len + CH - 1) / CH;
-  // active workgroups: two passes per workgroup, all of their loads in flight at once (one
-  // memory round trip for up to 256 keys); beyond 2 x gridDim.x chunks workgroups loop
-  const int P = max(1, min((nchunk + 1) / 2, P_max));
-  if (sp >= P) return;  // uniform: this workgroup has no chunk, issues no K/V traffic
   issue(kA, vA, sp);
   if (sp + P < nchunk) issue(kB, vB, sp + P);
   const float qs = a.scale * kLog2e;  // scores in the log2 domain: exp2 below
-  float q[G][8];
+  uint32_t q2[G][4];                  // q * scale as bf16 pairs
 #pragma unroll
   for (int g = 0; g < G; ++g) {
     const float* qp = a.q + ((size_t)b * a.n_heads + h0 + g) * HD + dsl * 8;
     const float4 q0 = *(const float4*)qp, q1 = *(const float4*)(qp + 4);
-    q[g][0] = q0.x * qs; q[g][1] = q0.y * qs; q[g][2] = q0.z * qs; q[g][3] = q0.w * qs;
-    q[g][4] = q1.x * qs; q[g][5] = q1.y * qs; q[g][6] = q1.z * qs; q[g][7] = q1.w * qs;
+    q2[g][0] = pk_bf16(q0.x * qs, q0.y * qs);
+    q2[g][1] = pk_bf16(q0.z * qs, q0.w * qs);
+    q2[g][2] = pk_bf16(q1.x * qs, q1.y * qs);
+    q2[g][3] = pk_bf16(q1.z * qs, q1.w * qs);
   }
-  float m[G], l[G], o[G][8];
+  float m[G], l[G];
+  gf32x2 o[G][4];
 #pragma unroll
   for (int g = 0; g < G; ++g) {
-    m[g] = -INFINITY;
+    m[g] = kNeg;
     l[g] = 0.f;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) o[g][i] = 0.f;
+    for (int i = 0; i < 4; ++i) o[g][i] = gf32x2{0.f, 0.f};
   }
   auto pass = [&](const uint4 (&kr)[STEPS], const uint4 (&vr)[STEPS], int c) __attribute__((always_inline)) {
     // ---- scores of this lane's STEPS keys for the G heads (reduced over the key's LPK lanes)
     float sc[STEPS][G];
 #pragma unroll
     for (int s = 0; s < STEPS; ++s) {
-      float kf[8];
-      bf16x8_to_f32(kr[s], kf);
       const bool valid = c * CH + koff + s * KPS < len;
 #pragma unroll
       for (int g = 0; g < G; ++g) {
-        float d = 0.f;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) d = fmaf(q[g][i], kf[i], d);
+        float d = dot2_bf16(kr[s].x, q2[g][0], 0.f);
+        d = dot2_bf16(kr[s].y, q2[g][1], d);
+        d = dot2_bf16(kr[s].z, q2[g][2], d);
+        d = dot2_bf16(kr[s].w, q2[g][3], d);
         d = group_sum<LPK>(d);
-        sc[s][g] = valid ? d : -INFINITY;
+        sc[s][g] = valid ? d : kNeg;
       }
     }
     // ---- per-wave online softmax over this pass's KPW keys
@@ -168,28 +181,32 @@ __device__ __forceinline__ void attn_core(const AttnDecodeArgs& a, int sp, int k
       for (int s = 1; s < STEPS; ++s) mx = fmaxf(mx, sc[s][g]);
       mx = keys_max<LPK>(mx);
       const float mn = fmaxf(m[g], mx);
-      const float alpha = (mn == -INFINITY) ? 1.f : exp2f(m[g] - mn);
+      const float alpha = fast_exp2(m[g] - mn);
       float ps = 0.f;
 #pragma unroll
       for (int s = 0; s < STEPS; ++s) {
-        const float p = (sc[s][g] == -INFINITY) ? 0.f : exp2f(sc[s][g] - mn);
+        const float p = fast_exp2(sc[s][g] - mn);
         sc[s][g] = p;
         ps += p;
       }
       l[g] = l[g] * alpha + keys_sum<LPK>(ps);
       m[g] = mn;
 #pragma unroll
-      for (int i = 0; i < 8; ++i) o[g][i] *= alpha;
+      for (int i = 0; i < 4; ++i) o[g][i] *= alpha;
     }
     // ---- P.V (lane-local over its keys; merged across key groups and waves at the end)
 #pragma unroll
     for (int s = 0; s < STEPS; ++s) {
-      float vf[8];
-      bf16x8_to_f32(vr[s], vf);
+      const uint32_t w[4] = {vr[s].x, vr[s].y, vr[s].z, vr[s].w};
+      gf32x2 vf[4];
 #pragma unroll
-      for (int g = 0; g < G; ++g)
+      for (int i = 0; i < 4; ++i) vf[i] = gf32x2{__uint_as_float(w[i] << 16), __uint_as_float(w[i] & 0xffff0000u)};
 #pragma unroll
-        for (int i = 0; i < 8; ++i) o[g][i] = fmaf(sc[s][g], vf[i], o[g][i]);
+      for (int g = 0; g < G; ++g) {
+        const gf32x2 pp = gf32x2{sc[s][g], sc[s][g]};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) o[g][i] = __builtin_elementwise_fma(pp, vf[i], o[g][i]);
+      }
     }
   };
   for (int c = sp; c < nchunk; c += 2 * P) {
@@ -201,15 +218,21 @@ __device__ __forceinline__ void attn_core(const AttnDecodeArgs& a, int sp, int k
     }
   }
   // ---- merge the key groups of a wave (shuffles), then the 8 waves in LDS (one barrier)
+  float of[G][8];
 #pragma unroll
   for (int g = 0; g < G; ++g)
 #pragma unroll
-    for (int i = 0; i < 8; ++i) o[g][i] = keys_sum<LPK>(o[g][i]);
+    for (int i = 0; i < 4; ++i) {
+      of[g][2 * i] = keys_sum<LPK>(o[g][i].x);
+      of[g][2 * i + 1] = keys_sum<LPK>(o[g][i].y);
+    }
   if (ksub == 0) {
 #pragma unroll
-    for (int g = 0; g < G; ++g)
-#pragma unroll
-      for (int i = 0; i < 8; ++i) s_o[wave][g][dsl * 8 + i] = o[g][i];
+    for (int g = 0; g < G; ++g) {
+      float4* dst = (float4*)&s_o[wave][g][dsl * 8];
+      dst[0] = make_float4(of[g][0], of[g][1], of[g][2], of[g][3]);
+      dst[1] = make_float4(of[g][4], of[g][5], of[g][6], of[g][7]);
+    }
   }
   if (lane < G) {
     // m/l are wave-uniform after keys_max/keys_sum; lane g publishes head g
@@ -230,7 +253,7 @@ __device__ __forceinline__ void attn_core(const AttnDecodeArgs& a, int sp, int k
     float L = 0.f, acc = 0.f;
 #pragma unroll
     for (int w = 0; w < NW; ++w) {
-      const float sw = (s_m[w][g] == -INFINITY) ? 0.f : exp2f(s_m[w][g] - M);
+      const float sw = fast_exp2(s_m[w][g] - M);
       L += sw * s_l[w][g];
       acc += sw * s_o[w][g][d];
     }
@@ -256,90 +279,117 @@ __device__ __forceinline__ void attn_core(const AttnDecodeArgs& a, int sp, int k
   }
   __syncthreads();
   if (!s_last) return;
-  // ---- last arriver: each output sums its partials; m, l and o of 8 partials are loaded
-  //      together (one memory round trip per 8 partials, online rescale across blocks)
+  // ---- last arriver.  (1) one thread per (head, partial) loads that partial's (m, l);
+  //      (2) wave g reduces head g's max M and total L and turns them into normalised weights
+  //      w_p = exp2(m_p - M) / L in LDS; (3) every output sums w_p * o_p with 16 loads in flight.
+  //      Two memory round trips for up to 64 partials (was one per 8 partials).
+  __shared__ float s_pm[G][64], s_pl[G][64];
+  for (int i = threadIdx.x; i < G * nact; i += NT) {
+    const int g = i / nact, p = i - g * nact;
+    const float* mlp = a.ml + (((size_t)b * a.n_heads + h0 + g) * a.n_chunks + p) * 2;
+    s_pm[g][p] = ld_wt(mlp);
+    s_pl[g][p] = ld_wt(mlp + 1);
+  }
+  __syncthreads();
+  if (wave < G) {
+    const int g = wave;
+    const float mv = lane < nact ? s_pm[g][lane] : kNeg;
+    const float lv = lane < nact ? s_pl[g][lane] : 0.f;
+    float M = mv;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) M = fmaxf(M, __shfl_xor(M, o));
+    const float e = fast_exp2(mv - M);
+    float L = e * lv;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) L += __shfl_xor(L, o);
+    if (lane < nact) s_pm[g][lane] = e / L;
+  }
+  __syncthreads();
   for (int idx = threadIdx.x; idx < G * HD; idx += NT) {
     const int g = idx / HD, d = idx - g * HD;
     const int h = h0 + g;
-    const float* mlp = a.ml + ((size_t)b * a.n_heads + h) * a.n_chunks * 2;
     const float* op = a.o_part + ((size_t)b * a.n_heads + h) * a.n_chunks * HD + d;
-    float M = -INFINITY, L = 0.f, acc = 0.f;
-    for (int c = 0; c < nact; c += 8) {
-      float mv[8], lv[8], ov[8];
+    float acc = 0.f;
+    for (int c = 0; c < nact; c += 16) {
+      float ov[16];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int cc = min(c + j, nact - 1);
-        mv[j] = ld_wt(mlp + 2 * cc);
-        lv[j] = ld_wt(mlp + 2 * cc + 1);
-        ov[j] = ld_wt(op + (size_t)cc * HD);
-      }
-      float mb = M;
+      for (int j = 0; j < 16; ++j) ov[j] = ld_wt(op + (size_t)min(c + j, nact - 1) * HD);
 #pragma unroll
-      for (int j = 0; j < 8; ++j)
-        if (c + j < nact) mb = fmaxf(mb, mv[j]);
-      const float al = (M == -INFINITY) ? 0.f : exp2f(M - mb);
-      L *= al;
-      acc *= al;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        if (c + j < nact) {
-          const float w = exp2f(mv[j] - mb);
-          L = fmaf(w, lv[j], L);
-          acc = fmaf(w, ov[j], acc);
-        }
-      }
-      M = mb;
+      for (int j = 0; j < 16; ++j)
+        if (c + j < nact) acc = fmaf(s_pm[g][c + j], ov[j], acc);
     }
-    a.out[((size_t)b * a.n_heads + h) * HD + d] = acc / L;
+    a.out[((size_t)b * a.n_heads + h) * HD + d] = acc;
   }
   if (threadIdx.x == 0) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
 }
 
 // Up to ATTN_SPLIT_LEN keys the G query heads of a KV head are split over G workgroups (one head
 // each; the K/V re-reads hit L2): 4x less dot / softmax / P.V work per workgroup on the latency-
-// bound short contexts of agent turns.  Beyond that one workgroup set per KV head computes all G
-// heads (the KV stream, not the arithmetic, dominates).  The grid is flat (one x-slot per role of
-// the larger mode) and each workgroup derives its role from seq_len, so a hipGraph-captured launch
-// sized for max_ctx carries at most n_heads * ATTN_SHORT_P idle workgroups, never Pmax * n_heads
-// (round-2 probe: 384 idle 512-thread workgroups cost 4 us at a 256-key context).
+// bound short contexts of agent turns.  Beyond that one workgroup set per (KV head, head set of
+// GL <= 4 query heads) computes its heads (the KV stream, not the arithmetic, dominates; GL = 4
+// keeps G = 8 groups in registers).  The grid is flat (one x-slot per role of the larger mode)
+// and each workgroup derives its role from seq_len, so a hipGraph-captured launch sized for
+// max_ctx carries no idle head-split grid (round-2 probe: 384 idle 512-thread workgroups cost
+// 4 us at a 256-key context).
 constexpr int ATTN_SPLIT_LEN = 512;
-constexpr int ATTN_SHORT_P = 2;  // (512 / 128 + 1) / 2 workgroups per head in the short mode
+template <int G>
+struct AttnGL { static constexpr int value = (G % 4 == 0) ? 4 : G; };
+
+struct AttnSplit {
+  int p_long;   // workgroups per (row, head set) in the long mode
+  int p_short;  // workgroups per (row, head) in the short mode
+  int ppw;      // passes per workgroup the split aims for
+};
+
 template <int HD, int G>
-__global__ void __launch_bounds__(512) attn_decode_kernel(AttnDecodeArgs a, int p_max) {
+__global__ void __launch_bounds__(512) attn_decode_kernel(AttnDecodeArgs a, AttnSplit sp_) {
   const int wg = blockIdx.x;
   const int len = a.seq_len[blockIdx.z];
   if (G > 1 && len <= ATTN_SPLIT_LEN) {
-    const int h = wg / ATTN_SHORT_P, sp = wg % ATTN_SHORT_P;
+    const int h = wg / sp_.p_short, sp = wg % sp_.p_short;
     if (h >= a.n_heads) return;
-    attn_core<HD, 1>(a, sp, h / G, h, h, ATTN_SHORT_P);
+    attn_core<HD, 1>(a, sp, h / G, h, h, sp_.p_short, sp_.ppw);
   } else {
-    const int kvh = wg / p_max, sp = wg % p_max;
-    if (kvh >= a.n_kv_heads) return;
-    attn_core<HD, G>(a, sp, kvh, kvh * G, kvh * G, p_max);
+    constexpr int GL = AttnGL<G>::value;
+    const int hsi = wg / sp_.p_long, sp = wg % sp_.p_long;
+    if (hsi >= a.n_kv_heads * (G / GL)) return;
+    const int kvh = hsi / (G / GL), h0 = kvh * G + (hsi % (G / GL)) * GL;
+    attn_core<HD, GL>(a, sp, kvh, h0, h0, sp_.p_long, sp_.ppw);
   }
+}
+
+static int env_int(const char* k, int dflt) {
+  const char* e = std::getenv(k);
+  return e ? std::atoi(e) : dflt;
 }
 
 template <int HD>
 static void launch_hd(const AttnDecodeArgs& a, int G, hipStream_t st) {
   const int nch = std::max(1, a.max_ctx / 128);  // 128-key passes
-  const int P = std::max(1, std::min(nch, a.split / ATTN_CHUNK));  // workgroups per (row, kv head)
-  if (P > a.n_chunks || P > 64 || ATTN_SHORT_P > a.n_chunks)
+  AttnSplit sp;
+  sp.p_long = std::max(1, std::min(nch, a.split / ATTN_CHUNK));
+  // short mode: one workgroup per query head walks all (<= 4) passes -- the probe's best at
+  // <= 256 keys (a combine costs more than the second pass it would spread)
+  sp.p_short = std::max(1, std::min(4, env_int("AIOS_ATTN_SHORT_P", 1)));
+  sp.ppw = std::max(1, std::min(2, env_int("AIOS_ATTN_PPW", 1)));
+  if (sp.p_long > a.n_chunks || sp.p_long > 64 || sp.p_short > a.n_chunks)
     throw std::runtime_error("attn_decode: more splits than partial buffers / 64");
-  const int nwg = std::max(a.n_kv_heads * P, G > 1 ? a.n_heads * ATTN_SHORT_P : 0);
+  const int GL = (G % 4 == 0) ? 4 : G;
+  const int nwg = std::max(a.n_kv_heads * (G / GL) * sp.p_long, G > 1 ? a.n_heads * sp.p_short : 0);
   dim3 grid(nwg, 1, a.B);
   switch (G) {
-    case 1: hipLaunchKernelGGL((attn_decode_kernel<HD, 1>), grid, dim3(512), 0, st, a, P); break;
-    case 2: hipLaunchKernelGGL((attn_decode_kernel<HD, 2>), grid, dim3(512), 0, st, a, P); break;
-    case 4: hipLaunchKernelGGL((attn_decode_kernel<HD, 4>), grid, dim3(512), 0, st, a, P); break;
-    case 5: hipLaunchKernelGGL((attn_decode_kernel<HD, 5>), grid, dim3(512), 0, st, a, P); break;
-    case 8: hipLaunchKernelGGL((attn_decode_kernel<HD, 8>), grid, dim3(512), 0, st, a, P); break;
+    case 1: hipLaunchKernelGGL((attn_decode_kernel<HD, 1>), grid, dim3(512), 0, st, a, sp); break;
+    case 2: hipLaunchKernelGGL((attn_decode_kernel<HD, 2>), grid, dim3(512), 0, st, a, sp); break;
+    case 4: hipLaunchKernelGGL((attn_decode_kernel<HD, 4>), grid, dim3(512), 0, st, a, sp); break;
+    case 5: hipLaunchKernelGGL((attn_decode_kernel<HD, 5>), grid, dim3(512), 0, st, a, sp); break;
+    case 8: hipLaunchKernelGGL((attn_decode_kernel<HD, 8>), grid, dim3(512), 0, st, a, sp); break;
     default: throw std::runtime_error("attn_decode: unsupported GQA group size " + std::to_string(G));
   }
 }
 
-// `split` (kept in the args for the API) now encodes P * ATTN_CHUNK: the number of workgroups
-// per (row, kv head) in the long-context mode.  Target one workgroup per CU for the whole grid
-// (a 512-thread workgroup of this kernel fills a CU's register file), 1..64 per head, each
+// `split` (kept in the args for the API) encodes P * ATTN_CHUNK: the number of workgroups per
+// (row, head set) in the long-context mode.  Target one workgroup per CU for the whole grid (a
+// 512-thread workgroup of this kernel fills a CU's register file), 1..64 per head set, each
 // owning at least one 128-key pass of a max_ctx context.
 int attn_decode_split(int max_ctx, int B, int n_kv_heads) {
   const int nch = std::max(1, max_ctx / 128);

@@ -200,13 +200,21 @@ def test_attention_decode(E, hd, H, Hkv, lens, max_ctx, split):
     torch.cuda.synchronize()
     assert int(cnt.abs().sum()) == 0
     G = H // Hkv
+    log2e = 1.4426950408889634
     for b in range(B):
         L, s = lens[b], b + 1
         k = kc[s, :, :L].float().cpu().repeat_interleave(G, 0)
         v = vc[s, :, :L].float().cpu().repeat_interleave(G, 0)
-        att = torch.softmax(torch.einsum("hd,hsd->hs", q[b].cpu(), k) * scale, -1)
+        # the op as the kernel defines it: q * scale * log2(e) rounded to bf16 (v_dot2_f32_bf16
+        # scores, as the MFMA prefill rounds q), then an fp32 base-2 softmax and fp32 P.V
+        qs = (q[b].cpu() * (scale * log2e)).to(torch.bfloat16).float()
+        att = torch.softmax(torch.einsum("hd,hsd->hs", qs, k) * math.log(2.0), -1)
         ref = torch.einsum("hs,hsd->hd", att, v).reshape(-1)
         assert torch.allclose(out[b].cpu(), ref, atol=2e-4, rtol=2e-3), (b, (out[b].cpu() - ref).abs().max())
+        # and against unrounded fp32 attention: the bf16 q costs < 1e-2 absolute here
+        att32 = torch.softmax(torch.einsum("hd,hsd->hs", q[b].cpu(), k) * scale, -1)
+        ref32 = torch.einsum("hs,hsd->hd", att32, v).reshape(-1)
+        assert (out[b].cpu() - ref32).abs().max() < 1e-2
 
 
 def test_rmsnorm(E):

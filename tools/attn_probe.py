@@ -49,7 +49,7 @@ def main():
                 continue
             seq = torch.tensor([L], dtype=torch.int32, device="cuda")
             row = []
-            for P in (0, 1, 4, 8, 16, 32, 64):
+            for P in (0, 8, 16, 32, 64):
                 if P > nch:
                     continue
                 split = P * E.ATTN_CHUNK
@@ -58,6 +58,19 @@ def main():
                                            ml.data_ptr(), out.data_ptr(), cnt.data_ptr(),
                                            torch.cuda.current_stream().cuda_stream, split)
                 row.append(f"P{P}={graph_time(fn):6.2f}")
+            # split-shape knobs at the launcher's P: passes per workgroup x short-mode splits
+            for ppw in (1, 2):
+                for sp in (1, 2, 4):
+                    os.environ["AIOS_ATTN_PPW"], os.environ["AIOS_ATTN_SHORT_P"] = str(ppw), str(sp)
+                    fn = lambda: E.attn_decode(q.data_ptr(), kc.data_ptr(), vc.data_ptr(), seq.data_ptr(),
+                                               slot.data_ptr(), 1, H, Hkv, hd, max_ctx, nch, 1 / math.sqrt(hd),
+                                               opart.data_ptr(), ml.data_ptr(), out.data_ptr(), cnt.data_ptr(),
+                                               torch.cuda.current_stream().cuda_stream, 0)
+                    row.append(f"w{ppw}s{sp}={graph_time(fn):6.2f}")
+            os.environ.pop("AIOS_ATTN_PPW")
+            os.environ.pop("AIOS_ATTN_SHORT_P")
+            kv_mb = 2 * Hkv * L * hd * 2 / 1e6
+            row.append(f"KV={kv_mb:.2f}MB")
             print(f"max_ctx={max_ctx:5d} len={L:5d}  " + "  ".join(row), flush=True)
     print("launch chain graph (256 blocks): %.2f us/kernel" % E.bench_launch_chain(200, 256, 1, 20))
 
