@@ -116,6 +116,7 @@ PYBIND11_MODULE(_engine, m) {
   m.attr("EPI_RESID") = (int)EPI_RESID;
   m.attr("EPI_SWIGLU") = (int)EPI_SWIGLU;
   m.attr("EPI_QKV") = (int)EPI_QKV;
+  m.attr("KV_BLOCK") = KV_BLOCK;
   m.attr("ATTN_CHUNK") = (int)ATTN_CHUNK;
 
   m.def("device_count", []() {
@@ -185,24 +186,26 @@ PYBIND11_MODULE(_engine, m) {
            py::arg("slot"), py::arg("tokens"), py::arg("start_pos") = 0, py::arg("want_logits") = true)
       .def("decode",
            [](Engine& e, const std::vector<int>& slots, const std::vector<int>& tokens, const std::vector<int>& pos,
-              const std::vector<float>& temperature, const std::vector<int>& top_k, uint64_t seed, py::bytes mask) {
+              const std::vector<float>& temperature, const std::vector<int>& top_k, uint64_t seed, py::bytes mask,
+              const std::vector<float>& top_p) {
              std::string m = mask;  // packed allowed-token bitmask, B rows of ceil(V/8) bytes (or empty)
              std::vector<uint8_t> mv(m.begin(), m.end());
              py::gil_scoped_release nogil;
-             return e.decode(slots, tokens, pos, temperature, top_k, seed, mv);
+             return e.decode(slots, tokens, pos, temperature, top_k, seed, mv, top_p);
            },
            py::arg("slots"), py::arg("tokens"), py::arg("pos"), py::arg("temperature") = std::vector<float>{},
-           py::arg("top_k") = std::vector<int>{}, py::arg("seed") = 0, py::arg("mask") = py::bytes())
+           py::arg("top_k") = std::vector<int>{}, py::arg("seed") = 0, py::arg("mask") = py::bytes(),
+           py::arg("top_p") = std::vector<float>{})
       .def("resample",
            [](Engine& e, int B, const std::vector<float>& temperature, const std::vector<int>& top_k, uint64_t seed,
-              py::bytes mask) {
+              py::bytes mask, const std::vector<float>& top_p) {
              std::string m = mask;
              std::vector<uint8_t> mv(m.begin(), m.end());
              py::gil_scoped_release nogil;
-             return e.resample(B, temperature, top_k, seed, mv);
+             return e.resample(B, temperature, top_k, seed, mv, top_p);
            },
            py::arg("B"), py::arg("temperature") = std::vector<float>{}, py::arg("top_k") = std::vector<int>{},
-           py::arg("seed") = 0, py::arg("mask") = py::bytes())
+           py::arg("seed") = 0, py::arg("mask") = py::bytes(), py::arg("top_p") = std::vector<float>{})
       .def("last_logits",
            [](Engine& e, int B) {
              std::vector<float> v;
@@ -221,6 +224,10 @@ PYBIND11_MODULE(_engine, m) {
       .def("synchronize", &Engine::synchronize, py::call_guard<py::gil_scoped_release>())
       .def("reset_graphs", &Engine::reset_graphs)
       .def("copy_slot", &Engine::copy_slot, py::call_guard<py::gil_scoped_release>())
+      .def("release_slot", &Engine::release_slot)
+      .def("block_table", &Engine::block_table)
+      .def_property_readonly("kv_blocks_free", &Engine::kv_blocks_free)
+      .def_property_readonly("kv_blocks_total", &Engine::kv_blocks_total)
       .def_property_readonly("stream", &Engine::stream_handle)
       .def_property_readonly("k_cache_ptr", &Engine::kv_cache_k)
       .def_property_readonly("v_cache_ptr", &Engine::kv_cache_v)
@@ -295,7 +302,8 @@ PYBIND11_MODULE(_engine, m) {
   m.def("gemv_qkv",
         [](std::vector<PyQMatrix*> segs, int B, uintptr_t x, int ldx, uintptr_t norm_w, float eps, uintptr_t q_out,
            uintptr_t bias, int head_dim, int n_heads, int n_kv_heads, int max_ctx, int rope_neox, float rope_base,
-           uintptr_t pos, uintptr_t slot, uintptr_t k_cache, uintptr_t v_cache, uintptr_t st, int act_q8) {
+           uintptr_t pos, uintptr_t slot, uintptr_t k_cache, uintptr_t v_cache, uintptr_t st, int act_q8,
+           uintptr_t block_table) {
           GemvArgs a;
           std::memset(&a, 0, sizeof(a));
           a.nseg = (int)segs.size();
@@ -308,18 +316,21 @@ PYBIND11_MODULE(_engine, m) {
           a.kv_dim = n_kv_heads * head_dim; a.n_kv_heads = n_kv_heads; a.max_ctx = max_ctx;
           a.rope_neox = rope_neox; a.rope_base = rope_base; a.rope_cs = nullptr; a.pos = (const int*)pos; a.slot = (const int*)slot;
           a.k_cache = (bf16_t*)k_cache; a.v_cache = (bf16_t*)v_cache; a.act_q8 = act_q8;
+          a.block_table = (const int*)block_table;
           launch_gemv(a, S(st));
         },
         py::arg("segs"), py::arg("B"), py::arg("x"), py::arg("ldx"), py::arg("norm_w"), py::arg("eps"),
         py::arg("q_out"), py::arg("bias"), py::arg("head_dim"), py::arg("n_heads"), py::arg("n_kv_heads"),
         py::arg("max_ctx"), py::arg("rope_neox"), py::arg("rope_base"), py::arg("pos"), py::arg("slot"),
-        py::arg("k_cache"), py::arg("v_cache"), py::arg("stream"), py::arg("act_q8") = 0);
+        py::arg("k_cache"), py::arg("v_cache"), py::arg("stream"), py::arg("act_q8") = 0,
+        py::arg("block_table") = 0);
   m.def("attn_decode",
         [](uintptr_t q, uintptr_t k, uintptr_t v, uintptr_t seq_len, uintptr_t slot, int B, int H, int Hkv, int hd,
            int max_ctx, int n_chunks, float scale, uintptr_t opart, uintptr_t ml, uintptr_t out, uintptr_t counters,
-           uintptr_t st, int split) {
+           uintptr_t st, int split, uintptr_t block_table, int bt_rows) {
           AttnDecodeArgs a;
           a.split = split;
+          a.block_table = (const int*)block_table; a.bt_rows = bt_rows;
           a.q = (const float*)q; a.k_cache = (const bf16_t*)k; a.v_cache = (const bf16_t*)v;
           a.seq_len = (const int*)seq_len; a.slot = (const int*)slot;
           a.B = B; a.n_heads = H; a.n_kv_heads = Hkv; a.head_dim = hd; a.max_ctx = max_ctx; a.n_chunks = n_chunks;
@@ -329,7 +340,8 @@ PYBIND11_MODULE(_engine, m) {
         },
         py::arg("q"), py::arg("k"), py::arg("v"), py::arg("seq_len"), py::arg("slot"), py::arg("B"), py::arg("H"),
         py::arg("Hkv"), py::arg("hd"), py::arg("max_ctx"), py::arg("n_chunks"), py::arg("scale"), py::arg("opart"),
-        py::arg("ml"), py::arg("out"), py::arg("counters"), py::arg("st"), py::arg("split") = 0);
+        py::arg("ml"), py::arg("out"), py::arg("counters"), py::arg("st"), py::arg("split") = 0,
+        py::arg("block_table") = 0, py::arg("bt_rows") = 0);
   m.def("attn_decode_split", &attn_decode_split);
   m.def("rmsnorm", [](uintptr_t x, int ldx, uintptr_t w, uintptr_t y, int ldy, int rows, int n, float eps, uintptr_t st) {
     launch_rmsnorm((const float*)x, ldx, (const float*)w, (float*)y, ldy, rows, n, eps, S(st));
@@ -343,24 +355,49 @@ PYBIND11_MODULE(_engine, m) {
   m.def("qkv_post",
         [](uintptr_t qkv, int ldqkv, int T, int H, int Hkv, int hd, uintptr_t q_norm, uintptr_t k_norm, float eps,
            int rope_neox, float rope_base, uintptr_t pos, uintptr_t slot, uintptr_t q_out, uintptr_t k_cache,
-           uintptr_t v_cache, int max_ctx, uintptr_t st) {
+           uintptr_t v_cache, int max_ctx, uintptr_t st, uintptr_t block_table) {
           QkvPostArgs a;
+          a.block_table = (const int*)block_table;
           a.qkv = (const float*)qkv; a.ldqkv = ldqkv; a.T = T; a.n_heads = H; a.n_kv_heads = Hkv; a.head_dim = hd;
           a.q_norm = (const float*)q_norm; a.k_norm = (const float*)k_norm; a.eps = eps; a.rope_neox = rope_neox;
           a.rope_base = rope_base; a.rope_cs = nullptr; a.pos = (const int*)pos; a.slot = (const int*)slot; a.q_out = (float*)q_out;
           a.k_cache = (bf16_t*)k_cache; a.v_cache = (bf16_t*)v_cache; a.max_ctx = max_ctx;
           launch_qkv_post(a, S(st));
-        });
+        },
+        py::arg("qkv"), py::arg("ldqkv"), py::arg("T"), py::arg("H"), py::arg("Hkv"), py::arg("hd"), py::arg("q_norm"),
+        py::arg("k_norm"), py::arg("eps"), py::arg("rope_neox"), py::arg("rope_base"), py::arg("pos"), py::arg("slot"),
+        py::arg("q_out"), py::arg("k_cache"), py::arg("v_cache"), py::arg("max_ctx"), py::arg("st"),
+        py::arg("block_table") = 0);
   m.def("sample",
         [](uintptr_t logits, int ldl, int B, int V, uintptr_t temperature, uintptr_t top_k, uint64_t seed,
-           uintptr_t tokens, uintptr_t pos, uintptr_t mask, uintptr_t st) {
+           uintptr_t tokens, uintptr_t pos, uintptr_t mask, uintptr_t st, uintptr_t top_p) {
+          // grow-on-demand scratch for the raw-op binding (the engine owns its own)
+          static void* ws = nullptr;
+          static size_t ws_bytes = 0;
+          static int* cnt = nullptr;
+          static int cnt_len = 0;
+          const size_t need = sample_ws_bytes(B, V);
+          if (need > ws_bytes) {
+            if (ws) HIP_CHECK(hipFree(ws));
+            HIP_CHECK(hipMalloc(&ws, need));
+            ws_bytes = need;
+          }
+          if (B > cnt_len) {
+            if (cnt) HIP_CHECK(hipFree(cnt));
+            HIP_CHECK(hipMalloc(&cnt, (size_t)B * 4));
+            HIP_CHECK(hipMemset(cnt, 0, (size_t)B * 4));
+            cnt_len = B;
+          }
           SampleArgs a;
           std::memset(&a, 0, sizeof(a));
           a.logits = (const float*)logits; a.ldl = ldl; a.B = B; a.V = V;
           a.temperature = (const float*)temperature; a.top_k = (const int*)top_k; a.seed = seed;
           a.tokens = (int*)tokens; a.pos = (int*)pos; a.mask = (const uint8_t*)mask;
+          a.top_p = (const float*)top_p; a.ws = ws; a.ws_bytes = ws_bytes; a.counters = cnt;
           launch_sample(a, S(st));
-        });
+        },
+        py::arg("logits"), py::arg("ldl"), py::arg("B"), py::arg("V"), py::arg("temperature"), py::arg("top_k"),
+        py::arg("seed"), py::arg("tokens"), py::arg("pos"), py::arg("mask"), py::arg("st"), py::arg("top_p") = 0);
   m.def("gemm",
         [](uintptr_t A, int lda, PyQMatrix* w, int M, uintptr_t C, int ldc, int accumulate, uintptr_t st) {
           GemmArgs a;
@@ -395,13 +432,17 @@ PYBIND11_MODULE(_engine, m) {
   m.def(
       "attn_prefill",
       [](uintptr_t q, uintptr_t k, uintptr_t v, int slot, int start, int T, int H, int Hkv, int hd, int max_ctx,
-         float scale, uintptr_t out, int ldo, uintptr_t st) {
+         float scale, uintptr_t out, int ldo, uintptr_t st, uintptr_t block_table) {
         AttnPrefillArgs a;
+        a.block_table = (const int*)block_table;
         a.q = (const float*)q; a.k_cache = (const bf16_t*)k; a.v_cache = (const bf16_t*)v;
         a.slot = slot; a.start = start; a.T = T; a.n_heads = H; a.n_kv_heads = Hkv; a.head_dim = hd;
         a.max_ctx = max_ctx; a.scale = scale; a.out = (bf16_t*)out; a.ldo = ldo;
         launch_attn_prefill(a, S(st));
-      });
+      },
+      py::arg("q"), py::arg("k"), py::arg("v"), py::arg("slot"), py::arg("start"), py::arg("T"), py::arg("H"),
+      py::arg("Hkv"), py::arg("hd"), py::arg("max_ctx"), py::arg("scale"), py::arg("out"), py::arg("ldo"),
+      py::arg("st"), py::arg("block_table") = 0);
   m.def("attn_prefill_supports", &attn_prefill_supports);
 
   // ------------------------------------------------------------------ JSON-mode grammar (K10)

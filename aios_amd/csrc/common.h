@@ -44,6 +44,22 @@ enum QType : int {
 typedef uint16_t bf16_t;
 
 __device__ __forceinline__ float bf16_to_f32(uint32_t h) { return __uint_as_float(h << 16); }
+
+// ---- paged KV cache ------------------------------------------------------------------------------
+// One layer's K (and V) pool is [n_blocks][n_kv_heads][KV_BLOCK][head_dim] bf16.  Row `slot` of a
+// block table [slots][max_blocks] maps position / KV_BLOCK to a physical block, so slots share the
+// full blocks of a common prompt prefix (refcounted, copy-on-write on the host: engine.hip).  A
+// null table is the identity map block = slot * max_blocks + position / KV_BLOCK.  KV_BLOCK is
+// the decode attention's pass length, so one pass reads one contiguous 32 KB block per KV head.
+constexpr int KV_BLOCK = 128;
+__host__ __device__ __forceinline__ int kv_block(const int* bt, int max_blocks, int slot, int pos) {
+  const int j = pos / KV_BLOCK;
+  return bt ? bt[slot * max_blocks + j] : slot * max_blocks + j;
+}
+__host__ __device__ __forceinline__ size_t kv_offset(const int* bt, int max_blocks, int slot, int n_kv_heads,
+                                                     int kvh, int pos, int hd) {
+  return (((size_t)kv_block(bt, max_blocks, slot, pos) * n_kv_heads + kvh) * KV_BLOCK + (pos % KV_BLOCK)) * hd;
+}
 __device__ __forceinline__ uint16_t f32_to_bf16(float f) {
   // round-to-nearest-even; NaN stays NaN
   uint32_t u = __float_as_uint(f);

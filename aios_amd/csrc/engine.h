@@ -99,10 +99,10 @@ class Engine {
   // with per-row temperature/top_k (0 = greedy) and optional grammar bitmasks; returns tokens.
   std::vector<int> decode(const std::vector<int>& slots, const std::vector<int>& tokens, const std::vector<int>& pos,
                           const std::vector<float>& temperature, const std::vector<int>& top_k, uint64_t seed,
-                          const std::vector<uint8_t>& mask);
+                          const std::vector<uint8_t>& mask, const std::vector<float>& top_p = {});
   // re-sample the last step's logits (no state advance), e.g. with a grammar mask
   std::vector<int> resample(int B, const std::vector<float>& temperature, const std::vector<int>& top_k, uint64_t seed,
-                            const std::vector<uint8_t>& mask);
+                            const std::vector<uint8_t>& mask, const std::vector<float>& top_p = {});
   // logits of the last decode (B x V) -- host copy
   std::vector<float> last_logits(int B);
 
@@ -119,7 +119,14 @@ class Engine {
   void set_allgather(AllGatherFn fn, void* ctx) { allgather_ = fn; allgather_ctx_ = ctx; }
   bool vocab_parallel() const { return cfg_.vocab_parallel != 0; }
   void reset_graphs();
-  void copy_slot(int src, int dst, int n_tokens);  // prefix-cache: duplicate KV rows [0, n)
+  // ---- paged KV (block table per slot; see kv_offset in common.h) --------------------------------
+  // prefix sharing: dst's positions [0, n) become src's -- full blocks shared (refcounted, never
+  // written again by either slot: writes un-share first), the partial last block copied
+  void copy_slot(int src, int dst, int n_tokens);
+  void release_slot(int slot);         // drop every block reference of the slot
+  int kv_blocks_free() const { return (int)free_blocks_.size(); }
+  int kv_blocks_total() const { return kv_nblocks_; }
+  std::vector<int> block_table(int slot) const;
 
   // raw device pointers for tests / custom kernels
   uintptr_t kv_cache_k() const { return (uintptr_t)k_cache_; }
@@ -162,6 +169,10 @@ class Engine {
   int *d_tokens_ = nullptr, *d_pos_ = nullptr, *d_seqlen_ = nullptr, *d_slot_ = nullptr, *d_history_ = nullptr;
   int *d_topk_ = nullptr, *d_step_ = nullptr;
   float* d_temp_ = nullptr;
+  float* d_topp_ = nullptr;
+  void* sample_ws_ = nullptr;
+  size_t sample_ws_bytes_ = 0;
+  int* sample_cnt_ = nullptr;
   uint64_t* d_seed_ = nullptr;
   uint8_t* d_mask_ = nullptr;
   int n_chunks_ = 0;
@@ -190,6 +201,25 @@ class Engine {
  private:
   void layer_decode_gemm(int l, int B);
   int *pf_tokens_ = nullptr, *pf_pos_ = nullptr, *pf_seqlen_ = nullptr, *pf_slot_ = nullptr;
+
+  // paged KV state: host tables are the truth, device copies uploaded (stream idle) when dirty
+  int kv_maxb_ = 0;                // blocks per slot = max_ctx / KV_BLOCK
+  int kv_nblocks_ = 0;             // allocatable blocks per layer pool (+1 null block at the end)
+  std::vector<int> bt_;            // [max_slots][kv_maxb_], -1 = unmapped
+  std::vector<int> refcnt_;        // [kv_nblocks_]
+  std::vector<int> free_blocks_;
+  std::vector<int> row_bt_host_;   // [max_batch][kv_maxb_] as last uploaded
+  int* d_bt_ = nullptr;            // [max_slots][kv_maxb_] slot-indexed (unmapped -> null block)
+  int* d_row_bt_ = nullptr;        // [max_batch][kv_maxb_] rows of the decode batch
+  bool bt_dirty_ = false;
+  std::vector<int> row_slots_, row_pos_;  // decode rows: slot and host-tracked next position
+  const int* attn_bt_ = nullptr;   // table the decode attention reads (rows / slot indexed)
+  int attn_bt_rows_ = 1;
+  int kv_alloc();
+  void kv_unref(int blk);
+  void kv_copy_block(int src, int dst);
+  void kv_prepare_write(int slot, int from, int to);  // map + un-share the blocks of [from, to)
+  void kv_sync(int B);                                 // upload dirty tables (rows 0..B-1)
 
   std::map<int, hipGraphExec_t> graphs_;
   AllReduceFn allreduce_ = nullptr;

@@ -373,8 +373,18 @@ void Engine::finalize() {
   }
   const int d = cfg_.d_model, hd = cfg_.head_dim, H = cfg_.n_heads, Hkv = cfg_.n_kv_heads;
   const int qd = H * hd, kvd = Hkv * hd, V = cfg_.vocab_size, Bm = cfg_.max_batch;
-  if (cfg_.max_ctx % 128) cfg_.max_ctx = (int)align_up(cfg_.max_ctx, 128);  // decode attention passes
-  layer_kv_elems_ = (size_t)cfg_.max_slots * Hkv * cfg_.max_ctx * hd;
+  if (cfg_.max_ctx % KV_BLOCK) cfg_.max_ctx = (int)align_up(cfg_.max_ctx, KV_BLOCK);  // whole KV blocks
+  // paged KV pool: max_slots * max_ctx / KV_BLOCK blocks always suffice (a mapping or
+  // un-sharing step never needs more distinct blocks than there are table entries) + one null
+  // block that unmapped table entries point to on the device
+  kv_maxb_ = cfg_.max_ctx / KV_BLOCK;
+  kv_nblocks_ = cfg_.max_slots * kv_maxb_;
+  bt_.assign((size_t)cfg_.max_slots * kv_maxb_, -1);
+  refcnt_.assign(kv_nblocks_, 0);
+  free_blocks_.clear();
+  for (int b = kv_nblocks_ - 1; b >= 0; --b) free_blocks_.push_back(b);
+  row_bt_host_.assign((size_t)Bm * kv_maxb_, kv_nblocks_);
+  layer_kv_elems_ = (size_t)(kv_nblocks_ + 1) * Hkv * KV_BLOCK * hd;
   kv_bytes_ = 2 * layer_kv_elems_ * cfg_.n_layers * sizeof(bf16_t);
   k_cache_ = (bf16_t*)dmalloc(kv_bytes_ / 2);
   v_cache_ = (bf16_t*)dmalloc(kv_bytes_ / 2);
@@ -414,11 +424,29 @@ void Engine::finalize() {
   d_pos_ = ibuf(Bm);
   d_seqlen_ = ibuf(Bm);
   d_slot_ = ibuf(Bm);
+  d_bt_ = ibuf((size_t)cfg_.max_slots * kv_maxb_);
+  d_row_bt_ = ibuf((size_t)Bm * kv_maxb_);
+  {
+    std::vector<int> nul((size_t)cfg_.max_slots * kv_maxb_, kv_nblocks_);
+    HIP_CHECK(hipMemcpy(d_bt_, nul.data(), nul.size() * 4, hipMemcpyHostToDevice));
+    HIP_CHECK(hipMemcpy(d_row_bt_, nul.data(), (size_t)Bm * kv_maxb_ * 4, hipMemcpyHostToDevice));
+  }
+  attn_bt_ = d_row_bt_;
+  attn_bt_rows_ = 1;
   d_topk_ = ibuf(Bm);
   d_step_ = ibuf(4);
   d_seed_ = (uint64_t*)ibuf(2);
   d_temp_ = fbuf(Bm);
   HIP_CHECK(hipMemset(d_temp_, 0, Bm * 4));
+  d_topp_ = fbuf(Bm);
+  {
+    std::vector<float> ones(Bm, 1.f);
+    HIP_CHECK(hipMemcpy(d_topp_, ones.data(), Bm * 4, hipMemcpyHostToDevice));
+  }
+  sample_ws_bytes_ = sample_ws_bytes(Bm, V);
+  sample_ws_ = dmalloc(sample_ws_bytes_);
+  ws += sample_ws_bytes_;
+  sample_cnt_ = ibuf(Bm);
   d_history_ = ibuf((size_t)Bm * (cfg_.max_ctx + 1));
   d_mask_ = (uint8_t*)dmalloc((size_t)Bm * ((V + 7) / 8));
   ws += (size_t)Bm * ((V + 7) / 8);
@@ -594,12 +622,13 @@ void Engine::layer_decode_gemm(int l, int B) {
   p.bias = L.bqkv; p.q_norm = L.q_norm; p.k_norm = L.k_norm; p.eps = cfg_.norm_eps;
   p.rope_neox = cfg_.rope_neox; p.rope_base = cfg_.rope_theta; p.rope_cs = rope_cs_;
   p.pos = d_pos_; p.slot = d_slot_; p.q_out = q_;
-  p.k_cache = kc; p.v_cache = vc; p.max_ctx = cfg_.max_ctx;
+  p.k_cache = kc; p.v_cache = vc; p.max_ctx = cfg_.max_ctx; p.block_table = d_bt_;
   launch_qkv_post(p, stream_);
   {
     AttnDecodeArgs a;
     a.split = 0;
     a.q = q_; a.k_cache = kc; a.v_cache = vc; a.seq_len = d_seqlen_; a.slot = d_slot_;
+    a.block_table = attn_bt_; a.bt_rows = attn_bt_rows_;
     a.B = B; a.n_heads = H; a.n_kv_heads = Hkv; a.head_dim = hd; a.max_ctx = cfg_.max_ctx;
     a.n_chunks = n_chunks_; a.scale = 1.f / std::sqrt((float)hd);
     a.o_part = opart_; a.ml = ml_; a.out = attn_; a.counters = attn_cnt_;
@@ -654,6 +683,7 @@ void Engine::layer_decode(int l, int B) {
         a.pos = d_pos_; a.slot = d_slot_;
         a.k_cache = k_cache_ + (size_t)l * layer_kv_elems_;
         a.v_cache = v_cache_ + (size_t)l * layer_kv_elems_;
+        a.block_table = d_bt_;
       } else {
         a.epi = EPI_STORE; a.y = qkv_; a.ldy = qd + 2 * kvd;
       }
@@ -672,6 +702,7 @@ void Engine::layer_decode(int l, int B) {
       p.k_cache = k_cache_ + (size_t)l * layer_kv_elems_;
       p.v_cache = v_cache_ + (size_t)l * layer_kv_elems_;
       p.max_ctx = cfg_.max_ctx;
+      p.block_table = d_bt_;
       launch_qkv_post(p, stream_);
     }
   }
@@ -684,6 +715,7 @@ void Engine::layer_decode(int l, int B) {
     a.v_cache = v_cache_ + (size_t)l * layer_kv_elems_;
     a.seq_len = d_seqlen_;
     a.slot = d_slot_;
+    a.block_table = attn_bt_; a.bt_rows = attn_bt_rows_;
     a.B = B; a.n_heads = cfg_.n_heads; a.n_kv_heads = cfg_.n_kv_heads; a.head_dim = hd; a.max_ctx = cfg_.max_ctx;
     a.n_chunks = n_chunks_;
     a.scale = 1.f / std::sqrt((float)hd);
@@ -749,6 +781,7 @@ void Engine::enqueue_decode_step(int B) {
   s.history = d_history_; s.hist_stride = cfg_.max_ctx + 1;
   s.advance = 1;
   s.mask = sample_mask_ ? d_mask_ : nullptr;
+  s.top_p = d_topp_; s.ws = sample_ws_; s.ws_bytes = sample_ws_bytes_; s.counters = sample_cnt_;
   launch_sample(s, stream_);
 }
 
@@ -793,10 +826,10 @@ void Engine::prefill_gemm(int slot, const std::vector<int>& tokens, int start_po
       p.bias = L.bqkv; p.q_norm = L.q_norm; p.k_norm = L.k_norm; p.eps = cfg_.norm_eps;
       p.rope_neox = cfg_.rope_neox; p.rope_base = cfg_.rope_theta; p.rope_cs = rope_cs_;
       p.pos = gm_pos_; p.slot = gm_slot_; p.q_out = gm_q_;
-      p.k_cache = kc; p.v_cache = vc; p.max_ctx = cfg_.max_ctx;
+      p.k_cache = kc; p.v_cache = vc; p.max_ctx = cfg_.max_ctx; p.block_table = d_bt_;
       launch_qkv_post(p, stream_);
       AttnPrefillArgs at;
-      at.q = gm_q_; at.k_cache = kc; at.v_cache = vc;
+      at.q = gm_q_; at.k_cache = kc; at.v_cache = vc; at.block_table = d_bt_;
       at.slot = slot; at.start = start_pos + r0; at.T = n;
       at.n_heads = H; at.n_kv_heads = Hkv; at.head_dim = hd; at.max_ctx = cfg_.max_ctx;
       at.scale = 1.f / std::sqrt((float)hd);
@@ -834,6 +867,8 @@ std::vector<float> Engine::prefill(int slot, const std::vector<int>& tokens, int
   if (slot < 0 || slot >= cfg_.max_slots) throw std::runtime_error("prefill: bad slot");
   for (int t : tokens)
     if (t < 0 || t >= cfg_.vocab_size) throw std::runtime_error("prefill: token id out of range");
+  kv_prepare_write(slot, start_pos, start_pos + T);
+  kv_sync(0);
   if (gemm_prefill_ok(T)) {
     prefill_gemm(slot, tokens, start_pos, want_logits);
     std::vector<float> out;
@@ -893,6 +928,7 @@ std::vector<float> Engine::prefill(int slot, const std::vector<int>& tokens, int
               a.pos = d_pos_; a.slot = d_slot_;
               a.k_cache = k_cache_ + (size_t)l * layer_kv_elems_;
               a.v_cache = v_cache_ + (size_t)l * layer_kv_elems_;
+              a.block_table = d_bt_;
             } else {
               a.epi = EPI_STORE; a.y = qkv_; a.ldy = qd + 2 * kvd;
             }
@@ -909,6 +945,7 @@ std::vector<float> Engine::prefill(int slot, const std::vector<int>& tokens, int
             p.k_cache = k_cache_ + (size_t)l * layer_kv_elems_;
             p.v_cache = v_cache_ + (size_t)l * layer_kv_elems_;
             p.max_ctx = cfg_.max_ctx;
+            p.block_table = d_bt_;
             launch_qkv_post(p, stream_);
           }
         }
@@ -920,6 +957,7 @@ std::vector<float> Engine::prefill(int slot, const std::vector<int>& tokens, int
           a.k_cache = k_cache_ + (size_t)l * layer_kv_elems_;
           a.v_cache = v_cache_ + (size_t)l * layer_kv_elems_;
           a.seq_len = pf_seqlen_; a.slot = pf_slot_;
+          a.block_table = d_bt_; a.bt_rows = 0;  // prefill rows: one slot, slot-indexed table
           a.B = n; a.n_heads = cfg_.n_heads; a.n_kv_heads = cfg_.n_kv_heads; a.head_dim = cfg_.head_dim;
           a.max_ctx = cfg_.max_ctx;
           a.n_chunks = n_chunks_;
@@ -985,7 +1023,8 @@ std::vector<float> Engine::prefill(int slot, const std::vector<int>& tokens, int
 
 std::vector<int> Engine::decode(const std::vector<int>& slots, const std::vector<int>& tokens,
                                 const std::vector<int>& pos, const std::vector<float>& temperature,
-                                const std::vector<int>& top_k, uint64_t seed, const std::vector<uint8_t>& mask) {
+                                const std::vector<int>& top_k, uint64_t seed, const std::vector<uint8_t>& mask,
+                                const std::vector<float>& top_p) {
   if (!finalized_) throw std::runtime_error("engine not finalized");
   HIP_CHECK(hipSetDevice(cfg_.device));
   const int B = (int)slots.size();
@@ -998,6 +1037,8 @@ std::vector<int> Engine::decode(const std::vector<int>& slots, const std::vector
     if (tokens[b] < 0 || tokens[b] >= cfg_.vocab_size) throw std::runtime_error("decode: token out of range");
     sl[b] = pos[b] + 1;
   }
+  row_slots_ = slots;
+  row_pos_ = pos;
   std::vector<float> temps(B, 0.f);
   std::vector<int> tks(B, 0);
   for (int b = 0; b < B && b < (int)temperature.size(); ++b) temps[b] = temperature[b];
@@ -1008,6 +1049,9 @@ std::vector<int> Engine::decode(const std::vector<int>& slots, const std::vector
   HIP_CHECK(hipMemcpyAsync(d_seqlen_, sl.data(), B * 4, hipMemcpyHostToDevice, stream_));
   HIP_CHECK(hipMemcpyAsync(d_temp_, temps.data(), B * 4, hipMemcpyHostToDevice, stream_));
   HIP_CHECK(hipMemcpyAsync(d_topk_, tks.data(), B * 4, hipMemcpyHostToDevice, stream_));
+  std::vector<float> tps(B, 1.f);
+  for (int b = 0; b < B && b < (int)top_p.size(); ++b) tps[b] = top_p[b];
+  HIP_CHECK(hipMemcpyAsync(d_topp_, tps.data(), B * 4, hipMemcpyHostToDevice, stream_));
   const size_t mbytes = (size_t)B * ((cfg_.vocab_size + 7) / 8);
   sample_mask_ = !mask.empty();
   if (sample_mask_) {
@@ -1025,7 +1069,7 @@ std::vector<int> Engine::decode(const std::vector<int>& slots, const std::vector
 }
 
 std::vector<int> Engine::resample(int B, const std::vector<float>& temperature, const std::vector<int>& top_k,
-                                  uint64_t seed, const std::vector<uint8_t>& mask) {
+                                  uint64_t seed, const std::vector<uint8_t>& mask, const std::vector<float>& top_p) {
   // re-run only the sampler on the logits of the last step (grammar fast path: the unmasked
   // sample was rejected on the host)
   HIP_CHECK(hipSetDevice(cfg_.device));
@@ -1035,6 +1079,9 @@ std::vector<int> Engine::resample(int B, const std::vector<float>& temperature, 
   for (int b = 0; b < B && b < (int)top_k.size(); ++b) tks[b] = top_k[b];
   HIP_CHECK(hipMemcpyAsync(d_temp_, temps.data(), B * 4, hipMemcpyHostToDevice, stream_));
   HIP_CHECK(hipMemcpyAsync(d_topk_, tks.data(), B * 4, hipMemcpyHostToDevice, stream_));
+  std::vector<float> tps(B, 1.f);
+  for (int b = 0; b < B && b < (int)top_p.size(); ++b) tps[b] = top_p[b];
+  HIP_CHECK(hipMemcpyAsync(d_topp_, tps.data(), B * 4, hipMemcpyHostToDevice, stream_));
   HIP_CHECK(hipMemcpyAsync(d_seed_, &seed, 8, hipMemcpyHostToDevice, stream_));
   const size_t mbytes = (size_t)B * ((cfg_.vocab_size + 7) / 8);
   if (!mask.empty()) {
@@ -1047,6 +1094,7 @@ std::vector<int> Engine::resample(int B, const std::vector<float>& temperature, 
   s.temperature = d_temp_; s.top_k = d_topk_; s.seed_dev = d_seed_;
   s.tokens = d_tokens_; s.pos = d_pos_; s.advance = 0;
   s.mask = mask.empty() ? nullptr : d_mask_;
+  s.top_p = d_topp_; s.ws = sample_ws_; s.ws_bytes = sample_ws_bytes_; s.counters = sample_cnt_;
   // pos was advanced by the step: RNG key uses pos[b] (a different stream than the first sample)
   launch_sample(s, stream_);
   std::vector<int> out(B);
@@ -1065,8 +1113,12 @@ std::vector<float> Engine::last_logits(int B) {
 void Engine::decode_loop_prepare(const std::vector<int>& slots, const std::vector<int>& tokens,
                                  const std::vector<int>& pos) {
   const int B = (int)slots.size();
+  if (B < 1 || B > cfg_.max_batch || (int)pos.size() != B || (int)tokens.size() != B)
+    throw std::runtime_error("decode_loop_prepare: bad batch");
   std::vector<int> sl(B);
   for (int b = 0; b < B; ++b) sl[b] = pos[b] + 1;
+  row_slots_ = slots;
+  row_pos_ = pos;
   std::vector<float> temps(B, 0.f);
   std::vector<int> tks(B, 0);
   HIP_CHECK(hipMemcpyAsync(d_slot_, slots.data(), B * 4, hipMemcpyHostToDevice, stream_));
@@ -1075,6 +1127,8 @@ void Engine::decode_loop_prepare(const std::vector<int>& slots, const std::vecto
   HIP_CHECK(hipMemcpyAsync(d_seqlen_, sl.data(), B * 4, hipMemcpyHostToDevice, stream_));
   HIP_CHECK(hipMemcpyAsync(d_temp_, temps.data(), B * 4, hipMemcpyHostToDevice, stream_));
   HIP_CHECK(hipMemcpyAsync(d_topk_, tks.data(), B * 4, hipMemcpyHostToDevice, stream_));
+  std::vector<float> ones(B, 1.f);
+  HIP_CHECK(hipMemcpyAsync(d_topp_, ones.data(), B * 4, hipMemcpyHostToDevice, stream_));
   const uint64_t zero = 0;
   HIP_CHECK(hipMemcpyAsync(d_seed_, &zero, 8, hipMemcpyHostToDevice, stream_));
   HIP_CHECK(hipStreamSynchronize(stream_));
@@ -1085,6 +1139,13 @@ void Engine::decode_loop_prepare(const std::vector<int>& slots, const std::vecto
 void Engine::decode_loop_run(int B, int n_steps, bool use_graph) {
   TraceRange tr(use_graph ? "aios.decode_graph_replay" : "aios.decode_eager");
   HIP_CHECK(hipSetDevice(cfg_.device));
+  if ((int)row_slots_.size() < B) throw std::runtime_error("decode_loop_run: rows not prepared");
+  // map (and un-share) the blocks the n steps will write, before any of them is enqueued
+  for (int b = 0; b < B; ++b) {
+    kv_prepare_write(row_slots_[b], row_pos_[b], std::min(row_pos_[b] + n_steps, cfg_.max_ctx));
+    row_pos_[b] = std::min(row_pos_[b] + n_steps, cfg_.max_ctx);
+  }
+  kv_sync(B);
   if (!use_graph) {
     for (int i = 0; i < n_steps; ++i) enqueue_decode_step(B);
     return;
@@ -1125,19 +1186,114 @@ void Engine::reset_graphs() {
   graphs_.clear();
 }
 
-void Engine::copy_slot(int src, int dst, int n) {
-  if (src == dst || n <= 0) return;
-  const int hd = cfg_.head_dim, Hkv = cfg_.n_kv_heads;
-  const size_t pitch = (size_t)cfg_.max_ctx * hd * 2;
-  for (int l = 0; l < cfg_.n_layers; ++l) {
+// ---- paged KV ----------------------------------------------------------------------------------
+int Engine::kv_alloc() {
+  if (free_blocks_.empty()) throw std::runtime_error("paged KV: pool exhausted");  // cannot happen, see finalize
+  const int b = free_blocks_.back();
+  free_blocks_.pop_back();
+  refcnt_[b] = 1;
+  return b;
+}
+
+void Engine::kv_unref(int blk) {
+  if (blk < 0) return;
+  if (--refcnt_[blk] == 0) free_blocks_.push_back(blk);
+}
+
+// one block of every layer's K and V pool: [n_kv_heads][KV_BLOCK][hd] contiguous
+void Engine::kv_copy_block(int src, int dst) {
+  const size_t blk = (size_t)cfg_.n_kv_heads * KV_BLOCK * cfg_.head_dim;
+  for (int l = 0; l < cfg_.n_layers; ++l)
     for (bf16_t* base : {k_cache_, v_cache_}) {
       bf16_t* lb = base + (size_t)l * layer_kv_elems_;
-      const bf16_t* s = lb + (size_t)src * Hkv * cfg_.max_ctx * hd;
-      bf16_t* d = lb + (size_t)dst * Hkv * cfg_.max_ctx * hd;
-      HIP_CHECK(hipMemcpy2DAsync(d, pitch, s, pitch, (size_t)n * hd * 2, Hkv, hipMemcpyDeviceToDevice, stream_));
+      HIP_CHECK(hipMemcpyAsync(lb + (size_t)dst * blk, lb + (size_t)src * blk, blk * sizeof(bf16_t),
+                               hipMemcpyDeviceToDevice, stream_));
+    }
+}
+
+void Engine::kv_prepare_write(int slot, int from, int to) {
+  if (slot < 0 || slot >= cfg_.max_slots) throw std::runtime_error("paged KV: bad slot");
+  if (to <= from) return;
+  int* row = bt_.data() + (size_t)slot * kv_maxb_;
+  for (int j = from / KV_BLOCK; j <= (to - 1) / KV_BLOCK && j < kv_maxb_; ++j) {
+    if (row[j] < 0) {
+      row[j] = kv_alloc();
+      bt_dirty_ = true;
+    } else if (refcnt_[row[j]] > 1) {  // shared prefix block about to be written: un-share
+      const int nb = kv_alloc();
+      kv_copy_block(row[j], nb);
+      kv_unref(row[j]);
+      row[j] = nb;
+      bt_dirty_ = true;
     }
   }
+}
+
+// Upload the slot table (when dirty) and the row table of decode rows 0..B-1 (when it changed).
+// Blocking uploads with the stream drained first: the captured decode graph reads the tables in
+// place, and a table changes only every KV_BLOCK tokens of a sequence or when rows change.
+void Engine::kv_sync(int B) {
+  bool rows_changed = false;
+  std::vector<int> rows((size_t)B * kv_maxb_);
+  for (int b = 0; b < B; ++b)
+    for (int j = 0; j < kv_maxb_; ++j) {
+      const int v = bt_[(size_t)row_slots_[b] * kv_maxb_ + j];
+      rows[(size_t)b * kv_maxb_ + j] = v < 0 ? kv_nblocks_ : v;
+    }
+  if (B > 0 && std::memcmp(rows.data(), row_bt_host_.data(), rows.size() * 4) != 0) rows_changed = true;
+  if (!bt_dirty_ && !rows_changed) return;
   HIP_CHECK(hipStreamSynchronize(stream_));
+  if (bt_dirty_) {
+    std::vector<int> dev(bt_.size());
+    for (size_t i = 0; i < bt_.size(); ++i) dev[i] = bt_[i] < 0 ? kv_nblocks_ : bt_[i];
+    HIP_CHECK(hipMemcpy(d_bt_, dev.data(), dev.size() * 4, hipMemcpyHostToDevice));
+    bt_dirty_ = false;
+  }
+  if (rows_changed) {
+    std::copy(rows.begin(), rows.end(), row_bt_host_.begin());
+    HIP_CHECK(hipMemcpy(d_row_bt_, rows.data(), rows.size() * 4, hipMemcpyHostToDevice));
+  }
+}
+
+void Engine::copy_slot(int src, int dst, int n) {
+  if (!finalized_) throw std::runtime_error("engine not finalized");
+  if (src < 0 || src >= cfg_.max_slots || dst < 0 || dst >= cfg_.max_slots) throw std::runtime_error("copy_slot: bad slot");
+  if (src == dst) return;
+  HIP_CHECK(hipSetDevice(cfg_.device));
+  n = std::min(n, cfg_.max_ctx);
+  int* s = bt_.data() + (size_t)src * kv_maxb_;
+  int* d = bt_.data() + (size_t)dst * kv_maxb_;
+  for (int j = 0; j < kv_maxb_; ++j) {  // dst's old content is dropped
+    kv_unref(d[j]);
+    d[j] = -1;
+  }
+  const int full = std::max(n, 0) / KV_BLOCK;
+  for (int j = 0; j < full; ++j) {
+    d[j] = s[j];
+    if (d[j] >= 0) ++refcnt_[d[j]];
+  }
+  if (n > 0 && n % KV_BLOCK && s[full] >= 0) {  // the partial block: private copy
+    d[full] = kv_alloc();
+    kv_copy_block(s[full], d[full]);
+  }
+  bt_dirty_ = true;
+  kv_sync(0);
+  HIP_CHECK(hipStreamSynchronize(stream_));
+}
+
+void Engine::release_slot(int slot) {
+  if (slot < 0 || slot >= cfg_.max_slots) throw std::runtime_error("release_slot: bad slot");
+  int* row = bt_.data() + (size_t)slot * kv_maxb_;
+  for (int j = 0; j < kv_maxb_; ++j) {
+    if (row[j] >= 0) bt_dirty_ = true;
+    kv_unref(row[j]);
+    row[j] = -1;
+  }
+}
+
+std::vector<int> Engine::block_table(int slot) const {
+  if (slot < 0 || slot >= cfg_.max_slots) throw std::runtime_error("block_table: bad slot");
+  return std::vector<int>(bt_.begin() + (size_t)slot * kv_maxb_, bt_.begin() + (size_t)(slot + 1) * kv_maxb_);
 }
 
 }  // namespace aios

@@ -42,7 +42,8 @@ struct GemvArgs {
   const float2* rope_cs;         // [max_ctx][head_dim/2] (cos, sin) table or null
   const int* pos;               // [B] position of the token being written
   const int* slot;              // [B] KV-cache slot (null -> b)
-  bf16_t* k_cache;              // layer base: [slots][n_kv][max_ctx][hd]
+  bf16_t* k_cache;              // layer base of the paged pool [blocks][n_kv][KV_BLOCK][hd]
+  const int* block_table;       // [slots][max_ctx / KV_BLOCK] or null (identity)
   bf16_t* v_cache;
 };
 

@@ -114,12 +114,17 @@ __device__ __forceinline__ void attn_core(const AttnDecodeArgs& a, int sp, int k
   const int b = blockIdx.z;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int ksub = lane / LPK, dsl = lane % LPK;
+  static_assert(CH == KV_BLOCK, "one decode pass = one paged KV block");
   const int slot = a.slot ? a.slot[b] : b;
-  const size_t kv_base = (((size_t)slot * a.n_kv_heads + kvh) * a.max_ctx) * HD;
-  const bf16_t* kc = a.k_cache + kv_base + dsl * 8;
-  const bf16_t* vc = a.v_cache + kv_base + dsl * 8;
+  // paged KV: pass c reads physical block bt[c]; a row-indexed table (bt_rows) is looked up
+  // without waiting for slot[b], so its load overlaps the seq_len / slot loads
+  const int maxb = a.max_ctx / KV_BLOCK;
+  const int* btr = a.block_table ? a.block_table + (size_t)(a.bt_rows ? b : slot) * maxb : nullptr;
+  const size_t blk_stride = (size_t)a.n_kv_heads * KV_BLOCK * HD;
   const int koff = wave * KPW + ksub;  // this lane's key within a pass (+ s * KPS)
-  const int cmax = a.max_ctx / CH - 1; // last chunk with valid memory
+  const bf16_t* kc = a.k_cache + (size_t)kvh * KV_BLOCK * HD + (size_t)koff * HD + dsl * 8;
+  const bf16_t* vc = a.v_cache + (size_t)kvh * KV_BLOCK * HD + (size_t)koff * HD + dsl * 8;
+  const int cmax = maxb - 1;           // last chunk with valid memory
 
   const int len = a.seq_len[b];
   const int nchunk = (len + CH - 1) / CH;
@@ -129,11 +134,12 @@ __device__ __forceinline__ void attn_core(const AttnDecodeArgs& a, int sp, int k
   // two passes in flight per workgroup: buffers A and B (static, so they stay in VGPRs)
   uint4 kA[STEPS], vA[STEPS], kB[STEPS], vB[STEPS];
   auto issue = [&](uint4 (&kr)[STEPS], uint4 (&vr)[STEPS], int chunk) __attribute__((always_inline)) {
-    const int k0 = min(chunk, cmax) * CH + koff;  // clamped: always valid memory
+    const int c = min(chunk, cmax);  // clamped: always a mapped block
+    const size_t base = (size_t)(btr ? btr[c] : slot * maxb + c) * blk_stride;
 #pragma unroll
-    for (int s = 0; s < STEPS; ++s) kr[s] = *(const uint4*)(kc + (size_t)(k0 + s * KPS) * HD);
+    for (int s = 0; s < STEPS; ++s) kr[s] = *(const uint4*)(kc + base + (size_t)s * KPS * HD);
 #pragma unroll
-    for (int s = 0; s < STEPS; ++s) vr[s] = *(const uint4*)(vc + (size_t)(k0 + s * KPS) * HD);
+    for (int s = 0; s < STEPS; ++s) vr[s] = *(const uint4*)(vc + base + (size_t)s * KPS * HD);
   };
   issue(kA, vA, sp);
   if (sp + P < nchunk) issue(kB, vB, sp + P);

@@ -77,9 +77,12 @@ __global__ void __launch_bounds__(256) attn_prefill_kernel(AttnPrefillArgs a) {
     for (int e = 0; e < 16; ++e) o[i][e] = 0.f;
   float m_run = -INFINITY, l_run = 0.f;
 
-  const size_t kv_base = (((size_t)a.slot * a.n_kv_heads + kvh) * a.max_ctx) * HD;
-  const bf16_t* kc = a.k_cache + kv_base;
-  const bf16_t* vc = a.v_cache + kv_base;
+  // paged KV: 64-key tile kt lives in block bt[kt / 2] at key offset (kt % 2) * 64
+  static_assert(KV_BLOCK == 2 * FP_KT, "two prefill key tiles per paged KV block");
+  const int maxb = a.max_ctx / KV_BLOCK;
+  const size_t blk_stride = (size_t)a.n_kv_heads * KV_BLOCK * HD;
+  const bf16_t* kc = a.k_cache + (size_t)kvh * KV_BLOCK * HD;
+  const bf16_t* vc = a.v_cache + (size_t)kvh * KV_BLOCK * HD;
   const int last_pos = start + min(T, t0 + BQ) - 1;  // highest query position of the block
   const int ntiles = last_pos / FP_KT + 1;
 
@@ -88,10 +91,12 @@ __global__ void __launch_bounds__(256) attn_prefill_kernel(AttnPrefillArgs a) {
   constexpr int PPT = PIECES / 256;        // per thread
   u32x4_t kreg[PPT], vreg[PPT];
   auto load = [&](int kt) {
+    const size_t tbase = (size_t)kv_block(a.block_table, maxb, a.slot, kt * FP_KT) * blk_stride +
+                         (size_t)(kt & 1) * FP_KT * HD;
     static_for<PPT>([&](auto I) {
       constexpr int i = decltype(I)::value;
       const int idx = tid + 256 * i, key = idx / (HD / 8), c = idx % (HD / 8);
-      const size_t off = (size_t)(kt * FP_KT + key) * HD + c * 8;  // < max_ctx rows: valid
+      const size_t off = tbase + (size_t)key * HD + c * 8;
       kreg[i] = *(const u32x4_t*)(kc + off);
       vreg[i] = *(const u32x4_t*)(vc + off);
     });

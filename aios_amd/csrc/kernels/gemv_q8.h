@@ -420,7 +420,7 @@ __device__ __forceinline__ void qkv_part(const GemvArgs& a, int grow, int& part,
   lr = r - head * hd;
 }
 __device__ __forceinline__ void gemv_epilogue1(const GemvArgs& a, int grow, float v0, float v1, const float2* rope_l,
-                                               int pos0, int slot0) {
+                                               int pos0, int kv_blk0) {
   const int nrow = a.row_base + a.N;
   switch (a.epi) {
     case EPI_STORE:
@@ -459,7 +459,8 @@ __device__ __forceinline__ void gemv_epilogue1(const GemvArgs& a, int grow, floa
         q[db] = v1;
       } else {
         bf16_t* cache = (part == 1 ? a.k_cache : a.v_cache);
-        const size_t base = (((size_t)slot0 * a.n_kv_heads + head) * a.max_ctx + pos0) * hd;
+        // kv_blk0: the physical block of (slot, pos), looked up once in the prologue
+        const size_t base = (((size_t)kv_blk0 * a.n_kv_heads + head) * KV_BLOCK + (pos0 % KV_BLOCK)) * hd;
         cache[base + da] = f32_to_bf16(v0);
         cache[base + db] = f32_to_bf16(v1);
       }
@@ -541,11 +542,11 @@ __global__ void __launch_bounds__(Q8_WAVES * 64) gemv_q8_rows(GemvArgs a) {
     q8_load_item<QT, U>(w, lrow, it, nch, r);
   };
 
-  int pos0 = 0, slot0 = 0;
+  int pos0 = 0, kv_blk0 = 0;
   if constexpr (B == 1) {
     if (a.epi == EPI_QKV) {
       pos0 = a.pos[0];
-      slot0 = a.slot ? a.slot[0] : 0;
+      kv_blk0 = kv_block(a.block_table, a.max_ctx / KV_BLOCK, a.slot ? a.slot[0] : 0, pos0);
       for (int i = threadIdx.x; i < (a.head_dim >> 1); i += blockDim.x) {
         float2 t;
         if (a.rope_cs) {
@@ -593,7 +594,7 @@ __global__ void __launch_bounds__(Q8_WAVES * 64) gemv_q8_rows(GemvArgs a) {
     }
     if constexpr (B == 1) {
       const float2 v = wave_sum_pair(acc[0][0], acc[1][0]);
-      if (lane == 0) gemv_epilogue1(a, a.row_base + 2 * p, v.x * s[0], v.y * s[0], rope_l, pos0, slot0);
+      if (lane == 0) gemv_epilogue1(a, a.row_base + 2 * p, v.x * s[0], v.y * s[0], rope_l, pos0, kv_blk0);
     } else {
 #pragma unroll
       for (int r = 0; r < GEMV_ROWS; ++r)

@@ -50,17 +50,20 @@ struct QkvPostArgs {
   const int* pos;    // [T]
   const int* slot;   // [T] or null (0)
   float* q_out;      // [T][n_heads*head_dim]
-  bf16_t* k_cache;   // layer base
+  bf16_t* k_cache;   // layer base of the paged pool [blocks][n_kv][KV_BLOCK][hd]
   bf16_t* v_cache;
   int max_ctx;
+  const int* block_table = nullptr;  // [slots][max_ctx / KV_BLOCK] or null (identity)
 };
 void launch_qkv_post(const QkvPostArgs& a, hipStream_t st);
 
 // ---- attention ---------------------------------------------------------------------------------
 struct AttnDecodeArgs {
   const float* q;          // [B][n_heads][head_dim]
-  const bf16_t* k_cache;   // layer base [slots][n_kv][max_ctx][hd]
+  const bf16_t* k_cache;   // layer base of the paged pool [blocks][n_kv][KV_BLOCK][hd]
   const bf16_t* v_cache;
+  const int* block_table = nullptr;  // [slots][max_ctx / KV_BLOCK] or null (identity)
+  int bt_rows = 0;         // block_table indexed by row b instead of slot[b]
   const int* seq_len;      // [B] number of valid keys (pos+1)
   const int* slot;         // [B] or null
   int B, n_heads, n_kv_heads, head_dim, max_ctx;
@@ -80,8 +83,9 @@ int attn_decode_split(int max_ctx, int B, int n_kv_heads);
 // slot, over the cached keys [0, start+T) (MFMA; kernels/attention_prefill.hip)
 struct AttnPrefillArgs {
   const float* q;          // [T][n_heads][head_dim] (RoPE applied)
-  const bf16_t* k_cache;   // layer base [slots][n_kv][max_ctx][hd]
+  const bf16_t* k_cache;   // layer base of the paged pool [blocks][n_kv][KV_BLOCK][hd]
   const bf16_t* v_cache;
+  const int* block_table = nullptr;  // [slots][max_ctx / KV_BLOCK] or null (identity)
   int slot, start, T;
   int n_heads, n_kv_heads, head_dim, max_ctx;
   float scale;
@@ -92,8 +96,9 @@ void launch_attn_prefill(const AttnPrefillArgs& a, hipStream_t st);
 bool attn_prefill_supports(int n_heads, int n_kv_heads, int head_dim);  // keys per workgroup the launcher picks
 
 // ---- sampling ---------------------------------------------------------------------------------
-// per row b: token[b] = argmax(logits[b])   (temperature[b] > 0 -> Gumbel-max sample with
-// top-k filtering when top_k[b] > 0); then pos[b] += 1, seq_len[b] = pos[b] + 1,
+// per row b: token[b] = argmax(logits[b])   (temperature[b] > 0 -> Gumbel-max sample from
+// softmax(logits / T) restricted to the top-k (top_k[b] > 0, <= 256) and the nucleus top_p[b]
+// (< 1; over the top-256 when top-k is off)); then pos[b] += 1, seq_len[b] = pos[b] + 1,
 // history[b][step] = token.
 struct SampleArgs {
   const float* logits;
@@ -110,8 +115,13 @@ struct SampleArgs {
   int hist_stride;
   int advance;
   const uint8_t* mask;       // [B][ceil(V/8)] allowed-token bitmask or null
+  const float* top_p;        // [B] nucleus mass (>= 1: off) or null
+  void* ws;                  // sample_ws_bytes(B, V) scratch (slice partials + candidates)
+  size_t ws_bytes;
+  int* counters;             // [B] arrival tickets, zero-initialised, self re-arming
 };
 void launch_sample(const SampleArgs& a, hipStream_t st);
+size_t sample_ws_bytes(int B, int V);
 
 // ---- MFMA GEMM (prefill) ----------------------------------------------------------------------
 // C[M][N] (fp32, epilogue) = A[M][K] (bf16) x W[N][K]^T (quantized, dequantized tile-wise in LDS)

@@ -59,7 +59,8 @@ class TPEngine:
     shard."""
 
     _FORWARD = frozenset({"prefill", "decode", "resample", "last_logits", "decode_loop_prepare",
-                          "decode_loop_run", "decode_loop_history", "synchronize", "reset_graphs", "copy_slot"})
+                          "decode_loop_run", "decode_loop_history", "synchronize", "reset_graphs", "copy_slot",
+                          "release_slot"})
 
     def __init__(self, engine, comm, group=None, send=None, on_close=None):
         self._eng = engine

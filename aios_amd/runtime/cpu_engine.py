@@ -82,7 +82,7 @@ class CpuEngine:
         self.last = logits[None]
         return logits if want_logits else []
 
-    def decode(self, slots, toks, pos, temps, topk, seed, mask: bytes = b""):
+    def decode(self, slots, toks, pos, temps, topk, seed, mask: bytes = b"", top_p=None):
         V = self.config.vocab_size
         row = (V + 7) // 8
         out, rows = [], []
@@ -96,7 +96,8 @@ class CpuEngine:
             t = float(temps[b]) if b < len(temps) else 0.0
             k = int(topk[b]) if b < len(topk) else 0
             rng = np.random.default_rng((int(seed) << 20) ^ (slot << 12) ^ p)
-            out.append(host_sampler.sample(logits, t, k, 1.0, m, rng))
+            tp = float(top_p[b]) if top_p is not None and b < len(top_p) else 1.0
+            out.append(host_sampler.sample(logits, t, k, tp, m, rng))
         self.last = np.stack(rows) if rows else None
         return out
 

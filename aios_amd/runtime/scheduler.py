@@ -3,10 +3,16 @@
 Replaces the per-request HTTP round trip to llama-server (`runtime/src/inference.rs:94-186`)
 with an in-process worker per model that owns the native Engine:
 
-* admission: a waiting request takes a free KV slot; the slot whose cached tokens share the
-  longest prefix with the prompt is preferred and only the remainder is prefilled (prefix KV
-  reuse -- the autonomy loop's tool catalogue and format rules repeat on every round, §6.1);
-* each iteration runs ONE batched decode step (hipGraph replay) for every active sequence, so
+* admission: a waiting request takes a free KV slot and inherits the longest cached prefix of
+  ANY slot -- free or still decoding: the engine's paged KV shares that prefix's full blocks
+  with the new slot (refcounted, no copy; csrc/engine.hip copy_slot) and only the remainder is
+  prefilled (the autonomy loop resends the tool catalogue and format rules every round, with up
+  to 3 concurrent loops, SURVEY §6.1);
+* chunked prefill interleaved with decode: while sequences are decoding, a new prompt is
+  prefilled AIOS_PREFILL_CHUNK tokens (default 512) per scheduler iteration between batched
+  decode steps, so a 3k-token admission does not stall every running stream for its whole
+  prefill; with nothing decoding the prompt goes through in one call;
+* each iteration runs ONE batched decode step (hipGraph replay) for every decoding sequence, so
   concurrent agents/reasoning loops share each weight pass;
 * JSON mode (the reference's `response_format: json_object`) builds the allowed-token mask per
   row with the native JsonGrammar and the device sampler applies it; generation stops as soon as
@@ -22,6 +28,7 @@ from __future__ import annotations
 import collections
 import dataclasses
 import logging
+import os
 import threading
 import time
 from typing import Callable, Deque, Dict, List, Optional
@@ -64,17 +71,18 @@ class GenResult:
 
 
 class _Seq:
-    __slots__ = ("req", "slot", "pos", "last", "out", "grammar_state", "emitted", "t_first", "cached")
+    __slots__ = ("req", "slot", "pos", "last", "out", "grammar_state", "emitted", "t_first", "cached", "todo")
 
     def __init__(self, req, slot):
         self.req, self.slot = req, slot
-        self.pos = 0
+        self.pos = 0                 # next position to write (prefill cursor, then decode position)
         self.last = 0
         self.out: List[int] = []
         self.grammar_state = None
         self.emitted = ""
         self.t_first = 0.0
         self.cached = 0
+        self.todo: List[int] = []    # prompt tokens still to prefill
 
 
 class Scheduler:
@@ -94,7 +102,11 @@ class Scheduler:
         self.slot_cache: Dict[int, List[int]] = {s: [] for s in range(max_slots)}
         self.free_slots = list(range(max_slots))
         self.queue: Deque[GenRequest] = collections.deque()
-        self.active: List[_Seq] = []
+        self.active: List[_Seq] = []          # decoding
+        self.prefilling: List[_Seq] = []      # admitted, prompt not fully prefilled yet
+        self.prefill_chunk = int(os.environ.get("AIOS_PREFILL_CHUNK", "512"))
+        self.share_prefix = hasattr(engine, "copy_slot")
+        self.min_shared_prefix = int(os.environ.get("AIOS_MIN_SHARED_PREFIX", "128"))
         self.cv = threading.Condition()
         self.stop_flag = False
         self.stats = dict(requests=0, tokens=0, prefill_tokens=0, cached_tokens=0, steps=0, batch_sum=0, errors=0)
@@ -123,23 +135,24 @@ class Scheduler:
 
     @property
     def load(self) -> int:
-        return len(self.queue) + len(self.active)
+        return len(self.queue) + len(self.active) + len(self.prefilling)
 
     # ------------------------------------------------------------------ worker
     def _run(self):
         while True:
             with self.cv:
-                while not self.stop_flag and not self.queue and not self.active:
+                while not self.stop_flag and not self.queue and not self.active and not self.prefilling:
                     self.cv.wait(timeout=1.0)
                 if self.stop_flag:
-                    for s in self.active:
+                    for s in list(self.active) + list(self.prefilling):
                         self._finish(s, "cancelled")
                     while self.queue:
                         r = self.queue.popleft()
                         self._done(r, GenResult("", [], len(r.prompt_ids), 0, "cancelled"))
                     return
                 admit = []
-                while self.queue and self.free_slots and len(self.active) + len(admit) < self.max_batch:
+                while (self.queue and self.free_slots and
+                       len(self.active) + len(self.prefilling) + len(admit) < self.max_batch):
                     admit.append(self.queue.popleft())
             for r in admit:
                 try:
@@ -151,6 +164,17 @@ class Scheduler:
                     log.exception("admission failed")
                     self._engine_failed(e)
                     self._done(r, GenResult("", [], len(r.prompt_ids), 0, "error", error=str(e)))
+            if self.prefilling:
+                seq = self.prefilling[0]
+                try:
+                    self._prefill_chunk(seq)
+                    self.last_progress = time.time()
+                except ValueError as e:
+                    self._finish(seq, "error", str(e))
+                except Exception as e:  # noqa: BLE001
+                    log.exception("prefill failed")
+                    self._engine_failed(e)
+                    self._finish(seq, "error", str(e))
             if self.active:
                 try:
                     t0 = time.time()
@@ -163,17 +187,37 @@ class Scheduler:
                     for s in list(self.active):
                         self._finish(s, "error", str(e))
 
+    @staticmethod
+    def _common(c: List[int], ids: List[int]) -> int:
+        n, lim = 0, min(len(c), len(ids) - 1)  # >= 1 token is always prefilled (its logits)
+        while n < lim and c[n] == ids[n]:
+            n += 1
+        return n
+
     def _pick_slot(self, ids: List[int]):
+        """(slot, reused tokens): the free slot whose own cache matches best, or -- when another
+        slot (free or decoding) holds a longer matching prefix -- the free slot with the least
+        cached content, which then shares that prefix through the paged KV."""
         best, best_len = None, -1
         for s in self.free_slots:
-            c = self.slot_cache[s]
-            n = 0
-            lim = min(len(c), len(ids) - 1)
-            while n < lim and c[n] == ids[n]:
-                n += 1
+            n = self._common(self.slot_cache[s], ids)
             if n > best_len:
                 best, best_len = s, n
-        return best, max(best_len, 0)
+        best_len = max(best_len, 0)
+        if self.share_prefix:
+            src, src_len = None, best_len
+            for s, c in self.slot_cache.items():
+                if s != best:
+                    n = self._common(c, ids)
+                    if n > src_len:
+                        src, src_len = s, n
+            if src is not None and src_len >= best_len + self.min_shared_prefix:
+                dst = min(self.free_slots, key=lambda f: len(self.slot_cache[f]))
+                self.engine.copy_slot(src, dst, src_len)
+                self.slot_cache[dst] = list(ids[:src_len])
+                self.stats["shared_prefix_tokens"] = self.stats.get("shared_prefix_tokens", 0) + src_len
+                return dst, src_len
+        return best, best_len
 
     def _admit(self, r: GenRequest):
         ids = r.prompt_ids
@@ -184,12 +228,37 @@ class Scheduler:
         self.free_slots.remove(slot)
         seq = _Seq(r, slot)
         seq.cached = common
+        seq.pos = common
+        seq.todo = list(ids[common:])
         self.slot_cache[slot] = list(ids[:common])
-        logits = self.engine.prefill(slot, ids[common:], common, True)
-        self.stats["prefill_tokens"] += len(ids) - common
         self.stats["cached_tokens"] += common
-        self.slot_cache[slot] = list(ids)
-        seq.pos = len(ids)
+        self.prefilling.append(seq)
+        if not self.active:  # nothing decoding: no stream to protect, prefill it right away
+            try:
+                self._prefill_chunk(seq, whole=True)
+            except Exception:
+                if seq in self.prefilling:  # the caller reports the error; the slot goes back
+                    self.prefilling.remove(seq)
+                    self.free_slots.append(slot)
+                raise
+
+    def _prefill_chunk(self, seq: _Seq, whole: bool = False):
+        """Prefill the next chunk of seq's prompt; the last chunk samples the first token and
+        moves the sequence to the decoding set."""
+        r = seq.req
+        if r.cancelled:
+            self._finish(seq, "cancelled")
+            return
+        n = len(seq.todo) if (whole or not self.active) else min(len(seq.todo), max(1, self.prefill_chunk))
+        chunk, last = seq.todo[:n], n == len(seq.todo)
+        logits = self.engine.prefill(seq.slot, chunk, seq.pos, last)
+        seq.todo = seq.todo[n:]
+        seq.pos += n
+        self.slot_cache[seq.slot].extend(chunk)
+        self.stats["prefill_tokens"] += n
+        if not last:
+            return
+        self.prefilling.remove(seq)
         mask = None
         if r.json_mode and self.grammar is not None:
             seq.grammar_state = self.grammar.initial()
@@ -270,7 +339,8 @@ class Scheduler:
             full = host_sampler.all_allowed(self.vocab)
             mask = b"".join(self.grammar.mask(s.grammar_state) if s.grammar_state is not None else full
                             for s in self.active)
-        out = self.engine.decode(slots, toks, pos, temps, topk, seed, mask)
+        topp = [float(s.req.top_p) if 0.0 < s.req.top_p < 1.0 else 1.0 for s in self.active]
+        out = self.engine.decode(slots, toks, pos, temps, topk, seed, mask, topp)
         self.stats["steps"] += 1
         self.stats["batch_sum"] += B
         for s, t in zip(list(self.active), out):
@@ -281,6 +351,8 @@ class Scheduler:
     def _finish(self, seq: _Seq, reason: str, error: str = ""):
         if seq in self.active:
             self.active.remove(seq)
+        if seq in self.prefilling:
+            self.prefilling.remove(seq)
         self.free_slots.append(seq.slot)
         r = seq.req
         text = self.tok.decode(seq.out)

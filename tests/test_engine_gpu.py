@@ -177,3 +177,46 @@ def test_prefill_one_chunk_matches_reference(model_files, recipe):
     eng, cfg = _load(path)
     got = torch.from_numpy(np.asarray(eng.prefill(0, prompt, 0, True)))
     assert (got - rl).abs().max().item() < 2e-2 * scale
+
+
+@pytest.mark.parametrize("gemm_prefill", ["0", "1"])
+def test_paged_kv_prefix_sharing_and_copy_on_write(model_files, monkeypatch, gemm_prefill):
+    """Paged KV: slot 1 inherits slot 0's first 300 tokens (two full 128-token blocks shared by
+    reference, the partial third block copied), prefills only its own suffix, and its logits and
+    greedy continuation equal a fresh full prefill of the same prompt in slot 2.  Then slot 0 is
+    re-prefilled from position 100 -- inside a shared block -- which must un-share (copy-on-write)
+    instead of corrupting slot 1."""
+    monkeypatch.setenv("AIOS_PREFILL_GEMM", gemm_prefill)
+    path = model_files["mistral_shape"]
+    from aios_amd.runtime.loader import load_engine
+
+    eng, cfg, _ = load_engine(path, max_ctx=512, max_slots=4, max_batch=2, act_q8=False)
+    rng = np.random.default_rng(11)
+    a = [1] + [int(t) for t in rng.integers(3, 900, 399)]
+    b = a[:300] + [int(t) for t in rng.integers(3, 900, 60)]
+    total = eng.kv_blocks_total
+    eng.prefill(0, a, 0, False)
+    assert eng.kv_blocks_free == total - 4  # 400 tokens -> 4 blocks
+    eng.copy_slot(0, 1, 300)
+    t0, t1 = eng.block_table(0), eng.block_table(1)
+    assert t1[:2] == t0[:2] and t1[2] not in t0 and t1[3] == -1
+    lb = np.asarray(eng.prefill(1, b[300:], 300, True))
+    lf = np.asarray(eng.prefill(2, b, 0, True))
+    scale = max(np.abs(lf).max(), 1.0)
+    assert np.abs(lb - lf).max() < 2e-2 * scale
+    # greedy continuation of the shared-prefix slot and the fresh slot, batched in one step
+    nb = int(np.argmax(lb))
+    toks = eng.decode([1, 2], [nb, nb], [len(b), len(b)])
+    l2 = np.asarray(eng.last_logits(2)).reshape(2, -1)
+    assert np.abs(l2[0] - l2[1]).max() < 2e-2 * scale
+    # copy-on-write: rewriting slot 0 from position 100 must not touch slot 1's shared blocks
+    c = a[:100] + [int(t) for t in rng.integers(3, 900, 50)]
+    eng.prefill(0, c[100:], 100, False)
+    assert eng.block_table(0)[0] != eng.block_table(1)[0]
+    eng.decode([1, 2], [int(toks[0]), int(toks[1])], [len(b) + 1, len(b) + 1])
+    l3 = np.asarray(eng.last_logits(2)).reshape(2, -1)
+    assert np.abs(l3[0] - l3[1]).max() < 2e-2 * scale
+    eng.release_slot(0)
+    eng.release_slot(1)
+    eng.release_slot(2)
+    assert eng.kv_blocks_free == total

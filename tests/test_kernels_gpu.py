@@ -12,6 +12,31 @@ pytestmark = pytest.mark.gpu
 QTS = [GGMLType.Q4_K, GGMLType.Q6_K, GGMLType.Q5_K, GGMLType.Q4_0, GGMLType.Q8_0, GGMLType.F16, GGMLType.BF16]
 
 
+KVB = 128  # paged KV block (E.KV_BLOCK)
+
+
+def paged_cache(x, shuffle=False, seed=0):
+    """Logical KV [S, Hkv, C, hd] -> (physical pool [S*C/KVB, Hkv, KVB, hd], block table [S, C/KVB] or
+    None for the identity map).  shuffle scatters the logical blocks over a random permutation."""
+    S, Hk, C, D = x.shape
+    nb = C // KVB
+    blocks = x.reshape(S, Hk, nb, KVB, D).permute(0, 2, 1, 3, 4).reshape(S * nb, Hk, KVB, D)
+    if not shuffle:
+        return blocks.contiguous(), None
+    perm = torch.randperm(S * nb, generator=torch.Generator().manual_seed(seed))
+    phys = torch.empty_like(blocks)
+    phys[perm] = blocks
+    return phys.contiguous(), perm.view(S, nb).to(torch.int32)
+
+
+def unpaged(phys, S, C, bt=None):
+    """Inverse of paged_cache: physical pool (+ table) -> logical [S, Hkv, C, hd]."""
+    nb = C // KVB
+    blocks = phys if bt is None else phys[bt.reshape(-1).long().to(phys.device)]
+    Hk, D = phys.shape[1], phys.shape[3]
+    return blocks.reshape(S, nb, Hk, KVB, D).permute(0, 2, 1, 3, 4).reshape(S, Hk, C, D)
+
+
 @pytest.fixture(scope="module")
 def E():
     from aios_amd.runtime import native
@@ -152,12 +177,15 @@ def test_gemv_qkv_rope_kv(E, mixed, q8):
     nw = torch.rand(d, device="cuda") + 0.5
     pos = torch.tensor([5, 17, 100], dtype=torch.int32, device="cuda")
     slot = torch.tensor([2, 0, 1], dtype=torch.int32, device="cuda")
-    kc = torch.zeros(slots, Hkv, max_ctx, hd, dtype=torch.bfloat16, device="cuda")
-    vc = torch.zeros_like(kc)
+    kp, bt = paged_cache(torch.zeros(slots, Hkv, max_ctx, hd, dtype=torch.bfloat16), shuffle=True, seed=3)
+    kp, bt = kp.cuda(), bt.cuda()
+    vp = torch.zeros_like(kp)
     q = torch.zeros(B, H * hd, device="cuda")
     E.gemv_qkv([wq, wk, wv], B, x.data_ptr(), d, nw.data_ptr(), 1e-5, q.data_ptr(), 0, hd, H, Hkv, max_ctx, 0,
-               10000.0, pos.data_ptr(), slot.data_ptr(), kc.data_ptr(), vc.data_ptr(), stream(), q8)
+               10000.0, pos.data_ptr(), slot.data_ptr(), kp.data_ptr(), vp.data_ptr(), stream(), q8,
+               block_table=bt.data_ptr())
     torch.cuda.synchronize()
+    kc, vc = unpaged(kp, slots, max_ctx, bt), unpaged(vp, slots, max_ctx, bt)
     xc = x.cpu()
     xn = xc * torch.rsqrt((xc * xc).mean(-1, keepdim=True) + 1e-5) * nw.cpu()
     if q8:
@@ -178,11 +206,20 @@ def test_gemv_qkv_rope_kv(E, mixed, q8):
                                           # several 512-key splits: exercises the cross-workgroup combine
                                           ([1500, 513, 512, 2048], 2048), ([1025, 3], 1280)])
 @pytest.mark.parametrize("split", [0, 64, 192])  # 0 = the launcher's choice
-def test_attention_decode(E, hd, H, Hkv, lens, max_ctx, split):
+@pytest.mark.parametrize("paging", ["identity", "slot_table", "row_table"])
+def test_attention_decode(E, hd, H, Hkv, lens, max_ctx, split, paging):
     B = len(lens)
     slots = B + 1
-    kc = (torch.randn(slots, Hkv, max_ctx, hd) * 0.5).to(torch.bfloat16).cuda()
-    vc = torch.randn(slots, Hkv, max_ctx, hd).to(torch.bfloat16).cuda()
+    kc = (torch.randn(slots, Hkv, max_ctx, hd) * 0.5).to(torch.bfloat16)
+    vc = torch.randn(slots, Hkv, max_ctx, hd).to(torch.bfloat16)
+    kp, bt = paged_cache(kc, shuffle=paging != "identity", seed=11)
+    vp, _ = paged_cache(vc, shuffle=paging != "identity", seed=11)
+    kp, vp = kp.cuda(), vp.cuda()
+    bt_rows = 0
+    if paging == "row_table":  # table indexed by batch row (the engine's decode rows)
+        bt = torch.stack([bt[b + 1] for b in range(B)])
+        bt_rows = 1
+    bt_dev = bt.cuda() if bt is not None else None
     q = torch.randn(B, H, hd, device="cuda")
     seq = torch.tensor(lens, dtype=torch.int32, device="cuda")
     slot = torch.tensor(list(range(1, B + 1)), dtype=torch.int32, device="cuda")
@@ -194,9 +231,9 @@ def test_attention_decode(E, hd, H, Hkv, lens, max_ctx, split):
     scale = 1 / math.sqrt(hd)
     for _ in range(2):  # second launch checks the counters re-armed themselves
         out.zero_()
-        E.attn_decode(q.data_ptr(), kc.data_ptr(), vc.data_ptr(), seq.data_ptr(), slot.data_ptr(), B, H, Hkv, hd,
+        E.attn_decode(q.data_ptr(), kp.data_ptr(), vp.data_ptr(), seq.data_ptr(), slot.data_ptr(), B, H, Hkv, hd,
                       max_ctx, nch, scale, opart.data_ptr(), ml.data_ptr(), out.data_ptr(), cnt.data_ptr(), stream(),
-                      split)
+                      split, bt_dev.data_ptr() if bt_dev is not None else 0, bt_rows)
     torch.cuda.synchronize()
     assert int(cnt.abs().sum()) == 0
     G = H // Hkv
@@ -232,17 +269,18 @@ def test_rmsnorm(E):
 
 @pytest.mark.parametrize("neox", [0, 1])
 def test_qkv_post_qknorm(E, neox):
-    T, H, Hkv, hd, max_ctx = 4, 4, 2, 128, 64
+    T, H, Hkv, hd, max_ctx = 4, 4, 2, 128, 128
     qkv = torch.randn(T, (H + 2 * Hkv) * hd, device="cuda")
     qn = torch.rand(hd, device="cuda") + 0.5
     kn = torch.rand(hd, device="cuda") + 0.5
     pos = torch.tensor([0, 1, 9, 33], dtype=torch.int32, device="cuda")
-    kc = torch.zeros(1, Hkv, max_ctx, hd, dtype=torch.bfloat16, device="cuda")
-    vc = torch.zeros_like(kc)
+    kp = torch.zeros(max_ctx // KVB, Hkv, KVB, hd, dtype=torch.bfloat16, device="cuda")
+    vp = torch.zeros_like(kp)
     q = torch.empty(T, H * hd, device="cuda")
     E.qkv_post(qkv.data_ptr(), qkv.shape[1], T, H, Hkv, hd, qn.data_ptr(), kn.data_ptr(), 1e-6, neox, 1e6,
-               pos.data_ptr(), 0, q.data_ptr(), kc.data_ptr(), vc.data_ptr(), max_ctx, stream())
+               pos.data_ptr(), 0, q.data_ptr(), kp.data_ptr(), vp.data_ptr(), max_ctx, stream())
     torch.cuda.synchronize()
+    kc = unpaged(kp, 1, max_ctx)
     c = qkv.cpu()
     rms = lambda x, w: x * torch.rsqrt((x * x).mean(-1, keepdim=True) + 1e-6) * w
     qr = rope_ref(rms(c[:, :H * hd].view(T, H, hd), qn.cpu()), pos.cpu(), 1e6, bool(neox))
@@ -286,6 +324,64 @@ def test_sample_temperature_topk_distribution(E):
     assert set(counts) <= {3, 7}
     p3 = counts.get(3, 0) / 400
     assert abs(p3 - math.e / (math.e + 1)) < 0.08
+
+
+@pytest.mark.parametrize("V", [1000, 32000, 128256])
+def test_sample_greedy_multi_slice(E, V):
+    """Greedy argmax through the two-phase sampler (V/4096 slice workgroups + last-arriver merge),
+    repeated to check the per-row tickets re-arm."""
+    B = 5
+    logits = torch.randn(B, V, device="cuda")
+    logits[1, V - 1] = 50.0  # winner in the last (partial) slice
+    logits[2, 0] = 50.0
+    tok = torch.zeros(B, dtype=torch.int32, device="cuda")
+    for _ in range(3):
+        tok.zero_()
+        E.sample(logits.data_ptr(), V, B, V, 0, 0, 0, tok.data_ptr(), 0, 0, stream())
+        torch.cuda.synchronize()
+        assert torch.equal(tok.cpu().long(), logits.argmax(-1).cpu())
+
+
+@pytest.mark.parametrize("top_k,top_p,V", [(0, 0.7, 32000), (3, 0.9, 32000), (4, 1.0, 128256), (0, 1.0, 5000)])
+def test_sample_topk_topp_distribution(E, top_k, top_p, V):
+    """Empirical distribution of the device sampler (B rows = independent RNG streams) against
+    the host sampler's exact top-k -> softmax -> nucleus distribution."""
+    B = 512
+    base = torch.full((V,), -30.0)
+    idx = [5, 4097, 9000 % V, 20001 % V, V - 2]
+    for j, i in enumerate(idx):
+        base[i] = 1.0 - 0.5 * j
+    logits = base.repeat(B, 1).cuda()
+    temp = torch.full((B,), 0.8, device="cuda")
+    tk = torch.full((B,), top_k, dtype=torch.int32, device="cuda")
+    tp = torch.full((B,), top_p, device="cuda")
+    pos = torch.arange(B, dtype=torch.int32, device="cuda")
+    tok = torch.zeros(B, dtype=torch.int32, device="cuda")
+    counts = {}
+    for rep in range(8):
+        E.sample(logits.data_ptr(), V, B, V, temp.data_ptr(), tk.data_ptr(), 77 + rep, tok.data_ptr(), pos.data_ptr(),
+                 0, stream(), tp.data_ptr())
+        torch.cuda.synchronize()
+        for t in tok.cpu().tolist():
+            counts[t] = counts.get(t, 0) + 1
+    # exact distribution
+    l = base.double() / 0.8
+    if top_k:
+        kth = torch.topk(l, top_k).values[-1]
+        l[l < kth] = -float("inf")
+    p = torch.softmax(l, 0)
+    if top_p < 1.0:
+        order = torch.argsort(-p)
+        cum = torch.cumsum(p[order], 0)
+        before = cum - p[order]
+        drop = order[before >= top_p]
+        p[drop] = 0
+        p /= p.sum()
+    n = sum(counts.values())
+    allowed = set(torch.nonzero(p > 1e-9).flatten().tolist())
+    assert set(counts) <= allowed, (set(counts) - allowed)
+    for i in allowed:
+        assert abs(counts.get(i, 0) / n - float(p[i])) < 0.04, (i, counts.get(i, 0) / n, float(p[i]))
 
 
 @pytest.mark.parametrize("t", QTS)
@@ -355,17 +451,22 @@ def test_gemm_q_swiglu_epilogue(E, M):
 
 @pytest.mark.parametrize("H,Hkv,hd", [(32, 8, 128), (32, 4, 64), (8, 8, 64), (16, 8, 128), (64, 8, 128)])
 @pytest.mark.parametrize("start,T", [(0, 1), (0, 37), (70, 130), (0, 300)])
-def test_attention_prefill_causal(E, H, Hkv, hd, start, T):
+@pytest.mark.parametrize("shuffle", [False, True])
+def test_attention_prefill_causal(E, H, Hkv, hd, start, T, shuffle):
     max_ctx = 512
     slot, slots = 1, 2
     G = H // Hkv
-    kc = (torch.randn(slots, Hkv, max_ctx, hd) * 0.5).to(torch.bfloat16).cuda()
-    vc = torch.randn(slots, Hkv, max_ctx, hd).to(torch.bfloat16).cuda()
+    kc = (torch.randn(slots, Hkv, max_ctx, hd) * 0.5).to(torch.bfloat16)
+    vc = torch.randn(slots, Hkv, max_ctx, hd).to(torch.bfloat16)
+    kp, bt = paged_cache(kc, shuffle, seed=5)
+    vp, _ = paged_cache(vc, shuffle, seed=5)
+    kp, vp = kp.cuda(), vp.cuda()
+    bt_dev = bt.cuda() if bt is not None else None
     q = torch.randn(T, H, hd, device="cuda")
     out = torch.zeros(T, H * hd, dtype=torch.bfloat16, device="cuda")
     scale = 1 / math.sqrt(hd)
-    E.attn_prefill(q.data_ptr(), kc.data_ptr(), vc.data_ptr(), slot, start, T, H, Hkv, hd, max_ctx, scale,
-                   out.data_ptr(), H * hd, stream())
+    E.attn_prefill(q.data_ptr(), kp.data_ptr(), vp.data_ptr(), slot, start, T, H, Hkv, hd, max_ctx, scale,
+                   out.data_ptr(), H * hd, stream(), bt_dev.data_ptr() if bt_dev is not None else 0)
     torch.cuda.synchronize()
     L = start + T
     k = kc[slot, :, :L].float().cpu().repeat_interleave(G, 0)  # [H, L, hd]
