@@ -26,6 +26,7 @@ from typing import List, Optional
 
 from ..rpc.schema import pb
 from .clients import InferResult
+from .remote import RemoteExecutor, find_node, tools_address_of
 from .state import LEVEL_ROUNDS, LEVEL_TOKENS, OrchestratorState, core
 
 log = logging.getLogger("aios.autonomy")
@@ -68,6 +69,8 @@ class AutonomyLoop:
         self.st = state
         self.tick_s = tick_s
         self.sem = asyncio.Semaphore(MAX_PARALLEL_AI)
+        self.remote = RemoteExecutor()
+        self._lost: set = set()  # agents already reported lost (agent_lost events fire once)
         self.bg: set = set()
         self.ticks = 0
 
@@ -146,21 +149,16 @@ class AutonomyLoop:
         t.add_done_callback(self.bg.discard)
 
     async def _remote(self, task: dict, node_id: str) -> bool:
-        nodes = {n["node_id"]: n for n in self.st.cluster.list(False)}
-        n = nodes.get(node_id)
+        n = find_node(self.st.cluster, node_id)
         if not n:
             return False
-        from ..rpc.client import Stub, channel
-
         try:
-            r = await Stub(channel(n["address"]), "aios.orchestrator.Orchestrator").SubmitGoal(
-                pb.orchestrator.SubmitGoalRequest(description=task["description"], priority=5,
-                                                  source=f"cluster:{task['id']}"), timeout=10)
+            rid = await self.remote.submit_remote_goal(n["address"], task["description"], 5, f"cluster:{task['id']}")
         except Exception as e:
             log.warning("remote dispatch of %s to %s failed: %s", task["id"], node_id, e)
             return False
         self._mark(task, "completed", completed_at=int(time.time()),
-                   output_json=json.dumps({"remote_node": node_id, "remote_goal_id": r.id}))
+                   output_json=json.dumps({"remote_node": node_id, "remote_goal_id": rid}))
         self.st.decisions.log("task_routing", [node_id], "cluster_dispatch",
                               f"Task {task['id']} routed to remote cluster node", task.get("intelligence_level", ""),
                               "cluster")
@@ -192,10 +190,37 @@ class AutonomyLoop:
     async def run_tools(self, task_id: str, calls: List[dict]):
         results, ok = [], True
         for c in calls:
-            r = await self.st.clients.execute_tool(c["tool"], c.get("input", {}), task_id)
+            node = c.get("node") or ""
+            if node and node != self.st.node_id:
+                r = await self.run_remote_tool(task_id, c, node)
+            else:
+                r = await self.st.clients.execute_tool(c["tool"], c.get("input", {}), task_id)
             ok = ok and r["success"]
             results.append(r)
         return results, ok
+
+    async def run_remote_tool(self, task_id: str, call: dict, node_id: str) -> dict:
+        """A tool call addressed to another cluster node runs on that node's tool service."""
+        tool = call["tool"]
+        n = find_node(self.st.cluster, node_id)
+        if n is None:
+            return {"tool": tool, "success": False, "node": node_id,
+                    "error": f"Remote node '{node_id}' is not registered or not healthy"}
+        data = json.dumps(call.get("input") or {}).encode()
+        try:
+            ok, out, err = await self.remote.execute_remote_tool(tools_address_of(n), tool, "autonomy-loop",
+                                                                 task_id, data)
+        except Exception as e:  # noqa: BLE001 - unreachable node: a failed tool call, not a crash
+            return {"tool": tool, "success": False, "node": node_id, "error": f"Remote tool execution failed: {e}"}
+        self.st.decisions.log("tool_routing", [node_id], "remote_tool", f"Tool {tool} for task {task_id} executed on "
+                              f"cluster node {node_id}", "", "cluster")
+        if not ok:
+            return {"tool": tool, "success": False, "node": node_id, "error": f"Tool '{tool}' failed on {node_id}: {err}"}
+        try:
+            parsed = json.loads(out) if out else {}
+        except ValueError:
+            parsed = out.decode("utf-8", "replace")
+        return {"tool": tool, "success": True, "node": node_id, "output": parsed}
 
     async def ai_call(self, task: dict, prompt_body: str, provider: str) -> AiResult:
         """execute_ai_task (autonomy.rs:823-983): system prompt + memory context + conversation +
@@ -351,14 +376,22 @@ class AutonomyLoop:
     def housekeeping(self):
         st = self.st
         ge = st.goal_engine
+        dead_now = set()
         for dead in st.router.dead_agents():
+            dead_now.add(dead["agent_id"])
+            if dead["agent_id"] not in self._lost:
+                st.emit("agent_lost", dead["agent_id"], {"task_id": dead["task_id"]}, "warning")
             if dead["task_id"]:
                 log.warning("agent %s is dead with task %s assigned — re-queuing", dead["agent_id"], dead["task_id"])
                 st.router.task_completed(dead["agent_id"], False)
                 ge.update_task({"id": dead["task_id"], "status": "pending", "assigned_agent": ""})
+        self._lost = dead_now
         goals, _ = ge.list("in_progress", 100, 0)
         for g in goals:
             ns = ge.check_completion(g["id"])
+            if ns:
+                st.emit(f"goal_{ns}", g["id"], {"goal_id": g["id"], "description": g["description"]},
+                        "warning" if ns == "failed" else "info")
             if ns == "completed":
                 log.info("goal %s completed", g["id"])
                 st.decisions.log("goal_completion", [g["id"]], "completed",

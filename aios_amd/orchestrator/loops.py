@@ -54,10 +54,12 @@ class ServiceHealth:
 
 class HealthChecker:
     def __init__(self, services: Optional[Dict[str, str]] = None, interval: float = 10.0, timeout: float = 2.0,
-                 grace: float = 60.0):
+                 grace: float = 60.0, on_change=None):
         names = services or {n: addr(n) for n in ("runtime", "tools", "memory", "api-gateway")}
         self.services = {n: ServiceHealth(n, a) for n, a in names.items()}
         self.interval, self.timeout, self.grace = interval, timeout, grace
+        self.on_change = on_change  # (service, healthy_now, ServiceHealth) on every transition
+        self._seen: Dict[str, bool] = {}
 
     async def _probe(self, s: ServiceHealth):
         host, _, port = s.address.rpartition(":")
@@ -78,6 +80,17 @@ class HealthChecker:
             s.consecutive_failures += 1
             if s.consecutive_failures <= 3:
                 log.warning("service %s health check failed (attempt %d)", s.name, s.consecutive_failures)
+        # transitions, debounced: down after 3 consecutive failed probes (also a service that never
+        # came up), up again on the first good probe after a reported down
+        was = self._seen.get(s.name)
+        now = True if s.healthy else (False if s.consecutive_failures >= 3 else was)
+        if now is not None and now != was:
+            self._seen[s.name] = now
+            if self.on_change is not None and (not now or was is False):
+                try:
+                    self.on_change(s.name, now, s)
+                except Exception:  # noqa: BLE001
+                    log.exception("health transition hook failed")
 
     async def check_all(self):
         await asyncio.gather(*(self._probe(s) for s in self.services.values()))
@@ -192,6 +205,8 @@ async def proactive_loop(st: OrchestratorState, stop: asyncio.Event, cfg: Option
         try:
             cands = await asyncio.get_running_loop().run_in_executor(None, proactive_candidates, st, cfg)
             for desc, prio in cands:
+                st.emit("proactive_trigger", "proactive", {"description": desc, "priority": prio},
+                        "critical" if prio >= 9 else "warning")
                 if has_similar_active_goal(st, desc):
                     continue
                 g = await st.submit_goal(desc, prio, "proactive")
@@ -235,7 +250,10 @@ class EventQueue:
             except asyncio.TimeoutError:
                 continue
             for goal in self.st.events.publish(ev):
-                g = await self.st.submit_goal(goal["description"], int(goal["priority"]), "event")
+                if has_similar_active_goal(self.st, goal["description"]):
+                    continue  # the same incident already has an open goal
+                g = await self.st.submit_goal(goal["description"], int(goal["priority"]),
+                                              f"event_bus:{ev.get('event_type', '')}")
                 log.info("event %s -> goal %s", ev.get("event_type"), g["id"])
 
 

@@ -27,7 +27,10 @@ log = logging.getLogger("aios.orchestrator")
 
 async def amain(args):
     st = OrchestratorState(args.data_dir or None)
-    st.health = HealthChecker(grace=args.health_grace)
+    st.health = HealthChecker(grace=args.health_grace, on_change=lambda name, up, s: st.emit(
+        "service_recovered" if up else "service_unhealthy", name,
+        {"address": s.address, "consecutive_failures": s.consecutive_failures}, "info" if up else "critical"))
+    st.install_default_subscriptions()
     svc = OrchestratorService(st)
     server = RpcServer(args.addr, {"aios.orchestrator.Orchestrator": svc})
     await server.start()

@@ -46,6 +46,9 @@ class ManagementConsole:
         r.add_get("/api/gpus", self.gpus)
         r.add_get("/api/decisions", self.decisions)
         r.add_get("/api/schedules", self.schedules)
+        r.add_get("/api/events", self.events)
+        r.add_post("/api/events", self.publish_event)
+        r.add_post("/api/events/subscriptions", self.subscribe_event)
         r.add_get("/api/metrics", self.metrics)
         r.add_get("/ws", self.ws)
         self.runner = None
@@ -162,6 +165,25 @@ class ManagementConsole:
 
     async def decisions(self, req):
         return web.json_response(self.st.decisions.recent(int(req.query.get("n", 50))))
+
+    async def events(self, req):
+        return web.json_response(self.st.events.recent(int(req.query.get("n", 50))))
+
+    async def publish_event(self, req):
+        """External producers (agents, scripts) push events into the bus."""
+        b = await req.json()
+        if not b.get("event_type"):
+            return web.json_response({"error": "event_type required"}, status=400)
+        ok = self.st.emit(b["event_type"], b.get("source", "api"), b.get("data") or {}, b.get("severity", "info"))
+        return web.json_response({"queued": ok})
+
+    async def subscribe_event(self, req):
+        b = await req.json()
+        if not b.get("event_pattern") or not b.get("goal_template"):
+            return web.json_response({"error": "event_pattern and goal_template required"}, status=400)
+        sid = self.st.events.subscribe(b["event_pattern"], b.get("min_severity", "info"), b["goal_template"],
+                                       int(b.get("priority", 5)))
+        return web.json_response({"subscription_id": sid})
 
     async def schedules(self, req):
         return web.json_response(self.st.schedules.list())

@@ -114,8 +114,12 @@ class OrchestratorService:
             st.goal_engine.update_task({"id": req.task_id, "status": "failed", "completed_at": now,
                                         "error": req.error})
             st.goal_engine.add_message(gid, "system", f"Task {req.task_id} failed: {req.error}")
+            st.emit("task_failed", t.get("assigned_agent") or "agent",
+                    {"task_id": req.task_id, "goal_id": gid, "error": req.error}, "warning")
         st.results.record(gid, to_dict(req))
-        st.goal_engine.check_completion(gid)
+        ns = st.goal_engine.check_completion(gid)
+        if ns:
+            st.emit(f"goal_{ns}", gid, {"goal_id": gid}, "warning" if ns == "failed" else "info")
         return C.Status(success=True, message=f"Result recorded for task {req.task_id}")
 
     # ------------------------------------------------------------------ capabilities

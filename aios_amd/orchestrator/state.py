@@ -43,6 +43,7 @@ class OrchestratorState:
         self.decisions = core.DecisionLog(10000)
         self.results = core.ResultAggregator()
         self.events = core.EventBus()
+        self.event_queue = None     # EventQueue (loops.py): producers publish through emit()
         self.clients = clients or ServiceClients(self.discovery)
         self.health = None          # HealthChecker (loops.py)
         self.inflight: Set[str] = set()
@@ -55,6 +56,33 @@ class OrchestratorState:
         resumed = self.goal_engine.resume_in_progress()
         if resumed:
             log.info("resumed %d in-progress tasks after restart", resumed)
+
+    # ------------------------------------------------------------------ events
+    def emit(self, event_type: str, source: str, data: Optional[dict] = None, severity: str = "info") -> bool:
+        """Publish a system event to the bus (event_bus.rs SystemEvent): the EventQueue matches it
+        against the subscriptions and turns matches into goals.  Producers: service health
+        transitions, lost agents, failed tasks, goal completion / failure, proactive triggers."""
+        ev = {"id": f"ev-{time.time_ns():x}", "event_type": event_type, "source": source,
+              "data": data or {}, "severity": severity, "timestamp": int(time.time())}
+        if self.event_queue is None:
+            self.events.publish(ev)  # recorded (recent events) even without a running queue
+            return False
+        return self.event_queue.publish(ev)
+
+    def install_default_subscriptions(self):
+        """Event -> goal rules on by default (AIOS_EVENT_SUBSCRIPTIONS=0 disables): a service that
+        stops answering and an agent that stops heartbeating become recovery goals right away,
+        instead of waiting for the proactive generator's next 60 s sweep."""
+        if os.environ.get("AIOS_EVENT_SUBSCRIPTIONS", "1") in ("0", "false", "no"):
+            return []
+        return [
+            self.events.subscribe("service_unhealthy", "critical",
+                                  "Service {source} stopped responding. Diagnose the failure, restart it and "
+                                  "verify it answers health checks.", 9),
+            self.events.subscribe("agent_lost", "warning",
+                                  "Agent {source} stopped sending heartbeats. Restart it, check its logs and "
+                                  "re-queue its work.", 8),
+        ]
 
     # ------------------------------------------------------------------ planning
     async def decompose(self, goal_id: str, description: str) -> List[dict]:

@@ -376,3 +376,96 @@ def test_gateway_router_selection_and_fallback():
     for i in range(3):
         asyncio.run(r.route(pb.api_gateway.ApiInferRequest(prompt=f"p{i}", preferred_provider="local")))
     assert len(r.cache) == 2
+
+
+# ------------------------------------------------------------------------------------ remote tools
+def test_remote_tool_execution_on_cluster_node(tmp_path):
+    """A tool call that names another cluster node runs on THAT node's tool service
+    (RemoteExecutor.execute_remote_tool, reference agent-core/src/remote_exec.rs:75-102); an
+    unknown node is a failed call, not a crash; goal forwarding uses the same executor."""
+    from aios_amd.orchestrator.autonomy import AutonomyLoop
+    from aios_amd.orchestrator.remote import tools_address_of
+    from aios_amd.tools.service import ToolRegistryService
+
+    async def go():
+        st, servers, addrs, local_tools = await _start(tmp_path)
+        class CountingTools(ToolRegistryService):
+            seen = []
+
+            async def Execute(self, req, ctx):
+                self.seen.append(req.input_json)
+                return await super().Execute(req, ctx)
+
+        remote_tools = CountingTools(str(tmp_path / "remote_tools"))
+        servers["remote_tools"] = await RpcServer("127.0.0.1:0", {"aios.tools.ToolRegistry": remote_tools}).start()
+        try:
+            st.cluster.register_node({"node_id": "worker-2", "hostname": "w2", "address": addrs["orchestrator"],
+                                      "metadata": {"tools_address": f"127.0.0.1:{servers['remote_tools'].port}"},
+                                      "max_tasks": 4})
+            assert tools_address_of({"address": "10.0.0.7:50051"}) == "10.0.0.7:50052"
+            loop = AutonomyLoop(st)
+            p_remote, p_local = tmp_path / "remote.txt", tmp_path / "local.txt"
+            calls = [{"tool": "fs.write", "input": {"path": str(p_remote), "content": "r"}, "node": "worker-2"},
+                     {"tool": "fs.write", "input": {"path": str(p_local), "content": "l"}}]
+            results, ok = await loop.run_tools("task-1", calls)
+            assert ok and p_remote.read_text() == "r" and p_local.read_text() == "l"
+            assert results[0]["node"] == "worker-2" and results[0]["success"]
+            # the remote node's tool service executed the first call only
+            assert len(remote_tools.seen) == 1 and b"remote.txt" in remote_tools.seen[0]
+            bad, ok2 = await loop.run_tools("task-2", [{"tool": "monitor.cpu", "input": {}, "node": "nope"}])
+            assert not ok2 and "not registered" in bad[0]["error"]
+            # cluster goal forwarding through the same executor (to this node's own orchestrator)
+            rid = await loop.remote.submit_remote_goal(addrs["orchestrator"], "forwarded goal", 5, "cluster:t")
+            assert rid
+        finally:
+            await _stop(servers)
+    run(go())
+
+
+# ------------------------------------------------------------------------------------ event bus
+def test_event_bus_producers_create_goals(tmp_path):
+    """Events now have producers: a service whose health probes fail 3 times emits
+    service_unhealthy (critical), which the default subscription turns into a recovery goal
+    (source event_bus:service_unhealthy); its recovery emits service_recovered; failed agent
+    tasks and goal completion are published too (reference bus: agent-core/src/event_bus.rs)."""
+    from aios_amd.orchestrator.loops import EventQueue, HealthChecker
+    from aios_amd.orchestrator.state import OrchestratorState
+
+    async def go():
+        st = OrchestratorState(str(tmp_path / "orch"), in_memory=True)
+        st.event_queue = EventQueue(st)
+        subs = st.install_default_subscriptions()
+        assert len(subs) == 2
+        stop = asyncio.Event()
+        runner = asyncio.ensure_future(st.event_queue.run(stop))
+        # a "service" on a port nobody listens on, then a real listener on the same port
+        import socket
+        s0 = socket.socket()
+        s0.bind(("127.0.0.1", 0))
+        port = s0.getsockname()[1]
+        s0.close()
+        hc = HealthChecker({"memory": f"127.0.0.1:{port}"}, timeout=0.5, grace=0,
+                           on_change=lambda n, up, s: st.emit("service_recovered" if up else "service_unhealthy", n,
+                                                              {"failures": s.consecutive_failures},
+                                                              "info" if up else "critical"))
+        for _ in range(3):
+            await hc.check_all()
+        srv = await asyncio.start_server(lambda r, w: w.close(), "127.0.0.1", port)
+        await hc.check_all()
+        srv.close()
+        st.emit("task_failed", "agent-x", {"task_id": "t1"}, "warning")
+        for _ in range(100):
+            goals, _ = st.goal_engine.list("", 50, 0)
+            if goals and st.event_queue.q.empty():
+                break
+            await asyncio.sleep(0.05)
+        await asyncio.sleep(0.1)
+        stop.set()
+        await runner
+        kinds = [e["event_type"] for e in st.events.recent(10)]
+        assert "service_unhealthy" in kinds and "service_recovered" in kinds and "task_failed" in kinds
+        assert kinds.count("service_unhealthy") == 1  # debounced: one event per outage
+        goals, _ = st.goal_engine.list("", 50, 0)
+        assert len(goals) == 1 and "memory" in goals[0]["description"]
+        assert goals[0]["source"] == "event_bus:service_unhealthy" and goals[0]["priority"] == 9
+    run(go())
