@@ -170,6 +170,10 @@ class Engine {
   int *d_topk_ = nullptr, *d_step_ = nullptr;
   float* d_temp_ = nullptr;
   float* d_topp_ = nullptr;
+  char* d_par_ = nullptr;          // per-step parameter block (seed, slot, token, pos, seq_len, top_k, T, top_p | masks)
+  char* h_par_ = nullptr;          // pinned mirror
+  int* h_tok_out_ = nullptr;       // pinned sampled tokens
+  size_t par_bytes_ = 0, par_mask_off_ = 0;
   void* sample_ws_ = nullptr;
   size_t sample_ws_bytes_ = 0;
   int* sample_cnt_ = nullptr;

@@ -73,6 +73,8 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
 Engine::~Engine() {
   for (auto& kv : graphs_) hipGraphExecDestroy(kv.second);
   for (void* p : allocs_) hipFree(p);
+  if (h_par_) hipHostFree(h_par_);
+  if (h_tok_out_) hipHostFree(h_tok_out_);
   if (stream_) hipStreamDestroy(stream_);
 }
 
@@ -420,10 +422,31 @@ void Engine::finalize() {
   opart_ = fbuf((size_t)Bm * H * n_chunks_ * hd);
   ml_ = fbuf((size_t)Bm * H * n_chunks_ * 2);
   logits_ = fbuf((size_t)Bm * V);
-  d_tokens_ = ibuf(Bm);
-  d_pos_ = ibuf(Bm);
-  d_seqlen_ = ibuf(Bm);
-  d_slot_ = ibuf(Bm);
+  {
+    // per-step decode parameters + grammar masks in ONE device block mirrored by a pinned host
+    // block: a scheduler decode() uploads all of them with a single async copy (round 1 issued 8
+    // pageable copies per step)
+    const size_t mb = (size_t)Bm * ((V + 7) / 8);
+    par_mask_off_ = align_up(8 + (size_t)Bm * 4 * 7, 256);
+    par_bytes_ = par_mask_off_ + mb;
+    d_par_ = (char*)dmalloc(par_bytes_);
+    ws += par_bytes_;
+    HIP_CHECK(hipHostMalloc(&h_par_, par_bytes_, hipHostMallocDefault));
+    HIP_CHECK(hipHostMalloc((void**)&h_tok_out_, (size_t)Bm * 4, hipHostMallocDefault));
+    std::memset(h_par_, 0, par_bytes_);
+    d_seed_ = (uint64_t*)d_par_;
+    d_slot_ = (int*)(d_par_ + 8);
+    d_tokens_ = d_slot_ + Bm;
+    d_pos_ = d_tokens_ + Bm;
+    d_seqlen_ = d_pos_ + Bm;
+    d_topk_ = d_seqlen_ + Bm;
+    d_temp_ = (float*)(d_topk_ + Bm);
+    d_topp_ = d_temp_ + Bm;
+    d_mask_ = (uint8_t*)(d_par_ + par_mask_off_);
+    float* htp = (float*)(h_par_ + 8) + 6 * (size_t)Bm;
+    for (int b = 0; b < Bm; ++b) htp[b] = 1.f;
+    HIP_CHECK(hipMemcpy(d_par_, h_par_, par_bytes_, hipMemcpyHostToDevice));
+  }
   d_bt_ = ibuf((size_t)cfg_.max_slots * kv_maxb_);
   d_row_bt_ = ibuf((size_t)Bm * kv_maxb_);
   {
@@ -433,23 +456,12 @@ void Engine::finalize() {
   }
   attn_bt_ = d_row_bt_;
   attn_bt_rows_ = 1;
-  d_topk_ = ibuf(Bm);
   d_step_ = ibuf(4);
-  d_seed_ = (uint64_t*)ibuf(2);
-  d_temp_ = fbuf(Bm);
-  HIP_CHECK(hipMemset(d_temp_, 0, Bm * 4));
-  d_topp_ = fbuf(Bm);
-  {
-    std::vector<float> ones(Bm, 1.f);
-    HIP_CHECK(hipMemcpy(d_topp_, ones.data(), Bm * 4, hipMemcpyHostToDevice));
-  }
   sample_ws_bytes_ = sample_ws_bytes(Bm, V);
   sample_ws_ = dmalloc(sample_ws_bytes_);
   ws += sample_ws_bytes_;
   sample_cnt_ = ibuf(Bm);
   d_history_ = ibuf((size_t)Bm * (cfg_.max_ctx + 1));
-  d_mask_ = (uint8_t*)dmalloc((size_t)Bm * ((V + 7) / 8));
-  ws += (size_t)Bm * ((V + 7) / 8);
   const int R = prefill_rows_;
   pf_x_ = fbuf((size_t)R * d);
   pf_q_ = fbuf((size_t)R * qd);
@@ -1039,33 +1051,33 @@ std::vector<int> Engine::decode(const std::vector<int>& slots, const std::vector
   }
   row_slots_ = slots;
   row_pos_ = pos;
-  std::vector<float> temps(B, 0.f);
-  std::vector<int> tks(B, 0);
-  for (int b = 0; b < B && b < (int)temperature.size(); ++b) temps[b] = temperature[b];
-  for (int b = 0; b < B && b < (int)top_k.size(); ++b) tks[b] = top_k[b];
-  HIP_CHECK(hipMemcpyAsync(d_slot_, slots.data(), B * 4, hipMemcpyHostToDevice, stream_));
-  HIP_CHECK(hipMemcpyAsync(d_tokens_, tokens.data(), B * 4, hipMemcpyHostToDevice, stream_));
-  HIP_CHECK(hipMemcpyAsync(d_pos_, pos.data(), B * 4, hipMemcpyHostToDevice, stream_));
-  HIP_CHECK(hipMemcpyAsync(d_seqlen_, sl.data(), B * 4, hipMemcpyHostToDevice, stream_));
-  HIP_CHECK(hipMemcpyAsync(d_temp_, temps.data(), B * 4, hipMemcpyHostToDevice, stream_));
-  HIP_CHECK(hipMemcpyAsync(d_topk_, tks.data(), B * 4, hipMemcpyHostToDevice, stream_));
-  std::vector<float> tps(B, 1.f);
-  for (int b = 0; b < B && b < (int)top_p.size(); ++b) tps[b] = top_p[b];
-  HIP_CHECK(hipMemcpyAsync(d_topp_, tps.data(), B * 4, hipMemcpyHostToDevice, stream_));
+  const int Bm = cfg_.max_batch;
   const size_t mbytes = (size_t)B * ((cfg_.vocab_size + 7) / 8);
   sample_mask_ = !mask.empty();
-  if (sample_mask_) {
-    if (mask.size() != mbytes) throw std::runtime_error("decode: mask size mismatch");
-    HIP_CHECK(hipMemcpyAsync(d_mask_, mask.data(), mbytes, hipMemcpyHostToDevice, stream_));
+  if (sample_mask_ && mask.size() != mbytes) throw std::runtime_error("decode: mask size mismatch");
+  // one pinned staging block -> one async copy (layout: see finalize)
+  *(uint64_t*)h_par_ = seed;  // device-resident seed: one captured graph per (B, masked) serves every request
+  int* hs = (int*)(h_par_ + 8);
+  int *ht = hs + Bm, *hp = ht + Bm, *hl = hp + Bm, *hk = hl + Bm;
+  float* hT = (float*)(hk + Bm);
+  float* hP = hT + Bm;
+  for (int b = 0; b < B; ++b) {
+    hs[b] = slots[b]; ht[b] = tokens[b]; hp[b] = pos[b]; hl[b] = sl[b];
+    hk[b] = b < (int)top_k.size() ? top_k[b] : 0;
+    hT[b] = b < (int)temperature.size() ? temperature[b] : 0.f;
+    hP[b] = b < (int)top_p.size() ? top_p[b] : 1.f;
   }
-  // the seed lives in device memory, so one captured graph per (B, masked) serves every request
-  HIP_CHECK(hipMemcpyAsync(d_seed_, &seed, 8, hipMemcpyHostToDevice, stream_));
+  size_t nbytes = (size_t)((char*)(hP + Bm) - h_par_);
+  if (sample_mask_) {
+    std::memcpy(h_par_ + par_mask_off_, mask.data(), mbytes);
+    nbytes = par_mask_off_ + mbytes;
+  }
+  HIP_CHECK(hipMemcpyAsync(d_par_, h_par_, nbytes, hipMemcpyHostToDevice, stream_));
   decode_loop_run(B, 1, true);
-  std::vector<int> out(B);
-  HIP_CHECK(hipMemcpyAsync(out.data(), d_tokens_, B * 4, hipMemcpyDeviceToHost, stream_));
+  HIP_CHECK(hipMemcpyAsync(h_tok_out_, d_tokens_, B * 4, hipMemcpyDeviceToHost, stream_));
   HIP_CHECK(hipStreamSynchronize(stream_));
   sample_mask_ = false;
-  return out;
+  return std::vector<int>(h_tok_out_, h_tok_out_ + B);
 }
 
 std::vector<int> Engine::resample(int B, const std::vector<float>& temperature, const std::vector<int>& top_k,

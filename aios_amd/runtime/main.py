@@ -101,7 +101,8 @@ async def amain(args):
     tp_env = cfg.tp_devices_env()
     if tp_env and "AIOS_TP_DEVICES" not in os.environ:
         os.environ["AIOS_TP_DEVICES"] = tp_env
-    mgr = ModelManager(device=args.device, max_batch=max_batch, max_slots=max_slots)
+    mgr = ModelManager(device=args.device, max_batch=max_batch, max_slots=max_slots,
+                       base_port=int(os.environ.get("AIOS_RUNTIME_BASE_PORT", "8080")))
     svc = AIRuntimeService(mgr, http=not args.no_http)
     server = RpcServer(args.addr, {"aios.runtime.AIRuntime": svc})
     await server.start()

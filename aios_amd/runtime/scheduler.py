@@ -71,7 +71,8 @@ class GenResult:
 
 
 class _Seq:
-    __slots__ = ("req", "slot", "pos", "last", "out", "grammar_state", "emitted", "t_first", "cached", "todo")
+    __slots__ = ("req", "slot", "pos", "last", "out", "grammar_state", "emitted", "t_first", "cached", "todo",
+                 "p_off", "r_off")
 
     def __init__(self, req, slot):
         self.req, self.slot = req, slot
@@ -83,6 +84,8 @@ class _Seq:
         self.t_first = 0.0
         self.cached = 0
         self.todo: List[int] = []    # prompt tokens still to prefill
+        self.p_off = 0               # incremental detokenization window [p_off, r_off) already emitted
+        self.r_off = 0
 
 
 class Scheduler:
@@ -105,6 +108,10 @@ class Scheduler:
         self.active: List[_Seq] = []          # decoding
         self.prefilling: List[_Seq] = []      # admitted, prompt not fully prefilled yet
         self.prefill_chunk = int(os.environ.get("AIOS_PREFILL_CHUNK", "512"))
+        self._full_mask = None
+        # host-side cost breakdown of the decode loop (bench_serving / HealthCheck)
+        self.timing = dict(mask_s=0.0, engine_decode_s=0.0, accept_s=0.0, prefill_s=0.0)
+        self.step_log: Deque = collections.deque(maxlen=4096)  # (end time, batch) per decode step
         self.share_prefix = hasattr(engine, "copy_slot")
         self.min_shared_prefix = int(os.environ.get("AIOS_MIN_SHARED_PREFIX", "128"))
         self.cv = threading.Condition()
@@ -251,7 +258,10 @@ class Scheduler:
             return
         n = len(seq.todo) if (whole or not self.active) else min(len(seq.todo), max(1, self.prefill_chunk))
         chunk, last = seq.todo[:n], n == len(seq.todo)
+        tp0 = time.perf_counter()
         logits = self.engine.prefill(seq.slot, chunk, seq.pos, last)
+        self.timing["prefill_s"] += time.perf_counter() - tp0
+        self.step_log.append((time.perf_counter(), -n))  # a prefill chunk between decode steps
         seq.todo = seq.todo[n:]
         seq.pos += n
         self.slot_cache[seq.slot].extend(chunk)
@@ -287,12 +297,15 @@ class Scheduler:
         self.stats["tokens"] += 1
         self._tok_times.append(time.time())
         if r.on_delta is not None:
-            text = self.tok.decode(seq.out)
-            if not text.endswith("�"):
-                delta = text[len(seq.emitted):]
-                if delta:
-                    seq.emitted = text
-                    r.on_delta(delta)
+            # incremental detokenization over a short window (decoding the whole output every
+            # token is O(n^2) per stream and dominated the host side of a step)
+            prev = self.tok.decode(seq.out[seq.p_off:seq.r_off])
+            text = self.tok.decode(seq.out[seq.p_off:])
+            if len(text) > len(prev) and not text.endswith("�"):
+                delta = text[len(prev):]
+                seq.emitted += delta
+                seq.p_off, seq.r_off = seq.r_off, len(seq.out)
+                r.on_delta(delta)
         if seq.grammar_state is not None and self.grammar.complete(seq.grammar_state):
             self._finish(seq, "grammar")
             return False
@@ -334,19 +347,29 @@ class Scheduler:
         temps = [float(s.req.temperature) for s in self.active]
         topk = [int(s.req.top_k) if s.req.temperature > 0 else 0 for s in self.active]
         seed = int(self.active[0].req.seed) & 0xFFFFFFFF
+        t0 = time.perf_counter()
         mask = b""
         if any(s.grammar_state is not None for s in self.active):
-            full = host_sampler.all_allowed(self.vocab)
-            mask = b"".join(self.grammar.mask(s.grammar_state) if s.grammar_state is not None else full
+            if self._full_mask is None:
+                self._full_mask = host_sampler.all_allowed(self.vocab)
+            mask = b"".join(self.grammar.mask(s.grammar_state) if s.grammar_state is not None else self._full_mask
                             for s in self.active)
         topp = [float(s.req.top_p) if 0.0 < s.req.top_p < 1.0 else 1.0 for s in self.active]
+        t1 = time.perf_counter()
         out = self.engine.decode(slots, toks, pos, temps, topk, seed, mask, topp)
+        t2 = time.perf_counter()
         self.stats["steps"] += 1
         self.stats["batch_sum"] += B
         for s, t in zip(list(self.active), out):
             s.pos += 1
             self.slot_cache[s.slot].append(s.last)
             self._accept(s, int(t))
+        t3 = time.perf_counter()
+        tm = self.timing
+        tm["mask_s"] += t1 - t0
+        tm["engine_decode_s"] += t2 - t1
+        tm["accept_s"] += t3 - t2
+        self.step_log.append((t3, B))
 
     def _finish(self, seq: _Seq, reason: str, error: str = ""):
         if seq in self.active:
@@ -356,7 +379,7 @@ class Scheduler:
         self.free_slots.append(seq.slot)
         r = seq.req
         text = self.tok.decode(seq.out)
-        if r.on_delta is not None and len(text) > len(seq.emitted):
+        if r.on_delta is not None and len(text) > len(seq.emitted) and text.startswith(seq.emitted):
             r.on_delta(text[len(seq.emitted):])
         now = time.time()
         if seq.t_first:

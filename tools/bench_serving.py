@@ -79,8 +79,16 @@ def main():
     run_round(2)  # warm-up: graphs captured, kernels loaded
     sched = m.scheduler
     st0 = dict(sched.stats)
+    tm0 = dict(sched.timing)
+    sched.step_log.clear()
     res, wall = run_round(args.streams)
     st1 = dict(sched.stats)
+    tm1 = dict(sched.timing)
+    log = list(sched.step_log)
+    # steady-state ITL: gaps between consecutive full-batch decode steps with no prefill chunk
+    # in between (admission-time gaps are in TTFT / itl_p50)
+    gaps = sorted((b[0] - a[0]) * 1e3 for a, b in zip(log, log[1:]) if a[1] > 0 and b[1] > 0)
+    steps_in_round = st1["steps"] - st0["steps"]
     errs = [r.error for r in res if r.finish_reason == "error"]
     if errs:
         raise SystemExit(f"requests failed: {errs[:2]}")
@@ -99,6 +107,16 @@ def main():
     eng.decode_loop_run(B, 32, True)
     eng.synchronize()
     step_ms = (time.time() - t) / 32 * 1e3
+    # the scheduler's engine call at the same batch: host upload + graph launch + token readback
+    toks_ = [5] * B
+    pos_ = [args.prompt + 40] * B
+    mask = m.grammar.mask(m.grammar.initial()) * B
+    for label, mk in (("engine_decode_call_ms", b""), ("engine_decode_call_masked_ms", mask)):
+        eng.decode(slots, toks_, pos_, [0.7] * B, [40] * B, 1, mk, [0.95] * B)
+        t = time.time()
+        for i in range(16):
+            eng.decode(slots, toks_, [p + i for p in pos_], [0.7] * B, [40] * B, 1, mk, [0.95] * B)
+        globals()[label] = (time.time() - t) / 16 * 1e3
 
     out = {
         "bench": "serving: concurrent JSON-mode streams sharing a prompt prefix",
@@ -108,7 +126,15 @@ def main():
         "json_mode": True,
         "ttft_p50_ms": round(ttft[len(ttft) // 2], 2), "ttft_p90_ms": round(ttft[int(len(ttft) * 0.9) - 1], 2),
         "itl_p50_ms": round(itl[len(itl) // 2], 3) if itl else None,
+        "steady_itl_p50_ms": round(gaps[len(gaps) // 2], 3) if gaps else None,
+        "steady_itl_over_step": round(gaps[len(gaps) // 2] / step_ms, 3) if gaps else None,
+        "host_breakdown_s": {k: round(tm1[k] - tm0[k], 4) for k in tm1},
         "decode_step_ms_same_batch": round(step_ms, 3),
+        "engine_decode_call_ms": round(globals()["engine_decode_call_ms"], 3),
+        "engine_decode_call_masked_ms": round(globals()["engine_decode_call_masked_ms"], 3),
+        "scheduler_engine_ms_per_step": round((tm1["engine_decode_s"] - tm0["engine_decode_s"]) * 1e3 /
+                                              max(1, steps_in_round), 3),
+        "decode_steps": steps_in_round,
         "itl_over_step": round(itl[len(itl) // 2] / step_ms, 3) if itl else None,
         "aggregate_tok_s": round(toks / wall, 1), "completion_tokens": toks, "wall_s": round(wall, 3),
         "prefill_tokens": st1["prefill_tokens"] - st0["prefill_tokens"],
