@@ -62,11 +62,12 @@ class TPEngine:
                           "decode_loop_run", "decode_loop_history", "synchronize", "reset_graphs", "copy_slot",
                           "release_slot"})
 
-    def __init__(self, engine, comm, group=None, send=None, on_close=None):
+    def __init__(self, engine, comm, group=None, send=None, on_close=None, on_abort=None):
         self._eng = engine
         self._comm = comm
         self._send = send or (lambda msg: _dist_bcast(msg, group))
         self._on_close = on_close
+        self._on_abort = on_abort
         self._closed = False
 
     def __getattr__(self, name):
@@ -88,6 +89,14 @@ class TPEngine:
             self._send(["__exit__", []])
             if self._on_close:
                 self._on_close()
+
+    def abort(self):
+        """Failure teardown (a rank timed out or died): no __exit__ handshake -- the workers are
+        killed and the channel closed, so nothing waits on a rank that will never answer."""
+        if not self._closed:
+            self._closed = True
+            if self._on_abort:
+                self._on_abort()
 
 
 def _dist_bcast(msg, group):
@@ -225,6 +234,17 @@ def launch_tp(spec: str, world: int, devices, max_ctx: int, max_slots: int, max_
                 p.kill()
         ch.close()
 
-    tp = TPEngine(eng, comm, send=ch.broadcast, on_close=shutdown)
+    def abort():
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+        for p in procs:
+            try:
+                p.wait(10)
+            except subprocess.TimeoutExpired:
+                pass
+        ch.close()
+
+    tp = TPEngine(eng, comm, send=ch.broadcast, on_close=shutdown, on_abort=abort)
     tp._keep = (comm, ch, procs)
     return tp, cfg

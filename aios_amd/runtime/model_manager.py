@@ -377,9 +377,7 @@ class ModelManager:
                 elif sch.stalled(stall_timeout_s):
                     reason = f"decode stalled for more than {stall_timeout_s:.0f} s"
                 if reason:
-                    log.error("model %s -> error: %s", m.name, reason)
-                    m.status, m.error = "error", reason
-                    self._abandon(m, stalled="stalled" in reason)
+                    self.fail_model(m, reason)
             if m.status == "error" and auto_recover:
                 now = time.time()
                 m.restarts[:] = [t for t in m.restarts if now - t < window_s]
@@ -393,10 +391,27 @@ class ModelManager:
         await self.unload_idle()
         return recovered
 
+    def fail_model(self, m: ManagedModel, reason: str):
+        """Take a model out of routing now (status `error`): its scheduler is abandoned, pending
+        requests fail, and a multi-process engine (TP ranks) is torn down so a dead or hung rank
+        cannot keep the others spinning; level routing then falls through to the next tier."""
+        if m.status != "ready":
+            return
+        log.error("model %s -> error: %s", m.name, reason)
+        m.status, m.error = "error", reason
+        self._abandon(m, stalled="stalled" in reason)
+
     def _abandon(self, m: ManagedModel, stalled: bool):
         sch = m.scheduler
         m.scheduler = None
+        eng = m.engine
+        if eng is not None and hasattr(eng, "abort"):
+            try:
+                eng.abort()  # TP: kill the worker ranks, close the command channel
+            except Exception:  # noqa: BLE001
+                log.exception("engine abort of %s failed", m.name)
         if sch is None:
+            m.engine = None
             return
         self.abandoned.append(sch)
         from .scheduler import GenResult

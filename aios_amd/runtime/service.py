@@ -106,6 +106,14 @@ class AIRuntimeService:
     async def ListModels(self, request, context):
         return pb.runtime.ModelList(models=[self._status(m) for m in self.mgr.list_models()])
 
+    def _engine_failed(self, m) -> bool:
+        """The model's engine (not the request) failed: take it out of routing."""
+        sch = m.scheduler
+        if sch is not None and sch.failed:
+            self.mgr.fail_model(m, f"engine failure: {sch.failed}")
+            return True
+        return m.status != "ready"
+
     async def Infer(self, request, context):
         try:
             m = await self._route(request)
@@ -113,8 +121,17 @@ class AIRuntimeService:
             await self._abort(context, e)
         temperature, max_tokens = _gen_params(request.temperature, request.max_tokens)
         t0 = time.time()
-        res = await generate(m, build_messages(request.prompt, request.system_prompt), max_tokens, temperature,
-                             json_mode=True)
+        msgs = build_messages(request.prompt, request.system_prompt)
+        res = await generate(m, msgs, max_tokens, temperature, json_mode=True)
+        if res.finish_reason == "error" and self._engine_failed(m):
+            # e.g. a TP rank timed out: the tier is torn down and the request re-routed once to
+            # the next ready model of its level (strategic -> tactical ...)
+            log.warning("model %s failed (%s); re-routing the request", m.name, res.error)
+            try:
+                m = await self._route(request)
+            except RoutingError as e:
+                await self._abort(context, e)
+            res = await generate(m, msgs, max_tokens, temperature, json_mode=True)
         if res.finish_reason == "error":
             await context.abort(grpc.StatusCode.INTERNAL, f"inference failed: {res.error}")
         return pb.runtime.InferResponse(text=res.text, tokens_used=res.prompt_tokens + res.completion_tokens,

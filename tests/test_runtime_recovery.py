@@ -183,3 +183,39 @@ def test_airuntime_grpc_on_cpu_engine_json_mode(small_gguf, monkeypatch):
             await svc.close()
 
     asyncio.run(run())
+
+
+def test_failed_strategic_tier_is_torn_down_and_request_rerouted(small_gguf, monkeypatch):
+    """A strategic-tier engine failure mid-request (what a TP rank timeout raises) takes that
+    tier out of routing, tears its engine down (abort: TP worker ranks killed) and the same
+    Infer is answered by the next ready model of the level."""
+    from aios_amd.rpc.schema import pb
+    from aios_amd.runtime.model_manager import ModelManager
+    from aios_amd.runtime.service import AIRuntimeService
+
+    monkeypatch.setenv("AIOS_RUNTIME_DEVICE", "cpu")
+    monkeypatch.setenv("AIOS_FAULT_INJECT", "decode:always")
+    monkeypatch.setenv("AIOS_FAULT_MODELS", "llama3-70b")
+
+    class Ctx:
+        async def abort(self, code, msg):
+            raise AssertionError(f"aborted: {code} {msg}")
+
+    async def run():
+        mgr = ModelManager(max_batch=2, max_slots=2, base_port=18190)
+        svc = AIRuntimeService(mgr, http=False)
+        try:
+            big = await mgr.load_model("llama3-70b", small_gguf, 256)
+            mid = await mgr.load_model("mistral-7b", small_gguf, 256)
+            assert big.status == mid.status == "ready"
+            aborted = []
+            big.engine.abort = lambda: aborted.append(True)  # the TPEngine teardown hook
+            r = await svc.Infer(pb.runtime.InferRequest(prompt="plan the migration", intelligence_level="strategic",
+                                                        max_tokens=8), Ctx())
+            assert r.model_used == "mistral-7b"
+            assert big.status == "error" and aborted == [True]
+            assert mgr.select_model_for_level("strategic") == "mistral-7b"
+        finally:
+            await svc.close()
+
+    asyncio.run(run())
