@@ -141,6 +141,17 @@ class Engine {
             float* y, int ldy, int epi, int layer);
   QMat alloc_qmat(int qt, int rows, int cols);
   QMat upload_qmat(int qt, int rows, int cols, const void* host, size_t nbytes);
+  // load-time staging: two device buffers (tensor i repacks while i+1 uploads) fed through two
+  // pinned 64 MB host chunks
+  void stage_upload(const void* host, size_t nbytes, void*& dev_staging);
+  void stage_done();
+  void stage_release();
+  void* stage_dev_[2] = {nullptr, nullptr};
+  size_t stage_dev_bytes_[2] = {0, 0};
+  hipEvent_t stage_ev_[2] = {nullptr, nullptr};
+  void* stage_host_[2] = {nullptr, nullptr};
+  hipEvent_t stage_host_ev_[2] = {nullptr, nullptr};
+  int stage_next_ = 0, stage_host_next_ = 0, stage_cur_ = 0;
   float* upload_f32(const void* host, size_t n, int qt);
   QMat interleave_rows(const QMat& a, const QMat& b);
   void* dmalloc(size_t bytes);

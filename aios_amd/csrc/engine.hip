@@ -71,6 +71,10 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
 }
 
 Engine::~Engine() {
+  try {
+    stage_release();
+  } catch (...) {
+  }
   for (auto& kv : graphs_) hipGraphExecDestroy(kv.second);
   for (void* p : allocs_) hipFree(p);
   if (h_par_) hipHostFree(h_par_);
@@ -116,28 +120,83 @@ QMat Engine::alloc_qmat(int qt, int rows, int cols) {
   return m;
 }
 
+// Load path (one hipMalloc + pageable copy + stream sync + hipFree per tensor).
+// Now: the GGUF bytes (mmap'd by the loader) are copied in 64 MB chunks through two pinned host
+// buffers into one of two device staging buffers (DMA from pinned memory, the next chunk's host
+// memcpy overlapping the previous chunk's transfer), and the repack kernel of tensor i runs while
+// tensor i+1 is being staged into the other buffer.  No per-tensor allocation or device sync.
+void Engine::stage_upload(const void* host, size_t nbytes, void*& dev_staging) {
+  constexpr size_t CHUNK = 64ull << 20;
+  const int k = stage_next_;
+  stage_next_ ^= 1;
+  if (stage_ev_[k]) HIP_CHECK(hipEventSynchronize(stage_ev_[k]));  // repack of the tensor two back is done
+  if (stage_dev_bytes_[k] < nbytes) {
+    if (stage_dev_[k]) HIP_CHECK(hipFree(stage_dev_[k]));
+    stage_dev_bytes_[k] = std::max(nbytes, (size_t)256 << 20);
+    HIP_CHECK(hipMalloc(&stage_dev_[k], stage_dev_bytes_[k]));
+  }
+  for (int i = 0; i < 2; ++i)
+    if (!stage_host_[i]) {
+      HIP_CHECK(hipHostMalloc(&stage_host_[i], CHUNK, hipHostMallocDefault));
+      HIP_CHECK(hipEventCreateWithFlags(&stage_host_ev_[i], hipEventDisableTiming));
+      HIP_CHECK(hipEventRecord(stage_host_ev_[i], stream_));
+    }
+  for (size_t off = 0; off < nbytes; off += CHUNK) {
+    const size_t n = std::min(CHUNK, nbytes - off);
+    const int h = stage_host_next_;
+    stage_host_next_ ^= 1;
+    HIP_CHECK(hipEventSynchronize(stage_host_ev_[h]));  // this pinned buffer's last transfer is done
+    std::memcpy(stage_host_[h], (const uint8_t*)host + off, n);
+    HIP_CHECK(hipMemcpyAsync((uint8_t*)stage_dev_[k] + off, stage_host_[h], n, hipMemcpyHostToDevice, stream_));
+    HIP_CHECK(hipEventRecord(stage_host_ev_[h], stream_));
+  }
+  dev_staging = stage_dev_[k];
+  stage_cur_ = k;
+}
+
+void Engine::stage_done() {
+  const int k = stage_cur_;
+  if (!stage_ev_[k]) HIP_CHECK(hipEventCreateWithFlags(&stage_ev_[k], hipEventDisableTiming));
+  HIP_CHECK(hipEventRecord(stage_ev_[k], stream_));
+}
+
+void Engine::stage_release() {
+  HIP_CHECK(hipStreamSynchronize(stream_));
+  for (int i = 0; i < 2; ++i) {
+    if (stage_dev_[i]) HIP_CHECK(hipFree(stage_dev_[i]));
+    if (stage_host_[i]) HIP_CHECK(hipHostFree(stage_host_[i]));
+    if (stage_ev_[i]) HIP_CHECK(hipEventDestroy(stage_ev_[i]));
+    if (stage_host_ev_[i]) HIP_CHECK(hipEventDestroy(stage_host_ev_[i]));
+    stage_dev_[i] = stage_host_[i] = nullptr;
+    stage_ev_[i] = stage_host_ev_[i] = nullptr;
+    stage_dev_bytes_[i] = 0;
+  }
+}
+
 QMat Engine::upload_qmat(int qt, int rows, int cols, const void* host, size_t nbytes) {
   const size_t expect = (size_t)rows * (cols / block_elems(qt)) * block_bytes(qt);
   if (nbytes != expect)
     throw std::runtime_error("tensor byte size mismatch: got " + std::to_string(nbytes) + " expected " +
                              std::to_string(expect));
-  void* staging = nullptr;
-  HIP_CHECK(hipMalloc(&staging, nbytes));
-  HIP_CHECK(hipMemcpyAsync(staging, host, nbytes, hipMemcpyHostToDevice, stream_));
   QMat m;
+  if ((qt == QT_F16 || qt == QT_BF16)) {  // final layout == file layout: straight into place
+    m = alloc_qmat(qt, rows, cols);
+    void* staging = nullptr;
+    stage_upload(host, nbytes, staging);
+    HIP_CHECK(hipMemcpyAsync(m.buf, staging, nbytes, hipMemcpyDeviceToDevice, stream_));
+    stage_done();
+    return m;
+  }
+  void* staging = nullptr;
+  stage_upload(host, nbytes, staging);
   if (native_qtype(qt)) {
     m = alloc_qmat(qt, rows, cols);
-    if (qt == QT_F16 || qt == QT_BF16) {
-      HIP_CHECK(hipMemcpyAsync(m.buf, staging, nbytes, hipMemcpyDeviceToDevice, stream_));
-    } else {
-      launch_repack(qt, staging, (size_t)rows * (cols / block_elems(qt)), m.w, stream_);
-    }
+    launch_repack(qt, staging, (size_t)rows * (cols / block_elems(qt)), m.w, stream_);
   } else {
     m = alloc_qmat(QT_BF16, rows, cols);
     launch_legacy_to_bf16(qt, staging, (size_t)rows * cols, m.buf, stream_);
   }
-  HIP_CHECK(hipStreamSynchronize(stream_));
-  HIP_CHECK(hipFree(staging));
+  stage_done();
   return m;
 }
 
@@ -366,6 +425,7 @@ std::string Engine::weight_type_summary() const {
 void Engine::finalize() {
   TraceRange tr("aios.finalize");
   HIP_CHECK(hipSetDevice(cfg_.device));
+  stage_release();  // weights are in place: drop the load-time staging buffers
   auto miss = missing_tensors();
   if (!miss.empty()) throw std::runtime_error("missing tensors, first: " + miss[0]);
   if (!output_.valid()) {

@@ -23,6 +23,26 @@
 
 namespace aios {
 
+// Segment `s` of a kernel argument by VALUE, selected field by field: indexing a.seg[s] with a
+// run-time s takes the address of the by-value kernarg struct and copies all of it to scratch
+// (352 B of private segment per launch of the fp32 GEMV before this).
+__device__ __forceinline__ QWeight seg_at(const GemvArgs& a, int s) {
+  QWeight w;
+  w.qtype = s == 0 ? a.seg[0].qtype : (s == 1 ? a.seg[1].qtype : a.seg[2].qtype);
+  w.rows = s == 0 ? a.seg[0].rows : (s == 1 ? a.seg[1].rows : a.seg[2].rows);
+  w.cols = s == 0 ? a.seg[0].cols : (s == 1 ? a.seg[1].cols : a.seg[2].cols);
+  w.pad_ = 0;
+  w.p0 = s == 0 ? a.seg[0].p0 : (s == 1 ? a.seg[1].p0 : a.seg[2].p0);
+  w.p1 = s == 0 ? a.seg[0].p1 : (s == 1 ? a.seg[1].p1 : a.seg[2].p1);
+  w.p2 = s == 0 ? a.seg[0].p2 : (s == 1 ? a.seg[1].p2 : a.seg[2].p2);
+  w.p3 = s == 0 ? a.seg[0].p3 : (s == 1 ? a.seg[1].p3 : a.seg[2].p3);
+  return w;
+}
+__device__ __forceinline__ int seg_row0_at(const GemvArgs& a, int s) {
+  return s == 0 ? a.seg_row0[0] : (s == 1 ? a.seg_row0[1] : a.seg_row0[2]);
+}
+
+
 constexpr int GEMV_THREADS = 256;
 constexpr int GEMV_WAVES = GEMV_THREADS / 64;
 constexpr int GEMV_ROWS = 2;  // rows per wave
@@ -242,7 +262,7 @@ __global__ void __launch_bounds__(GEMV_THREADS) gemv_kernel(GemvArgs a) {
 #pragma unroll
   for (int s = 1; s < GEMV_MAX_SEGS; ++s)
     if (s < a.nseg && row_blk >= a.seg_row0[s]) sidx = s;
-  const int seg_row0 = a.seg_row0[sidx];
+  const int seg_row0 = seg_row0_at(a, sidx);
   const int K = a.K;
   const int nb_act = a.B;  // real batch (<= B; padding columns are never stored)
 
@@ -272,9 +292,9 @@ __global__ void __launch_bounds__(GEMV_THREADS) gemv_kernel(GemvArgs a) {
   const bool active = (row_blk + wave * GEMV_ROWS) < a.N;
   // the type-0 segment(s) come first; type-1 is only ever the last segment
   if (QT0 == QT1 || sidx < a.nseg - 1 || a.nseg == 1)
-    gemv_seg<QT0, B, U>(a, a.seg[sidx], local_row, active, inv_rms, xl, xs, acc);
+    gemv_seg<QT0, B, U>(a, seg_at(a, sidx), local_row, active, inv_rms, xl, xs, acc);
   else
-    gemv_seg<QT1, B, U>(a, a.seg[sidx], local_row, active, inv_rms, xl, xs, acc);
+    gemv_seg<QT1, B, U>(a, seg_at(a, sidx), local_row, active, inv_rms, xl, xs, acc);
   if (!active) return;
 
 #pragma unroll
@@ -394,23 +414,23 @@ __global__ void __launch_bounds__(GP_THREADS) gemv_persistent(GemvArgs a) {
   float* xl1 = SEP ? xs0 + B * K / 16 : xl0;
   float* xs1 = SEP ? xl1 + B * K : xs0;
 
-  auto info = [&](int p, int& lrow, bool& t1, const QWeight*& w) {
+  auto info = [&](int p, int& lrow, bool& t1, QWeight& w) {
     const int row = 2 * p;
     int s = 0;
 #pragma unroll
     for (int k = 1; k < GEMV_MAX_SEGS; ++k)
       if (k < a.nseg && row >= a.seg_row0[k]) s = k;
-    lrow = row - a.seg_row0[s];
+    lrow = row - seg_row0_at(a, s);
     t1 = MIXED && (s == a.nseg - 1) && a.nseg > 1;
-    w = &a.seg[s];
+    w = seg_at(a, s);
   };
   auto load = [&](int p, int it, RawChunk (&r)[U][GEMV_ROWS]) {
     int lrow;
     bool t1;
-    const QWeight* w;
+    QWeight w;
     info(p, lrow, t1, w);
-    if (MIXED && t1) gp_load<QT1, U>(*w, lrow, it, nch1, r);
-    else gp_load<QT0, U>(*w, lrow, it, nch0, r);
+    if (MIXED && t1) gp_load<QT1, U>(w, lrow, it, nch1, r);
+    else gp_load<QT0, U>(w, lrow, it, nch0, r);
   };
 
   int p = blockIdx.x * GP_WAVES + wave;
@@ -446,7 +466,7 @@ __global__ void __launch_bounds__(GP_THREADS) gemv_persistent(GemvArgs a) {
   auto step = [&](RawChunk (&cur)[U][GEMV_ROWS], RawChunk (&nxt)[U][GEMV_ROWS]) -> bool {
     int lrow;
     bool t1;
-    const QWeight* w;
+    QWeight w;
     info(p, lrow, t1, w);
     const int nit = (MIXED && t1) ? nit1 : nit0;
     int pn = p, itn = it + 1;

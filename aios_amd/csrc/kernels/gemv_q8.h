@@ -692,8 +692,11 @@ __global__ void __launch_bounds__(Q8_WAVES * 64) gemv_q8_rows(GemvArgs a) {
       if (!(a.tune_dbg & 1)) q8_stage<QT0, B, NPF>(a, xq, ms, red, pf);
       __syncthreads();
       run(FmtTag<QT0>{}, wid, np0, stride, buf);
-      load(FmtTag<QT1>{}, np0 + wid, npairs, 0, bufA);
-      run(FmtTag<QT1>{}, np0 + wid, npairs, stride, buf);
+      // the second format gets its own register buffer: one array written through two different
+      // load sequences defeats SROA and lands in scratch
+      RawChunk bufT[PIPE][U][GEMV_ROWS];
+      load(FmtTag<QT1>{}, np0 + wid, npairs, 0, bufT[0]);
+      run(FmtTag<QT1>{}, np0 + wid, npairs, stride, bufT);
     } else if (wid < W0) {
       load(FmtTag<QT0>{}, wid, np0, 0, bufA);
       if (!(a.tune_dbg & 1)) q8_stage<QT0, B, NPF>(a, xq, ms, red, pf);
