@@ -16,6 +16,7 @@ using namespace aios;
 
 namespace aios {
 double bench_launch_chain(int n_kernels, int blocks, int use_graph, int reps);
+double bench_stream_read(size_t bytes, int nbuf, int wg_per_cu, int u, int threads, int reps);
 }
 
 namespace {
@@ -474,6 +475,8 @@ PYBIND11_MODULE(_engine, m) {
            })
       .def_property_readonly("vocab_size", &JsonGrammar::vocab_size)
       .def_property_readonly("cache_size", &JsonGrammar::cache_size);
+  m.def("bench_stream_read", &aios::bench_stream_read, py::arg("bytes"), py::arg("nbuf"), py::arg("wg_per_cu"),
+        py::arg("u"), py::arg("threads"), py::arg("reps"));
   m.def("bench_launch_chain", &aios::bench_launch_chain, py::arg("n_kernels"), py::arg("blocks"), py::arg("use_graph"),
         py::arg("reps"), py::call_guard<py::gil_scoped_release>());
 }

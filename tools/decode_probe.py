@@ -44,6 +44,8 @@ def main():
     ap.add_argument("--json", default=None)
     ap.add_argument("--ms", default="1,4")
     ap.add_argument("--shapes", default="")
+    ap.add_argument("--dbg", action="store_true", help="GEMV anatomy: prologue off (1) / compute off (2) x U")
+    ap.add_argument("--no-skinny", action="store_true")
     args = ap.parse_args()
     E = native.require()
     st = torch.cuda.current_stream().cuda_stream
@@ -72,12 +74,21 @@ def main():
         x = torch.randn(1, K, device="cuda")
         nw = torch.ones(K, device="cuda")
         y = torch.zeros(64, N, device="cuda")
-        for g in (0, 1, 2, 3, 4):
-            fns = [lambda m=m: E.gemv([m], 1, x.data_ptr(), K, nw.data_ptr(), 1e-5, y.data_ptr(), N, E.EPI_STORE, st,
-                                      0, 1, g, 0, 0, 0) for m in mats]
-            us = time_rot(fns, 4 * R)
-            emit(dict(shape=name, variant="gemv_q8", grid=g, us=round(us, 2), gbs=round(nbytes / us / 1e3, 1)))
-        for M in ms:
+        if args.dbg:
+            for u in (0, 1, 2, 3, 4, 13, 14, 21, 22):
+                for dbg in (0, 1, 2, 3):
+                    fns = [lambda m=m: E.gemv([m], 1, x.data_ptr(), K, nw.data_ptr(), 1e-5, y.data_ptr(), N,
+                                              E.EPI_STORE, st, 0, 1, 0, u, 0, dbg) for m in mats]
+                    us = time_rot(fns, 4 * R)
+                    emit(dict(shape=name, variant="gemv_q8", u=u, dbg=dbg, us=round(us, 2),
+                              gbs=round(nbytes / us / 1e3, 1)))
+        else:
+            for g in (0, 1, 2, 3, 4):
+                fns = [lambda m=m: E.gemv([m], 1, x.data_ptr(), K, nw.data_ptr(), 1e-5, y.data_ptr(), N, E.EPI_STORE,
+                                          st, 0, 1, g, 0, 0, 0) for m in mats]
+                us = time_rot(fns, 4 * R)
+                emit(dict(shape=name, variant="gemv_q8", grid=g, us=round(us, 2), gbs=round(nbytes / us / 1e3, 1)))
+        for M in ([] if args.no_skinny else ms):
             A = torch.randn(M, K, device="cuda").to(torch.bfloat16)
             for rb in (4, 8):
                 os.environ["AIOS_SKINNY_RB"] = str(rb)
