@@ -285,7 +285,8 @@ PYBIND11_MODULE(_engine, m) {
 
   m.def("gemv",
         [](std::vector<PyQMatrix*> segs, int B, uintptr_t x, int ldx, uintptr_t norm_w, float eps, uintptr_t y,
-           int ldy, int epi, uintptr_t st, int force_v1, int act_q8, int tune_grid, int tune_u, int tune_ksplit, int tune_dbg) {
+           int ldy, int epi, uintptr_t st, int force_v1, int act_q8, int tune_grid, int tune_u, int tune_ksplit, int tune_dbg,
+           int kernel_sel, uintptr_t dbg_ts) {
           GemvArgs a;
           std::memset(&a, 0, sizeof(a));
           a.nseg = (int)segs.size();
@@ -295,16 +296,18 @@ PYBIND11_MODULE(_engine, m) {
           a.x = (const float*)x; a.ldx = ldx; a.norm_w = (const float*)norm_w; a.eps = eps;
           a.y = (float*)y; a.ldy = ldy; a.epi = epi; a.force_v1 = force_v1; a.act_q8 = act_q8;
           a.tune_grid = tune_grid; a.tune_u = tune_u; a.tune_ksplit = tune_ksplit; a.tune_dbg = tune_dbg;
+          a.kernel_sel = kernel_sel; a.dbg_ts = (unsigned long long*)dbg_ts;
           launch_gemv(a, S(st));
         },
         py::arg("segs"), py::arg("B"), py::arg("x"), py::arg("ldx"), py::arg("norm_w"), py::arg("eps"), py::arg("y"),
         py::arg("ldy"), py::arg("epi"), py::arg("stream"), py::arg("force_v1") = 0, py::arg("act_q8") = 0,
-        py::arg("tune_grid") = 0, py::arg("tune_u") = 0, py::arg("tune_ksplit") = 0, py::arg("tune_dbg") = 0);
+        py::arg("tune_grid") = 0, py::arg("tune_u") = 0, py::arg("tune_ksplit") = 0, py::arg("tune_dbg") = 0,
+        py::arg("kernel_sel") = 0, py::arg("dbg_ts") = 0);
   m.def("gemv_qkv",
         [](std::vector<PyQMatrix*> segs, int B, uintptr_t x, int ldx, uintptr_t norm_w, float eps, uintptr_t q_out,
            uintptr_t bias, int head_dim, int n_heads, int n_kv_heads, int max_ctx, int rope_neox, float rope_base,
            uintptr_t pos, uintptr_t slot, uintptr_t k_cache, uintptr_t v_cache, uintptr_t st, int act_q8,
-           uintptr_t block_table) {
+           uintptr_t block_table, uintptr_t rope_cs, int tune_grid, int kernel_sel) {
           GemvArgs a;
           std::memset(&a, 0, sizeof(a));
           a.nseg = (int)segs.size();
@@ -315,16 +318,18 @@ PYBIND11_MODULE(_engine, m) {
           a.y = (float*)q_out; a.ldy = n_heads * head_dim; a.epi = EPI_QKV;
           a.bias = (const float*)bias; a.head_dim = head_dim; a.q_dim = n_heads * head_dim;
           a.kv_dim = n_kv_heads * head_dim; a.n_kv_heads = n_kv_heads; a.max_ctx = max_ctx;
-          a.rope_neox = rope_neox; a.rope_base = rope_base; a.rope_cs = nullptr; a.pos = (const int*)pos; a.slot = (const int*)slot;
+          a.rope_neox = rope_neox; a.rope_base = rope_base; a.rope_cs = (const float2*)rope_cs; a.pos = (const int*)pos; a.slot = (const int*)slot;
           a.k_cache = (bf16_t*)k_cache; a.v_cache = (bf16_t*)v_cache; a.act_q8 = act_q8;
           a.block_table = (const int*)block_table;
+          a.tune_grid = tune_grid;
+          a.kernel_sel = kernel_sel;
           launch_gemv(a, S(st));
         },
         py::arg("segs"), py::arg("B"), py::arg("x"), py::arg("ldx"), py::arg("norm_w"), py::arg("eps"),
         py::arg("q_out"), py::arg("bias"), py::arg("head_dim"), py::arg("n_heads"), py::arg("n_kv_heads"),
         py::arg("max_ctx"), py::arg("rope_neox"), py::arg("rope_base"), py::arg("pos"), py::arg("slot"),
         py::arg("k_cache"), py::arg("v_cache"), py::arg("stream"), py::arg("act_q8") = 0,
-        py::arg("block_table") = 0);
+        py::arg("block_table") = 0, py::arg("rope_cs") = 0, py::arg("tune_grid") = 0, py::arg("kernel_sel") = 0);
   m.def("attn_decode",
         [](uintptr_t q, uintptr_t k, uintptr_t v, uintptr_t seq_len, uintptr_t slot, int B, int H, int Hkv, int hd,
            int max_ctx, int n_chunks, float scale, uintptr_t opart, uintptr_t ml, uintptr_t out, uintptr_t counters,

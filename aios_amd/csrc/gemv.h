@@ -27,6 +27,9 @@ struct GemvArgs {
   int tune_u;                   // chunks per lane per work item override (0 = auto; 1, 2, 4)
   int tune_ksplit;              // -1 disables the K-split decomposition (testing / tuning)
   int tune_dbg;                 // microbenchmarks only: bit0 skip x staging, bit1 skip dot compute
+  int kernel_sel;               // testing / probes: 0 = launcher's choice, 1 = row-pair int8 kernel,
+                                //   2 = CU register-streaming kernel, 3 = LDS-DMA engine
+  unsigned long long* dbg_ts;   // probes: per-workgroup phase timestamps (s_memrealtime) or null
   const float* x;               // [B][ldx] fp32 input (residual stream if norm_w != null)
   int ldx;
   const float* norm_w;          // RMSNorm weight [K] or null

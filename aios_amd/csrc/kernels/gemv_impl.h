@@ -527,6 +527,8 @@ bool launch_gemv_persistent(GemvArgs a, hipStream_t st) {
 
 
 #include "gemv_q8.h"
+#include "gemv_cu.h"
+#include "gemv_lds.h"
 
 inline int qtype_block(int qt) {
   return (qt == QT_Q4_K || qt == QT_Q5_K || qt == QT_Q6_K) ? 256 : (qt == QT_F16 || qt == QT_BF16 ? 8 : 32);
@@ -552,6 +554,8 @@ void launch_gemv_pair(const GemvArgs& a, hipStream_t st) {
   constexpr bool Q8OK = QT0 != QT_F16 && QT0 != QT_BF16;
   if constexpr (Q8OK) {
     if (!a.force_v1 && a.act_q8) {
+      if (a.B == 1 && launch_gemv_lds<QT0, QT1>(a, st)) return;
+      if (a.B == 1 && launch_gemv_cu<QT0, QT1>(a, st)) return;
       if (a.B == 1 && launch_gemv_q8<QT0, QT1, 1>(a, st)) return;
       if (a.B == 2 && launch_gemv_q8<QT0, QT1, 2>(a, st)) return;
       if (a.B > 2 && a.B <= 4 && launch_gemv_q8<QT0, QT1, 4>(a, st)) return;

@@ -1,0 +1,450 @@
+// Loader / consumer batch-1 decode GEMV (int8 activations) with an LDS-DMA weight ring; included by
+// gemv_impl.h after gemv_cu.h.
+//
+// Measured on MI355X (tools/gemv_cu_probe.py, in-kernel s_memrealtime stamps): in a GEMV whose waves
+// both load weights into registers and compute, the weight stream STALLS while x is staged -- the
+// registers hold the first loads, no more can be issued until x (the previous kernel's output, ~1-2
+// us away) is quantised into LDS and the workgroup barrier passes, and x's own loads queue behind
+// the CU's weight loads.  gate_up: barrier at 6.5 us of a 19 us kernel whose bytes need 10.7 us.
+//
+// Here the roles are split, the MI355X batch-1 engine shape (MI355X_MICROARCH.md price list rows
+// 'ldsdma-fill', 'engine-vs-launches'): per CU one 1024-thread workgroup, waves 14-15 only move
+// weight bytes HBM -> LDS with LDS-DMA (global_load_lds_dwordx4 nt, no VGPR round trip) into a ring
+// of R slots (5-8), waves 0-13 stage x and then each computes one 64-chunk group per slot.  The loaders
+// never wait for compute: a slot is refilled one step after it was consumed, R-1 slots (95-112 KB)
+// stay in flight, so the x staging latency is covered by the ring instead of idling the stream.
+// Steps are lock-stepped with raw s_barrier (no fence: a __syncthreads would drain every in-flight
+// DMA, cdna_hip_programming.md 'Pipelining across barriers'); the loaders' counted vmcnt waits are
+// inline asm with immediates fixed by the format's DMA count per slot.
+//
+// Each slot holds NG = 14 groups (one per consumer wave); a group is 64 chunks of one row (so
+// nch % 64 == 0 is required), and every weight plane of the format is copied per slot as its own
+// contiguous region (group k of plane P at P_off + k * bytes_per_group(P)); a DMA lane computes its
+// own source address, so a slot may span segments (Q|K) and rows freely.
+#pragma once
+// (included inside namespace aios by gemv_impl.h)
+
+constexpr int LG_NG = 14;               // consumer waves
+constexpr int LG_NL = 2;                // loader waves
+constexpr int LG_THREADS = (LG_NG + LG_NL) * 64;
+// B0 (x loads queued ahead of the first weight DMA): measured slower -- the loaders' first slots
+// then start ~1.6 us late while x is an L2/MALL hit either way
+#ifndef LG_B0
+#define LG_B0 0
+#endif
+
+// planes of a format: bytes per 64-chunk group and the LDS-DMA width used to copy it
+template <int QT>
+struct LgPlanes;
+template <>
+struct LgPlanes<QT_Q4_K> {
+  static constexpr int n = 2;
+  static constexpr int bpg[4] = {1024, 128, 0, 0};
+  static constexpr int dsz[4] = {16, 16, 0, 0};
+};
+template <>
+struct LgPlanes<QT_Q5_K> {
+  static constexpr int n = 3;
+  static constexpr int bpg[4] = {1024, 128, 256, 0};
+  static constexpr int dsz[4] = {16, 16, 16, 0};
+};
+template <>
+struct LgPlanes<QT_Q6_K> {
+  static constexpr int n = 4;
+  static constexpr int bpg[4] = {1024, 512, 128, 16};
+  static constexpr int dsz[4] = {16, 16, 16, 4};
+};
+template <>
+struct LgPlanes<QT_Q4_0> {
+  static constexpr int n = 2;
+  static constexpr int bpg[4] = {1024, 128, 0, 0};
+  static constexpr int dsz[4] = {16, 16, 0, 0};
+};
+template <>
+struct LgPlanes<QT_Q8_0> {
+  static constexpr int n = 2;
+  static constexpr int bpg[4] = {1024, 64, 0, 0};
+  static constexpr int dsz[4] = {16, 16, 0, 0};
+};
+
+template <int QT>
+struct LgLayout {
+  using P = LgPlanes<QT>;
+  // groups per consumer wave per step: 2 for the 4.5-bit formats (the pair shares one row sum and
+  // gives each wave two independent chains per step), 1 where a slot would not fit R >= 5 in LDS
+  static constexpr int GPW = (QT == QT_Q6_K || QT == QT_Q5_K) ? 1 : 2;
+  static constexpr int NGS = LG_NG * GPW;  // groups per slot
+  // DMA instructions (one wave each) for plane p of a slot, and its padded LDS region
+  static constexpr int ninst(int p) { return (NGS * P::bpg[p] + 64 * P::dsz[p] - 1) / (64 * P::dsz[p]); }
+  static constexpr int region(int p) { return p < P::n ? ninst(p) * 64 * P::dsz[p] : 0; }
+  static constexpr int off(int p) { return p == 0 ? 0 : off(p - 1) + region(p - 1); }
+  static constexpr int slot_bytes = off(4);
+  static constexpr int total_inst = (P::n > 0 ? ninst(0) : 0) + (P::n > 1 ? ninst(1) : 0) + (P::n > 2 ? ninst(2) : 0) +
+                                    (P::n > 3 ? ninst(3) : 0);
+  // instructions per slot issued by one loader wave (instruction i goes to loader i % LG_NL); the
+  // loaders' vmcnt immediates assume every slot issues exactly this many
+  static constexpr int per_loader = (total_inst + LG_NL - 1) / LG_NL;
+  // ring slots: R - 1 slots in flight must cover HBM latency x the CU's share of the bandwidth
+  // (~2-3 us x 24 GB/s under full load): 3 x 32 KB for the 4.5-bit formats, 4 x 24 KB for Q6_K
+  static constexpr int R = slot_bytes > 28 * 1024 ? 4 : (slot_bytes <= 20 * 1024 ? 6 : 5);
+  static_assert((R - 2) * per_loader <= 63, "vmcnt immediate");
+};
+
+__device__ __forceinline__ const uint8_t* lg_plane_ptr(const QWeight& w, int p) {
+  return p == 0 ? w.p0 : (p == 1 ? w.p1 : (p == 2 ? w.p2 : w.p3));
+}
+
+// raw workgroup barrier (no fence: in-flight LDS-DMA survives it), a compiler memory barrier on
+// both sides so no LDS access moves across it
+__device__ __forceinline__ void lg_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+template <int N>
+__device__ __forceinline__ void lg_vmcnt() {
+  static_assert(N >= 0 && N <= 63, "vmcnt immediate");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// Copy slot s (groups [s*NGS, s*NGS+NGS) of this workgroup) into ring buffer `dst`.
+//
+// A 64-chunk group is 64 chunks of one row, so in every plane the group with global index
+// G = row * nit + it sits at plane_base(seg) + (G - first_group(seg)) * bytes_per_group: within a
+// segment a plane is LINEAR in the group index and one slot's plane region is one contiguous byte
+// range.  Fast path (the slot inside one segment, no tail clamp): buffer_load ... lds with the
+// segment's plane as the resource, the slot offset in an SGPR and lane * width as the only VGPR --
+// one SALU add per 1 KB instruction (a per-lane address version spent ~25-65 instructions per DMA
+// and the loaders' issue rate, not HBM, set the step time).  General path (a slot crossing Q|K, or
+// the last slot): per-lane segment select and clamp.  Loader wave lw issues instructions lw,
+// lw + NL, ...; every loader issues exactly per_loader instructions per slot (exact counted waits).
+template <int QT>
+__device__ __forceinline__ void lg_dma_slot(const GemvArgs& a, uint8_t* dst, int s, int lw, int r0, int nit,
+                                            int ngroups) {
+  using L = LgLayout<QT>;
+  using P = LgPlanes<QT>;
+  constexpr int NGS = L::NGS;
+  const int lane = threadIdx.x & 63;
+  const int g0 = r0 * nit + s * NGS;            // global group index of the slot's first group
+  const int glast = r0 * nit + ngroups - 1;     // last group of the workgroup
+  const int G1 = a.nseg > 1 ? a.seg_row0[1] * nit : 0x7fffffff;
+  const int G2 = a.nseg > 2 ? a.seg_row0[2] * nit : 0x7fffffff;
+  const int gend = g0 + NGS - 1;
+  const int sg0 = g0 >= G2 ? 2 : (g0 >= G1 ? 1 : 0);
+  const int Gs = sg0 == 0 ? 0 : (sg0 == 1 ? G1 : G2);
+  const int Gn = sg0 == 0 ? G1 : (sg0 == 1 ? G2 : 0x7fffffff);
+  const bool fast = gend <= glast && gend < Gn;
+  int issued = 0;
+  int idx = 0;  // running instruction index over the planes
+  static_for<4>([&](auto pc) {
+    constexpr int p = decltype(pc)::value;
+    if constexpr (p < P::n) {
+      constexpr int S = P::dsz[p], BPG = P::bpg[p];
+      constexpr int NI = L::ninst(p);
+      const uint8_t* pb0 = sgpr_ptr(lg_plane_ptr(a.seg[0], p));
+      const uint8_t* pb1 = sgpr_ptr(lg_plane_ptr(a.seg[1], p));
+      const uint8_t* pb2 = sgpr_ptr(lg_plane_ptr(a.seg[2], p));
+      if (fast) {
+        const __amdgpu_buffer_rsrc_t rs = mk_rsrc(sg0 == 0 ? pb0 : (sg0 == 1 ? pb1 : pb2));
+        const int soff0 = (g0 - Gs) * BPG;
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+          if ((idx + i) % LG_NL != lw) continue;
+          auto* ldst = (__attribute__((address_space(3))) void*)(dst + L::off(p) + i * 64 * S);
+          if constexpr (S == 16) __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, ldst, 16, lane * 16, soff0 + i * 1024, 0, 2);
+          else __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, ldst, 4, lane * 4, soff0 + i * 256, 0, 2 /* nt */);
+          ++issued;
+        }
+      } else {
+        // per-segment base shifted so that (group * BPG) indexes it directly
+        const uint64_t b0 = (uint64_t)pb0;
+        const uint64_t b1 = (uint64_t)pb1 - (uint64_t)(a.nseg > 1 ? G1 : 0) * BPG;
+        const uint64_t b2 = (uint64_t)pb2 - (uint64_t)(a.nseg > 2 ? G2 : 0) * BPG;
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+          if ((idx + i) % LG_NL != lw) continue;
+          const int b = i * 64 * S + lane * S;  // byte within the plane's slot region
+          int g = g0 + b / BPG;                 // BPG is a power of two: a shift
+          const int o = b & (BPG - 1);
+          g = min(g, glast);                    // the last slot's tail and the padding lanes
+          const uint64_t base = g >= G2 ? b2 : (g >= G1 ? b1 : b0);
+          const uint8_t* src = (const uint8_t*)(base + (uint64_t)g * BPG + o);
+          auto* ldst = (__attribute__((address_space(3))) void*)(dst + L::off(p) + i * 64 * S);
+          if constexpr (S == 16) __builtin_amdgcn_global_load_lds((const void*)src, ldst, 16, 0, 2 /* nt */);
+          else __builtin_amdgcn_global_load_lds((const void*)src, ldst, 4, 0, 2 /* nt */);
+          ++issued;
+        }
+      }
+      idx += NI;
+    }
+  });
+  // pad to per_loader instructions (re-issue the slot's first piece of plane 0 into its own place)
+  if (issued < L::per_loader) {
+    const int g = min(g0, glast);
+    const uint64_t b0 = (uint64_t)sgpr_ptr(a.seg[0].p0);
+    const uint64_t b1 = (uint64_t)sgpr_ptr(a.seg[1].p0) - (uint64_t)(a.nseg > 1 ? G1 : 0) * 1024;
+    const uint64_t b2 = (uint64_t)sgpr_ptr(a.seg[2].p0) - (uint64_t)(a.nseg > 2 ? G2 : 0) * 1024;
+    const uint64_t base = g >= G2 ? b2 : (g >= G1 ? b1 : b0);
+    const uint8_t* src = (const uint8_t*)(base + (uint64_t)g * 1024 + lane * 16);
+    for (; issued < L::per_loader; ++issued)
+      __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)dst, 16, 0, 2);
+  }
+}
+
+// consumer: the raw chunk of lane `lane` of group k from a ring slot
+template <int QT>
+__device__ __forceinline__ void lg_read(const uint8_t* slot, int k, int lane, RawChunk& r) {
+  using L = LgLayout<QT>;
+  const uint8_t* A = slot + L::off(0) + k * 1024;
+  r.a = *(const uint4*)(A + lane * 16);
+  if constexpr (QT == QT_Q4_K || QT == QT_Q5_K) {
+    r.b = *(const uint4*)(slot + L::off(1) + k * 128 + (lane >> 3) * 16);
+    if constexpr (QT == QT_Q5_K) r.c = *(const uint4*)(slot + L::off(2) + k * 256 + (lane >> 3) * 32 + 16 * (lane & 1));
+  } else if constexpr (QT == QT_Q6_K) {
+    const uint2 h = *(const uint2*)(slot + L::off(1) + k * 512 + lane * 8);
+    r.b.x = h.x;
+    r.b.y = h.y;
+    r.c.x = *(const uint16_t*)(slot + L::off(2) + k * 128 + lane * 2);
+    r.d = *(const uint16_t*)(slot + L::off(3) + k * 16 + (lane >> 3) * 2);
+  } else if constexpr (QT == QT_Q4_0) {
+    r.d = *(const uint16_t*)(slot + L::off(1) + k * 128 + lane * 2);
+  } else {  // Q8_0
+    r.d = *(const uint16_t*)(slot + L::off(1) + k * 64 + (lane >> 1) * 2);
+  }
+}
+
+template <int QT0, int QT1>
+__global__ void __launch_bounds__(LG_THREADS) gemv_lds_b1(GemvArgs a, CuPlan pl) {
+  static_assert(same_xlayout<QT0, QT1>, "mixed segments must share the activation layout");
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  constexpr bool MIXED = QT0 != QT1;
+  constexpr int W = QFmt<QT0>::W, R = QFmt<QT0>::RUNS;
+  const int nch = a.K / W;
+  const int nit = nch >> 6;
+  const int npairs = a.N >> 1;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const bool loader = wave >= LG_NG;
+  unsigned long long ts[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  CU_STAMP(0);
+
+  // ---- this workgroup's pair range (as gemv_cu_b1)
+  const int g = blockIdx.x;
+  const bool fmt1 = MIXED && g >= pl.g0;
+  int pb, pe;
+  if (!fmt1) {
+    const int np = MIXED ? pl.np0 : npairs, G = MIXED ? pl.g0 : (int)gridDim.x;
+    pb = (int)((long)g * np / G);
+    pe = (int)((long)(g + 1) * np / G);
+  } else {
+    const int np = npairs - pl.np0, G = (int)gridDim.x - pl.g0, gg = g - pl.g0;
+    pb = pl.np0 + (int)((long)gg * np / G);
+    pe = pl.np0 + (int)((long)(gg + 1) * np / G);
+  }
+  if (pb >= pe) return;  // whole workgroup, before any barrier
+  const int r0 = 2 * pb, nrows = 2 * (pe - pb);
+  const int ngroups = nrows * nit;
+
+  // ---- LDS: red[64] | rowacc[racc_n] | ms [nch][R] | xq [nch][W] | ring [LG_R][slot]
+  float* red = smem;
+  float* rowacc = smem + 64;
+  float2* ms = (float2*)(rowacc + pl.racc_n);
+  int8_t* xq = (int8_t*)(ms + (size_t)nch * R);
+  // (offset arithmetic on the __shared__ base: a pointer cast through uintptr_t loses the LDS
+  // address space and every ring read became a flat load waited with vmcnt)
+  const int ring_off = (int)(((const uint8_t*)(xq + a.K) - (const uint8_t*)smem + 255) & ~255);
+  uint8_t* ring = (uint8_t*)smem + ring_off;
+  for (int i = threadIdx.x; i < nrows; i += LG_THREADS) rowacc[i] = 0.f;
+  if (threadIdx.x < 64) red[threadIdx.x] = 0.f;
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // ordered before B0
+
+  // Loader and consumer paths are separate (no register merge between them: a phi of the
+  // consumers' in-flight x registers made the compiler wait for them before the first barrier,
+  // holding the loaders back).  Both execute the same T + 3 barriers.
+  auto loader_path = [&](auto tag) __attribute__((always_inline)) {
+    constexpr int QT = decltype(tag)::value;
+    using L = LgLayout<QT>;
+    constexpr int PL = L::per_loader;
+    constexpr int LG_R = L::R;
+    const int T = (ngroups + L::NGS - 1) / L::NGS;
+    const int lw = wave - LG_NG;
+    if (LG_B0) lg_barrier();  // B0: the consumers' x loads are queued ahead of any weight byte
+    const int npro = min(T, LG_R - 1);
+    for (int s = 0; s < npro; ++s) lg_dma_slot<QT>(a, ring + (size_t)s * L::slot_bytes, s, lw, r0, nit, ngroups);
+    if (npro == LG_R - 1) lg_vmcnt<(LG_R - 2) * PL>();
+    else lg_vmcnt<0>();
+    lg_barrier();  // B1: slot 0 landed, x staged
+    for (int t = 0; t < T; ++t) {
+      if (t + LG_R - 1 < T) {
+        lg_dma_slot<QT>(a, ring + (size_t)((t + LG_R - 1) % LG_R) * L::slot_bytes, t + LG_R - 1, lw, r0, nit,
+                        ngroups);
+        lg_vmcnt<(LG_R - 2) * PL>();  // slot t + 1 landed
+      } else {
+        lg_vmcnt<0>();
+      }
+      lg_barrier();
+    }
+    lg_barrier();  // final
+  };
+  auto consumer_path = [&](auto tag, float2& rope) __attribute__((always_inline)) {
+    constexpr int QT = decltype(tag)::value;
+    using L = LgLayout<QT>;
+    constexpr int LG_R = L::R;
+    constexpr int GPW = L::GPW;
+    const int T = (ngroups + L::NGS - 1) / L::NGS;
+    constexpr int NPF = 2;
+    StagePre<NPF> pf{};
+    q8_stage_prefetch(a, pf, threadIdx.x, LG_NG * 64);
+    if (LG_B0) lg_barrier();  // B0
+    CU_STAMP(1);
+    q8_stage<QT0, 1, NPF>(a, xq, ms, red, pf, threadIdx.x, LG_NG * 64);
+    // RoPE (cos, sin) of the epilogue lane's pair: issued now, waited for in the epilogue (the
+    // consumers issue no other global load until then)
+    if (a.epi == EPI_QKV && wave == 0 && a.rope_cs) {
+      const int pos0 = a.pos[0];
+      int part, head, lrr;
+      qkv_part(a, a.row_base + r0 + 2 * lane, part, head, lrr);
+      rope = a.rope_cs[(size_t)pos0 * (a.head_dim >> 1) + (part < 2 ? (lrr >> 1) : 0)];
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    CU_STAMP(2);
+    lg_barrier();  // B1
+    CU_STAMP(3);
+    for (int t = 0; t < T; ++t) {
+      const int gb = t * L::NGS + wave * GPW;  // this wave's first group of the slot
+      if (gb < ngroups) {
+        const uint8_t* slot = ring + (size_t)(t % LG_R) * L::slot_bytes;
+        RawChunk raw[GPW];
+        static_for<GPW>([&](auto j) { lg_read<QT>(slot, wave * GPW + j, lane, raw[j]); });
+        int row = gb / nit, it = gb - row * nit;
+        float acc = 0.f;
+        static_for<GPW>([&](auto j) {
+          const int gg = gb + j;
+          if (gg < ngroups) {
+            cu_compute<QT>(raw[j], it, nch, xq, ms, acc);
+            // one row sum per row this wave finished or leaves in this step
+            if (it == nit - 1 || j == GPW - 1 || gg == ngroups - 1) {
+              const float v = cu_wave_sum(acc);
+              if (lane == 0) atomicAdd(&rowacc[row], v);
+              acc = 0.f;
+            }
+          }
+          if (++it == nit) { it = 0; ++row; }
+        });
+      }
+      lg_barrier();
+    }
+    CU_STAMP(4);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    lg_barrier();  // final: every row sum is in rowacc
+    CU_STAMP(5);
+  };
+  float2 rope = make_float2(1.f, 0.f);
+  if (loader) {
+    if (!fmt1) loader_path(FmtTag<QT0>{});
+    else loader_path(FmtTag<QT1>{});
+    return;
+  }
+  if (!fmt1) consumer_path(FmtTag<QT0>{}, rope);
+  else consumer_path(FmtTag<QT1>{}, rope);
+  auto flush_ts = [&]() {
+    if (a.dbg_ts && lane == 0 && (wave == 0 || wave == LG_NG - 1))
+      for (int i = 0; i < 8; ++i) a.dbg_ts[((size_t)blockIdx.x * 2 + (wave != 0)) * 8 + i] = ts[i];
+  };
+  if (wave != 0) {
+    flush_ts();
+    return;
+  }
+
+  // ---- pair epilogues: wave 0, one lane per pair
+  float s = 1.f;
+  if (a.norm_w) {
+    float t = 0.f;
+#pragma unroll
+    for (int w = 0; w < LG_NG; ++w) t += red[w];
+    s = rsqrtf(t / (float)a.K + a.eps);
+  }
+  int pos0 = 0, kv_blk0 = 0;
+  if (a.epi == EPI_QKV) {
+    pos0 = a.pos[0];
+    kv_blk0 = kv_block(a.block_table, a.max_ctx / KV_BLOCK, a.slot ? a.slot[0] : 0, pos0);
+  }
+  for (int p = lane; 2 * p < nrows; p += 64) {
+    const int grow = a.row_base + r0 + 2 * p;
+    const float v0 = rowacc[2 * p] * s, v1 = rowacc[2 * p + 1] * s;
+    if (a.epi == EPI_QKV) {
+      float2 t = rope;
+      if (p >= 64 || !a.rope_cs) {
+        int part, head, lrr;
+        qkv_part(a, grow, part, head, lrr);
+        const int pp = lrr >> 1;
+        if (a.rope_cs) {
+          t = a.rope_cs[(size_t)pos0 * (a.head_dim >> 1) + pp];
+        } else {
+          float sn, cs;
+          sincosf((float)pos0 * powf(a.rope_base, -2.f * (float)pp / (float)a.head_dim), &sn, &cs);
+          t = make_float2(cs, sn);
+        }
+      }
+      cu_qkv_epilogue(a, grow, v0, v1, t, pos0, kv_blk0);
+    } else {
+      gemv_epilogue1(a, grow, v0, v1, nullptr, 0, 0);
+    }
+  }
+  CU_STAMP(6);
+  flush_ts();
+}
+
+template <int QT>
+constexpr bool lg_supported() {
+  return QT == QT_Q4_K || QT == QT_Q5_K || QT == QT_Q6_K || QT == QT_Q4_0 || QT == QT_Q8_0;
+}
+
+// returns false when the shape does not fit (then the register kernels run)
+template <int QT0, int QT1>
+bool launch_gemv_lds(const GemvArgs& a, hipStream_t st) {
+  if constexpr (!same_xlayout<QT0, QT1> || !lg_supported<QT0>() || !lg_supported<QT1>()) {
+    return false;
+  } else {
+    // AIOS_GEMV_LDS: 0 = off, 1 = projections >= 96 KB per CU (default), 2 = every shape
+    static const int mode = [] {
+      const char* e = std::getenv("AIOS_GEMV_LDS");
+      return e ? std::atoi(e) : 1;
+    }();
+    if (!mode || a.B != 1 || a.tune_dbg || (a.kernel_sel != 0 && a.kernel_sel != 3)) return false;
+    constexpr int W = QFmt<QT0>::W, R = QFmt<QT0>::RUNS;
+    const int nch = a.K / W;
+    if (nch % 64) return false;
+    const int npairs = a.N / 2;
+    const int G = std::min(a.tune_grid > 0 ? a.tune_grid : device_cu_count(), npairs);
+    auto rup = [](int n, int g) { return (n + g - 1) / g; };
+    CuPlan pl{G, npairs, (2 * rup(npairs, G) + 3) & ~3};
+    if (QT0 != QT1 && a.nseg > 1) {
+      const int np0 = a.seg_row0[a.nseg - 1] / 2;
+      if (G < 2 || np0 < 1 || np0 >= npairs) return false;
+      const double b0 = (double)np0 * cu_fmt_bytes_per_256(QT0), b1 = (double)(npairs - np0) * cu_fmt_bytes_per_256(QT1);
+      int g0 = (int)(G * b0 / (b0 + b1) + 0.5);
+      g0 = std::max(1, std::min(G - 1, g0));
+      const int most = std::max(rup(np0, g0), rup(npairs - np0, G - g0));
+      pl = CuPlan{g0, np0, (2 * most + 3) & ~3};
+    }
+    // small projections (QKV, O: <= ~60 KB per CU) stay on the row-pair kernel: the engine's fixed
+    // start-up (first slot lands ~3-4 us after issue, behind the CU's whole prologue burst) and its
+    // barrier steps cost more than the row kernel's x-staging stall there (tools/gemv_cu_probe.py:
+    // O 6.96 vs 5.60 us, QKV 8.73 vs 8.38; gate_up 17.35 vs 19.39, down 13.8 vs 15.2, lm_head 24.8
+    // vs 25.9).  AIOS_GEMV_LDS=2 forces the engine for every shape.
+    if (mode != 2 && a.kernel_sel != 3) {
+      double bytes = 0;
+      for (int sg = 0; sg < a.nseg; ++sg)
+        bytes += (double)a.seg[sg].rows * a.K / 256.0 * cu_fmt_bytes_per_256(a.seg[sg].qtype);
+      if (bytes / G < 96.0 * 1024) return false;
+    }
+    const size_t head = (64 + (size_t)pl.racc_n) * 4 + (size_t)nch * R * 8 + (size_t)a.K;
+    const size_t ringb = std::max(LgLayout<QT0>::R * LgLayout<QT0>::slot_bytes, LgLayout<QT1>::R * LgLayout<QT1>::slot_bytes);
+    const size_t lds = (head + 255) / 256 * 256 + ringb;
+    if (lds > 160 * 1024) return false;
+    hipLaunchKernelGGL((gemv_lds_b1<QT0, QT1>), dim3(G), dim3(LG_THREADS), lds, st, a, pl);
+    return true;
+  }
+}

@@ -214,25 +214,27 @@ __device__ __forceinline__ int dpp_xor1_i(int v) { return __builtin_amdgcn_mov_d
 // (1 for K <= 4096 at B = 1; 4 for the long-K down projection, K <= 16384)
 template <int NPF>
 struct StagePre {
-  float4 x0[NPF], x1[NPF], g0, g1;
+  float4 x0[NPF], x1[NPF], g0[NPF], g1[NPF];
 };
+// tid / nthr: the staging threads (default: the whole workgroup)
 template <int NPF>
-__device__ __forceinline__ void q8_stage_prefetch(const GemvArgs& a, StagePre<NPF>& pf) {
+__device__ __forceinline__ void q8_stage_prefetch(const GemvArgs& a, StagePre<NPF>& pf, int tid = -1, int nthr = 0) {
+  if (tid < 0) { tid = threadIdx.x; nthr = blockDim.x; }
   const int noct = a.K >> 3, total = a.B * noct;
 #pragma unroll
   for (int i = 0; i < NPF; ++i) {
-    const int t = threadIdx.x + i * blockDim.x;
+    const int t = tid + i * nthr;
     // past the end: re-read octet 0 (in bounds, unused) -- no branch around the load
     const int tt = t < total ? t : 0;
     const int b = tt / noct, o = tt - b * noct;
     const float* src = a.x + (size_t)b * a.ldx + 8 * o;
     pf.x0[i] = *(const float4*)src;
     pf.x1[i] = *(const float4*)(src + 4);
-    if (i == 0) {
-      const float* g = a.norm_w ? a.norm_w + 8 * o : src;
-      pf.g0 = *(const float4*)g;
-      pf.g1 = *(const float4*)(g + 4);
-    }
+    // the norm weights of every prefetched pass too: a load issued after the weight stream would
+    // make its wait cover every weight load in flight
+    const float* g = a.norm_w ? a.norm_w + 8 * o : src;
+    pf.g0[i] = *(const float4*)g;
+    pf.g1[i] = *(const float4*)(g + 4);
   }
 }
 
@@ -286,7 +288,8 @@ __device__ __forceinline__ void q8_octet(const GemvArgs& a, int b, int o, float4
 
 template <int QT, int B, int NPF>
 __device__ __forceinline__ void q8_stage(const GemvArgs& a, int8_t* xq, float2* ms, float* red,
-                                         const StagePre<NPF>& pf) {
+                                         const StagePre<NPF>& pf, int tid = -1, int nthr = 0) {
+  if (tid < 0) { tid = threadIdx.x; nthr = blockDim.x; }
   const int noct = a.K >> 3, total = a.B * noct;
   float ssq[B];
 #pragma unroll
@@ -294,18 +297,13 @@ __device__ __forceinline__ void q8_stage(const GemvArgs& a, int8_t* xq, float2* 
   // the prefetched passes, fully unrolled so the prefetch registers never become an indexed array
 #pragma unroll
   for (int i = 0; i < NPF; ++i) {
-    const int t = threadIdx.x + i * blockDim.x;
+    const int t = tid + i * nthr;
     if (t < total) {
       const int b = t / noct, o = t - b * noct;
-      float4 g0 = pf.g0, g1 = pf.g1;
-      if (i > 0 && a.norm_w) {
-        g0 = *(const float4*)(a.norm_w + 8 * o);
-        g1 = *(const float4*)(a.norm_w + 8 * o + 4);
-      }
-      q8_octet<QT, B>(a, b, o, pf.x0[i], pf.x1[i], g0, g1, xq, ms, ssq);
+      q8_octet<QT, B>(a, b, o, pf.x0[i], pf.x1[i], pf.g0[i], pf.g1[i], xq, ms, ssq);
     }
   }
-  for (int t = threadIdx.x + NPF * blockDim.x; t < total; t += blockDim.x) {
+  for (int t = tid + NPF * nthr; t < total; t += nthr) {
     const int b = t / noct, o = t - b * noct;
     const float* src = a.x + (size_t)b * a.ldx + 8 * o;
     const float4 f0 = *(const float4*)src, f1 = *(const float4*)(src + 4);
@@ -317,7 +315,7 @@ __device__ __forceinline__ void q8_stage(const GemvArgs& a, int8_t* xq, float2* 
     q8_octet<QT, B>(a, b, o, f0, f1, g0, g1, xq, ms, ssq);
   }
   if (a.norm_w) {
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int wave = tid >> 6, lane = tid & 63;
 #pragma unroll
     for (int b = 0; b < B; ++b) {
       const float s = wave_sum(ssq[b]);

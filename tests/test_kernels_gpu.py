@@ -225,6 +225,104 @@ def test_gemv_qkv_rope_kv(E, mixed, q8):
         assert torch.allclose(vc[s, :, p].float().cpu(), vr[b], atol=2e-2, rtol=1e-2)
 
 
+# ---- one-workgroup-per-CU batch-1 GEMVs: sel 2 = register-streaming (kernels/gemv_cu.h), 3 = the
+# LDS-DMA loader/consumer engine (kernels/gemv_lds.h; needs K / chunk % 64 == 0, else it falls back);
+# pair ranges split over workgroups, tune_grid forces the workgroup count (ragged splits, > 64 pairs
+# per workgroup so the epilogue wave takes a second pass, rows straddling two waves / two slots)
+B1_SELS = [2, 3]
+
+
+@pytest.mark.parametrize("t", [GGMLType.Q4_K, GGMLType.Q6_K, GGMLType.Q5_K, GGMLType.Q4_0, GGMLType.Q8_0])
+@pytest.mark.parametrize("K", [2304, 4096, 14336])
+@pytest.mark.parametrize("grid", [0, 3, 37])
+@pytest.mark.parametrize("sel", B1_SELS)
+def test_gemv_b1_cu_store(E, t, K, grid, sel):
+    N = 1030
+    m, W = qmat(E, t, N, K, seed=31, std=0.02)
+    x = torch.randn(1, K, device="cuda")
+    nw = torch.rand(K, device="cuda") + 0.5
+    y = torch.zeros(1, N, device="cuda")
+    E.gemv([m], 1, x.data_ptr(), K, nw.data_ptr(), 1e-5, y.data_ptr(), N, E.EPI_STORE, stream(), 0, 1, grid,
+           kernel_sel=sel)
+    torch.cuda.synchronize()
+    xc = x.cpu()
+    xn = q8_ref(xc * nw.cpu()) * torch.rsqrt((xc * xc).mean(-1, keepdim=True) + 1e-5)
+    ref = xn @ W.T
+    assert torch.allclose(y.cpu(), ref, atol=5e-3, rtol=5e-3), (y.cpu() - ref).abs().max()
+
+
+@pytest.mark.parametrize("grid", [0, 2, 11])
+@pytest.mark.parametrize("sel", B1_SELS)
+def test_gemv_b1_cu_swiglu_resid(E, grid, sel):
+    K, F = 4096, 600
+    gate, Wg = qmat(E, GGMLType.Q4_K, F, K, seed=32, std=0.02)
+    up, Wu = qmat(E, GGMLType.Q4_K, F, K, seed=33, std=0.02)
+    # interleaved (gate_i, up_i) rows in one Q4_K matrix, as the loader repacks ffn_gate/ffn_up
+    inter = torch.empty(2 * F, K)
+    inter[0::2], inter[1::2] = Wg, Wu
+    raw = quantize(inter.numpy(), GGMLType.Q4_K)
+    Wgu = torch.from_numpy(dequantize(raw, GGMLType.Q4_K).reshape(2 * F, K).copy())
+    gu = E.QMatrix(int(GGMLType.Q4_K), 2 * F, K, raw)
+    x = torch.randn(1, K, device="cuda") * 3
+    nw = torch.rand(K, device="cuda") + 0.5
+    out = torch.zeros(1, F, device="cuda")
+    E.gemv([gu], 1, x.data_ptr(), K, nw.data_ptr(), 1e-5, out.data_ptr(), F, E.EPI_SWIGLU, stream(), 0, 1, grid,
+           kernel_sel=sel)
+    torch.cuda.synchronize()
+    xc = x.cpu()
+    xn = q8_ref(xc * nw.cpu()) * torch.rsqrt((xc * xc).mean(-1, keepdim=True) + 1e-5)
+    h = xn @ Wgu.T
+    ref = torch.nn.functional.silu(h[:, 0::2]) * h[:, 1::2]
+    assert torch.allclose(out.cpu(), ref, atol=5e-3, rtol=5e-3), (out.cpu() - ref).abs().max()
+    y0 = torch.randn(1, 2 * F, device="cuda")
+    y = y0.clone()
+    E.gemv([gu], 1, x.data_ptr(), K, 0, 1e-5, y.data_ptr(), 2 * F, E.EPI_RESID, stream(), 0, 1, grid,
+           kernel_sel=sel)
+    torch.cuda.synchronize()
+    ref = y0.cpu() + q8_ref(xc) @ Wgu.T
+    assert torch.allclose(y.cpu(), ref, atol=5e-3, rtol=5e-3), (y.cpu() - ref).abs().max()
+
+
+@pytest.mark.parametrize("mixed", [False, True])
+@pytest.mark.parametrize("table", [False, True])
+@pytest.mark.parametrize("grid", [0, 1, 5])
+@pytest.mark.parametrize("sel", B1_SELS)
+def test_gemv_b1_cu_qkv(E, mixed, table, grid, sel):
+    d, H, Hkv, hd, max_ctx, slots = 2048, 8, 2, 64, 256, 2
+    wq, Wq = qmat(E, GGMLType.Q4_K, H * hd, d, seed=34)
+    wk, Wk = qmat(E, GGMLType.Q4_K, Hkv * hd, d, seed=35)
+    wv, Wv = qmat(E, GGMLType.Q6_K if mixed else GGMLType.Q4_K, Hkv * hd, d, seed=36)
+    x = torch.randn(1, d, device="cuda")
+    nw = torch.rand(d, device="cuda") + 0.5
+    pos = torch.tensor([141], dtype=torch.int32, device="cuda")
+    slot = torch.tensor([1], dtype=torch.int32, device="cuda")
+    kp, bt = paged_cache(torch.zeros(slots, Hkv, max_ctx, hd, dtype=torch.bfloat16), shuffle=True, seed=4)
+    kp, bt = kp.cuda(), bt.cuda()
+    vp = torch.zeros_like(kp)
+    q = torch.zeros(1, H * hd, device="cuda")
+    cs = 0
+    if table:
+        p = torch.arange(hd // 2, dtype=torch.float64)
+        ang = torch.arange(max_ctx, dtype=torch.float64)[:, None] * torch.pow(10000.0, -2.0 * p / hd)[None]
+        rope_t = torch.stack([torch.cos(ang), torch.sin(ang)], -1).float().contiguous().cuda()
+        cs = rope_t.data_ptr()
+    E.gemv_qkv([wq, wk, wv], 1, x.data_ptr(), d, nw.data_ptr(), 1e-5, q.data_ptr(), 0, hd, H, Hkv, max_ctx, 0,
+               10000.0, pos.data_ptr(), slot.data_ptr(), kp.data_ptr(), vp.data_ptr(), stream(), 1,
+               block_table=bt.data_ptr(), rope_cs=cs, tune_grid=grid, kernel_sel=sel)
+    torch.cuda.synchronize()
+    kc, vc = unpaged(kp, slots, max_ctx, bt), unpaged(vp, slots, max_ctx, bt)
+    xc = x.cpu()
+    xn = q8_ref(xc * nw.cpu()) * torch.rsqrt((xc * xc).mean(-1, keepdim=True) + 1e-5)
+    qr = rope_ref((xn @ Wq.T).view(1, H, hd), pos.cpu(), 10000.0)
+    kr = rope_ref((xn @ Wk.T).view(1, Hkv, hd), pos.cpu(), 10000.0)
+    vr = (xn @ Wv.T).view(1, Hkv, hd)
+    assert torch.allclose(q.cpu().view(1, H, hd), qr, atol=3e-3, rtol=3e-3), (q.cpu().view(1, H, hd) - qr).abs().max()
+    assert torch.allclose(kc[1, :, 141].float().cpu(), kr[0], atol=2e-2, rtol=1e-2)
+    assert torch.allclose(vc[1, :, 141].float().cpu(), vr[0], atol=2e-2, rtol=1e-2)
+    # nothing else in the cache was written
+    assert int((kc != 0).sum()) == Hkv * hd and int((vc != 0).sum()) == Hkv * hd
+
+
 @pytest.mark.parametrize("hd,H,Hkv", [(64, 8, 1), (128, 32, 8), (64, 32, 4), (128, 40, 8)])
 @pytest.mark.parametrize("lens,max_ctx", [([1], 256), ([37, 200], 256), ([64, 65, 129, 1], 256),
                                           ([256, 255, 192], 256),

@@ -1,0 +1,120 @@
+"""Decode-GEMV phase anatomy on MI355X: per Mistral-7B projection, the row-pair int8 GEMV vs the
+CU-balanced register-streaming one (kernels/gemv_cu.h) vs the LDS-DMA loader/consumer engine
+(kernels/gemv_lds.h, the default), all graph-replayed over rotating weight copies (> the 256 MB
+Infinity Cache, so the bytes come from HBM as in the decode step), plus the default kernel's
+in-kernel phase timestamps (s_memrealtime, 10 ns ticks) across its workgroups: start skew, first loads
+issued, x staged, barrier, compute done, epilogue done.
+
+python tools/gemv_cu_probe.py [--json out.json]
+"""
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import numpy as np
+import torch
+
+from aios_amd.gguf.quants import BLOCK_INFO, GGMLType
+from aios_amd.runtime import native
+
+Q4, Q6 = GGMLType.Q4_K, GGMLType.Q6_K
+SHAPES = [  # name, [(fmt, rows)], K, norm, epi
+    ("qkv", [(Q4, 5120), (Q6, 1024)], 4096, True, "STORE"),
+    ("o", [(Q4, 4096)], 4096, False, "RESID"),
+    ("gate_up", [(Q4, 28672)], 4096, True, "SWIGLU"),
+    ("down_q6k", [(Q6, 4096)], 14336, False, "RESID"),
+    ("down_q4k", [(Q4, 4096)], 14336, False, "RESID"),
+    ("lm_head", [(Q6, 32000)], 4096, True, "STORE"),
+]
+
+
+def pct(v, q):
+    return float(np.percentile(v, q))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--json", default=None)
+    ap.add_argument("--only", default="")
+    args = ap.parse_args()
+    E = native.require()
+    res = []
+    for name, segs, K, norm, epi in SHAPES:
+        if args.only and name not in args.only.split(","):
+            continue
+        nbytes = sum(BLOCK_INFO[t][1] * r * K // 256 for t, r in segs)
+        nrot = max(2, (640 << 20) // nbytes + 1)
+        mats = []
+        for i in range(nrot):
+            ms = []
+            for j, (t, r) in enumerate(segs):
+                m = E.QMatrix(int(t), r, K, np.zeros(BLOCK_INFO[t][1] * r * K // 256, dtype=np.uint8))
+                m.fill_random(7 + 3 * i + j, 0.02)
+                ms.append(m)
+            mats.append(ms)
+        N = sum(r for _, r in segs)
+        x = torch.randn(1, K, device="cuda")
+        nw = torch.rand(K, device="cuda") + 0.5
+        y = torch.zeros(1, N, device="cuda")
+        epic = getattr(E, "EPI_" + epi)
+        ldy = N // 2 if epi == "SWIGLU" else N
+
+        def launch(ms, sel, ts=0):
+            st = torch.cuda.current_stream().cuda_stream
+            E.gemv(ms, 1, x.data_ptr(), K, nw.data_ptr() if norm else 0, 1e-5, y.data_ptr(), ldy, epic, st, 0, 1,
+                   kernel_sel=sel, dbg_ts=ts)
+
+        row = dict(shape=name, mb=round(nbytes / 1e6, 1))
+        for sel, tag in ((1, "rows"), (2, "cu"), (3, "lds"), (0, "auto")):
+            for ms in mats:
+                launch(ms, sel)
+            torch.cuda.synchronize()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                for ms in mats:
+                    launch(ms, sel)
+            g.replay()
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            reps = 20
+            e0.record()
+            for _ in range(reps):
+                g.replay()
+            e1.record()
+            torch.cuda.synchronize()
+            us = e0.elapsed_time(e1) * 1e3 / (reps * nrot)
+            row[tag + "_us"] = round(us, 2)
+            row[tag + "_tbs"] = round(nbytes / us / 1e6, 2)
+        row["floor_us"] = round(E.bench_stream_read(nbytes // 4096 * 4096, nrot, 1, 4, 512, 20), 2)
+        # phase stamps of one cold launch (the copy least recently touched)
+        G = 256
+        ts = torch.zeros(G * 2 * 8, dtype=torch.int64, device="cuda")
+        launch(mats[0], 3)  # warm the code path
+        for ms in mats[1:]:
+            launch(ms, 3)
+        torch.cuda.synchronize()
+        launch(mats[0], 3, ts.data_ptr())
+        torch.cuda.synchronize()
+        t = ts.view(G, 2, 8).cpu().numpy().astype(np.float64)
+        live = t[:, 0, 0] > 0
+        t = t[live]
+        t0 = t[:, :, 0][t[:, :, 0] > 0].min()
+        rel = (t - t0) / 100.0  # 100 MHz -> us
+        phases = {"start": rel[:, 0, 0], "loads_issued": rel[:, 0, 1], "x_staged": rel[:, 0, 2],
+                  "barrier": rel[:, 0, 3], "compute_w0": rel[:, 0, 4], "compute_w15": rel[:, 1, 4],
+                  "final_barrier": rel[:, 0, 5], "epilogue": rel[:, 0, 6]}
+        row["stamps_us"] = {k: [round(pct(v, q), 2) for q in (0, 50, 100)] for k, v in phases.items()}
+        res.append(row)
+        print(json.dumps(row), flush=True)
+        del mats
+        torch.cuda.empty_cache()
+    if args.json:
+        with open(args.json, "w") as f:
+            json.dump(res, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
