@@ -139,6 +139,9 @@ class Engine {
   void layer_decode(int l, int B);
   void gemv(const std::vector<const QMat*>& segs, int N, int K, int B, const float* x, int ldx, const float* norm_w,
             float* y, int ldy, int epi, int layer);
+  GemvArgs gemv_args(const std::vector<const QMat*>& segs, int N, int K, int B, const float* x, int ldx,
+                     const float* norm_w, float* y, int ldy, int epi, int layer);
+  bool attn_block_on(int B) const;
   QMat alloc_qmat(int qt, int rows, int cols);
   QMat upload_qmat(int qt, int rows, int cols, const void* host, size_t nbytes);
   // load-time staging: two device buffers (tensor i repacks while i+1 uploads) fed through two
@@ -192,6 +195,12 @@ class Engine {
   uint8_t* d_mask_ = nullptr;
   int n_chunks_ = 0;
   int* attn_cnt_ = nullptr;  // [max(prefill_rows, max_batch)][n_kv_heads] combine tickets
+  // fused batch-1 attention block (kernels/attn_block.hip): per layer [QKV arrivals, heads
+  // published] hand-off counters zeroed at the start of every decode step, + a give-up flag
+  int* fuse_cnt_ = nullptr;
+  int* fuse_err_ = nullptr;
+  int fuse_attn_ = 0;        // AIOS_FUSE_ATTN: 0 three launches (default), 1 attention + O fused, 2 all three
+  void check_fuse_err();
   float2* rope_cs_ = nullptr;  // [max_ctx][head_dim/2] cos/sin computed in double on the host
   int prefill_rows_ = 64;  // rows of the prefill workspace
   float *pf_x_ = nullptr, *pf_q_ = nullptr, *pf_attn_ = nullptr, *pf_ff_ = nullptr, *pf_qkv_ = nullptr;

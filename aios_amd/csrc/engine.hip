@@ -457,6 +457,11 @@ void Engine::finalize() {
     const size_t nc = (size_t)std::max(prefill_rows_, Bm) * H;  // decode attention tickets [row][head]
     attn_cnt_ = (int*)dmalloc(nc * 4);
     HIP_CHECK(hipMemset(attn_cnt_, 0, nc * 4));
+    fuse_cnt_ = (int*)dmalloc(((size_t)cfg_.n_layers * 2 + 1) * 4);
+    HIP_CHECK(hipMemset(fuse_cnt_, 0, ((size_t)cfg_.n_layers * 2 + 1) * 4));
+    fuse_err_ = fuse_cnt_ + (size_t)cfg_.n_layers * 2;
+    const char* fe = std::getenv("AIOS_FUSE_ATTN");
+    fuse_attn_ = fe ? std::atoi(fe) : 0;  // measured slower than three launches: opt-in
   }
   {
     const int half = hd / 2;
@@ -611,6 +616,11 @@ static void apply_knobs(GemvArgs& a, const char* kind) {
 
 void Engine::gemv(const std::vector<const QMat*>& segs, int N, int K, int B, const float* x, int ldx,
                   const float* norm_w, float* y, int ldy, int epi, int layer) {
+  launch_gemv(gemv_args(segs, N, K, B, x, ldx, norm_w, y, ldy, epi, layer), stream_);
+}
+
+GemvArgs Engine::gemv_args(const std::vector<const QMat*>& segs, int N, int K, int B, const float* x, int ldx,
+                           const float* norm_w, float* y, int ldy, int epi, int layer) {
   GemvArgs a;
   std::memset(&a, 0, sizeof(a));
   a.act_q8 = cfg_.act_q8;
@@ -647,7 +657,24 @@ void Engine::gemv(const std::vector<const QMat*>& segs, int N, int K, int B, con
     a.v_cache = v_cache_ + (size_t)layer * layer_kv_elems_;
   }
   apply_knobs(a, K == cfg_.d_ff ? "DOWN" : (N == 2 * cfg_.d_ff ? "GU" : (N == cfg_.vocab_size ? "LM" : "O")));
-  launch_gemv(a, stream_);
+  return a;
+}
+
+// the fused attention block (kernels/attn_block.hip) serves batch-1 decode without TP on the
+// int8-activation GEMV path with the in-epilogue RoPE (shape / format checks per layer follow)
+bool Engine::attn_block_on(int B) const {
+  return fuse_attn_ && fuse_cnt_ && B == 1 && cfg_.tp_size == 1 && cfg_.act_q8 && !cfg_.qk_norm && !cfg_.rope_neox &&
+         !(dec_a16_ && dec_gemm_min_b_ > 0 && B >= dec_gemm_min_b_);
+}
+
+void Engine::check_fuse_err() {
+  if (!fuse_err_) return;
+  int e = 0;
+  HIP_CHECK(hipMemcpy(&e, fuse_err_, 4, hipMemcpyDeviceToHost));
+  if (e) {
+    HIP_CHECK(hipMemset(fuse_err_, 0, 4));
+    throw std::runtime_error("fused attention block: an in-launch hand-off gave up (50 ms wait)");
+  }
 }
 
 // QKV segments: group into launches where only the last segment may differ in format
@@ -733,6 +760,62 @@ void Engine::layer_decode(int l, int B) {
   const LayerW& L = layers_[l];
   const int d = cfg_.d_model, hd = cfg_.head_dim, qd = cfg_.n_heads * hd, kvd = cfg_.n_kv_heads * hd;
   const bool fused_qkv = !cfg_.qk_norm && !cfg_.rope_neox;
+  auto attn_args = [&]() {
+    AttnDecodeArgs a;
+    a.split = 0;
+    a.q = q_;
+    a.k_cache = k_cache_ + (size_t)l * layer_kv_elems_;
+    a.v_cache = v_cache_ + (size_t)l * layer_kv_elems_;
+    a.seq_len = d_seqlen_;
+    a.slot = d_slot_;
+    a.block_table = attn_bt_; a.bt_rows = attn_bt_rows_;
+    a.B = B; a.n_heads = cfg_.n_heads; a.n_kv_heads = cfg_.n_kv_heads; a.head_dim = hd; a.max_ctx = cfg_.max_ctx;
+    a.n_chunks = n_chunks_;
+    a.scale = 1.f / std::sqrt((float)hd);
+    a.o_part = opart_; a.ml = ml_; a.out = attn_; a.counters = attn_cnt_;
+    return a;
+  };
+  auto qkv_args = [&](const std::vector<const QMat*>& grp, int row0) {
+    int n = 0;
+    for (auto* m : grp) n += m->w.rows;
+    GemvArgs a;
+    std::memset(&a, 0, sizeof(a));
+    a.act_q8 = cfg_.act_q8;
+    a.nseg = (int)grp.size();
+    int r = 0;
+    for (int s = 0; s < a.nseg; ++s) { a.seg[s] = grp[s]->w; a.seg_row0[s] = r; r += grp[s]->w.rows; }
+    a.N = n; a.K = d; a.B = B; a.row_base = row0;
+    a.x = x_; a.ldx = d; a.norm_w = L.attn_norm; a.eps = cfg_.norm_eps;
+    if (fused_qkv) {
+      a.epi = EPI_QKV; a.y = q_; a.ldy = qd;
+      a.bias = L.bqkv;
+      a.head_dim = hd; a.q_dim = qd; a.kv_dim = kvd; a.n_kv_heads = cfg_.n_kv_heads; a.max_ctx = cfg_.max_ctx;
+      a.rope_neox = cfg_.rope_neox; a.rope_base = cfg_.rope_theta; a.rope_cs = rope_cs_;
+      a.pos = d_pos_; a.slot = d_slot_;
+      a.k_cache = k_cache_ + (size_t)l * layer_kv_elems_;
+      a.v_cache = v_cache_ + (size_t)l * layer_kv_elems_;
+      a.block_table = d_bt_;
+    } else {
+      a.epi = EPI_STORE; a.y = qkv_; a.ldy = qd + 2 * kvd;
+    }
+    apply_knobs(a, "QKV");
+    return a;
+  };
+  // ---- batch 1: QKV -> attention -> O as one launch
+  if (attn_block_on(B)) {
+    const auto grps = qkv_groups(L);
+    if (grps.size() == 1 && !L.bqkv) {
+      const GemvArgs qa = qkv_args(grps[0], 0);
+      const AttnDecodeArgs at = attn_args();
+      const GemvArgs oa = gemv_args({&L.wo}, d, qd, B, attn_, qd, nullptr, x_, d, EPI_RESID, l);
+      if (attn_block_supported(qa, at, oa)) {
+        launch_attn_block(qa, at, oa, fuse_cnt_ + 2 * (size_t)l, fuse_err_, fuse_attn_ >= 2, stream_);
+        gemv({&L.wgu}, 2 * cfg_.d_ff, d, B, x_, d, L.ffn_norm, ff_, cfg_.d_ff, EPI_SWIGLU, l);
+        gemv({&L.wdown}, d, cfg_.d_ff, B, ff_, cfg_.d_ff, nullptr, x_, d, EPI_RESID, l);
+        return;
+      }
+    }
+  }
   // ---- QKV (+RMSNorm prologue, RoPE + KV-cache epilogue)
   {
     int row0 = 0;
@@ -840,6 +923,8 @@ void Engine::lm_head(int B, const float* x, int ldx) {
 
 void Engine::enqueue_decode_step(int B) {
   const int d = cfg_.d_model, V = cfg_.vocab_size;
+  if (attn_block_on(B))  // the fused blocks' hand-off counters start every step at zero
+    HIP_CHECK(hipMemsetAsync(fuse_cnt_, 0, (size_t)cfg_.n_layers * 2 * 4, stream_));
   launch_get_rows(tok_embd_.w, d_tokens_, B, x_, d, 1.f, stream_);
   for (int l = 0; l < cfg_.n_layers; ++l) layer_decode(l, B);
   lm_head(B, x_, d);
@@ -1137,6 +1222,7 @@ std::vector<int> Engine::decode(const std::vector<int>& slots, const std::vector
   HIP_CHECK(hipMemcpyAsync(h_tok_out_, d_tokens_, B * 4, hipMemcpyDeviceToHost, stream_));
   HIP_CHECK(hipStreamSynchronize(stream_));
   sample_mask_ = false;
+  check_fuse_err();
   return std::vector<int>(h_tok_out_, h_tok_out_ + B);
 }
 
@@ -1251,7 +1337,10 @@ std::vector<int> Engine::decode_loop_history(int B, int from_pos, int n) {
   return out;
 }
 
-void Engine::synchronize() { HIP_CHECK(hipStreamSynchronize(stream_)); }
+void Engine::synchronize() {
+  HIP_CHECK(hipStreamSynchronize(stream_));
+  check_fuse_err();
+}
 
 void Engine::reset_graphs() {
   for (auto& kv : graphs_) hipGraphExecDestroy(kv.second);

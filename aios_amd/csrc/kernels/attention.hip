@@ -21,331 +21,9 @@
 // reads every partial's (m, l) in one parallel sweep (one lane per partial), then each thread
 // sums its outputs over the partials with independent loads -- the write-through hand-off of
 // CDNA guide §6 Guideline 16 / split-K item 2 -- and re-arms the counter.
-#include "../common.h"
-#include "../ops.h"
-#include "gemm_common.h"
+#include "attn_decode.h"
 
 namespace aios {
-
-__device__ __forceinline__ void st_wt(float* p, float v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ float ld_wt(const float* p) {
-  return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-template <int CTRL>
-__device__ __forceinline__ float dpp(float v) {
-  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, false));
-}
-// sum over aligned groups of N lanes (N = 8 or 16), result in every lane of the group
-template <int N>
-__device__ __forceinline__ float group_sum(float v) {
-  v += dpp<0xB1>(v);   // quad_perm [1,0,3,2]
-  v += dpp<0x4E>(v);   // quad_perm [2,3,0,1]
-  v += dpp<0x141>(v);  // row_half_mirror: lane i <-> 7-i within 8
-  if constexpr (N == 16) v += dpp<0x140>(v);  // row_mirror: lane i <-> 15-i within 16
-  return v;
-}
-// op(v[lane], v[lane ^ OFF]) for OFF = 8, 16, 32 without the LDS crossbar: DPP row rotate for 8;
-// for 16 / 32 the gfx950 v_permlane16/32_swap of v with itself returns the lower and the upper
-// row of every pair in r[0] / r[1] on all lanes, so op(r[0], r[1]) needs no lane select
-template <int OFF, typename Op>
-__device__ __forceinline__ float xlane_op(float v, Op op) {
-  if constexpr (OFF == 8) {
-    return op(v, dpp<0x128>(v));  // row_ror:8 within 16 lanes = lane ^ 8
-  } else if constexpr (OFF == 16) {
-    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-    return op(__uint_as_float(r[0]), __uint_as_float(r[1]));
-  } else {
-    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-    return op(__uint_as_float(r[0]), __uint_as_float(r[1]));
-  }
-}
-struct OpMax { __device__ float operator()(float a, float b) const { return fmaxf(a, b); } };
-struct OpAdd { __device__ float operator()(float a, float b) const { return a + b; } };
-// max / sum over the lanes that share (lane % LPK), i.e. across the 64/LPK key groups of a wave
-template <int LPK>
-__device__ __forceinline__ float keys_max(float v) {
-  if constexpr (LPK <= 8) v = xlane_op<8>(v, OpMax{});
-  if constexpr (LPK <= 16) v = xlane_op<16>(v, OpMax{});
-  return xlane_op<32>(v, OpMax{});
-}
-template <int LPK>
-__device__ __forceinline__ float keys_sum(float v) {
-  if constexpr (LPK <= 8) v = xlane_op<8>(v, OpAdd{});
-  if constexpr (LPK <= 16) v = xlane_op<16>(v, OpAdd{});
-  return xlane_op<32>(v, OpAdd{});
-}
-
-constexpr float kLog2e = 1.4426950408889634f;
-// masked-key score / empty-state max: finite, so exp2(kNeg - m) underflows to 0 and
-// exp2(kNeg - kNeg) = 1 without -inf compares on the hot path
-constexpr float kNeg = -1e30f;
-// raw v_exp_f32 (denormal results flush to 0, which is all a softmax weight needs); ocml's exp2f
-// adds a range-scaling compare + 2 selects per call
-__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
-
-__device__ __forceinline__ float dot2_bf16(uint32_t a, uint32_t b, float c) {
-  return __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(gbf16x2, a), __builtin_bit_cast(gbf16x2, b), c, false);
-}
-
-// One workgroup's share: heads [h0, h0 + G) of KV head kvh, keys of the passes sp, sp + P, ...
-// (P active workgroups per (row, head set); counters indexed by `ci`).  `ppw` = passes per
-// workgroup the split aims for (1: more workgroups, each one 128-key pass; 2: both buffers).
-//
-// VALU diet (the kernel is VALU-bound per CU once its loads are in flight): q . k runs on
-// v_dot2_f32_bf16 against q pre-rounded to bf16 pairs (4 instructions per 8 dims and head, as the
-// MFMA prefill path rounds q), P . V on packed v_pk_fma_f32 with the probabilities in fp32.
-template <int HD, int G>
-__device__ __forceinline__ void attn_core(const AttnDecodeArgs& a, int sp, int kvh, int h0, int ci, int P_max,
-                                          int ppw) {
-  constexpr int NW = 8;                // waves per workgroup
-  constexpr int LPK = HD / 8;          // lanes per key (8 dims per lane)
-  constexpr int KPS = 64 / LPK;        // keys per wave-instruction
-  constexpr int CH = 128;              // keys per workgroup pass
-  constexpr int KPW = CH / NW;         // keys per wave per pass
-  constexpr int STEPS = KPW / KPS;     // loads per lane per pass (each of K and V)
-  constexpr int NT = NW * 64;
-  __shared__ float s_o[NW][G][HD];
-  __shared__ float s_m[NW][G], s_l[NW][G];
-  __shared__ int s_last;
-
-  const int b = blockIdx.z;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int ksub = lane / LPK, dsl = lane % LPK;
-  static_assert(CH == KV_BLOCK, "one decode pass = one paged KV block");
-  const int slot = a.slot ? a.slot[b] : b;
-  // paged KV: pass c reads physical block bt[c]; a row-indexed table (bt_rows) is looked up
-  // without waiting for slot[b], so its load overlaps the seq_len / slot loads
-  const int maxb = a.max_ctx / KV_BLOCK;
-  const int* btr = a.block_table ? a.block_table + (size_t)(a.bt_rows ? b : slot) * maxb : nullptr;
-  const size_t blk_stride = (size_t)a.n_kv_heads * KV_BLOCK * HD;
-  const int koff = wave * KPW + ksub;  // this lane's key within a pass (+ s * KPS)
-  const bf16_t* kc = a.k_cache + (size_t)kvh * KV_BLOCK * HD + (size_t)koff * HD + dsl * 8;
-  const bf16_t* vc = a.v_cache + (size_t)kvh * KV_BLOCK * HD + (size_t)koff * HD + dsl * 8;
-  const int cmax = maxb - 1;           // last chunk with valid memory
-
-  const int len = a.seq_len[b];
-  const int nchunk = (len + CH - 1) / CH;
-  const int P = max(1, min((nchunk + ppw - 1) / ppw, P_max));
-  if (sp >= P) return;  // uniform: this workgroup has no chunk, issues no K/V traffic
-
-  // two passes in flight per workgroup: buffers A and B (static, so they stay in VGPRs)
-  uint4 kA[STEPS], vA[STEPS], kB[STEPS], vB[STEPS];
-  auto issue = [&](uint4 (&kr)[STEPS], uint4 (&vr)[STEPS], int chunk) __attribute__((always_inline)) {
-    const int c = min(chunk, cmax);  // clamped: always a mapped block
-    const size_t base = (size_t)(btr ? btr[c] : slot * maxb + c) * blk_stride;
-#pragma unroll
-    for (int s = 0; s < STEPS; ++s) kr[s] = *(const uint4*)(kc + base + (size_t)s * KPS * HD);
-#pragma unroll
-    for (int s = 0; s < STEPS; ++s) vr[s] = *(const uint4*)(vc + base + (size_t)s * KPS * HD);
-  };
-  issue(kA, vA, sp);
-  if (sp + P < nchunk) issue(kB, vB, sp + P);
-  const float qs = a.scale * kLog2e;  // scores in the log2 domain: exp2 below
-  uint32_t q2[G][4];                  // q * scale as bf16 pairs
-#pragma unroll
-  for (int g = 0; g < G; ++g) {
-    const float* qp = a.q + ((size_t)b * a.n_heads + h0 + g) * HD + dsl * 8;
-    const float4 q0 = *(const float4*)qp, q1 = *(const float4*)(qp + 4);
-    q2[g][0] = pk_bf16(q0.x * qs, q0.y * qs);
-    q2[g][1] = pk_bf16(q0.z * qs, q0.w * qs);
-    q2[g][2] = pk_bf16(q1.x * qs, q1.y * qs);
-    q2[g][3] = pk_bf16(q1.z * qs, q1.w * qs);
-  }
-  float m[G], l[G];
-  gf32x2 o[G][4];
-#pragma unroll
-  for (int g = 0; g < G; ++g) {
-    m[g] = kNeg;
-    l[g] = 0.f;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) o[g][i] = gf32x2{0.f, 0.f};
-  }
-  auto pass = [&](const uint4 (&kr)[STEPS], const uint4 (&vr)[STEPS], int c) __attribute__((always_inline)) {
-    // ---- scores of this lane's STEPS keys for the G heads (reduced over the key's LPK lanes)
-    float sc[STEPS][G];
-#pragma unroll
-    for (int s = 0; s < STEPS; ++s) {
-      const bool valid = c * CH + koff + s * KPS < len;
-#pragma unroll
-      for (int g = 0; g < G; ++g) {
-        float d = dot2_bf16(kr[s].x, q2[g][0], 0.f);
-        d = dot2_bf16(kr[s].y, q2[g][1], d);
-        d = dot2_bf16(kr[s].z, q2[g][2], d);
-        d = dot2_bf16(kr[s].w, q2[g][3], d);
-        d = group_sum<LPK>(d);
-        sc[s][g] = valid ? d : kNeg;
-      }
-    }
-    // ---- per-wave online softmax over this pass's KPW keys
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-      float mx = sc[0][g];
-#pragma unroll
-      for (int s = 1; s < STEPS; ++s) mx = fmaxf(mx, sc[s][g]);
-      mx = keys_max<LPK>(mx);
-      const float mn = fmaxf(m[g], mx);
-      const float alpha = fast_exp2(m[g] - mn);
-      float ps = 0.f;
-#pragma unroll
-      for (int s = 0; s < STEPS; ++s) {
-        const float p = fast_exp2(sc[s][g] - mn);
-        sc[s][g] = p;
-        ps += p;
-      }
-      l[g] = l[g] * alpha + keys_sum<LPK>(ps);
-      m[g] = mn;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) o[g][i] *= alpha;
-    }
-    // ---- P.V (lane-local over its keys; merged across key groups and waves at the end)
-#pragma unroll
-    for (int s = 0; s < STEPS; ++s) {
-      const uint32_t w[4] = {vr[s].x, vr[s].y, vr[s].z, vr[s].w};
-      gf32x2 vf[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) vf[i] = gf32x2{__uint_as_float(w[i] << 16), __uint_as_float(w[i] & 0xffff0000u)};
-#pragma unroll
-      for (int g = 0; g < G; ++g) {
-        const gf32x2 pp = gf32x2{sc[s][g], sc[s][g]};
-#pragma unroll
-        for (int i = 0; i < 4; ++i) o[g][i] = __builtin_elementwise_fma(pp, vf[i], o[g][i]);
-      }
-    }
-  };
-  for (int c = sp; c < nchunk; c += 2 * P) {
-    pass(kA, vA, c);
-    if (c + 2 * P < nchunk) issue(kA, vA, c + 2 * P);
-    if (c + P < nchunk) {
-      pass(kB, vB, c + P);
-      if (c + 3 * P < nchunk) issue(kB, vB, c + 3 * P);
-    }
-  }
-  // ---- merge the key groups of a wave (shuffles), then the 8 waves in LDS (one barrier)
-  float of[G][8];
-#pragma unroll
-  for (int g = 0; g < G; ++g)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      of[g][2 * i] = keys_sum<LPK>(o[g][i].x);
-      of[g][2 * i + 1] = keys_sum<LPK>(o[g][i].y);
-    }
-  if (ksub == 0) {
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-      float4* dst = (float4*)&s_o[wave][g][dsl * 8];
-      dst[0] = make_float4(of[g][0], of[g][1], of[g][2], of[g][3]);
-      dst[1] = make_float4(of[g][4], of[g][5], of[g][6], of[g][7]);
-    }
-  }
-  if (lane < G) {
-    // m/l are wave-uniform after keys_max/keys_sum; lane g publishes head g
-    float mv = m[0], lv = l[0];
-#pragma unroll
-    for (int g = 1; g < G; ++g)
-      if (lane == g) { mv = m[g]; lv = l[g]; }
-    s_m[wave][lane] = mv;
-    s_l[wave][lane] = lv;
-  }
-  __syncthreads();
-  const int nact = P;  // workgroups that arrive
-  for (int idx = threadIdx.x; idx < G * HD; idx += NT) {
-    const int g = idx / HD, d = idx - g * HD;
-    float M = s_m[0][g];
-#pragma unroll
-    for (int w = 1; w < NW; ++w) M = fmaxf(M, s_m[w][g]);
-    float L = 0.f, acc = 0.f;
-#pragma unroll
-    for (int w = 0; w < NW; ++w) {
-      const float sw = fast_exp2(s_m[w][g] - M);
-      L += sw * s_l[w][g];
-      acc += sw * s_o[w][g][d];
-    }
-    const int h = h0 + g;
-    if (nact == 1) {
-      a.out[((size_t)b * a.n_heads + h) * HD + d] = acc / L;
-    } else {
-      st_wt(a.o_part + (((size_t)b * a.n_heads + h) * a.n_chunks + sp) * HD + d, acc);
-      if (d == 0) {
-        float* ml = a.ml + (((size_t)b * a.n_heads + h) * a.n_chunks + sp) * 2;
-        st_wt(ml, M);
-        st_wt(ml + 1, L);
-      }
-    }
-  }
-  if (nact == 1) return;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
-  __syncthreads();
-  int* cnt = a.counters + (size_t)b * a.n_heads + ci;
-  if (threadIdx.x == 0) {
-    const int t = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    s_last = (t == nact - 1);
-  }
-  __syncthreads();
-  if (!s_last) return;
-  // ---- last arriver.  (1) one thread per (head, partial) loads that partial's (m, l);
-  //      (2) wave g reduces head g's max M and total L and turns them into normalised weights
-  //      w_p = exp2(m_p - M) / L in LDS; (3) every output sums w_p * o_p with 16 loads in flight.
-  //      Two memory round trips for up to 64 partials (was one per 8 partials).
-  __shared__ float s_pm[G][64], s_pl[G][64];
-  for (int i = threadIdx.x; i < G * nact; i += NT) {
-    const int g = i / nact, p = i - g * nact;
-    const float* mlp = a.ml + (((size_t)b * a.n_heads + h0 + g) * a.n_chunks + p) * 2;
-    s_pm[g][p] = ld_wt(mlp);
-    s_pl[g][p] = ld_wt(mlp + 1);
-  }
-  __syncthreads();
-  if (wave < G) {
-    const int g = wave;
-    const float mv = lane < nact ? s_pm[g][lane] : kNeg;
-    const float lv = lane < nact ? s_pl[g][lane] : 0.f;
-    float M = mv;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) M = fmaxf(M, __shfl_xor(M, o));
-    const float e = fast_exp2(mv - M);
-    float L = e * lv;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) L += __shfl_xor(L, o);
-    if (lane < nact) s_pm[g][lane] = e / L;
-  }
-  __syncthreads();
-  for (int idx = threadIdx.x; idx < G * HD; idx += NT) {
-    const int g = idx / HD, d = idx - g * HD;
-    const int h = h0 + g;
-    const float* op = a.o_part + ((size_t)b * a.n_heads + h) * a.n_chunks * HD + d;
-    float acc = 0.f;
-    for (int c = 0; c < nact; c += 16) {
-      float ov[16];
-#pragma unroll
-      for (int j = 0; j < 16; ++j) ov[j] = ld_wt(op + (size_t)min(c + j, nact - 1) * HD);
-#pragma unroll
-      for (int j = 0; j < 16; ++j)
-        if (c + j < nact) acc = fmaf(s_pm[g][c + j], ov[j], acc);
-    }
-    a.out[((size_t)b * a.n_heads + h) * HD + d] = acc;
-  }
-  if (threadIdx.x == 0) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
-}
-
-// Up to ATTN_SPLIT_LEN keys the G query heads of a KV head are split over G workgroups (one head
-// each; the K/V re-reads hit L2): 4x less dot / softmax / P.V work per workgroup on the latency-
-// bound short contexts of agent turns.  Beyond that one workgroup set per (KV head, head set of
-// GL <= 4 query heads) computes its heads (the KV stream, not the arithmetic, dominates; GL = 4
-// keeps G = 8 groups in registers).  The grid is flat (one x-slot per role of the larger mode)
-// and each workgroup derives its role from seq_len, so a hipGraph-captured launch sized for
-// max_ctx carries no idle head-split grid (round-2 probe: 384 idle 512-thread workgroups cost
-// 4 us at a 256-key context).
-constexpr int ATTN_SPLIT_LEN = 512;
-template <int G>
-struct AttnGL { static constexpr int value = (G % 4 == 0) ? 4 : G; };
-
-struct AttnSplit {
-  int p_long;   // workgroups per (row, head set) in the long mode
-  int p_short;  // workgroups per (row, head) in the short mode
-  int ppw;      // passes per workgroup the split aims for
-};
 
 template <int HD, int G>
 __global__ void __launch_bounds__(512) attn_decode_kernel(AttnDecodeArgs a, AttnSplit sp_) {
@@ -364,24 +42,10 @@ __global__ void __launch_bounds__(512) attn_decode_kernel(AttnDecodeArgs a, Attn
   }
 }
 
-static int env_int(const char* k, int dflt) {
-  const char* e = std::getenv(k);
-  return e ? std::atoi(e) : dflt;
-}
-
 template <int HD>
 static void launch_hd(const AttnDecodeArgs& a, int G, hipStream_t st) {
-  const int nch = std::max(1, a.max_ctx / 128);  // 128-key passes
   AttnSplit sp;
-  sp.p_long = std::max(1, std::min(nch, a.split / ATTN_CHUNK));
-  // short mode: one workgroup per query head walks all (<= 4) passes -- the probe's best at
-  // <= 256 keys (a combine costs more than the second pass it would spread)
-  sp.p_short = std::max(1, std::min(4, env_int("AIOS_ATTN_SHORT_P", 1)));
-  sp.ppw = std::max(1, std::min(2, env_int("AIOS_ATTN_PPW", 1)));
-  if (sp.p_long > a.n_chunks || sp.p_long > 64 || sp.p_short > a.n_chunks)
-    throw std::runtime_error("attn_decode: more splits than partial buffers / 64");
-  const int GL = (G % 4 == 0) ? 4 : G;
-  const int nwg = std::max(a.n_kv_heads * (G / GL) * sp.p_long, G > 1 ? a.n_heads * sp.p_short : 0);
+  const int nwg = attn_plan(a, G, sp);
   dim3 grid(nwg, 1, a.B);
   switch (G) {
     case 1: hipLaunchKernelGGL((attn_decode_kernel<HD, 1>), grid, dim3(512), 0, st, a, sp); break;

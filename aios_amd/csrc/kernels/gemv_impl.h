@@ -20,6 +20,7 @@
 #include "../common.h"
 #include "../gemv.h"
 #include "../qweight.h"
+#include "fuse.h"
 
 namespace aios {
 

@@ -217,7 +217,13 @@ struct StagePre {
   float4 x0[NPF], x1[NPF], g0[NPF], g1[NPF];
 };
 // tid / nthr: the staging threads (default: the whole workgroup)
-template <int NPF>
+// SC1: x was written earlier in the same (fused) launch -- read it with sc1 loads (fuse.h)
+template <bool SC1>
+__device__ __forceinline__ float4 ldx4(const float* p) {
+  if constexpr (SC1) return ld_sc1_f4(p);
+  else return *(const float4*)p;
+}
+template <int NPF, bool SC1 = false>
 __device__ __forceinline__ void q8_stage_prefetch(const GemvArgs& a, StagePre<NPF>& pf, int tid = -1, int nthr = 0) {
   if (tid < 0) { tid = threadIdx.x; nthr = blockDim.x; }
   const int noct = a.K >> 3, total = a.B * noct;
@@ -228,8 +234,8 @@ __device__ __forceinline__ void q8_stage_prefetch(const GemvArgs& a, StagePre<NP
     const int tt = t < total ? t : 0;
     const int b = tt / noct, o = tt - b * noct;
     const float* src = a.x + (size_t)b * a.ldx + 8 * o;
-    pf.x0[i] = *(const float4*)src;
-    pf.x1[i] = *(const float4*)(src + 4);
+    pf.x0[i] = ldx4<SC1>(src);
+    pf.x1[i] = ldx4<SC1>(src + 4);
     // the norm weights of every prefetched pass too: a load issued after the weight stream would
     // make its wait cover every weight load in flight
     const float* g = a.norm_w ? a.norm_w + 8 * o : src;
@@ -286,7 +292,7 @@ __device__ __forceinline__ void q8_octet(const GemvArgs& a, int b, int o, float4
   if (!(quarter & 1)) ms[((size_t)b * nch + c) * R + (s0 >> 4)] = make_float2(dx, dx * (float)isum);
 }
 
-template <int QT, int B, int NPF>
+template <int QT, int B, int NPF, bool SC1 = false>
 __device__ __forceinline__ void q8_stage(const GemvArgs& a, int8_t* xq, float2* ms, float* red,
                                          const StagePre<NPF>& pf, int tid = -1, int nthr = 0) {
   if (tid < 0) { tid = threadIdx.x; nthr = blockDim.x; }
@@ -306,7 +312,7 @@ __device__ __forceinline__ void q8_stage(const GemvArgs& a, int8_t* xq, float2* 
   for (int t = tid + NPF * nthr; t < total; t += nthr) {
     const int b = t / noct, o = t - b * noct;
     const float* src = a.x + (size_t)b * a.ldx + 8 * o;
-    const float4 f0 = *(const float4*)src, f1 = *(const float4*)(src + 4);
+    const float4 f0 = ldx4<SC1>(src), f1 = ldx4<SC1>(src + 4);
     float4 g0 = f0, g1 = f1;
     if (a.norm_w) {
       g0 = *(const float4*)(a.norm_w + 8 * o);
@@ -417,8 +423,10 @@ __device__ __forceinline__ void qkv_part(const GemvArgs& a, int grow, int& part,
   head = r / hd;
   lr = r - head * hd;
 }
+// wt: the outputs are consumed later in the same (fused) launch -- q and the K/V row are stored
+// write-through as 8- / 4-byte pairs (non-NeoX RoPE: the pair (da, db) is adjacent)
 __device__ __forceinline__ void gemv_epilogue1(const GemvArgs& a, int grow, float v0, float v1, const float2* rope_l,
-                                               int pos0, int kv_blk0) {
+                                               int pos0, int kv_blk0, bool wt = false) {
   const int nrow = a.row_base + a.N;
   switch (a.epi) {
     case EPI_STORE:
@@ -453,14 +461,25 @@ __device__ __forceinline__ void gemv_epilogue1(const GemvArgs& a, int grow, floa
       }
       if (part == 0) {
         float* q = a.y + head * hd;
-        q[da] = v0;
-        q[db] = v1;
+        if (wt && db == da + 1) {
+          st_sc1_f2(q + da, v0, v1);
+        } else if (wt) {
+          st_sc1_f32(q + da, v0);
+          st_sc1_f32(q + db, v1);
+        } else {
+          q[da] = v0;
+          q[db] = v1;
+        }
       } else {
         bf16_t* cache = (part == 1 ? a.k_cache : a.v_cache);
         // kv_blk0: the physical block of (slot, pos), looked up once in the prologue
         const size_t base = (((size_t)kv_blk0 * a.n_kv_heads + head) * KV_BLOCK + (pos0 % KV_BLOCK)) * hd;
-        cache[base + da] = f32_to_bf16(v0);
-        cache[base + db] = f32_to_bf16(v1);
+        if (wt) {  // the fused path requires the adjacent (non-NeoX) pair: one 4-byte store
+          st_sc1_u32(cache + base + da, (uint32_t)f32_to_bf16(v0) | ((uint32_t)f32_to_bf16(v1) << 16));
+        } else {
+          cache[base + da] = f32_to_bf16(v0);
+          cache[base + db] = f32_to_bf16(v1);
+        }
       }
     } break;
   }
@@ -492,9 +511,14 @@ struct FmtTag {
   static constexpr int value = QT;
 };
 
-template <int QT0, int QT1, int B, int U, int PIPE>
-__global__ void __launch_bounds__(Q8_WAVES * 64) gemv_q8_rows(GemvArgs a) {
+// The kernel body as a device function over a virtual grid (vblk of vgrid workgroups), so a fused
+// launch (attn_block.hip) can run it as one role.  FUSED: x is read with sc1 loads after the wait
+// on fz (the weights of the first item are already in flight), QKV outputs are stored write-through,
+// and the workgroup publishes on fz.sig when its rows are written.
+template <int QT0, int QT1, int B, int U, int PIPE, bool FUSED = false>
+__device__ __forceinline__ void q8_rows_body(const GemvArgs& a, int vblk, int vgrid, FuseEdge fz = FuseEdge{}) {
   static_assert(same_xlayout<QT0, QT1>, "mixed segments must share the activation layout");
+  static_assert(!FUSED || B == 1, "fused roles are batch-1");
   extern __shared__ __attribute__((aligned(16))) float smem[];
   constexpr bool MIXED = QT0 != QT1;
   constexpr int W = QFmt<QT0>::W, R = QFmt<QT0>::RUNS;
@@ -511,8 +535,8 @@ __global__ void __launch_bounds__(Q8_WAVES * 64) gemv_q8_rows(GemvArgs a) {
   const int srow2 = __builtin_amdgcn_readfirstlane(a.seg_row0[2]);
   const int np0 = (MIXED && a.nseg > 1) ? (a.nseg == 2 ? srow1 : srow2) >> 1 : npairs;
   const int nit = (nch + 64 * U - 1) / (64 * U);
-  const int stride = gridDim.x * Q8_WAVES;
-  const int wid = __builtin_amdgcn_readfirstlane(blockIdx.x * Q8_WAVES + wave);  // wave-uniform -> SGPR
+  const int stride = vgrid * Q8_WAVES;
+  const int wid = __builtin_amdgcn_readfirstlane(vblk * Q8_WAVES + wave);  // wave-uniform -> SGPR
 
   auto seg_idx = [&](int p, int& lrow) -> int {
     const int row = 2 * p;
@@ -592,7 +616,7 @@ __global__ void __launch_bounds__(Q8_WAVES * 64) gemv_q8_rows(GemvArgs a) {
     }
     if constexpr (B == 1) {
       const float2 v = wave_sum_pair(acc[0][0], acc[1][0]);
-      if (lane == 0) gemv_epilogue1(a, a.row_base + 2 * p, v.x * s[0], v.y * s[0], rope_l, pos0, kv_blk0);
+      if (lane == 0) gemv_epilogue1(a, a.row_base + 2 * p, v.x * s[0], v.y * s[0], rope_l, pos0, kv_blk0, FUSED);
     } else {
 #pragma unroll
       for (int r = 0; r < GEMV_ROWS; ++r)
@@ -669,10 +693,17 @@ __global__ void __launch_bounds__(Q8_WAVES * 64) gemv_q8_rows(GemvArgs a) {
 
   constexpr int NPF = (B == 1 && U >= 3) ? 4 : 1;
   StagePre<NPF> pf{};
-  q8_stage_prefetch(a, pf);  // x first: its wait then does not cover the weights
+  const bool waits = FUSED && fz.wait != nullptr;
+  if (!waits) q8_stage_prefetch(a, pf);  // x first: its wait then does not cover the weights
   if constexpr (!MIXED) {
     load(FmtTag<QT0>{}, wid, npairs, 0, bufA);  // weight loads in flight during the prologue
-    if (!(a.tune_dbg & 1)) q8_stage<QT0, B, NPF>(a, xq, ms, red, pf);
+    if constexpr (FUSED) {
+      if (waits) {  // x is produced in this launch: wait for it with the first weights in flight
+        fuse_wait(fz);
+        q8_stage_prefetch<NPF, true>(a, pf);
+      }
+    }
+    if (!(a.tune_dbg & 1)) q8_stage<QT0, B, NPF, FUSED>(a, xq, ms, red, pf);
     __syncthreads();
     run(FmtTag<QT0>{}, wid, npairs, stride, buf);
   } else {
@@ -708,6 +739,12 @@ __global__ void __launch_bounds__(Q8_WAVES * 64) gemv_q8_rows(GemvArgs a) {
       run(FmtTag<QT1>{}, np0 + (wid - W0), npairs, W - W0, buf1);
     }
   }
+  if constexpr (FUSED) fuse_signal(fz, 1);
+}
+
+template <int QT0, int QT1, int B, int U, int PIPE>
+__global__ void __launch_bounds__(Q8_WAVES * 64) gemv_q8_rows(GemvArgs a) {
+  q8_rows_body<QT0, QT1, B, U, PIPE>(a, blockIdx.x, gridDim.x);
 }
 
 template <int QT0, int QT1, int B>

@@ -79,6 +79,13 @@ constexpr int ATTN_CHUNK = 64;
 void launch_attn_decode(const AttnDecodeArgs& a, hipStream_t st);
 int attn_decode_split(int max_ctx, int B, int n_kv_heads);
 
+// batch-1 QKV GEMV -> attention -> O GEMV (+= residual) as one launch (kernels/attn_block.hip);
+// cnt: [2] hand-off counters zeroed before the launch, err: give-up flag; with_qkv = false: the
+// QKV GEMV is launched on its own first and only attention -> O share a launch
+bool attn_block_supported(const GemvArgs& qkv, const AttnDecodeArgs& at, const GemvArgs& o);
+void launch_attn_block(const GemvArgs& qkv, const AttnDecodeArgs& at, const GemvArgs& o, int* cnt, int* err,
+                       bool with_qkv, hipStream_t st);
+
 // causal flash attention for a prefill chunk of T tokens at positions [start, start+T) of one
 // slot, over the cached keys [0, start+T) (MFMA; kernels/attention_prefill.hip)
 struct AttnPrefillArgs {
