@@ -14,18 +14,19 @@ Reference: `api-gateway/src/{claude,openai,budget,router}.rs`.
   1000 entries, oldest evicted (router.rs:34-248).
 Streaming is real token streaming (SSE from the OpenAI-compatible / Anthropic APIs, the
 runtime's StreamInfer) -- the reference sent one chunk at the end.
+
+The ledger, the cache and the routing policy are the native C++ core (`aios_amd/native/gateway.cpp`,
+`_core.gateway`); this module keeps only the provider HTTP clients (aiohttp, streaming) and the
+asyncio request flow.
 """
 from __future__ import annotations
 
 import asyncio
-import hashlib
 import json
 import logging
 import os
-import sqlite3
-import threading
 import time
-from dataclasses import dataclass, field
+from dataclasses import dataclass
 from typing import AsyncIterator, Dict, List, Optional
 
 log = logging.getLogger("aios.gateway")
@@ -51,8 +52,14 @@ class Completion:
     provider: str = ""
 
 
+def _gw():
+    from ..core import load as load_core
+
+    return load_core().gateway
+
+
 def wants_json(prompt: str, system_prompt: str) -> bool:
-    return ("valid JSON" in prompt or "JSON object" in prompt or "respond with ONLY valid JSON" in system_prompt)
+    return _gw().wants_json(prompt, system_prompt)
 
 
 # ------------------------------------------------------------------------------------ providers
@@ -72,6 +79,8 @@ class Provider:
         yield c.text
 
     def cost(self, tin: int, tout: int) -> float:
+        if self.name in ("claude", "openai"):  # the native price table (gateway.cpp gw_cost)
+            return _gw().cost(self.name, int(tin), int(tout))
         return tin * self.price_in / 1e6 + tout * self.price_out / 1e6
 
 
@@ -324,144 +333,78 @@ def providers_from_env(env=os.environ) -> Dict[str, Provider]:
 
 
 # ------------------------------------------------------------------------------------ budget
-def _month_start(t: Optional[float] = None) -> int:
-    tm = time.gmtime(t if t is not None else time.time())
-    return int(time.mktime((tm.tm_year, tm.tm_mon, 1, 0, 0, 0, 0, 0, 0)) - time.timezone)
-
-
 class BudgetManager:
+    """Monthly budget ledger over the native `_core.gateway.BudgetLedger` (SQLite, persisted)."""
+
     def __init__(self, claude_budget=100.0, openai_budget=50.0, db_path: str = ":memory:"):
-        self.claude_budget, self.openai_budget = claude_budget, openai_budget
-        self.lock = threading.Lock()
         if db_path != ":memory:":
             os.makedirs(os.path.dirname(db_path) or ".", exist_ok=True)
-        self.db = sqlite3.connect(db_path, check_same_thread=False)
-        self.db.execute("CREATE TABLE IF NOT EXISTS usage (provider TEXT, model TEXT, input_tokens INTEGER,"
-                        " output_tokens INTEGER, cost_usd REAL, timestamp INTEGER, requesting_agent TEXT,"
-                        " task_id TEXT)")
-        self.db.commit()
-        self.month_start = _month_start()
-
-    def _used(self, provider: str) -> float:
-        row = self.db.execute("SELECT COALESCE(SUM(cost_usd), 0) FROM usage WHERE provider = ? AND timestamp >= ?",
-                              (provider, self.month_start)).fetchone()
-        return float(row[0])
-
-    def _maybe_reset(self):
-        ms = _month_start()
-        if ms > self.month_start:
-            log.info("new billing month: budget counters reset")
-            self.month_start = ms
+        self.ledger = _gw().BudgetLedger(float(claude_budget), float(openai_budget), db_path)
+        self.claude_budget, self.openai_budget = float(claude_budget), float(openai_budget)
 
     def record(self, provider: str, c: Completion, cost: float, agent: str = "", task: str = ""):
-        tin, tout = c.input_tokens, c.output_tokens
-        if tin == 0 and tout == 0 and c.tokens_used:
-            tin, tout = c.tokens_used // 2, c.tokens_used - c.tokens_used // 2
-        with self.lock:
-            self._maybe_reset()
-            self.db.execute("INSERT INTO usage VALUES (?,?,?,?,?,?,?,?)",
-                            (provider, c.model_used, tin, tout, cost, int(time.time()), agent, task))
-            self.db.commit()
-            for p, b in (("claude", self.claude_budget), ("openai", self.openai_budget)):
-                u = self._used(p)
-                if b > 0 and u > 0.8 * b:
-                    log.warning("%s budget warning: $%.2f / $%.2f (%d%%)", p, u, b, int(100 * u / b))
+        for w in self.ledger.record(provider, c.model_used, int(c.input_tokens), int(c.output_tokens),
+                                    int(c.tokens_used), float(cost), agent, task):
+            log.warning("%s", w)
 
     def provider_exceeded(self, provider: str) -> bool:
-        with self.lock:
-            self._maybe_reset()
-            if provider == "claude":
-                return self._used("claude") >= self.claude_budget
-            if provider == "openai":
-                return self._used("openai") >= self.openai_budget
-            return False  # qwen3 / local are not metered
+        return self.ledger.provider_exceeded(provider)
 
     def exceeded(self) -> bool:
-        return self.provider_exceeded("claude") and self.provider_exceeded("openai")
+        return self.ledger.exceeded()
 
     def status(self) -> dict:
-        with self.lock:
-            self._maybe_reset()
-            cu, ou = self._used("claude"), self._used("openai")
-        day = time.gmtime().tm_mday
-        return {"claude_monthly_budget_usd": self.claude_budget, "claude_used_usd": cu,
-                "openai_monthly_budget_usd": self.openai_budget, "openai_used_usd": ou,
-                "days_remaining": max(0, 30 - day), "daily_rate_usd": (cu + ou) / max(day, 1),
-                "budget_exceeded": cu >= self.claude_budget and ou >= self.openai_budget}
+        s = self.ledger.status()
+        return {k: (float(v) if k.endswith("_usd") else v) for k, v in s.items()}
 
     def usage(self, provider: str = "", days: int = 30) -> dict:
-        cutoff = int(time.time()) - max(days, 0) * 86400 if days > 0 else 0
-        q = "SELECT provider, model, input_tokens, output_tokens, cost_usd, timestamp, requesting_agent, task_id " \
-            "FROM usage WHERE timestamp >= ?"
-        args: list = [cutoff]
-        if provider:
-            q += " AND provider = ?"
-            args.append(provider)
-        with self.lock:
-            rows = self.db.execute(q + " ORDER BY timestamp", args).fetchall()
-        keys = ("provider", "model", "input_tokens", "output_tokens", "cost_usd", "timestamp", "requesting_agent",
-                "task_id")
-        recs = [dict(zip(keys, r)) for r in rows]
-        return {"records": recs, "total_cost_usd": sum(r["cost_usd"] for r in recs), "total_requests": len(recs),
-                "total_tokens": sum(r["input_tokens"] + r["output_tokens"] for r in recs)}
+        u = self.ledger.usage(provider, int(days))
+        u["total_cost_usd"] = float(u["total_cost_usd"])
+        for r in u["records"]:
+            r["cost_usd"] = float(r["cost_usd"])
+        return u
 
 
 # ------------------------------------------------------------------------------------ router
-FALLBACKS = {
-    "claude": ["openai", "qwen3", "local"],
-    "openai": ["claude", "qwen3", "local"],
-    "qwen3": ["claude", "openai", "local"],
-    "local": ["qwen3", "claude", "openai"],
-}
-
-
-@dataclass
-class _Cached:
-    resp: Completion
-    at: float
-
-
 class RequestRouter:
     def __init__(self, providers: Dict[str, Provider], budget: BudgetManager, ttl: float = 3600.0,
                  max_entries: int = 1000):
         self.providers, self.budget = providers, budget
-        self.ttl, self.max_entries = ttl, max_entries
-        self.cache: Dict[str, _Cached] = {}
+        self.ttl = float(ttl)
+        self.max_entries = max_entries  # builds the native cache
         self.stats = {"requests": 0, "cache_hits": 0, "fallbacks": 0, "errors": 0}
+
+    @property
+    def max_entries(self) -> int:
+        return self._max_entries
+
+    @max_entries.setter
+    def max_entries(self, n: int):
+        """Re-sizing starts an empty cache (the native cache's capacity is fixed)."""
+        self._max_entries = int(n)
+        self.cache = _gw().ResponseCache(self.ttl, self._max_entries)
 
     @staticmethod
     def key(prompt: str, system_prompt: str) -> str:
-        h = hashlib.sha256()
-        h.update(prompt.encode())
-        h.update(b"\x00")
-        h.update(system_prompt.encode())
-        return h.hexdigest()
+        return _gw().ResponseCache.key(prompt, system_prompt)
 
     def select(self, preferred: str) -> str:
-        if preferred:
-            return preferred
-        for p in ("claude", "openai", "qwen3"):
-            if self.providers[p].available() and not self.budget.provider_exceeded(p):
-                return p
-        return "local"
+        avail = {p: bool(self.providers[p].available()) for p in ("claude", "openai", "qwen3") if p in self.providers}
+        return _gw().select(preferred, avail, self.budget.ledger)
 
     def chain(self, primary: str, allow_fallback: bool) -> List[str]:
-        return [primary] + (FALLBACKS.get(primary, ["local"]) if allow_fallback else [])
+        return list(_gw().chain(primary, allow_fallback))
 
     def _cache_get(self, k: str) -> Optional[Completion]:
         c = self.cache.get(k)
         if c is None:
             return None
-        if time.time() - c.at >= self.ttl:
-            del self.cache[k]
-            return None
-        return c.resp
+        return Completion(text=c.text, tokens_used=c.tokens_used, latency_ms=c.latency_ms, model_used=c.model_used,
+                          input_tokens=c.input_tokens, output_tokens=c.output_tokens, provider=c.provider)
 
     def _cache_put(self, k: str, resp: Completion):
-        if k not in self.cache and len(self.cache) >= self.max_entries:
-            oldest = min(self.cache, key=lambda x: self.cache[x].at)
-            del self.cache[oldest]
-        self.cache[k] = _Cached(resp, time.time())
+        self.cache.put(k, _gw().Completion(resp.text, int(resp.tokens_used), int(resp.latency_ms), resp.model_used,
+                                           int(resp.input_tokens), int(resp.output_tokens), resp.provider))
 
     async def _try(self, name: str, req) -> Completion:
         p = self.providers.get(name)

@@ -6,6 +6,7 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include "gateway.h"
 #include "json.h"
 #include "memory.h"
 #include "orchestrator.h"
@@ -547,4 +548,53 @@ PYBIND11_MODULE(_core, m) {
         },
         py::arg("task"), py::arg("level"), py::arg("tools") = py::list(), py::arg("patterns") = py::list(),
         py::arg("max_tokens") = 2048);
+
+  // ---- api-gateway core (gateway.h)
+  auto gw = m.def_submodule("gateway", "api-gateway budget ledger, response cache and routing policy");
+  py::class_<GwCompletion>(gw, "Completion")
+      .def(py::init([](std::string text, int64_t tokens_used, int64_t latency_ms, std::string model_used,
+                       int64_t input_tokens, int64_t output_tokens, std::string provider) {
+             GwCompletion c;
+             c.text = std::move(text); c.tokens_used = tokens_used; c.latency_ms = latency_ms;
+             c.model_used = std::move(model_used); c.input_tokens = input_tokens; c.output_tokens = output_tokens;
+             c.provider = std::move(provider);
+             return c;
+           }),
+           py::arg("text") = "", py::arg("tokens_used") = 0, py::arg("latency_ms") = 0, py::arg("model_used") = "",
+           py::arg("input_tokens") = 0, py::arg("output_tokens") = 0, py::arg("provider") = "")
+      .def_readwrite("text", &GwCompletion::text)
+      .def_readwrite("tokens_used", &GwCompletion::tokens_used)
+      .def_readwrite("latency_ms", &GwCompletion::latency_ms)
+      .def_readwrite("model_used", &GwCompletion::model_used)
+      .def_readwrite("input_tokens", &GwCompletion::input_tokens)
+      .def_readwrite("output_tokens", &GwCompletion::output_tokens)
+      .def_readwrite("provider", &GwCompletion::provider);
+  py::class_<BudgetLedger>(gw, "BudgetLedger")
+      .def(py::init<double, double, const std::string&>(), py::arg("claude_budget") = 100.0,
+           py::arg("openai_budget") = 50.0, py::arg("db_path") = ":memory:")
+      .def("record", &BudgetLedger::record, py::arg("provider"), py::arg("model"), py::arg("input_tokens"),
+           py::arg("output_tokens"), py::arg("tokens_used"), py::arg("cost_usd"), py::arg("agent") = "",
+           py::arg("task") = "", py::arg("now") = 0, py::call_guard<py::gil_scoped_release>())
+      .def("used", &BudgetLedger::used, py::arg("provider"), py::arg("now") = 0, py::call_guard<py::gil_scoped_release>())
+      .def("provider_exceeded", &BudgetLedger::provider_exceeded, py::arg("provider"), py::arg("now") = 0,
+           py::call_guard<py::gil_scoped_release>())
+      .def("exceeded", &BudgetLedger::exceeded, py::arg("now") = 0, py::call_guard<py::gil_scoped_release>())
+      .def("status", [](BudgetLedger& b, int64_t now) { return to_py(b.status(now)); }, py::arg("now") = 0)
+      .def("usage", [](BudgetLedger& b, const std::string& p, int days, int64_t now) { return to_py(b.usage(p, days, now)); },
+           py::arg("provider") = "", py::arg("days") = 30, py::arg("now") = 0)
+      .def_property_readonly("claude_budget", &BudgetLedger::claude_budget)
+      .def_property_readonly("openai_budget", &BudgetLedger::openai_budget)
+      .def_static("month_start", &BudgetLedger::month_start);
+  py::class_<ResponseCache>(gw, "ResponseCache")
+      .def(py::init<double, size_t>(), py::arg("ttl") = 3600.0, py::arg("max_entries") = 1000)
+      .def_static("key", &ResponseCache::key)
+      .def("get", &ResponseCache::get, py::arg("key"), py::arg("now") = 0.0)
+      .def("put", &ResponseCache::put, py::arg("key"), py::arg("completion"), py::arg("now") = 0.0)
+      .def("__len__", &ResponseCache::size)
+      .def("clear", &ResponseCache::clear);
+  gw.def("select", &gw_select, py::arg("preferred"), py::arg("available"), py::arg("budget"), py::arg("now") = 0,
+         py::call_guard<py::gil_scoped_release>());
+  gw.def("chain", &gw_chain, py::arg("primary"), py::arg("allow_fallback"));
+  gw.def("cost", &gw_cost, py::arg("provider"), py::arg("input_tokens"), py::arg("output_tokens"));
+  gw.def("wants_json", &gw_wants_json, py::arg("prompt"), py::arg("system_prompt"));
 }
