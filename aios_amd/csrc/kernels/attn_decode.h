@@ -319,8 +319,10 @@ __device__ __forceinline__ void attn_core(const AttnDecodeArgs& a, int sp, int k
   // ---- last arriver.  (1) one thread per (head, partial) loads that partial's (m, l);
   //      (measured: one batch of (m, l) + o loads per output thread -- one round trip but 2x the
   //      loads, the (m, l) ones redundant across a head's 128 threads -- was 1.3 us SLOWER at 1000
-  //      keys, 10.09 vs 8.73 us; hoisting the block-table loads above the seq_len test did not
-  //      help either: 4.40 vs 4.18 us at 153 keys, tools/attn_probe.py)
+  //      keys, 10.09 vs 8.73 us; hoisting the block-table loads above the seq_len test, or
+  //      issuing pass 0's K/V before seq_len is read, did not help either: 4.32-4.40 vs 4.18 us
+  //      at 153 keys, tools/attn_probe.py -- the short-context launch is the 1.7 us launch chain
+  //      plus one K/V round trip plus the merge, not the table lookups)
   //      (2) wave g reduces head g's max M and total L and turns them into normalised weights
   //      w_p = exp2(m_p - M) / L in LDS; (3) every output sums w_p * o_p with 16 loads in flight.
   //      Two memory round trips for up to 64 partials (was one per 8 partials).
