@@ -11,6 +11,12 @@ from .base import BaseAgent, IntelligenceLevel, main_for
 
 WORKSPACE = os.environ.get("AIOS_WORKSPACE", "/var/lib/aios/workspace")
 LANGS = ("python", "rust", "cpp", "hip", "node", "go", "bash")
+EXT = {"python": "py", "rust": "rs", "cpp": "cpp", "hip": "hip", "node": "js", "go": "go", "bash": "sh"}
+AUTHOR = "aiOS creator <creator@aios.local>"  # git needs 'Name <email>'
+
+
+def gen_path(directory: str, stem: str, lang: str) -> str:
+    return os.path.join(directory, f"{slug(stem) or 'generated'}.{EXT.get(lang, 'txt')}")
 
 
 def slug(text: str) -> str:
@@ -52,17 +58,26 @@ class CreatorAgent(BaseAgent):
             r = await self.call_tool("fs.write", {"path": path, "content": spec["code"]})
             return {"success": r["success"], "path": path, **({} if r["success"] else {"error": r["error"]})}
         # no model available: the tool writes a documented skeleton
-        return await self.call_tool("code.generate", {"description": d, "language": lang,
-                                                      "path": inp.get("path", WORKSPACE)})
+        fp = inp.get("file_path") or gen_path(inp.get("path", WORKSPACE), d[:40], lang)
+        return await self.call_tool("code.generate", {"file_path": fp, "description": d, "language": lang,
+                                                      "create_dirs": True})
 
     async def init_repo(self, task: Dict[str, Any]) -> Dict[str, Any]:
         path = (task.get("input") or {}).get("path") or os.path.join(WORKSPACE, slug(task.get("description", "")))
         r = await self.call_tool("git.init", {"path": path})
         if not r["success"]:
             return r
-        await self.call_tool("git.add", {"path": path, "files": ["."]})
-        c = await self.call_tool("git.commit", {"path": path, "message": "Initial commit", "author": "aiOS creator"})
-        return {"success": True, "path": path, "commit": c.get("output", c.get("error"))}
+        try:
+            empty = not [n for n in os.listdir(path) if n != ".git"]
+        except OSError:
+            empty = False
+        if empty:  # a new repository: the initial commit carries a README
+            await self.call_tool("fs.write", {"path": os.path.join(path, "README.md"),
+                                              "content": f"# {os.path.basename(path)}\n\n{task.get('description', '')}\n"})
+        await self.call_tool("git.add", {"repo_path": path, "all": True})
+        c = await self.call_tool("git.commit", {"repo_path": path, "message": "Initial commit", "author": AUTHOR})
+        return {"success": c["success"], "path": path, "commit": c.get("output", {}).get("commit_hash") if c["success"]
+                else None, **({} if c["success"] else {"error": c.get("error")})}
 
     async def full_project(self, task: Dict[str, Any]) -> Dict[str, Any]:
         d = task.get("description", "")
@@ -78,8 +93,10 @@ class CreatorAgent(BaseAgent):
         files = plan.get("files", []) if isinstance(plan, dict) else []
         made = []
         for f in files[:10]:
-            r = await self.call_tool("code.generate", {"description": f.get("purpose", ""), "language": lang,
-                                                       "path": os.path.join(root, os.path.dirname(f.get("path", "")))})
+            rel = f.get("path") or gen_path("", f.get("purpose", "module"), lang)
+            r = await self.call_tool("code.generate", {"file_path": os.path.join(root, rel.lstrip("/")),
+                                                       "description": f.get("purpose", ""), "language": lang,
+                                                       "create_dirs": True})
             if r["success"]:
                 made.append(f.get("path"))
         repo = await self.init_repo({"input": {"path": root}})

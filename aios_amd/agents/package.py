@@ -22,6 +22,7 @@ class PackageAgent(BaseAgent):
     AGENT_TYPE = "package"
     CAPABILITIES = ("pkg.install", "pkg.remove", "pkg.update", "pkg.search", "pkg.list_installed", "sec.scan")
     ACTIONS = ((("uninstall", "remove", "purge"), "remove_package"),
+               (("list installed", "installed packages", "list packages"), "list_installed"),
                (("install",), "install_package"),
                (("upgrade", "update"), "update_all"),
                (("cve", "vulnerab"), "check_vulnerabilities"),

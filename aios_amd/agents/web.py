@@ -3,6 +3,7 @@
 webhook; think(OPERATIONAL) to summarise pages and to shape API calls)."""
 from __future__ import annotations
 
+import os
 import re
 import time
 from typing import Any, Dict
@@ -65,8 +66,12 @@ class WebAgent(BaseAgent):
 
     async def download(self, task: Dict[str, Any]) -> Dict[str, Any]:
         inp = task.get("input") or {}
-        return await self.call_tool("web.download", {"url": self._url(task),
-                                                     "path": inp.get("path", "/var/lib/aios/downloads/")})
+        url = self._url(task)
+        if not url:
+            return {"success": False, "error": "no URL in task"}
+        name = os.path.basename(url.split("?")[0].rstrip("/")) or "download"
+        dst = inp.get("destination") or os.path.join(inp.get("path", "/var/lib/aios/downloads"), name)
+        return await self.call_tool("web.download", {"url": url, "destination": dst, "create_dirs": True})
 
     async def monitor_url(self, task: Dict[str, Any]) -> Dict[str, Any]:
         url = self._url(task)

@@ -47,7 +47,7 @@ CapabilityChecker::CapabilityChecker() {
   register_agent("network-agent", {"net_read", "net_write", "net_scan", "firewall_read", "firewall_manage"});
   register_agent("security-agent",
                  {"sec_read", "sec_manage", "net_read", "net_scan", "process_read", "monitor_read", "fs_read"});
-  register_agent("monitoring-agent", {"monitor_read", "net_read", "process_read", "fs_read"});
+  register_agent("monitoring-agent", {"monitor_read", "net_read", "process_read", "fs_read", "hw_read"});
   register_agent("storage-agent",
                  {"fs_read", "fs_write", "fs_delete", "fs_permissions", "monitor_read", "process_manage"});
   register_agent("package-agent", {"pkg_read", "pkg_manage"});
