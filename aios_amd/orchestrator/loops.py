@@ -122,6 +122,7 @@ class ProactiveConfig:
     log_path: str = "/var/log/aios/orchestrator.log"
     network_probe: bool = True
     etc_probe: bool = True
+    sysfs_root: str = "/"
 
 
 def has_similar_active_goal(st: OrchestratorState, description: str) -> bool:
@@ -188,6 +189,21 @@ def proactive_candidates(st: OrchestratorState, cfg: ProactiveConfig) -> List[tu
             out.append((f"Log anomaly: {errs} ERROR/CRITICAL entries in recent logs. Investigate root cause and "
                         "resolve recurring errors.", 7))
     except OSError:
+        pass
+    try:  # MI355X RAS: uncorrectable HBM ECC / xGMI link errors, overtemperature (amdgpu sysfs)
+        gh = sysinfo.gpu_health(cfg.sysfs_root)
+        for p in gh["problems"]:
+            if p["kind"] == "uncorrectable_ecc":
+                out.append((f"GPU {p['card']} reports {p['count']} uncorrectable ECC errors "
+                            f"({', '.join(p['blocks'])}). Drain its model tiers, move them to healthy GPUs and "
+                            "schedule a GPU reset.", 9))
+            elif p["kind"] == "xgmi_link_errors":
+                out.append((f"GPU {p['card']} reports {p['count']} uncorrectable xGMI link errors. Move "
+                            "tensor-parallel tiers off this GPU and check the node's xGMI links.", 9))
+            else:
+                out.append((f"GPU {p['card']} is overheating ({p['temp_c']:.0f} C). Reduce its load and check "
+                            "cooling.", 8))
+    except Exception:  # pragma: no cover - no GPU sysfs
         pass
     if cfg.etc_probe:
         r = core.run_cmd(["find", "/etc", "-maxdepth", "2", "-perm", "-o+w", "-type", "f"], 10000)

@@ -198,6 +198,13 @@ class ManagementConsole:
         for g in sysinfo.amd_gpus():
             out.append(f'aios_gpu_busy_percent{{card="{g["card"]}"}} {g["busy_percent"]}')
             out.append(f'aios_gpu_vram_used_mb{{card="{g["card"]}"}} {g["vram_used_mb"]:.1f}')
+            out.append(f'aios_gpu_ecc_uncorrectable{{card="{g["card"]}"}} {g["ecc_ue"]}')
+            out.append(f'aios_gpu_ecc_correctable{{card="{g["card"]}"}} {g["ecc_ce"]}')
+            out.append(f'aios_gpu_xgmi_uncorrectable{{card="{g["card"]}"}} {g["xgmi_ue"]}')
+            out.append(f'aios_gpu_pcie_replays{{card="{g["card"]}"}} {g["pcie_replays"]}')
+            for k, v in g.items():
+                if k.startswith("temp_") or k == "power_w":
+                    out.append(f'aios_gpu_{k}{{card="{g["card"]}"}} {v:.1f}')
         return web.Response(text="\n".join(out) + "\n", content_type="text/plain")
 
     # ------------------------------------------------------------------ websocket

@@ -558,6 +558,10 @@ class ModelManager:
             from ..utils import sysinfo
 
             out["gpu.utilization"] = sysinfo.gpu_utilization()
+            gh = sysinfo.gpu_health()
+            out["gpu.ecc_ue_total"] = float(gh["ecc_ue_total"])
+            out["gpu.ecc_ce_total"] = float(gh["ecc_ce_total"])
+            out["gpu.healthy"] = 1.0 if gh["healthy"] else 0.0
         except Exception:  # pragma: no cover
             pass
         return out

@@ -166,6 +166,17 @@ class AIRuntimeService:
                                    uptime_seconds=int(time.time() - self.mgr.started))
         for k, v in self.mgr.health().items():
             h.details[k] = v
+        try:  # amdgpu RAS / thermal verdict (uncorrectable HBM ECC or xGMI errors -> unhealthy)
+            from ..utils import sysinfo
+
+            gh = sysinfo.gpu_health()
+            h.details["gpu_ecc_uncorrectable"] = str(gh["ecc_ue_total"])
+            h.details["gpu_ecc_correctable"] = str(gh["ecc_ce_total"])
+            if not gh["healthy"]:
+                h.details["gpu_problems"] = json.dumps(gh["problems"])
+                h.message += f"; GPU problems on {len(gh['problems'])} counter(s)"
+        except Exception:  # pragma: no cover - no GPU sysfs
+            pass
         return h
 
     # ------------------------------------------------------------------ HTTP (OpenAI-compatible)

@@ -4,7 +4,11 @@ Used by the orchestrator's GetSystemStatus, the memory service's GetSystemSnapsh
 proactive goal generator and the management console (reference: `agent-core/src/main.rs:
 103-133` read /proc/stat + /proc/meminfo; `memory/src/operational.rs:63-82` mapped metric keys).
 GPU utilisation comes from `/sys/class/drm/card*/device/gpu_busy_percent` (amdgpu), VRAM from
-`mem_info_vram_{used,total}` -- no rocm-smi subprocess on the hot path.
+`mem_info_vram_{used,total}` -- no rocm-smi subprocess on the hot path.  GPU health (SURVEY §5
+"amd-smi ECC/xGMI counters feed health"): the amdgpu RAS counters `device/ras/*_err_count`
+(`ue: N` / `ce: M` per block -- umc = HBM ECC, xgmi_wafl = the xGMI links, gfx, sdma, ...),
+`device/pcie_replay_count`, and hwmon temperatures (edge / junction / mem, millidegrees) and
+average socket power (microwatts).  `root` re-targets every read for tests.
 """
 from __future__ import annotations
 
@@ -80,23 +84,79 @@ def load_avg() -> List[float]:
         return [0.0, 0.0, 0.0]
 
 
-def amd_gpus() -> List[dict]:
-    """amdgpu devices visible through sysfs: busy %, VRAM used/total (MB)."""
+def _ras(dev: str) -> Dict[str, Dict[str, int]]:
+    """RAS error counts per block: {"umc": {"ue": 0, "ce": 3}, "xgmi_wafl": {...}, ...}."""
+    out: Dict[str, Dict[str, int]] = {}
+    for f in sorted(glob.glob(os.path.join(dev, "ras", "*_err_count"))):
+        block = os.path.basename(f)[: -len("_err_count")]
+        counts = {}
+        for ln in _read(f).splitlines():
+            k, _, v = ln.partition(":")
+            if v.strip().isdigit():
+                counts[k.strip()] = int(v.strip())
+        if counts:
+            out[block] = counts
+    return out
+
+
+def _hwmon(dev: str) -> dict:
+    out: Dict[str, float] = {}
+    for hw in sorted(glob.glob(os.path.join(dev, "hwmon", "hwmon*"))):
+        for t in sorted(glob.glob(os.path.join(hw, "temp*_input"))):
+            label = _read(t.replace("_input", "_label")).strip() or os.path.basename(t)[:-6]
+            v = _read(t).strip()
+            if v.lstrip("-").isdigit():
+                out[f"temp_{label}_c"] = int(v) / 1000.0
+        for name in ("power1_average", "power1_input"):
+            v = _read(os.path.join(hw, name)).strip()
+            if v.isdigit():
+                out["power_w"] = int(v) / 1e6
+                break
+    return out
+
+
+def amd_gpus(root: str = "/") -> List[dict]:
+    """amdgpu devices visible through sysfs: busy %, VRAM used/total (MB), RAS error counts,
+    PCIe replays, temperatures and power."""
     out = []
-    for dev in sorted(glob.glob("/sys/class/drm/card[0-9]*/device")):
+    for dev in sorted(glob.glob(os.path.join(root, "sys/class/drm/card[0-9]*/device"))):
         if _read(os.path.join(dev, "vendor")).strip() != "0x1002":
             continue
         busy = _read(os.path.join(dev, "gpu_busy_percent")).strip()
         vu = _read(os.path.join(dev, "mem_info_vram_used")).strip()
         vt = _read(os.path.join(dev, "mem_info_vram_total")).strip()
+        rp = _read(os.path.join(dev, "pcie_replay_count")).strip()
+        ras = _ras(dev)
         out.append({
             "card": dev.split("/")[-2],
             "device_id": _read(os.path.join(dev, "device")).strip(),
             "busy_percent": float(busy) if busy.isdigit() else 0.0,
             "vram_used_mb": int(vu) / 2**20 if vu.isdigit() else 0.0,
             "vram_total_mb": int(vt) / 2**20 if vt.isdigit() else 0.0,
+            "ras": ras,
+            "ecc_ue": sum(c.get("ue", 0) for c in ras.values()),
+            "ecc_ce": sum(c.get("ce", 0) for c in ras.values()),
+            "xgmi_ue": ras.get("xgmi_wafl", {}).get("ue", 0),
+            "pcie_replays": int(rp) if rp.isdigit() else 0,
+            **_hwmon(dev),
         })
     return out
+
+
+def gpu_health(root: str = "/", hot_c: float = 95.0) -> dict:
+    """Node GPU health from the RAS / thermal counters: per-card problems and a verdict."""
+    cards, problems = amd_gpus(root), []
+    for g in cards:
+        if g["ecc_ue"]:
+            problems.append({"card": g["card"], "kind": "uncorrectable_ecc", "count": g["ecc_ue"],
+                             "blocks": sorted(b for b, c in g["ras"].items() if c.get("ue"))})
+        if g["xgmi_ue"]:
+            problems.append({"card": g["card"], "kind": "xgmi_link_errors", "count": g["xgmi_ue"]})
+        hot = max([v for k, v in g.items() if k.startswith("temp_") and isinstance(v, float)] or [0.0])
+        if hot >= hot_c:
+            problems.append({"card": g["card"], "kind": "overtemperature", "temp_c": hot})
+    return {"gpus": len(cards), "healthy": not problems, "problems": problems,
+            "ecc_ce_total": sum(g["ecc_ce"] for g in cards), "ecc_ue_total": sum(g["ecc_ue"] for g in cards)}
 
 
 def gpu_utilization() -> float:
