@@ -33,8 +33,8 @@ TACTICAL = [
     "set up monitoring for the gpu temperature and alert on spikes",
     "update all packages, then restart the web services safely",
     "plan a rollout of the new tool plugin to the cluster nodes",
-    "investigate the failed login attempts and harden ssh",
-    "create a python project that summarises system logs daily",
+    "investigate the failed sign-in attempts and harden ssh",
+    "create a python project that summarises system journals daily",
 ]
 REACTIVE = ["check nginx status", "report cpu usage status", "ping 1.1.1.1 health", "check disk usage"]
 
@@ -51,6 +51,9 @@ async def main_async(args):
     from aios_amd.runtime.model_manager import ModelManager
     from aios_amd.runtime.service import AIRuntimeService
     from aios_amd.tools.service import ToolRegistryService
+    from aios_amd.core import load as load_core
+
+    core = load_core().planner
 
     tmp = tempfile.mkdtemp(prefix="aios_bench_")
     mgr = ModelManager(max_batch=8, max_slots=8)
@@ -88,6 +91,10 @@ async def main_async(args):
     t = time.perf_counter()
     burst = await asyncio.gather(*(submit(TACTICAL[i % len(TACTICAL)] + f" burst {i}") for i in range(args.burst)))
     burst_s = time.perf_counter() - t
+    # every measured goal must have gone through the LLM decomposition (tactical / strategic
+    # classification) -- a goal the classifier routes to the heuristic planner is not a sample
+    mislabelled = [d for d in TACTICAL if core.classify(d) not in ("tactical", "strategic")]
+    assert not mislabelled, f"goals planned without the LLM: {mislabelled}"
     lat = sorted(x[0] for x in tac)
     rlat = sorted(x[0] for x in rea)
     blat = sorted(x[0] for x in burst)
