@@ -11,12 +11,20 @@
 //                              the row max / sum need one cross-half shuffle, not a 32-lane tree.
 //   O^T[dim][row] += V^T P^T -- P^T is taken straight from the S^T accumulator registers: the key
 //                              order of the k-dimension is permuted (rho below) to match the
-//                              accumulator layout, and V is staged transposed in LDS in natural
-//                              key order, so the V^T fragment is two 8-byte LDS reads at rho.
+//                              accumulator layout; V is staged ROW-major (16-byte stores) and the
+//                              V^T fragment is two gfx950 transposed LDS reads (ds_read_b64_tr_b16:
+//                              4 keys x 16 dims per 16-lane group, delivered column-major) at rho.
+//                              (Round 2 staged V transposed with 2-byte stores: 32 ds_write_b16
+//                              per thread per tile and the kernel's worst bank conflicts.)
 // Online softmax per row in the log2 domain; fully masked rows cannot occur (key 0 <= pos).
 // Output: bf16 [T][n_heads * hd] (the O-projection GEMM's A operand).
+//
+// VALU diet (rocprofv3 PMC at 2048 tokens: ~12 VALU instructions per MFMA, 129 TF/s): bf16 packing
+// in hardware (v_cvt_pk_bf16_f32, not a software RNE with a NaN test), raw v_exp_f32 (ocml's
+// exp2f adds range scaling), and the O rescale skipped when no row max of the wave moved.
 #include "../common.h"
 #include "../ops.h"
+#include "gemm_common.h"
 
 namespace aios {
 
@@ -25,10 +33,10 @@ typedef float f32x16_t __attribute__((ext_vector_type(16)));
 // native vector type for register arrays (HIP's uint4 is a struct; arrays of it copied with
 // memcpy defeat SROA and land in scratch)
 typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+typedef short v4i16_t __attribute__((ext_vector_type(4)));
+typedef short v8i16_t __attribute__((ext_vector_type(8)));
 
-__device__ __forceinline__ uint32_t pk_bf16(float a, float b) {
-  return (uint32_t)f32_to_bf16(a) | ((uint32_t)f32_to_bf16(b) << 16);
-}
+__device__ __forceinline__ float raw_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
 constexpr int FP_KT = 64;  // keys per tile
 
@@ -38,9 +46,12 @@ __global__ void __launch_bounds__(256) attn_prefill_kernel(AttnPrefillArgs a) {
   constexpr int KS = HD / 16;          // k-steps of the S MFMA
   constexpr int OT = HD / 32;          // O^T accumulator tiles (32 dims each)
   constexpr int KROW = HD + 8;         // padded LDS row (bf16) of the K tile
-  constexpr int VROW = FP_KT + 4;      // padded LDS row (bf16) of the transposed V tile
+  // padded LDS row (bf16) of the row-major V tile: a 16-lane transposed read takes 4 rows x 4
+  // 8-byte column chunks and its 32-lane half two such groups 16 dims apart; rows HD + 32 elements
+  // apart put the 4 rows 16 banks apart (mod 64) and the two groups 8 banks apart: conflict-free
+  constexpr int VROW = HD + 32;
   __shared__ __attribute__((aligned(16))) bf16_t sK[FP_KT * KROW];
-  __shared__ __attribute__((aligned(16))) bf16_t sV[HD * VROW];
+  __shared__ __attribute__((aligned(16))) bf16_t sV[FP_KT * VROW];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int l32 = lane & 31, half = lane >> 5;
@@ -106,12 +117,7 @@ __global__ void __launch_bounds__(256) attn_prefill_kernel(AttnPrefillArgs a) {
       constexpr int i = decltype(I)::value;
       const int idx = tid + 256 * i, key = idx / (HD / 8), c = idx % (HD / 8);
       *(u32x4_t*)(sK + key * KROW + c * 8) = kreg[i];
-      const uint32_t w[4] = {vreg[i][0], vreg[i][1], vreg[i][2], vreg[i][3]};
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        sV[(c * 8 + 2 * j) * VROW + key] = (bf16_t)(w[j] & 0xffff);
-        sV[(c * 8 + 2 * j + 1) * VROW + key] = (bf16_t)(w[j] >> 16);
-      }
+      *(u32x4_t*)(sV + key * VROW + c * 8) = vreg[i];
     });
   };
 
@@ -150,24 +156,27 @@ __global__ void __launch_bounds__(256) attn_prefill_kernel(AttnPrefillArgs a) {
       }
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
     const float mn = fmaxf(m_run, mx);  // finite: key 0 of tile 0 is always visible
-    const float alpha = exp2f(m_run - mn);
+    const float alpha = raw_exp2(m_run - mn);  // exp2(-inf) = 0 on the first tile
     float ps = 0.f;
     uint32_t pb[2][8];  // P^T as packed bf16 pairs, accumulator order
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
       for (int r = 0; r < 16; r += 2) {
-        const float p0 = exp2f(st[t][r] - mn), p1 = exp2f(st[t][r + 1] - mn);
+        const float p0 = raw_exp2(st[t][r] - mn), p1 = raw_exp2(st[t][r + 1] - mn);
         ps += p0 + p1;
         pb[t][r >> 1] = pk_bf16(p0, p1);
       }
     ps += __shfl_xor(ps, 32, 64);
     l_run = l_run * alpha + ps;
+    // the O rescale only when some row max of this wave moved (alpha == 1 on every lane otherwise)
+    if (__any(mn != m_run)) {
+#pragma unroll
+      for (int i = 0; i < OT; ++i)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) o[i][e] *= alpha;
+    }
     m_run = mn;
-#pragma unroll
-    for (int i = 0; i < OT; ++i)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) o[i][e] *= alpha;
     // ---- O^T += V^T P^T over 4 k-steps of 16 keys: step s uses accumulator half t = s/2,
     //      registers 8*(s%2) .. +7, i.e. keys rho = 16s + 4*half + {0..3} and 16s + 8 + 4*half + {0..3}
 #pragma unroll
@@ -178,11 +187,16 @@ __global__ void __launch_bounds__(256) attn_prefill_kernel(AttnPrefillArgs a) {
       __builtin_memcpy(&pf, &pu, 16);
 #pragma unroll
       for (int i = 0; i < OT; ++i) {
-        const bf16_t* vr = sV + (i * 32 + l32) * VROW + 16 * s + 4 * half;
-        const uint2 v0 = *(const uint2*)vr, v1 = *(const uint2*)(vr + 8);
-        const uint4 vu = make_uint4(v0.x, v0.y, v1.x, v1.y);
+        // lane 4q+p of each 16-lane group addresses key row (16s + 4 half + q), dims
+        // 32 i + 16 (group & 1) + 4p .. +3; lane l32 receives dim 32 i + l32 of those 4 keys
+        const bf16_t* va = sV + (16 * s + 4 * half + ((lane & 15) >> 2)) * VROW + i * 32 + 16 * ((lane >> 4) & 1) +
+                           4 * (lane & 3);
+        const v4i16_t x0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4i16_t*)va);
+        const v4i16_t x1 =
+            __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4i16_t*)(va + 8 * VROW));
+        const v8i16_t xv = __builtin_shufflevector(x0, x1, 0, 1, 2, 3, 4, 5, 6, 7);
         bf16x8_t vf;
-        __builtin_memcpy(&vf, &vu, 16);
+        __builtin_memcpy(&vf, &xv, 16);
         o[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf, o[i], 0, 0, 0);
       }
     }
