@@ -63,7 +63,9 @@ static void launch_hd(const AttnDecodeArgs& a, int G, hipStream_t st) {
 // owning at least one 128-key pass of a max_ctx context.
 int attn_decode_split(int max_ctx, int B, int n_kv_heads) {
   const int nch = std::max(1, max_ctx / 128);
-  const int P = std::max(1, std::min({64, nch, 256 / std::max(1, B * n_kv_heads)}));
+  // AIOS_ATTN_WG_PER_CU (default 1): long-context workgroups per CU the split aims for
+  const int per_cu = std::max(1, std::min(4, attn_env_int("AIOS_ATTN_WG_PER_CU", 1)));
+  const int P = std::max(1, std::min({64, nch, 256 * per_cu / std::max(1, B * n_kv_heads)}));
   return P * ATTN_CHUNK;
 }
 
