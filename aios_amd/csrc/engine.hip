@@ -731,9 +731,9 @@ void Engine::layer_decode_gemm(int l, int B) {
     a.B = B; a.n_heads = H; a.n_kv_heads = Hkv; a.head_dim = hd; a.max_ctx = cfg_.max_ctx;
     a.n_chunks = n_chunks_; a.scale = 1.f / std::sqrt((float)hd);
     a.o_part = opart_; a.ml = ml_; a.out = attn_; a.counters = attn_cnt_;
+    a.out16 = dec_a16_;  // bf16 straight from the attention epilogue (no conversion launch)
     launch_attn_decode(a, stream_);
   }
-  launch_f32_to_bf16(attn_, dec_a16_, (size_t)B * qd, stream_);
   std::memset(&g, 0, sizeof(g));
   g.A = dec_a16_; g.lda = qd; g.M = B; g.K = qd; g.nseg = 1; g.seg[0] = L.wo.w; g.N = d; g.ldc = d;
   if (tp) { g.C = ff_; g.epi = GEPI_STORE; } else { g.C = x_; g.epi = GEPI_ACCUM; }

@@ -293,6 +293,7 @@ __device__ __forceinline__ void attn_core(const AttnDecodeArgs& a, int sp, int k
     const int h = h0 + g;
     if (nact == 1) {
       if constexpr (FUSED) st_sc1_f32(a.out + ((size_t)b * a.n_heads + h) * HD + d, acc / L);
+      else if (a.out16) a.out16[((size_t)b * a.n_heads + h) * HD + d] = f32_to_bf16(acc / L);
       else a.out[((size_t)b * a.n_heads + h) * HD + d] = acc / L;
     } else {
       st_wt(a.o_part + (((size_t)b * a.n_heads + h) * a.n_chunks + sp) * HD + d, acc);
@@ -362,6 +363,7 @@ __device__ __forceinline__ void attn_core(const AttnDecodeArgs& a, int sp, int k
         if (c + j < nact) acc = fmaf(s_pm[g][c + j], ov[j], acc);
     }
     if constexpr (FUSED) st_sc1_f32(a.out + ((size_t)b * a.n_heads + h) * HD + d, acc);
+    else if (a.out16) a.out16[((size_t)b * a.n_heads + h) * HD + d] = f32_to_bf16(acc);
     else a.out[((size_t)b * a.n_heads + h) * HD + d] = acc;
   }
   if (threadIdx.x == 0) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
