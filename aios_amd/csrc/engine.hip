@@ -714,7 +714,22 @@ void Engine::layer_decode_gemm(int l, int B) {
   g.seg[0] = L.wq.w; g.seg[1] = L.wk.w; g.seg[2] = L.wv.w;
   g.seg_n0[0] = 0; g.seg_n0[1] = qd; g.seg_n0[2] = qd + kvd;
   g.N = ldqkv; g.C = qkv_; g.ldc = ldqkv; g.epi = GEPI_STORE;
+  // RoPE + q store + KV-cache write in the GEMM epilogue (one launch per layer less) whenever
+  // qkv_post would only do that (non-NeoX pairs, no QK-norm, no QKV bias)
+  static const int qkv_epi_max_b = [] {
+    const char* e = std::getenv("AIOS_GEMM_QKV_EPI_MAX_B");
+    return e ? std::atoi(e) : 64;
+  }();
+  const bool qkv_epi = !cfg_.qk_norm && !cfg_.rope_neox && !L.bqkv && rope_cs_ && B <= qkv_epi_max_b;
+  if (qkv_epi) {
+    g.epi = GEPI_QKV; g.col0 = 0;
+    g.head_dim = hd; g.q_dim = qd; g.kv_dim = kvd; g.n_kv_heads = Hkv; g.max_ctx = cfg_.max_ctx;
+    g.rope_cs = rope_cs_; g.pos = d_pos_; g.slot = d_slot_; g.block_table = d_bt_;
+    g.q_out = q_; g.k_cache = kc; g.v_cache = vc;
+  }
   gemm(g);
+  static const bool attn_out16 = !(std::getenv("AIOS_ATTN_OUT16") && std::atoi(std::getenv("AIOS_ATTN_OUT16")) == 0);
+  if (!qkv_epi) {
   QkvPostArgs p;
   p.qkv = qkv_; p.ldqkv = ldqkv; p.T = B;
   p.n_heads = H; p.n_kv_heads = Hkv; p.head_dim = hd;
@@ -723,6 +738,7 @@ void Engine::layer_decode_gemm(int l, int B) {
   p.pos = d_pos_; p.slot = d_slot_; p.q_out = q_;
   p.k_cache = kc; p.v_cache = vc; p.max_ctx = cfg_.max_ctx; p.block_table = d_bt_;
   launch_qkv_post(p, stream_);
+  }
   {
     AttnDecodeArgs a;
     a.split = 0;
@@ -731,9 +747,10 @@ void Engine::layer_decode_gemm(int l, int B) {
     a.B = B; a.n_heads = H; a.n_kv_heads = Hkv; a.head_dim = hd; a.max_ctx = cfg_.max_ctx;
     a.n_chunks = n_chunks_; a.scale = 1.f / std::sqrt((float)hd);
     a.o_part = opart_; a.ml = ml_; a.out = attn_; a.counters = attn_cnt_;
-    a.out16 = dec_a16_;  // bf16 straight from the attention epilogue (no conversion launch)
+    if (attn_out16) a.out16 = dec_a16_;  // bf16 straight from the attention epilogue (no conversion launch)
     launch_attn_decode(a, stream_);
   }
+  if (!attn_out16) launch_f32_to_bf16(attn_, dec_a16_, (size_t)B * qd, stream_);
   std::memset(&g, 0, sizeof(g));
   g.A = dec_a16_; g.lda = qd; g.M = B; g.K = qd; g.nseg = 1; g.seg[0] = L.wo.w; g.N = d; g.ldc = d;
   if (tp) { g.C = ff_; g.epi = GEPI_STORE; } else { g.C = x_; g.epi = GEPI_ACCUM; }

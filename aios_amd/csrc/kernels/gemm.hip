@@ -235,6 +235,7 @@ bool launch_gemm_skinny(const GemmQArgs& a, hipStream_t st);
 static void launch_one(const GemmQArgs& a, hipStream_t st) {
   static const int skinny_max = env_int("AIOS_GEMM_SKINNY_MAX_M", 64);
   if (a.M <= skinny_max && launch_gemm_skinny(a, st)) return;
+  if (a.epi == GEPI_QKV) throw std::runtime_error("gemm: the QKV epilogue needs the skinny (M <= 64) kernel");
   switch (a.seg[0].qtype) {
     case QT_Q4_K: launch_big<QT_Q4_K>(a, st); break;
     case QT_Q5_K: launch_big<QT_Q5_K>(a, st); break;
@@ -271,6 +272,7 @@ void launch_gemm_q(const GemmQArgs& a, hipStream_t st) {
       b.seg_n0[s] = a.seg_n0[s0 + s] - c0;
     }
     b.N = (s1 < a.nseg ? a.seg_n0[s1] : a.N) - c0;
+    b.col0 = a.col0 + c0;  // global column of the launch's first column (GEPI_QKV)
     if (a.epi == GEPI_SWIGLU_BF16) {
       if (c0 % 2) throw std::runtime_error("gemm: odd swiglu segment start");
       b.C16 = a.C16 + c0 / 2;

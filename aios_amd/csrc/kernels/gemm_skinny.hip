@@ -201,6 +201,30 @@ __global__ void __launch_bounds__(RB * 64) gemm_skinny_kernel(GemmQArgs a, int S
     if constexpr (EPI == GEPI_SWIGLU_BF16) {
       const uint32_t pk = pk_bf16(v[0] / (1.f + __expf(-v[0])) * v[1], v[2] / (1.f + __expf(-v[2])) * v[3]);
       *(uint32_t*)(a.C16 + (size_t)m * a.ldc + (n >> 1)) = pk;
+    } else if constexpr (EPI == GEPI_QKV) {
+      // the lane's 4 consecutive columns are two RoPE pairs (2i, 2i + 1)
+      const int hd = a.head_dim, pos = a.pos[m], slot = a.slot ? a.slot[m] : 0;
+#pragma unroll
+      for (int j = 0; j < 4; j += 2) {
+        const int c = a.col0 + n + j;
+        float v0 = v[j], v1 = v[j + 1];
+        const int part = c < a.q_dim ? 0 : (c < a.q_dim + a.kv_dim ? 1 : 2);
+        const int r = c - (part == 0 ? 0 : (part == 1 ? a.q_dim : a.q_dim + a.kv_dim));
+        const int head = r / hd, lr = r - head * hd;
+        if (part < 2) {
+          const float2 t = a.rope_cs[(size_t)pos * (hd >> 1) + (lr >> 1)];
+          const float o0 = v0 * t.x - v1 * t.y, o1 = v0 * t.y + v1 * t.x;
+          v0 = o0;
+          v1 = o1;
+        }
+        if (part == 0) {
+          *(float2*)(a.q_out + (size_t)m * a.q_dim + c) = make_float2(v0, v1);
+        } else {
+          bf16_t* cache = part == 1 ? a.k_cache : a.v_cache;
+          const size_t base = kv_offset(a.block_table, a.max_ctx / KV_BLOCK, slot, a.n_kv_heads, head, pos, hd);
+          *(uint32_t*)(cache + base + lr) = pk_bf16(v0, v1);
+        }
+      }
     } else {
       float4* c = (float4*)(a.C + (size_t)m * a.ldc + n);
       if constexpr (EPI == GEPI_ACCUM) {
@@ -269,6 +293,9 @@ static void sk_launch(const GemmQArgs& a, int S, hipStream_t st) {
   switch (a.epi) {
     case GEPI_STORE:
       hipLaunchKernelGGL((gemm_skinny_kernel<QT, RB, MT, GEPI_STORE>), dim3(grid), dim3(RB * 64), 0, st, a, S);
+      break;
+    case GEPI_QKV:
+      hipLaunchKernelGGL((gemm_skinny_kernel<QT, RB, MT, GEPI_QKV>), dim3(grid), dim3(RB * 64), 0, st, a, S);
       break;
     case GEPI_ACCUM:
       hipLaunchKernelGGL((gemm_skinny_kernel<QT, RB, MT, GEPI_ACCUM>), dim3(grid), dim3(RB * 64), 0, st, a, S);

@@ -150,7 +150,7 @@ void launch_gemm(const GemmArgs& a, hipStream_t st);
 bool gemm_supports(int qt);
 
 // multi-segment GEMM with fused epilogues (the prefill path): C = A x [W0; W1; W2]^T
-enum GemmEpi { GEPI_STORE = 0, GEPI_ACCUM = 1, GEPI_SWIGLU_BF16 = 2 };
+enum GemmEpi { GEPI_STORE = 0, GEPI_ACCUM = 1, GEPI_SWIGLU_BF16 = 2, GEPI_QKV = 3 };
 struct GemmQArgs {
   const bf16_t* A;   // [M][lda] bf16
   int lda;
@@ -169,6 +169,18 @@ struct GemmQArgs {
   size_t ws_bytes;
   int* cnt;
   int cnt_len;
+  // GEPI_QKV (skinny kernel, batched decode; non-NeoX RoPE, no QK-norm / bias): global column
+  // col0 + n of the packed [q | k | v] product -> RoPE'd q to q_out[M][q_dim], RoPE'd k / v as bf16
+  // into the paged KV cache at (slot[m], pos[m]) -- the qkv_post launch folded into the epilogue
+  int col0;
+  int head_dim, q_dim, kv_dim, n_kv_heads, max_ctx;
+  const float2* rope_cs;  // [max_ctx][head_dim / 2] (cos, sin)
+  const int* pos;
+  const int* slot;
+  const int* block_table;
+  float* q_out;
+  bf16_t* k_cache;
+  bf16_t* v_cache;
 };
 // bytes of split-K workspace / ticket count the skinny GEMM may use for an M x N output
 size_t gemm_skinny_ws_bytes(int M, int N);
