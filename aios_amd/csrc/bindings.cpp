@@ -229,6 +229,7 @@ PYBIND11_MODULE(_engine, m) {
       .def("block_table", &Engine::block_table)
       .def_property_readonly("kv_blocks_free", &Engine::kv_blocks_free)
       .def_property_readonly("kv_blocks_total", &Engine::kv_blocks_total)
+      .def_property_readonly("norm_fused_parts", &Engine::norm_fused_parts)
       .def_property_readonly("stream", &Engine::stream_handle)
       .def_property_readonly("k_cache_ptr", &Engine::kv_cache_k)
       .def_property_readonly("v_cache_ptr", &Engine::kv_cache_v)

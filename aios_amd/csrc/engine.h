@@ -126,6 +126,7 @@ class Engine {
   void release_slot(int slot);         // drop every block reference of the slot
   int kv_blocks_free() const { return (int)free_blocks_.size(); }
   int kv_blocks_total() const { return kv_nblocks_; }
+  int norm_fused_parts() const { return nrm_parts_; }  // 0: batched-decode RMSNorm not split into the GEMMs
   std::vector<int> block_table(int slot) const;
 
   // raw device pointers for tests / custom kernels
@@ -224,8 +225,18 @@ class Engine {
   int* gk_cnt_ = nullptr;
   int gk_cnt_len_ = 0;
   void gemm(GemmQArgs& g);  // launch_gemm_q with the engine's split-K workspace
+  // RMSNorm split across the skinny GEMMs (AIOS_GEMM_NORM_FUSE, default on): the residual GEMMs
+  // (O, down) also write bf16(x * g_next) to dec_xn16_ and per-tile row sums of squares to
+  // nrm_part_; the next GEMM (gate/up, next layer's QKV, lm_head) scales its rows by the inverse
+  // RMS in the epilogue -- two normalisation launches per layer less
+  bf16_t* dec_xn16_ = nullptr;
+  float* nrm_part_ = nullptr;
+  int nrm_fuse_ = 1;
+  int nrm_parts_ = 0;  // tiles of the d_model-wide producer GEMM (0: fusion unavailable)
+  bool nrm_on(int B) const;
  private:
   void layer_decode_gemm(int l, int B);
+  bool nrm_lm_ = false;  // the last layer's down GEMM prepared dec_xn16_ / nrm_part_ for lm_head(x_)
   int *pf_tokens_ = nullptr, *pf_pos_ = nullptr, *pf_seqlen_ = nullptr, *pf_slot_ = nullptr;
 
   // paged KV state: host tables are the truth, device copies uploaded (stream idle) when dirty

@@ -579,6 +579,17 @@ void Engine::finalize() {
         ws += gk_ws_bytes_;
         gk_cnt_len_ = gemm_skinny_cnt_len(maxN);
         gk_cnt_ = ibuf(gk_cnt_len_);
+        if (const char* e = std::getenv("AIOS_GEMM_NORM_FUSE")) nrm_fuse_ = std::atoi(e);
+        GemmQArgs p;  // the residual producer's shape (O / down: N = d_model, one segment)
+        std::memset(&p, 0, sizeof(p));
+        p.M = std::min(Bm, 64); p.N = d; p.K = d; p.nseg = 1; p.seg[0] = layers_[0].wo.w;
+        const int parts = gemm_skinny_ntile(p);
+        if (nrm_fuse_ && Bm <= 64 && parts > 0 && parts % 4 == 0 && parts <= 64 && d % 128 == 0) {
+          nrm_parts_ = parts;
+          dec_xn16_ = (bf16_t*)dmalloc((size_t)Bm * d * 2);
+          nrm_part_ = fbuf((size_t)Bm * parts);
+          ws += (size_t)Bm * d * 2;
+        }
       }
     }
   }
@@ -700,17 +711,30 @@ void Engine::gemm(GemmQArgs& g) {
 // MFMA GEMM (weights dequantised once per step into MFMA operands, split-K reduced in-launch),
 // with explicit RMSNorm -> bf16 and RoPE/KV-write launches in place of the GEMV prologue /
 // epilogue fusions.  SwiGLU runs in the gate/up GEMM's epilogue (bf16 out for the down GEMM).
+bool Engine::nrm_on(int B) const { return nrm_parts_ > 0 && dec_xn16_ && cfg_.tp_size == 1 && B <= 64; }
+
 void Engine::layer_decode_gemm(int l, int B) {
   const LayerW& L = layers_[l];
   const int d = cfg_.d_model, hd = cfg_.head_dim, H = cfg_.n_heads, Hkv = cfg_.n_kv_heads, ff = cfg_.d_ff;
   const int qd = H * hd, kvd = Hkv * hd, ldqkv = qd + 2 * kvd;
   const bool tp = cfg_.tp_size > 1;
+  const bool fn = nrm_on(B);
   bf16_t* kc = k_cache_ + (size_t)l * layer_kv_elems_;
   bf16_t* vc = v_cache_ + (size_t)l * layer_kv_elems_;
-  launch_rmsnorm_bf16(x_, d, L.attn_norm, dec_a16_, d, B, d, cfg_.norm_eps, stream_);
+  // consumer side of the split RMSNorm: A = bf16(x * g) from the previous residual GEMM
+  auto nrm_in = [&](GemmQArgs& g) {
+    g.A = dec_xn16_; g.nrm_in = nrm_part_; g.nrm_parts = nrm_parts_; g.nrm_eps = cfg_.norm_eps;
+  };
+  // producer side: residual add + bf16(x_new * g_next) + per-tile sums of squares
+  auto nrm_out = [&](GemmQArgs& g, const float* g_next) {
+    g.epi = GEPI_ACCUM_NORM; g.nrm_g = g_next; g.nrm_out16 = dec_xn16_; g.nrm_part = nrm_part_;
+    g.nrm_parts = nrm_parts_;
+  };
+  if (!(fn && l > 0)) launch_rmsnorm_bf16(x_, d, L.attn_norm, dec_a16_, d, B, d, cfg_.norm_eps, stream_);
   GemmQArgs g;
   std::memset(&g, 0, sizeof(g));
   g.A = dec_a16_; g.lda = d; g.M = B; g.K = d; g.nseg = 3;
+  if (fn && l > 0) nrm_in(g);
   g.seg[0] = L.wq.w; g.seg[1] = L.wk.w; g.seg[2] = L.wv.w;
   g.seg_n0[0] = 0; g.seg_n0[1] = qd; g.seg_n0[2] = qd + kvd;
   g.N = ldqkv; g.C = qkv_; g.ldc = ldqkv; g.epi = GEPI_STORE;
@@ -754,16 +778,21 @@ void Engine::layer_decode_gemm(int l, int B) {
   std::memset(&g, 0, sizeof(g));
   g.A = dec_a16_; g.lda = qd; g.M = B; g.K = qd; g.nseg = 1; g.seg[0] = L.wo.w; g.N = d; g.ldc = d;
   if (tp) { g.C = ff_; g.epi = GEPI_STORE; } else { g.C = x_; g.epi = GEPI_ACCUM; }
+  if (fn) nrm_out(g, L.ffn_norm);
   gemm(g);
   if (tp) allreduce(ff_, (size_t)B * d, x_);
-  launch_rmsnorm_bf16(x_, d, L.ffn_norm, dec_a16_, d, B, d, cfg_.norm_eps, stream_);
+  if (!fn) launch_rmsnorm_bf16(x_, d, L.ffn_norm, dec_a16_, d, B, d, cfg_.norm_eps, stream_);
   std::memset(&g, 0, sizeof(g));
   g.A = dec_a16_; g.lda = d; g.M = B; g.K = d; g.nseg = 1; g.seg[0] = L.wgu.w; g.N = 2 * ff;
   g.C16 = dec_ff16_; g.ldc = ff; g.epi = GEPI_SWIGLU_BF16;
+  if (fn) nrm_in(g);
   gemm(g);
   std::memset(&g, 0, sizeof(g));
   g.A = dec_ff16_; g.lda = ff; g.M = B; g.K = ff; g.nseg = 1; g.seg[0] = L.wdown.w; g.N = d; g.ldc = d;
   if (tp) { g.C = attn_; g.epi = GEPI_STORE; } else { g.C = x_; g.epi = GEPI_ACCUM; }
+  // the next consumer: layer l + 1's QKV, or the lm_head after the last layer
+  if (fn) nrm_out(g, l + 1 < cfg_.n_layers ? layers_[l + 1].attn_norm : out_norm_);
+  nrm_lm_ = fn && l + 1 == cfg_.n_layers;
   gemm(g);
   if (tp) allreduce(attn_, (size_t)B * d, x_);
 }
@@ -923,11 +952,13 @@ void Engine::lm_head(int B, const float* x, int ldx) {
   float* y = logits_ + (vp ? (size_t)cfg_.tp_rank * Vl : 0);
   if (dec_a16_ && ((dec_gemm_min_b_ > 0 && B >= dec_gemm_min_b_) || B > 8) && Vl % 64 == 0 &&
       gemm_supports(output_.w.qtype)) {
-    launch_rmsnorm_bf16(x, ldx, out_norm_, dec_a16_, d, B, d, cfg_.norm_eps, stream_);
+    const bool fused = nrm_lm_ && x == x_ && ldx == d;  // normalised by the last down GEMM
+    if (!fused) launch_rmsnorm_bf16(x, ldx, out_norm_, dec_a16_, d, B, d, cfg_.norm_eps, stream_);
     GemmQArgs g;
     std::memset(&g, 0, sizeof(g));
     g.A = dec_a16_; g.lda = d; g.M = B; g.K = d; g.nseg = 1; g.seg[0] = output_.w; g.N = Vl;
     g.C = y; g.ldc = V; g.epi = GEPI_STORE;
+    if (fused) { g.A = dec_xn16_; g.nrm_in = nrm_part_; g.nrm_parts = nrm_parts_; g.nrm_eps = cfg_.norm_eps; }
     gemm(g);
   } else {
     gemv({&output_}, Vl, d, B, x, ldx, out_norm_, y, V, EPI_STORE, 0);
@@ -943,8 +974,10 @@ void Engine::enqueue_decode_step(int B) {
   if (attn_block_on(B))  // the fused blocks' hand-off counters start every step at zero
     HIP_CHECK(hipMemsetAsync(fuse_cnt_, 0, (size_t)cfg_.n_layers * 2 * 4, stream_));
   launch_get_rows(tok_embd_.w, d_tokens_, B, x_, d, 1.f, stream_);
+  nrm_lm_ = false;
   for (int l = 0; l < cfg_.n_layers; ++l) layer_decode(l, B);
   lm_head(B, x_, d);
+  nrm_lm_ = false;
   SampleArgs s;
   std::memset(&s, 0, sizeof(s));
   s.logits = logits_; s.ldl = V; s.B = B; s.V = V;

@@ -235,7 +235,8 @@ bool launch_gemm_skinny(const GemmQArgs& a, hipStream_t st);
 static void launch_one(const GemmQArgs& a, hipStream_t st) {
   static const int skinny_max = env_int("AIOS_GEMM_SKINNY_MAX_M", 64);
   if (a.M <= skinny_max && launch_gemm_skinny(a, st)) return;
-  if (a.epi == GEPI_QKV) throw std::runtime_error("gemm: the QKV epilogue needs the skinny (M <= 64) kernel");
+  if (a.epi == GEPI_QKV || a.epi == GEPI_ACCUM_NORM || a.nrm_in)
+    throw std::runtime_error("gemm: the QKV / fused-RMSNorm epilogues need the skinny (M <= 64) kernel");
   switch (a.seg[0].qtype) {
     case QT_Q4_K: launch_big<QT_Q4_K>(a, st); break;
     case QT_Q5_K: launch_big<QT_Q5_K>(a, st); break;

@@ -173,11 +173,38 @@ __global__ void __launch_bounds__(RB * 64) gemm_skinny_kernel(GemmQArgs a, int S
     }
   };
 
+  // ---- fused RMSNorm (consumer): the producer's per-tile sums of squares, nG <= 16 lanes per row
+  // (power of two >= parts / 4, one float4 each), loaded before everything else and reduced in a
+  // fixed order once the first X chunk has landed -> inv_s[m]
+  constexpr int NR = (MP * 16 + NT - 1) / NT;
+  __shared__ float inv_s[MP];
+  const bool nrm = a.nrm_in != nullptr;
+  int nlg = 0;
+  gf32x4 nv[NR];
+  if (nrm) {
+    const int p4 = a.nrm_parts >> 2;
+    while ((1 << nlg) < p4) ++nlg;
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+      const int u = tid + NT * r, m = u >> nlg, j = u & ((1 << nlg) - 1);
+      nv[r] = gf32x4{0.f, 0.f, 0.f, 0.f};
+      if (m < a.M && j < p4) nv[r] = *(const gf32x4*)(a.nrm_in + (size_t)m * a.nrm_parts + 4 * j);
+    }
+  }
   // prologue: X chunk c0 first (oldest loads), then the weight ring, then X chunk c0+1
   x_load(c0);
 #pragma unroll
   for (int u = 0; u < SK_NL; ++u) w_load(tb + u, ring[u], !MB || (u & 1) == 0);
   x_store(0, c0);
+  if (nrm) {
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+      const int u = tid + NT * r, m = u >> nlg;
+      float s = (nv[r][0] + nv[r][1]) + (nv[r][2] + nv[r][3]);
+      for (int o = 1; o < (1 << nlg); o <<= 1) s += __shfl_xor(s, o, 64);
+      if ((u & ((1 << nlg) - 1)) == 0 && m < MP) inv_s[m] = rsqrtf(s / (float)a.K + a.nrm_eps);
+    }
+  }
   x_load(min(c0 + 1, c1 - 1));
   __syncthreads();
   for (int c = c0; c < c1; ++c) {
@@ -196,8 +223,10 @@ __global__ void __launch_bounds__(RB * 64) gemm_skinny_kernel(GemmQArgs a, int S
 
   // ---- epilogue.  lane holds D[n = 4q + j][m = 16 mt + rr], j = 0..3
   const int nl = 16 * wave + 4 * q;  // tile-local first row of this lane's 4 outputs
-  auto finish = [&](int m, int n, gf32x4 v) __attribute__((always_inline)) {
-    if (m >= a.M) return;
+  // returns the sum of squares of the new residual row slice (GEPI_ACCUM_NORM), else 0
+  auto finish = [&](int m, int n, gf32x4 v) __attribute__((always_inline)) -> float {
+    if (m >= a.M) return 0.f;
+    if (nrm) v *= inv_s[m];
     if constexpr (EPI == GEPI_SWIGLU_BF16) {
       const uint32_t pk = pk_bf16(v[0] / (1.f + __expf(-v[0])) * v[1], v[2] / (1.f + __expf(-v[2])) * v[3]);
       *(uint32_t*)(a.C16 + (size_t)m * a.ldc + (n >> 1)) = pk;
@@ -227,17 +256,45 @@ __global__ void __launch_bounds__(RB * 64) gemm_skinny_kernel(GemmQArgs a, int S
       }
     } else {
       float4* c = (float4*)(a.C + (size_t)m * a.ldc + n);
-      if constexpr (EPI == GEPI_ACCUM) {
+      if constexpr (EPI == GEPI_ACCUM_NORM) {
+        const float4 o = *c;
+        const float4 x = make_float4(o.x + v[0], o.y + v[1], o.z + v[2], o.w + v[3]);
+        *c = x;
+        const float4 g = *(const float4*)(a.nrm_g + n);
+        *(uint2*)(a.nrm_out16 + (size_t)m * a.ldc + n) = make_uint2(pk_bf16(x.x * g.x, x.y * g.y),
+                                                                      pk_bf16(x.z * g.z, x.w * g.w));
+        return (x.x * x.x + x.y * x.y) + (x.z * x.z + x.w * x.w);
+      } else if constexpr (EPI == GEPI_ACCUM) {
         const float4 o = *c;
         *c = make_float4(o.x + v[0], o.y + v[1], o.z + v[2], o.w + v[3]);
       } else {
         *c = make_float4(v[0], v[1], v[2], v[3]);
       }
     }
+    return 0.f;
   };
   if (S == 1) {
+    float ss[MT];
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt) finish(16 * mt + rr, n0 + nl, acc[mt]);
+    for (int mt = 0; mt < MT; ++mt) ss[mt] = finish(16 * mt + rr, n0 + nl, acc[mt]);
+    if constexpr (EPI == GEPI_ACCUM_NORM) {
+      // tile partial per row: the 4 q lanes of a wave (shuffles), then the RB waves (LDS, in
+      // wave order); Xs is free after the main loop's last barrier
+      float* red = (float*)&Xs[0][0];
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        float s = ss[mt];
+        s += __shfl_xor(s, 16, 64);
+        s += __shfl_xor(s, 32, 64);
+        if (q == 0) red[wave * MP + 16 * mt + rr] = s;
+      }
+      __syncthreads();
+      if (tid < a.M) {
+        float s = red[tid];
+        for (int w = 1; w < RB; ++w) s += red[w * MP + tid];
+        a.nrm_part[(size_t)tid * a.nrm_parts + rg] = s;
+      }
+    }
     return;
   }
   // split-K: slab [sp][rg][MP][ROWS] written through (sc1: no release fence needed), then the
@@ -275,7 +332,13 @@ __global__ void __launch_bounds__(RB * 64) gemm_skinny_kernel(GemmQArgs a, int S
 #pragma unroll
     for (int k = 1; k < SK_SMAX; ++k)
       if (k < S) v += part[k];
-    finish(m, n0 + n4, v);
+    float s = finish(m, n0 + n4, v);
+    if constexpr (EPI == GEPI_ACCUM_NORM) {
+      // a row's ROWS / 4 units sit on consecutive lanes of one wave
+#pragma unroll
+      for (int o = 1; o < ROWS / 4; o <<= 1) s += __shfl_xor(s, o, 64);
+      if (n4 == 0 && m < a.M) a.nrm_part[(size_t)m * a.nrm_parts + rg] = s;
+    }
   }
 }
 
@@ -300,6 +363,9 @@ static void sk_launch(const GemmQArgs& a, int S, hipStream_t st) {
     case GEPI_ACCUM:
       hipLaunchKernelGGL((gemm_skinny_kernel<QT, RB, MT, GEPI_ACCUM>), dim3(grid), dim3(RB * 64), 0, st, a, S);
       break;
+    case GEPI_ACCUM_NORM:
+      hipLaunchKernelGGL((gemm_skinny_kernel<QT, RB, MT, GEPI_ACCUM_NORM>), dim3(grid), dim3(RB * 64), 0, st, a, S);
+      break;
     default:
       hipLaunchKernelGGL((gemm_skinny_kernel<QT, RB, MT, GEPI_SWIGLU_BF16>), dim3(grid), dim3(RB * 64), 0, st, a, S);
       break;
@@ -313,14 +379,34 @@ static void sk_mt(const GemmQArgs& a, int S, hipStream_t st) {
   else sk_launch<QT, RB, 4>(a, S, st);
 }
 
-template <int QT>
-static bool sk_qt(const GemmQArgs& a, hipStream_t st) {
-  using F = SkFmt<QT>;
+// waves (16-row groups) per workgroup: 8 when every segment splits into 128-row tiles
+static int sk_rb(const GemmQArgs& a) {
   bool rows128 = a.N % 128 == 0;
   for (int s = 0; s < a.nseg; ++s)
     if (a.seg_n0[s] % 128 || a.seg[s].rows % 128) rows128 = false;
   const int force_rb = sk_env("AIOS_SKINNY_RB", 0);
-  const int RB = force_rb == 4 ? 4 : (force_rb == 8 ? (rows128 ? 8 : 4) : (rows128 ? 8 : 4));
+  return force_rb == 4 ? 4 : (rows128 ? 8 : 4);
+}
+
+static bool sk_fits(const GemmQArgs& a) {
+  if (a.M > 64 || a.N % 64) return false;
+  if (a.epi == GEPI_SWIGLU_BF16 && a.ldc % 2) return false;
+  if ((a.epi != GEPI_SWIGLU_BF16 && a.ldc % 4) || a.lda % 8) return false;
+  if (a.nrm_in && (a.nrm_parts % 4 || a.nrm_parts > 64)) return false;
+  if (a.epi == GEPI_ACCUM_NORM && (!a.nrm_g || !a.nrm_out16 || !a.nrm_part || a.N / (16 * sk_rb(a)) != a.nrm_parts))
+    return false;
+  switch (a.seg[0].qtype) {
+    case QT_Q4_K: case QT_Q5_K: case QT_Q6_K: case QT_Q4_0: case QT_Q8_0: case QT_F16: case QT_BF16: return true;
+    default: return false;
+  }
+}
+
+int gemm_skinny_ntile(const GemmQArgs& a) { return a.M <= 64 && a.N % 64 == 0 ? a.N / (16 * sk_rb(a)) : 0; }
+
+template <int QT>
+static bool sk_qt(const GemmQArgs& a, hipStream_t st) {
+  using F = SkFmt<QT>;
+  const int RB = sk_rb(a);
   const int ntile = a.N / (16 * RB);
   const int nsteps = (a.K / F::W + 3) / 4, nchunk = (nsteps + SK_NL - 1) / SK_NL;
   const int MP = 16 * (a.M <= 16 ? 1 : (a.M <= 32 ? 2 : 4));
@@ -341,9 +427,7 @@ static bool sk_qt(const GemmQArgs& a, hipStream_t st) {
 }
 
 bool launch_gemm_skinny(const GemmQArgs& a, hipStream_t st) {
-  if (a.M > 64 || a.N % 64) return false;
-  if (a.epi == GEPI_SWIGLU_BF16 && a.ldc % 2) return false;
-  if ((a.epi != GEPI_SWIGLU_BF16 && a.ldc % 4) || a.lda % 8) return false;
+  if (!sk_fits(a)) return false;
   switch (a.seg[0].qtype) {
     case QT_Q4_K: return sk_qt<QT_Q4_K>(a, st);
     case QT_Q5_K: return sk_qt<QT_Q5_K>(a, st);

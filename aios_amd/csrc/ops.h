@@ -150,7 +150,7 @@ void launch_gemm(const GemmArgs& a, hipStream_t st);
 bool gemm_supports(int qt);
 
 // multi-segment GEMM with fused epilogues (the prefill path): C = A x [W0; W1; W2]^T
-enum GemmEpi { GEPI_STORE = 0, GEPI_ACCUM = 1, GEPI_SWIGLU_BF16 = 2, GEPI_QKV = 3 };
+enum GemmEpi { GEPI_STORE = 0, GEPI_ACCUM = 1, GEPI_SWIGLU_BF16 = 2, GEPI_QKV = 3, GEPI_ACCUM_NORM = 4 };
 struct GemmQArgs {
   const bf16_t* A;   // [M][lda] bf16
   int lda;
@@ -181,10 +181,24 @@ struct GemmQArgs {
   float* q_out;
   bf16_t* k_cache;
   bf16_t* v_cache;
+  // RMSNorm split across two skinny GEMMs (batched decode: no normalisation launch).
+  //  producer (GEPI_ACCUM_NORM = residual add): also writes bf16(x_new * nrm_g) to nrm_out16
+  //    [M][ldc] and, per output tile t, sum_n x_new[m][n]^2 to nrm_part[m * nrm_parts + t]
+  //    (nrm_parts = gemm_skinny_ntile(producer args); fixed-order reductions, no atomics)
+  //  consumer (any epilogue, nrm_in set): A is that bf16(x * g); output row m is scaled by
+  //    rsqrt(sum_t nrm_in[m * nrm_parts + t] / K + nrm_eps) before the epilogue
+  const float* nrm_g;
+  bf16_t* nrm_out16;
+  float* nrm_part;
+  const float* nrm_in;
+  int nrm_parts;
+  float nrm_eps;
 };
 // bytes of split-K workspace / ticket count the skinny GEMM may use for an M x N output
 size_t gemm_skinny_ws_bytes(int M, int N);
 int gemm_skinny_cnt_len(int N);
+// output tiles of the skinny kernel for these args (0: not served by the skinny kernel)
+int gemm_skinny_ntile(const GemmQArgs& a);
 void launch_gemm_q(const GemmQArgs& a, hipStream_t st);
 
 }  // namespace aios

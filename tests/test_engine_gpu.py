@@ -165,6 +165,36 @@ def test_batched_decode_gemm_path_matches_gemv_path(model_files, monkeypatch, B,
     assert np.abs(l0 - l1).max() < 2e-2 * scale
 
 
+@pytest.mark.parametrize("recipe,rb,split", [("Q4_K_M", "0", "0"), ("Q4_K_M", "4", "1"),
+                                             ("mistral_shape", "0", "1"), ("mistral_shape", "4", "0")])
+def test_batched_decode_split_rmsnorm_matches_explicit(model_files, monkeypatch, recipe, rb, split):
+    """AIOS_GEMM_NORM_FUSE: the residual GEMMs (O, down) emit bf16(x * g_next) plus per-tile row
+    sums of squares and the next GEMM scales its rows by the inverse RMS -- the explicit
+    normalisation launches' result to bf16 rounding, with the reduction tiles over 4..16 parts
+    (AIOS_SKINNY_RB) on both the split-K last-arriver and the one-slice epilogue (AIOS_SKINNY_S)."""
+    monkeypatch.setenv("AIOS_DECODE_GEMM_MIN_B", "2")
+    monkeypatch.setenv("AIOS_SKINNY_RB", rb)
+    if split == "1":
+        monkeypatch.setenv("AIOS_SKINNY_S", "1")
+    path = model_files[recipe]
+    B = 4
+    prompts = [[1, 5, 6, 7], [1, 9, 10, 11, 12, 13], [1, 100, 200], [1, 3, 4]]
+    outs = {}
+    for fuse in ("0", "1"):
+        monkeypatch.setenv("AIOS_GEMM_NORM_FUSE", fuse)
+        eng, cfg = _load(path, max_slots=4, max_batch=4, act_q8=False)
+        want_parts = cfg.d_model // (16 * (4 if rb == "4" else 8)) if fuse == "1" else 0
+        assert eng.norm_fused_parts == want_parts
+        firsts = [int(np.argmax(eng.prefill(s, p, 0, True))) for s, p in enumerate(prompts)]
+        eng.decode_loop_prepare(list(range(B)), firsts, [len(p) for p in prompts])
+        eng.decode_loop_run(B, 3, True)
+        outs[fuse] = np.asarray(eng.last_logits(B)).reshape(B, -1)
+        del eng
+    l0, l1 = outs["0"], outs["1"]
+    assert np.isfinite(l1).all()
+    assert np.abs(l0 - l1).max() < 1e-2 * max(np.abs(l0).max(), 1.0)
+
+
 @pytest.mark.parametrize("recipe", ["Q4_K_M", "mistral_shape"])
 def test_prefill_one_chunk_matches_reference(model_files, recipe):
     """A 140-token prompt prefills as ONE GEMM chunk (big-M MFMA kernel, dequant fused; no bf16
