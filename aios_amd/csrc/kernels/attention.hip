@@ -29,7 +29,7 @@ template <int HD, int G>
 __global__ void __launch_bounds__(512) attn_decode_kernel(AttnDecodeArgs a, AttnSplit sp_) {
   const int wg = blockIdx.x;
   const int len = a.seq_len[blockIdx.z];
-  if (G > 1 && len <= ATTN_SPLIT_LEN) {
+  if (G > 1 && len <= a.short_len) {
     const int h = wg / sp_.p_short, sp = wg % sp_.p_short;
     if (h >= a.n_heads) return;
     attn_core<HD, 1>(a, sp, h / G, h, h, sp_.p_short, sp_.ppw);
@@ -76,6 +76,14 @@ void launch_attn_decode(const AttnDecodeArgs& a, hipStream_t st) {
   const int G = a.n_heads / a.n_kv_heads;
   AttnDecodeArgs b = a;
   if (b.split <= 0) b.split = attn_decode_split(a.max_ctx, a.B, a.n_kv_heads);
+  // Batched decode fills the chip with (row, KV head) workgroups on its own: from
+  // AIOS_ATTN_GROUPED_MIN such workgroups up, every context length takes the grouped mode (one
+  // K/V read for the G query heads of a KV head) instead of the per-query-head split that buys
+  // batch-1 latency with G x the K/V reads and workgroups
+  if (b.short_len < 0) {
+    const int grouped_min = attn_env_int("AIOS_ATTN_GROUPED_MIN", 128);
+    b.short_len = (grouped_min > 0 && a.B * a.n_kv_heads >= grouped_min) ? 0 : ATTN_SPLIT_LEN;
+  }
   if (b.split % ATTN_CHUNK) throw std::runtime_error("attn_decode: split must be a multiple of ATTN_CHUNK");
   if (a.head_dim == 128) launch_hd<128>(b, G, st);
   else if (a.head_dim == 64) launch_hd<64>(b, G, st);

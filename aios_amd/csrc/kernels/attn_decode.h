@@ -406,6 +406,6 @@ inline int attn_plan(const AttnDecodeArgs& a, int G, AttnSplit& sp) {
   if (sp.p_long > a.n_chunks || sp.p_long > 64 || sp.p_short > a.n_chunks)
     throw std::runtime_error("attn_decode: more splits than partial buffers / 64");
   const int GL = (G % 4 == 0) ? 4 : G;
-  return std::max(a.n_kv_heads * (G / GL) * sp.p_long, G > 1 ? a.n_heads * sp.p_short : 0);
+  return std::max(a.n_kv_heads * (G / GL) * sp.p_long, G > 1 && a.short_len != 0 ? a.n_heads * sp.p_short : 0);
 }
 }  // namespace aios

@@ -74,6 +74,7 @@ struct AttnDecodeArgs {
   float* ml;               // [B][n_heads][n_chunks][2]
   float* out;              // [B][n_heads*hd]
   bf16_t* out16 = nullptr; // if set: the output as bf16 instead (the batched-decode GEMM's A operand)
+  int short_len = -1;      // contexts up to this many keys split by query head (-1: launcher decides)
   int* counters;           // [B][n_kv_heads] arrival tickets, zero-initialised, self re-arming
 };
 constexpr int ATTN_CHUNK = 64;

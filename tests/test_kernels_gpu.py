@@ -330,7 +330,12 @@ def test_gemv_b1_cu_qkv(E, mixed, table, grid, sel):
                                           ([1500, 513, 512, 2048], 2048), ([1025, 3], 1280)])
 @pytest.mark.parametrize("split", [0, 64, 192])  # 0 = the launcher's choice
 @pytest.mark.parametrize("paging", ["identity", "slot_table", "row_table"])
-def test_attention_decode(E, hd, H, Hkv, lens, max_ctx, split, paging):
+@pytest.mark.parametrize("grouped", ["", "1"])  # "1": AIOS_ATTN_GROUPED_MIN=1, the batched grouped mode
+def test_attention_decode(E, hd, H, Hkv, lens, max_ctx, split, paging, grouped, monkeypatch):
+    if grouped:
+        if split not in (0, 64):
+            pytest.skip("grouped mode: launcher and one-pass splits cover it")
+        monkeypatch.setenv("AIOS_ATTN_GROUPED_MIN", grouped)
     B = len(lens)
     slots = B + 1
     kc = (torch.randn(slots, Hkv, max_ctx, hd) * 0.5).to(torch.bfloat16)
