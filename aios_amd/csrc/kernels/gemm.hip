@@ -231,6 +231,7 @@ static void launch_big(const GemmQArgs& a, hipStream_t st) {
 // M <= 64: the skinny kernel (gemm_skinny.hip) streams the quantised weights straight into MFMA
 // operand registers; returns false when the shape / workspace does not fit it
 bool launch_gemm_skinny(const GemmQArgs& a, hipStream_t st);
+bool gemm_skinny_mixed_ok(const GemmQArgs& a);
 
 static void launch_one(const GemmQArgs& a, hipStream_t st) {
   static const int skinny_max = env_int("AIOS_GEMM_SKINNY_MAX_M", 64);
@@ -261,6 +262,9 @@ void launch_gemm_q(const GemmQArgs& a, hipStream_t st) {
     if (a.seg[s].rows % 64 || a.seg_n0[s] % 64) throw std::runtime_error("gemm: segment sizes must be multiples of 64");
   }
   if (a.N % 64) throw std::runtime_error("gemm: N must be a multiple of 64");
+  // mixed formats in ONE skinny launch where supported (the Q4_K_M QKV stack)
+  static const int skinny_max = env_int("AIOS_GEMM_SKINNY_MAX_M", 64);
+  if (a.M <= skinny_max && gemm_skinny_mixed_ok(a) && launch_gemm_skinny(a, st)) return;
   int s0 = 0;
   while (s0 < a.nseg) {
     int s1 = s0 + 1;

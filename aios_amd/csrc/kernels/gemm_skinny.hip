@@ -43,14 +43,16 @@ struct SkFmt {
   }
 };
 
+// the workgroup body for weight format QT (the kernel below picks it per tile); X chunks live in
+// the launch's dynamic LDS (two buffers of MP x XROW bf16, sized for the larger format)
 template <int QT, int RB, int MT, int EPI>
-__global__ void __launch_bounds__(RB * 64) gemm_skinny_kernel(GemmQArgs a, int S) {
+__device__ __forceinline__ void sk_body(const GemmQArgs& a, int S) {
   using F = SkFmt<QT>;
   constexpr int NT = RB * 64, ROWS = 16 * RB, MP = 16 * MT;
   constexpr int KC = F::KC, XROW = KC + 8;  // bf16 per LDS row (+16 B pad: conflict-free column reads)
   constexpr int XU = MP * KC / 8;           // 16-B units of one X chunk
   constexpr int XPT = (XU + NT - 1) / NT;   // per thread
-  __shared__ __attribute__((aligned(16))) bf16_t Xs[2][MP * XROW];
+  extern __shared__ __attribute__((aligned(16))) bf16_t sk_xs[];
   __shared__ int last_flag;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int rr = lane & 15, q = lane >> 4;
@@ -98,7 +100,7 @@ __global__ void __launch_bounds__(RB * 64) gemm_skinny_kernel(GemmQArgs a, int S
         const int m = u / (KC / 8), kl = 8 * (u % (KC / 8));
         gu32x4 v = xr[i];
         if (m >= a.M || kc0 + kl >= a.K) v = gu32x4{0u, 0u, 0u, 0u};
-        *(gu32x4*)&Xs[buf][m * XROW + kl] = v;
+        *(gu32x4*)&sk_xs[buf * (MP * XROW) + m * XROW + kl] = v;
       }
     }
   };
@@ -165,7 +167,7 @@ __global__ void __launch_bounds__(RB * 64) gemm_skinny_kernel(GemmQArgs a, int S
       const int kl = F::part_k(c, i) - kc0;
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
-        const uint4 xv = *(const uint4*)&Xs[buf][(16 * mt + rr) * XROW + kl];
+        const uint4 xv = *(const uint4*)&sk_xs[buf * (MP * XROW) + (16 * mt + rr) * XROW + kl];
         gbf16x8 xf;
         __builtin_memcpy(&xf, &xv, 16);
         acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, xf, acc[mt], 0, 0, 0);
@@ -280,7 +282,7 @@ __global__ void __launch_bounds__(RB * 64) gemm_skinny_kernel(GemmQArgs a, int S
     if constexpr (EPI == GEPI_ACCUM_NORM) {
       // tile partial per row: the 4 q lanes of a wave (shuffles), then the RB waves (LDS, in
       // wave order); Xs is free after the main loop's last barrier
-      float* red = (float*)&Xs[0][0];
+      float* red = (float*)&sk_xs[0];
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
         float s = ss[mt];
@@ -342,6 +344,21 @@ __global__ void __launch_bounds__(RB * 64) gemm_skinny_kernel(GemmQArgs a, int S
   }
 }
 
+// One launch for every tile: with mixed formats (Q4_K_M: Q|K Q4_K, V Q6_K) the tiles of the last
+// segment run the QT1 body -- the V rows then share the launch (and the chip) with Q|K instead of
+// following as a 64-workgroup launch of their own
+template <int QT0, int QT1, int RB, int MT, int EPI>
+__global__ void __launch_bounds__(RB * 64) gemm_skinny_kernel(GemmQArgs a, int S) {
+  if constexpr (QT0 != QT1) {
+    const int L = xcd_remap(blockIdx.x, (a.N / (16 * RB)) * S);
+    if ((L / S) * 16 * RB >= a.seg_n0[a.nseg - 1]) {
+      sk_body<QT1, RB, MT, EPI>(a, S);
+      return;
+    }
+  }
+  sk_body<QT0, RB, MT, EPI>(a, S);
+}
+
 size_t gemm_skinny_ws_bytes(int M, int N) { return (size_t)8 * 16 * ((M + 15) / 16) * N * 4; }
 int gemm_skinny_cnt_len(int N) { return N / 64 + 1; }
 
@@ -350,33 +367,31 @@ static int sk_env(const char* name, int dflt) {
   return e ? std::atoi(e) : dflt;
 }
 
-template <int QT, int RB, int MT>
+template <int QT0, int QT1, int RB, int MT>
 static void sk_launch(const GemmQArgs& a, int S, hipStream_t st) {
   const int grid = (a.N / (16 * RB)) * S;
-  switch (a.epi) {
-    case GEPI_STORE:
-      hipLaunchKernelGGL((gemm_skinny_kernel<QT, RB, MT, GEPI_STORE>), dim3(grid), dim3(RB * 64), 0, st, a, S);
-      break;
-    case GEPI_QKV:
-      hipLaunchKernelGGL((gemm_skinny_kernel<QT, RB, MT, GEPI_QKV>), dim3(grid), dim3(RB * 64), 0, st, a, S);
-      break;
-    case GEPI_ACCUM:
-      hipLaunchKernelGGL((gemm_skinny_kernel<QT, RB, MT, GEPI_ACCUM>), dim3(grid), dim3(RB * 64), 0, st, a, S);
-      break;
-    case GEPI_ACCUM_NORM:
-      hipLaunchKernelGGL((gemm_skinny_kernel<QT, RB, MT, GEPI_ACCUM_NORM>), dim3(grid), dim3(RB * 64), 0, st, a, S);
-      break;
-    default:
-      hipLaunchKernelGGL((gemm_skinny_kernel<QT, RB, MT, GEPI_SWIGLU_BF16>), dim3(grid), dim3(RB * 64), 0, st, a, S);
-      break;
+  const int lds = 2 * 16 * MT * (std::max(SkFmt<QT0>::KC, SkFmt<QT1>::KC) + 8) * 2;
+#define SK_GO(E) hipLaunchKernelGGL((gemm_skinny_kernel<QT0, QT1, RB, MT, E>), dim3(grid), dim3(RB * 64), lds, st, a, S)
+  if constexpr (QT0 != QT1) {  // mixed formats: the packed QKV projection only
+    if (a.epi == GEPI_QKV) SK_GO(GEPI_QKV);
+    else SK_GO(GEPI_STORE);
+  } else {
+    switch (a.epi) {
+      case GEPI_STORE: SK_GO(GEPI_STORE); break;
+      case GEPI_QKV: SK_GO(GEPI_QKV); break;
+      case GEPI_ACCUM: SK_GO(GEPI_ACCUM); break;
+      case GEPI_ACCUM_NORM: SK_GO(GEPI_ACCUM_NORM); break;
+      default: SK_GO(GEPI_SWIGLU_BF16); break;
+    }
   }
+#undef SK_GO
 }
 
-template <int QT, int RB>
+template <int QT0, int QT1, int RB>
 static void sk_mt(const GemmQArgs& a, int S, hipStream_t st) {
-  if (a.M <= 16) sk_launch<QT, RB, 1>(a, S, st);
-  else if (a.M <= 32) sk_launch<QT, RB, 2>(a, S, st);
-  else sk_launch<QT, RB, 4>(a, S, st);
+  if (a.M <= 16) sk_launch<QT0, QT1, RB, 1>(a, S, st);
+  else if (a.M <= 32) sk_launch<QT0, QT1, RB, 2>(a, S, st);
+  else sk_launch<QT0, QT1, RB, 4>(a, S, st);
 }
 
 // waves (16-row groups) per workgroup: 8 when every segment splits into 128-row tiles
@@ -403,15 +418,17 @@ static bool sk_fits(const GemmQArgs& a) {
 
 int gemm_skinny_ntile(const GemmQArgs& a) { return a.M <= 64 && a.N % 64 == 0 ? a.N / (16 * sk_rb(a)) : 0; }
 
-template <int QT>
+template <int QT0, int QT1>
 static bool sk_qt(const GemmQArgs& a, hipStream_t st) {
-  using F = SkFmt<QT>;
+  using F0 = SkFmt<QT0>;
+  using F1 = SkFmt<QT1>;
   const int RB = sk_rb(a);
   const int ntile = a.N / (16 * RB);
-  const int nsteps = (a.K / F::W + 3) / 4, nchunk = (nsteps + SK_NL - 1) / SK_NL;
+  auto nchunk_of = [&](int W) { return ((a.K / W + 3) / 4 + SK_NL - 1) / SK_NL; };
+  const int nchunk = std::min(nchunk_of(F0::W), nchunk_of(F1::W));
   const int MP = 16 * (a.M <= 16 ? 1 : (a.M <= 32 ? 2 : 4));
   // LDS per workgroup: two X chunks; resident workgroups per CU bounded by LDS and by 2048 threads
-  const int lds = 2 * MP * (F::KC + 8) * 2;
+  const int lds = 2 * MP * (std::max(F0::KC, F1::KC) + 8) * 2;
   const int per_cu = std::max(1, std::min(163840 / lds, 2048 / (RB * 64)));
   int S = a.ksplit > 0 ? a.ksplit : sk_env("AIOS_SKINNY_S", 0);
   if (S <= 0) {
@@ -421,21 +438,34 @@ static bool sk_qt(const GemmQArgs& a, hipStream_t st) {
   S = std::max(1, std::min({S, nchunk, SK_SMAX}));
   // split-K needs the slab workspace and tickets; without them, one workgroup per tile
   if (S > 1 && (!a.ws || !a.cnt || a.cnt_len < ntile || a.ws_bytes < (size_t)S * MP * a.N * 4)) S = 1;
-  if (RB == 8) sk_mt<QT, 8>(a, S, st);
-  else sk_mt<QT, 4>(a, S, st);
+  if (RB == 8) sk_mt<QT0, QT1, 8>(a, S, st);
+  else sk_mt<QT0, QT1, 4>(a, S, st);
   return true;
+}
+
+// the mixed-format launch (AIOS_SKINNY_MIXED, default on): leading segments Q4_K, last Q6_K (the
+// Q4_K_M QKV stack), the QKV / store epilogues
+bool gemm_skinny_mixed_ok(const GemmQArgs& a) {
+  if (a.nseg < 2 || !sk_env("AIOS_SKINNY_MIXED", 1)) return false;
+  const int q1 = a.seg[a.nseg - 1].qtype;
+  for (int s = 0; s + 1 < a.nseg; ++s)
+    if (a.seg[s].qtype != QT_Q4_K) return false;
+  return q1 == QT_Q6_K && (a.epi == GEPI_QKV || a.epi == GEPI_STORE);
 }
 
 bool launch_gemm_skinny(const GemmQArgs& a, hipStream_t st) {
   if (!sk_fits(a)) return false;
+  bool same = true;
+  for (int s = 1; s < a.nseg; ++s) same &= a.seg[s].qtype == a.seg[0].qtype;
+  if (!same) return gemm_skinny_mixed_ok(a) && sk_qt<QT_Q4_K, QT_Q6_K>(a, st);
   switch (a.seg[0].qtype) {
-    case QT_Q4_K: return sk_qt<QT_Q4_K>(a, st);
-    case QT_Q5_K: return sk_qt<QT_Q5_K>(a, st);
-    case QT_Q6_K: return sk_qt<QT_Q6_K>(a, st);
-    case QT_Q4_0: return sk_qt<QT_Q4_0>(a, st);
-    case QT_Q8_0: return sk_qt<QT_Q8_0>(a, st);
-    case QT_F16: return sk_qt<QT_F16>(a, st);
-    case QT_BF16: return sk_qt<QT_BF16>(a, st);
+    case QT_Q4_K: return sk_qt<QT_Q4_K, QT_Q4_K>(a, st);
+    case QT_Q5_K: return sk_qt<QT_Q5_K, QT_Q5_K>(a, st);
+    case QT_Q6_K: return sk_qt<QT_Q6_K, QT_Q6_K>(a, st);
+    case QT_Q4_0: return sk_qt<QT_Q4_0, QT_Q4_0>(a, st);
+    case QT_Q8_0: return sk_qt<QT_Q8_0, QT_Q8_0>(a, st);
+    case QT_F16: return sk_qt<QT_F16, QT_F16>(a, st);
+    case QT_BF16: return sk_qt<QT_BF16, QT_BF16>(a, st);
     default: return false;
   }
 }

@@ -196,6 +196,26 @@ def test_batched_decode_split_rmsnorm_matches_explicit(model_files, monkeypatch,
 
 
 @pytest.mark.parametrize("recipe", ["Q4_K_M", "mistral_shape"])
+def test_batched_decode_mixed_format_qkv_launch(model_files, monkeypatch, recipe):
+    """AIOS_SKINNY_MIXED: the Q4_K_M QKV stack (Q|K Q4_K, V Q6_K) as ONE skinny launch whose V
+    tiles run the Q6_K body -- the same logits as one launch per format."""
+    monkeypatch.setenv("AIOS_DECODE_GEMM_MIN_B", "2")
+    path = model_files[recipe]
+    B = 4
+    prompts = [[1, 5, 6, 7], [1, 9, 10, 11, 12, 13], [1, 100, 200], [1, 3, 4]]
+    outs = {}
+    for mixed in ("0", "1"):
+        monkeypatch.setenv("AIOS_SKINNY_MIXED", mixed)
+        eng, cfg = _load(path, max_slots=4, max_batch=4, act_q8=False)
+        firsts = [int(np.argmax(eng.prefill(s, p, 0, True))) for s, p in enumerate(prompts)]
+        eng.decode_loop_prepare(list(range(B)), firsts, [len(p) for p in prompts])
+        eng.decode_loop_run(B, 3, True)
+        outs[mixed] = np.asarray(eng.last_logits(B)).reshape(B, -1)
+        del eng
+    assert np.abs(outs["0"] - outs["1"]).max() < 1e-3 * max(np.abs(outs["0"]).max(), 1.0)
+
+
+@pytest.mark.parametrize("recipe", ["Q4_K_M", "mistral_shape"])
 def test_prefill_one_chunk_matches_reference(model_files, recipe):
     """A 140-token prompt prefills as ONE GEMM chunk (big-M MFMA kernel, dequant fused; no bf16
     weight copy exists) and matches the fp32 reference."""
