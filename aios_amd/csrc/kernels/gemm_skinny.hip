@@ -27,7 +27,8 @@
 namespace aios {
 
 constexpr int SK_NL = 4;    // weight ring depth = steps per X chunk
-constexpr int SK_SMAX = 8;  // K splits at most (slab workspace: gemm_skinny_ws_bytes)
+constexpr int SK_SMAX = 16;  // K splits at most (slab workspace: gemm_skinny_ws_bytes)
+constexpr int SK_SB = 8;     // slices summed per batch of loads in the last arriver
 
 template <int QT>
 struct SkFmt {
@@ -325,15 +326,17 @@ __device__ __forceinline__ void sk_body(const GemmQArgs& a, int S) {
   const float* base = a.ws + (size_t)rg * MP * ROWS;
   for (int u = tid; u < MP * ROWS / 4; u += NT) {
     const int m = u / (ROWS / 4), n4 = 4 * (u % (ROWS / 4));
-    // all slices' loads in flight at once (S <= SK_SMAX; clamped re-reads weighted by zero)
-    gf32x4 part[SK_SMAX];
+    // SK_SB slices' loads in flight at once (clamped re-reads weighted by zero), in fixed order
+    gf32x4 v = gf32x4{0.f, 0.f, 0.f, 0.f};
+    for (int k0 = 0; k0 < S; k0 += SK_SB) {
+      gf32x4 part[SK_SB];
 #pragma unroll
-    for (int k = 0; k < SK_SMAX; ++k)
-      part[k] = *(const gf32x4*)(base + min(k, S - 1) * sstride + (size_t)m * ROWS + n4);
-    gf32x4 v = part[0];
+      for (int k = 0; k < SK_SB; ++k)
+        part[k] = *(const gf32x4*)(base + min(k0 + k, S - 1) * sstride + (size_t)m * ROWS + n4);
 #pragma unroll
-    for (int k = 1; k < SK_SMAX; ++k)
-      if (k < S) v += part[k];
+      for (int k = 0; k < SK_SB; ++k)
+        if (k0 + k < S) v += part[k];
+    }
     float s = finish(m, n0 + n4, v);
     if constexpr (EPI == GEPI_ACCUM_NORM) {
       // a row's ROWS / 4 units sit on consecutive lanes of one wave
@@ -359,7 +362,7 @@ __global__ void __launch_bounds__(RB * 64) gemm_skinny_kernel(GemmQArgs a, int S
   sk_body<QT0, RB, MT, EPI>(a, S);
 }
 
-size_t gemm_skinny_ws_bytes(int M, int N) { return (size_t)8 * 16 * ((M + 15) / 16) * N * 4; }
+size_t gemm_skinny_ws_bytes(int M, int N) { return (size_t)SK_SMAX * 16 * ((M + 15) / 16) * N * 4; }
 int gemm_skinny_cnt_len(int N) { return N / 64 + 1; }
 
 static int sk_env(const char* name, int dflt) {
@@ -432,8 +435,22 @@ static bool sk_qt(const GemmQArgs& a, hipStream_t st) {
   const int per_cu = std::max(1, std::min(163840 / lds, 2048 / (RB * 64)));
   int S = a.ksplit > 0 ? a.ksplit : sk_env("AIOS_SKINNY_S", 0);
   if (S <= 0) {
-    const int target = device_cu_count() * std::min(per_cu, 2);
-    S = ntile >= target ? 1 : (target + ntile - 1) / ntile;
+    // resident workgroups: LDS / threads allow per_cu, the ~100-VGPR bodies 2 of 8 waves
+    const int cap = device_cu_count() * std::min(per_cu, 2);
+    if (sk_env("AIOS_SKINNY_SPLIT_MODE", 1) == 0) {
+      S = ntile >= cap ? 1 : (cap + ntile - 1) / ntile;
+    } else {
+      // fewest dispatch rounds per unit of K work: a partial second round of workgroups costs a
+      // whole round (224 gate/up tiles: S = 2 in one round, not S = 3 in 1.3).  At most 8 slices
+      // by default (AIOS_SKINNY_SMAX; tools/gpu_split_ab.sh, Mistral B = 32: 16 slices for the
+      // d_model-wide projections 8333 tok/s, 8 slices 8867, the old fill rule 8038)
+      double best = 1e30;
+      const int smax = std::min({nchunk, SK_SMAX, sk_env("AIOS_SKINNY_SMAX", 8)});
+      for (int s = 1; s <= smax; ++s) {
+        const double cost = (double)((ntile * s + cap - 1) / cap) / s;
+        if (cost < best - 1e-9) { best = cost; S = s; }
+      }
+    }
   }
   S = std::max(1, std::min({S, nchunk, SK_SMAX}));
   // split-K needs the slab workspace and tickets; without them, one workgroup per tile

@@ -633,9 +633,26 @@ def test_gemm_skinny(E, t, M, ksplit, epi):
     assert torch.allclose(C.cpu(), ref, atol=3e-3, rtol=3e-3), (C.cpu() - ref).abs().max()
 
 
+@pytest.mark.parametrize("t", [GGMLType.Q4_K, GGMLType.Q6_K])
+@pytest.mark.parametrize("M", [8, 40])
+@pytest.mark.parametrize("ksplit", [9, 16])
+def test_gemm_skinny_wide_split(E, t, M, ksplit):
+    # K = 14336 over 9 / 16 slices: the last arriver sums the slabs in batches of 8 (fixed order)
+    N, K = 256, 14336
+    m, W = qmat(E, t, N, K, seed=61, std=0.01)
+    A = torch.randn(M, K, device="cuda").to(torch.bfloat16)
+    C = torch.full((M, N), 1.0, device="cuda")
+    for _ in range(2):  # the second launch re-uses the re-armed tickets
+        C.fill_(1.0)
+        E.gemm_q(A.data_ptr(), K, [m], M, C.data_ptr(), 0, N, E.GEPI_ACCUM, stream(), ksplit)
+    torch.cuda.synchronize()
+    ref = A.float().cpu() @ W.to(torch.bfloat16).float().T + 1.0
+    assert torch.allclose(C.cpu(), ref, atol=5e-3, rtol=5e-3), (C.cpu() - ref).abs().max()
+
+
 @pytest.mark.parametrize("M", [4, 32])
 def test_gemm_skinny_mixed_segments_long_k(E, M):
-    # Q4_K_M-style QKV (Q4_K q/k + Q6_K v, two launches) and a K = 14336 down projection with the
+    # Q4_K_M-style QKV (Q4_K q/k + Q6_K v, one mixed-format launch) and a K = 14336 down projection with the
     # automatic split: every tile's last arriver reduces the slabs (tickets re-armed per launch)
     K = 4096
     segs = [(GGMLType.Q4_K, 512), (GGMLType.Q4_K, 128), (GGMLType.Q6_K, 128)]
