@@ -119,6 +119,7 @@ class Engine {
   void set_allgather(AllGatherFn fn, void* ctx) { allgather_ = fn; allgather_ctx_ = ctx; }
   bool vocab_parallel() const { return cfg_.vocab_parallel != 0; }
   void reset_graphs();
+  int capture_graphs(int max_b);  // pre-capture the decode-step graphs of B = 1..max_b (masked + unmasked)
   // ---- paged KV (block table per slot; see kv_offset in common.h) --------------------------------
   // prefix sharing: dst's positions [0, n) become src's -- full blocks shared (refcounted, never
   // written again by either slot: writes un-share first), the partial last block copied
@@ -236,6 +237,7 @@ class Engine {
   bool nrm_on(int B) const;
  private:
   void layer_decode_gemm(int l, int B);
+  hipGraphExec_t step_graph(int B);
   bool nrm_lm_ = false;  // the last layer's down GEMM prepared dec_xn16_ / nrm_part_ for lm_head(x_)
   int *pf_tokens_ = nullptr, *pf_pos_ = nullptr, *pf_seqlen_ = nullptr, *pf_slot_ = nullptr;
 

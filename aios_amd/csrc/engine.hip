@@ -1358,6 +1358,13 @@ void Engine::decode_loop_run(int B, int n_steps, bool use_graph) {
     for (int i = 0; i < n_steps; ++i) enqueue_decode_step(B);
     return;
   }
+  hipGraphExec_t ge = step_graph(B);
+  for (int i = 0; i < n_steps; ++i) HIP_CHECK(hipGraphLaunch(ge, stream_));
+}
+
+// the captured decode step for (B, sample_mask_): captured once, replayed for every request --
+// the kernels read tokens / positions / slots / sampling parameters from device arrays
+hipGraphExec_t Engine::step_graph(int B) {
   const int key = B * 2 + (sample_mask_ ? 1 : 0);
   auto it = graphs_.find(key);
   if (it == graphs_.end()) {
@@ -1375,7 +1382,23 @@ void Engine::decode_loop_run(int B, int n_steps, bool use_graph) {
     HIP_CHECK(hipGraphDestroy(g));
     it = graphs_.emplace(key, ge).first;
   }
-  for (int i = 0; i < n_steps; ++i) HIP_CHECK(hipGraphLaunch(it->second, stream_));
+  return it->second;
+}
+
+// capture (without running) the decode-step graphs of every batch size up to max_b, masked and
+// unmasked, so a serving scheduler whose batch grows and shrinks never stalls a step on a capture
+// (a 160-launch capture + instantiate costs milliseconds); returns the graphs held
+int Engine::capture_graphs(int max_b) {
+  if (!finalized_) throw std::runtime_error("engine not finalized");
+  HIP_CHECK(hipSetDevice(cfg_.device));
+  const bool saved = sample_mask_;
+  for (int B = 1; B <= std::min(max_b, cfg_.max_batch); ++B)
+    for (int m = 0; m < 2; ++m) {
+      sample_mask_ = m != 0;
+      step_graph(B);
+    }
+  sample_mask_ = saved;
+  return (int)graphs_.size();
 }
 
 std::vector<int> Engine::decode_loop_history(int B, int from_pos, int n) {

@@ -220,6 +220,11 @@ class ModelManager:
         batch = getattr(eng.config, "max_batch", self.max_batch)
         m.scheduler = Scheduler(eng, tok, min(batch, self.max_batch), min(slots, self.max_slots), m.context_length,
                                 m.grammar, name=m.name)
+        # capture every batch size's decode-step graph now, not on the first step that reaches it
+        # (a capture stalls that step by milliseconds; AIOS_GRAPH_WARMUP=0 skips)
+        capture = getattr(eng, "capture_graphs", None)
+        if capture is not None and os.environ.get("AIOS_GRAPH_WARMUP", "1") != "0":
+            capture(m.scheduler.max_batch)
         m.weight_bytes, m.kv_bytes = eng.weight_bytes, eng.kv_bytes
 
     # ------------------------------------------------------------------ tier lifecycle

@@ -94,6 +94,24 @@ def test_graph_loop_matches_eager(model_files):
     assert list(g) == list(e)
 
 
+def test_capture_graphs_precaptures_every_batch_size(model_files):
+    """capture_graphs(max_b) captures (without running) the masked and unmasked step graph of every
+    B; later decode calls replay them and give the same tokens as a fresh engine's lazily captured
+    graphs."""
+    path = model_files["Q4_K_M"]
+    prompts = [[1, 5, 6, 7], [1, 9, 10, 11, 12, 13], [1, 100, 200]]
+    outs = []
+    for pre in (False, True):
+        eng, cfg = _load(path, max_slots=4, max_batch=4)
+        if pre:
+            assert eng.capture_graphs(4) == 8
+            assert eng.capture_graphs(4) == 8  # idempotent
+        firsts = [int(np.argmax(eng.prefill(s, p, 0, True))) for s, p in enumerate(prompts)]
+        outs.append(eng.decode([0, 1, 2], firsts, [len(p) for p in prompts]))
+        del eng
+    assert outs[0] == outs[1]
+
+
 def test_random_init_engine_runs():
     from aios_amd.runtime.loader import random_engine
 
