@@ -217,8 +217,9 @@ class Engine {
   int *gm_tokens_ = nullptr, *gm_pos_ = nullptr, *gm_slot_ = nullptr;
   // batched decode through the skinny MFMA GEMM (B >= dec_gemm_min_b_): bf16 activation buffers
   // (MI355X, Mistral-7B Q4_K_M, tools/gpu_batch_ab.sh: B=2 GEMV 2.41 ms vs GEMM 3.25 ms, B=4 3.31 vs 3.26,
-  // B=8 5.80 vs 3.37 -- the skinny GEMM's per-step dequant floor loses below 4 rows)
-  int dec_gemm_min_b_ = 4;
+  // B=8 5.80 vs 3.37 -- the skinny GEMM's per-step dequant floor lost below 4 rows; after the split
+  // RMSNorm / mixed-QKV / split-K work, tools/gpu_minb_ab.sh: B=3 GEMV 956 vs GEMM 1065 tok/s, B=2 829 vs 712)
+  int dec_gemm_min_b_ = 3;
   bf16_t *dec_a16_ = nullptr, *dec_ff16_ = nullptr;
   // split-K slabs + arrival tickets of the skinny GEMM (shared by every decode GEMM of a step)
   float* gk_ws_ = nullptr;
