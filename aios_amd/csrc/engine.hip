@@ -953,6 +953,7 @@ void Engine::lm_head(int B, const float* x, int ldx) {
   if (dec_a16_ && ((dec_gemm_min_b_ > 0 && B >= dec_gemm_min_b_) || B > 8) && Vl % 64 == 0 &&
       gemm_supports(output_.w.qtype)) {
     const bool fused = nrm_lm_ && x == x_ && ldx == d;  // normalised by the last down GEMM
+    nrm_lm_ = false;  // one use: a later lm_head (prefill) normalises for itself
     if (!fused) launch_rmsnorm_bf16(x, ldx, out_norm_, dec_a16_, d, B, d, cfg_.norm_eps, stream_);
     GemmQArgs g;
     std::memset(&g, 0, sizeof(g));
