@@ -569,16 +569,21 @@ void Engine::finalize() {
       gm_pos_ = ibuf(G);
       gm_slot_ = ibuf(G);
       if (const char* e = std::getenv("AIOS_DECODE_GEMM_MIN_B")) dec_gemm_min_b_ = std::atoi(e);
+      // split-K slabs + tickets for every skinny-GEMM call: batched decode (M <= max_batch, the
+      // lm_head included) AND prefill chunks of 16-64 tokens (no lm_head) -- sized for the batch
+      // only, a 32-token prompt ran its projections unsplit (32 workgroups for N = d_model)
+      const int maxN = std::max({qd + 2 * kvd, d, 2 * cfg_.d_ff, V});
+      const int maxN_pf = std::max({qd + 2 * kvd, d, 2 * cfg_.d_ff});
+      gk_ws_bytes_ = std::max(Bm >= 2 ? gemm_skinny_ws_bytes(std::min(Bm, 64), maxN) : (size_t)0,
+                              gemm_skinny_ws_bytes(64, maxN_pf));
+      gk_ws_ = (float*)dmalloc(gk_ws_bytes_);
+      ws += gk_ws_bytes_;
+      gk_cnt_len_ = gemm_skinny_cnt_len(maxN);
+      gk_cnt_ = ibuf(gk_cnt_len_);
       if (Bm >= 2) {
         dec_a16_ = (bf16_t*)dmalloc((size_t)Bm * std::max(d, qd) * 2);
         dec_ff16_ = (bf16_t*)dmalloc((size_t)Bm * cfg_.d_ff * 2);
         ws += (size_t)Bm * (std::max(d, qd) + cfg_.d_ff) * 2;
-        const int maxN = std::max({qd + 2 * kvd, d, 2 * cfg_.d_ff, V});
-        gk_ws_bytes_ = gemm_skinny_ws_bytes(Bm, maxN);
-        gk_ws_ = (float*)dmalloc(gk_ws_bytes_);
-        ws += gk_ws_bytes_;
-        gk_cnt_len_ = gemm_skinny_cnt_len(maxN);
-        gk_cnt_ = ibuf(gk_cnt_len_);
         if (const char* e = std::getenv("AIOS_GEMM_NORM_FUSE")) nrm_fuse_ = std::atoi(e);
         GemmQArgs p;  // the residual producer's shape (O / down: N = d_model, one segment)
         std::memset(&p, 0, sizeof(p));
