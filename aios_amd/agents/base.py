@@ -276,6 +276,21 @@ class BaseAgent(ABC):
             return None
         return extract_json(text)
 
+    async def analyze(self, prompt: str, level: IntelligenceLevel | str = IntelligenceLevel.TACTICAL, **kw) -> str:
+        """think() for an analysis / advice paragraph; "" when the runtime is unavailable, so an
+        agent's action still returns its tool results without the model's reading of them."""
+        try:
+            return (await self.think(prompt, level, **kw)).strip()
+        except grpc.aio.AioRpcError as e:
+            logger.info("think unavailable: %s", e.details())
+            return ""
+
+    @staticmethod
+    def advice_lines(text: str, n: int = 5) -> List[str]:
+        """the first n non-empty lines of a model answer, list markers stripped"""
+        return [ln.strip().lstrip("-*0123456789.) ").strip() for ln in (text or "").splitlines()
+                if ln.strip().lstrip("-*0123456789.) ").strip()][:n]
+
     # ------------------------------------------------------------------ orchestrator
     async def register_with_orchestrator(self) -> bool:
         try:
@@ -402,10 +417,12 @@ class BaseAgent(ABC):
             except asyncio.TimeoutError:
                 pass
 
-    async def _heartbeat_loop(self):
+    async def heartbeat_loop(self):
+        """Heartbeat every heartbeat_interval_s until shutdown (reference base.py:684)."""
         await self.periodic(self.config.heartbeat_interval_s, self.send_heartbeat)
 
-    async def _poll_loop(self):
+    async def task_poll_loop(self):
+        """Poll GetAssignedTask, execute, report, until shutdown (reference base.py:728)."""
         while not self._stop.is_set():
             try:
                 busy = await self.poll_once()
@@ -430,7 +447,7 @@ class BaseAgent(ABC):
                 loop.add_signal_handler(sig, self.shutdown)
             except (NotImplementedError, RuntimeError):
                 pass
-        coros = [self._heartbeat_loop(), self._poll_loop(), *(await self.background())]
+        coros = [self.heartbeat_loop(), self.task_poll_loop(), *(await self.background())]
         self._bg = [asyncio.ensure_future(c) for c in coros]
         await self._stop.wait()
         for t in self._bg:

@@ -43,7 +43,14 @@ class LearningAgent(BaseAgent):
         for cat, n in by_cat.most_common(20):
             conf = min(1.0, n / total * 4) if total else 0.0
             patterns.append({"trigger": cat, "occurrences": n, "critical": crit.get(cat, 0), "confidence": conf})
-        return {"success": True, "patterns": patterns, "events_analyzed": total}
+        # which patterns are worth promoting to rules, which are anti-patterns (reference learning.py:181)
+        analysis = await self.analyze(
+            f"Pattern analysis over {total} recent events discovered {len(patterns)} patterns:\n" +
+            "\n".join(f"- '{p['trigger']}' (n={p['occurrences']}, critical={p['critical']}, "
+                      f"conf={p['confidence']:.2f})" for p in patterns[:15]) +
+            "\n\nWhich patterns are most valuable for the system? Any patterns that should be promoted to "
+            "automatic rules? Any concerning anti-patterns?", IntelligenceLevel.STRATEGIC) if patterns else ""
+        return {"success": True, "patterns": patterns, "events_analyzed": total, "analysis": analysis}
 
     async def update_patterns(self, task: Dict[str, Any]) -> Dict[str, Any]:
         ana = await self.analyze_patterns(task)
@@ -79,7 +86,24 @@ class LearningAgent(BaseAgent):
                     recs.append({"metric": k, "avg": avg, "suggestion": "sustained high load: scale out or throttle"})
                 elif peak < 20:
                     recs.append({"metric": k, "avg": avg, "suggestion": "resource mostly idle: consolidate work"})
-        return {"success": True, "recommendations": recs, "metrics_considered": len(hist)}
+        # the model's parameter changes from the same data (reference learning.py:268)
+        perf = {k: {"current": vs[-1], "mean": sum(vs) / len(vs), "min": min(vs), "max": max(vs)}
+                for k, vs in hist.items() if vs}
+        suggestions = []
+        if perf:
+            sug = await self.think_json(
+                "System parameter optimization analysis.\n\nPerformance data:\n" +
+                "\n".join(f"- {k}: current={v['current']:.1f}, mean={v['mean']:.1f}, "
+                          f"range=[{v['min']:.1f}, {v['max']:.1f}]" for k, v in perf.items()) +
+                "\n\nSuggest specific parameter changes to improve performance. JSON: {\"suggestions\": "
+                "[{\"parameter\": \"...\", \"current\": \"...\", \"suggested\": \"...\", \"impact\": \"...\"}]}",
+                IntelligenceLevel.STRATEGIC)
+            if isinstance(sug, dict) and isinstance(sug.get("suggestions"), list):
+                suggestions = [x for x in sug["suggestions"] if isinstance(x, dict)][:10]
+            elif isinstance(sug, list):
+                suggestions = [x for x in sug if isinstance(x, dict)][:10]
+        return {"success": True, "recommendations": recs, "ai_suggestions": suggestions,
+                "metrics_considered": len(hist)}
 
     async def tool_effectiveness(self, task: Dict[str, Any]) -> Dict[str, Any]:
         events = await self.get_recent_events(500)

@@ -9,7 +9,7 @@ import time
 from collections import defaultdict, deque
 from typing import Any, Deque, Dict, List
 
-from .base import BaseAgent, main_for
+from .base import BaseAgent, IntelligenceLevel, main_for
 
 METRIC_COLLECTION_INTERVAL_S = 30.0
 ANOMALY_CHECK_INTERVAL_S = 60.0
@@ -74,7 +74,16 @@ class MonitoringAgent(BaseAgent):
     async def generate_report(self, task: Dict[str, Any]) -> Dict[str, Any]:
         if not self.history:
             await self.collect_metrics(task)
-        return {"success": True, "report": {k: self._stats(k) for k in list(self.history)},
+        report = {k: self._stats(k) for k in list(self.history)}
+        kind = (task.get("input") or {}).get("report_type", "daily")
+        # executive summary of health and trends (reference monitoring.py:229)
+        summary = await self.analyze(
+            f"Generate a {kind} report summary.\n\nCurrent metrics (mean -> last over the window):\n" +
+            "\n".join(f"  {k}: {v['mean']:.1f} -> {v['last']:.1f} (min {v['min']:.1f}, max {v['max']:.1f})"
+                      for k, v in sorted(report.items()) if v) +
+            f"\n\nActive alerts: {len(self.active_alerts)}\n\nProvide a 3-5 sentence executive summary covering "
+            "system health, notable trends and recommended actions.", IntelligenceLevel.OPERATIONAL)
+        return {"success": True, "report": report, "summary": summary,
                 "active_alerts": list(self.active_alerts.values())}
 
     async def check_alerts(self, task: Dict[str, Any]) -> Dict[str, Any]:
@@ -106,12 +115,21 @@ class MonitoringAgent(BaseAgent):
                 z = (s["last"] - s["mean"]) / s["std"]
                 if abs(z) >= 3.0:
                     anomalies.append({"metric": k, "value": s["last"], "mean": s["mean"], "z": z})
+        analysis = ""
         if anomalies:
+            # are they concerning, likely causes, actions (reference monitoring.py:377)
+            analysis = await self.analyze(
+                f"Anomaly detection found {len(anomalies)} anomalies:\n" +
+                "\n".join(f"- {a['metric']}: {a['value']:.2f} ({'above' if a['z'] > 0 else 'below'} baseline "
+                          f"{a['mean']:.2f}, z={a['z']:.1f})" for a in anomalies) +
+                "\n\nAre these anomalies concerning? What might cause them? Provide brief analysis and "
+                "recommended actions.", IntelligenceLevel.TACTICAL)
             try:
-                await self.push_event("monitoring.anomalies_detected", {"anomalies": anomalies})
+                await self.push_event("monitoring.anomalies_detected", {"anomalies": anomalies},
+                                      critical=any(abs(a["z"]) > 4 for a in anomalies))
             except Exception:
                 pass
-        return {"success": True, "anomalies": anomalies}
+        return {"success": True, "anomalies": anomalies, "analysis": analysis}
 
     async def resource_forecast(self, task: Dict[str, Any]) -> Dict[str, Any]:
         out = {}
@@ -126,7 +144,18 @@ class MonitoringAgent(BaseAgent):
             slope = sum((x - mx) * (y - my) for x, y in zip(xs, ys)) / den  # %/s
             out[k] = {"slope_per_hour": slope * 3600, "forecast_1h": ys[-1] + slope * 3600,
                       "hours_to_100": (100 - ys[-1]) / (slope * 3600) if slope > 0 else None}
-        return {"success": True, "forecast": out}
+        summary = ""
+        if out:
+            # forecast summary + capacity planning advice (reference monitoring.py:468)
+            summary = await self.analyze(
+                "Resource forecast for the next hours:\n" +
+                "\n".join(f"- {k}: projected in 1h={v['forecast_1h']:.1f}, trend={v['slope_per_hour']:.2f}/hr"
+                          + (f" WARNING: capacity in {v['hours_to_100']:.1f}h"
+                             if v["hours_to_100"] is not None and v["hours_to_100"] < 24 else "")
+                          for k, v in out.items()) +
+                "\n\nProvide a brief forecast summary with any capacity planning recommendations.",
+                IntelligenceLevel.OPERATIONAL)
+        return {"success": True, "forecast": out, "summary": summary}
 
     async def dashboard_data(self, task: Dict[str, Any]) -> Dict[str, Any]:
         return {"success": True, "series": {k: list(v)[-30:] for k, v in self.history.items()},

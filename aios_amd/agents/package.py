@@ -37,9 +37,23 @@ class PackageAgent(BaseAgent):
         name = self._name(task)
         if not name:
             return {"success": False, "error": "no package name in task"}
-        found = await self.call_tool("pkg.search", {"query": name})
+        found, scan = await self.call_tools([("pkg.search", {"query": name}), ("sec.scan", {})])
         if found["success"] and not found["output"].get("results", found["output"].get("packages", [1])):
             return {"success": False, "error": f"package {name} not found"}
+        # known critical / high advisories for this package: ask before installing (reference
+        # package.py:139); `force` skips the question
+        cves = [f for f in (scan.get("output", {}).get("findings", []) if scan["success"] else [])
+                if name in str(f.get("package", f.get("issue", ""))).lower()
+                and str(f.get("severity", "")).lower() in ("critical", "high")]
+        if cves and not (task.get("input") or {}).get("force"):
+            decision = await self.analyze(
+                f"Package '{name}' has {len(cves)} critical/high advisories:\n" +
+                "\n".join(f"- {c.get('cve', 'N/A')}: {str(c.get('description', c.get('issue', '')))[:100]}"
+                          for c in cves[:5]) +
+                "\n\nShould I still install it? Consider the risk vs. necessity. Answer INSTALL or SKIP with "
+                "brief reason.", IntelligenceLevel.TACTICAL)
+            if "skip" in decision.lower()[:10]:
+                return {"success": False, "error": f"skipped {name}: {decision}", "advisories": cves}
         r = await self.call_tool("pkg.install", {"name": name}, reason=f"install {name}")
         try:
             await self.push_event("package.installed" if r["success"] else "package.install_failed", {"name": name})
@@ -53,6 +67,18 @@ class PackageAgent(BaseAgent):
             return {"success": False, "error": "no package name in task"}
         if name in ("libc6", "systemd", "bash", "coreutils", "apt", "dpkg", "python3", "rocm-core"):
             return {"success": False, "error": f"refusing to remove essential package {name}"}
+        # installed packages that name it as a dependency: ask whether removal is safe (reference
+        # package.py:243); `force` skips the question
+        inst = await self.call_tool("pkg.list_installed", {"filter": ""})
+        dependents = [p.get("name") for p in (inst.get("output", {}).get("packages", []) if inst["success"] else [])
+                      if isinstance(p, dict) and p.get("name") != name
+                      and name in " ".join(map(str, p.get("depends", [])))][:10]
+        if dependents and not (task.get("input") or {}).get("force"):
+            check = await self.analyze(
+                f"Package '{name}' is required by: {dependents}. Is it safe to remove? Could it break the system? "
+                "Answer REMOVE or KEEP with reason.", IntelligenceLevel.OPERATIONAL)
+            if "keep" in check.lower()[:10]:
+                return {"success": False, "error": f"kept {name}: {check}", "dependents": dependents}
         return await self.call_tool("pkg.remove", {"name": name}, reason=f"remove {name}")
 
     async def update_all(self, task: Dict[str, Any]) -> Dict[str, Any]:
@@ -75,8 +101,18 @@ class PackageAgent(BaseAgent):
         except Exception:
             pass
         n_pkgs = len(inst.get("output", {}).get("packages", [])) if inst["success"] else 0
+        recommendations = []
+        if by_sev["critical"] or by_sev["high"]:
+            # prioritised fixes (reference package.py:430)
+            recommendations = self.advice_lines(await self.analyze(
+                f"CVE scan results: {len(by_sev['critical'])} critical, {len(by_sev['high'])} high, "
+                f"{len(by_sev['medium'])} medium, {len(by_sev['low'])} low vulnerabilities.\n\nCritical / high:\n" +
+                "\n".join(f"- {v.get('cve', '')}: {v.get('package', '')} - "
+                          f"{str(v.get('description', v.get('issue', '')))[:80]}"
+                          for v in (by_sev["critical"] + by_sev["high"])[:5]) +
+                "\n\nProvide prioritised fix recommendations (max 5, one per line).", IntelligenceLevel.TACTICAL))
         return {"success": True, "installed_packages": n_pkgs, "vulnerabilities": findings,
-                "by_severity": {k: len(v) for k, v in by_sev.items()}}
+                "by_severity": {k: len(v) for k, v in by_sev.items()}, "recommendations": recommendations}
 
     async def search_packages(self, task: Dict[str, Any]) -> Dict[str, Any]:
         q = task.get("input", {}).get("query") or self._name(task) or task.get("description", "").split()[-1]

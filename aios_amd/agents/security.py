@@ -38,23 +38,39 @@ class SecurityAgent(BaseAgent):
             if r["success"] and r["output"].get("writable_by_others"):
                 findings.append({"severity": "high", "issue": f"{p} is world-writable"})
         score = risk_score(findings)
+        # the model's remediation plan for the critical / high findings (reference security.py:175)
+        severe = [f for f in findings if str(f.get("severity", "")).lower() in ("critical", "high")]
+        recommendations: List[str] = []
+        if severe:
+            recommendations = self.advice_lines(await self.analyze(
+                f"Security scan found {len(severe)} critical/high issues:\n" +
+                "\n".join(f"- [{f.get('severity')}] {str(f.get('issue', f.get('description', '')))[:100]}"
+                          for f in severe[:10]) +
+                "\n\nProvide prioritised remediation steps (one per line, max 5).", IntelligenceLevel.TACTICAL))
         try:
             await self.push_event("security.scan_complete", {"findings": len(findings), "risk_score": score},
                                   critical=score >= 50)
         except Exception:
             pass
-        return {"success": True, "findings": findings, "risk_score": score}
+        return {"success": True, "findings": findings, "risk_score": score, "recommendations": recommendations}
 
     async def check_integrity(self, task: Dict[str, Any]) -> Dict[str, Any]:
         mode = task.get("input", {}).get("mode", "check")
         r = await self.call_tool("sec.file_integrity", {"mode": mode, "paths": list(SENSITIVE_PATHS)})
         changed = r.get("output", {}).get("changed", []) if r["success"] else []
         if changed:
+            # is any change suspicious? (reference security.py:273)
+            analysis = await self.analyze(
+                f"File integrity check found {len(changed)} changes:\n" +
+                "\n".join(f"- {c if isinstance(c, str) else c.get('path', c)}" for c in changed[:20]) +
+                "\n\nAre any of these suspicious? Which need investigation? Reply with a brief risk assessment.",
+                IntelligenceLevel.TACTICAL)
             try:
                 await self.push_event("security.integrity_changes", {"changed": changed}, critical=True)
             except Exception:
                 pass
-        return r
+            return {**r, "analysis": analysis}
+        return {**r, "analysis": "No changes detected. All files match baseline."} if r["success"] else r
 
     async def check_permissions(self, task: Dict[str, Any]) -> Dict[str, Any]:
         path = task.get("input", {}).get("path")
@@ -68,12 +84,21 @@ class SecurityAgent(BaseAgent):
         alerts = [e for e in entries if any(k in str(e).lower() for k in ("failed password", "authentication failure",
                                                                             "invalid user", "segfault", "denied"))]
         chain = await self.call_tool("sec.audit", {"limit": 50})
+        analysis = ""
         if alerts:
+            # security assessment of the suspicious entries (reference security.py:382)
+            failed = sum("failed password" in str(e).lower() or "authentication failure" in str(e).lower()
+                         for e in alerts)
+            analysis = await self.analyze(
+                f"Audit log analysis:\n- Total entries: {len(entries)}\n- Failed logins: {failed}\n"
+                f"- Suspicious events: {len(alerts)}\n\nSample suspicious events:\n" +
+                "\n".join(f"  - {str(e)[:150]}" for e in alerts[:5]) +
+                "\n\nProvide a security assessment. Is immediate action needed?", IntelligenceLevel.TACTICAL)
             try:
                 await self.push_event("security.audit_alerts", {"count": len(alerts), "sample": alerts[:5]})
             except Exception:
                 pass
-        return {"success": True, "alerts": alerts[:50], "alert_count": len(alerts),
+        return {"success": True, "alerts": alerts[:50], "alert_count": len(alerts), "analysis": analysis,
                 "tool_audit": chain.get("output", {})}
 
     async def intrusion_check(self, task: Dict[str, Any]) -> Dict[str, Any]:
@@ -84,13 +109,19 @@ class SecurityAgent(BaseAgent):
         odd_ports = [p for p, r in zip((4444, 5555, 6667, 31337, 1337), ports)
                      if r["success"] and r.get("output", {}).get("open")]
         detected = bool(sus or odd_ports or (rk["success"] and rk["output"].get("suspicious")))
+        analysis = "No threats detected. System appears clean."
         if detected:
+            # threat assessment and immediate actions (reference security.py:464)
+            analysis = await self.analyze(
+                f"IDS check results:\n- Suspicious processes: {sus[:10]}\n- Unexpected open ports: {odd_ports}\n"
+                f"- Rootkit scan: {rk.get('output', rk.get('error'))}\n\n"
+                "Assess the threat and recommend immediate actions.", IntelligenceLevel.TACTICAL)
             try:
                 await self.push_event("security.intrusion_detected", {"processes": sus, "ports": odd_ports},
                                       critical=True)
             except Exception:
                 pass
-        return {"success": True, "intrusion_detected": detected, "suspicious_processes": sus,
+        return {"success": True, "intrusion_detected": detected, "analysis": analysis, "suspicious_processes": sus,
                 "unexpected_open_ports": odd_ports, "rootkit_scan": rk.get("output", rk.get("error"))}
 
     async def threat_analysis(self, task: Dict[str, Any]) -> Dict[str, Any]:

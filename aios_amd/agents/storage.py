@@ -7,7 +7,7 @@ import re
 import time
 from typing import Any, Dict
 
-from .base import BaseAgent, main_for
+from .base import BaseAgent, IntelligenceLevel, main_for
 
 DISK_CHECK_INTERVAL_S = 300.0
 DISK_WARN, DISK_CRIT = 85.0, 95.0
@@ -33,6 +33,12 @@ class StorageAgent(BaseAgent):
             return r
         pct = float(r["output"].get("percent", 0.0))
         status = "critical" if pct >= DISK_CRIT else "warning" if pct >= DISK_WARN else "ok"
+        warnings = []
+        if status != "ok":
+            # what to do about an unhealthy disk, is data at risk (reference storage.py:166)
+            warnings = self.advice_lines(await self.analyze(
+                f"Disk health check: {path} is {pct:.1f}% full ({status}); usage {r['output']}.\n"
+                "What actions should be taken? Is data at risk?", IntelligenceLevel.TACTICAL), 8)
         try:
             await self.update_metric("storage.disk_percent", pct)
             if status != "ok":
@@ -40,7 +46,8 @@ class StorageAgent(BaseAgent):
                                       critical=status == "critical")
         except Exception:
             pass
-        return {"success": True, "path": path, "percent": pct, "status": status, "usage": r["output"]}
+        return {"success": True, "path": path, "percent": pct, "status": status, "usage": r["output"],
+                "warnings": warnings}
 
     async def create_backup(self, task: Dict[str, Any]) -> Dict[str, Any]:
         inp = task.get("input") or {}
@@ -53,6 +60,15 @@ class StorageAgent(BaseAgent):
         avail = du_dst.get("output", {}).get("available_bytes", 1 << 62) if du_dst["success"] else 1 << 62
         if need and need > avail:
             return {"success": False, "error": f"not enough space for backup of {src}"}
+        if need and need > 0.9 * avail:
+            # tight on space: let the model decide between proceeding and aborting (reference
+            # storage.py:244); an unavailable runtime proceeds (the copy itself still checks space)
+            decision = await self.analyze(
+                f"Backup of {src} estimated at {need / 1e9:.1f}GB but only {avail / 1e9:.1f}GB available. "
+                "Should I proceed, skip some paths, or abort?", IntelligenceLevel.OPERATIONAL)
+            if "abort" in decision.lower():
+                return {"success": False, "error": f"aborted: backup of {src} would not fit",
+                        "ai_decision": decision}
         await self.call_tool("fs.mkdir", {"path": os.path.dirname(dst), "recursive": True})
         r = await self.call_tool("fs.copy", {"source": src, "destination": dst, "recursive": True})
         try:
@@ -79,8 +95,14 @@ class StorageAgent(BaseAgent):
         st = await self.call_tool("fs.stat", {"path": src})
         if not st["success"]:
             return {"success": False, "error": f"backup {src} missing"}
+        # safety review before overwriting (reference storage.py:359)
+        safety = await self.analyze(f"About to restore backup {src} to {dst}. Is this safe? What could go wrong?",
+                                    IntelligenceLevel.TACTICAL)
+        if inp.get("dry_run"):
+            return {"success": True, "dry_run": True, "restored": None, "from": src, "to": dst, "safety": safety}
         r = await self.call_tool("fs.copy", {"source": src, "destination": dst, "recursive": True})
-        return {"success": r["success"], "restored": dst, "from": src, **({} if r["success"] else {"error": r["error"]})}
+        return {"success": r["success"], "restored": dst, "from": src, "safety": safety,
+                **({} if r["success"] else {"error": r["error"]})}
 
     async def manage_mounts(self, task: Dict[str, Any]) -> Dict[str, Any]:
         r = await self.call_tool("fs.read", {"path": "/proc/mounts"})
@@ -115,7 +137,16 @@ class StorageAgent(BaseAgent):
         if len(hist) >= 2 and hist[-1][1] > hist[0][1]:
             rate = (hist[-1][1] - hist[0][1]) / max(hist[-1][0] - hist[0][0], 1)  # %/s
             eta_days = (100.0 - hist[-1][1]) / rate / 86400.0
-        return {"success": True, "percent": now.get("percent"), "samples": len(hist), "days_until_full": eta_days}
+        recommendations = []
+        pct = now.get("percent") or 0.0
+        if pct >= DISK_WARN or (eta_days is not None and eta_days < 30):
+            # free space / plan expansion (reference storage.py:569)
+            recommendations = self.advice_lines(await self.analyze(
+                f"Storage capacity warning: {pct:.1f}% used"
+                + (f", full in {eta_days:.1f} days at the current rate" if eta_days is not None else "")
+                + ".\nRecommend actions to free space or plan expansion.", IntelligenceLevel.OPERATIONAL))
+        return {"success": True, "percent": now.get("percent"), "samples": len(hist), "days_until_full": eta_days,
+                "recommendations": recommendations}
 
     async def background(self):
         return [self.periodic(DISK_CHECK_INTERVAL_S, lambda: self.capacity_planning({}))]

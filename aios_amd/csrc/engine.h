@@ -16,6 +16,7 @@
 
 #include "common.h"
 #include "ops.h"
+#include "mk.h"
 
 namespace aios {
 
@@ -128,6 +129,10 @@ class Engine {
   int kv_blocks_free() const { return (int)free_blocks_.size(); }
   int kv_blocks_total() const { return kv_nblocks_; }
   int norm_fused_parts() const { return nrm_parts_; }  // 0: batched-decode RMSNorm not split into the GEMMs
+  // persistent batch-1 decode step (kernels/decode_mk.hip): available / switched on
+  bool mk_available() const { return mk_ok_; }
+  void set_mk(bool on) { if (mk_enabled_ != on) { mk_enabled_ = on; reset_graphs(); } }
+  bool mk_enabled() const { return mk_enabled_; }
   std::vector<int> block_table(int slot) const;
 
   // raw device pointers for tests / custom kernels
@@ -264,6 +269,15 @@ class Engine {
   void kv_sync(int B);                                 // upload dirty tables (rows 0..B-1)
 
   std::map<int, hipGraphExec_t> graphs_;
+  // persistent decode kernel state
+  bool mk_ok_ = false, mk_enabled_ = true;
+  int mk_grid_ = 0;
+  MkArgs mk_args_{};
+  MkStage* d_mk_stages_ = nullptr;
+  int* mk_cnt_ = nullptr;
+  void mk_build();
+  bool mk_use(int B) const;
+  bool check_mk_err();  // true (and the persistent path switched off) when a launch gave up
   AllReduceFn allreduce_ = nullptr;
   void* allreduce_ctx_ = nullptr;
   AllGatherFn allgather_ = nullptr;

@@ -599,8 +599,85 @@ void Engine::finalize() {
     }
   }
   ws_bytes_ = ws;
+  mk_build();
   HIP_CHECK(hipDeviceSynchronize());
   finalized_ = true;
+}
+
+// The persistent batch-1 decode kernel (kernels/decode_mk.hip): one launch per step instead of
+// 5 per layer.  Served shapes: tp 1, int8 GEMV activations, K-quant weights (Q4_K / Q5_K / Q6_K),
+// interleaved (non-NeoX) RoPE without QK-norm or QKV bias, and an LDS plan that fits 160 KB.
+// AIOS_MK=0 switches it off (the launch-per-op path then serves batch 1).
+void Engine::mk_build() {
+  mk_ok_ = false;
+  if (const char* e = std::getenv("AIOS_MK"))
+    if (std::atoi(e) == 0) return;
+  if (cfg_.tp_size != 1 || !cfg_.act_q8 || cfg_.qk_norm || cfg_.rope_neox || !rope_cs_) return;
+  const int d = cfg_.d_model, hd = cfg_.head_dim, H = cfg_.n_heads, Hkv = cfg_.n_kv_heads;
+  const int qd = H * hd, kvd = Hkv * hd;
+  std::vector<MkStage> st;
+  auto proj = [&](int kind, int l, int K, std::vector<const QMat*> segs, const float* nw) {
+    MkStage s;
+    std::memset(&s, 0, sizeof(s));
+    s.kind = kind; s.layer = l; s.K = K; s.nseg = (int)segs.size(); s.norm_w = nw;
+    int row = 0;
+    for (int i = 0; i < s.nseg; ++i) { s.seg[i] = segs[i]->w; s.seg_row0[i] = row; row += segs[i]->w.rows; }
+    s.k_cache = k_cache_ + (size_t)l * layer_kv_elems_;
+    s.v_cache = v_cache_ + (size_t)l * layer_kv_elems_;
+    st.push_back(s);
+  };
+  for (int l = 0; l < cfg_.n_layers; ++l) {
+    const LayerW& L = layers_[l];
+    if (L.bqkv) return;
+    if (L.wq.w.rows != qd || L.wk.w.rows != kvd || L.wv.w.rows != kvd) return;
+    proj(MK_QKV, l, d, {&L.wq, &L.wk, &L.wv}, L.attn_norm);
+    proj(MK_ATT, l, 0, {}, nullptr);
+    proj(MK_O, l, qd, {&L.wo}, nullptr);
+    proj(MK_GU, l, d, {&L.wgu}, L.ffn_norm);
+    proj(MK_DOWN, l, cfg_.d_ff, {&L.wdown}, nullptr);
+  }
+  if (output_.w.rows != cfg_.vocab_size) return;
+  proj(MK_LM, cfg_.n_layers, d, {&output_}, out_norm_);
+  MkArgs& a = mk_args_;
+  std::memset(&a, 0, sizeof(a));
+  a.nstages = (int)st.size();
+  a.d = d; a.q_dim = qd; a.kv_dim = kvd; a.n_heads = H; a.n_kv_heads = Hkv; a.head_dim = hd;
+  a.d_ff = cfg_.d_ff; a.vocab = cfg_.vocab_size; a.eps = cfg_.norm_eps;
+  a.attn_scale = 1.f / std::sqrt((float)hd);
+  a.rope_cs = rope_cs_; a.max_ctx = cfg_.max_ctx;
+  a.n_layers = cfg_.n_layers;
+  mk_grid_ = device_cu_count();
+  if (!mk_plan(a, st, mk_grid_)) return;
+  d_mk_stages_ = (MkStage*)dmalloc(st.size() * sizeof(MkStage));
+  HIP_CHECK(hipMemcpy(d_mk_stages_, st.data(), st.size() * sizeof(MkStage), hipMemcpyHostToDevice));
+  const size_t nints = mk_counter_ints(a.nstages, cfg_.n_layers, Hkv);
+  mk_cnt_ = (int*)dmalloc(nints * 4);
+  HIP_CHECK(hipMemset(mk_cnt_, 0, nints * 4));
+  a.stages = d_mk_stages_;
+  a.cnt = mk_cnt_;
+  a.tick = mk_cnt_ + (size_t)a.nstages * 8 * 32;
+  a.done = a.tick + (size_t)cfg_.n_layers * Hkv * 32;
+  a.err = a.done + 32;
+  a.o_part = (float*)dmalloc((size_t)H * MK_MAXU * hd * 4);
+  a.ml = (float*)dmalloc((size_t)H * MK_MAXU * 2 * 4);
+  a.pos = d_pos_; a.seq_len = d_seqlen_; a.slot = d_slot_; a.block_table = d_bt_;
+  a.x = x_; a.q = q_; a.attn = attn_; a.ffb = ff_; a.logits = logits_;
+  a.timeout_us = 20000;
+  if (const char* e = std::getenv("AIOS_MK_TIMEOUT_US")) a.timeout_us = std::max(100, std::atoi(e));
+  mk_ok_ = true;
+}
+
+bool Engine::mk_use(int B) const { return mk_ok_ && mk_enabled_ && B == 1 && !attn_block_on(B); }
+
+bool Engine::check_mk_err() {
+  if (!mk_ok_) return false;
+  int e = 0;
+  HIP_CHECK(hipMemcpy(&e, mk_args_.err, 4, hipMemcpyDeviceToHost));
+  if (!e) return false;
+  HIP_CHECK(hipMemset(mk_args_.err, 0, 4));
+  mk_enabled_ = false;  // another kernel held CUs the persistent step needs: launches from now on
+  reset_graphs();
+  return true;
 }
 
 // TP: sum the row-parallel partials in `p` over the ranks and add the total into `residual`
@@ -981,8 +1058,12 @@ void Engine::enqueue_decode_step(int B) {
     HIP_CHECK(hipMemsetAsync(fuse_cnt_, 0, (size_t)cfg_.n_layers * 2 * 4, stream_));
   launch_get_rows(tok_embd_.w, d_tokens_, B, x_, d, 1.f, stream_);
   nrm_lm_ = false;
-  for (int l = 0; l < cfg_.n_layers; ++l) layer_decode(l, B);
-  lm_head(B, x_, d);
+  if (mk_use(B)) {
+    launch_decode_mk(mk_args_, mk_grid_, stream_);  // every layer + lm_head in one launch
+  } else {
+    for (int l = 0; l < cfg_.n_layers; ++l) layer_decode(l, B);
+    lm_head(B, x_, d);
+  }
   nrm_lm_ = false;
   SampleArgs s;
   std::memset(&s, 0, sizeof(s));
@@ -1279,6 +1360,9 @@ std::vector<int> Engine::decode(const std::vector<int>& slots, const std::vector
   HIP_CHECK(hipStreamSynchronize(stream_));
   sample_mask_ = false;
   check_fuse_err();
+  // the persistent step gave up (a CU it needs was held by another kernel): the same step again
+  // through the launch-per-op path -- every input is re-uploaded, the KV row is rewritten
+  if (check_mk_err()) return decode(slots, tokens, pos, temperature, top_k, seed, mask, top_p);
   return std::vector<int>(h_tok_out_, h_tok_out_ + B);
 }
 
@@ -1419,6 +1503,8 @@ std::vector<int> Engine::decode_loop_history(int B, int from_pos, int n) {
 void Engine::synchronize() {
   HIP_CHECK(hipStreamSynchronize(stream_));
   check_fuse_err();
+  if (check_mk_err())
+    throw std::runtime_error("persistent decode step: a bounded wait gave up (switched to the launch path)");
 }
 
 void Engine::reset_graphs() {

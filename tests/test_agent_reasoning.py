@@ -1,0 +1,195 @@
+"""The agents' LLM reasoning sites (reference aios_agent/agents/*.py think() calls): every action
+whose situation calls for the model's reading of its tool results issues exactly that Infer call,
+at the reference's intelligence level, and folds the answer into its result.  Tools and the
+runtime are stubbed, so each site is driven deterministically (the live-service paths are
+covered by test_agent_actions.py)."""
+import asyncio
+
+import grpc
+import pytest
+
+from aios_amd.agents import AGENT_REGISTRY
+from aios_amd.agents.base import AgentConfig, IntelligenceLevel
+
+
+class _Rec:
+    def __init__(self, tools, answer="1. isolate the host\n2. rotate keys\n3. patch", events=(), metrics=None,
+                 memory=None):
+        self.tools, self.answer = tools, answer
+        self.prompts = []
+        self.events = list(events)
+        self.metrics = metrics or {}
+        self.memory = dict(memory or {})
+
+
+def _agent(kind, rec: _Rec):
+    a = AGENT_REGISTRY[kind](agent_id=f"{kind}-t", config=AgentConfig())
+
+    async def call_tool(name, args=None, reason=""):
+        v = rec.tools.get(name, {"success": True, "output": {}})
+        return v(args or {}) if callable(v) else v
+
+    async def call_tools(calls):
+        return [await call_tool(n, a_) for n, a_ in calls]
+
+    async def think(prompt, level=IntelligenceLevel.OPERATIONAL, **kw):
+        rec.prompts.append((IntelligenceLevel(level), prompt))
+        return rec.answer
+
+    async def nop(*a_, **k):
+        return None
+
+    async def recall(key):
+        return rec.memory.get(key)
+
+    async def store(key, value):
+        rec.memory[key] = value
+
+    async def events(limit=100):
+        return rec.events
+
+    async def metric(k):
+        return rec.metrics.get(k)
+
+    a.call_tool, a.call_tools, a.think = call_tool, call_tools, think
+    a.push_event = a.update_metric = a.store_pattern = nop
+    a.recall_memory, a.store_memory, a.get_recent_events, a.get_metric = recall, store, events, metric
+    return a
+
+
+def _run(coro):
+    return asyncio.run(asyncio.wait_for(coro, 20))
+
+
+def _levels(rec):
+    return [lv for lv, _ in rec.prompts]
+
+
+# ----------------------------------------------------------------------------------------- security
+def test_security_scan_remediation():
+    rec = _Rec({"sec.scan": {"success": True, "output": {"findings": [
+        {"severity": "critical", "issue": "sshd permits root login"}, {"severity": "low", "issue": "motd"}]}}})
+    r = _run(_agent("security", rec).scan_vulnerabilities({}))
+    assert _levels(rec) == [IntelligenceLevel.TACTICAL] and "sshd permits root login" in rec.prompts[0][1]
+    assert r["recommendations"] == ["isolate the host", "rotate keys", "patch"]
+
+
+def test_security_clean_scan_asks_nothing():
+    rec = _Rec({"sec.scan": {"success": True, "output": {"findings": []}}})
+    r = _run(_agent("security", rec).scan_vulnerabilities({}))
+    assert rec.prompts == [] and r["recommendations"] == []
+
+
+def test_security_integrity_audit_intrusion():
+    rec = _Rec({"sec.file_integrity": {"success": True, "output": {"changed": ["/etc/sudoers"]}},
+                "monitor.logs": {"success": True, "output": {"entries": ["sshd: Failed password for root"]}},
+                "process.list": {"success": True, "output": {"processes": [{"name": "xmrig", "pid": 7}]}}})
+    a = _agent("security", rec)
+    ig = _run(a.check_integrity({}))
+    au = _run(a.audit_logs({}))
+    ic = _run(a.intrusion_check({}))
+    assert _levels(rec) == [IntelligenceLevel.TACTICAL] * 3
+    assert "/etc/sudoers" in rec.prompts[0][1] and "Failed password" in rec.prompts[1][1]
+    assert "xmrig" in rec.prompts[2][1]
+    assert ig["analysis"] and au["analysis"] and ic["intrusion_detected"] and ic["analysis"].startswith("1.")
+
+
+def test_think_unavailable_keeps_tool_results():
+    rec = _Rec({"sec.scan": {"success": True, "output": {"findings": [{"severity": "high", "issue": "x"}]}}})
+    a = _agent("security", rec)
+
+    class Down(grpc.aio.AioRpcError):
+        def __init__(self):
+            super().__init__(grpc.StatusCode.UNAVAILABLE, None, None, "runtime down")
+
+    async def think(*a_, **k):
+        raise Down()
+
+    a.think = think
+    r = _run(a.scan_vulnerabilities({}))
+    assert r["success"] and r["findings"] and r["recommendations"] == []
+
+
+# ----------------------------------------------------------------------------------------- storage
+def test_storage_sites():
+    rec = _Rec({"monitor.disk": {"success": True, "output": {"percent": 97.0}},
+                "fs.disk_usage": lambda a: {"success": True, "output": {"used_bytes": 95, "available_bytes": 100}},
+                "fs.stat": {"success": True, "output": {}}, "fs.copy": {"success": True, "output": {}}},
+               answer="abort: not enough room")
+    a = _agent("storage", rec)
+    h = _run(a.check_disk_health({"input": {"path": "/"}}))
+    assert h["status"] == "critical" and h["warnings"] == ["abort: not enough room"]
+    b = _run(a.create_backup({"input": {"source": "/srv", "destination": "/bk/srv"}}))
+    assert not b["success"] and "abort" in b["ai_decision"]
+    rs = _run(a.restore_backup({"input": {"backup": "/bk/srv", "destination": "/srv", "dry_run": True}}))
+    assert rs["dry_run"] and rs["safety"]
+    cp = _run(a.capacity_planning({"input": {"path": "/"}}))
+    assert cp["recommendations"]
+    assert _levels(rec) == [IntelligenceLevel.TACTICAL, IntelligenceLevel.OPERATIONAL, IntelligenceLevel.TACTICAL,
+                            IntelligenceLevel.TACTICAL, IntelligenceLevel.OPERATIONAL]
+
+
+# -------------------------------------------------------------------------------------- monitoring
+def test_monitoring_sites():
+    rec = _Rec({"monitor.cpu": {"success": True, "output": {"percent": 10.0}},
+                "monitor.memory": {"success": True, "output": {"percent": 40.0}},
+                "monitor.disk": {"success": True, "output": {"percent": 50.0}}})
+    a = _agent("monitoring", rec)
+    for i in range(12):
+        rec.tools["monitor.cpu"] = {"success": True, "output": {"percent": 10.0 + (i % 2)}}
+        _run(a.collect_metrics({}))
+    rec.tools["monitor.cpu"] = {"success": True, "output": {"percent": 95.0}}
+    _run(a.collect_metrics({}))
+    rep = _run(a.generate_report({}))
+    an = _run(a.anomaly_detection({}))
+    fc = _run(a.resource_forecast({}))
+    assert rep["summary"] and an["anomalies"] and an["analysis"] and fc["summary"]
+    assert _levels(rec) == [IntelligenceLevel.OPERATIONAL, IntelligenceLevel.TACTICAL, IntelligenceLevel.OPERATIONAL]
+    assert "cpu.usage_percent" in rec.prompts[1][1]
+
+
+# ----------------------------------------------------------------------------------------- package
+def test_package_sites():
+    rec = _Rec({"pkg.search": {"success": True, "output": {"packages": [{"name": "openssl"}]}},
+                "sec.scan": {"success": True, "output": {"findings": [
+                    {"severity": "critical", "package": "openssl", "cve": "CVE-2099-1", "description": "rce"}]}},
+                "pkg.list_installed": {"success": True, "output": {"packages": [
+                    {"name": "curl", "depends": ["openssl", "zlib"]}, {"name": "openssl", "depends": []}]}}},
+               answer="SKIP: unpatched remote code execution")
+    a = _agent("package", rec)
+    ins = _run(a.install_package({"input": {"name": "openssl"}}))
+    assert not ins["success"] and ins["advisories"]
+    rec.answer = "KEEP: curl needs it"
+    rm = _run(a.remove_package({"input": {"name": "openssl"}}))
+    assert not rm["success"] and rm["dependents"] == ["curl"]
+    rec.answer = "1. upgrade openssl"
+    cv = _run(a.check_vulnerabilities({}))
+    assert cv["recommendations"] == ["upgrade openssl"]
+    assert _levels(rec) == [IntelligenceLevel.TACTICAL, IntelligenceLevel.OPERATIONAL, IntelligenceLevel.TACTICAL]
+
+
+# ---------------------------------------------------------------------------------------- learning
+def test_learning_sites():
+    evs = [{"category": "tool_failure" if i % 3 else "goal", "critical": i % 5 == 0, "data": {}} for i in range(30)]
+    rec = _Rec({}, events=evs, metrics={"system.cpu_percent": 91.0},
+               memory={"metric_history": {"system.cpu_percent": [90.0] * 12}},
+               answer='{"suggestions": [{"parameter": "autonomy_tick_ms", "current": "500", "suggested": "250",'
+                      ' "impact": "faster goal pickup"}]}')
+    a = _agent("learning", rec)
+    pa = _run(a.analyze_patterns({}))
+    op = _run(a.optimize_parameters({}))
+    assert pa["analysis"] and op["ai_suggestions"][0]["parameter"] == "autonomy_tick_ms"
+    assert _levels(rec) == [IntelligenceLevel.STRATEGIC, IntelligenceLevel.STRATEGIC]
+
+
+def test_public_loop_names():
+    from aios_amd.agents.base import BaseAgent
+
+    assert callable(getattr(BaseAgent, "heartbeat_loop")) and callable(getattr(BaseAgent, "task_poll_loop"))
+
+
+@pytest.mark.parametrize("kind", ["security", "storage", "monitoring", "package", "learning"])
+def test_fallback_asks_for_an_action(kind):
+    rec = _Rec({}, answer='{"action": "nope"}')
+    r = _run(_agent(kind, rec).handle_task({"description": "zzz unrecognisable", "input": {}}))
+    assert not r["success"] and _levels(rec) == [IntelligenceLevel.OPERATIONAL]
