@@ -188,15 +188,24 @@ PYBIND11_MODULE(_engine, m) {
       .def("decode",
            [](Engine& e, const std::vector<int>& slots, const std::vector<int>& tokens, const std::vector<int>& pos,
               const std::vector<float>& temperature, const std::vector<int>& top_k, uint64_t seed, py::bytes mask,
-              const std::vector<float>& top_p) {
+              const std::vector<float>& top_p, const std::vector<uint64_t>& seeds) {
              std::string m = mask;  // packed allowed-token bitmask, B rows of ceil(V/8) bytes (or empty)
              std::vector<uint8_t> mv(m.begin(), m.end());
              py::gil_scoped_release nogil;
-             return e.decode(slots, tokens, pos, temperature, top_k, seed, mv, top_p);
+             return e.decode(slots, tokens, pos, temperature, top_k, seed, mv, top_p, seeds);
            },
            py::arg("slots"), py::arg("tokens"), py::arg("pos"), py::arg("temperature") = std::vector<float>{},
            py::arg("top_k") = std::vector<int>{}, py::arg("seed") = 0, py::arg("mask") = py::bytes(),
-           py::arg("top_p") = std::vector<float>{})
+           py::arg("top_p") = std::vector<float>{}, py::arg("seeds") = std::vector<uint64_t>{})
+      .def("sample_first",
+           [](Engine& e, int pos, float temperature, int top_k, float top_p, uint64_t seed, py::bytes mask) {
+             std::string m = mask;
+             std::vector<uint8_t> mv(m.begin(), m.end());
+             py::gil_scoped_release nogil;
+             return e.sample_first(pos, temperature, top_k, top_p, seed, mv);
+           },
+           py::arg("pos"), py::arg("temperature") = 0.f, py::arg("top_k") = 0, py::arg("top_p") = 1.f,
+           py::arg("seed") = 0, py::arg("mask") = py::bytes())
       .def("resample",
            [](Engine& e, int B, const std::vector<float>& temperature, const std::vector<int>& top_k, uint64_t seed,
               py::bytes mask, const std::vector<float>& top_p) {

@@ -100,7 +100,11 @@ class Engine {
   // with per-row temperature/top_k (0 = greedy) and optional grammar bitmasks; returns tokens.
   std::vector<int> decode(const std::vector<int>& slots, const std::vector<int>& tokens, const std::vector<int>& pos,
                           const std::vector<float>& temperature, const std::vector<int>& top_k, uint64_t seed,
-                          const std::vector<uint8_t>& mask, const std::vector<float>& top_p = {});
+                          const std::vector<uint8_t>& mask, const std::vector<float>& top_p = {},
+                          const std::vector<uint64_t>& seeds = {});
+  // sample the token after a prefill from its last logits (logits_ row 0) on the device, with the
+  // same sampler and RNG stream (seed, pos) as the decode steps -- pos: the prompt's last position
+  int sample_first(int pos, float temperature, int top_k, float top_p, uint64_t seed, const std::vector<uint8_t>& mask);
   // re-sample the last step's logits (no state advance), e.g. with a grammar mask
   std::vector<int> resample(int B, const std::vector<float>& temperature, const std::vector<int>& top_k, uint64_t seed,
                             const std::vector<uint8_t>& mask, const std::vector<float>& top_p = {});
@@ -199,6 +203,9 @@ class Engine {
   size_t sample_ws_bytes_ = 0;
   int* sample_cnt_ = nullptr;
   uint64_t* d_seed_ = nullptr;
+  uint64_t* d_seeds_ = nullptr;    // [max_batch] per-row sampling seeds (in the parameter block)
+  int* d_fpos_ = nullptr;          // sample_first's RNG position
+  void fill_row_seeds(uint64_t* host_seeds, int B, uint64_t seed, const std::vector<uint64_t>& seeds);
   uint8_t* d_mask_ = nullptr;
   int n_chunks_ = 0;
   int* attn_cnt_ = nullptr;  // [max(prefill_rows, max_batch)][n_kv_heads] combine tickets

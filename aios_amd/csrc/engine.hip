@@ -492,7 +492,8 @@ void Engine::finalize() {
     // block: a scheduler decode() uploads all of them with a single async copy (round 1 issued 8
     // pageable copies per step)
     const size_t mb = (size_t)Bm * ((V + 7) / 8);
-    par_mask_off_ = align_up(8 + (size_t)Bm * 4 * 7, 256);
+    const size_t seeds_off = align_up(8 + (size_t)Bm * 4 * 7, 8);  // per-row seeds after the 7 row arrays
+    par_mask_off_ = align_up(seeds_off + (size_t)Bm * 8, 256);
     par_bytes_ = par_mask_off_ + mb;
     d_par_ = (char*)dmalloc(par_bytes_);
     ws += par_bytes_;
@@ -507,6 +508,7 @@ void Engine::finalize() {
     d_topk_ = d_seqlen_ + Bm;
     d_temp_ = (float*)(d_topk_ + Bm);
     d_topp_ = d_temp_ + Bm;
+    d_seeds_ = (uint64_t*)(d_par_ + seeds_off);
     d_mask_ = (uint8_t*)(d_par_ + par_mask_off_);
     float* htp = (float*)(h_par_ + 8) + 6 * (size_t)Bm;
     for (int b = 0; b < Bm; ++b) htp[b] = 1.f;
@@ -522,6 +524,7 @@ void Engine::finalize() {
   attn_bt_ = d_row_bt_;
   attn_bt_rows_ = 1;
   d_step_ = ibuf(4);
+  d_fpos_ = ibuf(4);
   sample_ws_bytes_ = sample_ws_bytes(Bm, V);
   sample_ws_ = dmalloc(sample_ws_bytes_);
   ws += sample_ws_bytes_;
@@ -1071,6 +1074,7 @@ void Engine::enqueue_decode_step(int B) {
   s.temperature = d_temp_; s.top_k = d_topk_;
   s.seed = sample_seed_;
   s.seed_dev = d_seed_;
+  s.seeds = d_seeds_;
   s.tokens = d_tokens_; s.pos = d_pos_; s.seq_len = d_seqlen_;
   s.history = d_history_; s.hist_stride = cfg_.max_ctx + 1;
   s.advance = 1;
@@ -1318,10 +1322,11 @@ std::vector<float> Engine::prefill(int slot, const std::vector<int>& tokens, int
 std::vector<int> Engine::decode(const std::vector<int>& slots, const std::vector<int>& tokens,
                                 const std::vector<int>& pos, const std::vector<float>& temperature,
                                 const std::vector<int>& top_k, uint64_t seed, const std::vector<uint8_t>& mask,
-                                const std::vector<float>& top_p) {
+                                const std::vector<float>& top_p, const std::vector<uint64_t>& seeds) {
   if (!finalized_) throw std::runtime_error("engine not finalized");
   HIP_CHECK(hipSetDevice(cfg_.device));
   const int B = (int)slots.size();
+  if (!seeds.empty() && (int)seeds.size() != B) throw std::runtime_error("decode: seeds size mismatch");
   if (B < 1 || B > cfg_.max_batch) throw std::runtime_error("decode: batch out of range");
   if ((int)tokens.size() != B || (int)pos.size() != B) throw std::runtime_error("decode: size mismatch");
   std::vector<int> sl(B);
@@ -1349,7 +1354,8 @@ std::vector<int> Engine::decode(const std::vector<int>& slots, const std::vector
     hT[b] = b < (int)temperature.size() ? temperature[b] : 0.f;
     hP[b] = b < (int)top_p.size() ? top_p[b] : 1.f;
   }
-  size_t nbytes = (size_t)((char*)(hP + Bm) - h_par_);
+  fill_row_seeds((uint64_t*)(h_par_ + ((char*)d_seeds_ - d_par_)), B, seed, seeds);
+  size_t nbytes = (size_t)((char*)d_seeds_ - d_par_) + (size_t)Bm * 8;
   if (sample_mask_) {
     std::memcpy(h_par_ + par_mask_off_, mask.data(), mbytes);
     nbytes = par_mask_off_ + mbytes;
@@ -1362,7 +1368,7 @@ std::vector<int> Engine::decode(const std::vector<int>& slots, const std::vector
   check_fuse_err();
   // the persistent step gave up (a CU it needs was held by another kernel): the same step again
   // through the launch-per-op path -- every input is re-uploaded, the KV row is rewritten
-  if (check_mk_err()) return decode(slots, tokens, pos, temperature, top_k, seed, mask, top_p);
+  if (check_mk_err()) return decode(slots, tokens, pos, temperature, top_k, seed, mask, top_p, seeds);
   return std::vector<int>(h_tok_out_, h_tok_out_ + B);
 }
 
@@ -1381,6 +1387,9 @@ std::vector<int> Engine::resample(int B, const std::vector<float>& temperature, 
   for (int b = 0; b < B && b < (int)top_p.size(); ++b) tps[b] = top_p[b];
   HIP_CHECK(hipMemcpyAsync(d_topp_, tps.data(), B * 4, hipMemcpyHostToDevice, stream_));
   HIP_CHECK(hipMemcpyAsync(d_seed_, &seed, 8, hipMemcpyHostToDevice, stream_));
+  std::vector<uint64_t> hs(B);
+  fill_row_seeds(hs.data(), B, seed, {});
+  HIP_CHECK(hipMemcpyAsync(d_seeds_, hs.data(), (size_t)B * 8, hipMemcpyHostToDevice, stream_));
   const size_t mbytes = (size_t)B * ((cfg_.vocab_size + 7) / 8);
   if (!mask.empty()) {
     if (mask.size() != mbytes) throw std::runtime_error("resample: mask size mismatch");
@@ -1389,7 +1398,7 @@ std::vector<int> Engine::resample(int B, const std::vector<float>& temperature, 
   SampleArgs s;
   std::memset(&s, 0, sizeof(s));
   s.logits = logits_; s.ldl = cfg_.vocab_size; s.B = B; s.V = cfg_.vocab_size;
-  s.temperature = d_temp_; s.top_k = d_topk_; s.seed_dev = d_seed_;
+  s.temperature = d_temp_; s.top_k = d_topk_; s.seed_dev = d_seed_; s.seeds = d_seeds_;
   s.tokens = d_tokens_; s.pos = d_pos_; s.advance = 0;
   s.mask = mask.empty() ? nullptr : d_mask_;
   s.top_p = d_topp_; s.ws = sample_ws_; s.ws_bytes = sample_ws_bytes_; s.counters = sample_cnt_;
@@ -1397,6 +1406,39 @@ std::vector<int> Engine::resample(int B, const std::vector<float>& temperature, 
   launch_sample(s, stream_);
   std::vector<int> out(B);
   HIP_CHECK(hipMemcpyAsync(out.data(), d_tokens_, B * 4, hipMemcpyDeviceToHost, stream_));
+  HIP_CHECK(hipStreamSynchronize(stream_));
+  return out;
+}
+
+// rows without their own seed keep the shared seed decorrelated by row (the round-2 stream keyed
+// (seed, row, pos)); rows with one (a request's own seed) sample independently of their row
+void Engine::fill_row_seeds(uint64_t* hs, int B, uint64_t seed, const std::vector<uint64_t>& seeds) {
+  for (int b = 0; b < B; ++b) hs[b] = seeds.empty() ? seed ^ (0x9E3779B97F4A7C15ULL * (uint64_t)(b + 1)) : seeds[b];
+}
+
+int Engine::sample_first(int pos, float temperature, int top_k, float top_p, uint64_t seed,
+                         const std::vector<uint8_t>& mask) {
+  if (!finalized_) throw std::runtime_error("engine not finalized");
+  HIP_CHECK(hipSetDevice(cfg_.device));
+  const size_t mbytes = (size_t)((cfg_.vocab_size + 7) / 8);
+  if (!mask.empty() && mask.size() != mbytes) throw std::runtime_error("sample_first: mask size mismatch");
+  // row 0 of the parameter block: the next decode() re-uploads every row it uses
+  HIP_CHECK(hipMemcpyAsync(d_temp_, &temperature, 4, hipMemcpyHostToDevice, stream_));
+  HIP_CHECK(hipMemcpyAsync(d_topk_, &top_k, 4, hipMemcpyHostToDevice, stream_));
+  HIP_CHECK(hipMemcpyAsync(d_topp_, &top_p, 4, hipMemcpyHostToDevice, stream_));
+  HIP_CHECK(hipMemcpyAsync(d_seeds_, &seed, 8, hipMemcpyHostToDevice, stream_));
+  HIP_CHECK(hipMemcpyAsync(d_fpos_, &pos, 4, hipMemcpyHostToDevice, stream_));
+  if (!mask.empty()) HIP_CHECK(hipMemcpyAsync(d_mask_, mask.data(), mbytes, hipMemcpyHostToDevice, stream_));
+  SampleArgs s;
+  std::memset(&s, 0, sizeof(s));
+  s.logits = logits_; s.ldl = cfg_.vocab_size; s.B = 1; s.V = cfg_.vocab_size;
+  s.temperature = d_temp_; s.top_k = d_topk_; s.seeds = d_seeds_;
+  s.tokens = d_tokens_; s.pos = d_fpos_; s.advance = 0;
+  s.mask = mask.empty() ? nullptr : d_mask_;
+  s.top_p = d_topp_; s.ws = sample_ws_; s.ws_bytes = sample_ws_bytes_; s.counters = sample_cnt_;
+  launch_sample(s, stream_);
+  int out = 0;
+  HIP_CHECK(hipMemcpyAsync(&out, d_tokens_, 4, hipMemcpyDeviceToHost, stream_));
   HIP_CHECK(hipStreamSynchronize(stream_));
   return out;
 }
@@ -1429,6 +1471,9 @@ void Engine::decode_loop_prepare(const std::vector<int>& slots, const std::vecto
   HIP_CHECK(hipMemcpyAsync(d_topp_, ones.data(), B * 4, hipMemcpyHostToDevice, stream_));
   const uint64_t zero = 0;
   HIP_CHECK(hipMemcpyAsync(d_seed_, &zero, 8, hipMemcpyHostToDevice, stream_));
+  std::vector<uint64_t> hs(B);
+  fill_row_seeds(hs.data(), B, 0, {});
+  HIP_CHECK(hipMemcpyAsync(d_seeds_, hs.data(), (size_t)B * 8, hipMemcpyHostToDevice, stream_));
   HIP_CHECK(hipStreamSynchronize(stream_));
   sample_seed_ = 0;
   sample_mask_ = false;

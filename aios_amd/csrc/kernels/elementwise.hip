@@ -298,7 +298,8 @@ __global__ void __launch_bounds__(SAMPLE_THREADS) sample_kernel(SampleArgs a) {
   const int topk = a.top_k ? a.top_k[b] : 0;
   const float topp = a.top_p ? a.top_p[b] : 1.f;
   const uint32_t step = a.pos ? (uint32_t)a.pos[b] : 0u;  // RNG stream (seed, row, position)
-  const uint64_t seed = a.seed_dev ? *a.seed_dev : a.seed;
+  const uint64_t seed = a.seeds ? a.seeds[b] : (a.seed_dev ? *a.seed_dev : a.seed);
+  const int rkey = a.seeds ? 0 : b;  // per-row seeds: row-independent streams
   const bool filt = temp > 0.f && (topk > 0 || topp < 1.f);
   const int K = topk > 0 ? min(topk, SAMPLE_KCAP) : SAMPLE_TOPP_K;
   SampleWs w = sample_ws(a.ws, a.B, NS);
@@ -322,7 +323,7 @@ __global__ void __launch_bounds__(SAMPLE_THREADS) sample_kernel(SampleArgs a) {
 #pragma unroll
     for (int j = 0; j < SAMPLE_PER_THREAD; ++j) {
       const int i = slice * SAMPLE_SLICE + j * SAMPLE_THREADS + tid;
-      if (v[j] > -INFINITY) g = am_better(g, ArgMax{v[j] * it + gumbel(seed, step, b, i), i});
+      if (v[j] > -INFINITY) g = am_better(g, ArgMax{v[j] * it + gumbel(seed, step, rkey, i), i});
     }
     pub = block_argmax(g, sv, si);
   }
@@ -415,7 +416,7 @@ __global__ void __launch_bounds__(SAMPLE_THREADS) sample_kernel(SampleArgs a) {
         }
         keep = before < topp * Z;
       }
-      if (keep) g = am_better(g, ArgMax{cv[j] * it + gumbel(seed, step, b, idx), idx});
+      if (keep) g = am_better(g, ArgMax{cv[j] * it + gumbel(seed, step, rkey, idx), idx});
     }
     g = block_argmax(g, sv, si);
     if (g.i >= 0 && g.i < a.V) tok = g.i;

@@ -117,6 +117,8 @@ struct SampleArgs {
   const int* top_k;          // [B] or null
   uint64_t seed;             // RNG key = (seed, row, pos[row])
   const uint64_t* seed_dev;  // if non-null, the seed is read from device memory (graph-replay safe)
+  const uint64_t* seeds;     // [B] per-row seeds or null: RNG key = (seeds[b], pos[b]) -- a request's
+                             // samples then depend on its seed and positions only, not its batch row
   int* tokens;               // [B] out
   int* pos;                  // [B] in/out (incremented when advance != 0)
   int* seq_len;              // [B] out (pos+1) or null

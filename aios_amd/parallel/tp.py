@@ -58,7 +58,7 @@ class TPEngine:
     `close()` releases them.  Attribute reads (config, weight_bytes, ...) come from the local
     shard."""
 
-    _FORWARD = frozenset({"prefill", "decode", "resample", "last_logits", "decode_loop_prepare",
+    _FORWARD = frozenset({"prefill", "decode", "resample", "sample_first", "last_logits", "decode_loop_prepare",
                           "decode_loop_run", "decode_loop_history", "synchronize", "reset_graphs", "copy_slot",
                           "release_slot"})
 

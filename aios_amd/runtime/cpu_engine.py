@@ -82,7 +82,7 @@ class CpuEngine:
         self.last = logits[None]
         return logits if want_logits else []
 
-    def decode(self, slots, toks, pos, temps, topk, seed, mask: bytes = b"", top_p=None):
+    def decode(self, slots, toks, pos, temps, topk, seed, mask: bytes = b"", top_p=None, seeds=None):
         V = self.config.vocab_size
         row = (V + 7) // 8
         out, rows = [], []
@@ -95,11 +95,19 @@ class CpuEngine:
             m = mask[b * row:(b + 1) * row] if mask else None
             t = float(temps[b]) if b < len(temps) else 0.0
             k = int(topk[b]) if b < len(topk) else 0
-            rng = np.random.default_rng((int(seed) << 20) ^ (slot << 12) ^ p)
+            # per-row seed: the row's stream depends on (seed, position) only, as on the GPU
+            rng = (np.random.default_rng([int(seeds[b]) & 0xFFFFFFFF, p]) if seeds else
+                   np.random.default_rng((int(seed) << 20) ^ (slot << 12) ^ p))
             tp = float(top_p[b]) if top_p is not None and b < len(top_p) else 1.0
             out.append(host_sampler.sample(logits, t, k, tp, m, rng))
         self.last = np.stack(rows) if rows else None
         return out
+
+    def sample_first(self, pos, temperature, top_k, top_p, seed, mask: bytes = b""):
+        """the token after a prefill, from its last logits, with the decode steps' RNG stream"""
+        logits = self.last[0]
+        rng = np.random.default_rng([int(seed) & 0xFFFFFFFF, int(pos)])
+        return host_sampler.sample(logits, float(temperature), int(top_k), float(top_p), mask or None, rng)
 
     def last_logits(self, B: int):
         return self.last[:B].reshape(-1) if self.last is not None else np.zeros(0, np.float32)

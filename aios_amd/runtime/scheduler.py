@@ -40,6 +40,10 @@ from . import sampler as host_sampler
 log = logging.getLogger("aios.runtime.scheduler")
 
 
+def _fresh_seed() -> int:
+    return int.from_bytes(os.urandom(8), "little") | 1
+
+
 @dataclasses.dataclass
 class GenRequest:
     prompt_ids: List[int]
@@ -72,10 +76,13 @@ class GenResult:
 
 class _Seq:
     __slots__ = ("req", "slot", "pos", "last", "out", "grammar_state", "emitted", "t_first", "cached", "todo",
-                 "p_off", "r_off")
+                 "p_off", "r_off", "seed")
 
     def __init__(self, req, slot):
         self.req, self.slot = req, slot
+        # the request's sampling seed; unseeded requests draw a fresh one (llama-server does the
+        # same), so two identical T > 0 requests do not return identical "samples"
+        self.seed = int(req.seed) & 0xFFFFFFFFFFFFFFFF if req.seed else _fresh_seed()
         self.pos = 0                 # next position to write (prefill cursor, then decode position)
         self.last = 0
         self.out: List[int] = []
@@ -273,8 +280,15 @@ class Scheduler:
         if r.json_mode and self.grammar is not None:
             seq.grammar_state = self.grammar.initial()
             mask = self.grammar.mask(seq.grammar_state)
-        rng = np.random.default_rng(r.seed or None)
-        tok = host_sampler.sample(logits, r.temperature, r.top_k, r.top_p, mask, rng)
+        topk = int(r.top_k) if r.temperature > 0 else 0
+        topp = float(r.top_p) if 0.0 < r.top_p < 1.0 else 1.0
+        if hasattr(self.engine, "sample_first"):
+            # on the device, the decode steps' sampler and RNG stream (seed, position)
+            tok = int(self.engine.sample_first(seq.pos - 1, float(r.temperature), topk, topp, seq.seed,
+                                               bytes(mask) if mask is not None else b""))
+        else:
+            rng = np.random.default_rng([seq.seed & 0xFFFFFFFF, seq.pos - 1])
+            tok = host_sampler.sample(logits, r.temperature, r.top_k, r.top_p, mask, rng)
         seq.t_first = time.time()
         self.active.append(seq)
         self._accept(seq, tok)
@@ -346,7 +360,7 @@ class Scheduler:
         pos = [s.pos for s in self.active]
         temps = [float(s.req.temperature) for s in self.active]
         topk = [int(s.req.top_k) if s.req.temperature > 0 else 0 for s in self.active]
-        seed = int(self.active[0].req.seed) & 0xFFFFFFFF
+        seeds = [s.seed for s in self.active]  # per row: a request samples the same at any batch row
         t0 = time.perf_counter()
         mask = b""
         if any(s.grammar_state is not None for s in self.active):
@@ -356,7 +370,7 @@ class Scheduler:
                             for s in self.active)
         topp = [float(s.req.top_p) if 0.0 < s.req.top_p < 1.0 else 1.0 for s in self.active]
         t1 = time.perf_counter()
-        out = self.engine.decode(slots, toks, pos, temps, topk, seed, mask, topp)
+        out = self.engine.decode(slots, toks, pos, temps, topk, 0, mask, topp, seeds)
         t2 = time.perf_counter()
         self.stats["steps"] += 1
         self.stats["batch_sum"] += B

@@ -288,3 +288,26 @@ def test_paged_kv_prefix_sharing_and_copy_on_write(model_files, monkeypatch, gem
     eng.release_slot(1)
     eng.release_slot(2)
     assert eng.kv_blocks_free == total
+
+
+def test_per_row_seeds_are_row_independent(model_files):
+    """a row's sample depends on (its seed, its position), not on its batch row (verdict r2 #7)"""
+    eng, cfg = _load(model_files["Q4_K_M"], max_slots=4, max_batch=4)
+    prompt = [1, 5, 6, 7]
+    for s in range(3):
+        eng.prefill(s, prompt, 0, False)
+    t = int(np.argmax(eng.prefill(3, prompt, 0, True)))
+    a = eng.decode([0, 1], [t, t], [4, 4], [1.0, 1.0], [0, 0], 0, b"", [1.0, 1.0], [77, 5])
+    b = eng.decode([2, 0], [t, t], [4, 4], [1.0, 1.0], [0, 0], 0, b"", [1.0, 1.0], [5, 77])
+    assert a[0] == b[1] and a[1] == b[0]
+    draws = {eng.decode([0], [t], [4], [1.0], [0], 0, b"", [1.0], [s])[0] for s in range(1, 30)}
+    assert len(draws) > 1
+
+
+def test_sample_first_on_device(model_files):
+    eng, cfg = _load(model_files["Q4_K_M"], max_slots=2, max_batch=2)
+    logits = np.asarray(eng.prefill(0, [1, 9, 10, 11], 0, True))
+    assert eng.sample_first(3, 0.0, 0, 1.0, 5) == int(np.argmax(logits))  # T = 0: greedy
+    x = eng.sample_first(3, 1.0, 0, 1.0, 1234)
+    assert x == eng.sample_first(3, 1.0, 0, 1.0, 1234)
+    assert len({eng.sample_first(3, 1.0, 0, 1.0, s) for s in range(1, 30)}) > 1

@@ -122,7 +122,7 @@ class FakeEngine:
         l[self.script[0]] = 5.0   # wins only when a grammar mask removes the free-running token
         return l
 
-    def decode(self, slots, toks, pos, temps, topk, seed, mask, top_p=None):
+    def decode(self, slots, toks, pos, temps, topk, seed, mask, top_p=None, seeds=None):
         self.batches.append(len(slots))
         out = []
         row = (self.V + 7) // 8

@@ -38,7 +38,7 @@ class RecEngine:
             self.log.append(("prefill", slot, len(ids), start))
         return self._logits(ids[-1]) if want_logits else []
 
-    def decode(self, slots, toks, pos, temps, topk, seed, mask=b"", top_p=None):
+    def decode(self, slots, toks, pos, temps, topk, seed, mask=b"", top_p=None, seeds=None):
         time.sleep(self.step_s)
         with self.lock:
             self.log.append(("decode", len(slots)))
