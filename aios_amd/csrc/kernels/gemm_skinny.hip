@@ -372,12 +372,17 @@ __global__ void __launch_bounds__(RB * 64) gemm_skinny_kernel(GemmQArgs a, int S
   sk_body<QT0, RB, MT, EPI>(a, S);
 }
 
-size_t gemm_skinny_ws_bytes(int M, int N) { return (size_t)SK_SMAX * 16 * ((M + 15) / 16) * N * 4; }
 int gemm_skinny_cnt_len(int N) { return N / 64 + 1; }
 
 static int sk_env(const char* name, int dflt) {
   const char* e = std::getenv(name);
   return e ? std::atoi(e) : dflt;
+}
+// slab bytes for the largest split the launcher can pick: AIOS_SKINNY_SMAX (default 8) or an
+// explicit AIOS_SKINNY_S, never above SK_SMAX (sizing for SK_SMAX left half unused)
+size_t gemm_skinny_ws_bytes(int M, int N) {
+  const int smax = std::min(SK_SMAX, std::max(sk_env("AIOS_SKINNY_SMAX", 8), sk_env("AIOS_SKINNY_S", 0)));
+  return (size_t)smax * 16 * ((M + 15) / 16) * N * 4;
 }
 
 template <int QT0, int QT1, int RB, int MT>

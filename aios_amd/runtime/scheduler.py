@@ -348,8 +348,11 @@ class Scheduler:
         return {"tokens_per_s": len(self._tok_times) / 10.0,
                 "ttft_p50_ms": ttft[len(ttft) // 2] if ttft else 0.0,
                 "itl_ms": sum(self._step_ms) / len(self._step_ms) if self._step_ms else 0.0,
-                "active": len(self.active), "queued": len(self.queue),
-                "kv_slot_util": len(self.active) / max(1, self.max_slots),
+                # a sequence mid chunked-prefill holds a slot and is work in flight: it
+                # counts as active for idle-unload and replica routing
+                "active": len(self.active) + len(self.prefilling), "decoding": len(self.active),
+                "prefilling": len(self.prefilling), "queued": len(self.queue),
+                "kv_slot_util": (len(self.active) + len(self.prefilling)) / max(1, self.max_slots),
                 "avg_batch": st["batch_sum"] / st["steps"] if st["steps"] else 0.0,
                 "prefix_hit_tokens": st["cached_tokens"], "errors": st["errors"]}
 

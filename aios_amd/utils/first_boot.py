@@ -90,6 +90,16 @@ def hardware_inventory() -> Dict:
             "xgmi_links": sum(1 for g in gpus for l in g["links"] if l["type"] == "xgmi")}
 
 
+def _valid_key(path: str) -> bool:
+    """an existing private key openssl can parse (an empty or truncated file is not one)"""
+    if not os.path.exists(path) or os.path.getsize(path) == 0:
+        return False
+    if not shutil.which("openssl"):
+        return True
+    r = subprocess.run(["openssl", "pkey", "-in", path, "-noout"], capture_output=True, timeout=30)
+    return r.returncode == 0
+
+
 class FirstBoot:
     def __init__(self, data: str, etc: str, log: str, probe_network: bool = True, download_models: bool = False):
         self.data, self.etc, self.log = data, etc, log
@@ -114,17 +124,22 @@ class FirstBoot:
         keys = {}
         for name in ("node", "ledger-signing"):
             key = self.p("keys", f"{name}.key")
-            if not os.path.exists(key):
+            if not _valid_key(key):
+                # generated into a private temp file and renamed into place: a crash mid-way
+                # leaves no empty key behind that later runs would mistake for an identity
+                # (ADVICE r2); an empty or unparsable key is regenerated
                 if not shutil.which("openssl"):
                     raise RuntimeError("openssl not found: cannot create the Ed25519 identity")
-                fd = os.open(key, os.O_WRONLY | os.O_CREAT | os.O_EXCL, 0o600)
+                tmp = f"{key}.tmp.{os.getpid()}"
+                fd = os.open(tmp, os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o600)
                 os.close(fd)
-                r = subprocess.run(["openssl", "genpkey", "-algorithm", "ed25519", "-out", key],
+                r = subprocess.run(["openssl", "genpkey", "-algorithm", "ed25519", "-out", tmp],
                                    capture_output=True, text=True, timeout=30)
                 if r.returncode:
-                    os.unlink(key)
+                    os.unlink(tmp)
                     raise RuntimeError(f"openssl genpkey failed: {r.stderr.strip()}")
-                os.chmod(key, 0o600)
+                os.chmod(tmp, 0o600)
+                os.replace(tmp, key)
                 pub = subprocess.run(["openssl", "pkey", "-in", key, "-pubout"], capture_output=True, text=True,
                                      timeout=30)
                 with open(key[:-4] + ".pub", "w") as f:

@@ -4,7 +4,16 @@
 One process per GPU (torchrun / torch.distributed, RCCL backend on ROCm).  Each rank serves its
 own co-resident replica -- the agent router's request-level data parallelism (SURVEY.md §2.9 DP
 row) -- so per-GPU work is fixed as N grows ("weak" scaling) and `value` is the whole-job
-aggregate: total decoded tokens / max-over-ranks wall time.
+aggregate: total decoded tokens / max-over-ranks wall time.  `python bench.py --gpus N` without
+torchrun spawns the N ranks itself (a child `torch.distributed.run`, started before this process
+touches a GPU); under torchrun `--gpus` must equal WORLD_SIZE.
+
+Secondary `tp_strategic`: the strategic tier -- Llama-3-70B Q4_K_M, batch 1, 128-token prompt --
+tensor-parallel over the same N ranks (xGMI collectives inside the captured decode step,
+aios_amd/parallel/tp.py), so the 1 -> 8 curve also measures the TP data plane, not only
+independent replicas.  When ranks outnumber the visible GPUs they share one (correctness /
+overhead run, flagged `ranks_share_gpu`; the persistent decode kernel is then off, since two
+grid-resident kernels cannot share the CUs).
 
 Per rank: random-init Mistral-7B weights in the exact Q4_K_M per-tensor layout (Q6_K lm_head and
 "more bits" attn_v/ffn_down, Q4_K elsewhere; ~4.1 GB) generated directly in HBM (no network ->
@@ -43,11 +52,32 @@ def parse():
                     help="skip the secondary measurements (TinyLlama, fp32-activation Mistral)")
     ap.add_argument("--fp32-act", action="store_true",
                     help="headline with fp32 activations in the GEMVs instead of int8 (q8_1-style) ones")
+    ap.add_argument("--no-tp", action="store_true", help="skip the strategic-tier TP secondary")
+    ap.add_argument("--tp-model", default="llama3-70b")
+    ap.add_argument("--tp-steps", type=int, default=64)
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher check: set up the ranks and their process group, print one line per rank, "
+                         "touch no GPU")
     return ap.parse_args()
 
 
+def spawn(args) -> int:
+    """--gpus N without torchrun: run N ranks under a child torch.distributed.run (nothing in this
+    process has touched a GPU; the child's exit code is ours)."""
+    import socket
+    import subprocess
+
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__), *sys.argv[1:]]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    return subprocess.call(cmd, env=env)
+
+
 def measure(preset: str, recipe: str, batch: int, prompt: int, steps: int, warmup: int, use_graph: bool, dist,
-            device: int, act_q8: bool = True):
+            device: int, act_q8: bool = True, mk: bool = True):
     import torch
 
     from aios_amd.models.config import get_preset
@@ -57,6 +87,7 @@ def measure(preset: str, recipe: str, batch: int, prompt: int, steps: int, warmu
     max_ctx = ((prompt + warmup + steps + 2 + 63) // 64) * 64
     eng = random_engine(cfg, recipe, seed=1234, max_ctx=max_ctx, max_slots=max(batch, 1), max_batch=batch,
                         device=device, act_q8=act_q8)
+    eng.mk_enabled = mk
     slots = list(range(batch))
     toks = []
     for s in slots:
@@ -78,43 +109,101 @@ def measure(preset: str, recipe: str, batch: int, prompt: int, steps: int, warmu
     hist = eng.decode_loop_history(batch, prompt + warmup + 1, steps)
     assert all(0 <= t < cfg.vocab_size for t in hist), "invalid token ids from decode loop"
     info = dict(weight_gb=round(eng.weight_bytes / 1e9, 3), kv_gb=round(eng.kv_bytes / 1e9, 3),
-                workspace_gb=round(eng.workspace_bytes / 1e9, 3))
+                workspace_gb=round(eng.workspace_bytes / 1e9, 3),
+                persistent_decode=bool(batch == 1 and eng.mk_available and eng.mk_enabled))
+    del eng
+    return dt, info
+
+
+def measure_tp(args, rank: int, world: int, device: int, gloo):
+    """Strategic tier: Llama-3-70B TP=world, batch 1 (tools/bench_tp.py logic); seconds of the
+    timed steps on the leader (None on workers)."""
+    from aios_amd.models.config import get_preset
+    from aios_amd.parallel.tp import TPEngine, build_tp_engine, worker_loop
+
+    cfg = get_preset(args.tp_model)
+    steps, warmup = args.tp_steps, 8
+    max_ctx = ((args.prompt + warmup + steps + 2 + 63) // 64) * 64
+    eng, comm = build_tp_engine(cfg, rank, world, device, recipe=args.recipe, seed=1234, max_ctx=max_ctx,
+                                max_slots=1, max_batch=1, group=gloo)
+    if rank != 0:
+        worker_loop(eng, comm, group=gloo)
+        del eng
+        return None, None
+    tp = TPEngine(eng, comm, group=gloo) if world > 1 else eng
+    p = [cfg.bos_id] + [(7 * i) % (cfg.vocab_size - 3) + 3 for i in range(args.prompt - 1)]
+    tok = int(tp.prefill(0, p, 0, True).argmax())
+    tp.decode_loop_prepare([0], [tok], [args.prompt])
+    tp.decode_loop_run(1, warmup, True)
+    tp.synchronize()
+    t0 = time.perf_counter()
+    tp.decode_loop_run(1, steps, True)
+    tp.synchronize()
+    dt = time.perf_counter() - t0
+    if comm.error():
+        raise RuntimeError("TP all-reduce timed out")
+    info = {"weight_gb_per_rank": round(eng.weight_bytes / 1e9, 3)}
+    if world > 1:
+        tp.close()
     del eng
     return dt, info
 
 
 def main():
     args = parse()
+    if os.environ.get("WORLD_SIZE") is None and args.gpus > 1:
+        sys.exit(spawn(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world} (launch N ranks for --gpus N)")
     import torch
 
-    dist = None
+    n_dev = max(1, torch.cuda.device_count())  # counting devices does not initialise the GPU
+    share = world > n_dev                      # more ranks than GPUs: ranks share (not a scaling run)
+    device = local % n_dev
+    dist = gloo = None
+    if args.dry_run:
+        if world > 1:
+            import torch.distributed as td
+
+            td.init_process_group("gloo")
+            td.barrier()
+        print(json.dumps({"rank": rank, "world": world, "device": device, "ranks_share_gpu": share}), flush=True)
+        return
+    torch.cuda.set_device(device)
     if world > 1:
         import torch.distributed as td
 
-        torch.cuda.set_device(local)
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        td.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if share:  # RCCL refuses two ranks on one GPU
+            td.init_process_group("gloo")
+        else:
+            td.init_process_group("nccl", device_id=torch.device("cuda", device))
+        gloo = td.new_group(backend="gloo")  # the TP leader's command channel
         dist = td
-    else:
-        torch.cuda.set_device(local)
 
     act_q8 = not args.fp32_act
     dt, info = measure(args.model, args.recipe, args.batch, args.prompt, args.steps, args.warmup,
-                       not args.no_graph, dist, local, act_q8)
-    secondary = other_act = None
+                       not args.no_graph, dist, device, act_q8, mk=not share)
+    secondary = other_act = tp_dt = tp_info = None
     if not args.no_secondary:
         secondary, _ = measure("tinyllama-1.1b", "Q4_K_M", 1, args.prompt, args.steps, args.warmup,
-                               not args.no_graph, dist, local)
+                               not args.no_graph, dist, device, mk=not share)
         # the same Mistral decode with the other GEMV activation precision
         other_act, _ = measure(args.model, args.recipe, args.batch, args.prompt, args.steps, args.warmup,
-                               not args.no_graph, dist, local, not act_q8)
+                               not args.no_graph, dist, device, not act_q8, mk=not share)
+        if not args.no_tp:
+            if dist is not None:
+                dist.barrier()
+            tp_dt, tp_info = measure_tp(args, rank, world, device, gloo)
 
     # max over ranks
     if dist is not None:
-        t = torch.tensor([dt, secondary or 0.0, other_act or 0.0], device="cuda", dtype=torch.float64)
+        t = torch.tensor([dt, secondary or 0.0, other_act or 0.0], dtype=torch.float64)
+        if not share:
+            t = t.cuda()
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t[0])
         secondary = float(t[1]) if secondary is not None else None
@@ -151,6 +240,7 @@ def main():
                 "per_gpu_batch": args.batch,
                 "prompt_tokens": args.prompt,
                 "hipgraph": not args.no_graph,
+                "ranks_share_gpu": share,
                 **info,
             },
         }
@@ -170,6 +260,13 @@ def main():
                 "value": round(v2, 2),
                 "ms_per_step": round(other_act / args.steps * 1e3, 4),
                 "vs_baseline": round(v2 / BASELINE_MISTRAL_TOKS, 3),
+            }
+        if tp_dt is not None:
+            out["tp_strategic"] = {
+                "metric": f"decode tokens/sec {args.tp_model} {args.recipe} TP={world} (batch 1)",
+                "value": round(args.tp_steps / tp_dt, 2),
+                "ms_per_step": round(tp_dt / args.tp_steps * 1e3, 4),
+                "tp": world, "ranks_share_gpu": share, **(tp_info or {}),
             }
         print(json.dumps(out), flush=True)
     if dist is not None:

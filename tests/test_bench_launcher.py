@@ -1,0 +1,34 @@
+"""bench.py's --gpus contract on the CPU (multi-process, gloo): `--gpus N` without torchrun spawns N
+ranks itself, each seeing WORLD_SIZE=N; under torchrun a mismatching --gpus is refused."""
+import json
+import os
+import re
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _env():
+    e = dict(os.environ, MASTER_ADDR="127.0.0.1", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT"):
+        e.pop(k, None)
+    return e
+
+
+def test_gpus_n_spawns_n_ranks():
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run"],
+                       capture_output=True, text=True, timeout=240, env=_env(), cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [json.loads(m) for m in re.findall(r"\{[^{}]*\}", r.stdout)]
+    assert sorted(d["rank"] for d in lines) == [0, 1]
+    assert all(d["world"] == 2 for d in lines)
+    assert all(d["ranks_share_gpu"] for d in lines)  # no GPU here: both ranks share "one"
+
+
+def test_gpus_mismatch_is_refused():
+    env = _env()
+    env.update(WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4", "--dry-run"],
+                       capture_output=True, text=True, timeout=120, env=env, cwd=ROOT)
+    assert r.returncode != 0 and "WORLD_SIZE=2" in (r.stderr + r.stdout)
