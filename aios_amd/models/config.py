@@ -138,6 +138,16 @@ PRESETS: Dict[str, ModelConfig] = {
     "test-tp8-shape": ModelConfig(
         name="test-tp8-shape", vocab_size=1024, d_model=2048, n_layers=2, n_heads=16, n_kv_heads=8,
         head_dim=128, d_ff=4096, rope_theta=5e5, max_ctx=512),
+    # the router's other families at test size, full vocabularies and tokenizers (verdict r2 #9):
+    # Qwen3 (NeoX RoPE, QK-norm, 151,936-token byte-level BPE) and Llama-3 (128,256-token BPE)
+    "test-qwen3-shape": ModelConfig(
+        name="test-qwen3-shape", arch="qwen3", vocab_size=151936, d_model=512, n_layers=2, n_heads=4, n_kv_heads=1,
+        head_dim=128, d_ff=1536, rope_theta=1e6, rope_mode=ROPE_NEOX, norm_eps=1e-6, max_ctx=512, qk_norm=True,
+        bos_id=151643, eos_id=151645, tokenizer_model="gpt2", chat_template="chatml"),
+    "test-llama3-shape": ModelConfig(
+        name="test-llama3-shape", vocab_size=128256, d_model=512, n_layers=2, n_heads=4, n_kv_heads=1, head_dim=128,
+        d_ff=1536, rope_theta=5e5, max_ctx=512, bos_id=128000, eos_id=128009, tokenizer_model="gpt2",
+        chat_template="llama3"),
     "test-mistral-shape": ModelConfig(
         name="test-mistral-shape", vocab_size=1024, d_model=1024, n_layers=2, n_heads=8, n_kv_heads=2,
         head_dim=128, d_ff=2048, rope_theta=1e6, max_ctx=512, chat_template="mistral"),

@@ -71,6 +71,44 @@ def synthetic_vocab(n: int):
     return toks, np.array(scores, np.float32), np.array(types, np.int32)
 
 
+# the control tokens of the byte-level BPE families the router serves (Llama-3 / Qwen3 GGUF ids)
+BPE_SPECIALS = {
+    128000: "<|begin_of_text|>", 128001: "<|end_of_text|>", 128006: "<|start_header_id|>",
+    128007: "<|end_header_id|>", 128009: "<|eot_id|>",
+    151643: "<|endoftext|>", 151644: "<|im_start|>", 151645: "<|im_end|>",
+}
+
+
+def synthetic_bpe_vocab(n: int):
+    """GPT-2 style byte-level BPE vocab of n tokens: (tokens, merges, token_types) -- the 256 byte
+    symbols, ranked merges that build the common words (with and without a leading space), the
+    Llama-3 / Qwen control tokens at their real ids, reserved fillers elsewhere."""
+    from ..runtime.tokenizer import bytes_to_unicode
+
+    b2u = bytes_to_unicode()
+    toks: List[str] = [b2u[b] for b in range(256)]
+    types: List[int] = [1] * 256
+    seen = set(toks)
+    merges: List[str] = []
+    for w in _WORDS:
+        for word in (w, " " + w):
+            sym = [b2u[b] for b in word.encode()]
+            cur = sym[0]
+            for c in sym[1:]:
+                nxt = cur + c
+                if nxt not in seen and len(toks) < min(n, 100000):
+                    merges.append(f"{cur} {c}")
+                    seen.add(nxt)
+                    toks.append(nxt)
+                    types.append(1)
+                cur = nxt
+    while len(toks) < n:
+        i = len(toks)
+        toks.append(BPE_SPECIALS.get(i, f"<|reserved_{i}|>"))
+        types.append(3 if i in BPE_SPECIALS else 5)
+    return toks, merges, types
+
+
 def write_synthetic_gguf(path: str, cfg: ModelConfig, recipe: str = "Q4_K_M", seed: int = 0,
                          weight_std: float = 0.02, vocab: Optional[tuple] = None) -> str:
     rng = np.random.default_rng(seed)
@@ -89,14 +127,23 @@ def write_synthetic_gguf(path: str, cfg: ModelConfig, recipe: str = "Q4_K_M", se
     w.add(f"{arch}.rope.freq_base", float(cfg.rope_theta), GGUFValueType.FLOAT32)
     w.add(f"{arch}.rope.dimension_count", cfg.head_dim)
     w.add(f"{arch}.vocab_size", cfg.vocab_size)
-    toks, scores, types = vocab if vocab is not None else synthetic_vocab(cfg.vocab_size)
-    w.add("tokenizer.ggml.model", "llama")
-    w.add("tokenizer.ggml.tokens", toks)
-    w.add("tokenizer.ggml.scores", scores)
-    w.add("tokenizer.ggml.token_type", types)
+    if cfg.tokenizer_model == "gpt2" and vocab is None:  # Llama-3 / Qwen: byte-level BPE
+        toks, merges, types = synthetic_bpe_vocab(cfg.vocab_size)
+        w.add("tokenizer.ggml.model", "gpt2")
+        w.add("tokenizer.ggml.pre", "qwen2" if cfg.arch == "qwen3" else "llama-bpe")
+        w.add("tokenizer.ggml.tokens", toks)
+        w.add("tokenizer.ggml.merges", merges)
+        w.add("tokenizer.ggml.token_type", types)
+        w.add("tokenizer.ggml.add_bos_token", cfg.arch != "qwen3")
+    else:
+        toks, scores, types = vocab if vocab is not None else synthetic_vocab(cfg.vocab_size)
+        w.add("tokenizer.ggml.model", "llama")
+        w.add("tokenizer.ggml.tokens", toks)
+        w.add("tokenizer.ggml.scores", scores)
+        w.add("tokenizer.ggml.token_type", types)
+        w.add("tokenizer.ggml.add_bos_token", True)
     w.add("tokenizer.ggml.bos_token_id", cfg.bos_id)
     w.add("tokenizer.ggml.eos_token_id", cfg.eos_id)
-    w.add("tokenizer.ggml.add_bos_token", True)
     tmpl = CHAT_TEMPLATES.get(cfg.chat_template)
     if tmpl:
         w.add("tokenizer.chat_template", tmpl)

@@ -89,6 +89,23 @@ def context_for_size(nbytes: int) -> int:
     return 2048
 
 
+def estimated_q4_bytes(cfg) -> int:
+    """GGUF size of a preset at ~4.5 bits per weight (Q4_K_M), for the context heuristic of
+    synthetic tiers (no file to stat)"""
+    d, hd = cfg.d_model, cfg.head_dim
+    qd, kvd = cfg.n_heads * hd, cfg.n_kv_heads * hd
+    per_layer = d * (qd + 2 * kvd) + qd * d + 3 * d * cfg.d_ff
+    return int((cfg.n_layers * per_layer + 2 * cfg.vocab_size * d) * 4.5 / 8)
+
+
+def tier_context(cfg, path: str = "") -> int:
+    """Context for a tier without an explicit one: the reference's size heuristic (> 8 GB files:
+    8192, `runtime/src/main.rs:86-98`) on the GGUF file, or on the preset's estimated size for
+    synthetic tiers, capped by the model's window"""
+    nbytes = os.path.getsize(path) if path and os.path.exists(path) else estimated_q4_bytes(cfg)
+    return min(cfg.max_ctx, context_for_size(nbytes))
+
+
 class ModelManager:
     def __init__(self, device: int = 0, max_batch: int = 16, max_slots: int = 16, base_port: int = BASE_PORT):
         self.device = device
@@ -176,7 +193,12 @@ class ModelManager:
         elif tp > 1:
             # strategic tier: tensor parallel over the node's GPUs (ranks 1..tp-1 are worker
             # processes; the xGMI all-reduce runs inside each rank's captured decode graph)
-            ctx = context_length or 4096
+            if not context_length:
+                if base.startswith("synthetic:"):
+                    context_length = tier_context(get_preset(base.split(":")[1]))
+                else:
+                    context_length = context_for_size(os.path.getsize(base)) if os.path.exists(base) else 8192
+            ctx = context_length
             eng, cfg = launch_tp(base, tp, self.tp_devices(), ctx, self.max_slots, self.max_batch,
                                  seed=abs(hash(m.name)) % 1000, act_q8=act_q8)
             if base.startswith("synthetic:"):
@@ -192,7 +214,7 @@ class ModelManager:
             parts = base.split(":")
             cfg = get_preset(parts[1])
             recipe = parts[2] if len(parts) > 2 else "Q4_K_M"
-            ctx = context_length or min(cfg.max_ctx, 4096)
+            ctx = context_length or tier_context(cfg)
             eng = random_engine(cfg, recipe, seed=abs(hash(m.group or m.name)) % 1000, max_ctx=ctx,
                                 max_slots=self.max_slots, max_batch=self.max_batch, device=device, act_q8=act_q8)
             toks, scores, types = synthetic_vocab(cfg.vocab_size)

@@ -24,6 +24,7 @@ PRE_PATTERNS = {
     "qwen2": r"(?i:'s|'t|'re|'ve|'m|'ll|'d)|[^\r\n\p{L}\p{N}]?\p{L}+|\p{N}| ?[^\s\p{L}\p{N}]+[\r\n]*|\s*[\r\n]+|\s+(?!\S)|\s+",
     "gpt2": r"'s|'t|'re|'ve|'m|'ll|'d| ?\p{L}+| ?\p{N}+| ?[^\s\p{L}\p{N}]+|\s+(?!\S)|\s+",
 }
+PRE_PATTERNS["llama-bpe"] = PRE_PATTERNS["llama3"]  # the name Llama-3 GGUFs carry in tokenizer.ggml.pre
 
 
 @lru_cache(maxsize=1)

@@ -143,6 +143,22 @@ def test_prefill_gemm_chunks_match_reference(model_files, recipe, monkeypatch):
     assert (logits2 - rl).abs().max().item() < 2e-2 * scale
 
 
+@pytest.mark.parametrize("T", [4, 8, 15])
+@pytest.mark.parametrize("q8", [False, True])
+def test_short_prompt_gemm_prefill_matches_reference(model_files, monkeypatch, T, q8):
+    """4-15-token prompts go through the skinny MFMA GEMM (gm_min_rows_ = 4): their logits against
+    the fp32 reference for both GEMV activation settings (the decode steps' precision differs from
+    the GEMM's bf16 operands; the reference bounds both)"""
+    monkeypatch.setenv("AIOS_PREFILL_GEMM", "1")
+    path = model_files["mistral_shape"]
+    eng, cfg = _load(path, act_q8=q8)
+    ref = ReferenceModel.from_gguf(path, kv_bf16=True, act_q8=q8)
+    prompt = [1] + list(np.random.default_rng(T).integers(3, cfg.vocab_size, T - 1))
+    logits = torch.from_numpy(np.asarray(eng.prefill(0, prompt, 0, True)))
+    rl = ref.forward(prompt)[-1]
+    assert (logits - rl).abs().max().item() < 2e-2 * max(rl.abs().max().item(), 1.0)
+
+
 def test_prefill_gemm_vs_gemv_path(model_files, monkeypatch):
     path = model_files["Q4_K_M"]
     prompt = [1] + list(np.random.default_rng(4).integers(3, 200, 60))

@@ -297,3 +297,18 @@ def test_level_routing_table():
     assert mgr.resolve("tinyllama-1.1b-chat", "").request_count >= 1
     assert LEVEL_CANDIDATES["strategic"][0] == "llama3-70b"
     assert mgr.allocate_port() == 8082
+
+
+def test_tier_context_follows_reference_size_heuristic(tmp_path):
+    """reference runtime/src/main.rs:86-98: > 8 GB -> 8192, 2-8 GB -> 4096, else 2048; synthetic
+    tiers (the TP strategic tier included) use their preset's estimated Q4_K_M size"""
+    from aios_amd.runtime.model_manager import tier_context
+
+    assert tier_context(get_preset("llama3-70b")) == 8192
+    assert tier_context(get_preset("qwen3-14b")) == 8192
+    assert tier_context(get_preset("mistral-7b")) == 4096
+    assert tier_context(get_preset("tinyllama-1.1b")) == 2048
+    f = tmp_path / "big.gguf"
+    with open(f, "wb") as fh:
+        fh.truncate(9 * 10**9)  # sparse: only the size is read
+    assert tier_context(get_preset("mistral-7b").__class__(**{**get_preset("mistral-7b").__dict__}), str(f)) == 8192

@@ -113,14 +113,16 @@ def test_engine_config_vocab_parallel_rules():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world,gemm_prefill,prompt_len", [(2, 0, 21), (4, 0, 21), (2, 1, 21), (2, 1, 640)])
+@pytest.mark.parametrize("world,gemm_prefill,prompt_len", [(2, 0, 21), (4, 0, 21), (2, 1, 21), (2, 1, 640),
+                                                          (2, 1, 9)])
 def test_tp_xgmi_allreduce_and_sharded_model(tmp_path, world, gemm_prefill, prompt_len):
     """TP=N vs TP=1 on the same weights.  With the fp32-activation GEMV prefill (gemm_prefill=0)
     the only differences are fp32 summation order: 1e-3 of the logit scale.  The MFMA prefill
     path rounds activations to bf16 (and sums split-K partials atomically), so a rounding flip
     between the two shardings propagates: 1e-2 there -- a sharding bug is O(1).  The 640-token
     prompt runs the MFMA prefill in one chunk whose all-reduces (640 x d_model) take the two-shot
-    path with bf16 staging, split over several calls."""
+    path with bf16 staging, split over several calls; the 9-token one takes the skinny GEMM
+    (prompts of 4-15 tokens)."""
     out = tmp_path / f"tp{world}.json"
     port = 29600 + world + 10 * gemm_prefill + (20 if prompt_len > 100 else 0)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(world),
