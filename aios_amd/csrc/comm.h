@@ -48,7 +48,7 @@ struct ArDevCtx {
   float* buf[AR_MAX_RANKS];         // rank r's shared region: stage f32 [2][cap] | result f32 [2][cap] | stage bf16 [2][cap]
   uint32_t* flags[AR_MAX_RANKS];    // rank r's flags: [2 phases][AR_MAX_WG][AR_MAX_RANKS]
   uint32_t* epoch;                  // my per-WG epoch counters [AR_MAX_WG] (local)
-  uint32_t* error;                  // set to 1 when a wait timed out
+  uint32_t* error;                  // set to 1 when a wait timed out (device view of pinned host memory)
   int rank, world;
   size_t cap;                       // elements per half-buffer (<= AR_MAX_CALL)
 };
@@ -88,6 +88,10 @@ class XgmiComm {
   ArDevCtx* d_ = nullptr;        // device copy of h_
   float* mybuf_ = nullptr;
   uint32_t* myflags_ = nullptr;
+  // the give-up flag lives in pinned, device-mapped host memory: the kernels set it with
+  // system-scope stores and error() is a plain host load -- no per-call hipMemcpy (which
+  // serialised every leader call behind the device, verdict r2)
+  volatile uint32_t* host_error_ = nullptr;
   std::vector<void*> opened_;
   int device_ = 0;
   bool connected_ = false;

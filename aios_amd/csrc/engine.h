@@ -137,6 +137,11 @@ class Engine {
   bool mk_available() const { return mk_ok_; }
   void set_mk(bool on) { if (mk_enabled_ != on) { mk_enabled_ = on; reset_graphs(); } }
   bool mk_enabled() const { return mk_enabled_; }
+  // probes: one eager persistent decode step (rows prepared by decode_loop_prepare) with phase
+  // stamps; returns [grid][nstages][8] s_memrealtime ticks (100 MHz)
+  std::vector<unsigned long long> mk_probe();
+  int mk_nstages() const { return mk_args_.nstages; }
+  int mk_grid() const { return mk_grid_; }
   std::vector<int> block_table(int slot) const;
 
   // raw device pointers for tests / custom kernels

@@ -670,6 +670,33 @@ void Engine::mk_build() {
   mk_ok_ = true;
 }
 
+std::vector<unsigned long long> Engine::mk_probe() {
+  if (!mk_ok_) throw std::runtime_error("mk_probe: persistent decode kernel not available");
+  HIP_CHECK(hipSetDevice(cfg_.device));
+  const size_t n = (size_t)mk_grid_ * mk_args_.nstages * 8;
+  unsigned long long* d = nullptr;
+  HIP_CHECK(hipMalloc(&d, n * 8));
+  HIP_CHECK(hipMemset(d, 0, n * 8));
+  const bool was = mk_enabled_;
+  mk_enabled_ = true;
+  mk_args_.ts = d;
+  try {
+    enqueue_decode_step(1);  // eager: the captured graphs keep a.ts == null
+    HIP_CHECK(hipStreamSynchronize(stream_));
+  } catch (...) {
+    mk_args_.ts = nullptr;
+    mk_enabled_ = was;
+    hipFree(d);
+    throw;
+  }
+  mk_args_.ts = nullptr;
+  mk_enabled_ = was;
+  std::vector<unsigned long long> out(n);
+  HIP_CHECK(hipMemcpy(out.data(), d, n * 8, hipMemcpyDeviceToHost));
+  HIP_CHECK(hipFree(d));
+  return out;
+}
+
 bool Engine::mk_use(int B) const { return mk_ok_ && mk_enabled_ && B == 1 && !attn_block_on(B); }
 
 bool Engine::check_mk_err() {

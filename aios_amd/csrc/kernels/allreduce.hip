@@ -248,8 +248,15 @@ XgmiComm::XgmiComm(int rank, int world, int device, size_t cap_floats) : device_
   HIP_CHECK(hipMemset(myflags_, 0, 2 * AR_MAX_WG * AR_MAX_RANKS * sizeof(uint32_t)));
   HIP_CHECK(hipMalloc(&h_.epoch, AR_MAX_WG * sizeof(uint32_t)));
   HIP_CHECK(hipMemset(h_.epoch, 0, AR_MAX_WG * sizeof(uint32_t)));
-  h_.error = (uint32_t*)alloc_shared(64);
-  HIP_CHECK(hipMemset(h_.error, 0, 64));
+  {
+    void* hp = nullptr;
+    HIP_CHECK(hipHostMalloc(&hp, 64, hipHostMallocMapped));
+    std::memset(hp, 0, 64);
+    host_error_ = (volatile uint32_t*)hp;
+    void* dp = nullptr;
+    HIP_CHECK(hipHostGetDevicePointer(&dp, hp, 0));
+    h_.error = (uint32_t*)dp;
+  }
   h_.buf[rank] = mybuf_;
   h_.flags[rank] = myflags_;
   HIP_CHECK(hipMalloc(&d_, sizeof(ArDevCtx)));
@@ -266,7 +273,7 @@ XgmiComm::~XgmiComm() {
   for (void* p : opened_) hipIpcCloseMemHandle(p);
   hipFree(d_);
   hipFree(h_.epoch);
-  hipFree(h_.error);
+  hipHostFree((void*)host_error_);
   hipFree(mybuf_);
   hipFree(myflags_);
 }
@@ -338,13 +345,11 @@ void XgmiComm::allgather_cols(float* data, int rows, int slice, int ld, hipStrea
   }
 }
 
-bool XgmiComm::error() const {
-  uint32_t e = 0;
-  HIP_CHECK(hipMemcpy(&e, h_.error, sizeof(e), hipMemcpyDeviceToHost));
-  return e != 0;
-}
+// a host load of the mapped flag: reports give-ups of work that has COMPLETED (callers that need
+// the verdict of a step check after their synchronisation point)
+bool XgmiComm::error() const { return host_error_[0] != 0; }
 
-void XgmiComm::reset_error() { HIP_CHECK(hipMemset(h_.error, 0, 4)); }
+void XgmiComm::reset_error() { host_error_[0] = 0; }
 
 void XgmiComm::hook(void* self, float* data, size_t n, float* residual, hipStream_t st) {
   static_cast<XgmiComm*>(self)->allreduce(data, n, residual, st);

@@ -57,6 +57,14 @@ static_assert(LgLayout<QT_Q4_K>::slot_bytes <= MK_SLOT && LgLayout<QT_Q5_K>::slo
 static_assert(LgLayout<QT_Q4_K>::per_loader <= MK_PL && LgLayout<QT_Q5_K>::per_loader <= MK_PL &&
                   LgLayout<QT_Q6_K>::per_loader <= MK_PL, "loader count");
 
+// probes (tools/mk_probe.py): lane 0 of wave 0 (consumers) / wave MK_NC (loaders) stamps phase k of
+// stage s; a null a.ts costs one scalar compare
+#define MK_TS(s, k)                                                                                     \
+  do {                                                                                                  \
+    if (a.ts && (threadIdx.x & 63) == 0)                                                                \
+      a.ts[((size_t)blockIdx.x * a.nstages + (s)) * 8 + (k)] = __builtin_amdgcn_s_memrealtime();        \
+  } while (0)
+
 typedef const __attribute__((address_space(4))) MkStage* CStage;
 
 bool mk_format_ok(int qt) { return qt == QT_Q4_K || qt == QT_Q5_K || qt == QT_Q6_K; }
@@ -497,7 +505,9 @@ __device__ __forceinline__ void mk_attention(const MkArgs& a, int s, CStage st, 
   const int Hkv = a.n_kv_heads;
   const int nunits = Hkv * P;
   if (c < nunits && wave == 0) mk_wait(a, s - 1, false, GR);
+  if (wave == 0) MK_TS(s, 1);
   lg_barrier();
+  if (wave == 0) MK_TS(s, 2);
   float* s_o = (float*)scratch;
   float* s_m = s_o + MK_AW * G * HD;
   float* s_l = s_m + MK_AW * G;
@@ -628,6 +638,7 @@ __device__ __forceinline__ void mk_loader_prog(const MkArgs& a, uint8_t* ring, c
       mk_attention_loader<HD, G>(a, c, GR);
       continue;
     }
+    if (lw == 0) MK_TS(s, 6);
     lg_barrier();  // B_w
     if (t == 0) mk_loader_wait(issued, 0);
     lg_barrier();  // B_in
@@ -648,6 +659,7 @@ __device__ __forceinline__ void mk_loader_prog(const MkArgs& a, uint8_t* ring, c
         lg_barrier();
       }
     }
+    if (lw == 0) MK_TS(s, 7);
   }
   lg_vmcnt<0>();
 }
@@ -662,13 +674,17 @@ __device__ __forceinline__ void mk_consumer_prog(const MkArgs& a, uint8_t* ring,
   for (int s = 0; s < ns; ++s) {
     CStage st = stages + s;
     const int kind = st->kind;
+    if (wave == 0) MK_TS(s, 0);
     if (kind == MK_ATT) {
       mk_attention<HD, G>(a, s, st, scratch, flags, c, GR, wave, lane);
+      if (wave == 0) MK_TS(s, 5);
       continue;
     }
     // ---- input: wait for the previous stage, stage its output vector
     if (wave == 0 && s > 0) mk_wait(a, s - 1, stages[s - 1].kind == MK_ATT, GR);
+    if (wave == 0) MK_TS(s, 1);
     lg_barrier();  // B_w
+    if (wave == 0) MK_TS(s, 2);
     const int K = st->K;
     const int nch = K >> 5;
     float2* ms = (float2*)scratch;
@@ -677,6 +693,7 @@ __device__ __forceinline__ void mk_consumer_prog(const MkArgs& a, uint8_t* ring,
     mk_stage_in(src, K, st->norm_w, xq, ms, red);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     lg_barrier();  // B_in
+    if (wave == 0) MK_TS(s, 3);
     // ---- slot steps
     int roff = 0;
     for (int sg = 0; sg < st->nseg; ++sg) {
@@ -699,8 +716,10 @@ __device__ __forceinline__ void mk_consumer_prog(const MkArgs& a, uint8_t* ring,
     }
     // ---- epilogue + arrival
     if (wave == 0) {
+      MK_TS(s, 4);
       mk_epilogue(a, st, c, GR, rowacc, red);
       if (kind != MK_LM) mk_signal(a, s, c);
+      MK_TS(s, 5);
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

@@ -56,6 +56,7 @@ struct MkArgs {
   int scratch_off;        // LDS byte offset of the staging / attention scratch
   int lds_bytes;
   int timeout_us;         // per wait
+  unsigned long long* ts; // probes only: [grid][nstages][8] s_memrealtime stamps (null: off)
 };
 
 constexpr int MK_MAXU = 32;  // attention pieces per KV head

@@ -201,9 +201,11 @@ def launch_tp(spec: str, world: int, devices, max_ctx: int, max_slots: int, max_
 
     from ..runtime import native
     from .channel import LeaderChannel
+    from .ring import CommandRing
 
     devices = list(devices) or [0]
     ch = LeaderChannel(world)
+    ring = CommandRing(world)
     procs = []
     for r in range(1, world):
         env = dict(os.environ, AIOS_TP_TOKEN=ch.token)
@@ -220,10 +222,12 @@ def launch_tp(spec: str, world: int, devices, max_ctx: int, max_slots: int, max_
         ch.broadcast(handles)
         comm.connect(handles)
         eng.set_comm(comm)
+        ch.broadcast({"ring": ring.name})
     except Exception:
         for p in procs:
             p.kill()
         ch.close()
+        ring.close()
         raise
 
     def shutdown():
@@ -233,6 +237,7 @@ def launch_tp(spec: str, world: int, devices, max_ctx: int, max_slots: int, max_
             except subprocess.TimeoutExpired:
                 p.kill()
         ch.close()
+        ring.close()
 
     def abort():
         for p in procs:
@@ -244,7 +249,8 @@ def launch_tp(spec: str, world: int, devices, max_ctx: int, max_slots: int, max_
             except subprocess.TimeoutExpired:
                 pass
         ch.close()
+        ring.close()
 
-    tp = TPEngine(eng, comm, send=ch.broadcast, on_close=shutdown, on_abort=abort)
-    tp._keep = (comm, ch, procs)
+    tp = TPEngine(eng, comm, send=ring.send, on_close=shutdown, on_abort=abort)
+    tp._keep = (comm, ch, ring, procs)
     return tp, cfg

@@ -32,11 +32,17 @@ def main(argv=None):
     ch.send(comm.ipc_handle())
     comm.connect(ch.recv())
     eng.set_comm(comm)
+    # per-step commands arrive through the leader's shared-memory ring (ring.py); the TCP channel
+    # only carried the authenticated setup
+    from .ring import CommandRing
+
+    ring = CommandRing(a.world, name=str(ch.recv()["ring"]), worker=a.rank)
     try:
-        worker_loop(eng, comm, recv=ch.recv)
+        worker_loop(eng, comm, recv=ring.recv)
     except ConnectionError:
         pass
     finally:
+        ring.close()
         ch.close()
 
 
