@@ -139,7 +139,7 @@ class Engine {
   bool mk_enabled() const { return mk_enabled_; }
   // probes: one eager persistent decode step (rows prepared by decode_loop_prepare) with phase
   // stamps; returns [grid][nstages][8] s_memrealtime ticks (100 MHz)
-  std::vector<unsigned long long> mk_probe();
+  std::vector<unsigned long long> mk_probe(int dbg = 0);
   int mk_nstages() const { return mk_args_.nstages; }
   int mk_grid() const { return mk_grid_; }
   std::vector<int> block_table(int slot) const;
@@ -282,7 +282,7 @@ class Engine {
 
   std::map<int, hipGraphExec_t> graphs_;
   // persistent decode kernel state
-  bool mk_ok_ = false, mk_enabled_ = true;
+  bool mk_ok_ = false, mk_enabled_ = false;
   int mk_grid_ = 0;
   MkArgs mk_args_{};
   MkStage* d_mk_stages_ = nullptr;

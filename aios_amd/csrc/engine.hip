@@ -610,11 +610,14 @@ void Engine::finalize() {
 // The persistent batch-1 decode kernel (kernels/decode_mk.hip): one launch per step instead of
 // 5 per layer.  Served shapes: tp 1, int8 GEMV activations, K-quant weights (Q4_K / Q5_K / Q6_K),
 // interleaved (non-NeoX) RoPE without QK-norm or QKV bias, and an LDS plan that fits 160 KB.
-// AIOS_MK=0 switches it off (the launch-per-op path then serves batch 1).
+// It is built whenever the shape is served and enabled by AIOS_MK=1 (or set_mk): until it beats
+// the launch-per-op path on the bench model that path serves batch 1.  AIOS_MK=0 skips the build.
 void Engine::mk_build() {
   mk_ok_ = false;
-  if (const char* e = std::getenv("AIOS_MK"))
+  if (const char* e = std::getenv("AIOS_MK")) {
     if (std::atoi(e) == 0) return;
+    mk_enabled_ = std::atoi(e) == 1;
+  }
   if (cfg_.tp_size != 1 || !cfg_.act_q8 || cfg_.qk_norm || cfg_.rope_neox || !rope_cs_) return;
   const int d = cfg_.d_model, hd = cfg_.head_dim, H = cfg_.n_heads, Hkv = cfg_.n_kv_heads;
   const int qd = H * hd, kvd = Hkv * hd;
@@ -670,7 +673,7 @@ void Engine::mk_build() {
   mk_ok_ = true;
 }
 
-std::vector<unsigned long long> Engine::mk_probe() {
+std::vector<unsigned long long> Engine::mk_probe(int dbg) {
   if (!mk_ok_) throw std::runtime_error("mk_probe: persistent decode kernel not available");
   HIP_CHECK(hipSetDevice(cfg_.device));
   const size_t n = (size_t)mk_grid_ * mk_args_.nstages * 8;
@@ -680,16 +683,19 @@ std::vector<unsigned long long> Engine::mk_probe() {
   const bool was = mk_enabled_;
   mk_enabled_ = true;
   mk_args_.ts = d;
+  mk_args_.dbg = dbg;
   try {
     enqueue_decode_step(1);  // eager: the captured graphs keep a.ts == null
     HIP_CHECK(hipStreamSynchronize(stream_));
   } catch (...) {
     mk_args_.ts = nullptr;
+    mk_args_.dbg = 0;
     mk_enabled_ = was;
     hipFree(d);
     throw;
   }
   mk_args_.ts = nullptr;
+  mk_args_.dbg = 0;
   mk_enabled_ = was;
   std::vector<unsigned long long> out(n);
   HIP_CHECK(hipMemcpy(out.data(), d, n * 8, hipMemcpyDeviceToHost));

@@ -51,6 +51,7 @@ constexpr int MK_PL = 16;        // DMA instructions per loader wave per slot (p
 constexpr int MK_AW = 8;         // attention waves
 constexpr int MK_RED = 64;       // LDS floats of the staging reduction
 constexpr int MK_FLAGS = 16;     // LDS ints of flags
+constexpr int MK_ATT_SHORT = 256;  // contexts up to this many keys: one attention unit per KV head
 
 static_assert(LgLayout<QT_Q4_K>::slot_bytes <= MK_SLOT && LgLayout<QT_Q5_K>::slot_bytes <= MK_SLOT &&
                   LgLayout<QT_Q6_K>::slot_bytes <= MK_SLOT, "ring slot");
@@ -358,7 +359,7 @@ struct MkAtt {
   static constexpr int KPS = 64 / LPK;         // keys per wave-instruction
   static constexpr int ROUND = MK_AW * KPS;    // keys per round of the 8 waves
   static constexpr int HG = G > 5 ? 4 : G;     // query heads per register pass (VGPR budget: 128)
-  static constexpr int U = HG >= 4 ? 2 : 4;    // rounds in flight per lane
+  static constexpr int U = HG >= 5 ? 2 : 4;    // rounds in flight per lane (128 keys per pass at hd 128)
 };
 
 // the unit split of the live context: pieces of >= 128 keys (a multiple of the 8-wave round),
@@ -366,6 +367,11 @@ struct MkAtt {
 template <int HD, int G>
 __device__ __forceinline__ void mk_att_split(int len, int& piece, int& P) {
   using A = MkAtt<HD, G>;
+  if (len <= MK_ATT_SHORT) {  // one unit per KV head, no partials / combine round trips
+    piece = len;
+    P = 1;
+    return;
+  }
   piece = max(128, (len + MK_MAXU - 1) / MK_MAXU);
   piece = (piece + A::ROUND - 1) / A::ROUND * A::ROUND;
   P = (len + piece - 1) / piece;
@@ -385,7 +391,11 @@ __device__ __forceinline__ void mk_att_wave(const MkArgs& a, CStage st, int kvh,
   constexpr int LPK = A::LPK, KPS = A::KPS, ROUND = A::ROUND, U = A::U, HG = A::HG;
   const int ksub = lane / LPK, dsl = lane % LPK;
   const int maxb = a.max_ctx / KV_BLOCK;
-  const int* btr = a.block_table + (size_t)a.slot[0] * maxb;
+  // the block table through the constant address space: the KPS keys of one wave-instruction sit
+  // in one 128-key block, so each lookup is a wave-uniform scalar load (K$), not a vector load the
+  // K/V addresses would wait a memory round trip for
+  typedef const __attribute__((address_space(4))) int* CInt;
+  const CInt btr = (CInt)a.block_table + (size_t)(*(CInt)a.slot) * maxb;
   const size_t blk_stride = (size_t)a.n_kv_heads * KV_BLOCK * HD;
   const bf16_t* kc = st->k_cache + (size_t)kvh * KV_BLOCK * HD + dsl * 8;
   const bf16_t* vc = st->v_cache + (size_t)kvh * KV_BLOCK * HD + dsl * 8;
@@ -414,10 +424,12 @@ __device__ __forceinline__ void mk_att_wave(const MkArgs& a, CStage st, int kvh,
     bool valid[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int key = base + u * ROUND + ksub;
+      const int kb = base + u * ROUND;  // wave-uniform first key of the instruction
+      const int key = kb + ksub;
       valid[u] = key < k1;
-      const int kk = valid[u] ? key : k0;
-      const size_t off = (size_t)btr[kk / KV_BLOCK] * blk_stride + (size_t)(kk % KV_BLOCK) * HD;
+      const int blk = btr[min(kb / KV_BLOCK, maxb - 1)];
+      const int kk = valid[u] ? key : kb;
+      const size_t off = (size_t)blk * blk_stride + (size_t)(kk % KV_BLOCK) * HD;
       if (kk == newest) {  // written in this launch by another CU
         kr[u] = ld_sc1_16(kc + off);
         vr[u] = ld_sc1_16(vc + off);
@@ -524,6 +536,29 @@ __device__ __forceinline__ void mk_attention(const MkArgs& a, int s, CStage st, 
         mk_att_wave<HD, G>(a, st, kvh, hg0, k0, k1, newest, s_o, s_m, s_l, wave, lane);
     }
     lg_barrier();  // A1: the waves' partials are in LDS
+    if (P == 1) {  // short context: the merged, normalised output straight to the O stage
+      if (aw) {
+        for (int idx = tid; idx < G * HD; idx += MK_AW * 64) {
+          const int g = idx / HD, dd = idx - g * HD;
+          float M = s_m[g];
+#pragma unroll
+          for (int w = 1; w < MK_AW; ++w) M = fmaxf(M, s_m[w * G + g]);
+          float L = 0.f, acc = 0.f;
+#pragma unroll
+          for (int w = 0; w < MK_AW; ++w) {
+            const float sw = fast_exp2(s_m[w * G + g] - M);
+            L += sw * s_l[w * G + g];
+            acc += sw * s_o[((size_t)w * G + g) * HD + dd];
+          }
+          st_sc1_f32(a.attn + (size_t)(kvh * G + g) * HD + dd, acc / L);
+        }
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      lg_barrier();  // A2: drained
+      if (tid == 0)
+        __hip_atomic_fetch_add(a.cnt + ((size_t)s * 8 + (kvh & 7)) * 32, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      continue;
+    }
     if (aw) {
       for (int idx = tid; idx < G * HD; idx += MK_AW * 64) {
         const int g = idx / HD, dd = idx - g * HD;
@@ -608,6 +643,7 @@ __device__ __forceinline__ void mk_attention_loader(const MkArgs& a, int c, int 
   for (int u = c; u < nunits; u += GR) {
     lg_barrier();  // A1
     lg_barrier();  // A2
+    if (P == 1) continue;
     lg_barrier();  // A3
     lg_barrier();  // C1
     lg_barrier();  // C2
@@ -650,7 +686,7 @@ __device__ __forceinline__ void mk_loader_prog(const MkArgs& a, uint8_t* ring, c
       const int nsl = (r1 * nch - r0 * nch + cps - 1) / cps;
       for (int k = 0; k < nsl; ++k, ++t) {
         if (lc.s < ns) {
-          mk_issue(stages, lc, ring + (size_t)(issued % MK_R) * MK_SLOT, lw);
+          if (!(a.dbg & 2)) mk_issue(stages, lc, ring + (size_t)(issued % MK_R) * MK_SLOT, lw);
           ++issued;
           ++lc.t;
           mk_settle(stages, ns, c, GR, lc);
@@ -707,9 +743,10 @@ __device__ __forceinline__ void mk_consumer_prog(const MkArgs& a, uint8_t* ring,
         const uint8_t* slotp = ring + (size_t)(t % MK_R) * MK_SLOT;
         const int jb = cbeg + k * cps;
         const int n = min(cps, cend - jb);
-        mk_fmt(qt, [&](auto tag) {
-          mk_consume<decltype(tag)::value>(slotp, jb, n, nch, r0, rowacc + roff, xq, ms, wave, lane);
-        });
+        if (!(a.dbg & 1))
+          mk_fmt(qt, [&](auto tag) {
+            mk_consume<decltype(tag)::value>(slotp, jb, n, nch, r0, rowacc + roff, xq, ms, wave, lane);
+          });
         lg_barrier();
       }
       roff += r1 - r0;

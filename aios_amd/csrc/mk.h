@@ -57,6 +57,8 @@ struct MkArgs {
   int lds_bytes;
   int timeout_us;         // per wait
   unsigned long long* ts; // probes only: [grid][nstages][8] s_memrealtime stamps (null: off)
+  int dbg;                // probes only: bit0 consumers skip the slot dot products, bit1 loaders
+                          // issue no DMA (outputs garbage; tools/mk_probe.py --dbg)
 };
 
 constexpr int MK_MAXU = 32;  // attention pieces per KV head

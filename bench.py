@@ -87,7 +87,8 @@ def measure(preset: str, recipe: str, batch: int, prompt: int, steps: int, warmu
     max_ctx = ((prompt + warmup + steps + 2 + 63) // 64) * 64
     eng = random_engine(cfg, recipe, seed=1234, max_ctx=max_ctx, max_slots=max(batch, 1), max_batch=batch,
                         device=device, act_q8=act_q8)
-    eng.mk_enabled = mk
+    if not mk:
+        eng.mk_enabled = False
     slots = list(range(batch))
     toks = []
     for s in slots:

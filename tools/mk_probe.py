@@ -25,6 +25,8 @@ def main():
     ap.add_argument("--model", default="mistral-7b")
     ap.add_argument("--prompt", type=int, default=128)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--dbg", type=int, nargs="*", default=[0],
+                    help="probe modes: 0 real, 1 consumers skip the dot products, 2 loaders issue no DMA")
     args = ap.parse_args()
     from aios_amd.models.config import get_preset
     from aios_amd.runtime.loader import random_engine
@@ -37,8 +39,8 @@ def main():
     eng.decode_loop_run(1, 8, True)
     eng.synchronize()
     L = cfg.n_layers
-    for rep in range(args.reps):
-        ts = eng.mk_probe().astype(np.int64)  # [G][S][8] ticks of 10 ns
+    for rep, dbg in [(r, d) for d in args.dbg for r in range(args.reps)]:
+        ts = eng.mk_probe(dbg).astype(np.int64)  # [G][S][8] ticks of 10 ns
         t0 = ts[:, 0, 0].min()
         us = (ts - t0) / 100.0
         G, S, _ = ts.shape
@@ -61,7 +63,7 @@ def main():
             rows[k]["stage_span_med"] = round(float(np.median(span)), 2)
             rows[k]["end_skew"] = round(float(np.median(a[:, :, 5].max(axis=0) - a[:, :, 5].min(axis=0))), 2)
         total = float(us[:, -1, 5].max())
-        print(json.dumps({"rep": rep, "total_us": round(total, 1), "per_layer_us": round(total / L, 2), **rows}),
+        print(json.dumps({"rep": rep, "dbg": dbg, "total_us": round(total, 1), "per_layer_us": round(total / L, 2), **rows}),
               flush=True)
 
 
