@@ -739,6 +739,34 @@ __device__ __forceinline__ void mk_consumer_prog(const MkArgs& a, uint8_t* ring,
       const int cps = mk_cps(qt);
       const int cbeg = r0 * nch, cend = r1 * nch;
       const int nsl = (cend - cbeg + cps - 1) / cps;
+      constexpr int NGS4 = LgLayout<QT_Q4_K>::NGS;
+      if (qt == QT_Q4_K && (nch & 63) == 0 && NGS4 % (nch >> 6) == 0 && !(a.dbg & 1)) {
+        // Q4_K chunk pairs with x in registers (gemv_cu.h Q4PairX): every slot holds whole rows,
+        // so a lane sees the same K columns in every slot of the segment
+        const int m = nch >> 6;
+        const int half = lane >> 5, p = lane & 31, kk = wave * 2 + half;
+        Q4PairX X;
+        q4p_load_x(xq, ms, (kk % m) * 64 + 2 * p, X);
+        using L4 = LgLayout<QT_Q4_K>;
+        const int rps = NGS4 / m, rk = kk / m;
+        for (int k = 0; k < nsl; ++k, ++t) {
+          const uint8_t* slotp = ring + (size_t)(t % MK_R) * MK_SLOT;
+          const int n = min(cps, cend - cbeg - k * cps);
+          if (wave * 128 < n) {
+            const uint4 a0 = *(const uint4*)(slotp + L4::off(0) + kk * 1024 + p * 32);
+            const uint4 a1 = *(const uint4*)(slotp + L4::off(0) + kk * 1024 + p * 32 + 16);
+            const uint4 mt = *(const uint4*)(slotp + L4::off(1) + kk * 128 + (p >> 2) * 16);
+            const bool ok = kk * 64 < n;
+            const float v = cu_half_sum(ok ? q4p_dot(a0, a1, mt, p & 3, X) : 0.f);
+            if (p == 0 && ok)
+              __hip_atomic_fetch_add(rowacc + roff + k * rps + rk, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          }
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // row sums visible past the barrier
+          lg_barrier();
+        }
+        roff += r1 - r0;
+        continue;
+      }
       for (int k = 0; k < nsl; ++k, ++t) {
         const uint8_t* slotp = ring + (size_t)(t % MK_R) * MK_SLOT;
         const int jb = cbeg + k * cps;
@@ -747,6 +775,7 @@ __device__ __forceinline__ void mk_consumer_prog(const MkArgs& a, uint8_t* ring,
           mk_fmt(qt, [&](auto tag) {
             mk_consume<decltype(tag)::value>(slotp, jb, n, nch, r0, rowacc + roff, xq, ms, wave, lane);
           });
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         lg_barrier();
       }
       roff += r1 - r0;

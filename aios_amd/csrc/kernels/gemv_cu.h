@@ -51,6 +51,74 @@ __device__ __forceinline__ float cu_wave_sum(float v) {
   return v;
 }
 
+// sum over each 32-lane half (lanes 0-31 / 32-63), result in every lane of the half
+__device__ __forceinline__ float cu_half_sum(float v) {
+  v += cu_dpp<0xB1>(v);
+  v += cu_dpp<0x4E>(v);
+  v += cu_dpp<0x141>(v);
+  v += cu_dpp<0x140>(v);
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Q4_K chunk PAIRS with the activation operand in registers (batch-1 ring consumers).
+//
+// Chunks 2p and 2p+1 of a row hold the two 16-halves of one sub-block pair g = p & 3 of
+// superblock p >> 2: they share the scale/min decode, and run r of both is ONE 32-element int8 x
+// block (one dx), so both chunks' integer dot products add before the float scaling.  A lane
+// that takes a pair spends ~64 VALU per 64 weights against ~75 per 32 for one chunk with its x
+// read from LDS (measured issue-bound: gate_up's 8 ring slots per CU computed in 11 us of a 17 us
+// kernel, tools/mk_probe.py --dbg 2).  When every slot holds whole rows (NGS % groups-per-row
+// == 0) a wave's lanes see the same K columns in every slot, so x is loaded once per GEMV.
+// ---------------------------------------------------------------------------------------------
+struct Q4PairX {
+  int x0[8], x1[8];          // run 0 / run 1 codes: chunk 2p's 4 words, then chunk 2p+1's
+  float dx0, dx1, sx0, sx1;  // block scales; dx * code sums over both chunks' runs
+};
+
+// c0: the pair's first chunk (even) within the row, staged by q8_stage (x in QT_Q4_K order)
+__device__ __forceinline__ void q4p_load_x(const int8_t* xq, const float2* ms, int c0, Q4PairX& X) {
+  const int rot = (c0 >> 3) & 1;  // the staging swizzle (q8_octet): run r at 16 * (r ^ rot)
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int8_t* xc = xq + (size_t)(c0 + h) * 32;
+    const uint4 p0 = *(const uint4*)(xc + 16 * rot);
+    const uint4 p1 = *(const uint4*)(xc + 16 * (rot ^ 1));
+    X.x0[4 * h + 0] = p0.x; X.x0[4 * h + 1] = p0.y; X.x0[4 * h + 2] = p0.z; X.x0[4 * h + 3] = p0.w;
+    X.x1[4 * h + 0] = p1.x; X.x1[4 * h + 1] = p1.y; X.x1[4 * h + 2] = p1.z; X.x1[4 * h + 3] = p1.w;
+  }
+  const float4 m0 = *(const float4*)(ms + (size_t)c0 * 2);      // (dx, sx) of runs 0, 1 of chunk 2p
+  const float4 m1 = *(const float4*)(ms + (size_t)c0 * 2 + 2);  // ... of chunk 2p+1
+  X.dx0 = m0.x;
+  X.dx1 = m0.z;
+  X.sx0 = m0.y + m1.y;
+  X.sx1 = m0.w + m1.w;
+}
+
+// a0 / a1: the pair's two 16-B code chunks, mt: its superblock's repacked meta, g = p & 3
+__device__ __forceinline__ float q4p_dot(const uint4& a0, const uint4& a1, const uint4& mt, int g, const Q4PairX& X) {
+  const float d = __half2float(__ushort_as_half((uint16_t)(mt.x & 0xffff)));
+  const float dmin = __half2float(__ushort_as_half((uint16_t)(mt.x >> 16)));
+  const uint32_t f = kq_field(mt.y, mt.z, mt.w, g);
+  int s0 = 0, s1 = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const uint32_t w = u4_word(a0, i);
+    s0 = __builtin_amdgcn_sdot4((int)(w & 0x0f0f0f0fu), X.x0[i], s0, false);
+    s1 = __builtin_amdgcn_sdot4((int)((w >> 4) & 0x0f0f0f0fu), X.x1[i], s1, false);
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const uint32_t w = u4_word(a1, i);
+    s0 = __builtin_amdgcn_sdot4((int)(w & 0x0f0f0f0fu), X.x0[4 + i], s0, false);
+    s1 = __builtin_amdgcn_sdot4((int)((w >> 4) & 0x0f0f0f0fu), X.x1[4 + i], s1, false);
+  }
+  const float u = (float)(f & 63) * X.dx0 * (float)s0 + (float)((f >> 6) & 63) * X.dx1 * (float)s1;
+  const float o = (float)((f >> 12) & 63) * X.sx0 + (float)((f >> 18) & 63) * X.sx1;
+  return d * u - dmin * o;
+}
+
 // one 64-chunk item (chunk c = it * 64 + lane) of a row against the staged int8 x
 template <int QT>
 __device__ __forceinline__ void cu_compute(const RawChunk& raw, int it, int nch, const int8_t* xq,

@@ -311,6 +311,35 @@ __global__ void __launch_bounds__(LG_THREADS) gemv_lds_b1(GemvArgs a, CuPlan pl)
     CU_STAMP(2);
     lg_barrier();  // B1
     CU_STAMP(3);
+    if constexpr (QT == QT_Q4_K) {
+      if (L::NGS % nit == 0) {
+        // chunk pairs, x in registers (gemv_cu.h Q4PairX): lanes 0-31 take group 2w's 32 pairs,
+        // lanes 32-63 group 2w+1's; every slot holds NGS / nit whole rows
+        const int half = lane >> 5, p = lane & 31;
+        const int kk = wave * GPW + half;
+        Q4PairX X;
+        q4p_load_x(xq, ms, (kk % nit) * 64 + 2 * p, X);
+        const int rps = L::NGS / nit, rk = kk / nit;
+        for (int t = 0; t < T; ++t) {
+          if (t * L::NGS + wave * GPW < ngroups) {
+            const uint8_t* slot = ring + (size_t)(t % LG_R) * L::slot_bytes;
+            const uint4 a0 = *(const uint4*)(slot + L::off(0) + kk * 1024 + p * 32);
+            const uint4 a1 = *(const uint4*)(slot + L::off(0) + kk * 1024 + p * 32 + 16);
+            const uint4 mt = *(const uint4*)(slot + L::off(1) + kk * 128 + (p >> 2) * 16);
+            const bool ok = t * L::NGS + kk < ngroups;
+            const float v = cu_half_sum(ok ? q4p_dot(a0, a1, mt, p & 3, X) : 0.f);
+            if (p == 0 && ok)
+              __hip_atomic_fetch_add(&rowacc[t * rps + rk], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          }
+          lg_barrier();
+        }
+        CU_STAMP(4);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        lg_barrier();  // final
+        CU_STAMP(5);
+        return;
+      }
+    }
     for (int t = 0; t < T; ++t) {
       const int gb = t * L::NGS + wave * GPW;  // this wave's first group of the slot
       if (gb < ngroups) {
