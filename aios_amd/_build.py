@@ -64,12 +64,21 @@ def _flags():
     ]
 
 
+# The GEMV ring consumers add one lane's row sum to an LDS accumulator per step; LLVM's atomic
+# optimizer wraps every such uniform-address atomic in a readlane waterfall loop (~15 instructions
+# per group in a VALU-issue-bound loop) although only one lane is active.  Off for the GEMV objects
+# (elementwise.hip's many-lane candidate counters keep it).
+_NO_ATOMIC_OPT = ["-mllvm", "-amdgpu-atomic-optimizer-strategy=None"]
+_FILE_FLAGS = {n: _NO_ATOMIC_OPT for n in ("gemv_kquant.hip", "gemv_kquant2.hip", "gemv_legacy.hip",
+                                           "decode_mk.hip", "attn_block.hip")}
+
+
 def _compile(src: Path, flags, hipcc) -> Path:
     obj = BUILD / (src.stem + ".o")
     newest_dep = max([src.stat().st_mtime] + [h.stat().st_mtime for h in _headers()])
     if obj.exists() and obj.stat().st_mtime >= newest_dep:
         return obj
-    cmd = [hipcc, *flags, "-c", str(src), "-o", str(obj)]
+    cmd = [hipcc, *flags, *_FILE_FLAGS.get(src.name, []), "-c", str(src), "-o", str(obj)]
     if src.suffix == ".cpp":
         cmd = [hipcc, *flags, "-x", "hip", "-c", str(src), "-o", str(obj)]
     r = subprocess.run(cmd, capture_output=True, text=True)

@@ -17,6 +17,7 @@ using namespace aios;
 namespace aios {
 double bench_launch_chain(int n_kernels, int blocks, int use_graph, int reps);
 double bench_stream_read(size_t bytes, int nbuf, int wg_per_cu, int u, int threads, int reps);
+double bench_stream_read_part(size_t bytes, int nbuf, int mode, int threads, int reps);
 }
 
 namespace {
@@ -505,6 +506,8 @@ PYBIND11_MODULE(_engine, m) {
            })
       .def_property_readonly("vocab_size", &JsonGrammar::vocab_size)
       .def_property_readonly("cache_size", &JsonGrammar::cache_size);
+  m.def("bench_stream_read_part", &aios::bench_stream_read_part, py::arg("bytes"), py::arg("nbuf"), py::arg("mode"),
+        py::arg("threads") = 512, py::arg("reps") = 20);
   m.def("bench_stream_read", &aios::bench_stream_read, py::arg("bytes"), py::arg("nbuf"), py::arg("wg_per_cu"),
         py::arg("u"), py::arg("threads"), py::arg("reps"));
   m.def("bench_launch_chain", &aios::bench_launch_chain, py::arg("n_kernels"), py::arg("blocks"), py::arg("use_graph"),

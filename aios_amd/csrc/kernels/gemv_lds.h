@@ -152,6 +152,7 @@ __device__ __forceinline__ void lg_dma_slot(const GemvArgs& a, uint8_t* dst, int
         for (int i = 0; i < NI; ++i) {
           if ((idx + i) % LG_NL != lw) continue;
           auto* ldst = (__attribute__((address_space(3))) void*)(dst + L::off(p) + i * 64 * S);
+          // (default policy instead of nt: +6-7 % on gate_up / down / lm_head, tools/gemv_cu_probe.py)
           if constexpr (S == 16) __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, ldst, 16, lane * 16, soff0 + i * 1024, 0, 2);
           else __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, ldst, 4, lane * 4, soff0 + i * 256, 0, 2 /* nt */);
           ++issued;
@@ -269,6 +270,9 @@ __global__ void __launch_bounds__(LG_THREADS) gemv_lds_b1(GemvArgs a, CuPlan pl)
     constexpr int LG_R = L::R;
     const int T = (ngroups + L::NGS - 1) / L::NGS;
     const int lw = wave - LG_NG;
+    // (an L2 prefetch of the slots past the ring -- one 4-B LDS-DMA per 128-B line, default
+    // policy -- measured 25-30 % SLOWER on every shape, at any distance incl. the DMA'd slot
+    // itself: the per-line requests double the CU's TA / L2 request count)
     if (LG_B0) lg_barrier();  // B0: the consumers' x loads are queued ahead of any weight byte
     const int npro = min(T, LG_R - 1);
     for (int s = 0; s < npro; ++s) lg_dma_slot<QT>(a, ring + (size_t)s * L::slot_bytes, s, lw, r0, nit, ngroups);
@@ -335,6 +339,38 @@ __global__ void __launch_bounds__(LG_THREADS) gemv_lds_b1(GemvArgs a, CuPlan pl)
         }
         CU_STAMP(4);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        lg_barrier();  // final
+        CU_STAMP(5);
+        return;
+      }
+    } else if constexpr (GPW == 1 && QFmt<QT>::W == 32) {
+      if (L::NGS % nit == 0) {
+        // one group per wave per slot, the same K columns in every slot: x in registers
+        const int c = (wave % nit) * 64 + lane;
+        int xv[8];
+        const int8_t* xc = xq + (size_t)c * 32;
+        const int rot = (c >> 3) & 1;
+        const uint4 p0 = *(const uint4*)(xc + 16 * rot), p1 = *(const uint4*)(xc + 16 * (rot ^ 1));
+        xv[0] = p0.x; xv[1] = p0.y; xv[2] = p0.z; xv[3] = p0.w;
+        xv[4] = p1.x; xv[5] = p1.y; xv[6] = p1.z; xv[7] = p1.w;
+        const float4 m = *(const float4*)(ms + (size_t)c * 2);
+        const int rps = L::NGS / nit, rk = wave / nit;
+        for (int t = 0; t < T; ++t) {
+          if (t * L::NGS + wave < ngroups) {
+            const uint8_t* slot = ring + (size_t)(t % LG_R) * L::slot_bytes;
+            RawChunk raw;
+            lg_read<QT>(slot, wave, lane, raw);
+            float sc[2], of[2];
+            q8_scales_bf<QT>(raw, c, sc, of);
+            int is[2];
+            QDot<QT>::isums(raw, c, xv, is);
+            const float v = cu_wave_sum(sc[0] * m.x * (float)is[0] - of[0] * m.y + sc[1] * m.z * (float)is[1] - of[1] * m.w);
+            if (lane == 0) atomicAdd(&rowacc[t * rps + rk], v);
+          }
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          lg_barrier();
+        }
+        CU_STAMP(4);
         lg_barrier();  // final
         CU_STAMP(5);
         return;

@@ -135,7 +135,9 @@ def test_decode_stall_watchdog_fails_requests(small_gguf, monkeypatch):
     results = []
     ids = m.tokenizer.encode("x", add_bos=True)
     m.scheduler.submit(GenRequest(prompt_ids=ids, max_tokens=50, temperature=0.0, on_done=results.append))
-    time.sleep(0.8)  # admitted, now inside a stalled decode call
+    t_end = time.time() + 20  # admitted, now inside a stalled decode call (polled: a loaded host
+    while not m.scheduler.stalled(0.3) and time.time() < t_end:  # may take longer to get there)
+        time.sleep(0.02)
     monkeypatch.delenv("AIOS_FAULT_INJECT")
     recovered = _run(mgr.supervise(stall_timeout_s=0.3))
     assert results and results[0].finish_reason == "error" and "stalled" in results[0].error

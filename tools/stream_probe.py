@@ -30,6 +30,13 @@ def main():
                     if os.environ.get("STREAM_ALL"):
                         print(json.dumps(row), flush=True)
         print(json.dumps(dict(best, best=True)), flush=True)
+        # access pattern at the decode GEMV geometry (1 workgroup per CU, U = 4): grid-strided 16 B
+        # pieces vs per-CU contiguous slices vs 2 KB pieces dealt round-robin
+        for th in (512, 1024):
+            row = dict(shape=name, threads=th, strided=round(E.bench_stream_read(b, nbuf, 1, 4, th, 20), 2))
+            for mode, tag in ((1, "slices"), (2, "pieces2k")):
+                row[tag] = round(E.bench_stream_read_part(b, nbuf, mode, th, 20), 2)
+            print(json.dumps(row), flush=True)
     print(json.dumps({"launch_chain_us": round(E.bench_launch_chain(200, 256, 1, 20), 2)}))
 
 
