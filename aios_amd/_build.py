@@ -38,7 +38,7 @@ def target_path() -> Path:
 
 
 def _sources():
-    srcs = sorted((CSRC / "kernels").glob("*.hip")) + [CSRC / "engine.hip", CSRC / "grammar.cpp",
+    srcs = sorted((CSRC / "kernels").glob("*.hip")) + [CSRC / "engine.hip", CSRC / "grammar.cpp", CSRC / "rccl_comm.cpp",
                                                       CSRC / "bindings.cpp"]
     return srcs
 

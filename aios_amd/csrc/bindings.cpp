@@ -7,6 +7,7 @@
 #include <cstring>
 
 #include "comm.h"
+#include "rccl_comm.h"
 #include "engine.h"
 #include "grammar.h"
 #include "ops.h"
@@ -266,6 +267,10 @@ PYBIND11_MODULE(_engine, m) {
         e.set_allreduce(&XgmiComm::hook, &c);
         e.set_allgather(&XgmiComm::gather_hook, &c);
       })
+      .def("set_comm", [](Engine& e, RcclComm& c) {
+        e.set_allreduce(&RcclComm::hook, &c);
+        e.set_allgather(&RcclComm::gather_hook, &c);
+      })
       .def_property_readonly("vocab_parallel", &Engine::vocab_parallel);
 
   // ------------------------------------------------------------------ TP collectives (xGMI)
@@ -292,6 +297,26 @@ PYBIND11_MODULE(_engine, m) {
       .def_property_readonly("world", &XgmiComm::world)
       .def_property_readonly("capacity", &XgmiComm::capacity)
       .def_property_readonly("connected", &XgmiComm::connected);
+
+  // ------------------------------------------------------------------ TP collectives (RCCL, dlopen'd)
+  py::class_<RcclComm>(m, "RcclComm")
+      .def(py::init([](int rank, int world, int device, py::bytes id) {
+             return new RcclComm(rank, world, device, std::string(id));
+           }),
+           py::arg("rank"), py::arg("world"), py::arg("device"), py::arg("unique_id"),
+           py::call_guard<py::gil_scoped_release>())
+      .def_static("unique_id", []() { return py::bytes(RcclComm::unique_id()); })
+      .def_static("available", &RcclComm::available)
+      .def("allreduce", [](RcclComm& c, uintptr_t data, size_t n, uintptr_t residual, uintptr_t st) {
+        c.allreduce((float*)data, n, (float*)residual, S(st));
+      }, py::arg("data"), py::arg("n"), py::arg("residual") = 0, py::arg("stream") = 0)
+      .def("allgather_cols", [](RcclComm& c, uintptr_t data, int rows, int slice, int ld, uintptr_t st) {
+        c.allgather_cols((float*)data, rows, slice, ld, S(st));
+      }, py::arg("data"), py::arg("rows"), py::arg("slice"), py::arg("ld"), py::arg("stream") = 0)
+      .def("error", &RcclComm::error)
+      .def("reset_error", &RcclComm::reset_error)
+      .def_property_readonly("rank", &RcclComm::rank)
+      .def_property_readonly("world", &RcclComm::world);
 
   // ------------------------------------------------------------------ raw ops (tests / tools)
   py::class_<PyQMatrix>(m, "QMatrix")

@@ -158,6 +158,7 @@ class Engine {
   GemvArgs gemv_args(const std::vector<const QMat*>& segs, int N, int K, int B, const float* x, int ldx,
                      const float* norm_w, float* y, int ldy, int epi, int layer);
   bool attn_block_on(int B) const;
+  PfSpec attn_prefetch_spec(int l) const;  // MALL prefetch role of the batch-1 attention launch
   QMat alloc_qmat(int qt, int rows, int cols);
   QMat upload_qmat(int qt, int rows, int cols, const void* host, size_t nbytes);
   // load-time staging: two device buffers (tensor i repacks while i+1 uploads) fed through two

@@ -915,6 +915,53 @@ void Engine::layer_decode_gemm(int l, int B) {
   if (tp) allreduce(attn_, (size_t)B * d, x_);
 }
 
+// MALL prefetch carried by the batch-1 attention launch (PfSpec, ops.h): the whole O matrix and a
+// prefix of every CU slice of gate/up, read into the Infinity Cache while 224 CUs and HBM idle.
+// AIOS_PF=0 switches it off; AIOS_PF_O (0/1), AIOS_PF_GU_KB (KB per CU slice of the gate/up codes),
+// AIOS_PF_WG (prefetch workgroups), AIOS_PF_MAXLEN (keys up to which it runs).
+static int pf_knob(const char* k, int dflt) {
+  const char* e = std::getenv(k);
+  return e ? std::atoi(e) : dflt;
+}
+
+// plane bytes per 32-weight chunk of a K-quant format (the per-scale planes p3 of Q6_K skipped)
+static double plane_bpc(int qt, int p) {
+  static const double q4[4] = {16, 2, 0, 0}, q5[4] = {16, 2, 4, 0}, q6[4] = {16, 8, 2, 0};
+  return qt == QT_Q4_K ? q4[p] : (qt == QT_Q5_K ? q5[p] : (qt == QT_Q6_K ? q6[p] : 0));
+}
+
+PfSpec Engine::attn_prefetch_spec(int l) const {
+  PfSpec s{};
+  static const int on = pf_knob("AIOS_PF", 0);
+  if (!on || l >= cfg_.n_layers) return s;
+  static const int pf_o = pf_knob("AIOS_PF_O", 1);
+  static const int gu_kb = pf_knob("AIOS_PF_GU_KB", 0);
+  const LayerW& L = layers_[l];
+  auto add = [&](const QMat& m, int G, double frac_or_kb, bool whole) {
+    const QWeight& w = m.w;
+    if (!is_kquant(w.qtype) || w.cols % 32) return;
+    const int nch = w.cols / 32, np = w.rows / 2;
+    const uint8_t* planes[4] = {w.p0, w.p1, w.p2, w.p3};
+    for (int p = 0; p < 3 && s.n < PF_MAX; ++p) {
+      const double bpc = plane_bpc(w.qtype, p);
+      if (bpc <= 0 || !planes[p]) continue;
+      const uint32_t pair_bytes = (uint32_t)(2.0 * nch * bpc);
+      const int g = whole ? 1 : std::min(G, np);
+      const size_t part_min = (size_t)(np / g) * pair_bytes;
+      size_t want = whole ? part_min : (size_t)(frac_or_kb * 1024.0 * bpc / 16.0);  // KB of codes -> plane bytes
+      want = std::min(want, part_min) / 1024 * 1024;
+      if (want == 0) continue;
+      s.e[s.n++] = PfEntry{planes[p], pair_bytes, np, g, (uint32_t)want};
+    }
+  };
+  if (pf_o) add(L.wo, 1, 0, true);
+  if (gu_kb > 0) add(L.wgu, device_cu_count(), gu_kb, false);
+  s.nwg = pf_knob("AIOS_PF_WG", 224);
+  s.max_len = pf_knob("AIOS_PF_MAXLEN", 512);
+  if (s.nwg <= 0) s.n = 0;
+  return s;
+}
+
 void Engine::layer_decode(int l, int B) {
   if (dec_a16_ && ((dec_gemm_min_b_ > 0 && B >= dec_gemm_min_b_) || B > 8)) {
     layer_decode_gemm(l, B);
@@ -1039,6 +1086,7 @@ void Engine::layer_decode(int l, int B) {
     a.n_chunks = n_chunks_;
     a.scale = 1.f / std::sqrt((float)hd);
     a.o_part = opart_; a.ml = ml_; a.out = attn_; a.counters = attn_cnt_;
+    if (B == 1) a.pf = attn_prefetch_spec(l);
     launch_attn_decode(a, stream_);
   }
   // ---- O projection (+ residual; TP: partial -> all-reduce -> add)

@@ -386,6 +386,7 @@ struct AttnSplit {
   int p_long;   // workgroups per (row, head set) in the long mode
   int p_short;  // workgroups per (row, head) in the short mode
   int ppw;      // passes per workgroup the split aims for
+  int n_attn;   // attention workgroups of the flat grid (prefetch workgroups follow them)
 };
 
 
@@ -406,6 +407,7 @@ inline int attn_plan(const AttnDecodeArgs& a, int G, AttnSplit& sp) {
   if (sp.p_long > a.n_chunks || sp.p_long > 64 || sp.p_short > a.n_chunks)
     throw std::runtime_error("attn_decode: more splits than partial buffers / 64");
   const int GL = (G % 4 == 0) ? 4 : G;
+  sp.n_attn = std::max(a.n_kv_heads * (G / GL) * sp.p_long, G > 1 && a.short_len != 0 ? a.n_heads * sp.p_short : 0);
   return std::max(a.n_kv_heads * (G / GL) * sp.p_long, G > 1 && a.short_len != 0 ? a.n_heads * sp.p_short : 0);
 }
 }  // namespace aios

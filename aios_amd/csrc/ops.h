@@ -58,6 +58,27 @@ struct QkvPostArgs {
 void launch_qkv_post(const QkvPostArgs& a, hipStream_t st);
 
 // ---- attention ---------------------------------------------------------------------------------
+// Infinity-Cache (MALL) weight prefetch carried by a latency-bound launch: extra workgroups of the
+// batch-1 decode attention launch (32 busy workgroups on 256 CUs, HBM idle) read the first bytes
+// of every CU slice of the NEXT projections' weight planes with default-policy LDS-DMA loads (data
+// discarded), so the O / gate-up GEMVs that follow find them in the 256 MB die-level cache.
+// Entry: plane `base`, split the way the consuming GEMV splits it (part g of G starts at row pair
+// floor(g * np / G)); the first pf_bytes (multiple of 1 KB, <= the smallest part) of every part.
+struct PfEntry {
+  const uint8_t* base;
+  uint32_t pair_bytes;  // plane bytes per row pair
+  int np;               // row pairs
+  int G;                // parts (the consuming GEMV's workgroups)
+  uint32_t pf_bytes;    // prefix of every part to prefetch
+};
+constexpr int PF_MAX = 8;
+struct PfSpec {
+  PfEntry e[PF_MAX];
+  int n = 0;
+  int nwg = 0;       // prefetch workgroups appended to the launch
+  int max_len = 0;   // only while seq_len <= max_len (the launch's own workgroups are few)
+};
+
 struct AttnDecodeArgs {
   const float* q;          // [B][n_heads][head_dim]
   const bf16_t* k_cache;   // layer base of the paged pool [blocks][n_kv][KV_BLOCK][hd]
@@ -76,6 +97,7 @@ struct AttnDecodeArgs {
   bf16_t* out16 = nullptr; // if set: the output as bf16 instead (the batched-decode GEMM's A operand)
   int short_len = -1;      // contexts up to this many keys split by query head (-1: launcher decides)
   int* counters;           // [B][n_kv_heads] arrival tickets, zero-initialised, self re-arming
+  PfSpec pf{};             // optional MALL prefetch role (B = 1)
 };
 constexpr int ATTN_CHUNK = 64;
 void launch_attn_decode(const AttnDecodeArgs& a, hipStream_t st);

@@ -35,13 +35,28 @@ def comm_capacity(d_model: int, max_batch: int = 8, prefill_rows: int = DEFAULT_
     return max(max_batch, prefill_rows) * d_model
 
 
-def create_comm(rank: int, world: int, device: int, cap_floats: int, group=None):
-    """XgmiComm connected to every rank of `group` (default: the default process group)."""
+def comm_kind() -> str:
+    """AIOS_TP_COMM: 'xgmi' (default; the IPC one-shot / two-shot kernels, fused with the residual
+    add) or 'rccl' (librccl all-reduce / all-gather inside the same captured step; one GPU per rank)."""
+    k = os.environ.get("AIOS_TP_COMM", "xgmi").strip().lower()
+    if k not in ("xgmi", "rccl"):
+        raise ValueError(f"AIOS_TP_COMM must be 'xgmi' or 'rccl', not {k!r}")
+    return k
+
+
+def create_comm(rank: int, world: int, device: int, cap_floats: int, group=None, kind: Optional[str] = None):
+    """XgmiComm (or RcclComm, see comm_kind) connected to every rank of `group` (default: the
+    default process group)."""
     import torch.distributed as dist
 
     from ..runtime import native
 
     m = native.require()
+    if (kind or comm_kind()) == "rccl":
+        uid: List[Any] = [m.RcclComm.unique_id() if rank == 0 else None]
+        if world > 1:
+            dist.broadcast_object_list(uid, src=0, group=group)
+        return m.RcclComm(rank, world, device, uid[0])
     comm = m.XgmiComm(rank, world, device, cap_floats)
     if world > 1:
         handles: List[Any] = [None] * world
@@ -217,10 +232,15 @@ def launch_tp(spec: str, world: int, devices, max_ctx: int, max_slots: int, max_
     try:
         ch.accept_all()
         eng, cfg = _shard(spec, 0, world, devices[0], max_ctx, max_slots, max_batch, seed, act_q8)
-        comm = native.require().XgmiComm(0, world, devices[0], comm_capacity(cfg.d_model, max_batch))
-        handles = ch.gather(comm.ipc_handle())
-        ch.broadcast(handles)
-        comm.connect(handles)
+        if comm_kind() == "rccl":
+            uid = native.require().RcclComm.unique_id()
+            ch.broadcast(uid)
+            comm = native.require().RcclComm(0, world, devices[0], uid)  # collective with the workers
+        else:
+            comm = native.require().XgmiComm(0, world, devices[0], comm_capacity(cfg.d_model, max_batch))
+            handles = ch.gather(comm.ipc_handle())
+            ch.broadcast(handles)
+            comm.connect(handles)
         eng.set_comm(comm)
         ch.broadcast({"ring": ring.name})
     except Exception:

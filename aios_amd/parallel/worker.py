@@ -24,13 +24,16 @@ def main(argv=None):
 
     from ..runtime import native
     from .channel import WorkerChannel
-    from .tp import _shard, comm_capacity, worker_loop
+    from .tp import _shard, comm_capacity, comm_kind, worker_loop
 
     ch = WorkerChannel(a.leader, a.rank, os.environ.pop("AIOS_TP_TOKEN", ""))
     eng, cfg = _shard(a.spec, a.rank, a.world, a.device, a.max_ctx, a.max_slots, a.max_batch, a.seed, bool(a.q8))
-    comm = native.require().XgmiComm(a.rank, a.world, a.device, comm_capacity(cfg.d_model, a.max_batch))
-    ch.send(comm.ipc_handle())
-    comm.connect(ch.recv())
+    if comm_kind() == "rccl":  # the leader broadcasts the ncclUniqueId; the init is collective
+        comm = native.require().RcclComm(a.rank, a.world, a.device, ch.recv())
+    else:
+        comm = native.require().XgmiComm(a.rank, a.world, a.device, comm_capacity(cfg.d_model, a.max_batch))
+        ch.send(comm.ipc_handle())
+        comm.connect(ch.recv())
     eng.set_comm(comm)
     # per-step commands arrive through the leader's shared-memory ring (ring.py); the TCP channel
     # only carried the authenticated setup

@@ -193,3 +193,51 @@ def test_runtime_serves_tp_model(tmp_path):
         assert gen(m2, prompts) == ref
     finally:
         asyncio.run(mgr.unload_model("llama3-70b"))
+
+
+def test_comm_kind_selection(monkeypatch):
+    from aios_amd.parallel.tp import comm_kind
+
+    monkeypatch.delenv("AIOS_TP_COMM", raising=False)
+    assert comm_kind() == "xgmi"
+    monkeypatch.setenv("AIOS_TP_COMM", "RCCL")
+    assert comm_kind() == "rccl"
+    monkeypatch.setenv("AIOS_TP_COMM", "mpi")
+    with pytest.raises(ValueError):
+        comm_kind()
+
+
+@pytest.mark.gpu
+def test_rccl_comm_single_rank():
+    """RcclComm (librccl dlopen'd): a world-1 communicator on the box's GPU -- all-reduce is the
+    identity plus the fused residual add, the column all-gather a no-op; captured into a hipGraph
+    as the engine captures it.  (World > 1 needs one GPU per rank: RCCL refuses shared devices.)"""
+    import torch
+
+    from aios_amd.runtime import native
+
+    m = native.require()
+    assert m.RcclComm.available()
+    uid = m.RcclComm.unique_id()
+    assert isinstance(uid, bytes) and len(uid) == 128
+    comm = m.RcclComm(0, 1, 0, uid)
+    assert comm.rank == 0 and comm.world == 1 and not comm.error()
+    st = torch.cuda.current_stream()
+    data = torch.randn(4096, device="cuda")
+    res = torch.randn(4096, device="cuda")
+    want = res + data
+    comm.allreduce(data.data_ptr(), data.numel(), res.data_ptr(), st.cuda_stream)
+    torch.cuda.synchronize()
+    assert torch.allclose(res, want)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        comm.allreduce(data.data_ptr(), data.numel(), res.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    g.replay()
+    torch.cuda.synchronize()
+    assert torch.allclose(res, want + data)
+    logits = torch.randn(2, 64, device="cuda")
+    before = logits.clone()
+    comm.allgather_cols(logits.data_ptr(), 2, 64, 64, st.cuda_stream)
+    torch.cuda.synchronize()
+    assert torch.equal(logits, before)
+    assert not comm.error()

@@ -46,7 +46,7 @@ def main():
         if args.only and name not in args.only.split(","):
             continue
         nbytes = sum(BLOCK_INFO[t][1] * r * K // 256 for t, r in segs)
-        nrot = max(2, (640 << 20) // nbytes + 1)
+        nrot = int(os.environ.get("NROT", 0)) or max(2, (640 << 20) // nbytes + 1)  # NROT=1: MALL-resident weights
         mats = []
         for i in range(nrot):
             ms = []
