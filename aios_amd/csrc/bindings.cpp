@@ -300,11 +300,13 @@ PYBIND11_MODULE(_engine, m) {
 
   // ------------------------------------------------------------------ TP collectives (RCCL, dlopen'd)
   py::class_<RcclComm>(m, "RcclComm")
-      .def(py::init([](int rank, int world, int device, py::bytes id) {
-             return new RcclComm(rank, world, device, std::string(id));
+      // the id arrives as std::string (converted under the GIL); only the collective init runs
+      // without it (ncclCommInitRank blocks until every rank has joined)
+      .def(py::init([](int rank, int world, int device, const std::string& id) {
+             py::gil_scoped_release nogil;
+             return new RcclComm(rank, world, device, id);
            }),
-           py::arg("rank"), py::arg("world"), py::arg("device"), py::arg("unique_id"),
-           py::call_guard<py::gil_scoped_release>())
+           py::arg("rank"), py::arg("world"), py::arg("device"), py::arg("unique_id"))
       .def_static("unique_id", []() { return py::bytes(RcclComm::unique_id()); })
       .def_static("available", &RcclComm::available)
       .def("allreduce", [](RcclComm& c, uintptr_t data, size_t n, uintptr_t residual, uintptr_t st) {

@@ -499,8 +499,9 @@ __device__ __forceinline__ float2 wave_sum_pair(float a0, float a1) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// One wave owns a row pair; a workgroup of Q8_WAVES waves stages x once and walks row pairs
-// grid-stride.  U = 16-B chunks per lane per work item (U*64*W weights of K); host picks U so one
+// One wave owns a row pair; a workgroup of nw waves (blockDim / 64: Q8_WAVES, or at batch 1 as
+// many as make every CU's wave count equal its pair count, see launch_q8_rows) stages x once and
+// walks row pairs grid-stride.  U = 16-B chunks per lane per work item (U*64*W weights of K); host picks U so one
 // item spans all of K where it fits (the row pair's whole weight slice in flight at once).
 // PIPE = 2 double-buffers across items/pairs (short K), 1 = single buffer (large U).
 // ---------------------------------------------------------------------------------------------
@@ -523,11 +524,12 @@ __device__ __forceinline__ void q8_rows_body(const GemvArgs& a, int vblk, int vg
   constexpr bool MIXED = QT0 != QT1;
   constexpr int W = QFmt<QT0>::W, R = QFmt<QT0>::RUNS;
   const int nch = a.K / W;
-  float* red = smem;                                   // [Q8_WAVES][B]
+  float* red = smem;                                   // [nw][B] (nw * B <= 64)
   float2* ms = (float2*)(smem + 64);                   // [B][nch][R]
   int8_t* xq = (int8_t*)(ms + (size_t)B * nch * R);    // [B][nch][W]
   float2* rope_l = (float2*)(xq + (size_t)B * a.K);    // [head_dim/2] (cos, sin) at pos0 (B = 1, QKV)
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int nw = __builtin_amdgcn_readfirstlane(blockDim.x >> 6);
   const int npairs = a.N >> 1;
   // pairs [0, np0) use QT0, [np0, npairs) the last segment's QT1: one loop per format, so every
   // loop issues a fixed load sequence and the compiler's vmcnt waits stay exact
@@ -535,8 +537,8 @@ __device__ __forceinline__ void q8_rows_body(const GemvArgs& a, int vblk, int vg
   const int srow2 = __builtin_amdgcn_readfirstlane(a.seg_row0[2]);
   const int np0 = (MIXED && a.nseg > 1) ? (a.nseg == 2 ? srow1 : srow2) >> 1 : npairs;
   const int nit = (nch + 64 * U - 1) / (64 * U);
-  const int stride = vgrid * Q8_WAVES;
-  const int wid = __builtin_amdgcn_readfirstlane(vblk * Q8_WAVES + wave);  // wave-uniform -> SGPR
+  const int stride = vgrid * nw;
+  const int wid = __builtin_amdgcn_readfirstlane(vblk * nw + wave);  // wave-uniform -> SGPR
 
   auto seg_idx = [&](int p, int& lrow) -> int {
     const int row = 2 * p;
@@ -610,7 +612,7 @@ __device__ __forceinline__ void q8_rows_body(const GemvArgs& a, int vblk, int vg
       if (a.norm_w) {
         float t = 0.f;
 #pragma unroll
-        for (int w = 0; w < Q8_WAVES; ++w) t += red[w * B + b];
+        for (int w = 0; w < nw; ++w) t += red[w * B + b];
         s[b] = rsqrtf(t / (float)a.K + a.eps);
       }
     }
@@ -710,13 +712,14 @@ __device__ __forceinline__ void q8_rows_body(const GemvArgs& a, int vblk, int vg
     // Mixed formats (Q4_K q/k + Q6_K v of a Q4_K_M QKV): the waves are split in proportion to the
     // pair counts, whole workgroups per format, so both formats stream concurrently instead of a
     // Q6_K phase after the Q4_K one (which added a full memory round trip: 11.6 vs 8.3 us per QKV).
-    // W0 is a multiple of the workgroup's wave count, so every workgroup takes one branch (its
-    // barrier stays uniform); the x staging is the same for both formats (same_xlayout).
+    // The split is per WAVE: a workgroup may hold waves of both formats -- each branch runs the
+    // same x staging and exactly one workgroup barrier (s_barrier counts waves, not call sites),
+    // so when the launch gives every pair its own wave (W == npairs) W0 == np0 and no wave
+    // walks a second pair; the x staging is the same for both formats (same_xlayout).
     const int W = stride;
-    int W0 = (int)((long)W * np0 / npairs);
-    W0 = (W0 + Q8_WAVES / 2) / Q8_WAVES * Q8_WAVES;
-    W0 = max(Q8_WAVES, min(W - Q8_WAVES, W0));
-    if (W < 2 * Q8_WAVES) {  // tiny grid: the sequential schedule
+    int W0 = (int)(((long)W * np0 + npairs / 2) / npairs);
+    W0 = max(1, min(W - 1, W0));
+    if (W < 16) {  // tiny grid: the sequential schedule
       load(FmtTag<QT0>{}, wid, np0, 0, bufA);
       if (!(a.tune_dbg & 1)) q8_stage<QT0, B, NPF>(a, xq, ms, red, pf);
       __syncthreads();
@@ -742,8 +745,12 @@ __device__ __forceinline__ void q8_rows_body(const GemvArgs& a, int vblk, int vg
   if constexpr (FUSED) fuse_signal(fz, 1);
 }
 
+// up to 16 waves per workgroup for the register-light variants (U <= 2: the batch-1 QKV / O shapes)
+template <int U>
+constexpr int q8_max_threads() { return U <= 2 ? 1024 : Q8_WAVES * 64; }
+
 template <int QT0, int QT1, int B, int U, int PIPE>
-__global__ void __launch_bounds__(Q8_WAVES * 64) gemv_q8_rows(GemvArgs a) {
+__global__ void __launch_bounds__(q8_max_threads<U>()) gemv_q8_rows(GemvArgs a) {
   q8_rows_body<QT0, QT1, B, U, PIPE>(a, blockIdx.x, gridDim.x);
 }
 
@@ -766,9 +773,23 @@ void launch_q8_rows(const GemvArgs& a, size_t lds, hipStream_t st) {
   int per_cu = std::min(occ, 2);
   if (a.tune_grid > 0) per_cu = a.tune_grid;
   const int npairs = a.N / 2;
-  const int groups = (npairs + Q8_WAVES - 1) / Q8_WAVES;
-  const int blocks = std::min(groups, device_cu_count() * per_cu);
-  hipLaunchKernelGGL((gemv_q8_rows<QT0, QT1, B, U, PIPE>), dim3(blocks), dim3(Q8_WAVES * 64), lds, st, a);
+  const int cus = device_cu_count();
+  // Batch 1, one pair per wave: 8-wave workgroups leave CUs unequal whenever npairs / 8 is not a
+  // multiple of the CU count (Mistral QKV: 3072 pairs = 384 workgroups on 256 CUs -> half the CUs
+  // stream 16 pairs, half 8).  Instead size the workgroup to ceil(npairs / CUs) waves (<= 16) and
+  // launch one per CU: every CU streams the same bytes (AIOS_Q8_BALANCE=0: the 8-wave grid).
+  static const int balance = [] {
+    const char* e = std::getenv("AIOS_Q8_BALANCE");
+    return e ? std::atoi(e) : 1;
+  }();
+  int nw = Q8_WAVES;
+  if (B == 1 && balance && a.tune_grid <= 0 && q8_max_threads<U>() >= 1024) {
+    const int want = (npairs + cus - 1) / cus;
+    if (want >= 2 && want <= 16) nw = want;
+  }
+  const int groups = (npairs + nw - 1) / nw;
+  const int blocks = std::min(groups, cus * per_cu);
+  hipLaunchKernelGGL((gemv_q8_rows<QT0, QT1, B, U, PIPE>), dim3(blocks), dim3(nw * 64), lds, st, a);
 }
 
 template <int QT0, int QT1, int B>

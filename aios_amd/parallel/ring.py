@@ -34,6 +34,7 @@ _U32 = struct.Struct("<I")
 _U64 = struct.Struct("<Q")
 _I64 = struct.Struct("<q")
 _F64 = struct.Struct("<d")
+_I64_MAX = (1 << 63) - 1
 
 
 # ------------------------------------------------------------------------------------- encoding
@@ -45,7 +46,8 @@ def encode(obj: Any, out: bytearray) -> None:
     elif obj is False:
         out += b"F"
     elif isinstance(obj, int):
-        out += b"i" + _I64.pack(obj)
+        # uint64 sampling seeds exceed int64: their own tag ('u')
+        out += (b"u" + _U64.pack(obj)) if obj > _I64_MAX else (b"i" + _I64.pack(obj))
     elif isinstance(obj, float):
         out += b"f" + _F64.pack(obj)
     elif isinstance(obj, (bytes, bytearray, memoryview)):
@@ -55,7 +57,7 @@ def encode(obj: Any, out: bytearray) -> None:
         b = obj.encode()
         out += b"s" + _U32.pack(len(b)) + b
     elif isinstance(obj, (list, tuple)):
-        if obj and all(type(x) is int for x in obj):
+        if obj and all(type(x) is int and -_I64_MAX - 1 <= x <= _I64_MAX for x in obj):
             a = array("q", obj)
             out += b"I" + _U32.pack(len(a)) + a.tobytes()
         elif obj and all(type(x) is float for x in obj):
@@ -91,6 +93,8 @@ def decode(buf, pos: int = 0):
         return False, pos
     if t == b"i":
         return _I64.unpack_from(buf, pos)[0], pos + 8
+    if t == b"u":
+        return _U64.unpack_from(buf, pos)[0], pos + 8
     if t == b"f":
         return _F64.unpack_from(buf, pos)[0], pos + 8
     if t not in (b"b", b"s", b"I", b"D", b"L"):

@@ -22,6 +22,10 @@ def test_encoding_roundtrip():
                       [2**63 - 1, 5, 1]]]
     assert _rt(cmd) == cmd
     assert _rt([None, True, False, "x", [], [[1], [2.5]], b""]) == [None, True, False, "x", [], [[1], [2.5]], b""]
+    # fresh uint64 sampling seeds (above int64) as scalars and in int lists
+    big = 2**64 - 5
+    assert _rt(["sample_first", [12, 0.7, 40, 0.9, big, b""]]) == ["sample_first", [12, 0.7, 40, 0.9, big, b""]]
+    assert _rt([[big, 3, -1]]) == [[big, 3, -1]]
     with pytest.raises(TypeError):
         _rt(object())
     with pytest.raises(ValueError):
