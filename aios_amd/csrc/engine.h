@@ -239,7 +239,9 @@ class Engine {
   // (MI355X, Mistral-7B Q4_K_M, tools/gpu_batch_ab.sh: B=2 GEMV 2.41 ms vs GEMM 3.25 ms, B=4 3.31 vs 3.26,
   // B=8 5.80 vs 3.37 -- the skinny GEMM's per-step dequant floor lost below 4 rows; after the split
   // RMSNorm / mixed-QKV / split-K work, tools/gpu_minb_ab.sh: B=3 GEMV 956 vs GEMM 1065 tok/s, B=2 829 vs 712)
-  int dec_gemm_min_b_ = 3;
+  // round 3: the LDS-DMA GEMV engine serves B = 2..4 from one weight stream (gemv_lds.h):
+  // B = 2 / 3 / 4 1.82 / 2.29 / 2.45 ms vs the skinny GEMM's 3.25 / 2.83 / 2.84 (profiles/lds_batched_r3.txt)
+  int dec_gemm_min_b_ = 5;
   bf16_t *dec_a16_ = nullptr, *dec_ff16_ = nullptr;
   // split-K slabs + arrival tickets of the skinny GEMM (shared by every decode GEMM of a step)
   float* gk_ws_ = nullptr;

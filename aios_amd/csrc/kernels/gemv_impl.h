@@ -555,7 +555,7 @@ void launch_gemv_pair(const GemvArgs& a, hipStream_t st) {
   constexpr bool Q8OK = QT0 != QT_F16 && QT0 != QT_BF16;
   if constexpr (Q8OK) {
     if (!a.force_v1 && a.act_q8) {
-      if (a.B == 1 && launch_gemv_lds<QT0, QT1>(a, st)) return;
+      if (a.B <= 4 && launch_gemv_lds<QT0, QT1>(a, st)) return;  // B = 1..4: the LDS-DMA engine
       if (a.B == 1 && launch_gemv_cu<QT0, QT1>(a, st)) return;
       if (a.B == 1 && launch_gemv_q8<QT0, QT1, 1>(a, st)) return;
       if (a.B == 2 && launch_gemv_q8<QT0, QT1, 2>(a, st)) return;

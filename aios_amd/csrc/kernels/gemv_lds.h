@@ -67,7 +67,7 @@ struct LgPlanes<QT_Q8_0> {
   static constexpr int dsz[4] = {16, 16, 0, 0};
 };
 
-template <int QT>
+template <int QT, int RSUB = 0>
 struct LgLayout {
   using P = LgPlanes<QT>;
   // groups per consumer wave per step: 2 for the 4.5-bit formats (the pair shares one row sum and
@@ -86,8 +86,9 @@ struct LgLayout {
   static constexpr int per_loader = (total_inst + LG_NL - 1) / LG_NL;
   // ring slots: R - 1 slots in flight must cover HBM latency x the CU's share of the bandwidth
   // (~2-3 us x 24 GB/s under full load): 3 x 32 KB for the 4.5-bit formats, 4 x 24 KB for Q6_K
-  static constexpr int R = slot_bytes > 28 * 1024 ? 4 : (slot_bytes <= 20 * 1024 ? 6 : 5);
-  static_assert((R - 2) * per_loader <= 63, "vmcnt immediate");
+  // (RSUB: one slot fewer for the batched launches, whose B staged x vectors take the LDS)
+  static constexpr int R = (slot_bytes > 28 * 1024 ? 4 : (slot_bytes <= 20 * 1024 ? 6 : 5)) - RSUB;
+  static_assert(R >= 2 && (R - 2) * per_loader <= 63, "ring depth / vmcnt immediate");
 };
 
 __device__ __forceinline__ const uint8_t* lg_plane_ptr(const QWeight& w, int p) {
@@ -122,7 +123,7 @@ __device__ __forceinline__ void lg_vmcnt() {
 template <int QT>
 __device__ __forceinline__ void lg_dma_slot(const GemvArgs& a, uint8_t* dst, int s, int lw, int r0, int nit,
                                             int ngroups) {
-  using L = LgLayout<QT>;
+  using L = LgLayout<QT>;  // (slot geometry only: identical for every RSUB)
   using P = LgPlanes<QT>;
   constexpr int NGS = L::NGS;
   const int lane = threadIdx.x & 63;
@@ -215,7 +216,76 @@ __device__ __forceinline__ void lg_read(const uint8_t* slot, int k, int lane, Ra
   }
 }
 
-template <int QT0, int QT1>
+// ---- batched consumers (B = 2..4 rows of x, one weight read): the weight decode is shared, the
+// integer dot products and the float scaling run per row
+template <int B>
+__device__ __forceinline__ void q4p_dot_b(const uint4& a0, const uint4& a1, const uint4& mt, int g,
+                                          const Q4PairX (&X)[B], float (&out)[B]) {
+  const float d = __half2float(__ushort_as_half((uint16_t)(mt.x & 0xffff)));
+  const float dmin = __half2float(__ushort_as_half((uint16_t)(mt.x >> 16)));
+  const uint32_t f = kq_field(mt.y, mt.z, mt.w, g);
+  int s0[B], s1[B];
+#pragma unroll
+  for (int b = 0; b < B; ++b) s0[b] = s1[b] = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const uint32_t w = u4_word(i < 4 ? a0 : a1, i & 3);
+    const int lo = (int)(w & 0x0f0f0f0fu), hi = (int)((w >> 4) & 0x0f0f0f0fu);
+#pragma unroll
+    for (int b = 0; b < B; ++b) {
+      s0[b] = __builtin_amdgcn_sdot4(lo, X[b].x0[i], s0[b], false);
+      s1[b] = __builtin_amdgcn_sdot4(hi, X[b].x1[i], s1[b], false);
+    }
+  }
+  const float c0 = (float)(f & 63), c1 = (float)((f >> 6) & 63);
+  const float m0 = (float)((f >> 12) & 63), m1 = (float)((f >> 18) & 63);
+#pragma unroll
+  for (int b = 0; b < B; ++b)
+    out[b] = d * (c0 * X[b].dx0 * (float)s0[b] + c1 * X[b].dx1 * (float)s1[b]) - dmin * (m0 * X[b].sx0 + m1 * X[b].sx1);
+}
+
+// one 64-chunk group of a row against B staged x rows (x read from LDS)
+template <int QT, int B>
+__device__ __forceinline__ void lg_compute_b(const RawChunk& raw, int it, int nch, const int8_t* xq, const float2* ms,
+                                             float (&acc)[B]) {
+  using F_ = QFmt<QT>;
+  constexpr int W = F_::W, R = F_::RUNS;
+  const int lane = threadIdx.x & 63;
+  const int c0 = it * 64 + lane;
+  const bool valid = c0 < nch;
+  const int c = valid ? c0 : nch - 1;
+  float sc[R], of[R];
+  q8_scales_bf<QT>(raw, c, sc, of);
+#pragma unroll
+  for (int b = 0; b < B; ++b) {
+    int xv[8];
+    const int8_t* xc = xq + ((size_t)b * nch + c) * W;
+    if constexpr (W == 32) {
+      const int rot = (c >> 3) & 1;
+      const uint4 p0 = *(const uint4*)(xc + 16 * rot);
+      const uint4 p1 = *(const uint4*)(xc + 16 * (rot ^ 1));
+      xv[0] = p0.x; xv[1] = p0.y; xv[2] = p0.z; xv[3] = p0.w;
+      xv[4] = p1.x; xv[5] = p1.y; xv[6] = p1.z; xv[7] = p1.w;
+    } else {
+      const uint4 p0 = *(const uint4*)xc;
+      xv[0] = p0.x; xv[1] = p0.y; xv[2] = p0.z; xv[3] = p0.w;
+      xv[4] = xv[5] = xv[6] = xv[7] = 0;
+    }
+    int is[R];
+    QDot<QT>::isums(raw, c, xv, is);
+#pragma unroll
+    for (int rr = 0; rr < R; ++rr) {
+      float2 m = ms[((size_t)b * nch + c) * R + rr];
+      if (!valid) m = make_float2(0.f, 0.f);
+      acc[b] += sc[rr] * m.x * (float)is[rr] - of[rr] * m.y;
+    }
+  }
+}
+
+// B = 1: the batch-1 decode engine; B = 2..4 (RSUB = 1: one ring slot fewer, the B staged x rows
+// take its LDS): the same weight stream serves B rows -- the small-batch decode of the agent OS
+// (<= 3 concurrent reasoning loops + agents) at close to the batch-1 step time
+template <int QT0, int QT1, int B = 1, int RSUB = 0>
 __global__ void __launch_bounds__(LG_THREADS) gemv_lds_b1(GemvArgs a, CuPlan pl) {
   static_assert(same_xlayout<QT0, QT1>, "mixed segments must share the activation layout");
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -247,16 +317,16 @@ __global__ void __launch_bounds__(LG_THREADS) gemv_lds_b1(GemvArgs a, CuPlan pl)
   const int r0 = 2 * pb, nrows = 2 * (pe - pb);
   const int ngroups = nrows * nit;
 
-  // ---- LDS: red[64] | rowacc[racc_n] | ms [nch][R] | xq [nch][W] | ring [LG_R][slot]
+  // ---- LDS: red[64] | rowacc[B][racc_n] | ms [B][nch][R] | xq [B][nch][W] | ring [LG_R][slot]
   float* red = smem;
   float* rowacc = smem + 64;
-  float2* ms = (float2*)(rowacc + pl.racc_n);
-  int8_t* xq = (int8_t*)(ms + (size_t)nch * R);
+  float2* ms = (float2*)(rowacc + B * pl.racc_n);
+  int8_t* xq = (int8_t*)(ms + (size_t)B * nch * R);
   // (offset arithmetic on the __shared__ base: a pointer cast through uintptr_t loses the LDS
   // address space and every ring read became a flat load waited with vmcnt)
-  const int ring_off = (int)(((const uint8_t*)(xq + a.K) - (const uint8_t*)smem + 255) & ~255);
+  const int ring_off = (int)(((const uint8_t*)(xq + (size_t)B * a.K) - (const uint8_t*)smem + 255) & ~255);
   uint8_t* ring = (uint8_t*)smem + ring_off;
-  for (int i = threadIdx.x; i < nrows; i += LG_THREADS) rowacc[i] = 0.f;
+  for (int i = threadIdx.x; i < B * pl.racc_n; i += LG_THREADS) rowacc[i] = 0.f;
   if (threadIdx.x < 64) red[threadIdx.x] = 0.f;
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // ordered before B0
 
@@ -265,7 +335,7 @@ __global__ void __launch_bounds__(LG_THREADS) gemv_lds_b1(GemvArgs a, CuPlan pl)
   // holding the loaders back).  Both execute the same T + 3 barriers.
   auto loader_path = [&](auto tag) __attribute__((always_inline)) {
     constexpr int QT = decltype(tag)::value;
-    using L = LgLayout<QT>;
+    using L = LgLayout<QT, RSUB>;
     constexpr int PL = L::per_loader;
     constexpr int LG_R = L::R;
     const int T = (ngroups + L::NGS - 1) / L::NGS;
@@ -293,7 +363,7 @@ __global__ void __launch_bounds__(LG_THREADS) gemv_lds_b1(GemvArgs a, CuPlan pl)
   };
   auto consumer_path = [&](auto tag, float2& rope) __attribute__((always_inline)) {
     constexpr int QT = decltype(tag)::value;
-    using L = LgLayout<QT>;
+    using L = LgLayout<QT, RSUB>;
     constexpr int LG_R = L::R;
     constexpr int GPW = L::GPW;
     const int T = (ngroups + L::NGS - 1) / L::NGS;
@@ -302,10 +372,10 @@ __global__ void __launch_bounds__(LG_THREADS) gemv_lds_b1(GemvArgs a, CuPlan pl)
     q8_stage_prefetch(a, pf, threadIdx.x, LG_NG * 64);
     if (LG_B0) lg_barrier();  // B0
     CU_STAMP(1);
-    q8_stage<QT0, 1, NPF>(a, xq, ms, red, pf, threadIdx.x, LG_NG * 64);
+    q8_stage<QT0, B, NPF>(a, xq, ms, red, pf, threadIdx.x, LG_NG * 64);
     // RoPE (cos, sin) of the epilogue lane's pair: issued now, waited for in the epilogue (the
     // consumers issue no other global load until then)
-    if (a.epi == EPI_QKV && wave == 0 && a.rope_cs) {
+    if (B == 1 && a.epi == EPI_QKV && wave == 0 && a.rope_cs) {
       const int pos0 = a.pos[0];
       int part, head, lrr;
       qkv_part(a, a.row_base + r0 + 2 * lane, part, head, lrr);
@@ -315,6 +385,72 @@ __global__ void __launch_bounds__(LG_THREADS) gemv_lds_b1(GemvArgs a, CuPlan pl)
     CU_STAMP(2);
     lg_barrier();  // B1
     CU_STAMP(3);
+    if constexpr (B > 1) {
+      if constexpr (QT == QT_Q4_K) {
+        if (L::NGS % nit == 0) {
+          // chunk pairs with B x-operand sets in registers (as the B = 1 path below)
+          const int half = lane >> 5, p = lane & 31;
+          const int kk = wave * GPW + half;
+          Q4PairX X[B];
+#pragma unroll
+          for (int b = 0; b < B; ++b) q4p_load_x(xq + (size_t)b * a.K, ms + (size_t)b * nch * R, (kk % nit) * 64 + 2 * p, X[b]);
+          const int rps = L::NGS / nit, rk = kk / nit;
+          for (int t = 0; t < T; ++t) {
+            if (t * L::NGS + wave * GPW < ngroups) {
+              const uint8_t* slot = ring + (size_t)(t % LG_R) * L::slot_bytes;
+              const uint4 a0 = *(const uint4*)(slot + L::off(0) + kk * 1024 + p * 32);
+              const uint4 a1 = *(const uint4*)(slot + L::off(0) + kk * 1024 + p * 32 + 16);
+              const uint4 mt = *(const uint4*)(slot + L::off(1) + kk * 128 + (p >> 2) * 16);
+              const bool ok = t * L::NGS + kk < ngroups;
+              float v[B];
+              q4p_dot_b<B>(a0, a1, mt, p & 3, X, v);
+#pragma unroll
+              for (int b = 0; b < B; ++b) {
+                const float r = cu_half_sum(ok ? v[b] : 0.f);
+                if (p == 0 && ok)
+                  __hip_atomic_fetch_add(&rowacc[b * pl.racc_n + t * rps + rk], r, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_WORKGROUP);
+              }
+            }
+            lg_barrier();
+          }
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          lg_barrier();  // final
+          return;
+        }
+      }
+      for (int t = 0; t < T; ++t) {
+        const int gb = t * L::NGS + wave * GPW;
+        if (gb < ngroups) {
+          const uint8_t* slot = ring + (size_t)(t % LG_R) * L::slot_bytes;
+          RawChunk raw[GPW];
+          static_for<GPW>([&](auto j) { lg_read<QT>(slot, wave * GPW + j, lane, raw[j]); });
+          int row = gb / nit, it = gb - row * nit;
+          float acc[B];
+#pragma unroll
+          for (int b = 0; b < B; ++b) acc[b] = 0.f;
+          static_for<GPW>([&](auto j) {
+            const int gg = gb + j;
+            if (gg < ngroups) {
+              lg_compute_b<QT, B>(raw[j], it, nch, xq, ms, acc);
+              if (it == nit - 1 || j == GPW - 1 || gg == ngroups - 1) {
+#pragma unroll
+                for (int b = 0; b < B; ++b) {
+                  const float v = cu_wave_sum(acc[b]);
+                  if (lane == 0) atomicAdd(&rowacc[b * pl.racc_n + row], v);
+                  acc[b] = 0.f;
+                }
+              }
+            }
+            if (++it == nit) { it = 0; ++row; }
+          });
+        }
+        lg_barrier();
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      lg_barrier();  // final
+      return;
+    }
     if constexpr (QT == QT_Q4_K) {
       if (L::NGS % nit == 0) {
         // chunk pairs, x in registers (gemv_cu.h Q4PairX): lanes 0-31 take group 2w's 32 pairs,
@@ -422,6 +558,31 @@ __global__ void __launch_bounds__(LG_THREADS) gemv_lds_b1(GemvArgs a, CuPlan pl)
     return;
   }
 
+  if constexpr (B > 1) {
+    // ---- batched epilogues: wave 0, one lane per (row b, pair)
+    float sb[B];
+#pragma unroll
+    for (int b = 0; b < B; ++b) {
+      sb[b] = 1.f;
+      if (a.norm_w) {
+        float t = 0.f;
+#pragma unroll
+        for (int w = 0; w < LG_NG; ++w) t += red[w * B + b];
+        sb[b] = rsqrtf(t / (float)a.K + a.eps);
+      }
+    }
+    const int npl = nrows >> 1;
+    for (int i = lane; i < a.B * npl; i += 64) {
+      const int b = i / npl, p = i - b * npl;
+      float s_ = sb[0];
+#pragma unroll
+      for (int bb = 1; bb < B; ++bb)
+        if (b == bb) s_ = sb[bb];
+      gemv_epilogue(a, a.row_base + r0 + 2 * p, b, rowacc[b * pl.racc_n + 2 * p] * s_,
+                    rowacc[b * pl.racc_n + 2 * p + 1] * s_);
+    }
+    return;
+  }
   // ---- pair epilogues: wave 0, one lane per pair
   float s = 1.f;
   if (a.norm_w) {
@@ -467,6 +628,16 @@ constexpr bool lg_supported() {
 }
 
 // returns false when the shape does not fit (then the register kernels run)
+template <int QT0, int QT1, int B, int RSUB>
+size_t lg_lds_bytes(const GemvArgs& a, const CuPlan& pl) {
+  constexpr int W = QFmt<QT0>::W, R = QFmt<QT0>::RUNS;
+  const int nch = a.K / W;
+  const size_t head = (64 + (size_t)B * pl.racc_n) * 4 + (size_t)B * nch * R * 8 + (size_t)B * a.K;
+  const size_t ringb = std::max(LgLayout<QT0, RSUB>::R * LgLayout<QT0, RSUB>::slot_bytes,
+                                LgLayout<QT1, RSUB>::R * LgLayout<QT1, RSUB>::slot_bytes);
+  return (head + 255) / 256 * 256 + ringb;
+}
+
 template <int QT0, int QT1>
 bool launch_gemv_lds(const GemvArgs& a, hipStream_t st) {
   if constexpr (!same_xlayout<QT0, QT1> || !lg_supported<QT0>() || !lg_supported<QT1>()) {
@@ -477,7 +648,14 @@ bool launch_gemv_lds(const GemvArgs& a, hipStream_t st) {
       const char* e = std::getenv("AIOS_GEMV_LDS");
       return e ? std::atoi(e) : 1;
     }();
-    if (!mode || a.B != 1 || a.tune_dbg || (a.kernel_sel != 0 && a.kernel_sel != 3)) return false;
+    // AIOS_GEMV_LDS_MAXB: batch rows the engine serves (1..4, default 4; B = 3 runs the 4-row kernel
+    // with one idle row; whether B = 3 / 4 decode takes this path or the skinny MFMA GEMM is the
+    // engine's dec_gemm_min_b_, profiles/lds_batched_r3.txt)
+    static const int maxb = [] {
+      const char* e = std::getenv("AIOS_GEMV_LDS_MAXB");
+      return e ? std::max(1, std::min(4, std::atoi(e))) : 4;
+    }();
+    if (!mode || a.B < 1 || a.B > (a.kernel_sel == 3 ? 4 : maxb) || a.tune_dbg || (a.kernel_sel != 0 && a.kernel_sel != 3)) return false;
     constexpr int W = QFmt<QT0>::W, R = QFmt<QT0>::RUNS;
     const int nch = a.K / W;
     if (nch % 64) return false;
@@ -499,17 +677,37 @@ bool launch_gemv_lds(const GemvArgs& a, hipStream_t st) {
     // barrier steps cost more than the row kernel's x-staging stall there (tools/gemv_cu_probe.py:
     // O 6.96 vs 5.60 us, QKV 8.73 vs 8.38; gate_up 17.35 vs 19.39, down 13.8 vs 15.2, lm_head 24.8
     // vs 25.9).  AIOS_GEMV_LDS=2 forces the engine for every shape.
-    if (mode != 2 && a.kernel_sel != 3) {
+    // batched launches (B >= 2) take the engine for every shape: the row-pair kernels re-read the
+    // B x vectors per wave and measured 2-3x slower there (B = 2 QKV 26 us vs 9.6 at B = 1)
+    if (mode != 2 && a.kernel_sel != 3 && a.B == 1) {
+      // AIOS_GEMV_LDS_MIN_KB: per-CU weight bytes from which the engine serves a shape (default 96)
+      static const double min_kb = [] {
+        const char* e = std::getenv("AIOS_GEMV_LDS_MIN_KB");
+        return e ? std::atof(e) : 96.0;
+      }();
       double bytes = 0;
       for (int sg = 0; sg < a.nseg; ++sg)
         bytes += (double)a.seg[sg].rows * a.K / 256.0 * cu_fmt_bytes_per_256(a.seg[sg].qtype);
-      if (bytes / G < 96.0 * 1024) return false;
+      if (bytes / G < min_kb * 1024) return false;
     }
-    const size_t head = (64 + (size_t)pl.racc_n) * 4 + (size_t)nch * R * 8 + (size_t)a.K;
-    const size_t ringb = std::max(LgLayout<QT0>::R * LgLayout<QT0>::slot_bytes, LgLayout<QT1>::R * LgLayout<QT1>::slot_bytes);
-    const size_t lds = (head + 255) / 256 * 256 + ringb;
-    if (lds > 160 * 1024) return false;
-    hipLaunchKernelGGL((gemv_lds_b1<QT0, QT1>), dim3(G), dim3(LG_THREADS), lds, st, a, pl);
+    constexpr size_t LDS_MAX = 160 * 1024;
+    size_t lds = 0;
+    if (a.B == 1) {
+      lds = lg_lds_bytes<QT0, QT1, 1, 0>(a, pl);
+      if (lds > LDS_MAX) return false;
+      hipLaunchKernelGGL((gemv_lds_b1<QT0, QT1, 1, 0>), dim3(G), dim3(LG_THREADS), lds, st, a, pl);
+    } else if (a.B == 2) {
+      lds = lg_lds_bytes<QT0, QT1, 2, 1>(a, pl);
+      if (lds > LDS_MAX) return false;
+      hipLaunchKernelGGL((gemv_lds_b1<QT0, QT1, 2, 1>), dim3(G), dim3(LG_THREADS), lds, st, a, pl);
+    } else if ((lds = lg_lds_bytes<QT0, QT1, 4, 1>(a, pl)) <= LDS_MAX) {
+      hipLaunchKernelGGL((gemv_lds_b1<QT0, QT1, 4, 1>), dim3(G), dim3(LG_THREADS), lds, st, a, pl);
+    } else {
+      // long K (the d_ff-wide down projection): four staged x rows leave room for a shallower ring
+      lds = lg_lds_bytes<QT0, QT1, 4, 2>(a, pl);
+      if (lds > LDS_MAX) return false;
+      hipLaunchKernelGGL((gemv_lds_b1<QT0, QT1, 4, 2>), dim3(G), dim3(LG_THREADS), lds, st, a, pl);
+    }
     return true;
   }
 }

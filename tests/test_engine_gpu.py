@@ -199,6 +199,30 @@ def test_batched_decode_gemm_path_matches_gemv_path(model_files, monkeypatch, B,
     assert np.abs(l0 - l1).max() < 2e-2 * scale
 
 
+@pytest.mark.parametrize("B", [2, 3, 4])
+def test_batched_int8_gemv_engine_matches_single_rows(model_files, monkeypatch, B):
+    """B = 2..4 on the int8-activation path: every projection through the LDS-DMA GEMV engine
+    serving the B rows from ONE weight stream (kernels/gemv_lds.h, B-row consumers); each row's
+    logits must equal that sequence decoded alone (B = 1 engine) up to fp32 summation order."""
+    monkeypatch.setenv("AIOS_DECODE_GEMM_MIN_B", "0")
+    path = model_files["Q4_K_M"]
+    prompts = [[1, 5, 6, 7], [1, 9, 10, 11, 12, 13], [1, 100, 200], [1, 3, 4]][:B]
+    eng, cfg = _load(path, max_slots=4, max_batch=4, act_q8=True)
+    firsts = [int(np.argmax(eng.prefill(s, p, 0, True))) for s, p in enumerate(prompts)]
+    toks = eng.decode(list(range(B)), firsts, [len(p) for p in prompts])
+    batched = np.asarray(eng.last_logits(B)).reshape(B, -1)
+    del eng
+    for b in range(B):
+        e1, _ = _load(path, max_slots=4, max_batch=4, act_q8=True)
+        f = int(np.argmax(e1.prefill(0, prompts[b], 0, True)))
+        assert f == firsts[b]
+        t1 = e1.decode([0], [f], [len(prompts[b])])
+        single = np.asarray(e1.last_logits(1)).reshape(-1)
+        del e1
+        assert t1[0] == toks[b]
+        assert np.abs(single - batched[b]).max() < 2e-3 * max(np.abs(single).max(), 1.0)
+
+
 @pytest.mark.parametrize("recipe,rb,split", [("Q4_K_M", "0", "0"), ("Q4_K_M", "4", "1"),
                                              ("mistral_shape", "0", "1"), ("mistral_shape", "4", "0")])
 def test_batched_decode_split_rmsnorm_matches_explicit(model_files, monkeypatch, recipe, rb, split):

@@ -685,3 +685,106 @@ def test_gemm_big_tiles_match(E, M, N, K, t):
     torch.cuda.synchronize()
     ref = A.float() @ W.to(torch.bfloat16).float().cuda().T
     assert torch.allclose(C, ref, atol=3e-3, rtol=3e-3), (C - ref).abs().max()
+
+
+@pytest.mark.parametrize("t", [GGMLType.Q4_K, GGMLType.Q6_K, GGMLType.Q8_0])
+@pytest.mark.parametrize("M,ksplit", [(2, 1), (8, 3), (32, 1), (64, 4), (512, 0)])
+def test_gemm_error_vs_unquantized_product(E, t, M, ksplit):
+    """The MFMA paths (skinny GEMM for M <= 64: batched decode / short prefill; the dequant-fused
+    big GEMM beyond: prefill) against the UNQUANTIZED fp32 product -- exact dequantised weights x
+    the fp32 activations before their bf16 rounding -- not against an oracle that rounds W to bf16
+    as the kernel does: the bf16 operand rounding (weights and activations, 8 significant bits)
+    costs < 0.6 % relative L2 error of the outputs, fp32 accumulation over K = 4096 nothing
+    measurable on top."""
+    N, K = 256, 4096
+    m, W = qmat(E, t, N, K, seed=71, std=0.02)
+    x = torch.randn(M, K)
+    A = x.to(torch.bfloat16).cuda()
+    C = torch.zeros(M, N, device="cuda")
+    E.gemm_q(A.data_ptr(), K, [m], M, C.data_ptr(), 0, N, E.GEPI_STORE, stream(), ksplit)
+    torch.cuda.synchronize()
+    ref = x.double() @ W.double().T
+    rel = float((C.cpu().double() - ref).norm() / ref.norm())
+    assert rel < 6e-3, rel
+    # the same bound row by row: no batch row (M position) is treated differently
+    per_row = ((C.cpu().double() - ref).norm(dim=1) / ref.norm(dim=1)).max().item()
+    assert per_row < 1e-2, per_row
+
+
+# ---- the LDS-DMA engine serving B = 2..4 rows from one weight stream (small-batch decode) --------
+@pytest.mark.parametrize("t", [GGMLType.Q4_K, GGMLType.Q6_K, GGMLType.Q5_K, GGMLType.Q8_0])
+@pytest.mark.parametrize("K", [4096, 14336])
+@pytest.mark.parametrize("B", [2, 3, 4])
+@pytest.mark.parametrize("grid", [0, 37])
+def test_gemv_lds_batched_store(E, t, K, B, grid):
+    N = 1030
+    m, W = qmat(E, t, N, K, seed=41, std=0.02)
+    x = torch.randn(B, K, device="cuda")
+    x[1] *= 4.0  # rows with different norms / scales
+    nw = torch.rand(K, device="cuda") + 0.5
+    y = torch.full((B, N), 7.0, device="cuda")
+    E.gemv([m], B, x.data_ptr(), K, nw.data_ptr(), 1e-5, y.data_ptr(), N, E.EPI_STORE, stream(), 0, 1, grid,
+           kernel_sel=3)
+    torch.cuda.synchronize()
+    xc = x.cpu()
+    xn = q8_ref(xc * nw.cpu()) * torch.rsqrt((xc * xc).mean(-1, keepdim=True) + 1e-5)
+    ref = xn @ W.T
+    assert torch.allclose(y.cpu(), ref, atol=5e-3, rtol=5e-3), (y.cpu() - ref).abs().max()
+
+
+@pytest.mark.parametrize("B", [2, 3, 4])
+@pytest.mark.parametrize("grid", [0, 11])
+def test_gemv_lds_batched_swiglu_resid(E, B, grid):
+    K, F = 4096, 600
+    gu, Wgu = qmat(E, GGMLType.Q4_K, 2 * F, K, seed=42, std=0.02)
+    x = torch.randn(B, K, device="cuda") * 3
+    nw = torch.rand(K, device="cuda") + 0.5
+    out = torch.zeros(B, F, device="cuda")
+    E.gemv([gu], B, x.data_ptr(), K, nw.data_ptr(), 1e-5, out.data_ptr(), F, E.EPI_SWIGLU, stream(), 0, 1, grid,
+           kernel_sel=3)
+    torch.cuda.synchronize()
+    xc = x.cpu()
+    xn = q8_ref(xc * nw.cpu()) * torch.rsqrt((xc * xc).mean(-1, keepdim=True) + 1e-5)
+    h = xn @ Wgu.T
+    ref = torch.nn.functional.silu(h[:, 0::2]) * h[:, 1::2]
+    assert torch.allclose(out.cpu(), ref, atol=5e-3, rtol=5e-3), (out.cpu() - ref).abs().max()
+    y0 = torch.randn(B, 2 * F, device="cuda")
+    y = y0.clone()
+    E.gemv([gu], B, x.data_ptr(), K, 0, 1e-5, y.data_ptr(), 2 * F, E.EPI_RESID, stream(), 0, 1, grid, kernel_sel=3)
+    torch.cuda.synchronize()
+    ref = y0.cpu() + q8_ref(xc) @ Wgu.T
+    assert torch.allclose(y.cpu(), ref, atol=5e-3, rtol=5e-3), (y.cpu() - ref).abs().max()
+
+
+@pytest.mark.parametrize("mixed", [False, True])
+@pytest.mark.parametrize("B", [2, 4])
+def test_gemv_lds_batched_qkv(E, mixed, B):
+    d, H, Hkv, hd, max_ctx, slots = 2048, 8, 2, 64, 256, 4
+    wq, Wq = qmat(E, GGMLType.Q4_K, H * hd, d, seed=44)
+    wk, Wk = qmat(E, GGMLType.Q4_K, Hkv * hd, d, seed=45)
+    wv, Wv = qmat(E, GGMLType.Q6_K if mixed else GGMLType.Q4_K, Hkv * hd, d, seed=46)
+    x = torch.randn(B, d, device="cuda")
+    nw = torch.rand(d, device="cuda") + 0.5
+    pos = torch.tensor([141, 17, 200, 3][:B], dtype=torch.int32, device="cuda")
+    slot = torch.tensor([1, 0, 3, 2][:B], dtype=torch.int32, device="cuda")
+    kp, bt = paged_cache(torch.zeros(slots, Hkv, max_ctx, hd, dtype=torch.bfloat16), shuffle=True, seed=6)
+    kp, bt = kp.cuda(), bt.cuda()
+    vp = torch.zeros_like(kp)
+    q = torch.zeros(B, H * hd, device="cuda")
+    E.gemv_qkv([wq, wk, wv], B, x.data_ptr(), d, nw.data_ptr(), 1e-5, q.data_ptr(), 0, hd, H, Hkv, max_ctx, 0,
+               10000.0, pos.data_ptr(), slot.data_ptr(), kp.data_ptr(), vp.data_ptr(), stream(), 1,
+               block_table=bt.data_ptr(), kernel_sel=3)
+    torch.cuda.synchronize()
+    kc, vc = unpaged(kp, slots, max_ctx, bt), unpaged(vp, slots, max_ctx, bt)
+    xc = x.cpu()
+    xn = q8_ref(xc * nw.cpu()) * torch.rsqrt((xc * xc).mean(-1, keepdim=True) + 1e-5)
+    for b in range(B):
+        pb = pos[b:b + 1].cpu()
+        qr = rope_ref((xn[b:b + 1] @ Wq.T).view(1, H, hd), pb, 10000.0)
+        kr = rope_ref((xn[b:b + 1] @ Wk.T).view(1, Hkv, hd), pb, 10000.0)
+        vr = (xn[b:b + 1] @ Wv.T).view(1, Hkv, hd)
+        assert torch.allclose(q[b].cpu().view(1, H, hd), qr, atol=3e-3, rtol=3e-3)
+        s, p = int(slot[b]), int(pos[b])
+        assert torch.allclose(kc[s, :, p].float().cpu(), kr[0], atol=2e-2, rtol=1e-2)
+        assert torch.allclose(vc[s, :, p].float().cpu(), vr[0], atol=2e-2, rtol=1e-2)
+    assert int((kc != 0).sum()) == B * Hkv * hd and int((vc != 0).sum()) == B * Hkv * hd
