@@ -27,6 +27,9 @@
 constexpr int LG_NG = 14;               // consumer waves
 constexpr int LG_NL = 2;                // loader waves
 constexpr int LG_THREADS = (LG_NG + LG_NL) * 64;
+// tune_dbg bit (probes only): the consumers skip the slot reads and the dot work -- the bare
+// DMA ring + barrier cadence of the engine (tools/gemv_cu_probe.py 'ring' column)
+constexpr int LG_DBG_RING = 0x10000;
 // B0 (x loads queued ahead of the first weight DMA): measured slower -- the loaders' first slots
 // then start ~1.6 us late while x is an L2/MALL hit either way
 #ifndef LG_B0
@@ -463,6 +466,7 @@ __global__ void __launch_bounds__(LG_THREADS) gemv_lds_b1(GemvArgs a, CuPlan pl)
         for (int t = 0; t < T; ++t) {
           if (t * L::NGS + wave * GPW < ngroups) {
             const uint8_t* slot = ring + (size_t)(t % LG_R) * L::slot_bytes;
+            if (a.tune_dbg & LG_DBG_RING) { lg_barrier(); continue; }
             const uint4 a0 = *(const uint4*)(slot + L::off(0) + kk * 1024 + p * 32);
             const uint4 a1 = *(const uint4*)(slot + L::off(0) + kk * 1024 + p * 32 + 16);
             const uint4 mt = *(const uint4*)(slot + L::off(1) + kk * 128 + (p >> 2) * 16);
@@ -655,7 +659,10 @@ bool launch_gemv_lds(const GemvArgs& a, hipStream_t st) {
       const char* e = std::getenv("AIOS_GEMV_LDS_MAXB");
       return e ? std::max(1, std::min(4, std::atoi(e))) : 4;
     }();
-    if (!mode || a.B < 1 || a.B > (a.kernel_sel == 3 ? 4 : maxb) || a.tune_dbg || (a.kernel_sel != 0 && a.kernel_sel != 3)) return false;
+    // (tune_dbg LG_DBG_RING: the probe's ring-only mode; every other microbenchmark bit -> row kernels)
+    if (!mode || a.B < 1 || a.B > (a.kernel_sel == 3 ? 4 : maxb) || (a.tune_dbg & ~LG_DBG_RING) ||
+        (a.kernel_sel != 0 && a.kernel_sel != 3))
+      return false;
     constexpr int W = QFmt<QT0>::W, R = QFmt<QT0>::RUNS;
     const int nch = a.K / W;
     if (nch % 64) return false;

@@ -64,18 +64,21 @@ def main():
 
         def launch(ms, sel, ts=0):
             st = torch.cuda.current_stream().cuda_stream
+            # sel 4: the LDS engine with its consumers skipping the dot work (bare ring cadence)
             E.gemv(ms, 1, x.data_ptr(), K, nw.data_ptr() if norm else 0, 1e-5, y.data_ptr(), ldy, epic, st, 0, 1,
-                   kernel_sel=sel, dbg_ts=ts)
+                   kernel_sel=3 if sel == 4 else sel, tune_dbg=0x10000 if sel == 4 else 0, dbg_ts=ts)
 
         row = dict(shape=name, mb=round(nbytes / 1e6, 1))
-        for sel, tag in ((1, "rows"), (2, "cu"), (3, "lds"), (0, "auto")):
+        for sel, tag in ((1, "rows"), (2, "cu"), (3, "lds"), (4, "ring"), (0, "auto")):
             for ms in mats:
                 launch(ms, sel)
             torch.cuda.synchronize()
             g = torch.cuda.CUDAGraph()
+            nrep = int(os.environ.get("NREP", 1))  # > 1 with a small NROT: Infinity-Cache-resident weights
             with torch.cuda.graph(g):
-                for ms in mats:
-                    launch(ms, sel)
+                for _ in range(nrep):
+                    for ms in mats:
+                        launch(ms, sel)
             g.replay()
             torch.cuda.synchronize()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -85,7 +88,7 @@ def main():
                 g.replay()
             e1.record()
             torch.cuda.synchronize()
-            us = e0.elapsed_time(e1) * 1e3 / (reps * nrot)
+            us = e0.elapsed_time(e1) * 1e3 / (reps * nrot * nrep)
             row[tag + "_us"] = round(us, 2)
             row[tag + "_tbs"] = round(nbytes / us / 1e6, 2)
         row["floor_us"] = round(E.bench_stream_read(nbytes // 4096 * 4096, nrot, 1, 4, 512, 20), 2)
