@@ -237,7 +237,7 @@ def main():
                 "activations": ("int8 per-32-block activations with fp32 scales in the quantised GEMVs "
                                 "(q8_1 as llama.cpp), fp32 residual stream, fp32 accumulate" if act_q8 else
                                 "fp32 activations in the GEMVs, fp32 accumulate") +
-                               "; bf16 MFMA operands for B >= 2; attention: bf16 KV cache, bf16-rounded q, fp32 softmax",
+                               "; int8 GEMV engine up to B = 4, bf16 MFMA operands for B >= 5; attention: bf16 KV cache, bf16-rounded q, fp32 softmax",
                 "per_gpu_batch": args.batch,
                 "prompt_tokens": args.prompt,
                 "hipgraph": not args.no_graph,
