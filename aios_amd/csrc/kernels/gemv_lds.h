@@ -652,8 +652,7 @@ bool launch_gemv_lds(const GemvArgs& a, hipStream_t st) {
       const char* e = std::getenv("AIOS_GEMV_LDS");
       return e ? std::atoi(e) : 1;
     }();
-    // AIOS_GEMV_LDS_MAXB: batch rows the engine serves (1..4, default 4; B = 3 runs the 4-row kernel
-    // with one idle row; whether B = 3 / 4 decode takes this path or the skinny MFMA GEMM is the
+    // AIOS_GEMV_LDS_MAXB: batch rows the engine serves (1..4, default 4; whether B = 3 / 4 decode takes this path or the skinny MFMA GEMM is the
     // engine's dec_gemm_min_b_, profiles/lds_batched_r3.txt)
     static const int maxb = [] {
       const char* e = std::getenv("AIOS_GEMV_LDS_MAXB");
@@ -707,6 +706,14 @@ bool launch_gemv_lds(const GemvArgs& a, hipStream_t st) {
       lds = lg_lds_bytes<QT0, QT1, 2, 1>(a, pl);
       if (lds > LDS_MAX) return false;
       hipLaunchKernelGGL((gemv_lds_b1<QT0, QT1, 2, 1>), dim3(G), dim3(LG_THREADS), lds, st, a, pl);
+    } else if (a.B == 3) {  // its own instantiation: no idle fourth row in the dot work / staging
+      if ((lds = lg_lds_bytes<QT0, QT1, 3, 1>(a, pl)) <= LDS_MAX) {
+        hipLaunchKernelGGL((gemv_lds_b1<QT0, QT1, 3, 1>), dim3(G), dim3(LG_THREADS), lds, st, a, pl);
+      } else {
+        lds = lg_lds_bytes<QT0, QT1, 3, 2>(a, pl);
+        if (lds > LDS_MAX) return false;
+        hipLaunchKernelGGL((gemv_lds_b1<QT0, QT1, 3, 2>), dim3(G), dim3(LG_THREADS), lds, st, a, pl);
+      }
     } else if ((lds = lg_lds_bytes<QT0, QT1, 4, 1>(a, pl)) <= LDS_MAX) {
       hipLaunchKernelGGL((gemv_lds_b1<QT0, QT1, 4, 1>), dim3(G), dim3(LG_THREADS), lds, st, a, pl);
     } else {
