@@ -23,7 +23,8 @@ def _level(v: float, warn: float, crit: float) -> str:
 
 
 def service_name(text: str) -> str:
-    m = re.search(r"(?:service|restart|start|stop|status of)\s+([a-zA-Z0-9_.@-]+)", text)
+    """'restart service nginx' / 'restart nginx' / 'status of sshd' -> the unit name"""
+    m = re.search(r"(?:restart|start|stop|status of|service)\s+(?:the\s+)?(?:service\s+)?([a-zA-Z0-9_.@-]+)", text)
     return m.group(1) if m else ""
 
 
@@ -57,20 +58,38 @@ class SystemAgent(BaseAgent):
                 await self.update_metric(k, v)
             except Exception:
                 pass
+        recommended: list = []
         if overall == "critical":
             try:
                 await self.push_event("system.health_critical", {"status": status, "cpu": c, "memory": m, "disk": d},
                                       critical=True)
             except Exception:
                 pass
+            # the model proposes the immediate remediation (reference system.py:174, tactical)
+            failed = [k for k, v in status.items() if v != "ok"]
+            recommended = self.advice_lines(await self.analyze(
+                f"System health is CRITICAL. Issues: {failed}. Current metrics: CPU={c:.1f}%, MEM={m:.1f}%, "
+                f"DISK={d:.1f}%. What immediate actions should I take? List up to 3 actions, one per line.",
+                IntelligenceLevel.TACTICAL), 3)
         return {"success": True, "overall": overall, "status": status, "cpu_percent": c, "memory_percent": m,
-                "disk_percent": d, "gpus": gpus}
+                "disk_percent": d, "gpus": gpus, "recommended_actions": recommended}
 
     async def restart_service(self, task: Dict[str, Any]) -> Dict[str, Any]:
         name = task.get("input", {}).get("service") or service_name(task.get("description", ""))
         if not name:
             return {"success": False, "error": "no service name in task"}
-        r = await self.call_tool("service.restart", {"name": name}, reason=f"restart {name}")
+        pre = await self.call_tool("service.status", {"name": name}, reason=f"pre-restart status of {name}")
+        previous = str(pre.get("output", {}).get("status", "unknown")) if pre.get("success") else "unknown"
+        if previous in ("running", "active"):
+            # a running service is restarted only if the model judges it safe (reference system.py:238)
+            verdict = await self.analyze(
+                f"Service '{name}' is currently running (status: {previous}). Should I restart it? Consider: is it "
+                "a critical service? What are the risks? Answer YES or NO with a brief reason.",
+                IntelligenceLevel.OPERATIONAL)
+            if verdict.lower().lstrip(" *\"'").startswith("no"):
+                return {"success": False, "service": name, "action": "restart_skipped", "reason": verdict,
+                        "previous_status": previous}
+        r = await self.call_tool("service.restart", {"name": name}, reason=f"restart {name} (was: {previous})")
         if not r["success"]:
             return r
         st = await self.call_tool("service.status", {"name": name})

@@ -3,6 +3,7 @@
 webhook; think(OPERATIONAL) to summarise pages and to shape API calls)."""
 from __future__ import annotations
 
+import json
 import os
 import re
 import time
@@ -60,9 +61,19 @@ class WebAgent(BaseAgent):
         url = self._url(task)
         if not url:
             return {"success": False, "error": "no URL in task"}
-        return await self.call_tool("web.api_call", {"url": url, "method": inp.get("method", "GET"),
-                                                     "body": inp.get("body"), "headers": inp.get("headers", {}),
-                                                     "query_params": inp.get("query_params", {})})
+        method = inp.get("method", "GET")
+        r = await self.call_tool("web.api_call", {"url": url, "method": method,
+                                                  "body": inp.get("body"), "headers": inp.get("headers", {}),
+                                                  "query_params": inp.get("query_params", {})})
+        if r["success"] and inp.get("interpret"):
+            # the model's reading of the response when asked for (reference web.py:234)
+            out = r.get("output", {})
+            body = json.dumps(out.get("data", out.get("body", {})), default=str)[:3000]
+            r["interpretation"] = await self.analyze(
+                f"Interpret this API response:\nURL: {url}\nMethod: {method}\n"
+                f"Status: {out.get('status', 'unknown')}\nResponse: {body}\n\n"
+                "Provide a brief interpretation of what this response means.", IntelligenceLevel.OPERATIONAL)
+        return r
 
     async def download(self, task: Dict[str, Any]) -> Dict[str, Any]:
         inp = task.get("input") or {}

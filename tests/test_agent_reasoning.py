@@ -193,3 +193,61 @@ def test_fallback_asks_for_an_action(kind):
     rec = _Rec({}, answer='{"action": "nope"}')
     r = _run(_agent(kind, rec).handle_task({"description": "zzz unrecognisable", "input": {}}))
     assert not r["success"] and _levels(rec) == [IntelligenceLevel.OPERATIONAL]
+
+
+# ----------------------------------------------------------------------------------------- system / network / web
+def test_system_critical_health_asks_for_remediation():
+    rec = _Rec({"monitor.cpu": {"success": True, "output": {"percent": 99.0}},
+                "monitor.memory": {"success": True, "output": {"percent": 40.0}},
+                "monitor.disk": {"success": True, "output": {"percent": 10.0}}})
+    r = _run(_agent("system", rec).check_health({}))
+    assert r["overall"] == "critical" and _levels(rec) == [IntelligenceLevel.TACTICAL]
+    assert "CPU=99.0%" in rec.prompts[0][1]
+    assert r["recommended_actions"] == ["isolate the host", "rotate keys", "patch"]
+    calm = _Rec({"monitor.cpu": {"success": True, "output": {"percent": 10.0}}})
+    assert _run(_agent("system", calm).check_health({}))["recommended_actions"] == [] and calm.prompts == []
+
+
+@pytest.mark.parametrize("answer,restarted", [("NO - it serves the console", False), ("YES, safe", True)])
+def test_system_restart_safety_check(answer, restarted):
+    calls = []
+
+    def restart(args):
+        calls.append(args)
+        return {"success": True, "output": {}}
+
+    rec = _Rec({"service.status": {"success": True, "output": {"status": "running"}}, "service.restart": restart},
+               answer=answer)
+    r = _run(_agent("system", rec).restart_service({"description": "restart service nginx"}))
+    assert _levels(rec) == [IntelligenceLevel.OPERATIONAL] and "'nginx' is currently running" in rec.prompts[0][1]
+    assert bool(calls) == restarted and r["success"] == restarted
+    if not restarted:
+        assert r["action"] == "restart_skipped"
+    stopped = _Rec({"service.status": {"success": True, "output": {"status": "inactive"}}})
+    assert _run(_agent("system", stopped).restart_service({"description": "restart service x"}))["success"]
+    assert stopped.prompts == []  # a stopped service restarts without asking
+
+
+@pytest.mark.parametrize("answer,added", [("NO: it drops port 22", False), ("YES", True)])
+def test_network_firewall_lockout_check(answer, added):
+    calls = []
+
+    def add_rule(args):
+        calls.append(args)
+        return {"success": True, "output": {}}
+
+    rec = _Rec({"firewall.add_rule": add_rule}, answer=answer)
+    r = _run(_agent("network", rec).manage_firewall({"description": "block port 22"}))
+    assert _levels(rec) == [IntelligenceLevel.OPERATIONAL] and "tcp dport 22 drop" in rec.prompts[0][1]
+    assert bool(calls) == added and r["success"] == added
+
+
+def test_web_api_interpretation_on_request():
+    rec = _Rec({"web.api_call": {"success": True, "output": {"status": 200, "data": {"ok": True}}}},
+               answer="The service is healthy.")
+    a = _agent("web", rec)
+    plain = _run(a.api_interact({"input": {"url": "http://127.0.0.1:9/x"}}))
+    assert rec.prompts == [] and "interpretation" not in plain
+    r = _run(a.api_interact({"input": {"url": "http://127.0.0.1:9/x", "interpret": True}}))
+    assert _levels(rec) == [IntelligenceLevel.OPERATIONAL] and '"ok": true' in rec.prompts[0][1]
+    assert r["interpretation"] == "The service is healthy."
