@@ -386,9 +386,10 @@ PYBIND11_MODULE(_engine, m) {
   m.def("attn_decode",
         [](uintptr_t q, uintptr_t k, uintptr_t v, uintptr_t seq_len, uintptr_t slot, int B, int H, int Hkv, int hd,
            int max_ctx, int n_chunks, float scale, uintptr_t opart, uintptr_t ml, uintptr_t out, uintptr_t counters,
-           uintptr_t st, int split, uintptr_t block_table, int bt_rows) {
+           uintptr_t st, int split, uintptr_t block_table, int bt_rows, uintptr_t ts) {
           AttnDecodeArgs a;
           a.split = split;
+          a.ts = (unsigned long long*)ts;
           a.block_table = (const int*)block_table; a.bt_rows = bt_rows;
           a.q = (const float*)q; a.k_cache = (const bf16_t*)k; a.v_cache = (const bf16_t*)v;
           a.seq_len = (const int*)seq_len; a.slot = (const int*)slot;
@@ -400,7 +401,7 @@ PYBIND11_MODULE(_engine, m) {
         py::arg("q"), py::arg("k"), py::arg("v"), py::arg("seq_len"), py::arg("slot"), py::arg("B"), py::arg("H"),
         py::arg("Hkv"), py::arg("hd"), py::arg("max_ctx"), py::arg("n_chunks"), py::arg("scale"), py::arg("opart"),
         py::arg("ml"), py::arg("out"), py::arg("counters"), py::arg("st"), py::arg("split") = 0,
-        py::arg("block_table") = 0, py::arg("bt_rows") = 0);
+        py::arg("block_table") = 0, py::arg("bt_rows") = 0, py::arg("ts") = 0);
   m.def("attn_decode_split", &attn_decode_split);
   m.def("rmsnorm", [](uintptr_t x, int ldx, uintptr_t w, uintptr_t y, int ldy, int rows, int n, float eps, uintptr_t st) {
     launch_rmsnorm((const float*)x, ldx, (const float*)w, (float*)y, ldy, rows, n, eps, S(st));

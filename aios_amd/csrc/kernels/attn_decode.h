@@ -105,6 +105,14 @@ __device__ __forceinline__ void attn_core(const AttnDecodeArgs& a, int sp, int k
   const int b = blockIdx.z;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int ksub = lane / LPK, dsl = lane % LPK;
+  // probe stamps (a.ts, null in production: one scalar compare per site): 0 entry, 1 seq_len known,
+  // 2 first pass computed (its K/V landed), 3 waves merged, 4 partial published + ticket, 5 (m, l)
+  // weights ready (last arriver), 6 done
+  auto stamp = [&](int k) __attribute__((always_inline)) {
+    if (a.ts && threadIdx.x == 0)
+      a.ts[((size_t)blockIdx.z * gridDim.x + blockIdx.x) * 8 + k] = __builtin_amdgcn_s_memrealtime();
+  };
+  stamp(0);
   static_assert(CH == KV_BLOCK, "one decode pass = one paged KV block");
   const int slot = a.slot ? a.slot[b] : b;
   // paged KV: pass c reads physical block bt[c]; a row-indexed table (bt_rows) is looked up
@@ -121,6 +129,7 @@ __device__ __forceinline__ void attn_core(const AttnDecodeArgs& a, int sp, int k
   const int nchunk = (len + CH - 1) / CH;
   const int P = max(1, min((nchunk + ppw - 1) / ppw, P_max));
   if (sp >= P) return;  // uniform: this workgroup has no chunk, issues no K/V traffic
+  stamp(1);
 
   // two passes in flight per workgroup: buffers A and B (static, so they stay in VGPRs)
   uint4 kA[STEPS], vA[STEPS], kB[STEPS], vB[STEPS];
@@ -244,6 +253,7 @@ __device__ __forceinline__ void attn_core(const AttnDecodeArgs& a, int sp, int k
   };
   for (int c = sp; c < nchunk; c += 2 * P) {
     pass(kA, vA, c);
+    if (c == sp) stamp(2);
     if (c + 2 * P < nchunk) issue(kA, vA, c + 2 * P, true);
     if (c + P < nchunk) {
       pass(kB, vB, c + P);
@@ -277,6 +287,7 @@ __device__ __forceinline__ void attn_core(const AttnDecodeArgs& a, int sp, int k
     s_l[wave][lane] = lv;
   }
   __syncthreads();
+  stamp(3);
   const int nact = P;  // workgroups that arrive
   for (int idx = threadIdx.x; idx < G * HD; idx += NT) {
     const int g = idx / HD, d = idx - g * HD;
@@ -306,6 +317,7 @@ __device__ __forceinline__ void attn_core(const AttnDecodeArgs& a, int sp, int k
   }
   if (nact == 1) {
     if constexpr (FUSED) fuse_signal(fz, G);
+    stamp(6);
     return;
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
@@ -316,6 +328,7 @@ __device__ __forceinline__ void attn_core(const AttnDecodeArgs& a, int sp, int k
     s_last = (t == nact - 1);
   }
   __syncthreads();
+  stamp(4);
   if (!s_last) return;
   // ---- last arriver.  (1) one thread per (head, partial) loads that partial's (m, l);
   //      (measured: one batch of (m, l) + o loads per output thread -- one round trip but 2x the
@@ -349,6 +362,7 @@ __device__ __forceinline__ void attn_core(const AttnDecodeArgs& a, int sp, int k
     if (lane < nact) s_pm[g][lane] = e / L;
   }
   __syncthreads();
+  stamp(5);
   for (int idx = threadIdx.x; idx < G * HD; idx += NT) {
     const int g = idx / HD, d = idx - g * HD;
     const int h = h0 + g;
@@ -368,6 +382,7 @@ __device__ __forceinline__ void attn_core(const AttnDecodeArgs& a, int sp, int k
   }
   if (threadIdx.x == 0) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
   if constexpr (FUSED) fuse_signal(fz, G);
+  stamp(6);
 }
 
 // Up to ATTN_SPLIT_LEN keys the G query heads of a KV head are split over G workgroups (one head

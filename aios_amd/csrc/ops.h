@@ -98,6 +98,7 @@ struct AttnDecodeArgs {
   int short_len = -1;      // contexts up to this many keys split by query head (-1: launcher decides)
   int* counters;           // [B][n_kv_heads] arrival tickets, zero-initialised, self re-arming
   PfSpec pf{};             // optional MALL prefetch role (B = 1)
+  unsigned long long* ts = nullptr;  // probes: [grid][8] s_memrealtime phase stamps (tools/attn_probe.py --stamps)
 };
 constexpr int ATTN_CHUNK = 64;
 void launch_attn_decode(const AttnDecodeArgs& a, hipStream_t st);

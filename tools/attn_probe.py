@@ -1,5 +1,10 @@
 """Decode-attention microbenchmark on the GPU: per-launch time (hipGraph of back-to-back launches)
-of attn_decode over context lengths x split sizes.  python tools/attn_probe.py"""
+of attn_decode over context lengths x split sizes.  python tools/attn_probe.py
+--stamps: per-phase in-kernel timestamps (s_memrealtime, AttnDecodeArgs.ts) of one launch with the
+K/V cache evicted from the Infinity Cache first (a 512 MB write in between), median / max over the
+workgroups: entry -> seq_len known -> first pass computed -> waves merged -> partial published ->
+combine weights ready -> done."""
+import json
 import math
 import os
 import sys
@@ -31,8 +36,52 @@ def graph_time(fn, n=64, reps=20):
     return e0.elapsed_time(e1) * 1e3 / (reps * n)
 
 
+def stamps(E):
+    H, Hkv, hd, max_ctx = 32, 8, 128, 4096
+    kc = (torch.randn(1, Hkv, max_ctx, hd) * 0.5).to(torch.bfloat16).cuda()
+    vc = torch.randn(1, Hkv, max_ctx, hd).to(torch.bfloat16).cuda()
+    q = torch.randn(1, H, hd, device="cuda")
+    slot = torch.zeros(1, dtype=torch.int32, device="cuda")
+    nch = max_ctx // E.ATTN_CHUNK
+    opart = torch.empty(1, H, nch, hd, device="cuda")
+    ml = torch.empty(1, H, nch, 2, device="cuda")
+    out = torch.empty(1, H * hd, device="cuda")
+    cnt = torch.zeros(1, H, dtype=torch.int32, device="cuda")
+    flush = torch.empty(512 << 20, dtype=torch.uint8, device="cuda")
+    ts = torch.zeros(4096 * 8, dtype=torch.int64, device="cuda")
+    names = ["entry", "seq_len", "pass1", "merged", "published", "weights", "done"]
+    for L in (153, 1000, 4000):
+        seq = torch.tensor([L], dtype=torch.int32, device="cuda")
+        run = lambda t=0: E.attn_decode(q.data_ptr(), kc.data_ptr(), vc.data_ptr(), seq.data_ptr(), slot.data_ptr(),
+                                        1, H, Hkv, hd, max_ctx, nch, 1 / math.sqrt(hd), opart.data_ptr(), ml.data_ptr(),
+                                        out.data_ptr(), cnt.data_ptr(), torch.cuda.current_stream().cuda_stream, 0,
+                                        ts=t)
+        run()
+        rows = []
+        for rep in range(5):
+            flush.fill_(rep)
+            ts.zero_()
+            torch.cuda.synchronize()
+            run(ts.data_ptr())
+            torch.cuda.synchronize()
+            t = ts.view(-1, 8).cpu().numpy().astype("float64")
+            t = t[t[:, 0] > 0]
+            rows.append((t - t[:, 0].min()) / 100.0)  # 100 MHz ticks -> us from the first entry
+        import numpy as np
+        t = np.concatenate(rows[1:])
+        res = {}
+        for k, n in enumerate(names):
+            v = t[:, k][t[:, k] > 0] if k else t[:, 0]
+            if len(v):
+                res[n] = [round(float(np.median(v)), 2), round(float(v.max()), 2)]
+        print(json.dumps({"len": L, "workgroups": int(len(t) / 4), "phase_us_median_max": res}), flush=True)
+
+
 def main():
     E = native.require()
+    if "--stamps" in sys.argv:
+        stamps(E)
+        return
     H, Hkv, hd = 32, 8, 128
     for max_ctx in (512, 4096):
         kc = (torch.randn(1, Hkv, max_ctx, hd) * 0.5).to(torch.bfloat16).cuda()
