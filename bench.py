@@ -132,20 +132,22 @@ def measure_tp(args, rank: int, world: int, device: int, gloo):
         del eng
         return None, None
     tp = TPEngine(eng, comm, group=gloo) if world > 1 else eng
-    p = [cfg.bos_id] + [(7 * i) % (cfg.vocab_size - 3) + 3 for i in range(args.prompt - 1)]
-    tok = int(tp.prefill(0, p, 0, True).argmax())
-    tp.decode_loop_prepare([0], [tok], [args.prompt])
-    tp.decode_loop_run(1, warmup, True)
-    tp.synchronize()
-    t0 = time.perf_counter()
-    tp.decode_loop_run(1, steps, True)
-    tp.synchronize()
-    dt = time.perf_counter() - t0
-    if comm.error():
-        raise RuntimeError("TP all-reduce timed out")
-    info = {"weight_gb_per_rank": round(eng.weight_bytes / 1e9, 3)}
-    if world > 1:
-        tp.close()
+    try:
+        p = [cfg.bos_id] + [(7 * i) % (cfg.vocab_size - 3) + 3 for i in range(args.prompt - 1)]
+        tok = int(tp.prefill(0, p, 0, True).argmax())
+        tp.decode_loop_prepare([0], [tok], [args.prompt])
+        tp.decode_loop_run(1, warmup, True)
+        tp.synchronize()
+        t0 = time.perf_counter()
+        tp.decode_loop_run(1, steps, True)
+        tp.synchronize()
+        dt = time.perf_counter() - t0
+        if comm.error():
+            raise RuntimeError("TP all-reduce timed out")
+        info = {"weight_gb_per_rank": round(eng.weight_bytes / 1e9, 3)}
+    finally:
+        if world > 1:
+            tp.close()  # releases the workers' command loop whatever happened on the leader
     del eng
     return dt, info
 
@@ -182,7 +184,10 @@ def main():
             td.init_process_group("gloo")
         else:
             td.init_process_group("nccl", device_id=torch.device("cuda", device))
-        gloo = td.new_group(backend="gloo")  # the TP leader's command channel
+        import datetime
+
+        # the TP leader's command channel; bounded, so a rank lost in the secondary cannot hold the run
+        gloo = td.new_group(backend="gloo", timeout=datetime.timedelta(seconds=600))
         dist = td
 
     act_q8 = not args.fp32_act
@@ -198,7 +203,13 @@ def main():
         if not args.no_tp:
             if dist is not None:
                 dist.barrier()
-            tp_dt, tp_info = measure_tp(args, rank, world, device, gloo)
+            # a failure of the secondary (e.g. a peer mapping the node refuses) is reported in the JSON,
+            # it never costs the headline measurement above
+            try:
+                tp_dt, tp_info = measure_tp(args, rank, world, device, gloo)
+            except Exception as e:  # noqa: BLE001
+                tp_dt, tp_info = None, {"error": f"{type(e).__name__}: {e}"[:300]}
+                print(f"[rank {rank}] tp_strategic failed: {tp_info['error']}", file=sys.stderr, flush=True)
 
     # max over ranks
     if dist is not None:
@@ -269,6 +280,9 @@ def main():
                 "ms_per_step": round(tp_dt / args.tp_steps * 1e3, 4),
                 "tp": world, "ranks_share_gpu": share, **(tp_info or {}),
             }
+        elif tp_info and "error" in tp_info:
+            out["tp_strategic"] = {"metric": f"decode tokens/sec {args.tp_model} {args.recipe} TP={world} (batch 1)",
+                                   "value": None, "tp": world, "error": tp_info["error"]}
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.barrier()
