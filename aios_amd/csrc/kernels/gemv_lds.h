@@ -247,6 +247,39 @@ __device__ __forceinline__ void q4p_dot_b(const uint4& a0, const uint4& a1, cons
     out[b] = d * (c0 * X[b].dx0 * (float)s0[b] + c1 * X[b].dx1 * (float)s1[b]) - dmin * (m0 * X[b].sx0 + m1 * X[b].sx1);
 }
 
+// B row sums over each 32-lane half at the cost of ~one: a butterfly first halves the value set per
+// lane (xor 1: lanes keep rows {0,1} / {2,3}; xor 2: one row each), then the rows' classes reduce
+// with row rotations by 4 and 8 and the 16-lane swap.  Returns, in every lane, the half's total of row
+// lg_half_row<B>(p) (p = lane & 31): rows 0..B-1 end up in lanes 0..3 of each half (B = 3: the
+// fourth value is 0 and its lane idle).  ~13 VALU for B = 4 instead of 4 x cu_half_sum's ~7.
+template <int B>
+__device__ __forceinline__ int lg_half_row(int p) {
+  return B > 2 ? 2 * (p & 1) + ((p >> 1) & 1) : (p & 1);
+}
+template <int B>
+__device__ __forceinline__ float lg_half_sum_rows(const float (&v)[B], int p) {
+  static_assert(B >= 2 && B <= 4, "rows");
+  const bool b0 = p & 1;
+  float u;
+  if constexpr (B == 2) {
+    const float send = b0 ? v[0] : v[1], keep = b0 ? v[1] : v[0];
+    u = keep + cu_dpp<0xB1>(send);          // quad_perm [1,0,3,2]: lane ^ 1
+    u += cu_dpp<0x4E>(u);                   // lane ^ 2 (same row class)
+  } else {
+    const float v3 = B == 4 ? v[B - 1] : 0.f;
+    const float s0 = b0 ? v[0] : v[2], s1 = b0 ? v[1] : v3;
+    const float k0 = b0 ? v[2] : v[0], k1 = b0 ? v3 : v[1];
+    const float u0 = k0 + cu_dpp<0xB1>(s0), u1 = k1 + cu_dpp<0xB1>(s1);
+    const bool b1 = (p >> 1) & 1;
+    const float send = b1 ? u0 : u1, keep = b1 ? u1 : u0;
+    u = keep + cu_dpp<0x4E>(send);          // lane ^ 2
+  }
+  u += cu_dpp<0x124>(u);                    // row_ror:4 within 16 lanes (keeps lane & 3)
+  u += cu_dpp<0x128>(u);                    // row_ror:8
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(u), __float_as_uint(u), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
 // one 64-chunk group of a row against B staged x rows (x read from LDS)
 template <int QT, int B>
 __device__ __forceinline__ void lg_compute_b(const RawChunk& raw, int it, int nch, const int8_t* xq, const float2* ms,
@@ -407,13 +440,15 @@ __global__ void __launch_bounds__(LG_THREADS) gemv_lds_b1(GemvArgs a, CuPlan pl)
               const bool ok = t * L::NGS + kk < ngroups;
               float v[B];
               q4p_dot_b<B>(a0, a1, mt, p & 3, X, v);
+              if (!ok) {
 #pragma unroll
-              for (int b = 0; b < B; ++b) {
-                const float r = cu_half_sum(ok ? v[b] : 0.f);
-                if (p == 0 && ok)
-                  __hip_atomic_fetch_add(&rowacc[b * pl.racc_n + t * rps + rk], r, __ATOMIC_RELAXED,
-                                         __HIP_MEMORY_SCOPE_WORKGROUP);
+                for (int b = 0; b < B; ++b) v[b] = 0.f;
               }
+              const float r = lg_half_sum_rows<B>(v, p);
+              const int rb = lg_half_row<B>(p);
+              if (p < (B > 2 ? 4 : 2) && rb < B && ok)  // one LDS atomic instruction for all B rows
+                __hip_atomic_fetch_add(&rowacc[rb * pl.racc_n + t * rps + rk], r, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_WORKGROUP);
             }
             lg_barrier();
           }
