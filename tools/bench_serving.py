@@ -37,6 +37,8 @@ def main():
     ap.add_argument("--max-tokens", type=int, default=128)
     ap.add_argument("--temperature", type=float, default=0.7)
     ap.add_argument("--ctx", type=int, default=4096)
+    ap.add_argument("--tp", type=int, default=1, help="tensor-parallel ranks (#tp=N model spec; ranks share the GPU "
+                    "when the box has fewer GPUs)")
     ap.add_argument("--json", default="")
     args = ap.parse_args()
 
@@ -46,7 +48,7 @@ def main():
     from aios_amd.runtime.scheduler import GenRequest
 
     mgr = ModelManager(max_batch=args.streams, max_slots=2 * args.streams)
-    spec = f"synthetic:{args.model}:{args.recipe}"
+    spec = f"synthetic:{args.model}:{args.recipe}" + (f"#tp={args.tp}" if args.tp > 1 else "")
     t0 = time.time()
     m = asyncio.run(mgr.load_model("bench", spec, context_length=args.ctx))
     if m.status != "ready":
@@ -121,7 +123,7 @@ def main():
     out = {
         "bench": "serving: concurrent JSON-mode streams sharing a prompt prefix",
         "model": f"{args.model} {args.recipe} (random-init weights, synthetic prompts)",
-        "streams": args.streams, "prompt_tokens": args.prompt, "shared_prefix_tokens": args.shared,
+        "tp": args.tp, "streams": args.streams, "prompt_tokens": args.prompt, "shared_prefix_tokens": args.shared,
         "max_tokens": args.max_tokens, "temperature": args.temperature, "top_k": 40, "top_p": 0.95,
         "json_mode": True,
         "ttft_p50_ms": round(ttft[len(ttft) // 2], 2), "ttft_p90_ms": round(ttft[int(len(ttft) * 0.9) - 1], 2),
