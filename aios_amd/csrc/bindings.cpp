@@ -133,6 +133,7 @@ PYBIND11_MODULE(_engine, m) {
     return std::string(p.name) + " / " + p.gcnArchName;
   });
   m.def("synchronize", []() { HIP_CHECK(hipDeviceSynchronize()); });
+  m.def("resid_norm_parts", &resid_norm_parts, py::arg("d"));
 
   py::class_<EngineConfig>(m, "EngineConfig")
       .def(py::init<>())
@@ -266,10 +267,12 @@ PYBIND11_MODULE(_engine, m) {
         // the comm must outlive the engine's use of it (the Python wrapper keeps a reference)
         e.set_allreduce(&XgmiComm::hook, &c);
         e.set_allgather(&XgmiComm::gather_hook, &c);
+        e.set_allreduce_norm(&XgmiComm::norm_hook, &c);
       })
       .def("set_comm", [](Engine& e, RcclComm& c) {
         e.set_allreduce(&RcclComm::hook, &c);
         e.set_allgather(&RcclComm::gather_hook, &c);
+        e.set_allreduce_norm(&RcclComm::norm_hook, &c);
       })
       .def_property_readonly("vocab_parallel", &Engine::vocab_parallel);
 
@@ -286,6 +289,14 @@ PYBIND11_MODULE(_engine, m) {
       .def("allreduce", [](XgmiComm& c, uintptr_t data, size_t n, uintptr_t residual, uintptr_t st) {
         c.allreduce((float*)data, n, (float*)residual, S(st));
       }, py::arg("data"), py::arg("n"), py::arg("residual") = 0, py::arg("stream") = 0)
+      .def("allreduce_norm",
+           [](XgmiComm& c, uintptr_t data, int rows, int d, uintptr_t residual, uintptr_t g, uintptr_t out16, int ld16,
+              uintptr_t part, int parts, uintptr_t st) {
+             c.allreduce_norm((float*)data, rows, d, (float*)residual,
+                              ResidNorm{(const float*)g, (bf16_t*)out16, ld16, (float*)part, parts}, S(st));
+           },
+           py::arg("data"), py::arg("rows"), py::arg("d"), py::arg("residual"), py::arg("g"), py::arg("out16"),
+           py::arg("ld16"), py::arg("part"), py::arg("parts"), py::arg("stream") = 0)
       .def("allgather_cols", [](XgmiComm& c, uintptr_t data, int rows, int slice, int ld, uintptr_t st) {
         c.allgather_cols((float*)data, rows, slice, ld, S(st));
       }, py::arg("data"), py::arg("rows"), py::arg("slice"), py::arg("ld"), py::arg("stream") = 0)
@@ -312,6 +323,14 @@ PYBIND11_MODULE(_engine, m) {
       .def("allreduce", [](RcclComm& c, uintptr_t data, size_t n, uintptr_t residual, uintptr_t st) {
         c.allreduce((float*)data, n, (float*)residual, S(st));
       }, py::arg("data"), py::arg("n"), py::arg("residual") = 0, py::arg("stream") = 0)
+      .def("allreduce_norm",
+           [](RcclComm& c, uintptr_t data, int rows, int d, uintptr_t residual, uintptr_t g, uintptr_t out16, int ld16,
+              uintptr_t part, int parts, uintptr_t st) {
+             c.allreduce_norm((float*)data, rows, d, (float*)residual,
+                              ResidNorm{(const float*)g, (bf16_t*)out16, ld16, (float*)part, parts}, S(st));
+           },
+           py::arg("data"), py::arg("rows"), py::arg("d"), py::arg("residual"), py::arg("g"), py::arg("out16"),
+           py::arg("ld16"), py::arg("part"), py::arg("parts"), py::arg("stream") = 0)
       .def("allgather_cols", [](RcclComm& c, uintptr_t data, int rows, int slice, int ld, uintptr_t st) {
         c.allgather_cols((float*)data, rows, slice, ld, S(st));
       }, py::arg("data"), py::arg("rows"), py::arg("slice"), py::arg("ld"), py::arg("stream") = 0)

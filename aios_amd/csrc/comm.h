@@ -33,6 +33,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include "ops.h"
 #include <string>
 #include <vector>
 
@@ -67,6 +68,10 @@ class XgmiComm {
   // Messages above two_shot_min() floats use reduce-scatter + all-gather; messages above the
   // capacity are split into several calls.
   void allreduce(float* data, size_t n, float* residual, hipStream_t st);
+  // allreduce into `residual` ([rows][d]) plus the split-RMSNorm producer outputs of the consumer
+  // GEMM (ResidNorm, ops.h): one launch when the message is a one-shot call (decode sizes, d a
+  // multiple of RNORM_COLS), else the all-reduce followed by launch_add_norm
+  void allreduce_norm(float* data, int rows, int d, float* residual, const ResidNorm& nm, hipStream_t st);
   // every rank owns columns [r*slice, (r+1)*slice) of the rows x ld fp32 matrix `data`;
   // afterwards every rank holds all columns
   void allgather_cols(float* data, int rows, int slice, int ld, hipStream_t st);
@@ -82,6 +87,8 @@ class XgmiComm {
   // Engine hooks (AllReduceFn / AllGatherFn-compatible trampolines)
   static void hook(void* self, float* data, size_t n, float* residual, hipStream_t st);
   static void gather_hook(void* self, float* data, int rows, int slice, int ld, hipStream_t st);
+  static void norm_hook(void* self, float* data, int rows, int d, float* residual, const ResidNorm& nm,
+                        hipStream_t st);
 
  private:
   ArDevCtx h_{};

@@ -71,6 +71,10 @@ using AllReduceFn = void (*)(void* ctx, float* data, size_t n, float* residual, 
 // all-gather hook (vocab-parallel lm_head): rank r owns columns [r*slice, (r+1)*slice) of the
 // rows x ld fp32 matrix `data`; afterwards every rank holds all of them
 using AllGatherFn = void (*)(void* ctx, float* data, int rows, int slice, int ld, hipStream_t stream);
+// fused all-reduce + split-RMSNorm producer hook (batched TP decode, C1 / C2): residual ([rows][d]) +=
+// sum of partials, then the ResidNorm outputs (ops.h) the next skinny GEMM consumes -- no RMSNorm launch
+using AllReduceNormFn = void (*)(void* ctx, float* data, int rows, int d, float* residual, const ResidNorm& nm,
+                                 hipStream_t stream);
 
 class Engine {
  public:
@@ -122,6 +126,7 @@ class Engine {
   uintptr_t stream_handle() const { return (uintptr_t)stream_; }
   void set_allreduce(AllReduceFn fn, void* ctx) { allreduce_ = fn; allreduce_ctx_ = ctx; }
   void set_allgather(AllGatherFn fn, void* ctx) { allgather_ = fn; allgather_ctx_ = ctx; }
+  void set_allreduce_norm(AllReduceNormFn fn, void* ctx) { allreduce_norm_ = fn; allreduce_norm_ctx_ = ctx; }
   bool vocab_parallel() const { return cfg_.vocab_parallel != 0; }
   void reset_graphs();
   int capture_graphs(int max_b);  // pre-capture the decode-step graphs of B = 1..max_b (masked + unmasked)
@@ -258,6 +263,7 @@ class Engine {
   int nrm_fuse_ = 1;
   int nrm_parts_ = 0;  // tiles of the d_model-wide producer GEMM (0: fusion unavailable)
   bool nrm_on(int B) const;
+  bool tpn_on(int B) const;  // batched TP decode: C1 / C2 fused with the next RMSNorm
  private:
   void layer_decode_gemm(int l, int B);
   hipGraphExec_t step_graph(int B);
@@ -296,6 +302,14 @@ class Engine {
   AllReduceFn allreduce_ = nullptr;
   void* allreduce_ctx_ = nullptr;
   AllGatherFn allgather_ = nullptr;
+  AllReduceNormFn allreduce_norm_ = nullptr;
+  void* allreduce_norm_ctx_ = nullptr;
+  // batched TP decode: the fused all-reduce's split-norm partials [max_batch][tpn_parts_] (0: off)
+  int tpn_parts_ = 0;
+  float* tpn_part_ = nullptr;
+  // the split-norm partials the lm_head consumes when nrm_lm_ is set (nrm_part_ or tpn_part_)
+  const float* lm_nrm_in_ = nullptr;
+  int lm_nrm_parts_ = 0;
   void* allgather_ctx_ = nullptr;
   // sampling config for the enqueued step
   bool sample_temp_ = false;

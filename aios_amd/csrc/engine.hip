@@ -598,6 +598,11 @@ void Engine::finalize() {
           nrm_part_ = fbuf((size_t)Bm * parts);
           ws += (size_t)Bm * d * 2;
         }
+        // TP: the all-reduce after O / down writes the next GEMM's split-norm operand itself
+        if (cfg_.tp_size > 1 && dec_xn16_ && resid_norm_parts(d) > 0 && resid_norm_parts(d) <= 64) {
+          tpn_parts_ = resid_norm_parts(d);
+          tpn_part_ = fbuf((size_t)Bm * tpn_parts_);
+        }
       }
     }
   }
@@ -830,6 +835,11 @@ void Engine::gemm(GemmQArgs& g) {
 // with explicit RMSNorm -> bf16 and RoPE/KV-write launches in place of the GEMV prologue /
 // epilogue fusions.  SwiGLU runs in the gate/up GEMM's epilogue (bf16 out for the down GEMM).
 bool Engine::nrm_on(int B) const { return nrm_parts_ > 0 && dec_xn16_ && cfg_.tp_size == 1 && B <= 64; }
+// AIOS_TP_NORM_FUSE=0 restores the separate RMSNorm launches after C1 / C2 (A/B and tests)
+bool Engine::tpn_on(int B) const {
+  static const bool on = !(std::getenv("AIOS_TP_NORM_FUSE") && std::atoi(std::getenv("AIOS_TP_NORM_FUSE")) == 0);
+  return on && tpn_parts_ > 0 && allreduce_norm_ && cfg_.tp_size > 1 && B <= 64;
+}
 
 void Engine::layer_decode_gemm(int l, int B) {
   const LayerW& L = layers_[l];
@@ -837,6 +847,7 @@ void Engine::layer_decode_gemm(int l, int B) {
   const int qd = H * hd, kvd = Hkv * hd, ldqkv = qd + 2 * kvd;
   const bool tp = cfg_.tp_size > 1;
   const bool fn = nrm_on(B);
+  const bool tpn = tp && tpn_on(B);  // (fn and tpn are exclusive: fn needs tp_size 1)
   bf16_t* kc = k_cache_ + (size_t)l * layer_kv_elems_;
   bf16_t* vc = v_cache_ + (size_t)l * layer_kv_elems_;
   // consumer side of the split RMSNorm: A = bf16(x * g) from the previous residual GEMM
@@ -848,11 +859,21 @@ void Engine::layer_decode_gemm(int l, int B) {
     g.epi = GEPI_ACCUM_NORM; g.nrm_g = g_next; g.nrm_out16 = dec_xn16_; g.nrm_part = nrm_part_;
     g.nrm_parts = nrm_parts_;
   };
-  if (!(fn && l > 0)) launch_rmsnorm_bf16(x_, d, L.attn_norm, dec_a16_, d, B, d, cfg_.norm_eps, stream_);
+  // TP: the same contract, produced by the fused all-reduce (C1 / C2) into tpn_part_
+  auto tpn_in = [&](GemmQArgs& g) {
+    g.A = dec_xn16_; g.nrm_in = tpn_part_; g.nrm_parts = tpn_parts_; g.nrm_eps = cfg_.norm_eps;
+  };
+  auto tp_reduce = [&](float* part, const float* g_next) {
+    if (tpn) allreduce_norm_(allreduce_norm_ctx_, part, B, d, x_, ResidNorm{g_next, dec_xn16_, d, tpn_part_, tpn_parts_},
+                             stream_);
+    else allreduce(part, (size_t)B * d, x_);
+  };
+  if (!((fn || tpn) && l > 0)) launch_rmsnorm_bf16(x_, d, L.attn_norm, dec_a16_, d, B, d, cfg_.norm_eps, stream_);
   GemmQArgs g;
   std::memset(&g, 0, sizeof(g));
   g.A = dec_a16_; g.lda = d; g.M = B; g.K = d; g.nseg = 3;
   if (fn && l > 0) nrm_in(g);
+  if (tpn && l > 0) tpn_in(g);
   g.seg[0] = L.wq.w; g.seg[1] = L.wk.w; g.seg[2] = L.wv.w;
   g.seg_n0[0] = 0; g.seg_n0[1] = qd; g.seg_n0[2] = qd + kvd;
   g.N = ldqkv; g.C = qkv_; g.ldc = ldqkv; g.epi = GEPI_STORE;
@@ -898,21 +919,25 @@ void Engine::layer_decode_gemm(int l, int B) {
   if (tp) { g.C = ff_; g.epi = GEPI_STORE; } else { g.C = x_; g.epi = GEPI_ACCUM; }
   if (fn) nrm_out(g, L.ffn_norm);
   gemm(g);
-  if (tp) allreduce(ff_, (size_t)B * d, x_);
-  if (!fn) launch_rmsnorm_bf16(x_, d, L.ffn_norm, dec_a16_, d, B, d, cfg_.norm_eps, stream_);
+  if (tp) tp_reduce(ff_, L.ffn_norm);
+  if (!fn && !tpn) launch_rmsnorm_bf16(x_, d, L.ffn_norm, dec_a16_, d, B, d, cfg_.norm_eps, stream_);
   std::memset(&g, 0, sizeof(g));
   g.A = dec_a16_; g.lda = d; g.M = B; g.K = d; g.nseg = 1; g.seg[0] = L.wgu.w; g.N = 2 * ff;
   g.C16 = dec_ff16_; g.ldc = ff; g.epi = GEPI_SWIGLU_BF16;
   if (fn) nrm_in(g);
+  if (tpn) tpn_in(g);
   gemm(g);
   std::memset(&g, 0, sizeof(g));
   g.A = dec_ff16_; g.lda = ff; g.M = B; g.K = ff; g.nseg = 1; g.seg[0] = L.wdown.w; g.N = d; g.ldc = d;
   if (tp) { g.C = attn_; g.epi = GEPI_STORE; } else { g.C = x_; g.epi = GEPI_ACCUM; }
   // the next consumer: layer l + 1's QKV, or the lm_head after the last layer
-  if (fn) nrm_out(g, l + 1 < cfg_.n_layers ? layers_[l + 1].attn_norm : out_norm_);
-  nrm_lm_ = fn && l + 1 == cfg_.n_layers;
+  const float* g_next = l + 1 < cfg_.n_layers ? layers_[l + 1].attn_norm : out_norm_;
+  if (fn) nrm_out(g, g_next);
+  nrm_lm_ = (fn || tpn) && l + 1 == cfg_.n_layers;
+  lm_nrm_in_ = tpn ? tpn_part_ : nrm_part_;
+  lm_nrm_parts_ = tpn ? tpn_parts_ : nrm_parts_;
   gemm(g);
-  if (tp) allreduce(attn_, (size_t)B * d, x_);
+  if (tp) tp_reduce(attn_, g_next);
 }
 
 // MALL prefetch carried by the batch-1 attention launch (PfSpec, ops.h): the whole O matrix and a
@@ -1125,7 +1150,7 @@ void Engine::lm_head(int B, const float* x, int ldx) {
     std::memset(&g, 0, sizeof(g));
     g.A = dec_a16_; g.lda = d; g.M = B; g.K = d; g.nseg = 1; g.seg[0] = output_.w; g.N = Vl;
     g.C = y; g.ldc = V; g.epi = GEPI_STORE;
-    if (fused) { g.A = dec_xn16_; g.nrm_in = nrm_part_; g.nrm_parts = nrm_parts_; g.nrm_eps = cfg_.norm_eps; }
+    if (fused) { g.A = dec_xn16_; g.nrm_in = lm_nrm_in_; g.nrm_parts = lm_nrm_parts_; g.nrm_eps = cfg_.norm_eps; }
     gemm(g);
   } else {
     gemv({&output_}, Vl, d, B, x, ldx, out_norm_, y, V, EPI_STORE, 0);

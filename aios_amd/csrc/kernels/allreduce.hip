@@ -76,11 +76,55 @@ __device__ __forceinline__ void put(float* data, float* residual, size_t i, floa
   }
 }
 
+// ---- split-RMSNorm producer (ResidNorm, ops.h) for one RNORM_COLS-column block j of row m: r holds
+// this thread's 4 new residual values at column j * RNORM_COLS + 4 t.  The block's sum of squares is
+// reduced in a fixed order, so every TP rank (same residual bits) writes the same parts.  Every
+// thread of the workgroup calls it.
+static_assert(AR_CHUNK == RNORM_COLS, "one all-reduce workgroup = one norm column block");
+__device__ __forceinline__ void norm_block(const ResidNorm& nm, int m, int j, int ncb, int t, float4 r) {
+  __shared__ float s_red[AR_THREADS / 64];
+  const int col = j * RNORM_COLS + 4 * t;
+  const float4 g = *(const float4*)(nm.g + col);
+  *(uint2*)(nm.out16 + (size_t)m * nm.ld16 + col) =
+      make_uint2((uint32_t)f32_to_bf16(r.x * g.x) | ((uint32_t)f32_to_bf16(r.y * g.y) << 16),
+                 (uint32_t)f32_to_bf16(r.z * g.z) | ((uint32_t)f32_to_bf16(r.w * g.w) << 16));
+  float s = r.x * r.x + r.y * r.y + r.z * r.z + r.w * r.w;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  if ((t & 63) == 0) s_red[t >> 6] = s;
+  __syncthreads();
+  if (t == 0) {
+    float tot = 0.f;
+#pragma unroll
+    for (int w = 0; w < AR_THREADS / 64; ++w) tot += s_red[w];
+    nm.part[(size_t)m * nm.parts + j] = tot;
+  }
+  if (j == 0 && t >= ncb && t < nm.parts) nm.part[(size_t)m * nm.parts + t] = 0.f;  // padding parts
+}
+
+// residual += data (data null: residual already holds the sum), then the norm outputs
+__global__ __launch_bounds__(AR_THREADS) void add_norm_kernel(float* __restrict__ residual, const float* __restrict__ data,
+                                                              int d, ResidNorm nm) {
+  const int j = blockIdx.x, m = blockIdx.y, t = threadIdx.x;
+  const size_t i = (size_t)m * d + (size_t)j * RNORM_COLS + 4 * t;
+  float4 r = *(const float4*)(residual + i);
+  if (data) {
+    const float4 v = *(const float4*)(data + i);
+    r.x += v.x; r.y += v.y; r.z += v.z; r.w += v.w;
+    *(float4*)(residual + i) = r;
+  }
+  norm_block(nm, m, j, d / RNORM_COLS, t, r);
+}
+
 // ---- one-shot: every rank pulls every peer's whole partial (decode-size messages).  The sum runs
 // in rank order on every rank (own partial at its rank's position), so all ranks produce the
-// bit-identical result and their on-device samplers stay in lock step.
+// bit-identical result and their on-device samplers stay in lock step.  NORM (C1 / C2 of the
+// batched TP decode): residual required, n = rows * d with d % RNORM_COLS == 0, and the workgroup
+// also writes the split-RMSNorm outputs of its column block (no separate RMSNorm launch).
+template <bool NORM>
 __global__ __launch_bounds__(AR_THREADS) void allreduce_oneshot(const ArDevCtx* __restrict__ c, float* __restrict__ data,
-                                                                 size_t n, float* __restrict__ residual) {
+                                                                 size_t n, float* __restrict__ residual, int d,
+                                                                 ResidNorm nm) {
   __shared__ uint32_t s_e;
   const int g = blockIdx.x, t = threadIdx.x;
   const int rank = c->rank, world = c->world;
@@ -101,6 +145,14 @@ __global__ __launch_bounds__(AR_THREADS) void allreduce_oneshot(const ArDevCtx* 
         const float4 v = p == rank ? *(const float4*)(data + i) : ld_peer(c->buf[p] + half + i);
         acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
       }
+    }
+    if constexpr (NORM) {
+      float4 r = *(const float4*)(residual + i);
+      r.x += acc.x; r.y += acc.y; r.z += acc.z; r.w += acc.w;
+      *(float4*)(residual + i) = r;
+      const size_t e0 = (size_t)g * AR_CHUNK;  // the workgroup's first element: one row, one column block
+      norm_block(nm, (int)(e0 / d), (int)(e0 % d) / RNORM_COLS, d / RNORM_COLS, t, r);
+      return;
     }
     put(data, residual, i, acc);
   } else {
@@ -231,7 +283,15 @@ void launch_allreduce(const ArDevCtx* ctx, int world, float* data, size_t n, flo
   (void)world;
   if (n == 0) return;
   if (n > AR_MAX_CALL) throw std::runtime_error("launch_allreduce: call above AR_MAX_CALL elements");
-  hipLaunchKernelGGL(allreduce_oneshot, dim3(grid_for(n)), dim3(AR_THREADS), 0, st, ctx, data, n, residual);
+  hipLaunchKernelGGL((allreduce_oneshot<false>), dim3(grid_for(n)), dim3(AR_THREADS), 0, st, ctx, data, n, residual, 0,
+                     ResidNorm{});
+}
+
+void launch_add_norm(float* residual, const float* data, int rows, int d, const ResidNorm& nm, hipStream_t st) {
+  if (rows <= 0) return;
+  if (d % RNORM_COLS || nm.parts < d / RNORM_COLS || nm.parts > 64 || nm.parts % 4)
+    throw std::runtime_error("launch_add_norm: d must be a multiple of 1024 and parts = resid_norm_parts(d)");
+  hipLaunchKernelGGL(add_norm_kernel, dim3(d / RNORM_COLS, rows), dim3(AR_THREADS), 0, st, residual, data, d, nm);
 }
 
 XgmiComm::XgmiComm(int rank, int world, int device, size_t cap_floats) : device_(device) {
@@ -332,6 +392,22 @@ void XgmiComm::allreduce(float* data, size_t n, float* residual, hipStream_t st)
   }
 }
 
+void XgmiComm::allreduce_norm(float* data, int rows, int d, float* residual, const ResidNorm& nm, hipStream_t st) {
+  if (!connected_) throw std::runtime_error("XgmiComm: allreduce before connect()");
+  const size_t n = (size_t)rows * d;
+  if (h_.world == 1) {
+    launch_add_norm(residual, data, rows, d, nm, st);
+  } else if (d % RNORM_COLS == 0 && n <= h_.cap && n < two_shot_min_) {
+    if (nm.parts < d / RNORM_COLS || nm.parts > 64 || nm.parts % 4)
+      throw std::runtime_error("XgmiComm::allreduce_norm: parts must be resid_norm_parts(d)");
+    hipLaunchKernelGGL((allreduce_oneshot<true>), dim3(grid_for(n)), dim3(AR_THREADS), 0, st, d_, data, n, residual, d,
+                       nm);
+  } else {
+    allreduce(data, n, residual, st);
+    launch_add_norm(residual, nullptr, rows, d, nm, st);
+  }
+}
+
 void XgmiComm::allgather_cols(float* data, int rows, int slice, int ld, hipStream_t st) {
   if (!connected_) throw std::runtime_error("XgmiComm: allgather before connect()");
   if (h_.world == 1 || rows <= 0) return;
@@ -353,6 +429,11 @@ void XgmiComm::reset_error() { host_error_[0] = 0; }
 
 void XgmiComm::hook(void* self, float* data, size_t n, float* residual, hipStream_t st) {
   static_cast<XgmiComm*>(self)->allreduce(data, n, residual, st);
+}
+
+void XgmiComm::norm_hook(void* self, float* data, int rows, int d, float* residual, const ResidNorm& nm,
+                         hipStream_t st) {
+  static_cast<XgmiComm*>(self)->allreduce_norm(data, rows, d, residual, nm, st);
 }
 
 void XgmiComm::gather_hook(void* self, float* data, int rows, int slice, int ld, hipStream_t st) {

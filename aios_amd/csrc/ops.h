@@ -29,6 +29,21 @@ void launch_rmsnorm_bf16(const float* x, int ldx, const float* w, bf16_t* y, int
 void launch_f32_to_bf16(const float* x, bf16_t* y, size_t n, hipStream_t st);
 void launch_add(float* y, const float* x, size_t n, hipStream_t st);
 
+// Producer side of the split RMSNorm after a TP all-reduce (the skinny GEMM's nrm_in contract,
+// GemmQArgs below): out16[m][:] = bf16(x_new[m][:] * g) and part[m * parts + j] = sum of x_new^2 over
+// the j-th 1024-column block of row m (parts = round_up(d / 1024, 4) <= 64, the tail parts zero).
+constexpr int RNORM_COLS = 1024;
+struct ResidNorm {
+  const float* g;   // [d] RMSNorm weight of the consumer
+  bf16_t* out16;    // [rows][ld16]
+  int ld16;
+  float* part;      // [rows][parts]
+  int parts;
+};
+inline int resid_norm_parts(int d) { return d % RNORM_COLS ? 0 : ((d / RNORM_COLS + 3) & ~3); }
+// residual[m][:] += data[m][:] (data may be null: residual already holds the sum), then the outputs above
+void launch_add_norm(float* residual, const float* data, int rows, int d, const ResidNorm& nm, hipStream_t st);
+
 // out[b][i] = silu(gu[b][2i]) * gu[b][2i+1]
 void launch_swiglu_interleaved(const float* gu, int ldg, float* out, int ldo, int rows, int n, hipStream_t st);
 void launch_swiglu_interleaved_bf16(const float* gu, int ldg, bf16_t* out, int ldo, int rows, int n, hipStream_t st);

@@ -110,6 +110,12 @@ void RcclComm::allreduce(float* data, size_t n, float* residual, hipStream_t st)
   if (residual) launch_add(residual, data, n, st);
 }
 
+void RcclComm::allreduce_norm(float* data, int rows, int d, float* residual, const ResidNorm& nm, hipStream_t st) {
+  const size_t n = (size_t)rows * d;
+  if (world_ > 1) check(need().AllReduce(data, data, n, ncclFloat32, ncclSum, (ncclComm_t)comm_, st), "ncclAllReduce");
+  launch_add_norm(residual, data, rows, d, nm, st);
+}
+
 void RcclComm::allgather_cols(float* data, int rows, int slice, int ld, hipStream_t st) {
   if (world_ == 1) return;
   if (slice * world_ > ld) throw std::invalid_argument("RcclComm::allgather_cols: slice * world > ld");
@@ -133,6 +139,11 @@ bool RcclComm::error() const {
 
 void RcclComm::hook(void* self, float* data, size_t n, float* residual, hipStream_t st) {
   static_cast<RcclComm*>(self)->allreduce(data, n, residual, st);
+}
+
+void RcclComm::norm_hook(void* self, float* data, int rows, int d, float* residual, const ResidNorm& nm,
+                         hipStream_t st) {
+  static_cast<RcclComm*>(self)->allreduce_norm(data, rows, d, residual, nm, st);
 }
 
 void RcclComm::gather_hook(void* self, float* data, int rows, int slice, int ld, hipStream_t st) {

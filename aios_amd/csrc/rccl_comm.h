@@ -19,6 +19,8 @@
 #include <cstddef>
 #include <string>
 
+#include "ops.h"
+
 namespace aios {
 
 class RcclComm {
@@ -34,6 +36,9 @@ class RcclComm {
   // sum n floats of `data` over the ranks (in place); with `residual`, the sum is then added into
   // it (the engine's C1/C2 contract: residual += sum of partials)
   void allreduce(float* data, size_t n, float* residual, hipStream_t st);
+  // the same into `residual` ([rows][d]) with the split-RMSNorm producer outputs (ResidNorm, ops.h)
+  // written by the residual-add kernel that follows the library all-reduce
+  void allreduce_norm(float* data, int rows, int d, float* residual, const ResidNorm& nm, hipStream_t st);
   // every rank owns columns [r*slice, (r+1)*slice) of the rows x ld fp32 matrix `data`; afterwards
   // every rank holds all columns (in-place ncclAllGather per row, grouped)
   void allgather_cols(float* data, int rows, int slice, int ld, hipStream_t st);
@@ -44,6 +49,8 @@ class RcclComm {
 
   static void hook(void* self, float* data, size_t n, float* residual, hipStream_t st);
   static void gather_hook(void* self, float* data, int rows, int slice, int ld, hipStream_t st);
+  static void norm_hook(void* self, float* data, int rows, int d, float* residual, const ResidNorm& nm,
+                        hipStream_t st);
 
  private:
   int rank_ = 0, world_ = 1, device_ = 0;

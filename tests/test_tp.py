@@ -151,6 +151,33 @@ def test_tp_xgmi_allreduce_and_sharded_model(tmp_path, world, gemm_prefill, prom
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("norm_fuse", [1, 0])
+def test_tp_batched_decode_fused_norm(tmp_path, norm_fuse):
+    """Batched TP decode (B = 6: the skinny-GEMM path) with C1 / C2 fused with the next RMSNorm: the
+    all-reduce writes bf16(x * g) and per-1024-column sums of squares (d_model 2048: two real parts,
+    two zero pads) that the gate/up / next QKV / lm_head GEMMs consume -- every row's logits against
+    the unsharded engine at the same batch; norm_fuse 0 is the separate-RMSNorm control.  Also the
+    fused collective itself (one-shot and the two-shot + add-norm fallback) against torch."""
+    out = tmp_path / "tpb.json"
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(29680 + norm_fuse),
+           os.path.join(ROOT, "tools", "tp_check.py"), "--out", str(out), "--model", "test-tp8-shape",
+           "--prompt-len", "21", "--batch", "6", "--steps", "6"]
+    env = dict(os.environ, AIOS_TP_NORM_FUSE=str(norm_fuse))
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    res = json.loads(out.read_text())
+    assert not res["comm_error_flag"] and not res["comm_error_flag_model"]
+    for e in res["allreduce_norm"]:
+        tol = 2 * e["scale"] * 2.0 ** -8 if e["two_shot"] else 1e-4
+        assert e["resid_err"] < tol, e
+        assert e["out16_rel"] < 2.0 ** -7 and e["part_rel"] < (1e-2 if e["two_shot"] else 1e-5), e
+    assert any(e["two_shot"] for e in res["allreduce_norm"])
+    b = res["batched"]
+    assert max(b["decode_logit_max_abs_diff_per_step"]) < 1e-2 * max(1.0, b["logit_scale"]), b
+
+
+@pytest.mark.gpu
 def test_runtime_serves_tp_model(tmp_path):
     """ModelManager hosts a TP=2 strategic model (worker process + xGMI all-reduce) and its
     greedy generations through the continuous-batching scheduler equal the TP=1 model's."""
@@ -229,6 +256,21 @@ def test_rccl_comm_single_rank():
     comm.allreduce(data.data_ptr(), data.numel(), res.data_ptr(), st.cuda_stream)
     torch.cuda.synchronize()
     assert torch.allclose(res, want)
+    # fused residual add + split-RMSNorm producer (the batched TP decode's C1 / C2 epilogue)
+    rows, d = 3, 3072
+    parts = m.resid_norm_parts(d)
+    assert parts == 4
+    x, r0, gw = torch.randn(rows, d, device="cuda"), torch.randn(rows, d, device="cuda"), torch.rand(d, device="cuda")
+    r = r0.clone()
+    o16 = torch.empty(rows, d, dtype=torch.bfloat16, device="cuda")
+    pt = torch.full((rows, parts), 5.0, device="cuda")
+    comm.allreduce_norm(x.data_ptr(), rows, d, r.data_ptr(), gw.data_ptr(), o16.data_ptr(), d, pt.data_ptr(), parts,
+                        st.cuda_stream)
+    torch.cuda.synchronize()
+    assert torch.allclose(r, r0 + x)
+    assert torch.allclose(o16.float(), (r * gw).bfloat16().float())
+    wp = torch.cat([(r.reshape(rows, 3, 1024) ** 2).sum(-1), torch.zeros(rows, 1, device="cuda")], 1)
+    assert torch.allclose(pt, wp, rtol=1e-5)
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g):
         comm.allreduce(data.data_ptr(), data.numel(), res.data_ptr(), torch.cuda.current_stream().cuda_stream)

@@ -32,6 +32,9 @@ def main():
     ap.add_argument("--recipe", default="Q4_K_M")
     ap.add_argument("--steps", type=int, default=12)
     ap.add_argument("--prompt-len", type=int, default=21)
+    ap.add_argument("--batch", type=int, default=0,
+                    help="also decode B >= 5 rows (the skinny-GEMM path, C1 / C2 fused with the next RMSNorm) "
+                         "and compare every row's logits against the unsharded engine at the same batch")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -85,6 +88,36 @@ def main():
         torch.cuda.synchronize()
         gerr.append({"rows": rows, "slice": slice_, "err": float((md.cpu() - full).abs().max())})
     res["allgather"] = gerr
+    # fused all-reduce + split-RMSNorm producer (batched TP decode, C1 / C2): residual, bf16(x * g) and
+    # per-1024-column sums of squares (tail parts zero); 40 x 2048 exceeds the one-shot size and takes
+    # the two-shot all-reduce + add-norm fallback
+    from aios_amd.runtime import native
+
+    nerr = []
+    for rows, d in ((1, 2048), (6, 4096), (5, 5120), (40, 2048)):
+        parts = native.require().resid_norm_parts(d)
+        x = torch.randn(rows, d, generator=g)
+        resid = torch.randn(rows, d, generator=g)
+        gw = torch.rand(d, generator=g) + 0.5
+        allx = [torch.zeros(rows, d) for _ in range(world)]
+        dist.all_gather(allx, x)
+        want = resid + torch.stack(allx).sum(0)
+        xd, rd, gd = x.cuda(), resid.cuda(), gw.cuda()
+        o16 = torch.zeros(rows, d, dtype=torch.bfloat16, device="cuda")
+        pd = torch.full((rows, parts), 7.0, device="cuda")
+        comm.allreduce_norm(xd.data_ptr(), rows, d, rd.data_ptr(), gd.data_ptr(), o16.data_ptr(), d, pd.data_ptr(),
+                            parts, st)
+        torch.cuda.synchronize()
+        ncb = d // 1024
+        wp = torch.zeros(rows, parts)
+        wp[:, :ncb] = (want.reshape(rows, ncb, 1024).double() ** 2).sum(-1).float()
+        wx = want * gw
+        nerr.append({"rows": rows, "d": d, "parts": parts, "two_shot": world > 1 and rows * d >= comm.two_shot_min,
+                     "resid_err": float((rd.cpu() - want).abs().max()),
+                     "out16_rel": float((o16.float().cpu() - wx).abs().max() / wx.abs().max()),
+                     "part_rel": float((pd.cpu() - wp).abs().max() / wp.abs().max()),
+                     "scale": float(torch.stack(allx).abs().max())})
+    res["allreduce_norm"] = nerr
     res["comm_error_flag"] = bool(comm.error())
 
     # timing at decode size (B=1, d=8192): one-shot; at prefill size (512 x 8192): two-shot
@@ -113,7 +146,8 @@ def main():
     # rounding differs from TP=1 by design); greedy stream from TP, then TP=1 teacher-forced on
     # the same tokens, comparing logits at every step
     max_ctx = (args.prompt_len + args.steps + 64 + 127) // 128 * 128
-    eng, comm = build_tp_engine(cfg, rank, world, dev, path=path, max_ctx=max_ctx, max_slots=2, max_batch=2,
+    nb = max(2, args.batch)
+    eng, comm = build_tp_engine(cfg, rank, world, dev, path=path, max_ctx=max_ctx, max_slots=nb, max_batch=nb,
                                 act_q8=False)
     res["vocab_parallel"] = bool(eng.vocab_parallel)
     prompt = [cfg.bos_id] + [(11 * i + 5) % (cfg.vocab_size - 3) + 3 for i in range(args.prompt_len - 1)]
@@ -133,10 +167,22 @@ def main():
         tp.decode_loop_run(1, args.steps, True)
         tp.synchronize()
         hist = list(tp.decode_loop_history(1, len(prompt) + 1, args.steps))
+        B = args.batch
+        if B > 1:
+            prompts = [[cfg.bos_id] + [(7 * i + 13 * b + 3) % (cfg.vocab_size - 3) + 3 for i in range(args.prompt_len + b)]
+                       for b in range(B)]
+            btoks = [[int(np.asarray(tp.prefill(b, prompts[b], 0, True)).argmax()) for b in range(B)]]
+            blog = []
+            bpos = [len(p) for p in prompts]
+            for _ in range(args.steps):
+                t = tp.decode(list(range(B)), btoks[-1], bpos, [0.0] * B, [0] * B, 0, b"")
+                blog.append(np.asarray(tp.last_logits(B)).copy())
+                btoks.append([int(v) for v in t])
+                bpos = [p + 1 for p in bpos]
         tp.close()
         from aios_amd.runtime.loader import load_engine
 
-        ref, _, _ = load_engine(path, max_ctx=max_ctx, max_slots=2, max_batch=2, device=dev, act_q8=False)
+        ref, _, _ = load_engine(path, max_ctx=max_ctx, max_slots=nb, max_batch=nb, device=dev, act_q8=False)
         rl = np.asarray(ref.prefill(0, prompt, 0, True))
         pos = len(prompt)
         diffs = []
@@ -151,6 +197,17 @@ def main():
             "decode_logit_max_abs_diff_per_step": diffs, "logit_scale": float(np.abs(rl).max()),
             "graph_tokens_match": [toks[0]] + hist == toks[:len(hist) + 1],
         }
+        if B > 1:
+            for b in range(B):
+                ref.prefill(b, prompts[b], 0, False)
+            bpos = [len(p) for p in prompts]
+            bd = []
+            for i in range(args.steps):
+                ref.decode(list(range(B)), btoks[i], bpos, [0.0] * B, [0] * B, 0, b"")
+                bd.append(float(np.abs(np.asarray(ref.last_logits(B)) - blog[i]).max()))
+                bpos = [p + 1 for p in bpos]
+            res["batched"] = {"B": B, "decode_logit_max_abs_diff_per_step": bd,
+                              "logit_scale": float(max(np.abs(l).max() for l in blog))}
         res["comm_error_flag_model"] = bool(comm.error())
     else:
         worker_loop(eng, comm)
