@@ -233,9 +233,10 @@ class Engine {
   bf16_t* pf_a16_ = nullptr;
   // GEMM prefill workspace (chunks of gm_rows_ tokens through MFMA GEMMs + flash attention)
   int gm_rows_ = 512;
-  // prompts shorter than this take the GEMV path (tools/bench_prefill.py: 8 / 15 tokens 5.66 / 10.97 ms
-  // on the GEMV path, 3.24 / 3.33 ms through the skinny GEMM; equal at 4, GEMV ahead at 3)
-  int gm_min_rows_ = 4;
+  // prompts shorter than this take the GEMV path, whose batched LDS-DMA engine serves up to 4 rows
+  // (tools/bench_prefill.py, round 3: 2 / 3 / 4 tokens 1.85 / 2.02 / 2.29 ms there vs 3.25 ms for 4 through
+  // the skinny GEMM; from 5 rows the GEMV falls back to the row kernels, 8.5 ms, the GEMM 3.25)
+  int gm_min_rows_ = 5;
   bool gm_ok_ = false;    // every layer's weights / head shape supported
   float *gm_x_ = nullptr, *gm_qkv_ = nullptr, *gm_q_ = nullptr, *gm_part_ = nullptr;
   bf16_t *gm_a16_ = nullptr, *gm_ff16_ = nullptr, *gm_attn16_ = nullptr;

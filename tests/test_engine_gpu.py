@@ -143,12 +143,13 @@ def test_prefill_gemm_chunks_match_reference(model_files, recipe, monkeypatch):
     assert (logits2 - rl).abs().max().item() < 2e-2 * scale
 
 
-@pytest.mark.parametrize("T", [4, 8, 15])
+@pytest.mark.parametrize("T", [3, 4, 5, 8, 15])
 @pytest.mark.parametrize("q8", [False, True])
-def test_short_prompt_gemm_prefill_matches_reference(model_files, monkeypatch, T, q8):
-    """4-15-token prompts go through the skinny MFMA GEMM (gm_min_rows_ = 4): their logits against
-    the fp32 reference for both GEMV activation settings (the decode steps' precision differs from
-    the GEMM's bf16 operands; the reference bounds both)"""
+def test_short_prompt_prefill_matches_reference(model_files, monkeypatch, T, q8):
+    """2-4-token prompts go through the batched LDS-DMA GEMV engine (B = T rows), 5-15-token ones
+    through the skinny MFMA GEMM (gm_min_rows_ = 5): their logits against the fp32 reference for both
+    GEMV activation settings (the decode steps' precision differs from the GEMM's bf16 operands; the
+    reference bounds both)"""
     monkeypatch.setenv("AIOS_PREFILL_GEMM", "1")
     path = model_files["mistral_shape"]
     eng, cfg = _load(path, act_q8=q8)
