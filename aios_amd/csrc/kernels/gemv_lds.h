@@ -456,6 +456,52 @@ __global__ void __launch_bounds__(LG_THREADS) gemv_lds_b1(GemvArgs a, CuPlan pl)
           lg_barrier();  // final
           return;
         }
+      } else if constexpr (GPW == 1 && QFmt<QT>::W == 32) {
+        if (L::NGS % nit == 0) {
+          // Q6_K / Q5_K (the Q4_K_M down projection and lm_head): one group per wave per slot, the same K
+          // columns in every slot, so the B rows' x stay in registers (as the B = 1 path below); the
+          // scale decode is shared, the rows' partials fold with one butterfly + a 32-lane swap
+          const int c = (wave % nit) * 64 + lane;
+          int xv[B][8];
+          float4 m[B];
+#pragma unroll
+          for (int b = 0; b < B; ++b) {
+            const int8_t* xc = xq + ((size_t)b * nch + c) * 32;
+            const int rot = (c >> 3) & 1;
+            const uint4 p0 = *(const uint4*)(xc + 16 * rot), p1 = *(const uint4*)(xc + 16 * (rot ^ 1));
+            xv[b][0] = p0.x; xv[b][1] = p0.y; xv[b][2] = p0.z; xv[b][3] = p0.w;
+            xv[b][4] = p1.x; xv[b][5] = p1.y; xv[b][6] = p1.z; xv[b][7] = p1.w;
+            m[b] = *(const float4*)(ms + ((size_t)b * nch + c) * 2);
+          }
+          const int rps = L::NGS / nit, rk = wave / nit;
+          for (int t = 0; t < T; ++t) {
+            if (t * L::NGS + wave < ngroups) {
+              const uint8_t* slot = ring + (size_t)(t % LG_R) * L::slot_bytes;
+              RawChunk raw;
+              lg_read<QT>(slot, wave, lane, raw);
+              float sc[2], of[2];
+              q8_scales_bf<QT>(raw, c, sc, of);
+              float v[B];
+#pragma unroll
+              for (int b = 0; b < B; ++b) {
+                int is[2];
+                QDot<QT>::isums(raw, c, xv[b], is);
+                v[b] = sc[0] * m[b].x * (float)is[0] - of[0] * m[b].y + sc[1] * m[b].z * (float)is[1] - of[1] * m[b].w;
+              }
+              float r = lg_half_sum_rows<B>(v, lane & 31);
+              const auto h = __builtin_amdgcn_permlane32_swap(__float_as_uint(r), __float_as_uint(r), false, false);
+              r = __uint_as_float(h[0]) + __uint_as_float(h[1]);  // both 32-lane halves
+              const int rb = lg_half_row<B>(lane & 31);
+              if (lane < (B > 2 ? 4 : 2) && rb < B)
+                __hip_atomic_fetch_add(&rowacc[rb * pl.racc_n + t * rps + rk], r, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            lg_barrier();
+          }
+          lg_barrier();  // final
+          return;
+        }
       }
       for (int t = 0; t < T; ++t) {
         const int gb = t * L::NGS + wave * GPW;
