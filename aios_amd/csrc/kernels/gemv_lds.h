@@ -280,6 +280,27 @@ __device__ __forceinline__ float lg_half_sum_rows(const float (&v)[B], int p) {
   return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
 
+// the int8 weight codes of a Q6_K / Q5_K chunk (run 0 words, run 1 words) -- QDot::isums without the dots
+template <int QT>
+__device__ __forceinline__ void lg_codes(const RawChunk& r, int c, int (&lo)[4], int (&hi)[4]) {
+  if constexpr (QT == QT_Q6_K) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      lo[i] = (int)QFmt<QT_Q6_K>::code_lo(r, i);
+      hi[i] = (int)QFmt<QT_Q6_K>::code_hi(r, i);
+    }
+  } else {
+    static_assert(QT == QT_Q5_K, "Q6_K / Q5_K only");
+    const int g = (c & 7) >> 1;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint32_t wv = u4_word(r.a, i), hv = u4_word(r.c, i);
+      lo[i] = (int)((wv & 0x0f0f0f0fu) | (((hv >> (2 * g)) & 0x01010101u) << 4));
+      hi[i] = (int)(((wv >> 4) & 0x0f0f0f0fu) | (((hv >> (2 * g + 1)) & 0x01010101u) << 4));
+    }
+  }
+}
+
 // one 64-chunk group of a row against B staged x rows (x read from LDS)
 template <int QT, int B>
 __device__ __forceinline__ void lg_compute_b(const RawChunk& raw, int it, int nch, const int8_t* xq, const float2* ms,
@@ -481,12 +502,19 @@ __global__ void __launch_bounds__(LG_THREADS) gemv_lds_b1(GemvArgs a, CuPlan pl)
               lg_read<QT>(slot, wave, lane, raw);
               float sc[2], of[2];
               q8_scales_bf<QT>(raw, c, sc, of);
+              // the weight codes once, then the B rows' integer dots (isums per row would decode them B times)
+              int lo[4], hi[4];
+              lg_codes<QT>(raw, c, lo, hi);
               float v[B];
 #pragma unroll
               for (int b = 0; b < B; ++b) {
-                int is[2];
-                QDot<QT>::isums(raw, c, xv[b], is);
-                v[b] = sc[0] * m[b].x * (float)is[0] - of[0] * m[b].y + sc[1] * m[b].z * (float)is[1] - of[1] * m[b].w;
+                int s0 = 0, s1 = 0;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                  s0 = __builtin_amdgcn_sdot4(lo[i], xv[b][i], s0, false);
+                  s1 = __builtin_amdgcn_sdot4(hi[i], xv[b][4 + i], s1, false);
+                }
+                v[b] = sc[0] * m[b].x * (float)s0 - of[0] * m[b].y + sc[1] * m[b].z * (float)s1 - of[1] * m[b].w;
               }
               float r = lg_half_sum_rows<B>(v, lane & 31);
               const auto h = __builtin_amdgcn_permlane32_swap(__float_as_uint(r), __float_as_uint(r), false, false);
