@@ -473,8 +473,10 @@ __global__ void __launch_bounds__(LG_THREADS) gemv_lds_b1(GemvArgs a, CuPlan pl)
             }
             lg_barrier();
           }
+          CU_STAMP(4);
           asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
           lg_barrier();  // final
+          CU_STAMP(5);
           return;
         }
       } else if constexpr (GPW == 1 && QFmt<QT>::W == 32) {
@@ -527,7 +529,9 @@ __global__ void __launch_bounds__(LG_THREADS) gemv_lds_b1(GemvArgs a, CuPlan pl)
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             lg_barrier();
           }
+          CU_STAMP(4);
           lg_barrier();  // final
+          CU_STAMP(5);
           return;
         }
       }
@@ -694,6 +698,8 @@ __global__ void __launch_bounds__(LG_THREADS) gemv_lds_b1(GemvArgs a, CuPlan pl)
       gemv_epilogue(a, a.row_base + r0 + 2 * p, b, rowacc[b * pl.racc_n + 2 * p] * s_,
                     rowacc[b * pl.racc_n + 2 * p + 1] * s_);
     }
+    CU_STAMP(6);
+    flush_ts();
     return;
   }
   // ---- pair epilogues: wave 0, one lane per pair

@@ -56,20 +56,22 @@ def main():
                 ms.append(m)
             mats.append(ms)
         N = sum(r for _, r in segs)
-        x = torch.randn(1, K, device="cuda")
+        B = int(os.environ.get("PROBE_B", 1))  # batch rows (B = 2..4: the engine's batched consumers)
+        x = torch.randn(B, K, device="cuda")
         nw = torch.rand(K, device="cuda") + 0.5
-        y = torch.zeros(1, N, device="cuda")
+        y = torch.zeros(B, N, device="cuda")
         epic = getattr(E, "EPI_" + epi)
         ldy = N // 2 if epi == "SWIGLU" else N
 
         def launch(ms, sel, ts=0):
             st = torch.cuda.current_stream().cuda_stream
             # sel 4: the LDS engine with its consumers skipping the dot work (bare ring cadence)
-            E.gemv(ms, 1, x.data_ptr(), K, nw.data_ptr() if norm else 0, 1e-5, y.data_ptr(), ldy, epic, st, 0, 1,
+            E.gemv(ms, B, x.data_ptr(), K, nw.data_ptr() if norm else 0, 1e-5, y.data_ptr(), ldy, epic, st, 0, 1,
                    kernel_sel=3 if sel == 4 else sel, tune_dbg=0x10000 if sel == 4 else 0, dbg_ts=ts)
 
-        row = dict(shape=name, mb=round(nbytes / 1e6, 1))
-        for sel, tag in ((1, "rows"), (2, "cu"), (3, "lds"), (4, "ring"), (0, "auto")):
+        row = dict(shape=name, B=B, mb=round(nbytes / 1e6, 1))
+        sels = ((1, "rows"), (2, "cu"), (3, "lds"), (4, "ring"), (0, "auto")) if B == 1 else ((3, "lds"), (1, "rows"))
+        for sel, tag in sels:
             for ms in mats:
                 launch(ms, sel)
             torch.cuda.synchronize()
