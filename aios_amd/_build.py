@@ -69,8 +69,7 @@ def _flags():
 # per group in a VALU-issue-bound loop) although only one lane is active.  Off for the GEMV objects
 # (elementwise.hip's many-lane candidate counters keep it).
 _NO_ATOMIC_OPT = ["-mllvm", "-amdgpu-atomic-optimizer-strategy=None"]
-_FILE_FLAGS = {n: _NO_ATOMIC_OPT for n in ("gemv_kquant.hip", "gemv_kquant2.hip", "gemv_legacy.hip",
-                                           "decode_mk.hip", "attn_block.hip")}
+_FILE_FLAGS = {n: _NO_ATOMIC_OPT for n in ("gemv_kquant.hip", "gemv_kquant2.hip", "gemv_legacy.hip")}
 
 
 def _compile(src: Path, flags, hipcc) -> Path:

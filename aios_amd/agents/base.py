@@ -285,6 +285,24 @@ class BaseAgent(ABC):
             logger.info("think unavailable: %s", e.details())
             return ""
 
+    async def safety_check(self, prompt: str, level: IntelligenceLevel | str = IntelligenceLevel.OPERATIONAL,
+                           **kw) -> Optional[str]:
+        """think() at a gate in front of a side effect (firewall rule, service restart, package
+        install/remove, backup, restore): the model's answer, or None when the runtime is unreachable or
+        answers nothing.  Callers fail closed on None -- the reference calls think() directly at these
+        sites (agents/network.py:329, agents/system.py:238), so its RPC error fails the task."""
+        try:
+            text = (await self.think(prompt, level, **kw)).strip()
+        except grpc.aio.AioRpcError as e:
+            logger.warning("safety check unavailable: %s", e.details())
+            return None
+        return text or None
+
+    @staticmethod
+    def safety_unavailable(action: str, **extra) -> Dict[str, Any]:
+        return {"success": False, "error": f"safety check unavailable: not {action} without the model's review",
+                **extra}
+
     @staticmethod
     def advice_lines(text: str, n: int = 5) -> List[str]:
         """the first n non-empty lines of a model answer, list markers stripped"""

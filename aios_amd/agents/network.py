@@ -88,8 +88,10 @@ class NetworkAgent(BaseAgent):
                     return {"success": False, "error": "no rule / port in task"}
                 rule = f"tcp dport {m.group(1)} {'drop' if 'block' in d else 'accept'}"
             # lock-out check by the model before the rule goes in (reference network.py:329)
-            safety = await self.analyze(f"A firewall rule is being added: {rule}. Is this safe? Could it lock us out "
-                                        "of the system? Answer YES or NO.", IntelligenceLevel.OPERATIONAL)
+            safety = await self.safety_check(f"A firewall rule is being added: {rule}. Is this safe? Could it lock "
+                                             "us out of the system? Answer YES or NO.", IntelligenceLevel.OPERATIONAL)
+            if safety is None:
+                return self.safety_unavailable("adding the firewall rule", rule=rule)
             if safety.lower().lstrip(" *\"'").startswith("no"):
                 return {"success": False, "error": f"Firewall rule rejected by safety check: {safety}", "rule": rule}
             return await self.call_tool("firewall.add_rule", {"chain": inp.get("chain", "input"), "rule": rule})

@@ -46,12 +46,14 @@ class PackageAgent(BaseAgent):
                 if name in str(f.get("package", f.get("issue", ""))).lower()
                 and str(f.get("severity", "")).lower() in ("critical", "high")]
         if cves and not (task.get("input") or {}).get("force"):
-            decision = await self.analyze(
+            decision = await self.safety_check(
                 f"Package '{name}' has {len(cves)} critical/high advisories:\n" +
                 "\n".join(f"- {c.get('cve', 'N/A')}: {str(c.get('description', c.get('issue', '')))[:100]}"
                           for c in cves[:5]) +
                 "\n\nShould I still install it? Consider the risk vs. necessity. Answer INSTALL or SKIP with "
                 "brief reason.", IntelligenceLevel.TACTICAL)
+            if decision is None:
+                return self.safety_unavailable(f"installing {name}", advisories=cves)
             if "skip" in decision.lower()[:10]:
                 return {"success": False, "error": f"skipped {name}: {decision}", "advisories": cves}
         r = await self.call_tool("pkg.install", {"name": name}, reason=f"install {name}")
@@ -74,9 +76,11 @@ class PackageAgent(BaseAgent):
                       if isinstance(p, dict) and p.get("name") != name
                       and name in " ".join(map(str, p.get("depends", [])))][:10]
         if dependents and not (task.get("input") or {}).get("force"):
-            check = await self.analyze(
+            check = await self.safety_check(
                 f"Package '{name}' is required by: {dependents}. Is it safe to remove? Could it break the system? "
                 "Answer REMOVE or KEEP with reason.", IntelligenceLevel.OPERATIONAL)
+            if check is None:
+                return self.safety_unavailable(f"removing {name}", dependents=dependents)
             if "keep" in check.lower()[:10]:
                 return {"success": False, "error": f"kept {name}: {check}", "dependents": dependents}
         return await self.call_tool("pkg.remove", {"name": name}, reason=f"remove {name}")

@@ -62,10 +62,12 @@ class StorageAgent(BaseAgent):
             return {"success": False, "error": f"not enough space for backup of {src}"}
         if need and need > 0.9 * avail:
             # tight on space: let the model decide between proceeding and aborting (reference
-            # storage.py:244); an unavailable runtime proceeds (the copy itself still checks space)
-            decision = await self.analyze(
+            # storage.py:244); an unavailable runtime aborts (fail closed, as the reference's think())
+            decision = await self.safety_check(
                 f"Backup of {src} estimated at {need / 1e9:.1f}GB but only {avail / 1e9:.1f}GB available. "
                 "Should I proceed, skip some paths, or abort?", IntelligenceLevel.OPERATIONAL)
+            if decision is None:
+                return self.safety_unavailable(f"backing up {src} into a nearly full disk")
             if "abort" in decision.lower():
                 return {"success": False, "error": f"aborted: backup of {src} would not fit",
                         "ai_decision": decision}
@@ -96,8 +98,10 @@ class StorageAgent(BaseAgent):
         if not st["success"]:
             return {"success": False, "error": f"backup {src} missing"}
         # safety review before overwriting (reference storage.py:359)
-        safety = await self.analyze(f"About to restore backup {src} to {dst}. Is this safe? What could go wrong?",
-                                    IntelligenceLevel.TACTICAL)
+        safety = await self.safety_check(f"About to restore backup {src} to {dst}. Is this safe? What could go "
+                                         "wrong?", IntelligenceLevel.TACTICAL)
+        if safety is None and not inp.get("dry_run"):
+            return self.safety_unavailable(f"restoring {src} over {dst}")
         if inp.get("dry_run"):
             return {"success": True, "dry_run": True, "restored": None, "from": src, "to": dst, "safety": safety}
         r = await self.call_tool("fs.copy", {"source": src, "destination": dst, "recursive": True})

@@ -82,10 +82,13 @@ class SystemAgent(BaseAgent):
         previous = str(pre.get("output", {}).get("status", "unknown")) if pre.get("success") else "unknown"
         if previous in ("running", "active"):
             # a running service is restarted only if the model judges it safe (reference system.py:238)
-            verdict = await self.analyze(
+            verdict = await self.safety_check(
                 f"Service '{name}' is currently running (status: {previous}). Should I restart it? Consider: is it "
                 "a critical service? What are the risks? Answer YES or NO with a brief reason.",
                 IntelligenceLevel.OPERATIONAL)
+            if verdict is None:
+                return self.safety_unavailable(f"restarting the running service {name}", service=name,
+                                               previous_status=previous)
             if verdict.lower().lstrip(" *\"'").startswith("no"):
                 return {"success": False, "service": name, "action": "restart_skipped", "reason": verdict,
                         "previous_status": previous}

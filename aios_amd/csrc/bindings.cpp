@@ -242,20 +242,6 @@ PYBIND11_MODULE(_engine, m) {
       .def_property_readonly("kv_blocks_free", &Engine::kv_blocks_free)
       .def_property_readonly("kv_blocks_total", &Engine::kv_blocks_total)
       .def_property_readonly("norm_fused_parts", &Engine::norm_fused_parts)
-      .def_property_readonly("mk_available", &Engine::mk_available)
-      .def_property("mk_enabled", &Engine::mk_enabled, &Engine::set_mk)
-      .def("mk_probe",
-           [](Engine& e, int dbg) {
-             std::vector<unsigned long long> v;
-             {
-               py::gil_scoped_release nogil;
-               v = e.mk_probe(dbg);
-             }
-             py::array_t<unsigned long long> a({(py::ssize_t)e.mk_grid(), (py::ssize_t)e.mk_nstages(), (py::ssize_t)8});
-             std::memcpy(a.mutable_data(), v.data(), v.size() * 8);
-             return a;
-           },
-           py::arg("dbg") = 0)
       .def("capture_graphs", &Engine::capture_graphs, py::arg("max_b"), py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("stream", &Engine::stream_handle)
       .def_property_readonly("k_cache_ptr", &Engine::kv_cache_k)

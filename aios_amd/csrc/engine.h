@@ -16,7 +16,6 @@
 
 #include "common.h"
 #include "ops.h"
-#include "mk.h"
 
 namespace aios {
 
@@ -138,15 +137,6 @@ class Engine {
   int kv_blocks_free() const { return (int)free_blocks_.size(); }
   int kv_blocks_total() const { return kv_nblocks_; }
   int norm_fused_parts() const { return nrm_parts_; }  // 0: batched-decode RMSNorm not split into the GEMMs
-  // persistent batch-1 decode step (kernels/decode_mk.hip): available / switched on
-  bool mk_available() const { return mk_ok_; }
-  void set_mk(bool on) { if (mk_enabled_ != on) { mk_enabled_ = on; reset_graphs(); } }
-  bool mk_enabled() const { return mk_enabled_; }
-  // probes: one eager persistent decode step (rows prepared by decode_loop_prepare) with phase
-  // stamps; returns [grid][nstages][8] s_memrealtime ticks (100 MHz)
-  std::vector<unsigned long long> mk_probe(int dbg = 0);
-  int mk_nstages() const { return mk_args_.nstages; }
-  int mk_grid() const { return mk_grid_; }
   std::vector<int> block_table(int slot) const;
 
   // raw device pointers for tests / custom kernels
@@ -162,8 +152,6 @@ class Engine {
             float* y, int ldy, int epi, int layer);
   GemvArgs gemv_args(const std::vector<const QMat*>& segs, int N, int K, int B, const float* x, int ldx,
                      const float* norm_w, float* y, int ldy, int epi, int layer);
-  bool attn_block_on(int B) const;
-  PfSpec attn_prefetch_spec(int l) const;  // MALL prefetch role of the batch-1 attention launch
   QMat alloc_qmat(int qt, int rows, int cols);
   QMat upload_qmat(int qt, int rows, int cols, const void* host, size_t nbytes);
   // load-time staging: two device buffers (tensor i repacks while i+1 uploads) fed through two
@@ -220,12 +208,6 @@ class Engine {
   uint8_t* d_mask_ = nullptr;
   int n_chunks_ = 0;
   int* attn_cnt_ = nullptr;  // [max(prefill_rows, max_batch)][n_kv_heads] combine tickets
-  // fused batch-1 attention block (kernels/attn_block.hip): per layer [QKV arrivals, heads
-  // published] hand-off counters zeroed at the start of every decode step, + a give-up flag
-  int* fuse_cnt_ = nullptr;
-  int* fuse_err_ = nullptr;
-  int fuse_attn_ = 0;        // AIOS_FUSE_ATTN: 0 three launches (default), 1 attention + O fused, 2 all three
-  void check_fuse_err();
   float2* rope_cs_ = nullptr;  // [max_ctx][head_dim/2] cos/sin computed in double on the host
   int prefill_rows_ = 64;  // rows of the prefill workspace
   float *pf_x_ = nullptr, *pf_q_ = nullptr, *pf_attn_ = nullptr, *pf_ff_ = nullptr, *pf_qkv_ = nullptr;
@@ -291,15 +273,6 @@ class Engine {
   void kv_sync(int B);                                 // upload dirty tables (rows 0..B-1)
 
   std::map<int, hipGraphExec_t> graphs_;
-  // persistent decode kernel state
-  bool mk_ok_ = false, mk_enabled_ = false;
-  int mk_grid_ = 0;
-  MkArgs mk_args_{};
-  MkStage* d_mk_stages_ = nullptr;
-  int* mk_cnt_ = nullptr;
-  void mk_build();
-  bool mk_use(int B) const;
-  bool check_mk_err();  // true (and the persistent path switched off) when a launch gave up
   AllReduceFn allreduce_ = nullptr;
   void* allreduce_ctx_ = nullptr;
   AllGatherFn allgather_ = nullptr;

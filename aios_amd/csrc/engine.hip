@@ -457,11 +457,6 @@ void Engine::finalize() {
     const size_t nc = (size_t)std::max(prefill_rows_, Bm) * H;  // decode attention tickets [row][head]
     attn_cnt_ = (int*)dmalloc(nc * 4);
     HIP_CHECK(hipMemset(attn_cnt_, 0, nc * 4));
-    fuse_cnt_ = (int*)dmalloc(((size_t)cfg_.n_layers * 2 + 1) * 4);
-    HIP_CHECK(hipMemset(fuse_cnt_, 0, ((size_t)cfg_.n_layers * 2 + 1) * 4));
-    fuse_err_ = fuse_cnt_ + (size_t)cfg_.n_layers * 2;
-    const char* fe = std::getenv("AIOS_FUSE_ATTN");
-    fuse_attn_ = fe ? std::atoi(fe) : 0;  // measured slower than three launches: opt-in
   }
   {
     const int half = hd / 2;
@@ -607,118 +602,8 @@ void Engine::finalize() {
     }
   }
   ws_bytes_ = ws;
-  mk_build();
   HIP_CHECK(hipDeviceSynchronize());
   finalized_ = true;
-}
-
-// The persistent batch-1 decode kernel (kernels/decode_mk.hip): one launch per step instead of
-// 5 per layer.  Served shapes: tp 1, int8 GEMV activations, K-quant weights (Q4_K / Q5_K / Q6_K),
-// interleaved (non-NeoX) RoPE without QK-norm or QKV bias, and an LDS plan that fits 160 KB.
-// It is built whenever the shape is served and enabled by AIOS_MK=1 (or set_mk): until it beats
-// the launch-per-op path on the bench model that path serves batch 1.  AIOS_MK=0 skips the build.
-void Engine::mk_build() {
-  mk_ok_ = false;
-  if (const char* e = std::getenv("AIOS_MK")) {
-    if (std::atoi(e) == 0) return;
-    mk_enabled_ = std::atoi(e) == 1;
-  }
-  if (cfg_.tp_size != 1 || !cfg_.act_q8 || cfg_.qk_norm || cfg_.rope_neox || !rope_cs_) return;
-  const int d = cfg_.d_model, hd = cfg_.head_dim, H = cfg_.n_heads, Hkv = cfg_.n_kv_heads;
-  const int qd = H * hd, kvd = Hkv * hd;
-  std::vector<MkStage> st;
-  auto proj = [&](int kind, int l, int K, std::vector<const QMat*> segs, const float* nw) {
-    MkStage s;
-    std::memset(&s, 0, sizeof(s));
-    s.kind = kind; s.layer = l; s.K = K; s.nseg = (int)segs.size(); s.norm_w = nw;
-    int row = 0;
-    for (int i = 0; i < s.nseg; ++i) { s.seg[i] = segs[i]->w; s.seg_row0[i] = row; row += segs[i]->w.rows; }
-    s.k_cache = k_cache_ + (size_t)l * layer_kv_elems_;
-    s.v_cache = v_cache_ + (size_t)l * layer_kv_elems_;
-    st.push_back(s);
-  };
-  for (int l = 0; l < cfg_.n_layers; ++l) {
-    const LayerW& L = layers_[l];
-    if (L.bqkv) return;
-    if (L.wq.w.rows != qd || L.wk.w.rows != kvd || L.wv.w.rows != kvd) return;
-    proj(MK_QKV, l, d, {&L.wq, &L.wk, &L.wv}, L.attn_norm);
-    proj(MK_ATT, l, 0, {}, nullptr);
-    proj(MK_O, l, qd, {&L.wo}, nullptr);
-    proj(MK_GU, l, d, {&L.wgu}, L.ffn_norm);
-    proj(MK_DOWN, l, cfg_.d_ff, {&L.wdown}, nullptr);
-  }
-  if (output_.w.rows != cfg_.vocab_size) return;
-  proj(MK_LM, cfg_.n_layers, d, {&output_}, out_norm_);
-  MkArgs& a = mk_args_;
-  std::memset(&a, 0, sizeof(a));
-  a.nstages = (int)st.size();
-  a.d = d; a.q_dim = qd; a.kv_dim = kvd; a.n_heads = H; a.n_kv_heads = Hkv; a.head_dim = hd;
-  a.d_ff = cfg_.d_ff; a.vocab = cfg_.vocab_size; a.eps = cfg_.norm_eps;
-  a.attn_scale = 1.f / std::sqrt((float)hd);
-  a.rope_cs = rope_cs_; a.max_ctx = cfg_.max_ctx;
-  a.n_layers = cfg_.n_layers;
-  mk_grid_ = device_cu_count();
-  if (!mk_plan(a, st, mk_grid_)) return;
-  d_mk_stages_ = (MkStage*)dmalloc(st.size() * sizeof(MkStage));
-  HIP_CHECK(hipMemcpy(d_mk_stages_, st.data(), st.size() * sizeof(MkStage), hipMemcpyHostToDevice));
-  const size_t nints = mk_counter_ints(a.nstages, cfg_.n_layers, Hkv);
-  mk_cnt_ = (int*)dmalloc(nints * 4);
-  HIP_CHECK(hipMemset(mk_cnt_, 0, nints * 4));
-  a.stages = d_mk_stages_;
-  a.cnt = mk_cnt_;
-  a.tick = mk_cnt_ + (size_t)a.nstages * 8 * 32;
-  a.done = a.tick + (size_t)cfg_.n_layers * Hkv * 32;
-  a.err = a.done + 32;
-  a.o_part = (float*)dmalloc((size_t)H * MK_MAXU * hd * 4);
-  a.ml = (float*)dmalloc((size_t)H * MK_MAXU * 2 * 4);
-  a.pos = d_pos_; a.seq_len = d_seqlen_; a.slot = d_slot_; a.block_table = d_bt_;
-  a.x = x_; a.q = q_; a.attn = attn_; a.ffb = ff_; a.logits = logits_;
-  a.timeout_us = 20000;
-  if (const char* e = std::getenv("AIOS_MK_TIMEOUT_US")) a.timeout_us = std::max(100, std::atoi(e));
-  mk_ok_ = true;
-}
-
-std::vector<unsigned long long> Engine::mk_probe(int dbg) {
-  if (!mk_ok_) throw std::runtime_error("mk_probe: persistent decode kernel not available");
-  HIP_CHECK(hipSetDevice(cfg_.device));
-  const size_t n = (size_t)mk_grid_ * mk_args_.nstages * 8;
-  unsigned long long* d = nullptr;
-  HIP_CHECK(hipMalloc(&d, n * 8));
-  HIP_CHECK(hipMemset(d, 0, n * 8));
-  const bool was = mk_enabled_;
-  mk_enabled_ = true;
-  mk_args_.ts = d;
-  mk_args_.dbg = dbg;
-  try {
-    enqueue_decode_step(1);  // eager: the captured graphs keep a.ts == null
-    HIP_CHECK(hipStreamSynchronize(stream_));
-  } catch (...) {
-    mk_args_.ts = nullptr;
-    mk_args_.dbg = 0;
-    mk_enabled_ = was;
-    hipFree(d);
-    throw;
-  }
-  mk_args_.ts = nullptr;
-  mk_args_.dbg = 0;
-  mk_enabled_ = was;
-  std::vector<unsigned long long> out(n);
-  HIP_CHECK(hipMemcpy(out.data(), d, n * 8, hipMemcpyDeviceToHost));
-  HIP_CHECK(hipFree(d));
-  return out;
-}
-
-bool Engine::mk_use(int B) const { return mk_ok_ && mk_enabled_ && B == 1 && !attn_block_on(B); }
-
-bool Engine::check_mk_err() {
-  if (!mk_ok_) return false;
-  int e = 0;
-  HIP_CHECK(hipMemcpy(&e, mk_args_.err, 4, hipMemcpyDeviceToHost));
-  if (!e) return false;
-  HIP_CHECK(hipMemset(mk_args_.err, 0, 4));
-  mk_enabled_ = false;  // another kernel held CUs the persistent step needs: launches from now on
-  reset_graphs();
-  return true;
 }
 
 // TP: sum the row-parallel partials in `p` over the ranks and add the total into `residual`
@@ -792,23 +677,6 @@ GemvArgs Engine::gemv_args(const std::vector<const QMat*>& segs, int N, int K, i
   }
   apply_knobs(a, K == cfg_.d_ff ? "DOWN" : (N == 2 * cfg_.d_ff ? "GU" : (N == cfg_.vocab_size ? "LM" : "O")));
   return a;
-}
-
-// the fused attention block (kernels/attn_block.hip) serves batch-1 decode without TP on the
-// int8-activation GEMV path with the in-epilogue RoPE (shape / format checks per layer follow)
-bool Engine::attn_block_on(int B) const {
-  return fuse_attn_ && fuse_cnt_ && B == 1 && cfg_.tp_size == 1 && cfg_.act_q8 && !cfg_.qk_norm && !cfg_.rope_neox &&
-         !(dec_a16_ && dec_gemm_min_b_ > 0 && B >= dec_gemm_min_b_);
-}
-
-void Engine::check_fuse_err() {
-  if (!fuse_err_) return;
-  int e = 0;
-  HIP_CHECK(hipMemcpy(&e, fuse_err_, 4, hipMemcpyDeviceToHost));
-  if (e) {
-    HIP_CHECK(hipMemset(fuse_err_, 0, 4));
-    throw std::runtime_error("fused attention block: an in-launch hand-off gave up (50 ms wait)");
-  }
 }
 
 // QKV segments: group into launches where only the last segment may differ in format
@@ -940,53 +808,6 @@ void Engine::layer_decode_gemm(int l, int B) {
   if (tp) tp_reduce(attn_, g_next);
 }
 
-// MALL prefetch carried by the batch-1 attention launch (PfSpec, ops.h): the whole O matrix and a
-// prefix of every CU slice of gate/up, read into the Infinity Cache while 224 CUs and HBM idle.
-// AIOS_PF=0 switches it off; AIOS_PF_O (0/1), AIOS_PF_GU_KB (KB per CU slice of the gate/up codes),
-// AIOS_PF_WG (prefetch workgroups), AIOS_PF_MAXLEN (keys up to which it runs).
-static int pf_knob(const char* k, int dflt) {
-  const char* e = std::getenv(k);
-  return e ? std::atoi(e) : dflt;
-}
-
-// plane bytes per 32-weight chunk of a K-quant format (the per-scale planes p3 of Q6_K skipped)
-static double plane_bpc(int qt, int p) {
-  static const double q4[4] = {16, 2, 0, 0}, q5[4] = {16, 2, 4, 0}, q6[4] = {16, 8, 2, 0};
-  return qt == QT_Q4_K ? q4[p] : (qt == QT_Q5_K ? q5[p] : (qt == QT_Q6_K ? q6[p] : 0));
-}
-
-PfSpec Engine::attn_prefetch_spec(int l) const {
-  PfSpec s{};
-  static const int on = pf_knob("AIOS_PF", 0);
-  if (!on || l >= cfg_.n_layers) return s;
-  static const int pf_o = pf_knob("AIOS_PF_O", 1);
-  static const int gu_kb = pf_knob("AIOS_PF_GU_KB", 0);
-  const LayerW& L = layers_[l];
-  auto add = [&](const QMat& m, int G, double frac_or_kb, bool whole) {
-    const QWeight& w = m.w;
-    if (!is_kquant(w.qtype) || w.cols % 32) return;
-    const int nch = w.cols / 32, np = w.rows / 2;
-    const uint8_t* planes[4] = {w.p0, w.p1, w.p2, w.p3};
-    for (int p = 0; p < 3 && s.n < PF_MAX; ++p) {
-      const double bpc = plane_bpc(w.qtype, p);
-      if (bpc <= 0 || !planes[p]) continue;
-      const uint32_t pair_bytes = (uint32_t)(2.0 * nch * bpc);
-      const int g = whole ? 1 : std::min(G, np);
-      const size_t part_min = (size_t)(np / g) * pair_bytes;
-      size_t want = whole ? part_min : (size_t)(frac_or_kb * 1024.0 * bpc / 16.0);  // KB of codes -> plane bytes
-      want = std::min(want, part_min) / 1024 * 1024;
-      if (want == 0) continue;
-      s.e[s.n++] = PfEntry{planes[p], pair_bytes, np, g, (uint32_t)want};
-    }
-  };
-  if (pf_o) add(L.wo, 1, 0, true);
-  if (gu_kb > 0) add(L.wgu, device_cu_count(), gu_kb, false);
-  s.nwg = pf_knob("AIOS_PF_WG", 224);
-  s.max_len = pf_knob("AIOS_PF_MAXLEN", 512);
-  if (s.nwg <= 0) s.n = 0;
-  return s;
-}
-
 void Engine::layer_decode(int l, int B) {
   if (dec_a16_ && ((dec_gemm_min_b_ > 0 && B >= dec_gemm_min_b_) || B > 8)) {
     layer_decode_gemm(l, B);
@@ -996,21 +817,6 @@ void Engine::layer_decode(int l, int B) {
   const LayerW& L = layers_[l];
   const int d = cfg_.d_model, hd = cfg_.head_dim, qd = cfg_.n_heads * hd, kvd = cfg_.n_kv_heads * hd;
   const bool fused_qkv = !cfg_.qk_norm && !cfg_.rope_neox;
-  auto attn_args = [&]() {
-    AttnDecodeArgs a;
-    a.split = 0;
-    a.q = q_;
-    a.k_cache = k_cache_ + (size_t)l * layer_kv_elems_;
-    a.v_cache = v_cache_ + (size_t)l * layer_kv_elems_;
-    a.seq_len = d_seqlen_;
-    a.slot = d_slot_;
-    a.block_table = attn_bt_; a.bt_rows = attn_bt_rows_;
-    a.B = B; a.n_heads = cfg_.n_heads; a.n_kv_heads = cfg_.n_kv_heads; a.head_dim = hd; a.max_ctx = cfg_.max_ctx;
-    a.n_chunks = n_chunks_;
-    a.scale = 1.f / std::sqrt((float)hd);
-    a.o_part = opart_; a.ml = ml_; a.out = attn_; a.counters = attn_cnt_;
-    return a;
-  };
   auto qkv_args = [&](const std::vector<const QMat*>& grp, int row0) {
     int n = 0;
     for (auto* m : grp) n += m->w.rows;
@@ -1037,50 +843,13 @@ void Engine::layer_decode(int l, int B) {
     apply_knobs(a, "QKV");
     return a;
   };
-  // ---- batch 1: QKV -> attention -> O as one launch
-  if (attn_block_on(B)) {
-    const auto grps = qkv_groups(L);
-    if (grps.size() == 1 && !L.bqkv) {
-      const GemvArgs qa = qkv_args(grps[0], 0);
-      const AttnDecodeArgs at = attn_args();
-      const GemvArgs oa = gemv_args({&L.wo}, d, qd, B, attn_, qd, nullptr, x_, d, EPI_RESID, l);
-      if (attn_block_supported(qa, at, oa)) {
-        launch_attn_block(qa, at, oa, fuse_cnt_ + 2 * (size_t)l, fuse_err_, fuse_attn_ >= 2, stream_);
-        gemv({&L.wgu}, 2 * cfg_.d_ff, d, B, x_, d, L.ffn_norm, ff_, cfg_.d_ff, EPI_SWIGLU, l);
-        gemv({&L.wdown}, d, cfg_.d_ff, B, ff_, cfg_.d_ff, nullptr, x_, d, EPI_RESID, l);
-        return;
-      }
-    }
-  }
   // ---- QKV (+RMSNorm prologue, RoPE + KV-cache epilogue)
   {
     int row0 = 0;
     for (auto& grp : qkv_groups(L)) {
-      int n = 0;
-      for (auto* m : grp) n += m->w.rows;
-      GemvArgs a;
-      std::memset(&a, 0, sizeof(a));
-  a.act_q8 = cfg_.act_q8;
-      a.nseg = (int)grp.size();
-      int r = 0;
-      for (int s = 0; s < a.nseg; ++s) { a.seg[s] = grp[s]->w; a.seg_row0[s] = r; r += grp[s]->w.rows; }
-      a.N = n; a.K = d; a.B = B; a.row_base = row0;
-      a.x = x_; a.ldx = d; a.norm_w = L.attn_norm; a.eps = cfg_.norm_eps;
-      if (fused_qkv) {
-        a.epi = EPI_QKV; a.y = q_; a.ldy = qd;
-        a.bias = L.bqkv;
-        a.head_dim = hd; a.q_dim = qd; a.kv_dim = kvd; a.n_kv_heads = cfg_.n_kv_heads; a.max_ctx = cfg_.max_ctx;
-        a.rope_neox = cfg_.rope_neox; a.rope_base = cfg_.rope_theta; a.rope_cs = rope_cs_;
-        a.pos = d_pos_; a.slot = d_slot_;
-        a.k_cache = k_cache_ + (size_t)l * layer_kv_elems_;
-        a.v_cache = v_cache_ + (size_t)l * layer_kv_elems_;
-        a.block_table = d_bt_;
-      } else {
-        a.epi = EPI_STORE; a.y = qkv_; a.ldy = qd + 2 * kvd;
-      }
-      apply_knobs(a, "QKV");
+      const GemvArgs a = qkv_args(grp, row0);
       launch_gemv(a, stream_);
-      row0 += n;
+      row0 += a.N;
     }
     if (!fused_qkv) {
       if (L.bqkv) throw std::runtime_error("qkv bias with unfused QKV path not supported yet");
@@ -1111,7 +880,6 @@ void Engine::layer_decode(int l, int B) {
     a.n_chunks = n_chunks_;
     a.scale = 1.f / std::sqrt((float)hd);
     a.o_part = opart_; a.ml = ml_; a.out = attn_; a.counters = attn_cnt_;
-    if (B == 1) a.pf = attn_prefetch_spec(l);
     launch_attn_decode(a, stream_);
   }
   // ---- O projection (+ residual; TP: partial -> all-reduce -> add)
@@ -1163,16 +931,10 @@ void Engine::lm_head(int B, const float* x, int ldx) {
 
 void Engine::enqueue_decode_step(int B) {
   const int d = cfg_.d_model, V = cfg_.vocab_size;
-  if (attn_block_on(B))  // the fused blocks' hand-off counters start every step at zero
-    HIP_CHECK(hipMemsetAsync(fuse_cnt_, 0, (size_t)cfg_.n_layers * 2 * 4, stream_));
   launch_get_rows(tok_embd_.w, d_tokens_, B, x_, d, 1.f, stream_);
   nrm_lm_ = false;
-  if (mk_use(B)) {
-    launch_decode_mk(mk_args_, mk_grid_, stream_);  // every layer + lm_head in one launch
-  } else {
-    for (int l = 0; l < cfg_.n_layers; ++l) layer_decode(l, B);
-    lm_head(B, x_, d);
-  }
+  for (int l = 0; l < cfg_.n_layers; ++l) layer_decode(l, B);
+  lm_head(B, x_, d);
   nrm_lm_ = false;
   SampleArgs s;
   std::memset(&s, 0, sizeof(s));
@@ -1471,10 +1233,6 @@ std::vector<int> Engine::decode(const std::vector<int>& slots, const std::vector
   HIP_CHECK(hipMemcpyAsync(h_tok_out_, d_tokens_, B * 4, hipMemcpyDeviceToHost, stream_));
   HIP_CHECK(hipStreamSynchronize(stream_));
   sample_mask_ = false;
-  check_fuse_err();
-  // the persistent step gave up (a CU it needs was held by another kernel): the same step again
-  // through the launch-per-op path -- every input is re-uploaded, the KV row is rewritten
-  if (check_mk_err()) return decode(slots, tokens, pos, temperature, top_k, seed, mask, top_p, seeds);
   return std::vector<int>(h_tok_out_, h_tok_out_ + B);
 }
 
@@ -1653,9 +1411,6 @@ std::vector<int> Engine::decode_loop_history(int B, int from_pos, int n) {
 
 void Engine::synchronize() {
   HIP_CHECK(hipStreamSynchronize(stream_));
-  check_fuse_err();
-  if (check_mk_err())
-    throw std::runtime_error("persistent decode step: a bounded wait gave up (switched to the launch path)");
 }
 
 void Engine::reset_graphs() {

@@ -25,43 +25,10 @@
 
 namespace aios {
 
-// Prefetch role (PfSpec, ops.h): wave w of the nw prefetch waves takes 1 KB pieces w, w + nw, ...
-// of the concatenated (entry, part, piece) list -- consecutive waves read consecutive pieces of
-// one part -- with default-policy LDS-DMA (allocates in L2 and the Infinity Cache; the bytes land
-// in a 1 KB LDS sink and are never read), then drains before the workgroup retires its LDS.
-__device__ __forceinline__ void attn_prefetch_role(const PfSpec& s, int pwg) {
-  __shared__ __attribute__((aligned(16))) uint8_t sink[1024];
-  const int lane = threadIdx.x & 63;
-  const int nwv = blockDim.x >> 6;
-  const int nw = s.nwg * nwv;
-  const int w = pwg * nwv + (threadIdx.x >> 6);
-  auto* ldst = (__attribute__((address_space(3))) void*)sink;
-  int base_i = 0;
-  for (int e = 0; e < s.n; ++e) {
-    const PfEntry E = s.e[e];
-    const int ppp = (int)(E.pf_bytes >> 10);
-    const int tot = ppp * E.G;
-    // first piece index >= base_i owned by this wave
-    int i = w - base_i % nw;
-    if (i < 0) i += nw;
-    for (; i < tot; i += nw) {
-      const int g = i / ppp, k = i - g * ppp;
-      const size_t off = (size_t)((long)g * E.np / E.G) * E.pair_bytes + (size_t)k * 1024 + lane * 16;
-      __builtin_amdgcn_global_load_lds((const void*)(E.base + off), ldst, 16, 0, 0);
-    }
-    base_i += tot;
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
-
 template <int HD, int G>
 __global__ void __launch_bounds__(512) attn_decode_kernel(AttnDecodeArgs a, AttnSplit sp_) {
   const int wg = blockIdx.x;
   const int len = a.seq_len[blockIdx.z];
-  if (wg >= sp_.n_attn) {
-    if (blockIdx.z == 0 && len <= a.pf.max_len) attn_prefetch_role(a.pf, wg - sp_.n_attn);
-    return;
-  }
   if (G > 1 && len <= a.short_len) {
     const int h = wg / sp_.p_short, sp = wg % sp_.p_short;
     if (h >= a.n_heads) return;
@@ -80,7 +47,7 @@ static void launch_hd(const AttnDecodeArgs& a, int G, hipStream_t st) {
   AttnSplit sp;
   const int nwg = attn_plan(a, G, sp);
   sp.n_attn = nwg;
-  dim3 grid(nwg + (a.pf.n > 0 ? a.pf.nwg : 0), 1, a.B);
+  dim3 grid(nwg, 1, a.B);
   switch (G) {
     case 1: hipLaunchKernelGGL((attn_decode_kernel<HD, 1>), grid, dim3(512), 0, st, a, sp); break;
     case 2: hipLaunchKernelGGL((attn_decode_kernel<HD, 2>), grid, dim3(512), 0, st, a, sp); break;

@@ -1,10 +1,9 @@
-// Split-K flash-decode attention core (device code shared by attention.hip's standalone kernel
-// and attn_block.hip's fused QKV -> attention -> O launch).  See attention.hip for the design.
+// Split-K flash-decode attention core (device code of attention.hip's decode kernel).  See
+// attention.hip for the design.
 #pragma once
 #include "../common.h"
 #include "../ops.h"
 #include "gemm_common.h"
-#include "fuse.h"
 
 #include <algorithm>
 #include <cstdlib>
@@ -81,16 +80,9 @@ __device__ __forceinline__ float dot2_bf16(uint32_t a, uint32_t b, float c) {
 // VALU diet (the kernel is VALU-bound per CU once its loads are in flight): q . k runs on
 // v_dot2_f32_bf16 against q pre-rounded to bf16 pairs (4 instructions per 8 dims and head, as the
 // MFMA prefill path rounds q), P . V on packed v_pk_fma_f32 with the probabilities in fp32.
-//
-// FUSED (attn_block.hip): q and the newest key/value row (position len - 1) are written by the
-// QKV workgroups of the SAME launch.  The K/V of every older position is prefetched before the
-// wait on the QKV edge; the lane holding the newest key prefetches a neighbouring row of the same
-// block instead (its line must not enter this XCD's caches before the hand-off) and re-reads the
-// real row with sc1 loads after the wait; q is read with sc1 loads; the output is stored
-// write-through and published on fz.sig (+G heads).
-template <int HD, int G, bool FUSED = false>
+template <int HD, int G>
 __device__ __forceinline__ void attn_core(const AttnDecodeArgs& a, int sp, int kvh, int h0, int ci, int P_max,
-                                          int ppw, FuseEdge fz = FuseEdge{}) {
+                                          int ppw) {
   constexpr int NW = 8;                // waves per workgroup
   constexpr int LPK = HD / 8;          // lanes per key (8 dims per lane)
   constexpr int KPS = 64 / LPK;        // keys per wave-instruction
@@ -133,58 +125,23 @@ __device__ __forceinline__ void attn_core(const AttnDecodeArgs& a, int sp, int k
 
   // two passes in flight per workgroup: buffers A and B (static, so they stay in VGPRs)
   uint4 kA[STEPS], vA[STEPS], kB[STEPS], vB[STEPS];
-  const int newest = len - 1;  // FUSED: the row this launch's QKV workgroups write
-  auto issue = [&](uint4 (&kr)[STEPS], uint4 (&vr)[STEPS], int chunk, bool post) __attribute__((always_inline)) {
+  auto issue = [&](uint4 (&kr)[STEPS], uint4 (&vr)[STEPS], int chunk) __attribute__((always_inline)) {
     const int c = min(chunk, cmax);  // clamped: always a mapped block
     const size_t base = (size_t)(btr ? btr[c] : slot * maxb + c) * blk_stride;
-    if constexpr (!FUSED) {
 #pragma unroll
-      for (int s = 0; s < STEPS; ++s) kr[s] = *(const uint4*)(kc + base + (size_t)s * KPS * HD);
+    for (int s = 0; s < STEPS; ++s) kr[s] = *(const uint4*)(kc + base + (size_t)s * KPS * HD);
 #pragma unroll
-      for (int s = 0; s < STEPS; ++s) vr[s] = *(const uint4*)(vc + base + (size_t)s * KPS * HD);
-    } else {
-      // before the hand-off the lane holding the newest row reads a neighbour of the same block
-      // (masked or an older key); after it (post) every row is read plainly -- no CU of this XCD
-      // touched the newest row's lines earlier in the launch, so nothing stale can be cached
-#pragma unroll
-      for (int s = 0; s < STEPS; ++s) {
-        const int key = chunk * CH + koff + s * KPS;
-        const int sh = (key == newest && !post) ? ((key % CH) == CH - 1 ? -(CH - 1) : 1) * HD : 0;
-        kr[s] = *(const uint4*)(kc + base + (size_t)s * KPS * HD + sh);
-      }
-#pragma unroll
-      for (int s = 0; s < STEPS; ++s) {
-        const int key = chunk * CH + koff + s * KPS;
-        const int sh = (key == newest && !post) ? ((key % CH) == CH - 1 ? -(CH - 1) : 1) * HD : 0;
-        vr[s] = *(const uint4*)(vc + base + (size_t)s * KPS * HD + sh);
-      }
-    }
+    for (int s = 0; s < STEPS; ++s) vr[s] = *(const uint4*)(vc + base + (size_t)s * KPS * HD);
   };
-  // after the hand-off: the newest row into whichever prefetched pass holds it
-  auto fix = [&](uint4 (&kr)[STEPS], uint4 (&vr)[STEPS], int chunk) __attribute__((always_inline)) {
-    const int c = min(chunk, cmax);
-    const size_t base = (size_t)(btr ? btr[c] : slot * maxb + c) * blk_stride;
-#pragma unroll
-    for (int s = 0; s < STEPS; ++s)
-      if (chunk * CH + koff + s * KPS == newest) {
-        kr[s] = ld_sc1_16(kc + base + (size_t)s * KPS * HD);
-        vr[s] = ld_sc1_16(vc + base + (size_t)s * KPS * HD);
-      }
-  };
-  issue(kA, vA, sp, false);
-  if (sp + P < nchunk) issue(kB, vB, sp + P, false);
-  if constexpr (FUSED) {
-    fuse_wait(fz);
-    fix(kA, vA, sp);
-    if (sp + P < nchunk) fix(kB, vB, sp + P);
-  }
+  issue(kA, vA, sp);
+  if (sp + P < nchunk) issue(kB, vB, sp + P);
   const float qs = a.scale * kLog2e;  // scores in the log2 domain: exp2 below
   uint32_t q2[G][4];                  // q * scale as bf16 pairs
 #pragma unroll
   for (int g = 0; g < G; ++g) {
     const float* qp = a.q + ((size_t)b * a.n_heads + h0 + g) * HD + dsl * 8;
-    const float4 q0 = FUSED ? ld_sc1_f4(qp) : *(const float4*)qp;
-    const float4 q1 = FUSED ? ld_sc1_f4(qp + 4) : *(const float4*)(qp + 4);
+    const float4 q0 = *(const float4*)qp;
+    const float4 q1 = *(const float4*)(qp + 4);
     q2[g][0] = pk_bf16(q0.x * qs, q0.y * qs);
     q2[g][1] = pk_bf16(q0.z * qs, q0.w * qs);
     q2[g][2] = pk_bf16(q1.x * qs, q1.y * qs);
@@ -254,10 +211,10 @@ __device__ __forceinline__ void attn_core(const AttnDecodeArgs& a, int sp, int k
   for (int c = sp; c < nchunk; c += 2 * P) {
     pass(kA, vA, c);
     if (c == sp) stamp(2);
-    if (c + 2 * P < nchunk) issue(kA, vA, c + 2 * P, true);
+    if (c + 2 * P < nchunk) issue(kA, vA, c + 2 * P);
     if (c + P < nchunk) {
       pass(kB, vB, c + P);
-      if (c + 3 * P < nchunk) issue(kB, vB, c + 3 * P, true);
+      if (c + 3 * P < nchunk) issue(kB, vB, c + 3 * P);
     }
   }
   // ---- merge the key groups of a wave (shuffles), then the 8 waves in LDS (one barrier)
@@ -303,8 +260,7 @@ __device__ __forceinline__ void attn_core(const AttnDecodeArgs& a, int sp, int k
     }
     const int h = h0 + g;
     if (nact == 1) {
-      if constexpr (FUSED) st_sc1_f32(a.out + ((size_t)b * a.n_heads + h) * HD + d, acc / L);
-      else if (a.out16) a.out16[((size_t)b * a.n_heads + h) * HD + d] = f32_to_bf16(acc / L);
+      if (a.out16) a.out16[((size_t)b * a.n_heads + h) * HD + d] = f32_to_bf16(acc / L);
       else a.out[((size_t)b * a.n_heads + h) * HD + d] = acc / L;
     } else {
       st_wt(a.o_part + (((size_t)b * a.n_heads + h) * a.n_chunks + sp) * HD + d, acc);
@@ -316,7 +272,6 @@ __device__ __forceinline__ void attn_core(const AttnDecodeArgs& a, int sp, int k
     }
   }
   if (nact == 1) {
-    if constexpr (FUSED) fuse_signal(fz, G);
     stamp(6);
     return;
   }
@@ -376,12 +331,10 @@ __device__ __forceinline__ void attn_core(const AttnDecodeArgs& a, int sp, int k
       for (int j = 0; j < 16; ++j)
         if (c + j < nact) acc = fmaf(s_pm[g][c + j], ov[j], acc);
     }
-    if constexpr (FUSED) st_sc1_f32(a.out + ((size_t)b * a.n_heads + h) * HD + d, acc);
-    else if (a.out16) a.out16[((size_t)b * a.n_heads + h) * HD + d] = f32_to_bf16(acc);
+    if (a.out16) a.out16[((size_t)b * a.n_heads + h) * HD + d] = f32_to_bf16(acc);
     else a.out[((size_t)b * a.n_heads + h) * HD + d] = acc;
   }
   if (threadIdx.x == 0) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
-  if constexpr (FUSED) fuse_signal(fz, G);
   stamp(6);
 }
 

@@ -360,7 +360,7 @@ __global__ void __launch_bounds__(CU_THREADS) gemv_cu_b1(GemvArgs a, CuPlan pl) 
       }
       cu_qkv_epilogue(a, grow, v0, v1, t, pos0, kv_blk0);
     } else {
-      gemv_epilogue1(a, grow, v0, v1, nullptr, 0, 0);
+      gemv_epilogue1(a, grow, v0, v1);
     }
   }
   CU_STAMP(6);

@@ -20,7 +20,6 @@
 #include "../common.h"
 #include "../gemv.h"
 #include "../qweight.h"
-#include "fuse.h"
 
 namespace aios {
 

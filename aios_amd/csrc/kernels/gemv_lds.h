@@ -418,7 +418,7 @@ __global__ void __launch_bounds__(LG_THREADS) gemv_lds_b1(GemvArgs a, CuPlan pl)
     }
     lg_barrier();  // final
   };
-  auto consumer_path = [&](auto tag, float2& rope) __attribute__((always_inline)) {
+  auto consumer_path = [&](auto tag, float2& rope, int& pos0, int& kv_blk0) __attribute__((always_inline)) {
     constexpr int QT = decltype(tag)::value;
     using L = LgLayout<QT, RSUB>;
     constexpr int LG_R = L::R;
@@ -432,11 +432,16 @@ __global__ void __launch_bounds__(LG_THREADS) gemv_lds_b1(GemvArgs a, CuPlan pl)
     q8_stage<QT0, B, NPF>(a, xq, ms, red, pf, threadIdx.x, LG_NG * 64);
     // RoPE (cos, sin) of the epilogue lane's pair: issued now, waited for in the epilogue (the
     // consumers issue no other global load until then)
-    if (B == 1 && a.epi == EPI_QKV && wave == 0 && a.rope_cs) {
-      const int pos0 = a.pos[0];
-      int part, head, lrr;
-      qkv_part(a, a.row_base + r0 + 2 * lane, part, head, lrr);
-      rope = a.rope_cs[(size_t)pos0 * (a.head_dim >> 1) + (part < 2 ? (lrr >> 1) : 0)];
+    if (B == 1 && a.epi == EPI_QKV && wave == 0) {
+      // pos and the KV block too: a lookup after the final barrier put two dependent round trips
+      // on the epilogue's path
+      pos0 = a.pos[0];
+      kv_blk0 = kv_block(a.block_table, a.max_ctx / KV_BLOCK, a.slot ? a.slot[0] : 0, pos0);
+      if (a.rope_cs) {
+        int part, head, lrr;
+        qkv_part(a, a.row_base + r0 + 2 * lane, part, head, lrr);
+        rope = a.rope_cs[(size_t)pos0 * (a.head_dim >> 1) + (part < 2 ? (lrr >> 1) : 0)];
+      }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     CU_STAMP(2);
@@ -659,13 +664,14 @@ __global__ void __launch_bounds__(LG_THREADS) gemv_lds_b1(GemvArgs a, CuPlan pl)
     CU_STAMP(5);
   };
   float2 rope = make_float2(1.f, 0.f);
+  int pos0 = 0, kv_blk0 = 0;
   if (loader) {
     if (!fmt1) loader_path(FmtTag<QT0>{});
     else loader_path(FmtTag<QT1>{});
     return;
   }
-  if (!fmt1) consumer_path(FmtTag<QT0>{}, rope);
-  else consumer_path(FmtTag<QT1>{}, rope);
+  if (!fmt1) consumer_path(FmtTag<QT0>{}, rope, pos0, kv_blk0);
+  else consumer_path(FmtTag<QT1>{}, rope, pos0, kv_blk0);
   auto flush_ts = [&]() {
     if (a.dbg_ts && lane == 0 && (wave == 0 || wave == LG_NG - 1))
       for (int i = 0; i < 8; ++i) a.dbg_ts[((size_t)blockIdx.x * 2 + (wave != 0)) * 8 + i] = ts[i];
@@ -710,11 +716,6 @@ __global__ void __launch_bounds__(LG_THREADS) gemv_lds_b1(GemvArgs a, CuPlan pl)
     for (int w = 0; w < LG_NG; ++w) t += red[w];
     s = rsqrtf(t / (float)a.K + a.eps);
   }
-  int pos0 = 0, kv_blk0 = 0;
-  if (a.epi == EPI_QKV) {
-    pos0 = a.pos[0];
-    kv_blk0 = kv_block(a.block_table, a.max_ctx / KV_BLOCK, a.slot ? a.slot[0] : 0, pos0);
-  }
   for (int p = lane; 2 * p < nrows; p += 64) {
     const int grow = a.row_base + r0 + 2 * p;
     const float v0 = rowacc[2 * p] * s, v1 = rowacc[2 * p + 1] * s;
@@ -734,7 +735,7 @@ __global__ void __launch_bounds__(LG_THREADS) gemv_lds_b1(GemvArgs a, CuPlan pl)
       }
       cu_qkv_epilogue(a, grow, v0, v1, t, pos0, kv_blk0);
     } else {
-      gemv_epilogue1(a, grow, v0, v1, nullptr, 0, 0);
+      gemv_epilogue1(a, grow, v0, v1);
     }
   }
   CU_STAMP(6);

@@ -217,13 +217,8 @@ struct StagePre {
   float4 x0[NPF], x1[NPF], g0[NPF], g1[NPF];
 };
 // tid / nthr: the staging threads (default: the whole workgroup)
-// SC1: x was written earlier in the same (fused) launch -- read it with sc1 loads (fuse.h)
-template <bool SC1>
-__device__ __forceinline__ float4 ldx4(const float* p) {
-  if constexpr (SC1) return ld_sc1_f4(p);
-  else return *(const float4*)p;
-}
-template <int NPF, bool SC1 = false>
+__device__ __forceinline__ float4 ldx4(const float* p) { return *(const float4*)p; }
+template <int NPF>
 __device__ __forceinline__ void q8_stage_prefetch(const GemvArgs& a, StagePre<NPF>& pf, int tid = -1, int nthr = 0) {
   if (tid < 0) { tid = threadIdx.x; nthr = blockDim.x; }
   const int noct = a.K >> 3, total = a.B * noct;
@@ -234,8 +229,8 @@ __device__ __forceinline__ void q8_stage_prefetch(const GemvArgs& a, StagePre<NP
     const int tt = t < total ? t : 0;
     const int b = tt / noct, o = tt - b * noct;
     const float* src = a.x + (size_t)b * a.ldx + 8 * o;
-    pf.x0[i] = ldx4<SC1>(src);
-    pf.x1[i] = ldx4<SC1>(src + 4);
+    pf.x0[i] = ldx4(src);
+    pf.x1[i] = ldx4(src + 4);
     // the norm weights of every prefetched pass too: a load issued after the weight stream would
     // make its wait cover every weight load in flight
     const float* g = a.norm_w ? a.norm_w + 8 * o : src;
@@ -292,7 +287,7 @@ __device__ __forceinline__ void q8_octet(const GemvArgs& a, int b, int o, float4
   if (!(quarter & 1)) ms[((size_t)b * nch + c) * R + (s0 >> 4)] = make_float2(dx, dx * (float)isum);
 }
 
-template <int QT, int B, int NPF, bool SC1 = false>
+template <int QT, int B, int NPF>
 __device__ __forceinline__ void q8_stage(const GemvArgs& a, int8_t* xq, float2* ms, float* red,
                                          const StagePre<NPF>& pf, int tid = -1, int nthr = 0) {
   if (tid < 0) { tid = threadIdx.x; nthr = blockDim.x; }
@@ -312,7 +307,7 @@ __device__ __forceinline__ void q8_stage(const GemvArgs& a, int8_t* xq, float2* 
   for (int t = tid + NPF * nthr; t < total; t += nthr) {
     const int b = t / noct, o = t - b * noct;
     const float* src = a.x + (size_t)b * a.ldx + 8 * o;
-    const float4 f0 = ldx4<SC1>(src), f1 = ldx4<SC1>(src + 4);
+    const float4 f0 = ldx4(src), f1 = ldx4(src + 4);
     float4 g0 = f0, g1 = f1;
     if (a.norm_w) {
       g0 = *(const float4*)(a.norm_w + 8 * o);
@@ -410,9 +405,9 @@ __device__ __forceinline__ void q8_compute(const RawChunk (&raw)[U][GEMV_ROWS], 
 // ---------------------------------------------------------------------------------------------
 // B = 1 epilogue that issues no global LOAD: vmcnt drains in issue order, so a load here would
 // wait for the next item's whole weight prefetch.  The residual add is a no-return atomic add
-// (each element has exactly one writer, so the result is deterministic), the RoPE (cos, sin) row
-// of this step's position sits in LDS (staged in the prologue), pos/slot are read once up front.
-// Only the rare QKV-bias models load in the epilogue.
+// (each element has exactly one writer, so the result is deterministic); the RoPE (cos, sin) of
+// the pair, pos and the KV block were loaded behind the first weight loads (q8_rows_body).  Only
+// the rare QKV-bias models load in the epilogue.
 // ---------------------------------------------------------------------------------------------
 __device__ __forceinline__ void qkv_part(const GemvArgs& a, int grow, int& part, int& head, int& lr) {
   const int hd = a.head_dim, qd = a.q_dim, kvd = a.kv_dim;
@@ -423,10 +418,9 @@ __device__ __forceinline__ void qkv_part(const GemvArgs& a, int grow, int& part,
   head = r / hd;
   lr = r - head * hd;
 }
-// wt: the outputs are consumed later in the same (fused) launch -- q and the K/V row are stored
-// write-through as 8- / 4-byte pairs (non-NeoX RoPE: the pair (da, db) is adjacent)
-__device__ __forceinline__ void gemv_epilogue1(const GemvArgs& a, int grow, float v0, float v1, const float2* rope_l,
-                                               int pos0, int kv_blk0, bool wt = false) {
+// rope: (cos, sin) of this pair at pos0 (QKV; ignored for V rows and the other epilogues)
+__device__ __forceinline__ void gemv_epilogue1(const GemvArgs& a, int grow, float v0, float v1, float2 rope = {1.f, 0.f},
+                                               int pos0 = 0, int kv_blk0 = 0) {
   const int nrow = a.row_base + a.N;
   switch (a.epi) {
     case EPI_STORE:
@@ -454,28 +448,20 @@ __device__ __forceinline__ void gemv_epilogue1(const GemvArgs& a, int grow, floa
       else if (a.rope_neox) { da = pp; db = pp + (hd >> 1); }
       else { da = 2 * pp; db = 2 * pp + 1; }
       if (part < 2) {
-        const float2 t = rope_l[pp];
-        const float o0 = v0 * t.x - v1 * t.y, o1 = v0 * t.y + v1 * t.x;
+        const float o0 = v0 * rope.x - v1 * rope.y, o1 = v0 * rope.y + v1 * rope.x;
         v0 = o0;
         v1 = o1;
       }
       if (part == 0) {
         float* q = a.y + head * hd;
-        if (wt && db == da + 1) {
-          st_sc1_f2(q + da, v0, v1);
-        } else if (wt) {
-          st_sc1_f32(q + da, v0);
-          st_sc1_f32(q + db, v1);
-        } else {
-          q[da] = v0;
-          q[db] = v1;
-        }
+        q[da] = v0;
+        q[db] = v1;
       } else {
         bf16_t* cache = (part == 1 ? a.k_cache : a.v_cache);
-        // kv_blk0: the physical block of (slot, pos), looked up once in the prologue
+        // kv_blk0: the physical block of (slot, pos), looked up once behind the first weight loads
         const size_t base = (((size_t)kv_blk0 * a.n_kv_heads + head) * KV_BLOCK + (pos0 % KV_BLOCK)) * hd;
-        if (wt) {  // the fused path requires the adjacent (non-NeoX) pair: one 4-byte store
-          st_sc1_u32(cache + base + da, (uint32_t)f32_to_bf16(v0) | ((uint32_t)f32_to_bf16(v1) << 16));
+        if (db == da + 1) {  // adjacent pair (V rows, non-NeoX RoPE): one 4-byte store
+          *(uint32_t*)(cache + base + da) = (uint32_t)f32_to_bf16(v0) | ((uint32_t)f32_to_bf16(v1) << 16);
         } else {
           cache[base + da] = f32_to_bf16(v0);
           cache[base + db] = f32_to_bf16(v1);
@@ -506,20 +492,18 @@ __device__ __forceinline__ float2 wave_sum_pair(float a0, float a1) {
 // PIPE = 2 double-buffers across items/pairs (short K), 1 = single buffer (large U).
 // ---------------------------------------------------------------------------------------------
 constexpr int Q8_WAVES = 8;
+// up to 16 waves per workgroup for the register-light variants (U <= 2: the batch-1 QKV / O shapes)
+template <int U>
+constexpr int q8_max_threads() { return U <= 2 ? 1024 : Q8_WAVES * 64; }
 
 template <int QT>
 struct FmtTag {
   static constexpr int value = QT;
 };
 
-// The kernel body as a device function over a virtual grid (vblk of vgrid workgroups), so a fused
-// launch (attn_block.hip) can run it as one role.  FUSED: x is read with sc1 loads after the wait
-// on fz (the weights of the first item are already in flight), QKV outputs are stored write-through,
-// and the workgroup publishes on fz.sig when its rows are written.
-template <int QT0, int QT1, int B, int U, int PIPE, bool FUSED = false>
-__device__ __forceinline__ void q8_rows_body(const GemvArgs& a, int vblk, int vgrid, FuseEdge fz = FuseEdge{}) {
+template <int QT0, int QT1, int B, int U, int PIPE>
+__global__ void __launch_bounds__(q8_max_threads<U>()) gemv_q8_rows(GemvArgs a) {
   static_assert(same_xlayout<QT0, QT1>, "mixed segments must share the activation layout");
-  static_assert(!FUSED || B == 1, "fused roles are batch-1");
   extern __shared__ __attribute__((aligned(16))) float smem[];
   constexpr bool MIXED = QT0 != QT1;
   constexpr int W = QFmt<QT0>::W, R = QFmt<QT0>::RUNS;
@@ -527,7 +511,6 @@ __device__ __forceinline__ void q8_rows_body(const GemvArgs& a, int vblk, int vg
   float* red = smem;                                   // [nw][B] (nw * B <= 64)
   float2* ms = (float2*)(smem + 64);                   // [B][nch][R]
   int8_t* xq = (int8_t*)(ms + (size_t)B * nch * R);    // [B][nch][W]
-  float2* rope_l = (float2*)(xq + (size_t)B * a.K);    // [head_dim/2] (cos, sin) at pos0 (B = 1, QKV)
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int nw = __builtin_amdgcn_readfirstlane(blockDim.x >> 6);
   const int npairs = a.N >> 1;
@@ -537,8 +520,15 @@ __device__ __forceinline__ void q8_rows_body(const GemvArgs& a, int vblk, int vg
   const int srow2 = __builtin_amdgcn_readfirstlane(a.seg_row0[2]);
   const int np0 = (MIXED && a.nseg > 1) ? (a.nseg == 2 ? srow1 : srow2) >> 1 : npairs;
   const int nit = (nch + 64 * U - 1) / (64 * U);
-  const int stride = vgrid * nw;
-  const int wid = __builtin_amdgcn_readfirstlane(vblk * nw + wave);  // wave-uniform -> SGPR
+  const int stride = gridDim.x * nw;
+  const int wid = __builtin_amdgcn_readfirstlane(blockIdx.x * nw + wave);  // wave-uniform -> SGPR
+  // probes (tools/gemv_cu_probe.py): phase stamps of the first and last wave of every workgroup --
+  // 0 start, 1 first weight loads issued, 2 x staged, 3 barrier passed, 4 first pair computed, 5 done
+  unsigned long long ts[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  auto stamp = [&](int i) __attribute__((always_inline)) {
+    if (a.dbg_ts) ts[i] = __builtin_amdgcn_s_memrealtime();
+  };
+  stamp(0);
 
   auto seg_idx = [&](int p, int& lrow) -> int {
     const int row = 2 * p;
@@ -566,24 +556,33 @@ __device__ __forceinline__ void q8_rows_body(const GemvArgs& a, int vblk, int vg
     q8_load_item<QT, U>(w, lrow, it, nch, r);
   };
 
-  int pos0 = 0, kv_blk0 = 0;
-  if constexpr (B == 1) {
-    if (a.epi == EPI_QKV) {
-      pos0 = a.pos[0];
-      kv_blk0 = kv_block(a.block_table, a.max_ctx / KV_BLOCK, a.slot ? a.slot[0] : 0, pos0);
-      for (int i = threadIdx.x; i < (a.head_dim >> 1); i += blockDim.x) {
-        float2 t;
-        if (a.rope_cs) {
-          t = a.rope_cs[(size_t)pos0 * (a.head_dim >> 1) + i];
-        } else {
-          float sn, cs;
-          sincosf((float)pos0 * powf(a.rope_base, -2.f * (float)i / (float)a.head_dim), &sn, &cs);
-          t = make_float2(cs, sn);
+  // Batch-1 QKV: pos, the KV block and the pair's RoPE (cos, sin) are looked up AFTER the x and
+  // first weight loads are issued and x is staged (a dependent pos -> block table / rope chain in
+  // front of them held every weight byte back by two memory round trips,
+  // profiles/qkv_prologue_r4.txt); the values are waited for only in the epilogue.
+  int pos0 = 0, kv_blk0 = 0, rope_p = -1;
+  float2 rope_w = make_float2(1.f, 0.f);
+  auto rope_of = [&](int p) __attribute__((always_inline)) -> float2 {
+    int part, head, lr;
+    qkv_part(a, a.row_base + 2 * p, part, head, lr);
+    const int pp = lr >> 1;
+    if (a.rope_cs) return a.rope_cs[(size_t)pos0 * (a.head_dim >> 1) + (part < 2 ? pp : 0)];
+    float sn, cs;
+    sincosf((float)pos0 * powf(a.rope_base, -2.f * (float)pp / (float)a.head_dim), &sn, &cs);
+    return make_float2(cs, sn);
+  };
+  auto qkv_lookup = [&](int p_first) __attribute__((always_inline)) {
+    if constexpr (B == 1) {
+      if (a.epi == EPI_QKV) {
+        pos0 = a.pos[0];
+        kv_blk0 = kv_block(a.block_table, a.max_ctx / KV_BLOCK, a.slot ? a.slot[0] : 0, pos0);
+        if (p_first < npairs) {
+          rope_w = rope_of(p_first);
+          rope_p = p_first;
         }
-        rope_l[i] = t;
       }
     }
-  }
+  };
 
   float acc[GEMV_ROWS][B];
 #pragma unroll
@@ -616,9 +615,12 @@ __device__ __forceinline__ void q8_rows_body(const GemvArgs& a, int vblk, int vg
         s[b] = rsqrtf(t / (float)a.K + a.eps);
       }
     }
+    if (!ts[4]) stamp(4);
     if constexpr (B == 1) {
       const float2 v = wave_sum_pair(acc[0][0], acc[1][0]);
-      if (lane == 0) gemv_epilogue1(a, a.row_base + 2 * p, v.x * s[0], v.y * s[0], rope_l, pos0, kv_blk0, FUSED);
+      float2 rope = rope_w;
+      if (a.epi == EPI_QKV && p != rope_p) rope = rope_of(p);  // a grid-stride pair after the first
+      if (lane == 0) gemv_epilogue1(a, a.row_base + 2 * p, v.x * s[0], v.y * s[0], rope, pos0, kv_blk0);
     } else {
 #pragma unroll
       for (int r = 0; r < GEMV_ROWS; ++r)
@@ -695,18 +697,15 @@ __device__ __forceinline__ void q8_rows_body(const GemvArgs& a, int vblk, int vg
 
   constexpr int NPF = (B == 1 && U >= 3) ? 4 : 1;
   StagePre<NPF> pf{};
-  const bool waits = FUSED && fz.wait != nullptr;
-  if (!waits) q8_stage_prefetch(a, pf);  // x first: its wait then does not cover the weights
+  q8_stage_prefetch(a, pf);  // x first: its wait then does not cover the weights
   if constexpr (!MIXED) {
     load(FmtTag<QT0>{}, wid, npairs, 0, bufA);  // weight loads in flight during the prologue
-    if constexpr (FUSED) {
-      if (waits) {  // x is produced in this launch: wait for it with the first weights in flight
-        fuse_wait(fz);
-        q8_stage_prefetch<NPF, true>(a, pf);
-      }
-    }
-    if (!(a.tune_dbg & 1)) q8_stage<QT0, B, NPF, FUSED>(a, xq, ms, red, pf);
+    stamp(1);
+    if (!(a.tune_dbg & 1)) q8_stage<QT0, B, NPF>(a, xq, ms, red, pf);
+    qkv_lookup(wid);
+    stamp(2);
     __syncthreads();
+    stamp(3);
     run(FmtTag<QT0>{}, wid, npairs, stride, buf);
   } else {
     // Mixed formats (Q4_K q/k + Q6_K v of a Q4_K_M QKV): the waves are split in proportion to the
@@ -721,37 +720,43 @@ __device__ __forceinline__ void q8_rows_body(const GemvArgs& a, int vblk, int vg
     W0 = max(1, min(W - 1, W0));
     if (W < 16) {  // tiny grid: the sequential schedule
       load(FmtTag<QT0>{}, wid, np0, 0, bufA);
+      stamp(1);
       if (!(a.tune_dbg & 1)) q8_stage<QT0, B, NPF>(a, xq, ms, red, pf);
+      qkv_lookup(wid < np0 ? wid : npairs);
+      stamp(2);
       __syncthreads();
+      stamp(3);
       run(FmtTag<QT0>{}, wid, np0, stride, buf);
       // the second format gets its own register buffer: one array written through two different
       // load sequences defeats SROA and lands in scratch
       RawChunk bufT[PIPE][U][GEMV_ROWS];
       load(FmtTag<QT1>{}, np0 + wid, npairs, 0, bufT[0]);
+      stamp(1);
       run(FmtTag<QT1>{}, np0 + wid, npairs, stride, bufT);
     } else if (wid < W0) {
       load(FmtTag<QT0>{}, wid, np0, 0, bufA);
+      stamp(1);
       if (!(a.tune_dbg & 1)) q8_stage<QT0, B, NPF>(a, xq, ms, red, pf);
+      qkv_lookup(wid < np0 ? wid : npairs);
+      stamp(2);
       __syncthreads();
+      stamp(3);
       run(FmtTag<QT0>{}, wid, np0, W0, buf);
     } else {
       RawChunk buf1[PIPE][U][GEMV_ROWS];
       load(FmtTag<QT1>{}, np0 + (wid - W0), npairs, 0, buf1[0]);
+      stamp(1);
       if (!(a.tune_dbg & 1)) q8_stage<QT0, B, NPF>(a, xq, ms, red, pf);
+      qkv_lookup(np0 + (wid - W0));
+      stamp(2);
       __syncthreads();
+      stamp(3);
       run(FmtTag<QT1>{}, np0 + (wid - W0), npairs, W - W0, buf1);
     }
   }
-  if constexpr (FUSED) fuse_signal(fz, 1);
-}
-
-// up to 16 waves per workgroup for the register-light variants (U <= 2: the batch-1 QKV / O shapes)
-template <int U>
-constexpr int q8_max_threads() { return U <= 2 ? 1024 : Q8_WAVES * 64; }
-
-template <int QT0, int QT1, int B, int U, int PIPE>
-__global__ void __launch_bounds__(q8_max_threads<U>()) gemv_q8_rows(GemvArgs a) {
-  q8_rows_body<QT0, QT1, B, U, PIPE>(a, blockIdx.x, gridDim.x);
+  stamp(5);
+  if (a.dbg_ts && lane == 0 && (wave == 0 || wave == nw - 1))
+    for (int i = 0; i < 8; ++i) a.dbg_ts[((size_t)blockIdx.x * 2 + (wave != 0)) * 8 + i] = ts[i];
 }
 
 template <int QT0, int QT1, int B>

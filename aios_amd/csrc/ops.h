@@ -73,27 +73,6 @@ struct QkvPostArgs {
 void launch_qkv_post(const QkvPostArgs& a, hipStream_t st);
 
 // ---- attention ---------------------------------------------------------------------------------
-// Infinity-Cache (MALL) weight prefetch carried by a latency-bound launch: extra workgroups of the
-// batch-1 decode attention launch (32 busy workgroups on 256 CUs, HBM idle) read the first bytes
-// of every CU slice of the NEXT projections' weight planes with default-policy LDS-DMA loads (data
-// discarded), so the O / gate-up GEMVs that follow find them in the 256 MB die-level cache.
-// Entry: plane `base`, split the way the consuming GEMV splits it (part g of G starts at row pair
-// floor(g * np / G)); the first pf_bytes (multiple of 1 KB, <= the smallest part) of every part.
-struct PfEntry {
-  const uint8_t* base;
-  uint32_t pair_bytes;  // plane bytes per row pair
-  int np;               // row pairs
-  int G;                // parts (the consuming GEMV's workgroups)
-  uint32_t pf_bytes;    // prefix of every part to prefetch
-};
-constexpr int PF_MAX = 8;
-struct PfSpec {
-  PfEntry e[PF_MAX];
-  int n = 0;
-  int nwg = 0;       // prefetch workgroups appended to the launch
-  int max_len = 0;   // only while seq_len <= max_len (the launch's own workgroups are few)
-};
-
 struct AttnDecodeArgs {
   const float* q;          // [B][n_heads][head_dim]
   const bf16_t* k_cache;   // layer base of the paged pool [blocks][n_kv][KV_BLOCK][hd]
@@ -112,19 +91,11 @@ struct AttnDecodeArgs {
   bf16_t* out16 = nullptr; // if set: the output as bf16 instead (the batched-decode GEMM's A operand)
   int short_len = -1;      // contexts up to this many keys split by query head (-1: launcher decides)
   int* counters;           // [B][n_kv_heads] arrival tickets, zero-initialised, self re-arming
-  PfSpec pf{};             // optional MALL prefetch role (B = 1)
   unsigned long long* ts = nullptr;  // probes: [grid][8] s_memrealtime phase stamps (tools/attn_probe.py --stamps)
 };
 constexpr int ATTN_CHUNK = 64;
 void launch_attn_decode(const AttnDecodeArgs& a, hipStream_t st);
 int attn_decode_split(int max_ctx, int B, int n_kv_heads);
-
-// batch-1 QKV GEMV -> attention -> O GEMV (+= residual) as one launch (kernels/attn_block.hip);
-// cnt: [2] hand-off counters zeroed before the launch, err: give-up flag; with_qkv = false: the
-// QKV GEMV is launched on its own first and only attention -> O share a launch
-bool attn_block_supported(const GemvArgs& qkv, const AttnDecodeArgs& at, const GemvArgs& o);
-void launch_attn_block(const GemvArgs& qkv, const AttnDecodeArgs& at, const GemvArgs& o, int* cnt, int* err,
-                       bool with_qkv, hipStream_t st);
 
 // causal flash attention for a prefill chunk of T tokens at positions [start, start+T) of one
 // slot, over the cached keys [0, start+T) (MFMA; kernels/attention_prefill.hip)

@@ -7,6 +7,7 @@ leader writes each command ONCE into a single-producer / multi-consumer byte rin
 POSIX shared-memory segment and every worker reads it in place:
 
   layout  [0:8) head = bytes published   [8:8+8*W) tails[w] = bytes worker w consumed
+          [8+8*W] capacity   [16+8*W] the leader's pid (a worker whose leader died stops polling)
           [RING_HDR : RING_HDR + cap)     records: u32 length | payload (8-byte aligned);
                                           length 0xFFFFFFFF = "skip to the ring start"
   payload a tagged binary encoding: None / bool / int64 / float64 / bytes / str / int64 and float64
@@ -145,9 +146,11 @@ class CommandRing:
             self.cap = cap
             self.shm.buf[:RING_HDR] = bytes(RING_HDR)
             _U64.pack_into(self.shm.buf, 8 + 8 * world, cap)
+            _U64.pack_into(self.shm.buf, 16 + 8 * world, os.getpid())
         self.name = self.shm.name
         self.buf = self.shm.buf
         self._tail = _U64.unpack_from(self.buf, 8 * worker)[0] if worker else 0
+        self.leader_pid = _U64.unpack_from(self.buf, 16 + 8 * world)[0]
 
     # -- producer
     def _head(self) -> int:
@@ -181,8 +184,28 @@ class CommandRing:
         _U64.pack_into(self.buf, 0, head + need)  # publish after the record
 
     # -- consumer
-    def recv(self, spin_s: float = 0.002, idle_sleep_s: float = 0.0002) -> Any:
+    def leader_alive(self) -> bool:
+        """False once the producing process is gone (exited, killed, or a zombie awaiting its reaper)."""
+        pid = self.leader_pid
+        if not pid or pid == os.getpid():
+            return True
+        try:
+            os.kill(pid, 0)
+        except ProcessLookupError:
+            return False
+        except PermissionError:  # pragma: no cover (a foreign process reusing the pid)
+            return False
+        try:
+            with open(f"/proc/{pid}/stat", "rb") as f:
+                return f.read().rsplit(b")", 1)[1].split()[0] != b"Z"
+        except (OSError, IndexError):  # pragma: no cover
+            return True
+
+    def recv(self, spin_s: float = 0.002, idle_sleep_s: float = 0.0002, liveness_s: float = 0.05) -> Any:
+        """Next command; raises ConnectionError when the leader died without a shutdown command (a
+        SIGKILLed leader runs no abort(), so polling forever would orphan this rank's GPU shard)."""
         t_spin = time.monotonic() + spin_s
+        t_live = time.monotonic() + liveness_s
         while True:
             head = self._head()
             if head != self._tail:
@@ -195,8 +218,13 @@ class CommandRing:
                 self._tail += (4 + n + 7) & ~7
                 _U64.pack_into(self.buf, 8 * self.worker, self._tail)
                 return obj
-            if time.monotonic() > t_spin:
+            now = time.monotonic()
+            if now > t_spin:
                 time.sleep(idle_sleep_s)
+                if now > t_live:
+                    if not self.leader_alive():
+                        raise ConnectionError("TP command ring: the leader process is gone")
+                    t_live = now + liveness_s
 
     def close(self) -> None:
         self.buf = None

@@ -77,7 +77,7 @@ def spawn(args) -> int:
 
 
 def measure(preset: str, recipe: str, batch: int, prompt: int, steps: int, warmup: int, use_graph: bool, dist,
-            device: int, act_q8: bool = True, mk: bool = True):
+            device: int, act_q8: bool = True):
     import torch
 
     from aios_amd.models.config import get_preset
@@ -87,8 +87,6 @@ def measure(preset: str, recipe: str, batch: int, prompt: int, steps: int, warmu
     max_ctx = ((prompt + warmup + steps + 2 + 63) // 64) * 64
     eng = random_engine(cfg, recipe, seed=1234, max_ctx=max_ctx, max_slots=max(batch, 1), max_batch=batch,
                         device=device, act_q8=act_q8)
-    if not mk:
-        eng.mk_enabled = False
     slots = list(range(batch))
     toks = []
     for s in slots:
@@ -110,8 +108,7 @@ def measure(preset: str, recipe: str, batch: int, prompt: int, steps: int, warmu
     hist = eng.decode_loop_history(batch, prompt + warmup + 1, steps)
     assert all(0 <= t < cfg.vocab_size for t in hist), "invalid token ids from decode loop"
     info = dict(weight_gb=round(eng.weight_bytes / 1e9, 3), kv_gb=round(eng.kv_bytes / 1e9, 3),
-                workspace_gb=round(eng.workspace_bytes / 1e9, 3),
-                persistent_decode=bool(batch == 1 and eng.mk_available and eng.mk_enabled))
+                workspace_gb=round(eng.workspace_bytes / 1e9, 3))
     del eng
     return dt, info
 
@@ -192,14 +189,14 @@ def main():
 
     act_q8 = not args.fp32_act
     dt, info = measure(args.model, args.recipe, args.batch, args.prompt, args.steps, args.warmup,
-                       not args.no_graph, dist, device, act_q8, mk=not share)
+                       not args.no_graph, dist, device, act_q8)
     secondary = other_act = tp_dt = tp_info = None
     if not args.no_secondary:
         secondary, _ = measure("tinyllama-1.1b", "Q4_K_M", 1, args.prompt, args.steps, args.warmup,
-                               not args.no_graph, dist, device, mk=not share)
+                               not args.no_graph, dist, device)
         # the same Mistral decode with the other GEMV activation precision
         other_act, _ = measure(args.model, args.recipe, args.batch, args.prompt, args.steps, args.warmup,
-                               not args.no_graph, dist, device, not act_q8, mk=not share)
+                               not args.no_graph, dist, device, not act_q8)
         if not args.no_tp:
             if dist is not None:
                 dist.barrier()

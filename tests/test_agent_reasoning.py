@@ -251,3 +251,55 @@ def test_web_api_interpretation_on_request():
     r = _run(a.api_interact({"input": {"url": "http://127.0.0.1:9/x", "interpret": True}}))
     assert _levels(rec) == [IntelligenceLevel.OPERATIONAL] and '"ok": true' in rec.prompts[0][1]
     assert r["interpretation"] == "The service is healthy."
+
+
+# ----------------------------------------------------------------------------------------- fail closed
+def _down(a):
+    """the runtime is unreachable: every think() raises the RPC error"""
+    async def think(prompt, level=IntelligenceLevel.OPERATIONAL, **kw):
+        raise grpc.aio.AioRpcError(grpc.StatusCode.UNAVAILABLE, grpc.aio.Metadata(), grpc.aio.Metadata(),
+                                   details="runtime down")
+    a.think = think
+    return a
+
+
+def _recorder(calls, name):
+    def f(args):
+        calls.append((name, args))
+        return {"success": True, "output": {}}
+    return f
+
+
+def test_gates_fail_closed_when_runtime_down(tmp_path):
+    """firewall rule, running-service restart, package install/remove, tight backup and restore must
+    not run their side effect without the model's review (analyze() returned '' there)"""
+    calls = []
+    fw = _down(_agent("network", _Rec({"firewall.add_rule": _recorder(calls, "fw")})))
+    r = _run(fw.manage_firewall({"description": "block port 22"}))
+    assert not r["success"] and "safety check unavailable" in r["error"]
+
+    sysa = _down(_agent("system", _Rec({"service.status": {"success": True, "output": {"status": "running"}},
+                                        "service.restart": _recorder(calls, "restart")})))
+    r = _run(sysa.restart_service({"description": "restart service nginx"}))
+    assert not r["success"] and "safety check unavailable" in r["error"]
+
+    pkg = _down(_agent("package", _Rec({
+        "pkg.search": {"success": True, "output": {"results": [{"name": "openssl"}]}},
+        "sec.scan": {"success": True, "output": {"findings": [
+            {"package": "openssl", "severity": "critical", "cve": "CVE-1"}]}},
+        "pkg.install": _recorder(calls, "install"),
+        "pkg.list_installed": {"success": True, "output": {"packages": [{"name": "curl", "depends": ["openssl"]}]}},
+        "pkg.remove": _recorder(calls, "remove")})))
+    r = _run(pkg.install_package({"description": "install package openssl", "input": {"name": "openssl"}}))
+    assert not r["success"] and "safety check unavailable" in r["error"]
+    r = _run(pkg.remove_package({"description": "remove package openssl", "input": {"name": "openssl"}}))
+    assert not r["success"] and "safety check unavailable" in r["error"]
+
+    st = _down(_agent("storage", _Rec({
+        "fs.disk_usage": lambda a_: {"success": True, "output": {"used_bytes": 95, "available_bytes": 100}},
+        "fs.copy": _recorder(calls, "copy"), "fs.stat": {"success": True, "output": {}}})))
+    r = _run(st.create_backup({"input": {"source": str(tmp_path)}}))
+    assert not r["success"] and "safety check unavailable" in r["error"]
+    r = _run(st.restore_backup({"input": {"backup": str(tmp_path / "b"), "destination": str(tmp_path / "d")}}))
+    assert not r["success"] and "safety check unavailable" in r["error"]
+    assert calls == []  # no side effect ran

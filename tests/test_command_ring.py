@@ -64,3 +64,40 @@ def test_fanout_wraps_and_backpressures():
     assert [r[1] for r in res] == [n, n]
     assert all(r[2] == ["decode", [[n - 1], [n], mask if (n - 1) % 3 == 0 else b""]] for r in res)
     assert not os.path.exists("/dev/shm/" + ring.name)
+
+
+def _leader(world, q, hold):
+    r = CommandRing(world)
+    q.put(r.name)
+    hold.wait(60)  # never sends: the test SIGKILLs this process
+
+
+def test_worker_exits_when_leader_is_killed():
+    """a SIGKILLed leader runs no shutdown, so recv() must notice and raise ConnectionError
+    (the worker then exits and frees its shard) instead of polling forever"""
+    import signal
+    import time
+    from multiprocessing import shared_memory
+
+    ctx = mp.get_context("spawn")
+    q, hold = ctx.Queue(), ctx.Event()
+    p = ctx.Process(target=_leader, args=(2, q, hold))
+    p.start()
+    name = q.get(timeout=60)
+    r = CommandRing(2, name=name, worker=1)
+    assert r.leader_pid == p.pid and r.leader_alive()
+    try:
+        os.kill(p.pid, signal.SIGKILL)
+        t0 = time.monotonic()
+        with pytest.raises(ConnectionError):
+            r.recv()  # the dead leader is a zombie until joined: still detected
+        assert time.monotonic() - t0 < 5
+    finally:
+        r.close()
+        p.join(10)
+        try:
+            shm = shared_memory.SharedMemory(name=name)
+            shm.close()
+            shm.unlink()
+        except FileNotFoundError:
+            pass

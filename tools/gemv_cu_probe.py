@@ -28,6 +28,13 @@ SHAPES = [  # name, [(fmt, rows)], K, norm, epi
     ("down_q6k", [(Q6, 4096)], 14336, False, "RESID"),
     ("down_q4k", [(Q4, 4096)], 14336, False, "RESID"),
     ("lm_head", [(Q6, 32000)], 4096, True, "STORE"),
+    # diagnostics (--only): QKV with V in Q4_K too (no mixed format), QKV without the RMSNorm,
+    # O with one
+    ("qkv_q4", [(Q4, 6144)], 4096, True, "STORE"),
+    ("qkv_nonorm", [(Q4, 5120), (Q6, 1024)], 4096, False, "STORE"),
+    ("o_norm", [(Q4, 4096)], 4096, True, "RESID"),
+    ("v_q6", [(Q6, 1024)], 4096, True, "STORE"),
+    ("qk_q4", [(Q4, 5120)], 4096, True, "STORE"),
 ]
 
 
@@ -43,7 +50,8 @@ def main():
     E = native.require()
     res = []
     for name, segs, K, norm, epi in SHAPES:
-        if args.only and name not in args.only.split(","):
+        if (args.only and name not in args.only.split(",")) or (not args.only and name in (
+                "qkv_q4", "qkv_nonorm", "o_norm", "v_q6", "qk_q4")):
             continue
         nbytes = sum(BLOCK_INFO[t][1] * r * K // 256 for t, r in segs)
         nrot = int(os.environ.get("NROT", 0)) or max(2, (640 << 20) // nbytes + 1)  # NROT=1: MALL-resident weights
@@ -94,23 +102,30 @@ def main():
             row[tag + "_us"] = round(us, 2)
             row[tag + "_tbs"] = round(nbytes / us / 1e6, 2)
         row["floor_us"] = round(E.bench_stream_read(nbytes // 4096 * 4096, nrot, 1, 4, 512, 20), 2)
-        # phase stamps of one cold launch (the copy least recently touched)
+        # phase stamps of one cold launch (the copy least recently touched); STAMP_SEL=1: the row
+        # kernel's stamps (start, loads issued, x staged, barrier, first pair computed, done)
         G = 256
+        ssel = int(os.environ.get("STAMP_SEL", 3))
         ts = torch.zeros(G * 2 * 8, dtype=torch.int64, device="cuda")
-        launch(mats[0], 3)  # warm the code path
+        launch(mats[0], ssel)  # warm the code path
         for ms in mats[1:]:
-            launch(ms, 3)
+            launch(ms, ssel)
         torch.cuda.synchronize()
-        launch(mats[0], 3, ts.data_ptr())
+        launch(mats[0], ssel, ts.data_ptr())
         torch.cuda.synchronize()
         t = ts.view(G, 2, 8).cpu().numpy().astype(np.float64)
         live = t[:, 0, 0] > 0
         t = t[live]
         t0 = t[:, :, 0][t[:, :, 0] > 0].min()
         rel = (t - t0) / 100.0  # 100 MHz -> us
-        phases = {"start": rel[:, 0, 0], "loads_issued": rel[:, 0, 1], "x_staged": rel[:, 0, 2],
-                  "barrier": rel[:, 0, 3], "compute_w0": rel[:, 0, 4], "compute_w15": rel[:, 1, 4],
-                  "final_barrier": rel[:, 0, 5], "epilogue": rel[:, 0, 6]}
+        if ssel == 1:
+            phases = {"start": rel[:, 0, 0], "loads_issued": rel[:, 0, 1], "x_staged": rel[:, 0, 2],
+                      "barrier": rel[:, 0, 3], "pair_w0": rel[:, 0, 4], "pair_wlast": rel[:, 1, 4],
+                      "done_w0": rel[:, 0, 5], "done_wlast": rel[:, 1, 5]}
+        else:
+            phases = {"start": rel[:, 0, 0], "loads_issued": rel[:, 0, 1], "x_staged": rel[:, 0, 2],
+                      "barrier": rel[:, 0, 3], "compute_w0": rel[:, 0, 4], "compute_w15": rel[:, 1, 4],
+                      "final_barrier": rel[:, 0, 5], "epilogue": rel[:, 0, 6]}
         row["stamps_us"] = {k: [round(pct(v, q), 2) for q in (0, 50, 100)] for k, v in phases.items()}
         res.append(row)
         print(json.dumps(row), flush=True)
