@@ -114,6 +114,24 @@ __device__ __forceinline__ void static_for(F&& f) {
   }
 }
 
+// Touch every 64-byte line of the kernel's argument block (BYTES of explicit arguments + the
+// hidden-argument line after them) in ONE scalar-load clause, waited for once.  Left to itself the
+// compiler loads kernarg fields where they are first used, and each s_waitcnt behind a scalar-cache
+// miss costs an L2 round trip: the batch-1 row GEMV spent 0.67 us between its first instruction and
+// its first weight load in four such waits (tools/gemv_cu_probe.py stamps, round 4).  After this the
+// real field loads hit the scalar cache.
+template <int BYTES>
+__device__ __forceinline__ void kernarg_warm() {
+  using kp_t = const __attribute__((address_space(4))) uint32_t*;
+  const auto* kp = (const __attribute__((address_space(4))) uint8_t*)__builtin_amdgcn_kernarg_segment_ptr();
+  uint32_t acc = 0;
+  static_for<(BYTES + 63) / 64 + 1>([&](auto i) {
+    constexpr int off = decltype(i)::value * 64;
+    acc ^= *(kp_t)(kp + off);
+  });
+  asm volatile("" ::"s"(acc));
+}
+
 // roctx ranges around the engine's host-side phases (load, prefill chunk, decode step / graph
 // replay, sampling): visible with `rocprofv3 --marker-trace` next to the kernel trace; ~free
 // when no profiler is attached.  AIOS_TRACE=0 turns them off.

@@ -27,6 +27,7 @@ namespace aios {
 
 template <int HD, int G>
 __global__ void __launch_bounds__(512) attn_decode_kernel(AttnDecodeArgs a, AttnSplit sp_) {
+  kernarg_warm<sizeof(AttnDecodeArgs) + sizeof(AttnSplit)>();
   const int wg = blockIdx.x;
   const int len = a.seq_len[blockIdx.z];
   if (G > 1 && len <= a.short_len) {

@@ -345,6 +345,7 @@ __device__ __forceinline__ void lg_compute_b(const RawChunk& raw, int it, int nc
 template <int QT0, int QT1, int B = 1, int RSUB = 0>
 __global__ void __launch_bounds__(LG_THREADS) gemv_lds_b1(GemvArgs a, CuPlan pl) {
   static_assert(same_xlayout<QT0, QT1>, "mixed segments must share the activation layout");
+  kernarg_warm<sizeof(GemvArgs) + sizeof(CuPlan)>();
   extern __shared__ __attribute__((aligned(16))) float smem[];
   constexpr bool MIXED = QT0 != QT1;
   constexpr int W = QFmt<QT0>::W, R = QFmt<QT0>::RUNS;

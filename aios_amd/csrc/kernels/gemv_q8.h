@@ -504,6 +504,7 @@ struct FmtTag {
 template <int QT0, int QT1, int B, int U, int PIPE>
 __global__ void __launch_bounds__(q8_max_threads<U>()) gemv_q8_rows(GemvArgs a) {
   static_assert(same_xlayout<QT0, QT1>, "mixed segments must share the activation layout");
+  kernarg_warm<sizeof(GemvArgs)>();
   extern __shared__ __attribute__((aligned(16))) float smem[];
   constexpr bool MIXED = QT0 != QT1;
   constexpr int W = QFmt<QT0>::W, R = QFmt<QT0>::RUNS;
@@ -525,9 +526,7 @@ __global__ void __launch_bounds__(q8_max_threads<U>()) gemv_q8_rows(GemvArgs a) 
   // probes (tools/gemv_cu_probe.py): phase stamps of the first and last wave of every workgroup --
   // 0 start, 1 first weight loads issued, 2 x staged, 3 barrier passed, 4 first pair computed, 5 done
   unsigned long long ts[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  auto stamp = [&](int i) __attribute__((always_inline)) {
-    if (a.dbg_ts) ts[i] = __builtin_amdgcn_s_memrealtime();
-  };
+  auto stamp = [&](int i) __attribute__((always_inline)) { ts[i] = __builtin_amdgcn_s_memrealtime(); };
   stamp(0);
 
   auto seg_idx = [&](int p, int& lrow) -> int {
@@ -708,16 +707,18 @@ __global__ void __launch_bounds__(q8_max_threads<U>()) gemv_q8_rows(GemvArgs a) 
     stamp(3);
     run(FmtTag<QT0>{}, wid, npairs, stride, buf);
   } else {
-    // Mixed formats (Q4_K q/k + Q6_K v of a Q4_K_M QKV): the waves are split in proportion to the
-    // pair counts, whole workgroups per format, so both formats stream concurrently instead of a
-    // Q6_K phase after the Q4_K one (which added a full memory round trip: 11.6 vs 8.3 us per QKV).
-    // The split is per WAVE: a workgroup may hold waves of both formats -- each branch runs the
-    // same x staging and exactly one workgroup barrier (s_barrier counts waves, not call sites),
-    // so when the launch gives every pair its own wave (W == npairs) W0 == np0 and no wave
-    // walks a second pair; the x staging is the same for both formats (same_xlayout).
+    // Mixed formats (Q4_K q/k + Q6_K v of a Q4_K_M QKV): the waves of EVERY workgroup are split
+    // in proportion to the pair counts (Mistral: 10 Q4_K + 2 Q6_K pairs per 12-wave workgroup), so
+    // each CU streams the same bytes -- a split by whole workgroups left the Q6_K CUs 1.46x the
+    // bytes of the others (QKV 8.25 us vs 7.09 with V in Q4_K, profiles/qkv_prologue_r4.txt) -- and
+    // both formats stream concurrently (a Q6_K phase after the Q4_K one added a full memory round
+    // trip: 11.6 vs 8.3 us).  Each branch runs the same x staging and exactly one workgroup barrier
+    // (s_barrier counts waves, not call sites); the x staging is the same for both formats
+    // (same_xlayout).
     const int W = stride;
-    int W0 = (int)(((long)W * np0 + npairs / 2) / npairs);
-    W0 = max(1, min(W - 1, W0));
+    int nw0 = (int)(((long)nw * np0 + npairs / 2) / npairs);
+    nw0 = max(1, min(nw - 1, nw0));
+    const int nw1 = nw - nw0;
     if (W < 16) {  // tiny grid: the sequential schedule
       load(FmtTag<QT0>{}, wid, np0, 0, bufA);
       stamp(1);
@@ -733,25 +734,27 @@ __global__ void __launch_bounds__(q8_max_threads<U>()) gemv_q8_rows(GemvArgs a) 
       load(FmtTag<QT1>{}, np0 + wid, npairs, 0, bufT[0]);
       stamp(1);
       run(FmtTag<QT1>{}, np0 + wid, npairs, stride, bufT);
-    } else if (wid < W0) {
-      load(FmtTag<QT0>{}, wid, np0, 0, bufA);
+    } else if (wave < nw0) {
+      const int p0 = __builtin_amdgcn_readfirstlane(blockIdx.x * nw0 + wave);
+      load(FmtTag<QT0>{}, p0, np0, 0, bufA);
       stamp(1);
       if (!(a.tune_dbg & 1)) q8_stage<QT0, B, NPF>(a, xq, ms, red, pf);
-      qkv_lookup(wid < np0 ? wid : npairs);
+      qkv_lookup(p0 < np0 ? p0 : npairs);
       stamp(2);
       __syncthreads();
       stamp(3);
-      run(FmtTag<QT0>{}, wid, np0, W0, buf);
+      run(FmtTag<QT0>{}, p0, np0, (int)gridDim.x * nw0, buf);
     } else {
+      const int p1 = __builtin_amdgcn_readfirstlane(np0 + blockIdx.x * nw1 + (wave - nw0));
       RawChunk buf1[PIPE][U][GEMV_ROWS];
-      load(FmtTag<QT1>{}, np0 + (wid - W0), npairs, 0, buf1[0]);
+      load(FmtTag<QT1>{}, p1, npairs, 0, buf1[0]);
       stamp(1);
       if (!(a.tune_dbg & 1)) q8_stage<QT0, B, NPF>(a, xq, ms, red, pf);
-      qkv_lookup(np0 + (wid - W0));
+      qkv_lookup(p1);
       stamp(2);
       __syncthreads();
       stamp(3);
-      run(FmtTag<QT1>{}, np0 + (wid - W0), npairs, W - W0, buf1);
+      run(FmtTag<QT1>{}, p1, npairs, (int)gridDim.x * nw1, buf1);
     }
   }
   stamp(5);
@@ -808,7 +811,7 @@ bool launch_gemv_q8(GemvArgs a, hipStream_t st) {
     if constexpr (B == 1) {
       const int nch = a.K / QFmt<QT0>::W;
       int u = a.tune_u;
-      if (u <= 0 || (u > 8 && u != 13 && u != 14 && u != 21 && u != 22 && u != 31)) {
+      if (u <= 0 || (u > 8 && u != 11 && u != 12 && u != 13 && u != 14 && u != 21 && u != 22 && u != 31)) {
         // MI355X sweep (tools/gemv_probe.py --sweep): one chunk per lane per item for short K,
         // except the mid-sized Q4_K/Q5_K projections; the whole K slice in flight for long K
         // (U = 1 for the small/huge-N shapes won in the eager sweep but lost 2-3 % inside the
@@ -816,8 +819,22 @@ bool launch_gemv_q8(GemvArgs a, hipStream_t st) {
         // (re-swept in the captured step, tools/gemv_knob_sweep.sh: U = 1 for K = 4096 gate/up
         // +1.8 %, QKV +1 %, O / lm_head neutral)
         u = nch <= 128 ? 1 : (nch <= 512 ? (nch + 63) / 64 : 2);
+        // Round 4 (tools/gemv_cu_probe.py row-kernel stamps): when the balanced launch gives every
+        // wave exactly ONE row pair, the double-buffered U = 1 pipeline issued the pair's second K
+        // half only after the x-staging barrier -- a second memory round trip on the critical path
+        // (O: barrier 1.9 us, pair computed 3.6 us).  The pair's whole K slice in one single-buffered
+        // item instead: QKV 8.27 -> 7.36 us, O 5.71 -> 5.05 (profiles/qkv_prologue_r4.txt).
+        const int npairs = a.N / 2;
+        static const int balance = [] {
+          const char* e = std::getenv("AIOS_Q8_BALANCE");
+          return e ? std::atoi(e) : 1;
+        }();
+        if (balance && a.tune_grid <= 0 && npairs <= 16 * device_cu_count() && nch <= 128)
+          u = nch <= 64 ? 11 : 12;
       }
       switch (u) {
+        case 11: launch_q8_rows<QT0, QT1, 1, 1, 1>(a, lds, st); break;  // one pair per wave: the K slice in
+        case 12: launch_q8_rows<QT0, QT1, 1, 2, 1>(a, lds, st); break;  // one single-buffered item
         case 13: launch_q8_rows<QT0, QT1, 1, 3, 2>(a, lds, st); break;  // tuning: U = 3/4 double-buffered
         case 14: launch_q8_rows<QT0, QT1, 1, 4, 2>(a, lds, st); break;
         case 21: launch_q8_rows<QT0, QT1, 1, 1, 3>(a, lds, st); break;  // tuning: triple / quad buffers

@@ -53,6 +53,8 @@ def parse():
     ap.add_argument("--fp32-act", action="store_true",
                     help="headline with fp32 activations in the GEMVs instead of int8 (q8_1-style) ones")
     ap.add_argument("--no-tp", action="store_true", help="skip the strategic-tier TP secondary")
+    ap.add_argument("--no-goal-plan", action="store_true",
+                    help="skip the goal->plan latency secondary (BASELINE.json's agent metric)")
     ap.add_argument("--tp-model", default="llama3-70b")
     ap.add_argument("--tp-steps", type=int, default=64)
     ap.add_argument("--dry-run", action="store_true",
@@ -111,6 +113,21 @@ def measure(preset: str, recipe: str, batch: int, prompt: int, steps: int, warmu
                 workspace_gb=round(eng.workspace_bytes / 1e9, 3))
     del eng
     return dt, info
+
+
+def measure_goal_plan(goals: int = 16, timeout_s: float = 60.0):
+    """BASELINE.json's agent metric: p50 goal -> plan latency of tactical goals through the real
+    planner (classification, LLM decomposition over gRPC, task persistence) on an in-process runtime
+    serving the synthetic Mistral-7B tier (tools/bench_goal_plan.py; reference path
+    agent-core/src/task_planner.rs:163-218).  Bounded: a run past timeout_s reports an error."""
+    import argparse as _ap
+    import asyncio
+
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "tools"))
+    from bench_goal_plan import main_async
+
+    ns = _ap.Namespace(model="mistral-7b", goals=goals, warmup=2, burst=0, plan_tokens=160)
+    return asyncio.run(asyncio.wait_for(main_async(ns), timeout_s))
 
 
 def measure_tp(args, rank: int, world: int, device: int, gloo):
@@ -208,6 +225,14 @@ def main():
                 tp_dt, tp_info = None, {"error": f"{type(e).__name__}: {e}"[:300]}
                 print(f"[rank {rank}] tp_strategic failed: {tp_info['error']}", file=sys.stderr, flush=True)
 
+    goal_plan = None
+    if not args.no_secondary and not args.no_goal_plan and rank == 0:
+        try:
+            goal_plan = measure_goal_plan()
+        except Exception as e:  # noqa: BLE001  (reported, never costs the headline)
+            goal_plan = {"error": f"{type(e).__name__}: {e}"[:300]}
+            print(f"goal_plan failed: {goal_plan['error']}", file=sys.stderr, flush=True)
+
     # max over ranks
     if dist is not None:
         t = torch.tensor([dt, secondary or 0.0, other_act or 0.0], dtype=torch.float64)
@@ -285,6 +310,15 @@ def main():
         elif tp_info and "error" in tp_info:
             out["tp_strategic"] = {"metric": f"decode tokens/sec {args.tp_model} {args.recipe} TP={world} (batch 1)",
                                    "value": None, "tp": world, "error": tp_info["error"]}
+        if goal_plan is not None:
+            if "error" in goal_plan:
+                out["goal_plan_p50_ms"] = None
+                out["goal_plan"] = goal_plan
+            else:
+                out["goal_plan_p50_ms"] = goal_plan["value"]
+                out["goal_plan"] = {k: goal_plan[k] for k in ("metric", "p90_ms", "goals", "tasks_per_goal",
+                                                              "reactive_p50_ms", "plan_tokens_cap", "model",
+                                                              "baseline_ms")}
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.barrier()

@@ -32,3 +32,21 @@ def test_gpus_mismatch_is_refused():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4", "--dry-run"],
                        capture_output=True, text=True, timeout=120, env=env, cwd=ROOT)
     assert r.returncode != 0 and "WORLD_SIZE=2" in (r.stderr + r.stdout)
+
+
+def test_gpus_8_through_torchrun_dry_run():
+    """the driver's 8-GPU scaling launch shape (torch.distributed.run, 8 ranks, 127.0.0.1) on the CPU:
+    every rank joins the process group and reports WORLD_SIZE 8"""
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port),
+                        os.path.join(ROOT, "bench.py"), "--gpus", "8", "--dry-run"],
+                       capture_output=True, text=True, timeout=300, env=_env(), cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [json.loads(m) for m in re.findall(r"\{[^{}]*\}", r.stdout)]
+    assert sorted(d["rank"] for d in lines) == list(range(8))
+    assert all(d["world"] == 8 for d in lines)

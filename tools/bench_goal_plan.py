@@ -91,28 +91,29 @@ async def main_async(args):
     t = time.perf_counter()
     burst = await asyncio.gather(*(submit(TACTICAL[i % len(TACTICAL)] + f" burst {i}") for i in range(args.burst)))
     burst_s = time.perf_counter() - t
+    n_burst = len(burst)
     # every measured goal must have gone through the LLM decomposition (tactical / strategic
     # classification) -- a goal the classifier routes to the heuristic planner is not a sample
     mislabelled = [d for d in TACTICAL if core.classify(d) not in ("tactical", "strategic")]
     assert not mislabelled, f"goals planned without the LLM: {mislabelled}"
     lat = sorted(x[0] for x in tac)
     rlat = sorted(x[0] for x in rea)
-    blat = sorted(x[0] for x in burst)
+    blat = sorted(x[0] for x in burst) or [0.0]
     q = lambda v, p: v[min(len(v) - 1, int(p * len(v)))]
     out = {"metric": "p50 agent goal->plan latency (tactical goals, LLM decomposition)",
            "value": round(statistics.median(lat), 1), "unit": "ms", "higher_is_better": False,
            "p90_ms": round(q(lat, 0.9), 1), "mean_ms": round(statistics.mean(lat), 1), "goals": len(lat),
            "tasks_per_goal": round(statistics.mean(x[1] for x in tac), 2),
            "reactive_p50_ms": round(statistics.median(rlat), 2),
-           "burst": {"concurrent_goals": args.burst, "wall_s": round(burst_s, 3), "p50_ms": round(statistics.median(blat), 1)},
+           "burst": {"concurrent_goals": n_burst, "wall_s": round(burst_s, 3), "p50_ms": round(statistics.median(blat), 1)},
            "plan_tokens_cap": args.plan_tokens, "model": f"{args.model} Q4_K_M (random-init, synthetic vocab)",
            "baseline_ms": "200-500 (tactical tier, docs/VISION.md:45)", "model_load_s": round(load_s, 1),
            "data": "synthetic goals; decomposition output length fixed by plan_tokens_cap (random weights)"}
-    print(json.dumps(out), flush=True)
     for s in servers.values():
         await s.stop(0)
     await close_all()
     await mgr.unload_model("mistral-7b")
+    return out
 
 
 def main():
@@ -122,7 +123,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--burst", type=int, default=8)
     ap.add_argument("--plan-tokens", type=int, default=160)
-    asyncio.run(main_async(ap.parse_args()))
+    print(json.dumps(asyncio.run(main_async(ap.parse_args()))), flush=True)
 
 
 if __name__ == "__main__":

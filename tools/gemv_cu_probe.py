@@ -71,11 +71,26 @@ def main():
         epic = getattr(E, "EPI_" + epi)
         ldy = N // 2 if epi == "SWIGLU" else N
 
+        # PROBE_XDIRTY: x rewritten before every launch, as the decode step's residual producers do --
+        # "store" (plain stores, torch mul_) or "atomic" (memory-side float atomics, torch index_add_);
+        # the writer's own time (a graph of writers alone) is subtracted
+        xdirty = os.environ.get("PROBE_XDIRTY", "")
+        xidx = torch.arange(K, device="cuda")
+        xzero = torch.zeros(B, K, device="cuda")
+
+        def writer():
+            if xdirty == "store":
+                x.mul_(1.0)
+            elif xdirty == "atomic":
+                x.index_add_(1, xidx, xzero)
+
         def launch(ms, sel, ts=0):
+            writer()
             st = torch.cuda.current_stream().cuda_stream
             # sel 4: the LDS engine with its consumers skipping the dot work (bare ring cadence)
             E.gemv(ms, B, x.data_ptr(), K, nw.data_ptr() if norm else 0, 1e-5, y.data_ptr(), ldy, epic, st, 0, 1,
-                   kernel_sel=3 if sel == 4 else sel, tune_dbg=0x10000 if sel == 4 else 0, dbg_ts=ts)
+                   kernel_sel=3 if sel == 4 else sel, tune_dbg=0x10000 if sel == 4 else 0, dbg_ts=ts,
+                   tune_u=int(os.environ.get("PROBE_U", 0)))  # PROBE_U: the row kernel's U (12: U 2 unbuffered)
 
         row = dict(shape=name, B=B, mb=round(nbytes / 1e6, 1))
         sels = ((1, "rows"), (2, "cu"), (3, "lds"), (4, "ring"), (0, "auto")) if B == 1 else ((3, "lds"), (1, "rows"))
@@ -99,6 +114,21 @@ def main():
             e1.record()
             torch.cuda.synchronize()
             us = e0.elapsed_time(e1) * 1e3 / (reps * nrot * nrep)
+            if xdirty and "writer_us" not in row:
+                gw = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(gw):
+                    for _ in range(nrep * nrot):
+                        writer()
+                gw.replay()
+                torch.cuda.synchronize()
+                e0.record()
+                for _ in range(reps):
+                    gw.replay()
+                e1.record()
+                torch.cuda.synchronize()
+                row["writer_us"] = round(e0.elapsed_time(e1) * 1e3 / (reps * nrot * nrep), 2)
+            if xdirty:
+                us -= row["writer_us"]
             row[tag + "_us"] = round(us, 2)
             row[tag + "_tbs"] = round(nbytes / us / 1e6, 2)
         row["floor_us"] = round(E.bench_stream_read(nbytes // 4096 * 4096, nrot, 1, 4, 512, 20), 2)
