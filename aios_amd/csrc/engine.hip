@@ -841,6 +841,11 @@ void Engine::layer_decode(int l, int B) {
       a.epi = EPI_STORE; a.y = qkv_; a.ldy = qd + 2 * kvd;
     }
     apply_knobs(a, "QKV");
+    static const int qkv_dbg = [] {  // probes only (AIOS_QKV_DBG=0x20000: epilogue lookups skipped)
+      const char* e = std::getenv("AIOS_QKV_DBG");
+      return e ? (int)std::strtol(e, nullptr, 0) : 0;
+    }();
+    a.tune_dbg = qkv_dbg;
     return a;
   };
   // ---- QKV (+RMSNorm prologue, RoPE + KV-cache epilogue)

@@ -572,7 +572,7 @@ __global__ void __launch_bounds__(q8_max_threads<U>()) gemv_q8_rows(GemvArgs a) 
   };
   auto qkv_lookup = [&](int p_first) __attribute__((always_inline)) {
     if constexpr (B == 1) {
-      if (a.epi == EPI_QKV) {
+      if (a.epi == EPI_QKV && !(a.tune_dbg & 0x20000)) {  // (probe bit: lookups skipped, timing only)
         pos0 = a.pos[0];
         kv_blk0 = kv_block(a.block_table, a.max_ctx / KV_BLOCK, a.slot ? a.slot[0] : 0, pos0);
         if (p_first < npairs) {
