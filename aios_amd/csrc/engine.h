@@ -189,6 +189,9 @@ class Engine {
 
   // workspace
   float *x_ = nullptr, *q_ = nullptr, *attn_ = nullptr, *ff_ = nullptr, *qkv_ = nullptr;
+  // the GEMV path's SwiGLU hand-off in bf16 (gate/up epilogue -> down staging: half the bytes every
+  // down workgroup re-reads; AIOS_FF16=0 keeps fp32), [max_batch][d_ff]
+  bf16_t* gv_ff16_ = nullptr;
   float *opart_ = nullptr, *ml_ = nullptr, *logits_ = nullptr;
   int *d_tokens_ = nullptr, *d_pos_ = nullptr, *d_seqlen_ = nullptr, *d_slot_ = nullptr, *d_history_ = nullptr;
   int *d_topk_ = nullptr, *d_step_ = nullptr;

@@ -32,10 +32,13 @@ struct GemvArgs {
   unsigned long long* dbg_ts;   // probes: per-workgroup phase timestamps (s_memrealtime) or null
   const float* x;               // [B][ldx] fp32 input (residual stream if norm_w != null)
   int ldx;
+  const bf16_t* x16;            // int8-activation kernels only: bf16 input [B][ldx] read instead of x
+                                //   (the SwiGLU output handed from gate/up to down at half the bytes)
   const float* norm_w;          // RMSNorm weight [K] or null
   float eps;
   float* y;                     // output, see epilogue
   int ldy;
+  bf16_t* y16;                  // EPI_SWIGLU: bf16 output [B][ldy] written instead of y (or null)
   int epi;
   // QKV epilogue
   const float* bias;            // [N] or null

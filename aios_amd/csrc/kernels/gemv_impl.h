@@ -197,7 +197,9 @@ __device__ __forceinline__ void gemv_epilogue(const GemvArgs& a, int grow, int b
     } break;
     case EPI_SWIGLU: {
       const float g = v0, u = v1;  // rows (2i, 2i+1) = (gate_i, up_i)
-      a.y[(size_t)b * a.ldy + (grow >> 1)] = g / (1.f + __expf(-g)) * u;
+      const float h = g / (1.f + __expf(-g)) * u;
+      if (a.y16) a.y16[(size_t)b * a.ldy + (grow >> 1)] = f32_to_bf16(h);
+      else a.y[(size_t)b * a.ldy + (grow >> 1)] = h;
     } break;
     case EPI_QKV: {
       if (a.bias) { v0 += a.bias[grow]; v1 += a.bias[grow + 1]; }
@@ -562,6 +564,7 @@ void launch_gemv_pair(const GemvArgs& a, hipStream_t st) {
       if (a.B > 4 && launch_gemv_q8<QT0, QT1, 8>(a, st)) return;
     }
   }
+  if (a.x16 || a.y16) throw std::runtime_error("bf16 GEMV input / SwiGLU output: int8-activation kernels only");
   if (!a.force_v1) {
     if (a.B == 1 && launch_gemv_persistent<QT0, QT1, 1, 2>(a, st)) return;
     if (a.B == 2 && launch_gemv_persistent<QT0, QT1, 2, 2>(a, st)) return;

@@ -229,14 +229,29 @@ __device__ __forceinline__ void q8_stage_prefetch(const GemvArgs& a, StagePre<NP
     const int tt = t < total ? t : 0;
     const int b = tt / noct, o = tt - b * noct;
     const float* src = a.x + (size_t)b * a.ldx + 8 * o;
-    pf.x0[i] = ldx4(src);
-    pf.x1[i] = ldx4(src + 4);
+    if (a.x16) {  // 8 bf16 in one 16-B load, widened in q8_stage (no wait here)
+      const uint4 u = *(const uint4*)(a.x16 + (size_t)b * a.ldx + 8 * o);
+      pf.x0[i] = make_float4(__uint_as_float(u.x), __uint_as_float(u.y), __uint_as_float(u.z), __uint_as_float(u.w));
+    } else {
+      pf.x0[i] = ldx4(src);
+      pf.x1[i] = ldx4(src + 4);
+    }
     // the norm weights of every prefetched pass too: a load issued after the weight stream would
     // make its wait cover every weight load in flight
     const float* g = a.norm_w ? a.norm_w + 8 * o : src;
     pf.g0[i] = *(const float4*)g;
     pf.g1[i] = *(const float4*)(g + 4);
   }
+}
+
+// 8 bf16 (as the 4 raw words of a float4) -> two float4
+__device__ __forceinline__ void bf16x8_widen(float4 raw, float4& f0, float4& f1) {
+  const uint32_t w0 = __float_as_uint(raw.x), w1 = __float_as_uint(raw.y), w2 = __float_as_uint(raw.z),
+                 w3 = __float_as_uint(raw.w);
+  f0 = make_float4(__uint_as_float(w0 << 16), __uint_as_float(w0 & 0xffff0000u), __uint_as_float(w1 << 16),
+                   __uint_as_float(w1 & 0xffff0000u));
+  f1 = make_float4(__uint_as_float(w2 << 16), __uint_as_float(w2 & 0xffff0000u), __uint_as_float(w3 << 16),
+                   __uint_as_float(w3 & 0xffff0000u));
 }
 
 // quantise one octet (t -> row b, octet o) of x (times the norm weight) into the staging layout
@@ -301,13 +316,23 @@ __device__ __forceinline__ void q8_stage(const GemvArgs& a, int8_t* xq, float2* 
     const int t = tid + i * nthr;
     if (t < total) {
       const int b = t / noct, o = t - b * noct;
-      q8_octet<QT, B>(a, b, o, pf.x0[i], pf.x1[i], pf.g0[i], pf.g1[i], xq, ms, ssq);
+      float4 f0 = pf.x0[i], f1 = pf.x1[i];
+      if (a.x16) bf16x8_widen(pf.x0[i], f0, f1);
+      q8_octet<QT, B>(a, b, o, f0, f1, pf.g0[i], pf.g1[i], xq, ms, ssq);
     }
   }
   for (int t = tid + NPF * nthr; t < total; t += nthr) {
     const int b = t / noct, o = t - b * noct;
     const float* src = a.x + (size_t)b * a.ldx + 8 * o;
-    const float4 f0 = ldx4(src), f1 = ldx4(src + 4);
+    float4 f0, f1;
+    if (a.x16) {
+      const uint4 u = *(const uint4*)(a.x16 + (size_t)b * a.ldx + 8 * o);
+      bf16x8_widen(make_float4(__uint_as_float(u.x), __uint_as_float(u.y), __uint_as_float(u.z), __uint_as_float(u.w)),
+                   f0, f1);
+    } else {
+      f0 = ldx4(src);
+      f1 = ldx4(src + 4);
+    }
     float4 g0 = f0, g1 = f1;
     if (a.norm_w) {
       g0 = *(const float4*)(a.norm_w + 8 * o);
@@ -431,9 +456,11 @@ __device__ __forceinline__ void gemv_epilogue1(const GemvArgs& a, int grow, floa
       unsafeAtomicAdd(a.y + grow, v0);
       if (grow + 1 < nrow) unsafeAtomicAdd(a.y + grow + 1, v1);
       break;
-    case EPI_SWIGLU:
-      a.y[grow >> 1] = v0 / (1.f + __expf(-v0)) * v1;
-      break;
+    case EPI_SWIGLU: {
+      const float h = v0 / (1.f + __expf(-v0)) * v1;
+      if (a.y16) a.y16[grow >> 1] = f32_to_bf16(h);
+      else a.y[grow >> 1] = h;
+    } break;
     case EPI_QKV: {
       if (a.bias) {
         v0 += a.bias[grow];
