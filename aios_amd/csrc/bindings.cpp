@@ -287,6 +287,7 @@ PYBIND11_MODULE(_engine, m) {
         c.allgather_cols((float*)data, rows, slice, ld, S(st));
       }, py::arg("data"), py::arg("rows"), py::arg("slice"), py::arg("ld"), py::arg("stream") = 0)
       .def_property("two_shot_min", &XgmiComm::two_shot_min, &XgmiComm::set_two_shot_min)
+      .def_property("call_wg", &XgmiComm::call_wg, &XgmiComm::set_call_wg)
       .def_property("bf16_payload", &XgmiComm::bf16_payload, &XgmiComm::set_bf16_payload)
       .def("error", &XgmiComm::error)
       .def("reset_error", &XgmiComm::reset_error)

@@ -81,6 +81,12 @@ class XgmiComm {
   int world() const { return h_.world; }
   size_t capacity() const { return h_.cap; }
   size_t two_shot_min() const { return two_shot_min_; }
+  // workgroups per collective launch (elements per call = wg * AR_CHUNK, larger messages split):
+  // AR_MAX_WG by default; ranks that SHARE one GPU (the single-GPU test setting) must fit all their
+  // spinning workgroups on it at once, so tp.create_comm lowers it to 1024 / ranks-per-GPU.  Every
+  // rank must use the same value (the per-workgroup epochs follow the call sequence).
+  int call_wg() const { return (int)(call_cap_ / AR_CHUNK); }
+  void set_call_wg(int wg);
   void set_two_shot_min(size_t n) { two_shot_min_ = n; }
   bool bf16_payload() const { return bf16_; }
   void set_bf16_payload(bool on) { bf16_ = on; }
@@ -103,6 +109,7 @@ class XgmiComm {
   int device_ = 0;
   bool connected_ = false;
   size_t two_shot_min_ = 64 * 1024;  // floats (256 KB)
+  size_t call_cap_ = AR_MAX_CALL;    // elements per launch (see set_call_wg)
   bool bf16_ = true;                 // bf16 staging for the two-shot (prefill) path
 };
 

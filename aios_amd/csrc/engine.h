@@ -207,6 +207,11 @@ class Engine {
   uint64_t* d_seed_ = nullptr;
   uint64_t* d_seeds_ = nullptr;    // [max_batch] per-row sampling seeds (in the parameter block)
   int* d_fpos_ = nullptr;          // sample_first's RNG position
+  // StepPrep outputs of the decode step's embedding launch: [max_batch][2] {pos, KV block} and
+  // [max_batch][head_dim / 2] rope rows, read by the batch-1 QKV epilogue while step_prep_on_
+  int* d_step_kv_ = nullptr;
+  float2* d_step_rope_ = nullptr;
+  bool step_prep_on_ = false;
   void fill_row_seeds(uint64_t* host_seeds, int B, uint64_t seed, const std::vector<uint64_t>& seeds);
   uint8_t* d_mask_ = nullptr;
   int n_chunks_ = 0;

@@ -523,6 +523,8 @@ void Engine::finalize() {
   attn_bt_ = d_row_bt_;
   attn_bt_rows_ = 1;
   d_step_ = ibuf(4);
+  d_step_kv_ = ibuf((size_t)Bm * 2);
+  d_step_rope_ = (float2*)fbuf((size_t)Bm * hd);
   d_fpos_ = ibuf(4);
   sample_ws_bytes_ = sample_ws_bytes(Bm, V);
   sample_ws_ = dmalloc(sample_ws_bytes_);
@@ -841,6 +843,7 @@ void Engine::layer_decode(int l, int B) {
       a.k_cache = k_cache_ + (size_t)l * layer_kv_elems_;
       a.v_cache = v_cache_ + (size_t)l * layer_kv_elems_;
       a.block_table = d_bt_;
+      if (step_prep_on_ && B == 1) { a.step_kv = d_step_kv_; a.step_rope = d_step_rope_; }
     } else {
       a.epi = EPI_STORE; a.y = qkv_; a.ldy = qd + 2 * kvd;
     }
@@ -949,9 +952,14 @@ void Engine::lm_head(int B, const float* x, int ldx) {
 
 void Engine::enqueue_decode_step(int B) {
   const int d = cfg_.d_model, V = cfg_.vocab_size;
-  launch_get_rows(tok_embd_.w, d_tokens_, B, x_, d, 1.f, stream_);
+  {
+    StepPrep sp{d_pos_, d_slot_, d_bt_, kv_maxb_, rope_cs_, cfg_.head_dim / 2, d_step_kv_, d_step_rope_};
+    launch_get_rows_step(tok_embd_.w, d_tokens_, B, x_, d, 1.f, sp, stream_);
+  }
+  step_prep_on_ = rope_cs_ != nullptr;
   nrm_lm_ = false;
   for (int l = 0; l < cfg_.n_layers; ++l) layer_decode(l, B);
+  step_prep_on_ = false;
   lm_head(B, x_, d);
   nrm_lm_ = false;
   SampleArgs s;

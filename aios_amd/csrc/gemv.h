@@ -51,6 +51,11 @@ struct GemvArgs {
   bf16_t* k_cache;              // layer base of the paged pool [blocks][n_kv][KV_BLOCK][hd]
   const int* block_table;       // [slots][max_ctx / KV_BLOCK] or null (identity)
   bf16_t* v_cache;
+  // batch-1 decode: {pos, physical KV block} and the RoPE (cos, sin) row of this step's position,
+  // prepared by the step's embedding launch (StepPrep, ops.h) -- no pos -> block table / rope chain
+  // in the QKV kernel (null: looked up from pos / slot / block_table)
+  const int* step_kv;
+  const float2* step_rope;
 };
 
 void launch_gemv(const GemvArgs& a, hipStream_t st);

@@ -371,14 +371,18 @@ void XgmiComm::connect(const std::vector<std::string>& handles) {
   connected_ = true;
 }
 
+void XgmiComm::set_call_wg(int wg) {
+  call_cap_ = (size_t)std::max(1, std::min(AR_MAX_WG, wg)) * AR_CHUNK;
+}
+
 void XgmiComm::allreduce(float* data, size_t n, float* residual, hipStream_t st) {
   if (!connected_) throw std::runtime_error("XgmiComm: allreduce before connect()");
   if (h_.world == 1) {
     if (residual) launch_add(residual, data, n, st);
     return;
   }
-  for (size_t off = 0; off < n; off += h_.cap) {
-    const size_t m = std::min(h_.cap, n - off);
+  for (size_t off = 0; off < n; off += call_cap_) {
+    const size_t m = std::min(call_cap_, n - off);
     float* d = data + off;
     float* r = residual ? residual + off : nullptr;
     if (m >= two_shot_min_ && m % 4 == 0) {
@@ -397,7 +401,7 @@ void XgmiComm::allreduce_norm(float* data, int rows, int d, float* residual, con
   const size_t n = (size_t)rows * d;
   if (h_.world == 1) {
     launch_add_norm(residual, data, rows, d, nm, st);
-  } else if (d % RNORM_COLS == 0 && n <= h_.cap && n < two_shot_min_) {
+  } else if (d % RNORM_COLS == 0 && n <= call_cap_ && n < two_shot_min_) {
     if (nm.parts < d / RNORM_COLS || nm.parts > 64 || nm.parts % 4)
       throw std::runtime_error("XgmiComm::allreduce_norm: parts must be resid_norm_parts(d)");
     hipLaunchKernelGGL((allreduce_oneshot<true>), dim3(grid_for(n)), dim3(AR_THREADS), 0, st, d_, data, n, residual, d,
@@ -411,8 +415,8 @@ void XgmiComm::allreduce_norm(float* data, int rows, int d, float* residual, con
 void XgmiComm::allgather_cols(float* data, int rows, int slice, int ld, hipStream_t st) {
   if (!connected_) throw std::runtime_error("XgmiComm: allgather before connect()");
   if (h_.world == 1 || rows <= 0) return;
-  if ((size_t)h_.world * slice > h_.cap) throw std::runtime_error("XgmiComm: all-gather slice above capacity");
-  const int rows_per = (int)std::max<size_t>(1, h_.cap / ((size_t)h_.world * slice));
+  if ((size_t)h_.world * slice > call_cap_) throw std::runtime_error("XgmiComm: all-gather slice above capacity");
+  const int rows_per = (int)std::max<size_t>(1, call_cap_ / ((size_t)h_.world * slice));
   for (int r0 = 0; r0 < rows; r0 += rows_per) {
     const int nr = std::min(rows_per, rows - r0);
     const size_t total = (size_t)h_.world * nr * slice;

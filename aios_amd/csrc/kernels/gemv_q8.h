@@ -428,6 +428,13 @@ __device__ __forceinline__ void q8_compute(const RawChunk (&raw)[U][GEMV_ROWS], 
 }
 
 // ---------------------------------------------------------------------------------------------
+// a zero the compiler cannot see through: keeps a uniform load on the vector path (vmcnt-ordered)
+__device__ __forceinline__ int opaque_zero() {
+  int z;
+  asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+  return z;
+}
+
 // B = 1 epilogue that issues no global LOAD: vmcnt drains in issue order, so a load here would
 // wait for the next item's whole weight prefetch.  The residual add is a no-return atomic add
 // (each element has exactly one writer, so the result is deterministic); the RoPE (cos, sin) of
@@ -588,10 +595,16 @@ __global__ void __launch_bounds__(q8_max_threads<U>()) gemv_q8_rows(GemvArgs a) 
   // profiles/qkv_prologue_r4.txt); the values are waited for only in the epilogue.
   int pos0 = 0, kv_blk0 = 0, rope_p = -1;
   float2 rope_w = make_float2(1.f, 0.f);
+  // decode steps: the step's embedding launch prepared pos / KV block / rope row (StepPrep) -- loads
+  // with no dependency, issued here, waited for only in the epilogue
+  // (vector loads through an opaque zero offset: a scalar load's lgkmcnt wait would also gate every
+  // LDS access of the compute until it returned)
+  const bool prepped = B == 1 && a.epi == EPI_QKV && a.step_kv;
   auto rope_of = [&](int p) __attribute__((always_inline)) -> float2 {
     int part, head, lr;
     qkv_part(a, a.row_base + 2 * p, part, head, lr);
     const int pp = lr >> 1;
+    if (prepped) return a.step_rope[(part < 2 ? pp : 0) + opaque_zero()];
     if (a.rope_cs) return a.rope_cs[(size_t)pos0 * (a.head_dim >> 1) + (part < 2 ? pp : 0)];
     float sn, cs;
     sincosf((float)pos0 * powf(a.rope_base, -2.f * (float)pp / (float)a.head_dim), &sn, &cs);
@@ -599,7 +612,15 @@ __global__ void __launch_bounds__(q8_max_threads<U>()) gemv_q8_rows(GemvArgs a) 
   };
   auto qkv_lookup = [&](int p_first) __attribute__((always_inline)) {
     if constexpr (B == 1) {
-      if (a.epi == EPI_QKV && !(a.tune_dbg & 0x20000)) {  // (probe bit: lookups skipped, timing only)
+      if (prepped) {
+        const int2 kv = *(const int2*)(a.step_kv + opaque_zero());
+        pos0 = kv.x;
+        kv_blk0 = kv.y;
+        if (p_first < npairs) {
+          rope_w = rope_of(p_first);
+          rope_p = p_first;
+        }
+      } else if (a.epi == EPI_QKV && !prepped && !(a.tune_dbg & 0x20000)) {  // (probe bit: timing only)
         pos0 = a.pos[0];
         kv_blk0 = kv_block(a.block_table, a.max_ctx / KV_BLOCK, a.slot ? a.slot[0] : 0, pos0);
         if (p_first < npairs) {

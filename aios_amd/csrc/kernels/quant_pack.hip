@@ -158,6 +158,34 @@ __global__ void get_rows_kernel(QWeight w, const int* __restrict__ rows, int nro
     out[(size_t)i * ldo + k] = dq_elem(w, r, k) * scale;
 }
 
+// the same gather; workgroup (0, i) also prepares row i's StepPrep outputs
+__global__ void get_rows_step_kernel(QWeight w, const int* __restrict__ rows, int nrows, float* __restrict__ out,
+                                     int ldo, float scale, StepPrep sp) {
+  const int i = blockIdx.y;
+  if (i >= nrows) return;
+  if (blockIdx.x == 0) {
+    const int pos = sp.pos[i];
+    if (threadIdx.x == 0) {
+      const int slot = sp.slot ? sp.slot[i] : i;
+      sp.kv[2 * i] = pos;
+      sp.kv[2 * i + 1] = kv_block(sp.block_table, sp.maxb, slot, pos);
+    }
+    if (sp.rope_cs)
+      for (int t = threadIdx.x; t < sp.half; t += blockDim.x)
+        sp.rope[(size_t)i * sp.half + t] = sp.rope_cs[(size_t)pos * sp.half + t];
+  }
+  const int r = rows ? rows[i] : i;
+  for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < w.cols; k += gridDim.x * blockDim.x)
+    out[(size_t)i * ldo + k] = dq_elem(w, r, k) * scale;
+}
+
+void launch_get_rows_step(const QWeight& w, const int* rows, int nrows, float* out, int ldo, float scale,
+                          const StepPrep& prep, hipStream_t st) {
+  const int T = 256;
+  const int gx = std::min(64, (w.cols + T - 1) / T);
+  hipLaunchKernelGGL(get_rows_step_kernel, dim3(gx, nrows), dim3(T), 0, st, w, rows, nrows, out, ldo, scale, prep);
+}
+
 void launch_get_rows(const QWeight& w, const int* rows, int nrows, float* out, int ldo, float scale, hipStream_t st) {
   const int T = 256;
   const int gx = std::min(64, (w.cols + T - 1) / T);

@@ -13,6 +13,21 @@ namespace aios {
 void launch_repack(int qt, const void* raw, size_t nblocks, const QWeight& w, hipStream_t st);
 void launch_get_rows(const QWeight& w, const int* rows, int nrows, float* out, int ldo, float scale,
                      hipStream_t st);
+// Per-step lookups the batch-1 QKV epilogue needs, done by the step's first (embedding) launch while
+// it gathers the rows: kv[b] = {pos[b], physical KV block of (slot[b], pos[b])}, rope[b][:] = the
+// (cos, sin) row of pos[b].  Every layer's QKV GEMV then loads them with no dependent round trip.
+struct StepPrep {
+  const int* pos;          // [B]
+  const int* slot;         // [B] or null (row b)
+  const int* block_table;  // [slots][maxb] or null (identity)
+  int maxb;
+  const float2* rope_cs;   // [max_ctx][half] or null (no rope rows)
+  int half;
+  int* kv;                 // out [B][2]
+  float2* rope;            // out [B][half]
+};
+void launch_get_rows_step(const QWeight& w, const int* rows, int nrows, float* out, int ldo, float scale,
+                          const StepPrep& prep, hipStream_t st);
 void launch_dequant_bf16(const QWeight& w, void* out, hipStream_t st);
 void launch_legacy_to_bf16(int qt, const void* raw, size_t n, void* out, hipStream_t st);
 void fill_random_weight(const QWeight& w, uint64_t seed, float amp, hipStream_t st);

@@ -44,6 +44,17 @@ def comm_kind() -> str:
     return k
 
 
+def ranks_per_gpu(world: int) -> int:
+    """TP ranks that share one GPU on this node (1 on a node with a GPU per rank)."""
+    try:
+        import torch
+
+        n = torch.cuda.device_count()
+    except Exception:  # noqa: BLE001
+        n = 0
+    return max(1, -(-world // n)) if n > 0 else 1
+
+
 def create_comm(rank: int, world: int, device: int, cap_floats: int, group=None, kind: Optional[str] = None):
     """XgmiComm (or RcclComm, see comm_kind) connected to every rank of `group` (default: the
     default process group)."""
@@ -58,6 +69,9 @@ def create_comm(rank: int, world: int, device: int, cap_floats: int, group=None,
             dist.broadcast_object_list(uid, src=0, group=group)
         return m.RcclComm(rank, world, device, uid[0])
     comm = m.XgmiComm(rank, world, device, cap_floats)
+    per_gpu = ranks_per_gpu(world)
+    if per_gpu > 1:  # every spinning workgroup of every rank must be resident on the shared GPU at once
+        comm.call_wg = max(1, min(512, 1024 // per_gpu))
     if world > 1:
         handles: List[Any] = [None] * world
         dist.all_gather_object(handles, comm.ipc_handle(), group=group)

@@ -1,6 +1,8 @@
 """Tensor parallelism: weight sharding (CPU), the leader/worker command channel over gloo with
 world_size 2 (CPU, multi-process), and -- on a GPU box -- the xGMI one-shot all-reduce and a
-TP=2/TP=4 sharded model against TP=1 (several ranks sharing one GPU; tools/tp_check.py)."""
+TP=2/4/8 sharded model against TP=1 (several ranks sharing one GPU; tools/tp_check.py).  World 8 is
+the strategic tier's target degree and AR_MAX_RANKS: its IPC mesh, one-shot pull over 7 peers and
+vocab-parallel all-gather run here with 8 processes on one GPU (not a scaling measurement)."""
 import json
 import os
 import subprocess
@@ -113,8 +115,8 @@ def test_engine_config_vocab_parallel_rules():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world,gemm_prefill,prompt_len", [(2, 0, 21), (4, 0, 21), (2, 1, 21), (2, 1, 640),
-                                                          (2, 1, 9)])
+@pytest.mark.parametrize("world,gemm_prefill,prompt_len", [(2, 0, 21), (4, 0, 21), (8, 0, 21), (2, 1, 21),
+                                                          (2, 1, 640), (2, 1, 9)])
 def test_tp_xgmi_allreduce_and_sharded_model(tmp_path, world, gemm_prefill, prompt_len):
     """TP=N vs TP=1 on the same weights.  With the fp32-activation GEMV prefill (gemm_prefill=0)
     the only differences are fp32 summation order: 1e-3 of the logit scale.  The MFMA prefill

@@ -48,6 +48,13 @@ def main():
     torch.cuda.set_device(dev)
     dist.init_process_group("gloo")
     res = {"world": world, "device_count": torch.cuda.device_count()}
+    t_start = time.time()
+
+    def log(msg):  # progress on stderr (rank 0): a silent multi-minute run reads as a hang
+        if rank == 0:
+            print(f"[tp_check {time.time() - t_start:6.1f}s] {msg}", file=sys.stderr, flush=True)
+
+    log(f"world {world}, {torch.cuda.device_count()} device(s)")
 
     # ---- 1. collective numerics
     comm = create_comm(rank, world, dev, 64 * 8192)
@@ -76,6 +83,7 @@ def main():
                          "scale": float(torch.stack(allx).abs().max())})
     comm.bf16_payload = True
     res["allreduce"] = errs
+    log("all-reduce numerics done")
     # column all-gather (vocab-parallel logits): rank r fills its slice, every rank gets all
     gerr = []
     for rows, slice_ in ((1, 512), (3, 4000), (8, 64)):
@@ -119,6 +127,7 @@ def main():
                      "scale": float(torch.stack(allx).abs().max())})
     res["allreduce_norm"] = nerr
     res["comm_error_flag"] = bool(comm.error())
+    log("all-gather / all-reduce+norm done")
 
     # timing at decode size (B=1, d=8192): one-shot; at prefill size (512 x 8192): two-shot
     for n, key, reps in ((8192, "allreduce_us_8192", 500), (512 * 8192, "allreduce_us_512x8192", 20)):
@@ -135,6 +144,7 @@ def main():
     del comm
 
     # ---- 2. sharded model vs unsharded
+    log("loading the sharded model")
     cfg = get_preset(args.model)
     path = os.path.join("/tmp", f"tp_check_{args.model}_{args.recipe}.gguf")
     if rank == 0 and not os.path.exists(path):
