@@ -477,7 +477,7 @@ PYBIND11_MODULE(_engine, m) {
   m.def(
       "gemm_q",
       [](uintptr_t A, int lda, std::vector<PyQMatrix*> segs, int M, uintptr_t C, uintptr_t C16, int ldc, int epi,
-         uintptr_t st, int ksplit) {
+         uintptr_t st, int ksplit, uintptr_t dbg_ts) {
         GemmQArgs a;
         std::memset(&a, 0, sizeof(a));
         if (segs.empty() || segs.size() > 3) throw std::runtime_error("gemm_q: 1..3 segments");
@@ -486,12 +486,13 @@ PYBIND11_MODULE(_engine, m) {
         for (int s = 0; s < a.nseg; ++s) { a.seg[s] = segs[s]->w; a.seg_n0[s] = n0; n0 += segs[s]->w.rows; }
         a.M = M; a.N = n0; a.K = segs[0]->w.cols;
         a.C = (float*)C; a.C16 = (bf16_t*)C16; a.ldc = ldc; a.epi = epi; a.ksplit = ksplit;
+        a.dbg_ts = (unsigned long long*)dbg_ts;
         GemmWs& g = gemm_ws(M, a.N);
         a.ws = g.ws; a.ws_bytes = g.bytes; a.cnt = g.cnt; a.cnt_len = g.cnt_len;
         launch_gemm_q(a, S(st));
       },
       py::arg("A"), py::arg("lda"), py::arg("segs"), py::arg("M"), py::arg("C"), py::arg("C16"), py::arg("ldc"),
-      py::arg("epi"), py::arg("stream"), py::arg("ksplit") = 0);
+      py::arg("epi"), py::arg("stream"), py::arg("ksplit") = 0, py::arg("dbg_ts") = 0);
   m.attr("GEPI_STORE") = (int)GEPI_STORE;
   m.attr("GEPI_ACCUM") = (int)GEPI_ACCUM;
   m.attr("GEPI_SWIGLU_BF16") = (int)GEPI_SWIGLU_BF16;

@@ -422,6 +422,8 @@ std::string Engine::weight_type_summary() const {
   return os.str();
 }
 
+static std::vector<std::vector<const QMat*>> qkv_groups(const LayerW& L);
+
 void Engine::finalize() {
   TraceRange tr("aios.finalize");
   HIP_CHECK(hipSetDevice(cfg_.device));
@@ -572,7 +574,33 @@ void Engine::finalize() {
       gm_tokens_ = ibuf(G);
       gm_pos_ = ibuf(G);
       gm_slot_ = ibuf(G);
-      if (const char* e = std::getenv("AIOS_DECODE_GEMM_MIN_B")) dec_gemm_min_b_ = std::atoi(e);
+      if (const char* e = std::getenv("AIOS_DECODE_GEMM_MIN_B")) {
+        dec_gemm_min_b_ = std::atoi(e);
+      } else {
+        // B rows go through the B-row LDS-DMA engine only if EVERY projection's LDS plan fits at that
+        // B; where one does not (e.g. a 28672-wide down projection at B = 4: 115 KB of staged x), the
+        // row-pair fallback is 2-3x slower than the skinny GEMM, so that B takes the GEMM path
+        // (ADVICE r3).  Also bounds the short-prompt prefill rows that use the GEMV path.
+        for (int b = 2; b < dec_gemm_min_b_ && b <= Bm; ++b) {
+          bool ok = true;
+          for (int l = 0; l < cfg_.n_layers && ok; ++l) {
+            const LayerW& L = layers_[l];
+            for (auto& grp : qkv_groups(L)) {
+              int n = 0;
+              for (auto* m : grp) n += m->w.rows;
+              ok = ok && gemv_engine_fits(gemv_args(grp, n, d, b, x_, d, L.attn_norm, q_, n, EPI_STORE, l));
+            }
+            ok = ok && gemv_engine_fits(gemv_args({&L.wo}, d, qd, b, attn_, qd, nullptr, x_, d, EPI_RESID, l)) &&
+                 gemv_engine_fits(gemv_args({&L.wgu}, 2 * cfg_.d_ff, d, b, x_, d, L.ffn_norm, ff_, cfg_.d_ff,
+                                            EPI_SWIGLU, l)) &&
+                 gemv_engine_fits(gemv_args({&L.wdown}, d, cfg_.d_ff, b, ff_, cfg_.d_ff, nullptr, x_, d, EPI_RESID, l));
+          }
+          if (!ok) {
+            dec_gemm_min_b_ = b;
+            gm_min_rows_ = std::min(gm_min_rows_, b);
+          }
+        }
+      }
       // split-K slabs + tickets for every skinny-GEMM call: batched decode (M <= max_batch, the
       // lm_head included) AND prefill chunks of 16-64 tokens (no lm_head) -- sized for the batch
       // only, a 32-token prompt ran its projections unsplit (32 workgroups for N = d_model)
@@ -956,7 +984,8 @@ void Engine::enqueue_decode_step(int B) {
     StepPrep sp{d_pos_, d_slot_, d_bt_, kv_maxb_, rope_cs_, cfg_.head_dim / 2, d_step_kv_, d_step_rope_};
     launch_get_rows_step(tok_embd_.w, d_tokens_, B, x_, d, 1.f, sp, stream_);
   }
-  step_prep_on_ = rope_cs_ != nullptr;
+  static const bool step_prep = !(std::getenv("AIOS_STEP_PREP") && std::atoi(std::getenv("AIOS_STEP_PREP")) == 0);
+  step_prep_on_ = step_prep && rope_cs_ != nullptr;
   nrm_lm_ = false;
   for (int l = 0; l < cfg_.n_layers; ++l) layer_decode(l, B);
   step_prep_on_ = false;

@@ -59,5 +59,6 @@ struct GemvArgs {
 };
 
 void launch_gemv(const GemvArgs& a, hipStream_t st);
+bool gemv_engine_fits(const GemvArgs& a);  // the B-row LDS-DMA engine serves a (gemv_dispatch.hip)
 
 }  // namespace aios

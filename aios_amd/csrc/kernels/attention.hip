@@ -31,7 +31,20 @@ __global__ void __launch_bounds__(512) attn_decode_kernel(AttnDecodeArgs a, Attn
   const int wg = blockIdx.x;
   const int len = a.seq_len[blockIdx.z];
   if (G > 1 && len <= a.short_len) {
-    const int h = wg / sp_.p_short, sp = wg % sp_.p_short;
+    // XCD-aware roles: workgroups are dealt round-robin over the 8 XCDs (blockIdx % 8), so
+    // workgroup wg takes query head (wg % 8) * (H / 8) + (wg / 8) / P -- the G query heads of a KV
+    // head then run on one XCD and read its K/V from that XCD's L2 after the first miss (the plain
+    // mapping put them on G different XCDs: G MALL/HBM reads of every K/V line)
+    int h, sp;
+    if ((a.n_heads & 7) == 0 && sp_.xcd) {
+      if (wg >= a.n_heads * sp_.p_short) return;
+      const int j = wg >> 3;
+      h = (wg & 7) * (a.n_heads >> 3) + j / sp_.p_short;
+      sp = j % sp_.p_short;
+    } else {
+      h = wg / sp_.p_short;
+      sp = wg % sp_.p_short;
+    }
     if (h >= a.n_heads) return;
     attn_core<HD, 1>(a, sp, h / G, h, h, sp_.p_short, sp_.ppw);
   } else {
@@ -47,6 +60,7 @@ template <int HD>
 static void launch_hd(const AttnDecodeArgs& a, int G, hipStream_t st) {
   AttnSplit sp;
   const int nwg = attn_plan(a, G, sp);
+  sp.xcd = attn_env_int("AIOS_ATTN_XCD", 1);  // XCD-aware short-mode roles (0: the plain mapping)
   sp.n_attn = nwg;
   dim3 grid(nwg, 1, a.B);
   switch (G) {

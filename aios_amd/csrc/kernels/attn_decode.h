@@ -354,7 +354,8 @@ struct AttnSplit {
   int p_long;   // workgroups per (row, head set) in the long mode
   int p_short;  // workgroups per (row, head) in the short mode
   int ppw;      // passes per workgroup the split aims for
-  int n_attn;   // attention workgroups of the flat grid (prefetch workgroups follow them)
+  int n_attn;   // attention workgroups of the flat grid
+  int xcd;      // short mode: the G query heads of a KV head on one XCD (attention.hip)
 };
 
 

@@ -65,6 +65,15 @@ __device__ __forceinline__ void sk_body(const GemmQArgs& a, int S) {
   constexpr int XPT = (XU + NT - 1) / NT;   // per thread
   extern __shared__ __attribute__((aligned(16))) bf16_t sk_xs[];
   __shared__ int last_flag;
+  // probes (tools/skinny_probe.py): 0 start, 1 prologue loads issued, 2 first X chunk staged,
+  // 3 main loop done, 4 slab published + ticket, 5 last arriver done
+  unsigned long long ts[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  auto stamp = [&](int i) __attribute__((always_inline)) { ts[i] = __builtin_amdgcn_s_memrealtime(); };
+  auto flush = [&]() __attribute__((always_inline)) {
+    if (a.dbg_ts && threadIdx.x == 0)
+      for (int i = 0; i < 8; ++i) a.dbg_ts[(size_t)blockIdx.x * 8 + i] = ts[i];
+  };
+  stamp(0);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int rr = lane & 15, q = lane >> 4;
   const int ntile = a.N / ROWS, total = ntile * S;
@@ -208,6 +217,7 @@ __device__ __forceinline__ void sk_body(const GemmQArgs& a, int S) {
   x_load(c0);
 #pragma unroll
   for (int u = 0; u < SK_NL; ++u) w_load(tb + u, ring[u], !MB || (u & 1) == 0);
+  stamp(1);
   x_store(0, c0);
   if (nrm) {
 #pragma unroll
@@ -220,6 +230,7 @@ __device__ __forceinline__ void sk_body(const GemmQArgs& a, int S) {
   }
   x_load(min(c0 + 1, c1 - 1));
   __syncthreads();
+  stamp(2);
   for (int c = c0; c < c1; ++c) {
     const int buf = (c - c0) & 1, kc0 = c * KC;
 #pragma unroll
@@ -234,6 +245,7 @@ __device__ __forceinline__ void sk_body(const GemmQArgs& a, int S) {
     __syncthreads();
   }
 
+  stamp(3);
   // ---- epilogue.  lane holds D[n = 4q + j][m = 16 mt + rr], j = 0..3
   const int nl = 16 * wave + 4 * q;  // tile-local first row of this lane's 4 outputs
   // returns the sum of squares of the new residual row slice (GEPI_ACCUM_NORM), else 0
@@ -308,6 +320,8 @@ __device__ __forceinline__ void sk_body(const GemmQArgs& a, int S) {
         a.nrm_part[(size_t)tid * a.nrm_parts + rg] = s;
       }
     }
+    stamp(5);
+    flush();
     return;
   }
   // split-K: slab [sp][rg][MP][ROWS] written through (sc1: no release fence needed), then the
@@ -331,7 +345,11 @@ __device__ __forceinline__ void sk_body(const GemmQArgs& a, int S) {
     last_flag = last;
   }
   __syncthreads();
-  if (!last_flag) return;
+  stamp(4);
+  if (!last_flag) {
+    flush();
+    return;
+  }
   const size_t sstride = (size_t)ntile * MP * ROWS;
   const float* base = a.ws + (size_t)rg * MP * ROWS;
   for (int u = tid; u < MP * ROWS / 4; u += NT) {
@@ -355,6 +373,8 @@ __device__ __forceinline__ void sk_body(const GemmQArgs& a, int S) {
       if (n4 == 0 && m < a.M) a.nrm_part[(size_t)m * a.nrm_parts + rg] = s;
     }
   }
+  stamp(5);
+  flush();
 }
 
 // One launch for every tile: with mixed formats (Q4_K_M: Q|K Q4_K, V Q6_K) the tiles of the last

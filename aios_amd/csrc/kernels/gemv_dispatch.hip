@@ -15,6 +15,35 @@ void gemv_q8_0(const GemvArgs&, hipStream_t);
 void gemv_f16(const GemvArgs&, hipStream_t);
 void gemv_bf16(const GemvArgs&, hipStream_t);
 
+bool gemv_q4k_q4k_engine_fits(const GemvArgs&);
+bool gemv_q4k_q6k_engine_fits(const GemvArgs&);
+bool gemv_q6k_q6k_engine_fits(const GemvArgs&);
+bool gemv_q5k_q5k_engine_fits(const GemvArgs&);
+bool gemv_q5k_q6k_engine_fits(const GemvArgs&);
+bool gemv_q4_0_engine_fits(const GemvArgs&);
+bool gemv_q8_0_engine_fits(const GemvArgs&);
+
+// Whether the B-row LDS-DMA engine serves these args (B = 1..4, int8 activations, the shape's LDS
+// plan fits 160 KB).  16-bit weights never take the engine and report true (their B-row kernels are
+// the only GEMV path).  The engine's batched-decode path choice asks this per projection.
+bool gemv_engine_fits(const GemvArgs& a) {
+  const int qt0 = a.seg[0].qtype, qt1 = a.seg[a.nseg - 1].qtype;
+  if (qt0 == QT_F16 || qt0 == QT_BF16) return true;
+  if (qt0 == qt1) {
+    switch (qt0) {
+      case QT_Q4_K: return gemv_q4k_q4k_engine_fits(a);
+      case QT_Q6_K: return gemv_q6k_q6k_engine_fits(a);
+      case QT_Q5_K: return gemv_q5k_q5k_engine_fits(a);
+      case QT_Q4_0: return gemv_q4_0_engine_fits(a);
+      case QT_Q8_0: return gemv_q8_0_engine_fits(a);
+    }
+  } else if (qt1 == QT_Q6_K) {
+    if (qt0 == QT_Q4_K) return gemv_q4k_q6k_engine_fits(a);
+    if (qt0 == QT_Q5_K) return gemv_q5k_q6k_engine_fits(a);
+  }
+  return false;
+}
+
 bool gemv_supports(int qt0, int qt1) {
   if (qt0 == qt1)
     return qt0 == QT_Q4_K || qt0 == QT_Q6_K || qt0 == QT_Q5_K || qt0 == QT_Q4_0 || qt0 == QT_Q8_0 ||

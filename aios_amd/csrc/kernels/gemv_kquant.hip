@@ -3,4 +3,6 @@
 namespace aios {
 void gemv_q4k_q4k(const GemvArgs& a, hipStream_t st) { launch_gemv_pair<QT_Q4_K, QT_Q4_K>(a, st); }
 void gemv_q4k_q6k(const GemvArgs& a, hipStream_t st) { launch_gemv_pair<QT_Q4_K, QT_Q6_K>(a, st); }
+bool gemv_q4k_q4k_engine_fits(const GemvArgs& a) { return launch_gemv_lds<QT_Q4_K, QT_Q4_K>(a, nullptr, true); }
+bool gemv_q4k_q6k_engine_fits(const GemvArgs& a) { return launch_gemv_lds<QT_Q4_K, QT_Q6_K>(a, nullptr, true); }
 }  // namespace aios

@@ -759,8 +759,9 @@ size_t lg_lds_bytes(const GemvArgs& a, const CuPlan& pl) {
   return (head + 255) / 256 * 256 + ringb;
 }
 
+// dry = true: only whether the engine WOULD serve these args (the engine's per-B path choice)
 template <int QT0, int QT1>
-bool launch_gemv_lds(const GemvArgs& a, hipStream_t st) {
+bool launch_gemv_lds(const GemvArgs& a, hipStream_t st, bool dry = false) {
   if constexpr (!same_xlayout<QT0, QT1> || !lg_supported<QT0>() || !lg_supported<QT1>()) {
     return false;
   } else {
@@ -818,25 +819,31 @@ bool launch_gemv_lds(const GemvArgs& a, hipStream_t st) {
     if (a.B == 1) {
       lds = lg_lds_bytes<QT0, QT1, 1, 0>(a, pl);
       if (lds > LDS_MAX) return false;
+      if (dry) return true;
       hipLaunchKernelGGL((gemv_lds_b1<QT0, QT1, 1, 0>), dim3(G), dim3(LG_THREADS), lds, st, a, pl);
     } else if (a.B == 2) {
       lds = lg_lds_bytes<QT0, QT1, 2, 1>(a, pl);
       if (lds > LDS_MAX) return false;
+      if (dry) return true;
       hipLaunchKernelGGL((gemv_lds_b1<QT0, QT1, 2, 1>), dim3(G), dim3(LG_THREADS), lds, st, a, pl);
     } else if (a.B == 3) {  // its own instantiation: no idle fourth row in the dot work / staging
       if ((lds = lg_lds_bytes<QT0, QT1, 3, 1>(a, pl)) <= LDS_MAX) {
+        if (dry) return true;
         hipLaunchKernelGGL((gemv_lds_b1<QT0, QT1, 3, 1>), dim3(G), dim3(LG_THREADS), lds, st, a, pl);
       } else {
         lds = lg_lds_bytes<QT0, QT1, 3, 2>(a, pl);
         if (lds > LDS_MAX) return false;
+        if (dry) return true;
         hipLaunchKernelGGL((gemv_lds_b1<QT0, QT1, 3, 2>), dim3(G), dim3(LG_THREADS), lds, st, a, pl);
       }
     } else if ((lds = lg_lds_bytes<QT0, QT1, 4, 1>(a, pl)) <= LDS_MAX) {
+      if (dry) return true;
       hipLaunchKernelGGL((gemv_lds_b1<QT0, QT1, 4, 1>), dim3(G), dim3(LG_THREADS), lds, st, a, pl);
     } else {
       // long K (the d_ff-wide down projection): four staged x rows leave room for a shallower ring
       lds = lg_lds_bytes<QT0, QT1, 4, 2>(a, pl);
       if (lds > LDS_MAX) return false;
+      if (dry) return true;
       hipLaunchKernelGGL((gemv_lds_b1<QT0, QT1, 4, 2>), dim3(G), dim3(LG_THREADS), lds, st, a, pl);
     }
     return true;

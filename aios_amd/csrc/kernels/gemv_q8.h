@@ -839,12 +839,27 @@ void launch_q8_rows(const GemvArgs& a, size_t lds, hipStream_t st) {
     return e ? std::atoi(e) : 1;
   }();
   int nw = Q8_WAVES;
-  if (B == 1 && balance && a.tune_grid <= 0 && q8_max_threads<U>() >= 1024) {
-    const int want = (npairs + cus - 1) / cus;
-    if (want >= 2 && want <= 16) nw = want;
+  int blocks = 0;
+  if (B == 1 && balance && a.tune_grid <= 0 && npairs >= 2 * cus) {
+    // round 4: also for the register-heavy U >= 3 variants (<= 8 waves) and for shapes with more
+    // pairs than waves (ppw pairs per wave, one workgroup per CU): TinyLlama's down (1024 pairs,
+    // U = 3) ran 128 8-wave workgroups on half the chip, its gate/up (5632 pairs) 512 workgroups with
+    // 1 or 2 pairs per wave
+    const int maxw = q8_max_threads<U>() / 64;
+    const int ppw = (npairs + cus * maxw - 1) / (cus * maxw);
+    int want = (npairs + cus * ppw - 1) / (cus * ppw);
+    if (QT0 != QT1 && a.nseg > 1 && ppw == 1) {
+      // mixed formats: whole waves per format in every workgroup (the kernel splits nw by pair
+      // counts), e.g. TinyLlama's QKV 1152 Q4_K + 128 Q6_K pairs -> 5 + 1 waves, not 4 + 1
+      const int np0 = a.seg_row0[a.nseg - 1] / 2;
+      want = (np0 + cus - 1) / cus + (npairs - np0 + cus - 1) / cus;
+    }
+    if (want >= 2 && want <= maxw) {
+      nw = want;
+      blocks = std::min(cus, (npairs + nw - 1) / nw);
+    }
   }
-  const int groups = (npairs + nw - 1) / nw;
-  const int blocks = std::min(groups, cus * per_cu);
+  if (!blocks) blocks = std::min((npairs + nw - 1) / nw, cus * per_cu);
   hipLaunchKernelGGL((gemv_q8_rows<QT0, QT1, B, U, PIPE>), dim3(blocks), dim3(nw * 64), lds, st, a);
 }
 

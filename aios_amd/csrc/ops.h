@@ -220,6 +220,7 @@ struct GemmQArgs {
   const float* nrm_in;
   int nrm_parts;
   float nrm_eps;
+  unsigned long long* dbg_ts;  // probes (skinny kernel): [grid][8] s_memrealtime phase stamps or null
 };
 // bytes of split-K workspace / ticket count the skinny GEMM may use for an M x N output
 size_t gemm_skinny_ws_bytes(int M, int N);
