@@ -132,6 +132,16 @@ __device__ __forceinline__ void kernarg_warm() {
   asm volatile("" ::"s"(acc));
 }
 
+// per-lane choice between two kernel-argument pointers (K vs V cache of a QKV epilogue).  A plain
+// `c ? a.p : a.q` lets LLVM turn it into a load through a selected address, i.e. an alloca copy of
+// the two fields indexed per lane -- scratch in every kernel using it (round 4: 24 B in each
+// batched LDS GEMV).  Pinning both values in SGPRs first keeps it a register select.
+template <typename T>
+__device__ __forceinline__ T* pick_ptr(bool first, T* p, T* q) {
+  asm("" : "+s"(p), "+s"(q));
+  return first ? p : q;
+}
+
 // roctx ranges around the engine's host-side phases (load, prefill chunk, decode step / graph
 // replay, sampling): visible with `rocprofv3 --marker-trace` next to the kernel trace; ~free
 // when no profiler is attached.  AIOS_TRACE=0 turns them off.

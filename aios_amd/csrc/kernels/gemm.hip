@@ -232,9 +232,12 @@ static void launch_big(const GemmQArgs& a, hipStream_t st) {
 // operand registers; returns false when the shape / workspace does not fit it
 bool launch_gemm_skinny(const GemmQArgs& a, hipStream_t st);
 bool gemm_skinny_mixed_ok(const GemmQArgs& a);
+// M <= 32, Q4_K / Q6_K: the LDS-DMA ring GEMM (gemm_ring.hip); false when it does not serve the shape
+bool launch_gemm_ring(const GemmQArgs& a, hipStream_t st);
 
 static void launch_one(const GemmQArgs& a, hipStream_t st) {
   static const int skinny_max = env_int("AIOS_GEMM_SKINNY_MAX_M", 64);
+  if (launch_gemm_ring(a, st)) return;
   if (a.M <= skinny_max && launch_gemm_skinny(a, st)) return;
   if (a.epi == GEPI_QKV || a.epi == GEPI_ACCUM_NORM || a.nrm_in)
     throw std::runtime_error("gemm: the QKV / fused-RMSNorm epilogues need the skinny (M <= 64) kernel");
@@ -264,6 +267,7 @@ void launch_gemm_q(const GemmQArgs& a, hipStream_t st) {
   if (a.N % 64) throw std::runtime_error("gemm: N must be a multiple of 64");
   // mixed formats in ONE skinny launch where supported (the Q4_K_M QKV stack)
   static const int skinny_max = env_int("AIOS_GEMM_SKINNY_MAX_M", 64);
+  if (launch_gemm_ring(a, st)) return;  // the mixed Q4_K_M QKV stack in one ring launch
   if (a.M <= skinny_max && gemm_skinny_mixed_ok(a) && launch_gemm_skinny(a, st)) return;
   int s0 = 0;
   while (s0 < a.nseg) {

@@ -22,13 +22,12 @@
 //     them and runs the epilogue -- no float atomics, deterministic result, one launch.
 // The B = 1 step keeps the int8-activation GEMV (gemv_q8.h, 4 MACs per VALU op); from B = 2 the
 // dequant-once MFMA form is cheaper than B passes of v_dot4.
-#include "gemm_common.h"
+#include "skinny_epi.h"
 
 namespace aios {
 
 constexpr int SK_NL = 4;    // weight ring depth = steps per X chunk
 constexpr int SK_SMAX = 16;  // K splits at most (slab workspace: gemm_skinny_ws_bytes)
-constexpr int SK_SB = 8;     // slices summed per batch of loads in the last arriver
 
 template <int QT>
 struct SkFmt {
@@ -66,7 +65,8 @@ __device__ __forceinline__ void sk_body(const GemmQArgs& a, int S) {
   extern __shared__ __attribute__((aligned(16))) bf16_t sk_xs[];
   __shared__ int last_flag;
   // probes (tools/skinny_probe.py): 0 start, 1 prologue loads issued, 2 first X chunk staged,
-  // 3 main loop done, 4 slab published + ticket, 5 last arriver done
+  // 3 main loop done, 4 done (a slice that handed its slab to the tile's last arriver), 5 done
+  // (the epilogue written)
   unsigned long long ts[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   auto stamp = [&](int i) __attribute__((always_inline)) { ts[i] = __builtin_amdgcn_s_memrealtime(); };
   auto flush = [&]() __attribute__((always_inline)) {
@@ -246,134 +246,8 @@ __device__ __forceinline__ void sk_body(const GemmQArgs& a, int S) {
   }
 
   stamp(3);
-  // ---- epilogue.  lane holds D[n = 4q + j][m = 16 mt + rr], j = 0..3
-  const int nl = 16 * wave + 4 * q;  // tile-local first row of this lane's 4 outputs
-  // returns the sum of squares of the new residual row slice (GEPI_ACCUM_NORM), else 0
-  auto finish = [&](int m, int n, gf32x4 v) __attribute__((always_inline)) -> float {
-    if (m >= a.M) return 0.f;
-    if (nrm) v *= inv_s[m];
-    if constexpr (EPI == GEPI_SWIGLU_BF16) {
-      const uint32_t pk = pk_bf16(v[0] / (1.f + __expf(-v[0])) * v[1], v[2] / (1.f + __expf(-v[2])) * v[3]);
-      *(uint32_t*)(a.C16 + (size_t)m * a.ldc + (n >> 1)) = pk;
-    } else if constexpr (EPI == GEPI_QKV) {
-      // the lane's 4 consecutive columns are two RoPE pairs (2i, 2i + 1)
-      const int hd = a.head_dim, pos = a.pos[m], slot = a.slot ? a.slot[m] : 0;
-#pragma unroll
-      for (int j = 0; j < 4; j += 2) {
-        const int c = a.col0 + n + j;
-        float v0 = v[j], v1 = v[j + 1];
-        const int part = c < a.q_dim ? 0 : (c < a.q_dim + a.kv_dim ? 1 : 2);
-        const int r = c - (part == 0 ? 0 : (part == 1 ? a.q_dim : a.q_dim + a.kv_dim));
-        const int head = r / hd, lr = r - head * hd;
-        if (part < 2) {
-          const float2 t = a.rope_cs[(size_t)pos * (hd >> 1) + (lr >> 1)];
-          const float o0 = v0 * t.x - v1 * t.y, o1 = v0 * t.y + v1 * t.x;
-          v0 = o0;
-          v1 = o1;
-        }
-        if (part == 0) {
-          *(float2*)(a.q_out + (size_t)m * a.q_dim + c) = make_float2(v0, v1);
-        } else {
-          bf16_t* cache = part == 1 ? a.k_cache : a.v_cache;
-          const size_t base = kv_offset(a.block_table, a.max_ctx / KV_BLOCK, slot, a.n_kv_heads, head, pos, hd);
-          *(uint32_t*)(cache + base + lr) = pk_bf16(v0, v1);
-        }
-      }
-    } else {
-      float4* c = (float4*)(a.C + (size_t)m * a.ldc + n);
-      if constexpr (EPI == GEPI_ACCUM_NORM) {
-        const float4 o = *c;
-        const float4 x = make_float4(o.x + v[0], o.y + v[1], o.z + v[2], o.w + v[3]);
-        *c = x;
-        const float4 g = *(const float4*)(a.nrm_g + n);
-        *(uint2*)(a.nrm_out16 + (size_t)m * a.ldc + n) = make_uint2(pk_bf16(x.x * g.x, x.y * g.y),
-                                                                      pk_bf16(x.z * g.z, x.w * g.w));
-        return (x.x * x.x + x.y * x.y) + (x.z * x.z + x.w * x.w);
-      } else if constexpr (EPI == GEPI_ACCUM) {
-        const float4 o = *c;
-        *c = make_float4(o.x + v[0], o.y + v[1], o.z + v[2], o.w + v[3]);
-      } else {
-        *c = make_float4(v[0], v[1], v[2], v[3]);
-      }
-    }
-    return 0.f;
-  };
-  if (S == 1) {
-    float ss[MT];
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt) ss[mt] = finish(16 * mt + rr, n0 + nl, acc[mt]);
-    if constexpr (EPI == GEPI_ACCUM_NORM) {
-      // tile partial per row: the 4 q lanes of a wave (shuffles), then the RB waves (LDS, in
-      // wave order); Xs is free after the main loop's last barrier
-      float* red = (float*)&sk_xs[0];
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) {
-        float s = ss[mt];
-        s += __shfl_xor(s, 16, 64);
-        s += __shfl_xor(s, 32, 64);
-        if (q == 0) red[wave * MP + 16 * mt + rr] = s;
-      }
-      __syncthreads();
-      if (tid < a.M) {
-        float s = red[tid];
-        for (int w = 1; w < RB; ++w) s += red[w * MP + tid];
-        a.nrm_part[(size_t)tid * a.nrm_parts + rg] = s;
-      }
-    }
-    stamp(5);
-    flush();
-    return;
-  }
-  // split-K: slab [sp][rg][MP][ROWS] written through (sc1: no release fence needed), then the
-  // last arriver of the tile (relaxed agent ticket) acquires and reduces (CDNA guide §5 item 2)
-  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)a.ws, (short)0, 0x7fffffff, 0x00020000);
-  const int sbase = (int)(((size_t)sp * ntile + rg) * MP * ROWS * 4);
-#pragma unroll
-  for (int mt = 0; mt < MT; ++mt)
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(gu32x4, acc[mt]), rs,
-                                           sbase + ((16 * mt + rr) * ROWS + nl) * 4, 0, 16 /* sc1 */);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its slab stores
-  __syncthreads();
-  if (tid == 0) {
-    const int t = __hip_atomic_fetch_add(a.cnt + rg, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int last = t == S - 1;
-    if (last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_store(a.cnt + rg, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
-    }
-    last_flag = last;
-  }
-  __syncthreads();
-  stamp(4);
-  if (!last_flag) {
-    flush();
-    return;
-  }
-  const size_t sstride = (size_t)ntile * MP * ROWS;
-  const float* base = a.ws + (size_t)rg * MP * ROWS;
-  for (int u = tid; u < MP * ROWS / 4; u += NT) {
-    const int m = u / (ROWS / 4), n4 = 4 * (u % (ROWS / 4));
-    // SK_SB slices' loads in flight at once (clamped re-reads weighted by zero), in fixed order
-    gf32x4 v = gf32x4{0.f, 0.f, 0.f, 0.f};
-    for (int k0 = 0; k0 < S; k0 += SK_SB) {
-      gf32x4 part[SK_SB];
-#pragma unroll
-      for (int k = 0; k < SK_SB; ++k)
-        part[k] = *(const gf32x4*)(base + min(k0 + k, S - 1) * sstride + (size_t)m * ROWS + n4);
-#pragma unroll
-      for (int k = 0; k < SK_SB; ++k)
-        if (k0 + k < S) v += part[k];
-    }
-    float s = finish(m, n0 + n4, v);
-    if constexpr (EPI == GEPI_ACCUM_NORM) {
-      // a row's ROWS / 4 units sit on consecutive lanes of one wave
-#pragma unroll
-      for (int o = 1; o < ROWS / 4; o <<= 1) s += __shfl_xor(s, o, 64);
-      if (n4 == 0 && m < a.M) a.nrm_part[(size_t)m * a.nrm_parts + rg] = s;
-    }
-  }
-  stamp(5);
+  const bool wrote = sk_epilogue<RB, MT, EPI>(a, acc, n0, rg, sp, S, ntile, inv_s, nrm, (float*)&sk_xs[0], last_flag);
+  if (wrote) stamp(5); else stamp(4);  // 4: a split-K slice that was not its tile's last arriver
   flush();
 }
 
@@ -471,7 +345,7 @@ static bool sk_qt(const GemmQArgs& a, hipStream_t st) {
   int S = a.ksplit > 0 ? a.ksplit : sk_env("AIOS_SKINNY_S", 0);
   if (S <= 0) {
     // resident workgroups: LDS / threads allow per_cu, the ~100-VGPR bodies 2 of 8 waves
-    const int cap = device_cu_count() * std::min(per_cu, 2);
+    const int cap = device_cu_count() * std::min(per_cu, sk_env("AIOS_SKINNY_WGCU", 2));
     if (sk_env("AIOS_SKINNY_SPLIT_MODE", 1) == 0) {
       S = ntile >= cap ? 1 : (cap + ntile - 1) / ntile;
     } else {

@@ -181,7 +181,7 @@ __device__ __forceinline__ void cu_qkv_epilogue(const GemvArgs& a, int grow, flo
     q[da] = v0;
     q[db] = v1;
   } else {
-    bf16_t* cache = (part == 1 ? a.k_cache : a.v_cache);
+    bf16_t* cache = pick_ptr(part == 1, a.k_cache, a.v_cache);
     const size_t base = (((size_t)kv_blk0 * a.n_kv_heads + head) * KV_BLOCK + (pos0 % KV_BLOCK)) * hd;
     cache[base + da] = f32_to_bf16(v0);
     cache[base + db] = f32_to_bf16(v1);

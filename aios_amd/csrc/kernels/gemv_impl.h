@@ -231,7 +231,7 @@ __device__ __forceinline__ void gemv_epilogue(const GemvArgs& a, int grow, int b
         float* q = a.y + (size_t)b * a.ldy + head * hd;
         q[da] = v0; q[db] = v1;
       } else {
-        bf16_t* cache = (part == 1 ? a.k_cache : a.v_cache);
+        bf16_t* cache = pick_ptr(part == 1, a.k_cache, a.v_cache);
         const size_t base = kv_offset(a.block_table, a.max_ctx / KV_BLOCK, slot, a.n_kv_heads, head, pos, hd);
         cache[base + da] = f32_to_bf16(v0);
         cache[base + db] = f32_to_bf16(v1);

@@ -229,13 +229,19 @@ __device__ __forceinline__ void q8_stage_prefetch(const GemvArgs& a, StagePre<NP
     const int tt = t < total ? t : 0;
     const int b = tt / noct, o = tt - b * noct;
     const float* src = a.x + (size_t)b * a.ldx + 8 * o;
+    // both registers are written on both paths: a member left unwritten on one side of the branch
+    // sends the whole StagePre to scratch (measured: 80 B/lane in the B=1 engine, -15 % decode)
+    float4 r0, r1;
     if (a.x16) {  // 8 bf16 in one 16-B load, widened in q8_stage (no wait here)
       const uint4 u = *(const uint4*)(a.x16 + (size_t)b * a.ldx + 8 * o);
-      pf.x0[i] = make_float4(__uint_as_float(u.x), __uint_as_float(u.y), __uint_as_float(u.z), __uint_as_float(u.w));
+      r0 = make_float4(__uint_as_float(u.x), __uint_as_float(u.y), __uint_as_float(u.z), __uint_as_float(u.w));
+      r1 = r0;
     } else {
-      pf.x0[i] = ldx4(src);
-      pf.x1[i] = ldx4(src + 4);
+      r0 = ldx4(src);
+      r1 = ldx4(src + 4);
     }
+    pf.x0[i] = r0;
+    pf.x1[i] = r1;
     // the norm weights of every prefetched pass too: a load issued after the weight stream would
     // make its wait cover every weight load in flight
     const float* g = a.norm_w ? a.norm_w + 8 * o : src;
@@ -491,7 +497,7 @@ __device__ __forceinline__ void gemv_epilogue1(const GemvArgs& a, int grow, floa
         q[da] = v0;
         q[db] = v1;
       } else {
-        bf16_t* cache = (part == 1 ? a.k_cache : a.v_cache);
+        bf16_t* cache = pick_ptr(part == 1, a.k_cache, a.v_cache);
         // kv_blk0: the physical block of (slot, pos), looked up once behind the first weight loads
         const size_t base = (((size_t)kv_blk0 * a.n_kv_heads + head) * KV_BLOCK + (pos0 % KV_BLOCK)) * hd;
         if (db == da + 1) {  // adjacent pair (V rows, non-NeoX RoPE): one 4-byte store
@@ -526,9 +532,11 @@ __device__ __forceinline__ float2 wave_sum_pair(float a0, float a1) {
 // PIPE = 2 double-buffers across items/pairs (short K), 1 = single buffer (large U).
 // ---------------------------------------------------------------------------------------------
 constexpr int Q8_WAVES = 8;
-// up to 16 waves per workgroup for the register-light variants (U <= 2: the batch-1 QKV / O shapes)
-template <int U>
-constexpr int q8_max_threads() { return U <= 2 ? 1024 : Q8_WAVES * 64; }
+// up to 16 waves per workgroup for the register-light variants (U <= 2 single-buffered: the batch-1
+// QKV / O shapes).  The double-buffered ones keep 8: at 16 waves (128 VGPRs) they spilled 12-230 B
+// per lane to scratch (tools/kernel_resources.py)
+template <int U, int PIPE>
+constexpr int q8_max_threads() { return U <= 2 && PIPE == 1 ? 1024 : Q8_WAVES * 64; }
 
 template <int QT>
 struct FmtTag {
@@ -536,7 +544,7 @@ struct FmtTag {
 };
 
 template <int QT0, int QT1, int B, int U, int PIPE>
-__global__ void __launch_bounds__(q8_max_threads<U>()) gemv_q8_rows(GemvArgs a) {
+__global__ void __launch_bounds__((q8_max_threads<U, PIPE>())) gemv_q8_rows(GemvArgs a) {
   static_assert(same_xlayout<QT0, QT1>, "mixed segments must share the activation layout");
   kernarg_warm<sizeof(GemvArgs)>();
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -845,7 +853,7 @@ void launch_q8_rows(const GemvArgs& a, size_t lds, hipStream_t st) {
     // pairs than waves (ppw pairs per wave, one workgroup per CU): TinyLlama's down (1024 pairs,
     // U = 3) ran 128 8-wave workgroups on half the chip, its gate/up (5632 pairs) 512 workgroups with
     // 1 or 2 pairs per wave
-    const int maxw = q8_max_threads<U>() / 64;
+    const int maxw = q8_max_threads<U, PIPE>() / 64;
     const int ppw = (npairs + cus * maxw - 1) / (cus * maxw);
     int want = (npairs + cus * ppw - 1) / (cus * ppw);
     if (QT0 != QT1 && a.nseg > 1 && ppw == 1) {

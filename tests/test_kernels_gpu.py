@@ -711,6 +711,46 @@ def test_gemm_error_vs_unquantized_product(E, t, M, ksplit):
     assert per_row < 1e-2, per_row
 
 
+# ---- the LDS-DMA ring GEMM (gemm_ring.hip): batched decode M = 5..32 on Q4_K / Q6_K / mixed stacks ----
+@pytest.mark.parametrize("M", [5, 8, 13, 16, 17, 24, 32])
+@pytest.mark.parametrize("segs,K", [([(GGMLType.Q4_K, 384)], 4096), ([(GGMLType.Q6_K, 256)], 14336),
+                                    ([(GGMLType.Q4_K, 256), (GGMLType.Q4_K, 128), (GGMLType.Q6_K, 128)], 4096),
+                                    ([(GGMLType.Q4_K, 128)], 1024)])
+@pytest.mark.parametrize("epi", ["store", "accum"])
+def test_gemm_ring_vs_unquantized(E, M, segs, K, epi):
+    """Against the UNQUANTIZED fp32 product (exact dequantised weights x the fp32 activations): ring
+    slots of one 256-k superblock, the automatic split-K (one dispatch round) reduced by the tile's
+    last arriver, padded activation rows (M not a multiple of 16), the mixed-format QKV launch"""
+    mats, refs = zip(*[qmat(E, t, n, K, seed=80 + i, std=0.02) for i, (t, n) in enumerate(segs)])
+    W = torch.cat(refs, 0)
+    N = W.shape[0]
+    x = torch.randn(M, K)
+    A = x.to(torch.bfloat16).cuda()
+    C = torch.full((M, N), 2.0, device="cuda")
+    for _ in range(2):  # the second launch re-uses the re-armed tickets
+        C.fill_(2.0)
+        E.gemm_q(A.data_ptr(), K, list(mats), M, C.data_ptr(), 0, N,
+                 E.GEPI_STORE if epi == "store" else E.GEPI_ACCUM, stream())
+    torch.cuda.synchronize()
+    ref = x.double() @ W.double().T + (0.0 if epi == "store" else 2.0)
+    got = C.cpu().double()
+    rel = float((got - ref).norm() / (ref - (0.0 if epi == "store" else 2.0)).norm())
+    assert rel < 6e-3, rel
+
+
+@pytest.mark.parametrize("M", [6, 16, 32])
+def test_gemm_ring_swiglu(E, M):
+    N, K = 512, 4096
+    m, W = qmat(E, GGMLType.Q4_K, N, K, seed=91, std=0.05)
+    A = torch.randn(M, K, device="cuda").to(torch.bfloat16)
+    out = torch.zeros(M, N // 2, dtype=torch.bfloat16, device="cuda")
+    E.gemm_q(A.data_ptr(), K, [m], M, 0, out.data_ptr(), N // 2, E.GEPI_SWIGLU_BF16, stream())
+    torch.cuda.synchronize()
+    y = A.float().cpu() @ W.to(torch.bfloat16).float().T
+    ref = torch.nn.functional.silu(y[:, 0::2]) * y[:, 1::2]
+    assert torch.allclose(out.float().cpu(), ref, atol=2e-2, rtol=2e-2), (out.float().cpu() - ref).abs().max()
+
+
 # ---- the LDS-DMA engine serving B = 2..4 rows from one weight stream (small-batch decode) --------
 @pytest.mark.parametrize("t", [GGMLType.Q4_K, GGMLType.Q6_K, GGMLType.Q5_K, GGMLType.Q8_0])
 @pytest.mark.parametrize("K", [4096, 14336])

@@ -86,7 +86,7 @@ def main():
         row["workgroups"] = int(len(t))
         t0 = t[:, 0].min()
         rel = (t - t0) / 100.0
-        names = ["start", "loads_issued", "x_staged", "loop_done", "published", "done"]
+        names = ["start", "loads_issued", "x_staged", "loop_done", "done_slice", "done_epilogue"]
         st = {}
         for i, nm in enumerate(names):
             v = rel[:, i][t[:, i] > 0]
