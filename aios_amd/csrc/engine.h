@@ -16,6 +16,7 @@
 
 #include "common.h"
 #include "ops.h"
+#include "blas.h"
 
 namespace aios {
 
@@ -137,6 +138,8 @@ class Engine {
   int kv_blocks_free() const { return (int)free_blocks_.size(); }
   int kv_blocks_total() const { return kv_nblocks_; }
   int norm_fused_parts() const { return nrm_parts_; }  // 0: batched-decode RMSNorm not split into the GEMMs
+  bool blas_prefill() const { return blas_ != nullptr; }  // long prefill chunks on hipBLASLt (blas.h)
+  int blas_prefill_min_rows() const { return blas_min_rows_; }
   std::vector<int> block_table(int slot) const;
 
   // raw device pointers for tests / custom kernels
@@ -231,6 +234,15 @@ class Engine {
   float *gm_x_ = nullptr, *gm_qkv_ = nullptr, *gm_q_ = nullptr, *gm_part_ = nullptr;
   bf16_t *gm_a16_ = nullptr, *gm_ff16_ = nullptr, *gm_attn16_ = nullptr;
   int *gm_tokens_ = nullptr, *gm_pos_ = nullptr, *gm_slot_ = nullptr;
+  // long prefill chunks (>= blas_min_rows_ tokens) through hipBLASLt against a resident bf16 copy of
+  // the projection weights (blas.h): per layer {QKV stacked [q+2kv][d], O [d][q], gate/up [2ff][d],
+  // down [d][ff]}; gate/up lands in fp32 (gm_gu32_) for the SwiGLU kernel
+  std::unique_ptr<BlasGemm> blas_;
+  std::vector<bf16_t*> w16_;  // 4 per layer
+  float* gm_gu32_ = nullptr;
+  int blas_min_rows_ = 256;
+  size_t w16_bytes_ = 0;
+  void setup_blas_prefill();
   // batched decode through the skinny MFMA GEMM (B >= dec_gemm_min_b_): bf16 activation buffers
   // (MI355X, Mistral-7B Q4_K_M, tools/gpu_batch_ab.sh: B=2 GEMV 2.41 ms vs GEMM 3.25 ms, B=4 3.31 vs 3.26,
   // B=8 5.80 vs 3.37 -- the skinny GEMM's per-step dequant floor lost below 4 rows; after the split

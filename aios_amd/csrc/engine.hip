@@ -635,9 +635,59 @@ void Engine::finalize() {
       }
     }
   }
+  setup_blas_prefill();
+  if (blas_) ws += w16_bytes_ + (size_t)gm_rows_ * 2 * cfg_.d_ff * 4;
   ws_bytes_ = ws;
   HIP_CHECK(hipDeviceSynchronize());
   finalized_ = true;
+}
+
+// Resident bf16 projection weights + hipBLASLt for prefill chunks of >= blas_min_rows_ tokens
+// (blas.h).  AIOS_PREFILL_BLAS=0 turns it off; the copy is made only when it fits comfortably:
+// <= AIOS_PREFILL_BF16_MAX_GB (default 48) and under a quarter of the free HBM at finalize (Mistral-7B
+// 14 GB, Llama-3-70B at TP=8 17.5 GB per rank; the 70B at TP=1 stays on the fused GEMM).
+void Engine::setup_blas_prefill() {
+  if (!gm_ok_) return;
+  if (const char* e = std::getenv("AIOS_PREFILL_BLAS"))
+    if (std::atoi(e) == 0) return;
+  if (const char* e = std::getenv("AIOS_PREFILL_BLAS_MIN")) blas_min_rows_ = std::max(1, std::atoi(e));
+  if (gm_rows_ < blas_min_rows_) return;
+  const int d = cfg_.d_model, qd = cfg_.n_heads * cfg_.head_dim, kvd = cfg_.n_kv_heads * cfg_.head_dim;
+  const int ff = cfg_.d_ff;
+  for (const auto& L : layers_) {
+    if (L.wq.w.rows != qd || L.wk.w.rows != kvd || L.wv.w.rows != kvd || L.wq.w.cols != d || L.wk.w.cols != d ||
+        L.wv.w.cols != d || L.wo.w.rows != d || L.wo.w.cols != qd || L.wgu.w.rows != 2 * ff || L.wgu.w.cols != d ||
+        L.wdown.w.rows != d || L.wdown.w.cols != ff)
+      return;
+  }
+  const size_t per = ((size_t)(qd + 2 * kvd) * d + (size_t)d * qd + (size_t)2 * ff * d + (size_t)d * ff) * 2;
+  const size_t bytes = per * cfg_.n_layers;
+  double max_gb = 48.0;
+  if (const char* e = std::getenv("AIOS_PREFILL_BF16_MAX_GB")) max_gb = std::atof(e);
+  size_t fr = 0, tot = 0;
+  HIP_CHECK(hipMemGetInfo(&fr, &tot));
+  if ((double)bytes > max_gb * 1e9 || bytes > fr / 4) return;
+  auto b = std::make_unique<BlasGemm>();
+  if (!b->ok()) return;
+  w16_.assign((size_t)4 * cfg_.n_layers, nullptr);
+  for (int l = 0; l < cfg_.n_layers; ++l) {
+    const LayerW& L = layers_[l];
+    bf16_t* base = (bf16_t*)dmalloc(per);
+    bf16_t* wqkv = base;
+    bf16_t* wo = wqkv + (size_t)(qd + 2 * kvd) * d;
+    bf16_t* wgu = wo + (size_t)d * qd;
+    bf16_t* wdn = wgu + (size_t)2 * ff * d;
+    launch_dequant_bf16(L.wq.w, wqkv, stream_);
+    launch_dequant_bf16(L.wk.w, wqkv + (size_t)qd * d, stream_);
+    launch_dequant_bf16(L.wv.w, wqkv + (size_t)(qd + kvd) * d, stream_);
+    launch_dequant_bf16(L.wo.w, wo, stream_);
+    launch_dequant_bf16(L.wgu.w, wgu, stream_);
+    launch_dequant_bf16(L.wdown.w, wdn, stream_);
+    w16_[4 * l] = wqkv; w16_[4 * l + 1] = wo; w16_[4 * l + 2] = wgu; w16_[4 * l + 3] = wdn;
+  }
+  gm_gu32_ = (float*)dmalloc((size_t)gm_rows_ * 2 * ff * 4);
+  w16_bytes_ = bytes;
+  blas_ = std::move(b);
 }
 
 // TP: sum the row-parallel partials in `p` over the ranks and add the total into `residual`
@@ -1040,7 +1090,9 @@ void Engine::prefill_gemm(int slot, const std::vector<int>& tokens, int start_po
       g.seg[0] = L.wq.w; g.seg[1] = L.wk.w; g.seg[2] = L.wv.w;
       g.seg_n0[0] = 0; g.seg_n0[1] = qd; g.seg_n0[2] = qd + kvd;
       g.N = ldqkv; g.C = gm_qkv_; g.ldc = ldqkv; g.epi = GEPI_STORE;
-      gemm(g);
+      // long chunks: hipBLASLt on the resident bf16 weights (blas.h); falls back per call
+      const bool lib = blas_ && n >= blas_min_rows_;
+      if (!(lib && blas_->gemm(gm_a16_, d, w16_[4 * l], gm_qkv_, ldqkv, n, ldqkv, d, false, stream_))) gemm(g);
       QkvPostArgs p;
       p.qkv = gm_qkv_; p.ldqkv = ldqkv; p.T = n;
       p.n_heads = H; p.n_kv_heads = Hkv; p.head_dim = hd;
@@ -1060,18 +1112,21 @@ void Engine::prefill_gemm(int slot, const std::vector<int>& tokens, int start_po
       std::memset(&g, 0, sizeof(g));
       g.A = gm_attn16_; g.lda = qd; g.M = n; g.K = qd; g.nseg = 1; g.seg[0] = L.wo.w; g.N = d; g.ldc = d;
       if (tp) { g.C = gm_part_; g.epi = GEPI_STORE; } else { g.C = gm_x_; g.epi = GEPI_ACCUM; }
-      gemm(g);
+      if (!(lib && blas_->gemm(gm_attn16_, qd, w16_[4 * l + 1], g.C, d, n, d, qd, !tp, stream_))) gemm(g);
       if (tp) allreduce(gm_part_, (size_t)n * d, gm_x_);
       // FFN
       launch_rmsnorm_bf16(gm_x_, d, L.ffn_norm, gm_a16_, d, n, d, cfg_.norm_eps, stream_);
       std::memset(&g, 0, sizeof(g));
       g.A = gm_a16_; g.lda = d; g.M = n; g.K = d; g.nseg = 1; g.seg[0] = L.wgu.w; g.N = 2 * ff;
       g.C16 = gm_ff16_; g.ldc = ff; g.epi = GEPI_SWIGLU_BF16;
-      gemm(g);
+      if (lib && blas_->gemm(gm_a16_, d, w16_[4 * l + 2], gm_gu32_, 2 * ff, n, 2 * ff, d, false, stream_))
+        launch_swiglu_interleaved_bf16(gm_gu32_, 2 * ff, gm_ff16_, ff, n, ff, stream_);
+      else
+        gemm(g);
       std::memset(&g, 0, sizeof(g));
       g.A = gm_ff16_; g.lda = ff; g.M = n; g.K = ff; g.nseg = 1; g.seg[0] = L.wdown.w; g.N = d; g.ldc = d;
       if (tp) { g.C = gm_part_; g.epi = GEPI_STORE; } else { g.C = gm_x_; g.epi = GEPI_ACCUM; }
-      gemm(g);
+      if (!(lib && blas_->gemm(gm_ff16_, ff, w16_[4 * l + 3], g.C, d, n, d, ff, !tp, stream_))) gemm(g);
       if (tp) allreduce(gm_part_, (size_t)n * d, gm_x_);
     }
     if (r0 + n == T && want_logits) lm_head(1, gm_x_ + (size_t)(n - 1) * d, d);

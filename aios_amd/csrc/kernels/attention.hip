@@ -52,7 +52,9 @@ __global__ void __launch_bounds__(512) attn_decode_kernel(AttnDecodeArgs a, Attn
     const int hsi = wg / sp_.p_long, sp = wg % sp_.p_long;
     if (hsi >= a.n_kv_heads * (G / GL)) return;
     const int kvh = hsi / (G / GL), h0 = kvh * G + (hsi % (G / GL)) * GL;
-    attn_core<HD, GL>(a, sp, kvh, h0, h0, sp_.p_long, sp_.ppw);
+    // long mode: every K/V line is read by exactly one workgroup -> streaming loads (round 4,
+    // same box: --prompt 4000 546.9 -> 567.0 tok/s, 16000 467.6 -> 487.3)
+    attn_core<HD, GL>(a, sp, kvh, h0, h0, sp_.p_long, sp_.ppw, a.kv_nt != 0);
   }
 }
 
@@ -92,6 +94,9 @@ void launch_attn_decode(const AttnDecodeArgs& a, hipStream_t st) {
   const int G = a.n_heads / a.n_kv_heads;
   AttnDecodeArgs b = a;
   if (b.split <= 0) b.split = attn_decode_split(a.max_ctx, a.B, a.n_kv_heads);
+  if (b.combine_trips == 0) b.combine_trips = attn_env_int("AIOS_ATTN_COMBINE", 1);
+  if (b.kv_nt < 0) b.kv_nt = attn_env_int("AIOS_ATTN_NT", 1);
+  if (b.kv_tail < 0) b.kv_tail = attn_env_int("AIOS_ATTN_TAIL", 1);
   // Batched decode fills the chip with (row, KV head) workgroups on its own: from
   // AIOS_ATTN_GROUPED_MIN such workgroups up, every context length takes the grouped mode (one
   // K/V read for the G query heads of a KV head) instead of the per-query-head split that buys

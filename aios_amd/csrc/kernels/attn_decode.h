@@ -69,6 +69,11 @@ constexpr float kNeg = -1e30f;
 // adds a range-scaling compare + 2 selects per call
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
+__device__ __forceinline__ uint4 ld_nt16(const bf16_t* p) {
+  const gu32x4 v = __builtin_nontemporal_load((const gu32x4*)p);
+  return make_uint4(v[0], v[1], v[2], v[3]);
+}
+
 __device__ __forceinline__ float dot2_bf16(uint32_t a, uint32_t b, float c) {
   return __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(gbf16x2, a), __builtin_bit_cast(gbf16x2, b), c, false);
 }
@@ -82,7 +87,7 @@ __device__ __forceinline__ float dot2_bf16(uint32_t a, uint32_t b, float c) {
 // MFMA prefill path rounds q), P . V on packed v_pk_fma_f32 with the probabilities in fp32.
 template <int HD, int G>
 __device__ __forceinline__ void attn_core(const AttnDecodeArgs& a, int sp, int kvh, int h0, int ci, int P_max,
-                                          int ppw) {
+                                          int ppw, bool nt = false) {
   constexpr int NW = 8;                // waves per workgroup
   constexpr int LPK = HD / 8;          // lanes per key (8 dims per lane)
   constexpr int KPS = 64 / LPK;        // keys per wave-instruction
@@ -125,13 +130,34 @@ __device__ __forceinline__ void attn_core(const AttnDecodeArgs& a, int sp, int k
 
   // two passes in flight per workgroup: buffers A and B (static, so they stay in VGPRs)
   uint4 kA[STEPS], vA[STEPS], kB[STEPS], vB[STEPS];
+  const bool tail = a.kv_tail != 0;
   auto issue = [&](uint4 (&kr)[STEPS], uint4 (&vr)[STEPS], int chunk) __attribute__((always_inline)) {
     const int c = min(chunk, cmax);  // clamped: always a mapped block
     const size_t base = (size_t)(btr ? btr[c] : slot * maxb + c) * blk_stride;
+    if (tail && (chunk + 1) * CH > len) {
+      // the context's last, partly filled block: only the lanes of live keys load (a 153-key context
+      // fetched 2 x 64 KB for 25 keys of its second block); dead keys hold zeros (scores masked, V x 0)
+      const int k0 = chunk * CH + koff;
 #pragma unroll
-    for (int s = 0; s < STEPS; ++s) kr[s] = *(const uint4*)(kc + base + (size_t)s * KPS * HD);
+      for (int s = 0; s < STEPS; ++s) {
+        kr[s] = make_uint4(0u, 0u, 0u, 0u);
+        vr[s] = make_uint4(0u, 0u, 0u, 0u);
+        if (k0 + s * KPS < len) {
+          kr[s] = *(const uint4*)(kc + base + (size_t)s * KPS * HD);
+          vr[s] = *(const uint4*)(vc + base + (size_t)s * KPS * HD);
+        }
+      }
+    } else if (nt) {  // streaming (nt) policy: K/V lines read once per launch (long mode)
 #pragma unroll
-    for (int s = 0; s < STEPS; ++s) vr[s] = *(const uint4*)(vc + base + (size_t)s * KPS * HD);
+      for (int s = 0; s < STEPS; ++s) kr[s] = ld_nt16(kc + base + (size_t)s * KPS * HD);
+#pragma unroll
+      for (int s = 0; s < STEPS; ++s) vr[s] = ld_nt16(vc + base + (size_t)s * KPS * HD);
+    } else {
+#pragma unroll
+      for (int s = 0; s < STEPS; ++s) kr[s] = *(const uint4*)(kc + base + (size_t)s * KPS * HD);
+#pragma unroll
+      for (int s = 0; s < STEPS; ++s) vr[s] = *(const uint4*)(vc + base + (size_t)s * KPS * HD);
+    }
   };
   issue(kA, vA, sp);
   if (sp + P < nchunk) issue(kB, vB, sp + P);
@@ -296,6 +322,57 @@ __device__ __forceinline__ void attn_core(const AttnDecodeArgs& a, int sp, int k
   //      w_p = exp2(m_p - M) / L in LDS; (3) every output sums w_p * o_p with 16 loads in flight.
   //      Two memory round trips for up to 64 partials (was one per 8 partials).
   __shared__ float s_pm[G][64], s_pl[G][64];
+  // one memory round trip (round 4): when every output has one thread and the partials fit one
+  // register batch, each thread issues its output's nact partial loads TOGETHER with the (m, l)
+  // sweep and folds them after the weights are ready -- same order of sums as the two-trip path
+  auto one_trip = [&](auto ob) __attribute__((always_inline)) {
+    constexpr int OB = decltype(ob)::value;
+    const int idx = threadIdx.x;
+    const bool act = idx < G * HD;
+    const int g = act ? idx / HD : 0, d = act ? idx - g * HD : 0;
+    const float* op = a.o_part + ((size_t)b * a.n_heads + h0 + g) * a.n_chunks * HD + d;
+    float ov[OB];
+#pragma unroll
+    for (int j = 0; j < OB; ++j) ov[j] = ld_wt(op + (size_t)min(j, nact - 1) * HD);  // clamped: in bounds
+    for (int i = threadIdx.x; i < G * nact; i += NT) {
+      const int gg = i / nact, p = i - gg * nact;
+      const float* mlp = a.ml + (((size_t)b * a.n_heads + h0 + gg) * a.n_chunks + p) * 2;
+      s_pm[gg][p] = ld_wt(mlp);
+      s_pl[gg][p] = ld_wt(mlp + 1);
+    }
+    __syncthreads();
+    if (wave < G) {
+      const float mv = lane < nact ? s_pm[wave][lane] : kNeg;
+      const float lv = lane < nact ? s_pl[wave][lane] : 0.f;
+      float M = mv;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) M = fmaxf(M, __shfl_xor(M, o));
+      const float e = fast_exp2(mv - M);
+      float L = e * lv;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) L += __shfl_xor(L, o);
+      if (lane < nact) s_pm[wave][lane] = e / L;
+    }
+    __syncthreads();
+    stamp(5);
+    if (act) {
+      float acc = 0.f;
+#pragma unroll
+      for (int j = 0; j < OB; ++j)
+        if (j < nact) acc = fmaf(s_pm[g][j], ov[j], acc);
+      const int h = h0 + g;
+      if (a.out16) a.out16[((size_t)b * a.n_heads + h) * HD + d] = f32_to_bf16(acc);
+      else a.out[((size_t)b * a.n_heads + h) * HD + d] = acc;
+    }
+  };
+  if (G * HD <= NT && nact <= 32 && a.combine_trips != 2) {
+    if (nact <= 8) one_trip(std::integral_constant<int, 8>{});
+    else if (nact <= 16) one_trip(std::integral_constant<int, 16>{});
+    else one_trip(std::integral_constant<int, 32>{});
+    if (threadIdx.x == 0) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
+    stamp(6);
+    return;
+  }
   for (int i = threadIdx.x; i < G * nact; i += NT) {
     const int g = i / nact, p = i - g * nact;
     const float* mlp = a.ml + (((size_t)b * a.n_heads + h0 + g) * a.n_chunks + p) * 2;

@@ -568,7 +568,11 @@ __global__ void __launch_bounds__((q8_max_threads<U, PIPE>())) gemv_q8_rows(Gemv
   // probes (tools/gemv_cu_probe.py): phase stamps of the first and last wave of every workgroup --
   // 0 start, 1 first weight loads issued, 2 x staged, 3 barrier passed, 4 first pair computed, 5 done
   unsigned long long ts[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  auto stamp = [&](int i) __attribute__((always_inline)) { ts[i] = __builtin_amdgcn_s_memrealtime(); };
+  // (probe launches only: a wave-uniform branch on the kernarg, no s_memrealtime in production)
+  const bool stamps = a.dbg_ts != nullptr;
+  auto stamp = [&](int i) __attribute__((always_inline)) {
+    if (stamps) ts[i] = __builtin_amdgcn_s_memrealtime();
+  };
   stamp(0);
 
   auto seg_idx = [&](int p, int& lrow) -> int {
@@ -670,7 +674,7 @@ __global__ void __launch_bounds__((q8_max_threads<U, PIPE>())) gemv_q8_rows(Gemv
         s[b] = rsqrtf(t / (float)a.K + a.eps);
       }
     }
-    if (!ts[4]) stamp(4);
+    if (stamps && !ts[4]) stamp(4);
     if constexpr (B == 1) {
       const float2 v = wave_sum_pair(acc[0][0], acc[1][0]);
       float2 rope = rope_w;
@@ -856,15 +860,29 @@ void launch_q8_rows(const GemvArgs& a, size_t lds, hipStream_t st) {
     const int maxw = q8_max_threads<U, PIPE>() / 64;
     const int ppw = (npairs + cus * maxw - 1) / (cus * maxw);
     int want = (npairs + cus * ppw - 1) / (cus * ppw);
+    bool mixed = false;
+    int np0 = 0;
     if (QT0 != QT1 && a.nseg > 1 && ppw == 1) {
       // mixed formats: whole waves per format in every workgroup (the kernel splits nw by pair
       // counts), e.g. TinyLlama's QKV 1152 Q4_K + 128 Q6_K pairs -> 5 + 1 waves, not 4 + 1
-      const int np0 = a.seg_row0[a.nseg - 1] / 2;
+      np0 = a.seg_row0[a.nseg - 1] / 2;
       want = (np0 + cus - 1) / cus + (npairs - np0 + cus - 1) / cus;
+      mixed = true;
     }
-    if (want >= 2 && want <= maxw) {
+    // several pairs per wave only for the long-K (U >= 3) shapes: TinyLlama's 5632-pair gate/up at
+    // U = 1 went 6.96 -> 9.15 us as 3 pairs per wave on one 8-wave workgroup per CU
+    // (profiles/decode_tinyllama_rocprof_r4.txt)
+    if (want >= 2 && want <= maxw && (ppw == 1 || U >= 3)) {
       nw = want;
       blocks = std::min(cus, (npairs + nw - 1) / nw);
+      if (mixed) {
+        // the grid must cover each format's pairs with ITS waves (the kernel's split below):
+        // 214 blocks x 5 Q4_K waves left 82 of TinyLlama's 1152 Q|K pairs to a second pass (9.5 us)
+        int nw0 = (int)(((long)nw * np0 + npairs / 2) / npairs);
+        nw0 = std::max(1, std::min(nw - 1, nw0));
+        const int nw1 = nw - nw0;
+        blocks = std::min(cus, std::max((np0 + nw0 - 1) / nw0, (npairs - np0 + nw1 - 1) / nw1));
+      }
     }
   }
   if (!blocks) blocks = std::min((npairs + nw - 1) / nw, cus * per_cu);

@@ -107,6 +107,9 @@ struct AttnDecodeArgs {
   int short_len = -1;      // contexts up to this many keys split by query head (-1: launcher decides)
   int* counters;           // [B][n_kv_heads] arrival tickets, zero-initialised, self re-arming
   unsigned long long* ts = nullptr;  // probes: [grid][8] s_memrealtime phase stamps (tools/attn_probe.py --stamps)
+  int kv_nt = -1;          // long mode: K/V loads with the streaming (nt) policy (-1: AIOS_ATTN_NT, default 1)
+  int kv_tail = -1;        // last partial block: loads only for live keys (-1: AIOS_ATTN_TAIL, default 1)
+  int combine_trips = 0;   // split-K combine: 0 = launcher (AIOS_ATTN_COMBINE, default one round trip), 2 = two
 };
 constexpr int ATTN_CHUNK = 64;
 void launch_attn_decode(const AttnDecodeArgs& a, hipStream_t st);

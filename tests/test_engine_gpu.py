@@ -143,6 +143,27 @@ def test_prefill_gemm_chunks_match_reference(model_files, recipe, monkeypatch):
     assert (logits2 - rl).abs().max().item() < 2e-2 * scale
 
 
+@pytest.mark.parametrize("recipe", ["Q4_K_M", "mistral_shape"])
+def test_prefill_blas_chunks_match_reference(model_files, recipe, monkeypatch):
+    """long prefill chunks through hipBLASLt on the resident bf16 weights (blas.h): 64-row chunks of
+    a 150-token prompt with the library threshold at 32 rows -- two chunks on hipBLASLt, the 22-row
+    tail on the fused GEMM -- against the fp32 reference, continued at start_pos > 0 too"""
+    monkeypatch.setenv("AIOS_PREFILL_GEMM_ROWS", "64")
+    monkeypatch.setenv("AIOS_PREFILL_BLAS_MIN", "32")
+    path = model_files[recipe]
+    eng, cfg = _load(path)
+    assert eng.blas_prefill and eng.blas_prefill_min_rows == 32
+    ref = ReferenceModel.from_gguf(path, kv_bf16=True)
+    prompt = [1] + list(np.random.default_rng(5).integers(3, cfg.vocab_size, 149))
+    rl = ref.forward(prompt)[-1]
+    logits = torch.from_numpy(np.asarray(eng.prefill(0, prompt, 0, True)))
+    scale = max(rl.abs().max().item(), 1.0)
+    assert (logits - rl).abs().max().item() < 2e-2 * scale
+    eng.prefill(1, prompt[:70], 0, False)
+    logits2 = torch.from_numpy(np.asarray(eng.prefill(1, prompt[70:], 70, True)))
+    assert (logits2 - rl).abs().max().item() < 2e-2 * scale
+
+
 @pytest.mark.parametrize("T", [3, 4, 5, 8, 15])
 @pytest.mark.parametrize("q8", [False, True])
 def test_short_prompt_prefill_matches_reference(model_files, monkeypatch, T, q8):

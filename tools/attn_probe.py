@@ -50,7 +50,9 @@ def stamps(E):
     flush = torch.empty(512 << 20, dtype=torch.uint8, device="cuda")
     ts = torch.zeros(4096 * 8, dtype=torch.int64, device="cuda")
     names = ["entry", "seq_len", "pass1", "merged", "published", "weights", "done"]
-    for L in (153, 1000, 4000):
+    for L, comb in ((153, 1), (1000, 2), (1000, 1), (4000, 2), (4000, 1)):
+        # AIOS_ATTN_COMBINE: 2 = two-round-trip split-K combine, 1 = one round trip (round 4)
+        os.environ["AIOS_ATTN_COMBINE"] = str(comb)
         seq = torch.tensor([L], dtype=torch.int32, device="cuda")
         run = lambda t=0: E.attn_decode(q.data_ptr(), kc.data_ptr(), vc.data_ptr(), seq.data_ptr(), slot.data_ptr(),
                                         1, H, Hkv, hd, max_ctx, nch, 1 / math.sqrt(hd), opart.data_ptr(), ml.data_ptr(),
@@ -74,7 +76,10 @@ def stamps(E):
             v = t[:, k][t[:, k] > 0] if k else t[:, 0]
             if len(v):
                 res[n] = [round(float(np.median(v)), 2), round(float(v.max()), 2)]
-        print(json.dumps({"len": L, "workgroups": int(len(t) / 4), "phase_us_median_max": res}), flush=True)
+        us = graph_time(lambda: run())
+        print(json.dumps({"len": L, "combine_trips": comb, "graph_us": round(us, 2), "workgroups": int(len(t) / 4),
+                          "phase_us_median_max": res}), flush=True)
+    os.environ.pop("AIOS_ATTN_COMBINE")
 
 
 def main():
