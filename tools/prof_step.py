@@ -31,7 +31,8 @@ for k, v in sorted(agg.items(), key=lambda x: -x[1][1]):
     print(f"{v[1]:9.1f} us {v[0]:4d}x  avg {v[1] / v[0]:7.2f}  {k}")
 print("--- layer 1 (median over steps)")
 s0 = steps[0]
-first = next(i for i, r in enumerate(s0) if i > 0 and name(r) == name(s0[1]) and i > 2)  # layer 1 starts where layer 0 did
+# layer 1 starts where layer 0 did (the step's second kernel seen again); none: print from kernel 1
+first = next((i for i, r in enumerate(s0) if i > 2 and name(r) == name(s0[1])), 1)
 for i in range(first, min(first + 9, n_mode)):
     r = s0[i]
     print(f"  +{med_g[i]:5.2f} gap  {med_d[i]:7.2f} us  grid={r['Grid_Size_X']:>7} wg={r['Workgroup_Size_X']:>4} "
