@@ -256,19 +256,23 @@ PYBIND11_MODULE(_engine, m) {
         e.set_allreduce(&XgmiComm::hook, &c);
         e.set_allgather(&XgmiComm::gather_hook, &c);
         e.set_allreduce_norm(&XgmiComm::norm_hook, &c);
+        e.set_tp_fuse(c.fuse_ctx(), c.fuse_grid());
       })
       .def("set_comm", [](Engine& e, RcclComm& c) {
         e.set_allreduce(&RcclComm::hook, &c);
         e.set_allgather(&RcclComm::gather_hook, &c);
         e.set_allreduce_norm(&RcclComm::norm_hook, &c);
       })
-      .def_property_readonly("vocab_parallel", &Engine::vocab_parallel);
+      .def_property_readonly("vocab_parallel", &Engine::vocab_parallel)
+      .def_property_readonly("tp_fused", &Engine::tp_fused);
 
   // ------------------------------------------------------------------ TP collectives (xGMI)
   py::class_<XgmiComm>(m, "XgmiComm")
       .def(py::init<int, int, int, size_t>(), py::arg("rank"), py::arg("world"), py::arg("device"),
            py::arg("cap_floats"))
       .def("ipc_handle", [](const XgmiComm& c) { return py::bytes(c.ipc_handle()); })
+      .def("set_ranks_per_gpu", &XgmiComm::set_ranks_per_gpu)
+      .def_property_readonly("fuse_grid", &XgmiComm::fuse_grid)
       .def("connect", [](XgmiComm& c, const std::vector<py::bytes>& hs) {
         std::vector<std::string> v;
         for (auto& h : hs) v.push_back(std::string(h));

@@ -44,6 +44,11 @@ constexpr int AR_MAX_WG = 512;
 constexpr int AR_THREADS = 256;
 constexpr int AR_CHUNK = AR_THREADS * 4;              // elements per workgroup per call
 constexpr size_t AR_MAX_CALL = (size_t)AR_MAX_WG * AR_CHUNK;  // elements per kernel call
+// C1 / C2 fused into the batch <= 4 GEMV engine's epilogue (EPI_TP_RESID, gemv_lds.h): per engine
+// workgroup ("slot") a private double-buffered stage of up to TPF_CAP partial outputs behind the
+// one-shot region, and one flag per (slot, rank) behind the collectives' flags
+constexpr int TPF_SLOTS = 256;
+constexpr int TPF_CAP = 1024;
 
 struct ArDevCtx {
   float* buf[AR_MAX_RANKS];         // rank r's shared region: stage f32 [2][cap] | result f32 [2][cap] | stage bf16 [2][cap]
@@ -52,7 +57,13 @@ struct ArDevCtx {
   uint32_t* error;                  // set to 1 when a wait timed out (device view of pinned host memory)
   int rank, world;
   size_t cap;                       // elements per half-buffer (<= AR_MAX_CALL)
+  uint32_t* fepoch;                 // my per-slot epochs of the fused GEMV epilogue [TPF_SLOTS] (local)
 };
+// the fused epilogue's regions of rank p (same offsets on every rank)
+__host__ __device__ inline float* tpf_stage(const ArDevCtx* c, int p) { return c->buf[p] + 5 * c->cap; }
+__host__ __device__ inline uint32_t* tpf_flags(const ArDevCtx* c, int p) {
+  return c->flags[p] + 2 * AR_MAX_WG * AR_MAX_RANKS;
+}
 
 class XgmiComm {
  public:
@@ -88,6 +99,12 @@ class XgmiComm {
   int call_wg() const { return (int)(call_cap_ / AR_CHUNK); }
   void set_call_wg(int wg);
   void set_two_shot_min(size_t n) { two_shot_min_ = n; }
+  // the fused O / down epilogue (EPI_TP_RESID): device context for GemvArgs::tp (null when off:
+  // world 1 or AIOS_TP_FUSE=0) and the engine-workgroup cap that lets every rank's grid be resident
+  // at once when ranks share a GPU (0: one workgroup per CU)
+  const ArDevCtx* fuse_ctx() const { return fuse_on_ && uncached_ && h_.world > 1 ? d_ : nullptr; }
+  int fuse_grid() const { return fuse_grid_; }
+  void set_ranks_per_gpu(int n);
   bool bf16_payload() const { return bf16_; }
   void set_bf16_payload(bool on) { bf16_ = on; }
   // Engine hooks (AllReduceFn / AllGatherFn-compatible trampolines)
@@ -111,6 +128,9 @@ class XgmiComm {
   size_t two_shot_min_ = 64 * 1024;  // floats (256 KB)
   size_t call_cap_ = AR_MAX_CALL;    // elements per launch (see set_call_wg)
   bool bf16_ = true;                 // bf16 staging for the two-shot (prefill) path
+  bool fuse_on_ = true;              // AIOS_TP_FUSE (default 1)
+  bool uncached_ = false;            // shared regions got uncached memory (required by the fused path)
+  int fuse_grid_ = 0;
 };
 
 void launch_allreduce(const ArDevCtx* ctx, int world, float* data, size_t n, float* residual, hipStream_t st);

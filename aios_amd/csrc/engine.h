@@ -127,6 +127,10 @@ class Engine {
   void set_allreduce(AllReduceFn fn, void* ctx) { allreduce_ = fn; allreduce_ctx_ = ctx; }
   void set_allgather(AllGatherFn fn, void* ctx) { allgather_ = fn; allgather_ctx_ = ctx; }
   void set_allreduce_norm(AllReduceNormFn fn, void* ctx) { allreduce_norm_ = fn; allreduce_norm_ctx_ = ctx; }
+  // TP: the O / down all-reduces fused into the B <= 4 GEMV engine's epilogue (EPI_TP_RESID);
+  // ctx null = separate all-reduce launches; grid = engine workgroups per launch (0: one per CU)
+  void set_tp_fuse(const ArDevCtx* ctx, int grid) { tp_fuse_ = ctx; tp_fuse_grid_ = grid; }
+  bool tp_fused() const { return tp_fuse_ != nullptr; }
   bool vocab_parallel() const { return cfg_.vocab_parallel != 0; }
   void reset_graphs();
   int capture_graphs(int max_b);  // pre-capture the decode-step graphs of B = 1..max_b (masked + unmasked)
@@ -241,6 +245,9 @@ class Engine {
   std::vector<bf16_t*> w16_;  // 4 per layer
   float* gm_gu32_ = nullptr;
   int blas_min_rows_ = 256;
+  const ArDevCtx* tp_fuse_ = nullptr;
+  int tp_fuse_grid_ = 0;
+  bool tp_fuse_gemv(GemvArgs a);  // EPI_TP_RESID launch when the engine serves the shape (else false)
   size_t w16_bytes_ = 0;
   void setup_blas_prefill();
   // batched decode through the skinny MFMA GEMM (B >= dec_gemm_min_b_): bf16 activation buffers

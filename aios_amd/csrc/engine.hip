@@ -1,5 +1,6 @@
 // Engine implementation -- see engine.h.
 #include "engine.h"
+#include "comm.h"
 #include <cstdlib>
 #include <map>
 
@@ -972,12 +973,15 @@ void Engine::layer_decode(int l, int B) {
     a.o_part = opart_; a.ml = ml_; a.out = attn_; a.counters = attn_cnt_;
     launch_attn_decode(a, stream_);
   }
-  // ---- O projection (+ residual; TP: partial -> all-reduce -> add)
+  // ---- O projection (+ residual; TP: partial -> all-reduce -> add, fused into the GEMV epilogue
+  // when the comm provides it)
   {
     const bool tp = cfg_.tp_size > 1;
-    GemvArgs a = gemv_args({&L.wo}, d, qd, B, attn_, qd, nullptr, tp ? ff_ : x_, d, tp ? EPI_STORE : EPI_RESID, l);
-    launch_gemv(a, stream_);
-    if (tp) allreduce(ff_, (size_t)B * d, x_);
+    if (!(tp && tp_fuse_gemv(gemv_args({&L.wo}, d, qd, B, attn_, qd, nullptr, x_, d, EPI_TP_RESID, l)))) {
+      GemvArgs a = gemv_args({&L.wo}, d, qd, B, attn_, qd, nullptr, tp ? ff_ : x_, d, tp ? EPI_STORE : EPI_RESID, l);
+      launch_gemv(a, stream_);
+      if (tp) allreduce(ff_, (size_t)B * d, x_);
+    }
   }
   // ---- gate/up (+RMSNorm, SwiGLU; bf16 out when the down GEMV stages int8 activations, i.e. both
   // matrices take the int8-activation kernels: quantised formats, not F16 / BF16)
@@ -991,12 +995,49 @@ void Engine::layer_decode(int l, int B) {
   // ---- down (+ residual)
   {
     const bool tp = cfg_.tp_size > 1;
-    GemvArgs a = gemv_args({&L.wdown}, d, cfg_.d_ff, B, ff_, cfg_.d_ff, nullptr, tp ? attn_ : x_, d,
-                           tp ? EPI_STORE : EPI_RESID, l);
-    a.x16 = ff16;
-    launch_gemv(a, stream_);
-    if (tp) allreduce(attn_, (size_t)B * d, x_);
+    GemvArgs f = gemv_args({&L.wdown}, d, cfg_.d_ff, B, ff_, cfg_.d_ff, nullptr, x_, d, EPI_TP_RESID, l);
+    f.x16 = ff16;
+    if (!(tp && tp_fuse_gemv(f))) {
+      GemvArgs a = gemv_args({&L.wdown}, d, cfg_.d_ff, B, ff_, cfg_.d_ff, nullptr, tp ? attn_ : x_, d,
+                             tp ? EPI_STORE : EPI_RESID, l);
+      a.x16 = ff16;
+      launch_gemv(a, stream_);
+      if (tp) allreduce(attn_, (size_t)B * d, x_);
+    }
   }
+}
+
+// EPI_TP_RESID through the LDS-DMA engine (kernel_sel 3: every shape, no size floor) when the comm
+// provides the fused context, the engine serves the shape and each workgroup's B x rows fit its
+// stage slot (comm.h TPF_*); the grid is capped when ranks share a GPU so that every rank's
+// workgroups are resident together (their epilogues wait on each other)
+bool Engine::tp_fuse_gemv(GemvArgs a) {
+  if (!tp_fuse_ || a.B > 4 || !a.act_q8 || a.force_v1) return false;  // (int8-activation kernels only)
+  a.tp = tp_fuse_;
+  a.tune_ksplit = 0;
+  const int qt0 = a.seg[0].qtype;
+  if (a.B == 1) {
+    // batch 1: the row-pair kernel (any K; the shapes a TP rank holds are below the LDS engine's
+    // size floor anyway), grid capped when ranks share the GPU
+    if (a.nseg != 1 || !(qt0 == QT_Q4_K || qt0 == QT_Q5_K || qt0 == QT_Q6_K || qt0 == QT_Q4_0 || qt0 == QT_Q8_0))
+      return false;
+    a.kernel_sel = 1;
+    a.tune_grid = 0;
+    a.tune_u = 0;
+    a.grid_cap = tp_fuse_grid_;
+    launch_gemv(a, stream_);
+    return true;
+  }
+  a.kernel_sel = 3;
+  a.tune_grid = tp_fuse_grid_;
+  const int npairs = a.N / 2;
+  const int G = std::min(tp_fuse_grid_ > 0 ? tp_fuse_grid_ : device_cu_count(), npairs);
+  const int rows_max = 2 * ((npairs + G - 1) / G);
+  const int qt = a.seg[0].qtype;
+  const bool engine_fmt = qt == QT_Q4_K || qt == QT_Q5_K || qt == QT_Q6_K || qt == QT_Q4_0 || qt == QT_Q8_0;
+  if (!engine_fmt || G > TPF_SLOTS || a.B * rows_max > TPF_CAP || a.nseg != 1 || !gemv_engine_fits(a)) return false;
+  launch_gemv(a, stream_);
+  return true;
 }
 
 // logits_[B][V] = rmsnorm(x) . output^T.  Vocab-parallel TP: this rank holds V/tp rows of

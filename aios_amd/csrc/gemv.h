@@ -12,7 +12,11 @@ enum GemvEpilogue : int {
   EPI_RESID = 1,   // y[b][n] += acc        (residual stream update)
   EPI_SWIGLU = 2,  // y[b][n/2] = silu(acc[2i]) * acc[2i+1]   (rows interleaved gate/up)
   EPI_QKV = 3,     // (+bias) RoPE on Q/K, Q -> y, K/V -> bf16 KV cache at pos[b]
+  EPI_TP_RESID = 4,  // TP row-parallel O / down: y[b][n] += sum over ranks of acc (the one-shot all-reduce
+                     //   in the epilogue, GemvArgs::tp; the B <= 4 LDS-DMA engine only, gemv_lds.h)
 };
+
+struct ArDevCtx;  // comm.h
 
 struct GemvArgs {
   QWeight seg[GEMV_MAX_SEGS];   // row-range segments (e.g. Q,K in Q4_K + V in Q6_K)
@@ -56,6 +60,8 @@ struct GemvArgs {
   // in the QKV kernel (null: looked up from pos / slot / block_table)
   const int* step_kv;
   const float2* step_rope;
+  const ArDevCtx* tp;           // EPI_TP_RESID: the XgmiComm device context (XgmiComm::fuse_ctx)
+  int grid_cap;                 // EPI_TP_RESID row kernel: workgroups at most (0: no cap; ranks sharing a GPU)
 };
 
 void launch_gemv(const GemvArgs& a, hipStream_t st);

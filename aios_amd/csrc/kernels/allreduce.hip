@@ -264,10 +264,12 @@ __global__ __launch_bounds__(AR_THREADS) void allgather_cols_kernel(const ArDevC
   }
 }
 
-void* alloc_shared(size_t bytes) {
+void* alloc_shared(size_t bytes, bool* uncached = nullptr) {
   // uncached device memory: remote stores / loads bypass both GPUs' caches
   void* p = nullptr;
+  if (uncached) *uncached = true;
   if (hipExtMallocWithFlags(&p, bytes, hipDeviceMallocUncached) == hipSuccess) return p;
+  if (uncached) *uncached = false;
   (void)hipGetLastError();
   if (hipExtMallocWithFlags(&p, bytes, hipDeviceMallocFinegrained) == hipSuccess) return p;
   (void)hipGetLastError();
@@ -303,11 +305,19 @@ XgmiComm::XgmiComm(int rank, int world, int device, size_t cap_floats) : device_
   // are sized for that regardless of the requested capacity: 5 x 2 MB per rank
   (void)cap_floats;
   h_.cap = AR_MAX_CALL;
-  mybuf_ = (float*)alloc_shared(5 * h_.cap * sizeof(float));
-  myflags_ = (uint32_t*)alloc_shared(2 * AR_MAX_WG * AR_MAX_RANKS * sizeof(uint32_t));
-  HIP_CHECK(hipMemset(myflags_, 0, 2 * AR_MAX_WG * AR_MAX_RANKS * sizeof(uint32_t)));
+  // + the fused GEMV epilogue's stage [TPF_SLOTS][2][TPF_CAP] and flags [TPF_SLOTS][ranks]
+  bool unc0 = false, unc1 = false;
+  mybuf_ = (float*)alloc_shared((5 * h_.cap + (size_t)2 * TPF_SLOTS * TPF_CAP) * sizeof(float), &unc0);
+  const size_t nflags = (size_t)(2 * AR_MAX_WG + TPF_SLOTS) * AR_MAX_RANKS;
+  myflags_ = (uint32_t*)alloc_shared(nflags * sizeof(uint32_t), &unc1);
+  // the fused epilogue's fence-free hand-off relies on uncached stage / flags (lg_tp_fuse)
+  uncached_ = unc0 && unc1;
+  HIP_CHECK(hipMemset(myflags_, 0, nflags * sizeof(uint32_t)));
   HIP_CHECK(hipMalloc(&h_.epoch, AR_MAX_WG * sizeof(uint32_t)));
   HIP_CHECK(hipMemset(h_.epoch, 0, AR_MAX_WG * sizeof(uint32_t)));
+  HIP_CHECK(hipMalloc(&h_.fepoch, TPF_SLOTS * sizeof(uint32_t)));
+  HIP_CHECK(hipMemset(h_.fepoch, 0, TPF_SLOTS * sizeof(uint32_t)));
+  if (const char* e = std::getenv("AIOS_TP_FUSE")) fuse_on_ = std::atoi(e) != 0;
   {
     void* hp = nullptr;
     HIP_CHECK(hipHostMalloc(&hp, 64, hipHostMallocMapped));
@@ -333,6 +343,7 @@ XgmiComm::~XgmiComm() {
   for (void* p : opened_) hipIpcCloseMemHandle(p);
   hipFree(d_);
   hipFree(h_.epoch);
+  hipFree(h_.fepoch);
   hipHostFree((void*)host_error_);
   hipFree(mybuf_);
   hipFree(myflags_);
@@ -369,6 +380,10 @@ void XgmiComm::connect(const std::vector<std::string>& handles) {
   HIP_CHECK(hipMemcpy(d_, &h_, sizeof(ArDevCtx), hipMemcpyHostToDevice));
   HIP_CHECK(hipDeviceSynchronize());
   connected_ = true;
+}
+
+void XgmiComm::set_ranks_per_gpu(int n) {
+  fuse_grid_ = n > 1 ? std::max(1, device_cu_count() / n) : 0;
 }
 
 void XgmiComm::set_call_wg(int wg) {

@@ -117,7 +117,9 @@ __device__ __forceinline__ void rg_dma_slot(const GemmQArgs& a, const QWeight& w
 
 // one MFMA wave: the 2 chunk steps of slot s (chunks q, q + 4 of its rows) into acc
 template <int QT, int MT>
-__device__ __forceinline__ void rg_compute_slot(const uint8_t* slot, int sb, int row0, int nbk, gf32x4 (&acc)[MT]) {
+// dbg (probes only, AIOS_RING_DBG): bit 0 = no dequant (raw code words as the MFMA operand), bit 1 = no MFMA
+__device__ __forceinline__ void rg_compute_slot(const uint8_t* slot, int sb, int row0, int nbk, gf32x4 (&acc)[MT],
+                                                int dbg = 0) {
   using L = RgLayout<QT, MT>;
   constexpr bool MB = QT == QT_Q4_K;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -154,8 +156,12 @@ __device__ __forceinline__ void rg_compute_slot(const uint8_t* slot, int sb, int
       }
       const int run = i >> 1;
       uint32_t p[4];
+      if (dbg & 1) {
+        p[0] = w0; p[1] = w1; p[2] = w0 ^ w1; p[3] = w1 + w0;
+      } else {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) p[e] = pk_bf16(fmaf(sc[run], qv[2 * e], -of[run]), fmaf(sc[run], qv[2 * e + 1], -of[run]));
+        for (int e = 0; e < 4; ++e) p[e] = pk_bf16(fmaf(sc[run], qv[2 * e], -of[run]), fmaf(sc[run], qv[2 * e + 1], -of[run]));
+      }
       gbf16x8 wf;
       __builtin_memcpy(&wf, p, 16);
       const int kl = QFmt<QT>::chunk_k0(cc, i >> 1) + 8 * (i & 1);  // k of this fragment within the superblock
@@ -165,14 +171,15 @@ __device__ __forceinline__ void rg_compute_slot(const uint8_t* slot, int sb, int
         const uint4 xv = *(const uint4*)(xs + m * 256 + (kl ^ (rg_xh(m) << 3)));
         gbf16x8 xf;
         __builtin_memcpy(&xf, &xv, 16);
-        acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, xf, acc[mt], 0, 0, 0);
+        if (dbg & 2) acc[mt][0] += __builtin_bit_cast(float, xv.x ^ p[0]);
+        else acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, xf, acc[mt], 0, 0, 0);
       }
     }
   }
 }
 
 template <int QT, int MT, int EPI>
-__device__ __forceinline__ void rg_body(const GemmQArgs& a, int S, int rg, int sp, float* inv_s) {
+__device__ __forceinline__ void rg_body(const GemmQArgs& a, int S, int rg, int sp, float* inv_s, int dbg) {
   using L = RgLayout<QT, MT>;
   extern __shared__ __attribute__((aligned(16))) uint8_t rg_smem[];
   __shared__ int last_flag;
@@ -220,7 +227,7 @@ __device__ __forceinline__ void rg_body(const GemmQArgs& a, int S, int rg, int s
   } else {
     rg_barrier();  // B1
     for (int t = 0; t < T; ++t) {
-      rg_compute_slot<QT, MT>(ring + (size_t)(t % L::R) * L::SLOT, sb0 + t, row0, nbk, acc);
+      if (!(dbg & 4)) rg_compute_slot<QT, MT>(ring + (size_t)(t % L::R) * L::SLOT, sb0 + t, row0, nbk, acc, dbg);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this slot's LDS reads done before it is refilled
       rg_barrier();
     }
@@ -233,8 +240,9 @@ __device__ __forceinline__ void rg_body(const GemmQArgs& a, int S, int rg, int s
 // one launch for every tile; mixed formats (Q4_K_M QKV: Q|K Q4_K, V Q6_K): the last segment's
 // tiles run the QT1 body
 template <int QT0, int QT1, int MT, int EPI>
-__global__ void __launch_bounds__(RG_THREADS) gemm_ring_kernel(GemmQArgs a, int S) {
+__global__ void __launch_bounds__(RG_THREADS) gemm_ring_kernel(GemmQArgs a, int sdbg) {
   kernarg_warm<sizeof(GemmQArgs) + sizeof(int)>();
+  const int S = sdbg & 0xffff, dbg = sdbg >> 16;  // split count | probe bits (AIOS_RING_DBG)
   constexpr int MP = 16 * MT;
   const int ntile = a.N / 128, total = ntile * S;
   const int L = xcd_remap(blockIdx.x, total);
@@ -254,11 +262,11 @@ __global__ void __launch_bounds__(RG_THREADS) gemm_ring_kernel(GemmQArgs a, int 
   float* is = nrm ? inv_s : nullptr;
   if constexpr (QT0 != QT1) {
     if (rg * 128 >= a.seg_n0[a.nseg - 1]) {
-      rg_body<QT1, MT, EPI>(a, S, rg, sp, is);
+      rg_body<QT1, MT, EPI>(a, S, rg, sp, is, dbg);
       return;
     }
   }
-  rg_body<QT0, MT, EPI>(a, S, rg, sp, is);
+  rg_body<QT0, MT, EPI>(a, S, rg, sp, is, dbg);
 }
 
 static int rg_env(const char* name, int dflt) {
@@ -278,7 +286,9 @@ static bool rg_launch(const GemmQArgs& a, hipStream_t st) {
   const size_t lds = (size_t)std::max(RgLayout<QT0, MT>::R * RgLayout<QT0, MT>::SLOT,
                                       RgLayout<QT1, MT>::R * RgLayout<QT1, MT>::SLOT);
   const dim3 grid(ntile * S), block(RG_THREADS);
-#define RG_GO(E) hipLaunchKernelGGL((gemm_ring_kernel<QT0, QT1, MT, E>), grid, block, lds, st, a, S)
+  static const int dbg = rg_env("AIOS_RING_DBG", 0) & 7;
+  const int sdbg = S | (dbg << 16);
+#define RG_GO(E) hipLaunchKernelGGL((gemm_ring_kernel<QT0, QT1, MT, E>), grid, block, lds, st, a, sdbg)
   switch (a.epi) {
     case GEPI_STORE: RG_GO(GEPI_STORE); break;
     case GEPI_QKV: RG_GO(GEPI_QKV); break;

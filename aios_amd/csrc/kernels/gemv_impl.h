@@ -17,6 +17,7 @@
 #pragma once
 #include <algorithm>
 
+#include "../comm.h"
 #include "../common.h"
 #include "../gemv.h"
 #include "../qweight.h"

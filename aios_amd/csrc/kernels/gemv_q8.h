@@ -574,6 +574,16 @@ __global__ void __launch_bounds__((q8_max_threads<U, PIPE>())) gemv_q8_rows(Gemv
     if (stamps) ts[i] = __builtin_amdgcn_s_memrealtime();
   };
   stamp(0);
+  // EPI_TP_RESID (batch 1, single format): the one-shot all-reduce of the O / down partials in the
+  // epilogue -- see lg_tp_fuse (gemv_lds.h) for the protocol.  Slot = workgroup; the wave's j-th
+  // pair goes to stage position j * nw + wave.  The slot's epoch is read here (ordered before use by
+  // the x-staging barrier) and written back at the end.
+  __shared__ uint32_t s_tpe;
+  const bool tpf = B == 1 && !MIXED && a.epi == EPI_TP_RESID;
+  if (tpf && threadIdx.x == 0) s_tpe = a.tp->fepoch[blockIdx.x] + 1;
+  int tpj = 0;          // pairs this wave has finished
+  float* tp_mine = nullptr;
+  size_t tp_half = 0;
 
   auto seg_idx = [&](int p, int& lrow) -> int {
     const int row = 2 * p;
@@ -679,7 +689,17 @@ __global__ void __launch_bounds__((q8_max_threads<U, PIPE>())) gemv_q8_rows(Gemv
       const float2 v = wave_sum_pair(acc[0][0], acc[1][0]);
       float2 rope = rope_w;
       if (a.epi == EPI_QKV && p != rope_p) rope = rope_of(p);  // a grid-stride pair after the first
-      if (lane == 0) gemv_epilogue1(a, a.row_base + 2 * p, v.x * s[0], v.y * s[0], rope, pos0, kv_blk0);
+      if (tpf) {
+        if (!tp_mine) {  // first pair: the epoch is in LDS (written before the staging barrier)
+          const uint32_t e = s_tpe;
+          tp_half = ((size_t)blockIdx.x * 2 + (e & 1u)) * TPF_CAP;
+          tp_mine = tpf_stage(a.tp, a.tp->rank) + tp_half;
+        }
+        if (lane == 0) *(float2*)(tp_mine + 2 * (tpj * nw + wave)) = make_float2(v.x * s[0], v.y * s[0]);
+        ++tpj;
+      } else if (lane == 0) {
+        gemv_epilogue1(a, a.row_base + 2 * p, v.x * s[0], v.y * s[0], rope, pos0, kv_blk0);
+      }
     } else {
 #pragma unroll
       for (int r = 0; r < GEMV_ROWS; ++r)
@@ -766,6 +786,46 @@ __global__ void __launch_bounds__((q8_max_threads<U, PIPE>())) gemv_q8_rows(Gemv
     __syncthreads();
     stamp(3);
     run(FmtTag<QT0>{}, wid, npairs, stride, buf);
+    if (tpf) {
+      // every wave's stage stores, then one flag per peer (wave 0), the bounded wait, and the
+      // rank-ordered sum of each of this wave's pairs into the residual
+      const ArDevCtx* c = a.tp;
+      const int rank = c->rank, world = c->world;
+      const uint32_t e = s_tpe;
+      const size_t half = ((size_t)blockIdx.x * 2 + (e & 1u)) * TPF_CAP;
+      // (uncached stage / flags: retired stores are visible to the peers -- no system-scope fence,
+      // which writes back the whole L2 and cost ~80 us per launch from every wave, see lg_tp_fuse)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (wave == 0) {
+        constexpr uint64_t TIMEOUT = 100ull * 1000 * 1000 * 3;  // 3 s of the 100 MHz wall clock
+        if (lane < world && lane != rank)
+          __hip_atomic_store(tpf_flags(c, lane) + blockIdx.x * AR_MAX_RANKS + rank, e, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_SYSTEM);
+        if (lane < world && lane != rank) {
+          uint32_t* f = tpf_flags(c, rank) + blockIdx.x * AR_MAX_RANKS + lane;
+          const uint64_t t0 = wall_clock64();
+          while ((int)(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - e) < 0) {
+            __builtin_amdgcn_s_sleep(2);
+            if (wall_clock64() - t0 > TIMEOUT) {
+              __hip_atomic_store(c->error, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+              break;
+            }
+          }
+        }
+      }
+      __syncthreads();
+      int j = 0;
+      for (int p = wid; p < npairs; p += stride, ++j) {
+        if (lane < 2) {  // lane 0: the pair's first row, lane 1: its second
+          const size_t o = half + 2 * (j * nw + wave) + lane;
+          float acc = 0.f;
+          for (int q = 0; q < world; ++q) acc += __builtin_nontemporal_load(tpf_stage(c, q) + o);
+          unsafeAtomicAdd(a.y + a.row_base + 2 * p + lane, acc);
+        }
+      }
+      if (threadIdx.x == 0) c->fepoch[blockIdx.x] = e;
+    }
   } else {
     // Mixed formats (Q4_K q/k + Q6_K v of a Q4_K_M QKV): the waves of EVERY workgroup are split
     // in proportion to the pair counts (Mistral: 10 Q4_K + 2 Q6_K pairs per 12-wave workgroup), so
@@ -886,6 +946,15 @@ void launch_q8_rows(const GemvArgs& a, size_t lds, hipStream_t st) {
     }
   }
   if (!blocks) blocks = std::min((npairs + nw - 1) / nw, cus * per_cu);
+  if (a.epi == EPI_TP_RESID) {
+    // fused all-reduce: at most grid_cap workgroups (every rank sharing a GPU resident at once),
+    // at most TPF_SLOTS, and each workgroup's pairs inside its stage slot (TPF_CAP values)
+    if (a.grid_cap > 0) blocks = std::min(blocks, a.grid_cap);
+    blocks = std::min(blocks, TPF_SLOTS);
+    auto per_wg = [&](int g) { return 2 * nw * ((npairs + g * nw - 1) / (g * nw)); };
+    while (per_wg(blocks) > TPF_CAP && blocks < TPF_SLOTS) ++blocks;
+    if (per_wg(blocks) > TPF_CAP) throw std::runtime_error("EPI_TP_RESID: output rows above the fused stage capacity");
+  }
   hipLaunchKernelGGL((gemv_q8_rows<QT0, QT1, B, U, PIPE>), dim3(blocks), dim3(nw * 64), lds, st, a);
 }
 

@@ -72,6 +72,8 @@ def create_comm(rank: int, world: int, device: int, cap_floats: int, group=None,
     per_gpu = ranks_per_gpu(world)
     if per_gpu > 1:  # every spinning workgroup of every rank must be resident on the shared GPU at once
         comm.call_wg = max(1, min(512, 1024 // per_gpu))
+        # ... including the O / down GEMV engines whose epilogue runs the all-reduce (EPI_TP_RESID)
+        comm.set_ranks_per_gpu(per_gpu)
     if world > 1:
         handles: List[Any] = [None] * world
         dist.all_gather_object(handles, comm.ipc_handle(), group=group)

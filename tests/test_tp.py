@@ -137,6 +137,9 @@ def test_tp_xgmi_allreduce_and_sharded_model(tmp_path, world, gemm_prefill, prom
     res = json.loads(out.read_text())
     assert not res["comm_error_flag"] and not res["comm_error_flag_model"]
     assert res["vocab_parallel"]
+    # the batch-1 O / down all-reduces run in the GEMV engine's epilogue (EPI_TP_RESID) by default,
+    # with the engine grid capped so that every rank sharing this GPU is resident at once
+    assert res["tp_fused"] == (os.environ.get("AIOS_TP_FUSE", "1") != "0")
     for e in res["allreduce"]:
         # fp32 staging: summation order only; bf16 two-shot staging: one bf16 rounding per partial
         tol = world * e["scale"] * 2.0 ** -8 if (e["bf16"] and e["two_shot"]) else 1e-4

@@ -160,6 +160,7 @@ def main():
     eng, comm = build_tp_engine(cfg, rank, world, dev, path=path, max_ctx=max_ctx, max_slots=nb, max_batch=nb,
                                 act_q8=False)
     res["vocab_parallel"] = bool(eng.vocab_parallel)
+    res["tp_fused"] = bool(getattr(eng, "tp_fused", False))  # C1 / C2 in the GEMV engine's epilogue
     prompt = [cfg.bos_id] + [(11 * i + 5) % (cfg.vocab_size - 3) + 3 for i in range(args.prompt_len - 1)]
     if rank == 0:
         tp = TPEngine(eng, comm)
