@@ -27,7 +27,14 @@ constexpr int RG_NL = 2;  // loader waves
 constexpr int RG_SMAX = 8;  // K slices at most (the engine sizes its split-K slabs for 8: gemm_skinny_ws_bytes)
 constexpr int RG_THREADS = (RG_RB + RG_NL) * 64;
 
-template <int QT, int MT>
+// XR (M <= 8): the workgroup's X slice (8 rows x <= 4096 k, bf16, row stride + 16 B against bank
+// conflicts) is staged ONCE into LDS ahead of the ring instead of riding in every slot -- at B = 8 the
+// per-slot X made each CU move 1.4x the weight bytes and the bare ring (no compute) took 16.7 us for
+// gate/up against the batch-1 engine's 13.5 (tools/gpu_r4_ringprobe.sh, profiles/lds_batched_r3.txt)
+constexpr int RG_XR_ROWS = 8, RG_XR_KMAX = 4096;
+constexpr int RG_XR_BYTES = (RG_XR_ROWS * (RG_XR_KMAX + 8) * 2 + 255) / 256 * 256;
+
+template <int QT, int MT, bool XR = false>
 struct RgLayout {
   static constexpr bool Q6 = QT == QT_Q6_K;
   static constexpr int MP = 16 * MT;
@@ -35,7 +42,7 @@ struct RgLayout {
   static constexpr int HI = Q6 ? 128 * 64 : 0;      // Q6_K: 8 B of high bits per chunk
   static constexpr int META = 128 * 16;             // Q4_K: scale/min record; Q6_K: 8 int8 scale pairs
   static constexpr int DQ = Q6 ? 512 : 0;           // Q6_K: the aligned dword holding the row's f16 d
-  static constexpr int XB = MP * 256 * 2;           // X rows, bf16
+  static constexpr int XB = XR ? 0 : MP * 256 * 2;  // X rows, bf16 (XR: resident, not in the slot)
   static constexpr int OFF_HI = CODES, OFF_META = OFF_HI + HI, OFF_D = OFF_META + META, OFF_X = OFF_D + DQ;
   static constexpr int SLOT = (OFF_X + XB + 255) / 256 * 256;
   // DMA instructions per slot: 1 KB each, Q6_K d as 4-byte pieces (256 B per instruction: a narrow
@@ -43,7 +50,7 @@ struct RgLayout {
   static constexpr int NI_CODES = 16, NI_HI = HI / 1024, NI_META = 2, NI_D = Q6 ? 2 : 0, NI_X = XB / 1024;
   static constexpr int TI = NI_CODES + NI_HI + NI_META + NI_D + NI_X;
   static constexpr int PL = (TI + RG_NL - 1) / RG_NL;  // per loader (exact: the vmcnt immediates)
-  static constexpr int R = std::min(6, (150 * 1024) / SLOT);
+  static constexpr int R = std::min(6, (150 * 1024 - (XR ? RG_XR_BYTES : 0)) / SLOT);
   static_assert(R >= 3 && (R - 2) * PL <= 63, "ring depth / vmcnt immediate");
 };
 
@@ -62,10 +69,10 @@ __device__ __forceinline__ void rg_vmcnt() {
 __device__ __forceinline__ int rg_xh(int m) { return (m ^ (m << 1)) & 15; }
 
 // Loader wave lw issues its PL instructions of slot s (superblock sb) into dst.
-template <int QT, int MT>
+template <int QT, int MT, bool XR>
 __device__ __forceinline__ void rg_dma_slot(const GemmQArgs& a, const QWeight& w, int row0, int nbk, int sb,
                                             uint8_t* dst, int lw) {
-  using L = RgLayout<QT, MT>;
+  using L = RgLayout<QT, MT, XR>;
   const int lane = threadIdx.x & 63;
   int issued = 0;
 #pragma unroll
@@ -115,12 +122,15 @@ __device__ __forceinline__ void rg_dma_slot(const GemmQArgs& a, const QWeight& w
   }
 }
 
-// one MFMA wave: the 2 chunk steps of slot s (chunks q, q + 4 of its rows) into acc
-template <int QT, int MT>
-// dbg (probes only, AIOS_RING_DBG): bit 0 = no dequant (raw code words as the MFMA operand), bit 1 = no MFMA
+// one MFMA wave: the 2 chunk steps of slot s (chunks q, q + 4 of its rows) into acc.
+// (Measured alternatives, profiles/ring_gemm_r4.txt: every LDS read of the slot issued up front and
+// waited for once -- neutral at B = 5 / 8, 2-3 % slower at B = 16 / 32; probe branches in the slot
+// loop -- even one around this call -- cost up to ~3 us of gate/up, so the anatomy knobs are gone.)
+// XR: X from the resident slice xr (row stride xst bf16, this superblock at k offset xk)
+template <int QT, int MT, bool XR>
 __device__ __forceinline__ void rg_compute_slot(const uint8_t* slot, int sb, int row0, int nbk, gf32x4 (&acc)[MT],
-                                                int dbg = 0) {
-  using L = RgLayout<QT, MT>;
+                                                const bf16_t* xr, int xst, int xk) {
+  using L = RgLayout<QT, MT, XR>;
   constexpr bool MB = QT == QT_Q4_K;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int rr = lane & 15, q = lane >> 4;
@@ -156,31 +166,28 @@ __device__ __forceinline__ void rg_compute_slot(const uint8_t* slot, int sb, int
       }
       const int run = i >> 1;
       uint32_t p[4];
-      if (dbg & 1) {
-        p[0] = w0; p[1] = w1; p[2] = w0 ^ w1; p[3] = w1 + w0;
-      } else {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) p[e] = pk_bf16(fmaf(sc[run], qv[2 * e], -of[run]), fmaf(sc[run], qv[2 * e + 1], -of[run]));
-      }
+      for (int e = 0; e < 4; ++e) p[e] = pk_bf16(fmaf(sc[run], qv[2 * e], -of[run]), fmaf(sc[run], qv[2 * e + 1], -of[run]));
       gbf16x8 wf;
       __builtin_memcpy(&wf, p, 16);
       const int kl = QFmt<QT>::chunk_k0(cc, i >> 1) + 8 * (i & 1);  // k of this fragment within the superblock
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
         const int m = 16 * mt + rr;
-        const uint4 xv = *(const uint4*)(xs + m * 256 + (kl ^ (rg_xh(m) << 3)));
+        uint4 xv;
+        if constexpr (XR) xv = *(const uint4*)(xr + (rr & 7) * xst + xk + kl);  // lanes 8-15: duplicate columns
+        else xv = *(const uint4*)(xs + m * 256 + (kl ^ (rg_xh(m) << 3)));
         gbf16x8 xf;
         __builtin_memcpy(&xf, &xv, 16);
-        if (dbg & 2) acc[mt][0] += __builtin_bit_cast(float, xv.x ^ p[0]);
-        else acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, xf, acc[mt], 0, 0, 0);
+        acc[mt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf, xf, acc[mt], 0, 0, 0);
       }
     }
   }
 }
 
-template <int QT, int MT, int EPI>
-__device__ __forceinline__ void rg_body(const GemmQArgs& a, int S, int rg, int sp, float* inv_s, int dbg) {
-  using L = RgLayout<QT, MT>;
+template <int QT, int MT, int EPI, bool XR>
+__device__ __forceinline__ void rg_body(const GemmQArgs& a, int S, int rg, int sp, float* inv_s) {
+  using L = RgLayout<QT, MT, XR>;
   extern __shared__ __attribute__((aligned(16))) uint8_t rg_smem[];
   __shared__ int last_flag;
   const int tid = threadIdx.x, wave = tid >> 6;
@@ -202,7 +209,9 @@ __device__ __forceinline__ void rg_body(const GemmQArgs& a, int S, int rg, int s
   const int nbk = a.K >> 8;
   const int sb0 = (int)((long)sp * nbk / S), sb1 = (int)((long)(sp + 1) * nbk / S);
   const int T = sb1 - sb0;  // ring steps (>= 1: S <= nbk)
-  uint8_t* ring = rg_smem;
+  uint8_t* ring = rg_smem + (XR ? RG_XR_BYTES : 0);
+  bf16_t* xr = (bf16_t*)rg_smem;
+  const int xst = T * 256 + 8;  // XR: resident row stride (bf16)
   gf32x4 acc[MT];
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) acc[mt] = gf32x4{0.f, 0.f, 0.f, 0.f};
@@ -211,13 +220,14 @@ __device__ __forceinline__ void rg_body(const GemmQArgs& a, int S, int rg, int s
     // ---- loaders: R - 1 slots in flight, a slot refilled one step after it was consumed
     const int lw = wave - RG_RB;
     const int npro = min(T, L::R - 1);
-    for (int t = 0; t < npro; ++t) rg_dma_slot<QT, MT>(a, w, row0, nbk, sb0 + t, ring + (size_t)t * L::SLOT, lw);
+    for (int t = 0; t < npro; ++t) rg_dma_slot<QT, MT, XR>(a, w, row0, nbk, sb0 + t, ring + (size_t)t * L::SLOT, lw);
     if (npro == L::R - 1) rg_vmcnt<(L::R - 2) * L::PL>();
     else rg_vmcnt<0>();
     rg_barrier();  // B1: slot 0 landed
     for (int t = 0; t < T; ++t) {
       if (t + L::R - 1 < T) {
-        rg_dma_slot<QT, MT>(a, w, row0, nbk, sb0 + t + L::R - 1, ring + (size_t)((t + L::R - 1) % L::R) * L::SLOT, lw);
+        rg_dma_slot<QT, MT, XR>(a, w, row0, nbk, sb0 + t + L::R - 1, ring + (size_t)((t + L::R - 1) % L::R) * L::SLOT,
+                                lw);
         rg_vmcnt<(L::R - 2) * L::PL>();  // slot t + 1 landed
       } else {
         rg_vmcnt<0>();
@@ -225,9 +235,31 @@ __device__ __forceinline__ void rg_body(const GemmQArgs& a, int S, int rg, int s
       rg_barrier();
     }
   } else {
+    if constexpr (XR) {
+      // the MFMA waves stage the X slice (rows past M re-read row M - 1) while the loaders' prologue
+      // slots are in flight: 8 x 16-B loads per thread per batch, then their LDS stores
+      const int nu = RG_XR_ROWS * T * 32;  // 16-B units
+      for (int u0 = tid; u0 < nu; u0 += 8 * RG_RB * 64) {
+        uint4 v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int u = min(u0 + j * RG_RB * 64, nu - 1), m = u / (T * 32), k8 = u - m * (T * 32);
+          v[j] = *(const uint4*)(a.A + (size_t)min(m, a.M - 1) * a.lda + sb0 * 256 + 8 * k8);
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int u = u0 + j * RG_RB * 64;
+          if (u < nu) {
+            const int m = u / (T * 32), k8 = u - m * (T * 32);
+            *(uint4*)(xr + m * xst + 8 * k8) = v[j];
+          }
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slice in LDS before B1
+    }
     rg_barrier();  // B1
     for (int t = 0; t < T; ++t) {
-      if (!(dbg & 4)) rg_compute_slot<QT, MT>(ring + (size_t)(t % L::R) * L::SLOT, sb0 + t, row0, nbk, acc, dbg);
+      rg_compute_slot<QT, MT, XR>(ring + (size_t)(t % L::R) * L::SLOT, sb0 + t, row0, nbk, acc, xr, xst, t * 256);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this slot's LDS reads done before it is refilled
       rg_barrier();
     }
@@ -239,10 +271,9 @@ __device__ __forceinline__ void rg_body(const GemmQArgs& a, int S, int rg, int s
 
 // one launch for every tile; mixed formats (Q4_K_M QKV: Q|K Q4_K, V Q6_K): the last segment's
 // tiles run the QT1 body
-template <int QT0, int QT1, int MT, int EPI>
-__global__ void __launch_bounds__(RG_THREADS) gemm_ring_kernel(GemmQArgs a, int sdbg) {
+template <int QT0, int QT1, int MT, int EPI, bool XR>
+__global__ void __launch_bounds__(RG_THREADS) gemm_ring_kernel(GemmQArgs a, int S) {
   kernarg_warm<sizeof(GemmQArgs) + sizeof(int)>();
-  const int S = sdbg & 0xffff, dbg = sdbg >> 16;  // split count | probe bits (AIOS_RING_DBG)
   constexpr int MP = 16 * MT;
   const int ntile = a.N / 128, total = ntile * S;
   const int L = xcd_remap(blockIdx.x, total);
@@ -262,11 +293,11 @@ __global__ void __launch_bounds__(RG_THREADS) gemm_ring_kernel(GemmQArgs a, int 
   float* is = nrm ? inv_s : nullptr;
   if constexpr (QT0 != QT1) {
     if (rg * 128 >= a.seg_n0[a.nseg - 1]) {
-      rg_body<QT1, MT, EPI>(a, S, rg, sp, is, dbg);
+      rg_body<QT1, MT, EPI, XR>(a, S, rg, sp, is);
       return;
     }
   }
-  rg_body<QT0, MT, EPI>(a, S, rg, sp, is, dbg);
+  rg_body<QT0, MT, EPI, XR>(a, S, rg, sp, is);
 }
 
 static int rg_env(const char* name, int dflt) {
@@ -274,7 +305,7 @@ static int rg_env(const char* name, int dflt) {
   return e ? std::atoi(e) : dflt;
 }
 
-template <int QT0, int QT1, int MT>
+template <int QT0, int QT1, int MT, bool XR>
 static bool rg_launch(const GemmQArgs& a, hipStream_t st) {
   const int ntile = a.N / 128;
   const int nbk = a.K / 256;
@@ -283,12 +314,12 @@ static bool rg_launch(const GemmQArgs& a, hipStream_t st) {
   int S = a.ksplit > 0 ? a.ksplit : std::max(1, cus / ntile);
   S = std::max(1, std::min({S, nbk, RG_SMAX}));
   if (S > 1 && (!a.ws || !a.cnt || a.cnt_len < ntile || a.ws_bytes < (size_t)S * 16 * MT * a.N * 4)) S = 1;
-  const size_t lds = (size_t)std::max(RgLayout<QT0, MT>::R * RgLayout<QT0, MT>::SLOT,
-                                      RgLayout<QT1, MT>::R * RgLayout<QT1, MT>::SLOT);
+  if (XR && ((nbk + S - 1) / S) * 256 > RG_XR_KMAX) return false;  // the resident slice must fit
+  const size_t lds = (size_t)(XR ? RG_XR_BYTES : 0) +
+                     (size_t)std::max(RgLayout<QT0, MT, XR>::R * RgLayout<QT0, MT, XR>::SLOT,
+                                      RgLayout<QT1, MT, XR>::R * RgLayout<QT1, MT, XR>::SLOT);
   const dim3 grid(ntile * S), block(RG_THREADS);
-  static const int dbg = rg_env("AIOS_RING_DBG", 0) & 7;
-  const int sdbg = S | (dbg << 16);
-#define RG_GO(E) hipLaunchKernelGGL((gemm_ring_kernel<QT0, QT1, MT, E>), grid, block, lds, st, a, sdbg)
+#define RG_GO(E) hipLaunchKernelGGL((gemm_ring_kernel<QT0, QT1, MT, E, XR>), grid, block, lds, st, a, S)
   switch (a.epi) {
     case GEPI_STORE: RG_GO(GEPI_STORE); break;
     case GEPI_QKV: RG_GO(GEPI_QKV); break;
@@ -316,16 +347,20 @@ bool launch_gemm_ring(const GemmQArgs& a, hipStream_t st) {
   const int qt0 = a.seg[0].qtype, qt1 = a.seg[a.nseg - 1].qtype;
   for (int s = 0; s + 1 < a.nseg; ++s)
     if (a.seg[s].qtype != qt0) return false;
-  auto go = [&](auto mt) {
+  auto go = [&](auto mt, auto xr) {
     constexpr int MT = decltype(mt)::value;
-    if (qt0 == QT_Q4_K && qt1 == QT_Q4_K) return rg_launch<QT_Q4_K, QT_Q4_K, MT>(a, st);
-    if (qt0 == QT_Q6_K && qt1 == QT_Q6_K) return rg_launch<QT_Q6_K, QT_Q6_K, MT>(a, st);
+    constexpr bool XR = decltype(xr)::value;
+    if (qt0 == QT_Q4_K && qt1 == QT_Q4_K) return rg_launch<QT_Q4_K, QT_Q4_K, MT, XR>(a, st);
+    if (qt0 == QT_Q6_K && qt1 == QT_Q6_K) return rg_launch<QT_Q6_K, QT_Q6_K, MT, XR>(a, st);
     if (qt0 == QT_Q4_K && qt1 == QT_Q6_K && (a.epi == GEPI_QKV || a.epi == GEPI_STORE))
-      return rg_launch<QT_Q4_K, QT_Q6_K, MT>(a, st);
+      return rg_launch<QT_Q4_K, QT_Q6_K, MT, XR>(a, st);
     return false;
   };
-  if (a.M <= 16) return go(std::integral_constant<int, 1>{});
-  return go(std::integral_constant<int, 2>{});
+  // AIOS_RING_XR (default 1): M <= 8 with the X slice resident in LDS (falls back when it does not fit)
+  static const int xr_on = rg_env("AIOS_RING_XR", 1);
+  if (a.M <= RG_XR_ROWS && xr_on && go(std::integral_constant<int, 1>{}, std::true_type{})) return true;
+  if (a.M <= 16) return go(std::integral_constant<int, 1>{}, std::false_type{});
+  return go(std::integral_constant<int, 2>{}, std::false_type{});
 }
 
 }  // namespace aios

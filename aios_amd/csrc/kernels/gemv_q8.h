@@ -376,6 +376,14 @@ __device__ __forceinline__ void q8_scales_bf(const RawChunk& r, int c, float* sc
   else q8_scales<QT>(r, c, sc, of);
 }
 
+// Microbenchmark bits of tune_dbg inside the dot loop (2: no dot work, 4: no x LDS reads, 8: no
+// scale decode) exist only in probe builds (-DAIOS_GEMV_PROBES=1): as runtime branches they cut the
+// loop body into basic blocks, and every x LDS read was then waited for right where it was issued
+// (the ring GEMM's hot loop measured the same effect, profiles/ring_gemm_r4.txt)
+#ifndef AIOS_GEMV_PROBES
+#define AIOS_GEMV_PROBES 0
+#endif
+
 template <int QT, int B, int U>
 __device__ __forceinline__ void q8_compute(const RawChunk (&raw)[U][GEMV_ROWS], int it, int nch, const int8_t* xq,
                                            const float2* ms, float (&acc)[GEMV_ROWS][B], int dbg = 0) {
@@ -390,7 +398,7 @@ __device__ __forceinline__ void q8_compute(const RawChunk (&raw)[U][GEMV_ROWS], 
     float sc[GEMV_ROWS][R], of[GEMV_ROWS][R];
 #pragma unroll
     for (int r = 0; r < GEMV_ROWS; ++r) {
-      if (dbg & 8) {  // microbenchmark: scale decode skipped
+      if (AIOS_GEMV_PROBES && (dbg & 8)) {  // microbenchmark: scale decode skipped
 #pragma unroll
         for (int rr = 0; rr < R; ++rr) { sc[r][rr] = __int_as_float(raw[u][r].b.y | 0x3f000000); of[r][rr] = 0.5f; }
       } else {
@@ -401,7 +409,7 @@ __device__ __forceinline__ void q8_compute(const RawChunk (&raw)[U][GEMV_ROWS], 
     for (int b = 0; b < B; ++b) {
       int xv[8];
       const int8_t* xc = xq + ((size_t)b * nch + c) * W;
-      if (dbg & 4) {  // microbenchmark: x LDS reads skipped
+      if (AIOS_GEMV_PROBES && (dbg & 4)) {  // microbenchmark: x LDS reads skipped
 #pragma unroll
         for (int i = 0; i < 8; ++i) xv[i] = c * 0x01010101 + i;
       } else if constexpr (W == 32) {
@@ -419,7 +427,7 @@ __device__ __forceinline__ void q8_compute(const RawChunk (&raw)[U][GEMV_ROWS], 
       const float2* mp = ms + ((size_t)b * nch + c) * R;
 #pragma unroll
       for (int rr = 0; rr < R; ++rr) {
-        m[rr] = (dbg & 4) ? make_float2(1.f, (float)c) : mp[rr];
+        m[rr] = (AIOS_GEMV_PROBES && (dbg & 4)) ? make_float2(1.f, (float)c) : mp[rr];
         if (!valid) m[rr] = make_float2(0.f, 0.f);
       }
 #pragma unroll
@@ -660,7 +668,7 @@ __global__ void __launch_bounds__((q8_max_threads<U, PIPE>())) gemv_q8_rows(Gemv
     for (int b = 0; b < B; ++b) acc[r][b] = 0.f;
   auto compute = [&](auto tag, int it, const RawChunk (&cur)[U][GEMV_ROWS]) __attribute__((always_inline)) {
     constexpr int QT = decltype(tag)::value;
-    if (a.tune_dbg & 2) {
+    if (AIOS_GEMV_PROBES && (a.tune_dbg & 2)) {
 #pragma unroll
       for (int u = 0; u < U; ++u)
 #pragma unroll
