@@ -646,7 +646,7 @@ __global__ void __launch_bounds__(LG_THREADS) gemv_lds_b1(GemvArgs a, CuPlan pl)
         for (int t = 0; t < T; ++t) {
           if (t * L::NGS + wave * GPW < ngroups) {
             const uint8_t* slot = ring + (size_t)(t % LG_R) * L::slot_bytes;
-            if (a.tune_dbg & LG_DBG_RING) { lg_barrier(); continue; }
+            if (AIOS_GEMV_PROBES && (a.tune_dbg & LG_DBG_RING)) { lg_barrier(); continue; }  // probe builds only
             const uint4 a0 = *(const uint4*)(slot + L::off(0) + kk * 1024 + p * 32);
             const uint4 a1 = *(const uint4*)(slot + L::off(0) + kk * 1024 + p * 32 + 16);
             const uint4 mt = *(const uint4*)(slot + L::off(1) + kk * 128 + (p >> 2) * 16);
