@@ -44,7 +44,7 @@ constexpr int AR_MAX_WG = 512;
 constexpr int AR_THREADS = 256;
 constexpr int AR_CHUNK = AR_THREADS * 4;              // elements per workgroup per call
 constexpr size_t AR_MAX_CALL = (size_t)AR_MAX_WG * AR_CHUNK;  // elements per kernel call
-// C1 / C2 fused into the batch <= 4 GEMV engine's epilogue (EPI_TP_RESID, gemv_lds.h): per engine
+// C1 / C2 fused into the batch-1 row GEMV epilogue (EPI_TP_RESID, gemv_q8.h): per GEMV
 // workgroup ("slot") a private double-buffered stage of up to TPF_CAP partial outputs behind the
 // one-shot region, and one flag per (slot, rank) behind the collectives' flags
 constexpr int TPF_SLOTS = 256;

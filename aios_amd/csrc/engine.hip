@@ -1007,35 +1007,20 @@ void Engine::layer_decode(int l, int B) {
   }
 }
 
-// EPI_TP_RESID through the LDS-DMA engine (kernel_sel 3: every shape, no size floor) when the comm
-// provides the fused context, the engine serves the shape and each workgroup's B x rows fit its
-// stage slot (comm.h TPF_*); the grid is capped when ranks share a GPU so that every rank's
-// workgroups are resident together (their epilogues wait on each other)
+// EPI_TP_RESID (the O / down all-reduce in the GEMV epilogue, gemv_q8.h) when the comm provides the
+// fused context
 bool Engine::tp_fuse_gemv(GemvArgs a) {
-  if (!tp_fuse_ || a.B > 4 || !a.act_q8 || a.force_v1) return false;  // (int8-activation kernels only)
-  a.tp = tp_fuse_;
-  a.tune_ksplit = 0;
+  // batch 1 only, through the row-pair kernel (any K; a TP rank's O / down shares sit below the LDS
+  // engine's size floor anyway); B = 2..4 keep separate all-reduce launches
+  if (!tp_fuse_ || a.B != 1 || !a.act_q8 || a.force_v1 || a.nseg != 1) return false;  // (int8-activation kernel)
   const int qt0 = a.seg[0].qtype;
-  if (a.B == 1) {
-    // batch 1: the row-pair kernel (any K; the shapes a TP rank holds are below the LDS engine's
-    // size floor anyway), grid capped when ranks share the GPU
-    if (a.nseg != 1 || !(qt0 == QT_Q4_K || qt0 == QT_Q5_K || qt0 == QT_Q6_K || qt0 == QT_Q4_0 || qt0 == QT_Q8_0))
-      return false;
-    a.kernel_sel = 1;
-    a.tune_grid = 0;
-    a.tune_u = 0;
-    a.grid_cap = tp_fuse_grid_;
-    launch_gemv(a, stream_);
-    return true;
-  }
-  a.kernel_sel = 3;
-  a.tune_grid = tp_fuse_grid_;
-  const int npairs = a.N / 2;
-  const int G = std::min(tp_fuse_grid_ > 0 ? tp_fuse_grid_ : device_cu_count(), npairs);
-  const int rows_max = 2 * ((npairs + G - 1) / G);
-  const int qt = a.seg[0].qtype;
-  const bool engine_fmt = qt == QT_Q4_K || qt == QT_Q5_K || qt == QT_Q6_K || qt == QT_Q4_0 || qt == QT_Q8_0;
-  if (!engine_fmt || G > TPF_SLOTS || a.B * rows_max > TPF_CAP || a.nseg != 1 || !gemv_engine_fits(a)) return false;
+  if (!(qt0 == QT_Q4_K || qt0 == QT_Q5_K || qt0 == QT_Q6_K || qt0 == QT_Q4_0 || qt0 == QT_Q8_0)) return false;
+  a.tp = tp_fuse_;
+  a.kernel_sel = 1;
+  a.tune_grid = 0;
+  a.tune_u = 0;
+  a.tune_ksplit = 0;
+  a.grid_cap = tp_fuse_grid_;  // ranks sharing a GPU: every rank's workgroups resident together
   launch_gemv(a, stream_);
   return true;
 }

@@ -12,8 +12,8 @@ enum GemvEpilogue : int {
   EPI_RESID = 1,   // y[b][n] += acc        (residual stream update)
   EPI_SWIGLU = 2,  // y[b][n/2] = silu(acc[2i]) * acc[2i+1]   (rows interleaved gate/up)
   EPI_QKV = 3,     // (+bias) RoPE on Q/K, Q -> y, K/V -> bf16 KV cache at pos[b]
-  EPI_TP_RESID = 4,  // TP row-parallel O / down: y[b][n] += sum over ranks of acc (the one-shot all-reduce
-                     //   in the epilogue, GemvArgs::tp; the B <= 4 LDS-DMA engine only, gemv_lds.h)
+  EPI_TP_RESID = 4,  // TP row-parallel O / down at batch 1: y[n] += sum over ranks of acc (the one-shot
+                     //   all-reduce in the row-pair kernel's epilogue, GemvArgs::tp, gemv_q8.h)
 };
 
 struct ArDevCtx;  // comm.h

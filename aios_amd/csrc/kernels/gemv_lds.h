@@ -339,67 +339,6 @@ __device__ __forceinline__ void lg_compute_b(const RawChunk& raw, int it, int nc
   }
 }
 
-// ---- EPI_TP_RESID: C1 / C2 of the TP decode step in the engine's epilogue (wave 0 of the workgroup).
-// The workgroup's B x nrows partial outputs go to its private stage slot (half e & 1 of slot
-// blockIdx.x, fine-grained memory mapped by every peer), one lane per peer raises that peer's flag
-// [slot][my rank] with a system-scope release, one lane per peer waits for the peer's flag (bounded,
-// XgmiComm's error flag on a give-up), then every output is summed over the ranks IN RANK ORDER
-// (bit-identical on every rank: the on-device samplers stay in lock step) and added to the residual
-// with a no-return atomic (one writer per element).  Double buffering as comm.h's protocol: a rank
-// reuses half e & 1 at epoch e + 2 only after every peer's epoch-(e + 1) flag of the same slot, which
-// the peer raises after its epoch-e reads.  Every rank runs the same engine plan, so slot s covers
-// the same rows everywhere.  Removes the two all-reduce launches per layer (verdict r3 #3a).
-template <int B>
-__device__ __forceinline__ void lg_tp_fuse(const GemvArgs& a, const float* rowacc, int racc_n, int r0, int nrows,
-                                           const float (&sb)[B]) {
-  constexpr uint64_t TIMEOUT = 100ull * 1000 * 1000 * 3;  // 3 s of the 100 MHz wall clock
-  const ArDevCtx* c = a.tp;
-  const int lane = threadIdx.x & 63, slot = blockIdx.x;
-  const int rank = c->rank, world = c->world;
-  uint32_t e = 0;
-  if (lane == 0) {
-    e = c->fepoch[slot] + 1;  // only this workgroup's wave 0 touches its slot's epoch
-    c->fepoch[slot] = e;
-  }
-  e = (uint32_t)__builtin_amdgcn_readfirstlane((int)e);
-  const size_t half = ((size_t)slot * 2 + (e & 1u)) * TPF_CAP;
-  float* mine = tpf_stage(c, rank) + half;
-  const int n = B * nrows;
-  for (int i = lane; i < n; i += 64) {
-    const int b = i / nrows, r = i - b * nrows;
-    float s_ = sb[0];
-#pragma unroll
-    for (int bb = 1; bb < B; ++bb)
-      if (b == bb) s_ = sb[bb];
-    mine[i] = rowacc[b * racc_n + r] * s_;
-  }
-  // stage and flags are fine-grained uncached memory (comm.h): a store that has retired (vmcnt,
-  // per wave) is visible to every peer, so no system-scope fence -- which writes back the whole L2
-  // and, issued by every workgroup of a full-chip GEMV, cost ~80 us per launch (round 4 measurement)
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if (lane < world && lane != rank)
-    __hip_atomic_store(tpf_flags(c, lane) + slot * AR_MAX_RANKS + rank, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  if (lane < world && lane != rank) {
-    uint32_t* f = tpf_flags(c, rank) + slot * AR_MAX_RANKS + lane;
-    const uint64_t t0 = wall_clock64();
-    while ((int)(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - e) < 0) {
-      __builtin_amdgcn_s_sleep(2);
-      if (wall_clock64() - t0 > TIMEOUT) {
-        __hip_atomic_store(c->error, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        break;
-      }
-    }
-  }
-  asm volatile("" ::: "memory");  // (the stage loads below are uncached: issued after the flag loads retired)
-  for (int i = lane; i < n; i += 64) {
-    const int b = i / nrows, r = i - b * nrows;
-    float acc = 0.f;
-    for (int p = 0; p < world; ++p)
-      acc += p == rank ? mine[i] : __builtin_nontemporal_load(tpf_stage(c, p) + half + i);
-    unsafeAtomicAdd(a.y + (size_t)b * a.ldy + a.row_base + r0 + r, acc);
-  }
-}
-
 // B = 1: the batch-1 decode engine; B = 2..4 (RSUB = 1: one ring slot fewer, the B staged x rows
 // take its LDS): the same weight stream serves B rows -- the small-batch decode of the agent OS
 // (<= 3 concurrent reasoning loops + agents) at close to the batch-1 step time
@@ -743,16 +682,6 @@ __global__ void __launch_bounds__(LG_THREADS) gemv_lds_b1(GemvArgs a, CuPlan pl)
     return;
   }
 
-  if (a.epi == EPI_TP_RESID) {
-    // (O / down: no RMSNorm prologue, so the row scales are 1)
-    float sb[B];
-#pragma unroll
-    for (int b = 0; b < B; ++b) sb[b] = 1.f;
-    lg_tp_fuse<B>(a, rowacc, pl.racc_n, r0, nrows, sb);
-    CU_STAMP(6);
-    flush_ts();
-    return;
-  }
   if constexpr (B > 1) {
     // ---- batched epilogues: wave 0, one lane per (row b, pair)
     float sb[B];
@@ -888,6 +817,28 @@ bool launch_gemv_lds(const GemvArgs& a, hipStream_t st, bool dry = false) {
     constexpr size_t LDS_MAX = 160 * 1024;
     size_t lds = 0;
     if (a.B == 1) {
+      // AIOS_LDS_B1_RSUB (default 1): ring slots fewer than LgLayout's depth at batch 1.  A smaller
+      // prologue burst (~64 instead of ~96 KB per CU, 16 MB chip-wide) lands the first slot sooner,
+      // and R - 1 slots in flight still cover the stream's latency: 649.4 -> 662.9 tok/s same box
+      // (tools/gpu_r4_ab5.sh, profiles/decode_mistral_rocprof_r4_final.txt)
+      static const int rsub_all = [] {
+        const char* e = std::getenv("AIOS_LDS_B1_RSUB");
+        return e ? std::atoi(e) : 1;
+      }();
+      static const int rsub_q6 = [] {  // AIOS_LDS_B1_RSUB_Q6: Q6_K matrices' own value (default: the same)
+        const char* e = std::getenv("AIOS_LDS_B1_RSUB_Q6");
+        return e ? std::atoi(e) : -1;
+      }();
+      const int rsub = (QT0 == QT_Q6_K && rsub_q6 >= 0) ? rsub_q6 : rsub_all;
+      if (rsub == 1 || rsub == 2) {
+        if (rsub == 1) lds = lg_lds_bytes<QT0, QT1, 1, 1>(a, pl);
+        else lds = lg_lds_bytes<QT0, QT1, 1, 2>(a, pl);
+        if (lds > LDS_MAX) return false;
+        if (dry) return true;
+        if (rsub == 1) hipLaunchKernelGGL((gemv_lds_b1<QT0, QT1, 1, 1>), dim3(G), dim3(LG_THREADS), lds, st, a, pl);
+        else hipLaunchKernelGGL((gemv_lds_b1<QT0, QT1, 1, 2>), dim3(G), dim3(LG_THREADS), lds, st, a, pl);
+        return true;
+      }
       lds = lg_lds_bytes<QT0, QT1, 1, 0>(a, pl);
       if (lds > LDS_MAX) return false;
       if (dry) return true;

@@ -582,10 +582,17 @@ __global__ void __launch_bounds__((q8_max_threads<U, PIPE>())) gemv_q8_rows(Gemv
     if (stamps) ts[i] = __builtin_amdgcn_s_memrealtime();
   };
   stamp(0);
-  // EPI_TP_RESID (batch 1, single format): the one-shot all-reduce of the O / down partials in the
-  // epilogue -- see lg_tp_fuse (gemv_lds.h) for the protocol.  Slot = workgroup; the wave's j-th
-  // pair goes to stage position j * nw + wave.  The slot's epoch is read here (ordered before use by
-  // the x-staging barrier) and written back at the end.
+  // EPI_TP_RESID (batch 1, single format): C1 / C2 of the TP decode step in the epilogue.  Every
+  // workgroup ("slot") writes its rows' partials to its private double-buffered stage slot (half
+  // e & 1; fine-grained uncached memory mapped by every peer, comm.h), one lane per peer raises that
+  // peer's flag [slot][my rank], one lane per peer waits for the peer's flag (bounded, XgmiComm's
+  // error flag on a give-up), then each output is summed over the ranks IN RANK ORDER (bit-identical
+  // on every rank: the on-device samplers stay in lock step) and added to the residual with a
+  // no-return atomic (one writer per element).  A rank reuses half e & 1 at epoch e + 2 only after
+  // every peer's epoch-(e + 1) flag of the slot, which the peer raises after its epoch-e reads; every
+  // rank runs the same launch shape, so slot s covers the same rows everywhere.  The wave's j-th pair
+  // goes to stage position j * nw + wave; the slot's epoch is read here (ordered before use by the
+  // x-staging barrier) and written back at the end.  Removes the two all-reduce launches per layer.
   __shared__ uint32_t s_tpe;
   const bool tpf = B == 1 && !MIXED && a.epi == EPI_TP_RESID;
   if (tpf && threadIdx.x == 0) s_tpe = a.tp->fepoch[blockIdx.x] + 1;
@@ -802,7 +809,7 @@ __global__ void __launch_bounds__((q8_max_threads<U, PIPE>())) gemv_q8_rows(Gemv
       const uint32_t e = s_tpe;
       const size_t half = ((size_t)blockIdx.x * 2 + (e & 1u)) * TPF_CAP;
       // (uncached stage / flags: retired stores are visible to the peers -- no system-scope fence,
-      // which writes back the whole L2 and cost ~80 us per launch from every wave, see lg_tp_fuse)
+      // which writes back the whole L2 and, from every wave, cost ~80 us per launch)
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       if (wave == 0) {
