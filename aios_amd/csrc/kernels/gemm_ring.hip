@@ -32,6 +32,9 @@ constexpr int RG_THREADS = (RG_RB + RG_NL) * 64;
 // per-slot X made each CU move 1.4x the weight bytes and the bare ring (no compute) took 16.7 us for
 // gate/up against the batch-1 engine's 13.5 (tools/gpu_r4_ringprobe.sh, profiles/lds_batched_r3.txt)
 constexpr int RG_XR_ROWS = 8, RG_XR_KMAX = 4096;
+#ifndef RG_RSUB
+#define RG_RSUB 1
+#endif
 constexpr int RG_XR_BYTES = (RG_XR_ROWS * (RG_XR_KMAX + 8) * 2 + 255) / 256 * 256;
 
 template <int QT, int MT, bool XR = false>
@@ -50,7 +53,10 @@ struct RgLayout {
   static constexpr int NI_CODES = 16, NI_HI = HI / 1024, NI_META = 2, NI_D = Q6 ? 2 : 0, NI_X = XB / 1024;
   static constexpr int TI = NI_CODES + NI_HI + NI_META + NI_D + NI_X;
   static constexpr int PL = (TI + RG_NL - 1) / RG_NL;  // per loader (exact: the vmcnt immediates)
-  static constexpr int R = std::min(6, (150 * 1024 - (XR ? RG_XR_BYTES : 0)) / SLOT);
+  // (one slot below what fits: a smaller chip-wide prologue burst lands the first slot sooner, as
+  // measured for the batch-1 engine, profiles/decode_mistral_rocprof_r4_final.txt)
+  static constexpr int RFIT = std::min(6, (150 * 1024 - (XR ? RG_XR_BYTES : 0)) / SLOT);
+  static constexpr int R = RFIT >= 4 ? RFIT - RG_RSUB : RFIT;
   static_assert(R >= 3 && (R - 2) * PL <= 63, "ring depth / vmcnt immediate");
 };
 
