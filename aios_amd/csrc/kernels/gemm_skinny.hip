@@ -67,11 +67,9 @@ __device__ __forceinline__ void sk_body(const GemmQArgs& a, int S) {
   // probes (tools/skinny_probe.py): 0 start, 1 prologue loads issued, 2 first X chunk staged,
   // 3 main loop done, 4 done (a slice that handed its slab to the tile's last arriver), 5 done
   // (the epilogue written)
-  unsigned long long ts[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  auto stamp = [&](int i) __attribute__((always_inline)) { ts[i] = __builtin_amdgcn_s_memrealtime(); };
-  auto flush = [&]() __attribute__((always_inline)) {
-    if (a.dbg_ts && threadIdx.x == 0)
-      for (int i = 0; i < 8; ++i) a.dbg_ts[(size_t)blockIdx.x * 8 + i] = ts[i];
+  // (stored as taken, probe launches only: no stamp state live through the kernel)
+  auto stamp = [&](int i) __attribute__((always_inline)) {
+    if (a.dbg_ts && threadIdx.x == 0) a.dbg_ts[(size_t)blockIdx.x * 8 + i] = __builtin_amdgcn_s_memrealtime();
   };
   stamp(0);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -248,7 +246,6 @@ __device__ __forceinline__ void sk_body(const GemmQArgs& a, int S) {
   stamp(3);
   const bool wrote = sk_epilogue<RB, MT, EPI>(a, acc, n0, rg, sp, S, ntile, inv_s, nrm, (float*)&sk_xs[0], last_flag);
   if (wrote) stamp(5); else stamp(4);  // 4: a split-K slice that was not its tile's last arriver
-  flush();
 }
 
 // One launch for every tile: with mixed formats (Q4_K_M: Q|K Q4_K, V Q6_K) the tiles of the last

@@ -575,11 +575,13 @@ __global__ void __launch_bounds__((q8_max_threads<U, PIPE>())) gemv_q8_rows(Gemv
   const int wid = __builtin_amdgcn_readfirstlane(blockIdx.x * nw + wave);  // wave-uniform -> SGPR
   // probes (tools/gemv_cu_probe.py): phase stamps of the first and last wave of every workgroup --
   // 0 start, 1 first weight loads issued, 2 x staged, 3 barrier passed, 4 first pair computed, 5 done
-  unsigned long long ts[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  // (probe launches only: a wave-uniform branch on the kernarg, no s_memrealtime in production)
+  // (probe launches only: a wave-uniform branch on the kernarg; each stamp is stored when taken --
+  // an array held to the end kept 16 SGPRs live through the kernel and the row GEMVs spilled SGPRs)
   const bool stamps = a.dbg_ts != nullptr;
+  bool stamped4 = false;
   auto stamp = [&](int i) __attribute__((always_inline)) {
-    if (stamps) ts[i] = __builtin_amdgcn_s_memrealtime();
+    if (stamps && lane == 0 && (wave == 0 || wave == nw - 1))
+      a.dbg_ts[((size_t)blockIdx.x * 2 + (wave != 0)) * 8 + i] = __builtin_amdgcn_s_memrealtime();
   };
   stamp(0);
   // EPI_TP_RESID (batch 1, single format): C1 / C2 of the TP decode step in the epilogue.  Every
@@ -699,7 +701,10 @@ __global__ void __launch_bounds__((q8_max_threads<U, PIPE>())) gemv_q8_rows(Gemv
         s[b] = rsqrtf(t / (float)a.K + a.eps);
       }
     }
-    if (stamps && !ts[4]) stamp(4);
+    if (stamps && !stamped4) {
+      stamp(4);
+      stamped4 = true;
+    }
     if constexpr (B == 1) {
       const float2 v = wave_sum_pair(acc[0][0], acc[1][0]);
       float2 rope = rope_w;
@@ -893,8 +898,6 @@ __global__ void __launch_bounds__((q8_max_threads<U, PIPE>())) gemv_q8_rows(Gemv
     }
   }
   stamp(5);
-  if (a.dbg_ts && lane == 0 && (wave == 0 || wave == nw - 1))
-    for (int i = 0; i < 8; ++i) a.dbg_ts[((size_t)blockIdx.x * 2 + (wave != 0)) * 8 + i] = ts[i];
 }
 
 template <int QT0, int QT1, int B>
