@@ -1,6 +1,6 @@
 #!/usr/bin/env bash
 # round-4 validation: every GPU test, the driver's default bench (all secondaries), B=1 against the
-# cmp_r4a build on the same box, and the B=1 rocprof decode profile
+# cmp_r4c build on the same box, and the B=1 rocprof decode profile
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
@@ -12,7 +12,7 @@ tail -1 gpurun_out/t_final.log
 timeout -k 10 900 python bench.py > gpurun_out/bench_final.log 2>&1 || { tail -20 gpurun_out/bench_final.log; exit 1; }
 grep -v amdgpu.ids gpurun_out/bench_final.log | tail -1 | cut -c1-400
 for r in 0 1; do
-  for d in cmp_r4a .; do
+  for d in cmp_r4c .; do
     echo -n "B1 $d "; (cd $d && timeout -k 10 300 python bench.py --steps 256 --warmup 16 --no-secondary 2>/dev/null | j) || exit 1
   done
 done
