@@ -188,13 +188,12 @@ __device__ __forceinline__ void cu_qkv_epilogue(const GemvArgs& a, int grow, flo
   }
 }
 
-// probes (tools/gemv_cu_probe.py): phase timestamps of the first and the last wave (`stamp_last`,
-// declared by the kernel) of every workgroup, stored as they are taken -- an array of stamps held to
-// the end kept 16 SGPRs live through the whole kernel (round 4: the row GEMV's SGPR spills)
-#define CU_STAMP(i)                                                                                 \
-  do {                                                                                              \
-    if (a.dbg_ts && (threadIdx.x & 63) == 0 && ((threadIdx.x >> 6) == 0 || (threadIdx.x >> 6) == stamp_last)) \
-      a.dbg_ts[((size_t)blockIdx.x * 2 + ((threadIdx.x >> 6) != 0)) * 8 + (i)] = __builtin_amdgcn_s_memrealtime(); \
+// probes (tools/gemv_cu_probe.py): phase timestamps of waves 0 and 15 of every workgroup, held in
+// `ts` and flushed at the end (the engine has SGPRs to spare: stamps stored as taken -- what the row
+// GEMV now does -- measured 0.2-0.6 us slower per engine launch, profiles/decode_tinyllama_rocprof_r4.txt)
+#define CU_STAMP(i)                                                   \
+  do {                                                                \
+    if (a.dbg_ts) ts[i] = __builtin_amdgcn_s_memrealtime();           \
   } while (0)
 
 // f(integral_constant<I>) for the run-time n in [0, N]: every case is a fully static body
@@ -215,8 +214,8 @@ __device__ __forceinline__ void cu_dispatch(int n, F&& f) {
 // issuing its loads and computing them.  Row sums land in rowacc.
 template <int QT, int QTX, int DMAX>
 __device__ __forceinline__ void cu_body(const GemvArgs& a, int r0, int j0, int j1, int nit, int nch, float* red,
-                                        float* rowacc, float2* ms, int8_t* xq, float2& rope) {
-  constexpr int stamp_last = CU_WAVES - 1;
+                                        float* rowacc, float2* ms, int8_t* xq, float2& rope,
+                                        unsigned long long* ts) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   auto load_item = [&](int row, int it, RawChunk& r) __attribute__((always_inline)) {
     int s = 0;
@@ -286,8 +285,12 @@ __global__ void __launch_bounds__(CU_THREADS) gemv_cu_b1(GemvArgs a, CuPlan pl) 
   const int nit = (nch + 63) >> 6;
   const int npairs = a.N >> 1;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  constexpr int stamp_last = CU_WAVES - 1;
+  unsigned long long ts[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   CU_STAMP(0);
+  auto flush_ts = [&]() {
+    if (a.dbg_ts && lane == 0 && (wave == 0 || wave == CU_WAVES - 1))
+      for (int i = 0; i < 8; ++i) a.dbg_ts[((size_t)blockIdx.x * 2 + (wave != 0)) * 8 + i] = ts[i];
+  };
 
   // ---- this workgroup's pair range
   const int g = blockIdx.x;
@@ -318,13 +321,16 @@ __global__ void __launch_bounds__(CU_THREADS) gemv_cu_b1(GemvArgs a, CuPlan pl) 
   for (int i = threadIdx.x; i < nrows; i += CU_THREADS) rowacc[i] = 0.f;  // ordered by q8_stage's barrier
 
   float2 rope = make_float2(1.f, 0.f);
-  if (!fmt1) cu_body<QT0, QT0, D>(a, r0, j0, j1, nit, nch, red, rowacc, ms, xq, rope);
-  else cu_body<QT1, QT0, D>(a, r0, j0, j1, nit, nch, red, rowacc, ms, xq, rope);
+  if (!fmt1) cu_body<QT0, QT0, D>(a, r0, j0, j1, nit, nch, red, rowacc, ms, xq, rope, ts);
+  else cu_body<QT1, QT0, D>(a, r0, j0, j1, nit, nch, red, rowacc, ms, xq, rope, ts);
   __syncthreads();
   CU_STAMP(5);
 
   // ---- pair epilogues: wave 0, one lane per pair (a second pass for > 64 pairs)
-  if (wave != 0) return;
+  if (wave != 0) {
+    flush_ts();
+    return;
+  }
   float s = 1.f;
   if (a.norm_w) {
     float t = 0.f;
@@ -360,6 +366,7 @@ __global__ void __launch_bounds__(CU_THREADS) gemv_cu_b1(GemvArgs a, CuPlan pl) 
     }
   }
   CU_STAMP(6);
+  flush_ts();
 }
 
 template <int QT0, int QT1>

@@ -355,7 +355,7 @@ __global__ void __launch_bounds__(LG_THREADS) gemv_lds_b1(GemvArgs a, CuPlan pl)
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const bool loader = wave >= LG_NG;
-  constexpr int stamp_last = LG_NG - 1;
+  unsigned long long ts[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   CU_STAMP(0);
 
   // ---- this workgroup's pair range (as gemv_cu_b1)
@@ -673,7 +673,14 @@ __global__ void __launch_bounds__(LG_THREADS) gemv_lds_b1(GemvArgs a, CuPlan pl)
   }
   if (!fmt1) consumer_path(FmtTag<QT0>{}, rope, pos0, kv_blk0);
   else consumer_path(FmtTag<QT1>{}, rope, pos0, kv_blk0);
-  if (wave != 0) return;
+  auto flush_ts = [&]() {
+    if (a.dbg_ts && lane == 0 && (wave == 0 || wave == LG_NG - 1))
+      for (int i = 0; i < 8; ++i) a.dbg_ts[((size_t)blockIdx.x * 2 + (wave != 0)) * 8 + i] = ts[i];
+  };
+  if (wave != 0) {
+    flush_ts();
+    return;
+  }
 
   if constexpr (B > 1) {
     // ---- batched epilogues: wave 0, one lane per (row b, pair)
@@ -699,6 +706,7 @@ __global__ void __launch_bounds__(LG_THREADS) gemv_lds_b1(GemvArgs a, CuPlan pl)
                     rowacc[b * pl.racc_n + 2 * p + 1] * s_);
     }
     CU_STAMP(6);
+    flush_ts();
     return;
   }
   // ---- pair epilogues: wave 0, one lane per pair
@@ -732,6 +740,7 @@ __global__ void __launch_bounds__(LG_THREADS) gemv_lds_b1(GemvArgs a, CuPlan pl)
     }
   }
   CU_STAMP(6);
+  flush_ts();
 }
 
 template <int QT>
