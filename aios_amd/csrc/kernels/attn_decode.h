@@ -8,6 +8,10 @@
 #include <algorithm>
 #include <cstdlib>
 
+#ifndef AIOS_ATTN_PROBES
+#define AIOS_ATTN_PROBES 0
+#endif
+
 namespace aios {
 
 __device__ __forceinline__ void st_wt(float* p, float v) {
@@ -105,8 +109,10 @@ __device__ __forceinline__ void attn_core(const AttnDecodeArgs& a, int sp, int k
   // probe stamps (a.ts, null in production: one scalar compare per site): 0 entry, 1 seq_len known,
   // 2 first pass computed (its K/V landed), 3 waves merged, 4 partial published + ticket, 5 (m, l)
   // weights ready (last arriver), 6 done
+  // (probe builds only, -DAIOS_ATTN_PROBES=1 / AIOS_BUILD_PROBES=1: a branch per stamp site in the
+  // pass loop costs production launches, as the GEMVs' probe branches did)
   auto stamp = [&](int k) __attribute__((always_inline)) {
-    if (a.ts && threadIdx.x == 0)
+    if (AIOS_ATTN_PROBES && a.ts && threadIdx.x == 0)
       a.ts[((size_t)blockIdx.z * gridDim.x + blockIdx.x) * 8 + k] = __builtin_amdgcn_s_memrealtime();
   };
   stamp(0);

@@ -1,6 +1,7 @@
 """Decode-attention microbenchmark on the GPU: per-launch time (hipGraph of back-to-back launches)
 of attn_decode over context lengths x split sizes.  python tools/attn_probe.py
---stamps: per-phase in-kernel timestamps (s_memrealtime, AttnDecodeArgs.ts) of one launch with the
+--stamps (needs a probe build: AIOS_BUILD_PROBES=1 with the build dir removed -- production builds
+compile the stamps out): per-phase in-kernel timestamps (s_memrealtime, AttnDecodeArgs.ts) of one launch with the
 K/V cache evicted from the Infinity Cache first (a 512 MB write in between), median / max over the
 workgroups: entry -> seq_len known -> first pass computed -> waves merged -> partial published ->
 combine weights ready -> done."""
