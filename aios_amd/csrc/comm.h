@@ -12,6 +12,10 @@
 //    lm_head: each rank computes V/world logits, every rank needs all of them for the identical
 //    on-device sampler and the JSON-grammar mask).
 // All three are fused with their consumer where it is an elementwise op (residual add).
+//  * C1 / C2 of the batch-1 TP decode step fused into the PRODUCER instead (round 4): the O / down row
+//    GEMV's workgroups publish their rows' partials to per-workgroup stage slots behind the one-shot
+//    region and exchange per-slot flags (EPI_TP_RESID, gemv_q8.h) -- no all-reduce launch.  Stage and
+//    flags are uncached, so a retired store is visible to every peer without a system-scope fence.
 //
 // Why not a ring: a ring pays 2(W-1) latency hops and is bound by one link.
 //
