@@ -193,7 +193,7 @@ __device__ __forceinline__ void cu_qkv_epilogue(const GemvArgs& a, int grow, flo
 // GEMV now does -- measured 0.2-0.6 us slower per engine launch, profiles/decode_tinyllama_rocprof_r4.txt)
 #define CU_STAMP(i)                                                   \
   do {                                                                \
-    if (a.dbg_ts) ts[i] = __builtin_amdgcn_s_memrealtime();           \
+    if (AIOS_GEMV_PROBES && a.dbg_ts) ts[i] = __builtin_amdgcn_s_memrealtime();  \
   } while (0)
 
 // f(integral_constant<I>) for the run-time n in [0, N]: every case is a fully static body

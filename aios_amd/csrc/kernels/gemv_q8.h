@@ -577,7 +577,7 @@ __global__ void __launch_bounds__((q8_max_threads<U, PIPE>())) gemv_q8_rows(Gemv
   // 0 start, 1 first weight loads issued, 2 x staged, 3 barrier passed, 4 first pair computed, 5 done
   // (probe launches only: a wave-uniform branch on the kernarg; each stamp is stored when taken --
   // an array held to the end kept 16 SGPRs live through the kernel and the row GEMVs spilled SGPRs)
-  const bool stamps = a.dbg_ts != nullptr;
+  const bool stamps = AIOS_GEMV_PROBES && a.dbg_ts != nullptr;  // (probe builds only)
   bool stamped4 = false;
   auto stamp = [&](int i) __attribute__((always_inline)) {
     if (stamps && lane == 0 && (wave == 0 || wave == nw - 1))
