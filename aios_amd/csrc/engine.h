@@ -238,6 +238,10 @@ class Engine {
   float *gm_x_ = nullptr, *gm_qkv_ = nullptr, *gm_q_ = nullptr, *gm_part_ = nullptr;
   bf16_t *gm_a16_ = nullptr, *gm_ff16_ = nullptr, *gm_attn16_ = nullptr;
   int *gm_tokens_ = nullptr, *gm_pos_ = nullptr, *gm_slot_ = nullptr;
+  // chunks of <= 64 rows: the residual GEMMs' bf16(x * g_next) + per-tile sums (split RMSNorm)
+  bf16_t* gm_xn16_ = nullptr;
+  float* gm_npart_ = nullptr;
+  int gm_nparts_ = 0;
   // long prefill chunks (>= blas_min_rows_ tokens) through hipBLASLt against a resident bf16 copy of
   // the projection weights (blas.h): per layer {QKV stacked [q+2kv][d], O [d][q], gate/up [2ff][d],
   // down [d][ff]}; gate/up lands in fp32 (gm_gu32_) for the SwiGLU kernel

@@ -613,11 +613,24 @@ void Engine::finalize() {
       ws += gk_ws_bytes_;
       gk_cnt_len_ = gemm_skinny_cnt_len(maxN);
       gk_cnt_ = ibuf(gk_cnt_len_);
+      if (const char* e = std::getenv("AIOS_GEMM_NORM_FUSE")) nrm_fuse_ = std::atoi(e);
+      {  // split-RMSNorm operands of short (<= 64-row) prefill chunks, independent of max_batch
+        GemmQArgs p;
+        std::memset(&p, 0, sizeof(p));
+        p.M = 64; p.N = d; p.K = d; p.nseg = 1; p.seg[0] = layers_[0].wo.w;
+        const int parts = gemm_skinny_ntile(p);
+        if (nrm_fuse_ && parts > 0 && parts % 4 == 0 && parts <= 64 && d % 128 == 0) {
+          const int Gs = std::min(G, 64);
+          gm_nparts_ = parts;
+          gm_xn16_ = (bf16_t*)dmalloc((size_t)Gs * d * 2);
+          gm_npart_ = fbuf((size_t)Gs * parts);
+          ws += (size_t)Gs * d * 2;
+        }
+      }
       if (Bm >= 2) {
         dec_a16_ = (bf16_t*)dmalloc((size_t)Bm * std::max(d, qd) * 2);
         dec_ff16_ = (bf16_t*)dmalloc((size_t)Bm * cfg_.d_ff * 2);
         ws += (size_t)Bm * (std::max(d, qd) + cfg_.d_ff) * 2;
-        if (const char* e = std::getenv("AIOS_GEMM_NORM_FUSE")) nrm_fuse_ = std::atoi(e);
         GemmQArgs p;  // the residual producer's shape (O / down: N = d_model, one segment)
         std::memset(&p, 0, sizeof(p));
         p.M = std::min(Bm, 64); p.N = d; p.K = d; p.nseg = 1; p.seg[0] = layers_[0].wo.w;
@@ -1097,8 +1110,14 @@ void Engine::prefill_gemm(int slot, const std::vector<int>& tokens, int start_po
   const int qd = H * hd, kvd = Hkv * hd, ldqkv = qd + 2 * kvd, V = cfg_.vocab_size;
   const bool tp = cfg_.tp_size > 1;
   std::vector<int> hp(gm_rows_), hs(gm_rows_, slot);
+  // short chunks (n <= max_batch, the batched-decode GEMMs' shapes): the decode step's fusions --
+  // RoPE + KV write in the QKV GEMM's epilogue and the split RMSNorm (the residual GEMMs write
+  // bf16(x * g_next) + per-tile sums, the next GEMM scales its rows) -- 3 launches per layer fewer
+  static const bool short_fuse = !(std::getenv("AIOS_PREFILL_SHORT_FUSE") && std::atoi(std::getenv("AIOS_PREFILL_SHORT_FUSE")) == 0);
   for (int r0 = 0; r0 < T; r0 += gm_rows_) {
     const int n = std::min(gm_rows_, T - r0);
+    const bool sh = short_fuse && !tp && n <= 64 && !(blas_ && n >= blas_min_rows_);
+    const bool fnp = sh && gm_nparts_ > 0;
     for (int i = 0; i < n; ++i) hp[i] = start_pos + r0 + i;
     HIP_CHECK(hipMemcpyAsync(gm_tokens_, tokens.data() + r0, n * 4, hipMemcpyHostToDevice, stream_));
     HIP_CHECK(hipMemcpyAsync(gm_pos_, hp.data(), n * 4, hipMemcpyHostToDevice, stream_));
@@ -1108,17 +1127,34 @@ void Engine::prefill_gemm(int slot, const std::vector<int>& tokens, int start_po
       const LayerW& L = layers_[l];
       bf16_t* kc = k_cache_ + (size_t)l * layer_kv_elems_;
       bf16_t* vc = v_cache_ + (size_t)l * layer_kv_elems_;
-      launch_rmsnorm_bf16(gm_x_, d, L.attn_norm, gm_a16_, d, n, d, cfg_.norm_eps, stream_);
+      const bool qepi = sh && !cfg_.qk_norm && !cfg_.rope_neox && !L.bqkv && rope_cs_;
+      // split-RMSNorm consumer / producer (as in layer_decode_gemm, on this chunk's rows)
+      auto nrm_in = [&](GemmQArgs& g) {
+        g.A = gm_xn16_; g.nrm_in = gm_npart_; g.nrm_parts = gm_nparts_; g.nrm_eps = cfg_.norm_eps;
+      };
+      auto nrm_out = [&](GemmQArgs& g, const float* g_next) {
+        g.epi = GEPI_ACCUM_NORM; g.nrm_g = g_next; g.nrm_out16 = gm_xn16_; g.nrm_part = gm_npart_;
+        g.nrm_parts = gm_nparts_;
+      };
+      if (!(fnp && l > 0)) launch_rmsnorm_bf16(gm_x_, d, L.attn_norm, gm_a16_, d, n, d, cfg_.norm_eps, stream_);
       GemmQArgs g;
       std::memset(&g, 0, sizeof(g));
       g.A = gm_a16_; g.lda = d; g.M = n; g.K = d;
+      if (fnp && l > 0) nrm_in(g);
       g.nseg = 3;
       g.seg[0] = L.wq.w; g.seg[1] = L.wk.w; g.seg[2] = L.wv.w;
       g.seg_n0[0] = 0; g.seg_n0[1] = qd; g.seg_n0[2] = qd + kvd;
       g.N = ldqkv; g.C = gm_qkv_; g.ldc = ldqkv; g.epi = GEPI_STORE;
+      if (qepi) {
+        g.epi = GEPI_QKV; g.col0 = 0;
+        g.head_dim = hd; g.q_dim = qd; g.kv_dim = kvd; g.n_kv_heads = Hkv; g.max_ctx = cfg_.max_ctx;
+        g.rope_cs = rope_cs_; g.pos = gm_pos_; g.slot = gm_slot_; g.block_table = d_bt_;
+        g.q_out = gm_q_; g.k_cache = kc; g.v_cache = vc;
+      }
       // long chunks: hipBLASLt on the resident bf16 weights (blas.h); falls back per call
       const bool lib = blas_ && n >= blas_min_rows_;
       if (!(lib && blas_->gemm(gm_a16_, d, w16_[4 * l], gm_qkv_, ldqkv, n, ldqkv, d, false, stream_))) gemm(g);
+      if (!qepi) {
       QkvPostArgs p;
       p.qkv = gm_qkv_; p.ldqkv = ldqkv; p.T = n;
       p.n_heads = H; p.n_kv_heads = Hkv; p.head_dim = hd;
@@ -1127,6 +1163,7 @@ void Engine::prefill_gemm(int slot, const std::vector<int>& tokens, int start_po
       p.pos = gm_pos_; p.slot = gm_slot_; p.q_out = gm_q_;
       p.k_cache = kc; p.v_cache = vc; p.max_ctx = cfg_.max_ctx; p.block_table = d_bt_;
       launch_qkv_post(p, stream_);
+      }
       AttnPrefillArgs at;
       at.q = gm_q_; at.k_cache = kc; at.v_cache = vc; at.block_table = d_bt_;
       at.slot = slot; at.start = start_pos + r0; at.T = n;
@@ -1138,13 +1175,15 @@ void Engine::prefill_gemm(int slot, const std::vector<int>& tokens, int start_po
       std::memset(&g, 0, sizeof(g));
       g.A = gm_attn16_; g.lda = qd; g.M = n; g.K = qd; g.nseg = 1; g.seg[0] = L.wo.w; g.N = d; g.ldc = d;
       if (tp) { g.C = gm_part_; g.epi = GEPI_STORE; } else { g.C = gm_x_; g.epi = GEPI_ACCUM; }
+      if (fnp) nrm_out(g, L.ffn_norm);
       if (!(lib && blas_->gemm(gm_attn16_, qd, w16_[4 * l + 1], g.C, d, n, d, qd, !tp, stream_))) gemm(g);
       if (tp) allreduce(gm_part_, (size_t)n * d, gm_x_);
       // FFN
-      launch_rmsnorm_bf16(gm_x_, d, L.ffn_norm, gm_a16_, d, n, d, cfg_.norm_eps, stream_);
+      if (!fnp) launch_rmsnorm_bf16(gm_x_, d, L.ffn_norm, gm_a16_, d, n, d, cfg_.norm_eps, stream_);
       std::memset(&g, 0, sizeof(g));
       g.A = gm_a16_; g.lda = d; g.M = n; g.K = d; g.nseg = 1; g.seg[0] = L.wgu.w; g.N = 2 * ff;
       g.C16 = gm_ff16_; g.ldc = ff; g.epi = GEPI_SWIGLU_BF16;
+      if (fnp) nrm_in(g);
       if (lib && blas_->gemm(gm_a16_, d, w16_[4 * l + 2], gm_gu32_, 2 * ff, n, 2 * ff, d, false, stream_))
         launch_swiglu_interleaved_bf16(gm_gu32_, 2 * ff, gm_ff16_, ff, n, ff, stream_);
       else
@@ -1152,6 +1191,7 @@ void Engine::prefill_gemm(int slot, const std::vector<int>& tokens, int start_po
       std::memset(&g, 0, sizeof(g));
       g.A = gm_ff16_; g.lda = ff; g.M = n; g.K = ff; g.nseg = 1; g.seg[0] = L.wdown.w; g.N = d; g.ldc = d;
       if (tp) { g.C = gm_part_; g.epi = GEPI_STORE; } else { g.C = gm_x_; g.epi = GEPI_ACCUM; }
+      if (fnp && l + 1 < cfg_.n_layers) nrm_out(g, layers_[l + 1].attn_norm);  // (lm_head normalises its row)
       if (!(lib && blas_->gemm(gm_ff16_, ff, w16_[4 * l + 3], g.C, d, n, d, ff, !tp, stream_))) gemm(g);
       if (tp) allreduce(gm_part_, (size_t)n * d, gm_x_);
     }

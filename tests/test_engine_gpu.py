@@ -181,6 +181,27 @@ def test_short_prompt_prefill_matches_reference(model_files, monkeypatch, T, q8)
     assert (logits - rl).abs().max().item() < 2e-2 * max(rl.abs().max().item(), 1.0)
 
 
+@pytest.mark.parametrize("recipe", ["Q4_K_M", "mistral_shape"])
+@pytest.mark.parametrize("fuse", ["0", "1"])
+def test_short_chunk_prefill_fusions_match_reference(model_files, monkeypatch, recipe, fuse):
+    """chunks of <= 64 rows take the decode step's fusions (RoPE + KV write in the QKV GEMM epilogue,
+    split RMSNorm through the residual GEMMs, AIOS_PREFILL_SHORT_FUSE): a 40-token prompt in one chunk
+    and its continuation at start_pos 40 (24 more rows) against the fp32 reference, fused and not"""
+    monkeypatch.setenv("AIOS_PREFILL_GEMM", "1")
+    monkeypatch.setenv("AIOS_PREFILL_SHORT_FUSE", fuse)
+    path = model_files[recipe]
+    eng, cfg = _load(path, max_batch=1)
+    ref = ReferenceModel.from_gguf(path, kv_bf16=True)
+    prompt = [1] + list(np.random.default_rng(11).integers(3, cfg.vocab_size, 63))
+    rl = ref.forward(prompt)[-1]
+    scale = max(rl.abs().max().item(), 1.0)
+    eng.prefill(0, prompt[:40], 0, False)
+    logits = torch.from_numpy(np.asarray(eng.prefill(0, prompt[40:], 40, True)))
+    assert (logits - rl).abs().max().item() < 2e-2 * scale
+    logits1 = torch.from_numpy(np.asarray(eng.prefill(1, prompt, 0, True)))
+    assert (logits1 - rl).abs().max().item() < 2e-2 * scale
+
+
 def test_prefill_gemm_vs_gemv_path(model_files, monkeypatch):
     path = model_files["Q4_K_M"]
     prompt = [1] + list(np.random.default_rng(4).integers(3, 200, 60))
