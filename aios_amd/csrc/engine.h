@@ -249,6 +249,8 @@ class Engine {
   std::vector<bf16_t*> w16_;  // 4 per layer
   float* gm_gu32_ = nullptr;
   int blas_min_rows_ = 256;
+  int blas_lo_ = 33, blas_hi_ = 128;  // AIOS_PREFILL_BLAS_WINDOW: shorter chunks on the library too
+  bool blas_rows(int n) const { return blas_ && (n >= blas_min_rows_ || (n >= blas_lo_ && n <= blas_hi_)); }
   const ArDevCtx* tp_fuse_ = nullptr;
   int tp_fuse_grid_ = 0;
   bool tp_fuse_gemv(GemvArgs a);  // EPI_TP_RESID launch when the engine serves the shape (else false)

@@ -665,6 +665,13 @@ void Engine::setup_blas_prefill() {
   if (const char* e = std::getenv("AIOS_PREFILL_BLAS"))
     if (std::atoi(e) == 0) return;
   if (const char* e = std::getenv("AIOS_PREFILL_BLAS_MIN")) blas_min_rows_ = std::max(1, std::atoi(e));
+  // "lo,hi": chunks of lo..hi rows take the library too (the fused GEMM's 33..64-row tiles lose to
+  // it: 64 tokens 6.0 vs 4.9 ms, profiles/prefill_blas_r4.txt); "0" turns the window off
+  if (const char* e = std::getenv("AIOS_PREFILL_BLAS_WINDOW")) {
+    blas_lo_ = std::atoi(e);
+    const char* c = std::strchr(e, ',');
+    blas_hi_ = c ? std::atoi(c + 1) : 0;
+  }
   if (gm_rows_ < blas_min_rows_) return;
   const int d = cfg_.d_model, qd = cfg_.n_heads * cfg_.head_dim, kvd = cfg_.n_kv_heads * cfg_.head_dim;
   const int ff = cfg_.d_ff;
@@ -1116,7 +1123,7 @@ void Engine::prefill_gemm(int slot, const std::vector<int>& tokens, int start_po
   static const bool short_fuse = !(std::getenv("AIOS_PREFILL_SHORT_FUSE") && std::atoi(std::getenv("AIOS_PREFILL_SHORT_FUSE")) == 0);
   for (int r0 = 0; r0 < T; r0 += gm_rows_) {
     const int n = std::min(gm_rows_, T - r0);
-    const bool sh = short_fuse && !tp && n <= 64 && !(blas_ && n >= blas_min_rows_);
+    const bool sh = short_fuse && !tp && n <= 64 && !blas_rows(n);
     const bool fnp = sh && gm_nparts_ > 0;
     for (int i = 0; i < n; ++i) hp[i] = start_pos + r0 + i;
     HIP_CHECK(hipMemcpyAsync(gm_tokens_, tokens.data() + r0, n * 4, hipMemcpyHostToDevice, stream_));
@@ -1152,7 +1159,7 @@ void Engine::prefill_gemm(int slot, const std::vector<int>& tokens, int start_po
         g.q_out = gm_q_; g.k_cache = kc; g.v_cache = vc;
       }
       // long chunks: hipBLASLt on the resident bf16 weights (blas.h); falls back per call
-      const bool lib = blas_ && n >= blas_min_rows_;
+      const bool lib = blas_rows(n);
       if (!(lib && blas_->gemm(gm_a16_, d, w16_[4 * l], gm_qkv_, ldqkv, n, ldqkv, d, false, stream_))) gemm(g);
       if (!qepi) {
       QkvPostArgs p;
