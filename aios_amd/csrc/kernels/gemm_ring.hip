@@ -288,10 +288,22 @@ __global__ void __launch_bounds__(RG_THREADS) gemm_ring_kernel(GemmQArgs a, int 
   __shared__ float inv_s[MP];
   const bool nrm = a.nrm_in != nullptr;
   if (nrm) {
+    // all of a row's (<= 64, multiple-of-4) partial sums requested at once: a dependent load per
+    // part held wave 0 -- a loader wave -- ~3 us before its first weight request
     for (int m = threadIdx.x; m < MP; m += RG_THREADS) {
       float t = 0.f;
-      if (m < a.M)
-        for (int j = 0; j < a.nrm_parts; ++j) t += a.nrm_in[(size_t)m * a.nrm_parts + j];
+      if (m < a.M) {
+        const float4* p = (const float4*)(a.nrm_in + (size_t)m * a.nrm_parts);
+        const int n4 = a.nrm_parts >> 2;
+#pragma unroll
+        for (int h = 0; h < 16; h += 8) {
+          float4 v[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] = h + j < n4 ? p[h + j] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) t += (v[j].x + v[j].y) + (v[j].z + v[j].w);
+        }
+      }
       inv_s[m] = rsqrtf(t / (float)a.K + a.nrm_eps);
     }
     // ordered before the epilogue by the ring's barriers
@@ -343,7 +355,7 @@ bool launch_gemm_ring(const GemmQArgs& a, hipStream_t st) {
   static const int on = rg_env("AIOS_GEMM_RING", 1);
   static const int min_m = rg_env("AIOS_GEMM_RING_MIN_M", 2);
   if (!on || a.M < min_m || a.M > 32 || a.N % 128 || a.K % 256 || a.lda % 8) return false;
-  if (a.nrm_in && (a.nrm_parts <= 0 || a.nrm_parts > 64)) return false;
+  if (a.nrm_in && (a.nrm_parts <= 0 || a.nrm_parts > 64 || a.nrm_parts % 4)) return false;
   if (a.epi == GEPI_SWIGLU_BF16 && a.ldc % 2) return false;
   if (a.epi != GEPI_SWIGLU_BF16 && a.ldc % 4) return false;
   for (int s = 0; s < a.nseg; ++s)
