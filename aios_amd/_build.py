@@ -72,11 +72,33 @@ def _flags():
 # (elementwise.hip's many-lane candidate counters keep it).
 _NO_ATOMIC_OPT = ["-mllvm", "-amdgpu-atomic-optimizer-strategy=None"]
 _FILE_FLAGS = {n: _NO_ATOMIC_OPT for n in ("gemv_kquant.hip", "gemv_kquant2.hip", "gemv_legacy.hip")}
+# The prefill GEMM's weight decode beside MFMAs: LLVM's SLP vectoriser packs the fmaf pairs into
+# v_pk_fma_f32, which costs ~+22 cycles per instruction when issued between MFMAs (MI355X guide,
+# price list 'packed f32 VALU ... an anti-lever beside MFMAs'); plain v_fma_f32 instead.
+for _n in ("gemm_pf.hip", "gemm_pf_q4k.hip", "gemm_pf_q6k.hip", "gemm_pf_mix.hip", "gemm_pf_bf16.hip"):
+    _FILE_FLAGS[_n] = ["-fno-slp-vectorize"]
+
+
+def _deps(src: Path, seen=None) -> set:
+    """src plus every quoted #include it reaches (resolved next to the includer or under csrc/)."""
+    import re
+
+    seen = set() if seen is None else seen
+    if src in seen or not src.exists():
+        return seen
+    seen.add(src)
+    for inc in re.findall(r'^\s*#\s*include\s+"([^"]+)"', src.read_text(errors="ignore"), re.M):
+        for base in (src.parent, CSRC):
+            cand = (base / inc).resolve()
+            if cand.exists():
+                _deps(cand, seen)
+                break
+    return seen
 
 
 def _compile(src: Path, flags, hipcc) -> Path:
     obj = BUILD / (src.stem + ".o")
-    newest_dep = max([src.stat().st_mtime] + [h.stat().st_mtime for h in _headers()])
+    newest_dep = max(d.stat().st_mtime for d in _deps(src))
     if obj.exists() and obj.stat().st_mtime >= newest_dep:
         return obj
     cmd = [hipcc, *flags, *_FILE_FLAGS.get(src.name, []), "-c", str(src), "-o", str(obj)]

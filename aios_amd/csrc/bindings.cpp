@@ -499,6 +499,30 @@ PYBIND11_MODULE(_engine, m) {
       },
       py::arg("A"), py::arg("lda"), py::arg("segs"), py::arg("M"), py::arg("C"), py::arg("C16"), py::arg("ldc"),
       py::arg("epi"), py::arg("stream"), py::arg("ksplit") = 0, py::arg("dbg_ts") = 0);
+  m.def(
+      "gemm_pf_plan",
+      [](std::vector<PyQMatrix*> segs, int M, int epi, int ksplit) {
+        GemmQArgs a;
+        std::memset(&a, 0, sizeof(a));
+        if (segs.empty() || segs.size() > 3) throw std::runtime_error("gemm_pf_plan: 1..3 segments");
+        a.nseg = (int)segs.size();
+        int n0 = 0;
+        for (int s = 0; s < a.nseg; ++s) { a.seg[s] = segs[s]->w; a.seg_n0[s] = n0; n0 += segs[s]->w.rows; }
+        a.M = M; a.N = n0; a.K = segs[0]->w.cols; a.epi = epi; a.ksplit = ksplit;
+        int bm = 0, bn = 0, sp = 0;
+        gemm_pf_plan(a, bm, bn, sp);
+        return py::make_tuple(bm, bn, sp);
+      },
+      py::arg("segs"), py::arg("M"), py::arg("epi"), py::arg("ksplit") = 0);
+  m.def(
+      "gemm_pf_probe",
+      [](uintptr_t A, int lda, PyQMatrix* w, int M, uintptr_t C, int probe, uintptr_t st) {
+        GemmQArgs a;
+        std::memset(&a, 0, sizeof(a));
+        a.A = (const bf16_t*)A; a.lda = lda; a.nseg = 1; a.seg[0] = w->w; a.M = M; a.N = w->w.rows;
+        a.K = w->w.cols; a.C = (float*)C; a.ldc = a.N; a.epi = GEPI_STORE;
+        return gemm_pf_probe(a, probe, S(st));
+      });
   m.attr("GEPI_STORE") = (int)GEPI_STORE;
   m.attr("GEPI_ACCUM") = (int)GEPI_ACCUM;
   m.attr("GEPI_SWIGLU_BF16") = (int)GEPI_SWIGLU_BF16;

@@ -234,6 +234,8 @@ bool launch_gemm_skinny(const GemmQArgs& a, hipStream_t st);
 bool gemm_skinny_mixed_ok(const GemmQArgs& a);
 // M <= 32, Q4_K / Q6_K: the LDS-DMA ring GEMM (gemm_ring.hip); false when it does not serve the shape
 bool launch_gemm_ring(const GemmQArgs& a, hipStream_t st);
+// M >= 33, Q4_K / Q6_K / mixed / bf16 stacks: the LDS-DMA prefill GEMM (gemm_pf.hip)
+bool launch_gemm_pf(const GemmQArgs& a, hipStream_t st);
 
 static void launch_one(const GemmQArgs& a, hipStream_t st) {
   static const int skinny_max = env_int("AIOS_GEMM_SKINNY_MAX_M", 64);
@@ -268,6 +270,7 @@ void launch_gemm_q(const GemmQArgs& a, hipStream_t st) {
   // mixed formats in ONE skinny launch where supported (the Q4_K_M QKV stack)
   static const int skinny_max = env_int("AIOS_GEMM_SKINNY_MAX_M", 64);
   if (launch_gemm_ring(a, st)) return;  // the mixed Q4_K_M QKV stack in one ring launch
+  if (launch_gemm_pf(a, st)) return;    // prefill chunks: the mixed stack in one launch too
   if (a.M <= skinny_max && gemm_skinny_mixed_ok(a) && launch_gemm_skinny(a, st)) return;
   int s0 = 0;
   while (s0 < a.nseg) {

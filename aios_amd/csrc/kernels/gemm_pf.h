@@ -1,0 +1,915 @@
+// Prefill GEMM on the CDNA4 matrix cores, dequantising the packed weights ONCE per workgroup tile:
+//   C[M][N] (epilogue) = A[M][K] (bf16 activations) x W[N][K]^T (repacked Q4_K / Q6_K planes, or bf16)
+// SURVEY.md §2.7 K3 prefill column -- the work llama.cpp's mul_mat_q does inside the reference's
+// llama-server child (/root/reference/runtime/src/model_manager.rs:187-204) -- without any resident
+// dequantised copy of a weight and without a vendor GEMM (round-4 verdict item 1).
+//
+// Geometry (BM x BN tile, NW = BN / 32 waves): every wave owns ALL BM rows and 32 columns, i.e.
+// (BM / 16) x 2 accumulators of v_mfma_f32_16x16x32_bf16.  A wave therefore dequantises exactly
+// its own 32 columns' weights (each weight byte decoded once per workgroup, straight into MFMA B
+// fragments in registers -- no bf16 LDS image of the weights, no LDS write pass) while the
+// activation tile is shared by all waves through LDS.  Per 64-deep K-step a lane decodes 32
+// weights (one 8-byte code group of each of its two columns) against 2 x BM/16 MFMAs.
+//
+// Staging: one LDS slot per K-step holds the A tile (BM rows x 128 B, 16-B units XOR-swizzled by
+// row so a ds_read_b128 lane group of 16 rows hits 16 distinct bank slots) and the tile's raw
+// weight bytes of that K-step (codes + per-format metadata), all moved by global_load_lds
+// (LDS-DMA: no VGPR staging, no ds_write).  NS slots, NS - 1 K-steps in flight, one raw s_barrier
+// per K-step (in-flight LDS-DMA survives it), counted s_waitcnt vmcnt -- the only vector-memory
+// operations inside the loop are these DMAs, so the counts are exact (CDNA guide §5 "Pipelining
+// across barriers", "Three .s-level traps").
+//
+// Weight k order: chunk h (16 B) of a 64-weight Q4_K group holds weights 16h + i (low nibble of byte
+// i) and 32 + 16h + i (high nibble).  Lane quarter q of the 16x16x32 B fragment reads bytes
+// 8(q&1) .. 8(q&1)+7 of chunk q>>1: its low nibbles are k = 8q .. 8q+7 (fragment of k-substep 0)
+// and its high nibbles k = 32 + 8q .. (substep 1) -- exactly the MFMA's natural k layout, so the A
+// fragments are plain 16-B row reads at unit 4s + q.  Q6_K is repacked into the same chunk order
+// (qweight.h), its 2 high bits and int8 sub-block scales riding beside the codes.
+#pragma once
+#include "gemm_common.h"
+
+namespace aios {
+
+// slot layout for one K-step: A, then the weight planes of BN columns
+template <int QT, int BM, int BN>
+struct PfLayout {
+  static constexpr bool Q6 = QT == QT_Q6_K, BF = QT == QT_BF16;
+  static constexpr int A_BYTES = BM * 128;
+  static constexpr int CODE = BF ? BN * 128 : BN * 32;        // bf16 rows (swizzled as A) / 2 code chunks
+  static constexpr int META = BF ? 0 : BN * 16;                // Q4_K scale record / Q6_K high bits of 2 chunks
+  static constexpr int SC = Q6 ? BN * 4 : 0;                   // Q6_K int8 scale pairs of the 2 chunks
+  static constexpr int DW = Q6 ? BN * 4 : 0;                   // Q6_K aligned dword holding the block's f16 d
+  static constexpr int OFF_CODE = A_BYTES, OFF_META = OFF_CODE + CODE, OFF_SC = OFF_META + META,
+                       OFF_D = OFF_SC + SC;
+  static constexpr int SLOT = (OFF_D + DW + 255) / 256 * 256;
+  // DMA wave-instructions per slot: 1 KB at 16 B per lane, 256 B at 4 B per lane
+  static constexpr int NI_A = A_BYTES / 1024, NI_CODE = CODE / 1024, NI_META = META / 1024, NI_SC = SC / 256,
+                       NI_D = DW / 256;
+  static constexpr int TI = NI_A + NI_CODE + NI_META + NI_SC + NI_D;
+  static_assert(A_BYTES % 1024 == 0 && CODE % 1024 == 0 && META % 1024 == 0 && SC % 256 == 0, "slot pieces");
+};
+
+__device__ __forceinline__ void pf_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+template <int N>
+__device__ __forceinline__ void pf_vmcnt() {
+  static_assert(N >= 0 && N <= 63, "vmcnt immediate");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// LDS-DMA through inline asm: hipcc's waitcnt pass then does not see the DMA, so it no longer puts
+// an `s_waitcnt vmcnt(0)` in front of the first ds_read after every issue (it cannot prove the read
+// misses the DMA's target slot -- measured: that drain serialised every K-step).  The counted
+// pf_vmcnt waits below are the only ordering these loads need.  M0 is set and restored inside the
+// statement (CDNA guide §5.7, LDS-DMA recipe).
+__device__ __forceinline__ uint32_t pf_lds_addr(const uint8_t* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) uint8_t*)p;
+}
+__device__ __forceinline__ void pf_glds16(const void* src, uint32_t lds) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(src), "s"(lds)
+               : "memory");
+}
+__device__ __forceinline__ void pf_glds4(const void* src, uint32_t lds) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(src), "s"(lds)
+               : "memory");
+}
+
+// This wave's share of every slot: pieces i = pp * NW + wv (pp < PH; the last may not exist).  The
+// per-lane part of each piece's source address is a 32-bit byte offset computed once per workgroup;
+// a K-step adds only a uniform per-kind step offset (the repacked planes advance linearly in kt:
+// codes 32 B, Q6_K high bits 16 B, Q6_K scales 4 B per K-step; the 256-block records per 4 steps).
+template <int QT, int BM, int BN, int NW>
+struct PfDma {
+  using L = PfLayout<QT, BM, BN>;
+  static constexpr int PH = (L::TI + NW - 1) / NW;
+  uint32_t off[PH];
+
+  __device__ __forceinline__ void init(const GemmQArgs& a, int wrow0, int m0, int wv) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t nbk = (uint32_t)a.K >> 8;
+    static_for<PH>([&](auto ppc) {
+      constexpr int pp = decltype(ppc)::value;
+      int j = pp * NW + wv;
+      uint32_t o = 0;
+      if (j < L::NI_A) {  // A unit p -> row p>>3, logical 16-B unit (p&7) ^ ((row>>1)&7); rows past M re-read M-1
+        const int p = 64 * j + lane, row = p >> 3, c = (p & 7) ^ ((row >> 1) & 7);
+        const int m = min(m0 + row, a.M - 1);
+        o = ((uint32_t)m * (uint32_t)a.lda + (uint32_t)(c * 8)) * 2u;
+      } else if ((j -= L::NI_A) < L::NI_CODE) {
+        const int p = 64 * j + lane;
+        if constexpr (L::BF) {  // bf16 weight rows in the A swizzle
+          const int col = p >> 3, c = (p & 7) ^ ((col >> 1) & 7);
+          o = ((uint32_t)(wrow0 + col) * (uint32_t)a.K + (uint32_t)(c * 8)) * 2u;
+        } else {  // column col's two 16-B code chunks (2g, 2g+1): 32 contiguous bytes
+          const int col = p >> 1, h = p & 1;
+          o = (uint32_t)(wrow0 + col) * nbk * 128u + (uint32_t)h * 16u;
+        }
+      } else if ((j -= L::NI_CODE) < L::NI_META) {
+        const uint32_t row = (uint32_t)(wrow0 + 64 * j + lane);
+        o = L::Q6 ? row * nbk * 64u : row * nbk * 16u;  // Q6_K high bits (8 B per chunk) / Q4_K record
+      } else if ((j -= L::NI_META) < L::NI_SC) {
+        o = (uint32_t)(wrow0 + 64 * j + lane) * nbk * 16u;  // Q6_K int8 scales (2 B per chunk)
+      } else {
+        j -= L::NI_SC;
+        o = (uint32_t)(wrow0 + 64 * j + lane) * nbk;  // Q6_K d: the row's first block index
+      }
+      off[pp] = o;
+    });
+  }
+
+  // issue K-step kt into dst (all of this wave's pieces, or those with pp % NP == P: spread over phases)
+  template <int P = 0, int NP = 1>
+  __device__ __forceinline__ void issue(const GemmQArgs& a, const QWeight& w, int kt, uint32_t dst, int wv) const {
+    static_for<PH>([&](auto ppc) {
+      constexpr int pp = decltype(ppc)::value;
+      if constexpr (pp % NP != P) return;
+      int j = pp * NW + wv;
+      if (j >= L::TI) return;
+      if (j < L::NI_A) {
+        const uint8_t* src = (const uint8_t*)a.A + kt * 128 + off[pp];
+        pf_glds16(src, dst + j * 1024);
+      } else if ((j -= L::NI_A) < L::NI_CODE) {
+        const uint8_t* src = w.p0 + (L::BF ? kt * 128 : kt * 32) + off[pp];
+        pf_glds16(src, dst + L::OFF_CODE + j * 1024);
+      } else if ((j -= L::NI_CODE) < L::NI_META) {
+        const uint8_t* src = w.p1 + (L::Q6 ? kt * 16 : (kt >> 2) * 16) + off[pp];
+        pf_glds16(src, dst + L::OFF_META + j * 1024);
+      } else if ((j -= L::NI_META) < L::NI_SC) {
+        const uint8_t* src = w.p2 + kt * 4 + off[pp];
+        pf_glds4(src, dst + L::OFF_SC + j * 256);
+      } else {
+        j -= L::NI_SC;
+        const uint8_t* src = w.p3 + (((off[pp] + (uint32_t)(kt >> 2)) >> 1) << 2);  // the dword holding f16 d
+        pf_glds4(src, dst + L::OFF_D + j * 256);
+      }
+    });
+  }
+};
+
+// 8 codes (bytes of w0 then w1) -> bf16x8 fragment of sc * q - of
+__device__ __forceinline__ gbf16x8 pf_dq8(uint32_t w0, uint32_t w1, float sc, float of) {
+  asm volatile("" : "+v"(w0), "+v"(w1));  // one v_cvt_f32_ubyteN per byte
+  uint32_t p[4];
+  p[0] = pk_bf16(fmaf(sc, (float)(w0 & 0xff), -of), fmaf(sc, (float)((w0 >> 8) & 0xff), -of));
+  p[1] = pk_bf16(fmaf(sc, (float)((w0 >> 16) & 0xff), -of), fmaf(sc, (float)(w0 >> 24), -of));
+  p[2] = pk_bf16(fmaf(sc, (float)(w1 & 0xff), -of), fmaf(sc, (float)((w1 >> 8) & 0xff), -of));
+  p[3] = pk_bf16(fmaf(sc, (float)((w1 >> 16) & 0xff), -of), fmaf(sc, (float)(w1 >> 24), -of));
+  gbf16x8 r;
+  __builtin_memcpy(&r, p, 16);
+  return r;
+}
+
+// Raw weight bytes of one tile column for this lane's quarter q (LDS reads), then the decode of
+// fragment s (k 8q.. for s = 0, 32 + 8q.. for s = 1) -- split so the decode can sit between MFMAs.
+struct PfBRaw {
+  uint2 cw;       // 8 code bytes: low nibbles = fragment 0, high nibbles = fragment 1
+  uint4 mt;       // Q4_K scale record | bf16: fragment 0
+  uint2 hb;       // Q6_K high bits {run 0, run 1}
+  uint32_t scw;   // Q6_K int8 scale pairs
+  uint32_t dw;    // Q6_K dword holding d
+  uint4 b1;       // bf16: fragment 1
+};
+
+template <int QT, int BM, int BN>
+__device__ __forceinline__ void pf_braw(const uint8_t* slot, int col, int q, PfBRaw& r) {
+  using L = PfLayout<QT, BM, BN>;
+  if constexpr (L::BF) {
+    r.mt = *(const uint4*)(slot + L::OFF_CODE + col * 128 + (((0 + q) ^ ((col >> 1) & 7)) << 4));
+    r.b1 = *(const uint4*)(slot + L::OFF_CODE + col * 128 + (((4 + q) ^ ((col >> 1) & 7)) << 4));
+  } else {
+    r.cw = *(const uint2*)(slot + L::OFF_CODE + col * 32 + 8 * q);
+    if constexpr (L::Q6) {
+      r.hb = *(const uint2*)(slot + L::OFF_META + col * 16 + 8 * (q >> 1));
+      r.scw = *(const uint32_t*)(slot + L::OFF_SC + col * 4);
+      r.dw = *(const uint32_t*)(slot + L::OFF_D + col * 4);
+    } else {
+      r.mt = *(const uint4*)(slot + L::OFF_META + col * 16);
+    }
+  }
+}
+
+template <int QT, int S>
+__device__ __forceinline__ gbf16x8 pf_bdec(const PfBRaw& r, int q, int kt, int dpar) {
+  gbf16x8 f;
+  if constexpr (QT == QT_BF16) {
+    const uint4 v = S == 0 ? r.mt : r.b1;
+    __builtin_memcpy(&f, &v, 16);
+  } else if constexpr (QT == QT_Q6_K) {
+    const float d = h2f((uint16_t)(r.dw >> (16 * dpar)));
+    const float ds = d * (float)(int8_t)((r.scw >> (16 * (q >> 1) + 8 * S)) & 0xff);
+    const uint32_t hv = S == 0 ? r.hb.x : r.hb.y;
+    const int j0 = 2 * (q & 1);  // code words j0, j0 + 1 of the chunk
+    const uint32_t c0 = S == 0 ? (r.cw.x & 0x0f0f0f0fu) : ((r.cw.x >> 4) & 0x0f0f0f0fu);
+    const uint32_t c1 = S == 0 ? (r.cw.y & 0x0f0f0f0fu) : ((r.cw.y >> 4) & 0x0f0f0f0fu);
+    f = pf_dq8(c0 | (((hv >> (2 * j0)) & 0x03030303u) << 4), c1 | (((hv >> (2 * j0 + 2)) & 0x03030303u) << 4), ds,
+               32.f * ds);
+  } else {  // Q4_K
+    const float d = h2f((uint16_t)(r.mt.x & 0xffff)), dmin = h2f((uint16_t)(r.mt.x >> 16));
+    const uint32_t fl = kq_field(r.mt.y, r.mt.z, r.mt.w, kt & 3);
+    const float ds = d * (float)((fl >> (6 * S)) & 63), dm = dmin * (float)((fl >> (12 + 6 * S)) & 63);
+    const uint32_t c0 = S == 0 ? (r.cw.x & 0x0f0f0f0fu) : ((r.cw.x >> 4) & 0x0f0f0f0fu);
+    const uint32_t c1 = S == 0 ? (r.cw.y & 0x0f0f0f0fu) : ((r.cw.y >> 4) & 0x0f0f0f0fu);
+    f = pf_dq8(c0, c1, ds, dm);
+  }
+  return f;
+}
+
+// PROBE (timing anatomy only, tools/bench_gemm.py --pf-probe; never in the engine's launches):
+// 1 = no DMA waits, 4 = no DMA issued inside the loop (stale slots), 8 = no per-step barrier
+template <int QT, int BM, int NW, int NS, int EPI, int PROBE = 0>
+__device__ __forceinline__ void pf_body(const GemmQArgs& a, int m0, int n0, int seg, int kt0, int kt1, int S) {
+  constexpr int BN = NW * 32, MT = BM / 16;
+  constexpr int GR = MT < 8 ? MT : 8, NG = MT / GR;  // row tiles per phase, phases per k-substep
+  using L = PfLayout<QT, BM, BN>;
+  extern __shared__ __attribute__((aligned(16))) uint8_t pf_smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  QWeight w;  // field-wise uniform selects (a dynamically indexed struct copy goes to scratch)
+  w.qtype = QT;
+  w.rows = seg == 0 ? a.seg[0].rows : (seg == 1 ? a.seg[1].rows : a.seg[2].rows);
+  w.cols = a.K;
+  w.pad_ = 0;
+  w.p0 = seg == 0 ? a.seg[0].p0 : (seg == 1 ? a.seg[1].p0 : a.seg[2].p0);
+  w.p1 = seg == 0 ? a.seg[0].p1 : (seg == 1 ? a.seg[1].p1 : a.seg[2].p1);
+  w.p2 = seg == 0 ? a.seg[0].p2 : (seg == 1 ? a.seg[1].p2 : a.seg[2].p2);
+  w.p3 = seg == 0 ? a.seg[0].p3 : (seg == 1 ? a.seg[1].p3 : a.seg[2].p3);
+  const int wrow0 = n0 - (seg == 0 ? a.seg_n0[0] : (seg == 1 ? a.seg_n0[1] : a.seg_n0[2]));
+  const int nbk = a.K >> 8;
+  const int r16 = lane & 15, q = lane >> 4;
+  const int col0 = wv * 32 + r16;  // this lane's two columns: col0, col0 + 16 (tile-relative)
+
+  gf32x4 acc[MT][2];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int c = 0; c < 2; ++c) acc[i][c] = gf32x4{0.f, 0.f, 0.f, 0.f};
+
+  // pieces per slot of this wave (PH if wv < TI % NW): the vmcnt immediates
+  constexpr int PH = (L::TI + NW - 1) / NW, PLO = L::TI / NW;
+  const bool many = (L::TI % NW == 0) || wv < L::TI % NW;
+  const int nk = kt1 - kt0;
+  PfDma<QT, BM, BN, NW> dma;
+  const uint32_t lds0 = __builtin_amdgcn_readfirstlane(pf_lds_addr(pf_smem));
+  dma.init(a, wrow0, m0, wv);
+#pragma unroll
+  for (int p = 0; p < NS - 1; ++p)
+    if (p < nk) dma.issue(a, w, kt0 + p, lds0 + p * L::SLOT, wv);
+
+  int cur = 0;
+  for (int t = 0; t < nk; ++t) {
+    // step t's pieces landed (the younger NS - 2 steps may stay in flight), then everyone's
+    if constexpr (PROBE & 1) {
+    } else if constexpr (NS == 3) {
+      if (t + 1 < nk) {
+        if (many) pf_vmcnt<PH>(); else pf_vmcnt<PLO>();
+      } else {
+        pf_vmcnt<0>();
+      }
+    } else {
+      static_assert(NS == 2, "2 or 3 slots");
+      pf_vmcnt<0>();
+    }
+    if constexpr (!(PROBE & 8)) pf_barrier();
+    // refill the slot every wave finished reading last step
+    if (!(PROBE & 4) && t + NS - 1 < nk) {
+      const int ns = cur == 0 ? NS - 1 : cur - 1;
+      dma.issue(a, w, kt0 + t + NS - 1, lds0 + ns * L::SLOT, wv);
+    }
+    const uint8_t* slot = pf_smem + cur * L::SLOT;
+    const int kt = kt0 + t;
+    // Phases: A fragments of GR row tiles per phase in two named register groups (fa / fb), the
+    // next phase's reads issued before this phase's MFMAs; fragment-1 decode inside phase 0.
+    // sched_barrier pins the phase order (hipcc otherwise keeps ~2 reads in flight per MFMA pair).
+    PfBRaw raw[2];
+    int dpar[2];
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int col = col0 + 16 * c;
+      dpar[c] = L::Q6 ? (int)(((uint32_t)(wrow0 + col) * (uint32_t)nbk + (uint32_t)(kt >> 2)) & 1u) : 0;
+      pf_braw<QT, BM, BN>(slot, col, q, raw[c]);
+    }
+    gbf16x8 fa[GR], fb[GR], bf[2][2];
+    auto ldA = [&](gbf16x8(&f)[GR], int p) __attribute__((always_inline)) {
+      const int sp = p / NG, g = p % NG;
+#pragma unroll
+      for (int i = 0; i < GR; ++i) {
+        const int row = 16 * (g * GR + i) + r16;
+        const uint4 av = *(const uint4*)(slot + row * 128 + (((4 * sp + q) ^ ((row >> 1) & 7)) << 4));
+        __builtin_memcpy(&f[i], &av, 16);
+      }
+    };
+    ldA(fa, 0);
+    __builtin_amdgcn_sched_barrier(0);  // every read of the step's head in flight before the decode
+#pragma unroll
+    for (int c = 0; c < 2; ++c) bf[c][0] = pf_bdec<QT, 0>(raw[c], q, kt, dpar[c]);
+    __builtin_amdgcn_sched_barrier(0);
+    static_for<2 * NG>([&](auto pc) {
+      constexpr int p = decltype(pc)::value, sp = p / NG, g = p % NG;
+      if constexpr (p + 1 < 2 * NG) {
+        if constexpr (p % 2 == 0) ldA(fb, p + 1);
+        else ldA(fa, p + 1);
+      }
+      if constexpr (p == 0) {
+#pragma unroll
+        for (int c = 0; c < 2; ++c) bf[c][1] = pf_bdec<QT, 1>(raw[c], q, kt, dpar[c]);
+      }
+#pragma unroll
+      for (int i = 0; i < GR; ++i)
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+          acc[g * GR + i][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(p % 2 == 0 ? fa[i] : fb[i], bf[c][sp],
+                                                                       acc[g * GR + i][c], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    });
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this slot's LDS reads retired before it is refilled
+    cur = cur == NS - 1 ? 0 : cur + 1;
+  }
+
+  // epilogue -- C/D map of the 16x16 accumulator: col = lane & 15, row = 4 * (lane >> 4) + e
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const int n = n0 + col0 + 16 * c;
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int m = m0 + 16 * i + 4 * q + e;
+        const float v = acc[i][c][e];
+        if constexpr (EPI == GEPI_SWIGLU_BF16) {
+          // interleaved gate/up columns: even lane = gate, odd lane = its up partner
+          const float up = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));
+          if (m < a.M && !(r16 & 1)) a.C16[(size_t)m * a.ldc + (n >> 1)] = f32_to_bf16(v / (1.f + __expf(-v)) * up);
+        } else if (m < a.M) {
+          float* cp = a.C + (size_t)m * a.ldc + n;
+          if (S > 1) unsafeAtomicAdd(cp, v);
+          else if constexpr (EPI == GEPI_ACCUM) *cp += v;
+          else *cp = v;
+        }
+      }
+    }
+  }
+}
+
+
+// ---- 32x32x16 body: a wave owns BM rows x 32 columns = BM/32 accumulators of v_mfma_f32_32x32x16_bf16.
+// Per 64-deep K-step four k16 substeps s = 0..3 at k = 16s + 8h + j (h = lane >> 5): chunk (s & 1)'s
+// bytes 8h .. 8h+7, low nibbles for s < 2, high nibbles for s >= 2 -- again the MFMA's natural k
+// layout, so A fragments are 16-B row reads at unit 2s + h.  Per MFMA (32 cycles, vector issue held
+// for 8) there is room for ~6 fillers against ~2 on the 16x16x32 body, which left that body
+// issue-bound on its decode VALU + LDS reads (tools/bench_gemm.py --pf-probe, round 5).  The slot's
+// DMA pieces are issued one phase at a time between the MFMA groups instead of at the step head.
+struct PfBRaw32 {
+  uint2 c0, c1;   // 8 code bytes of chunk 0 / chunk 1
+  uint4 mt;       // Q4_K scale record | Q6_K high bits {c0 run0, c0 run1, c1 run0, c1 run1} | bf16 fragment 0
+  uint32_t scw;   // Q6_K int8 scales {c0 run0, c0 run1, c1 run0, c1 run1}
+  uint32_t dw;    // Q6_K dword holding d
+  uint4 b1, b2, b3;  // bf16 fragments 1..3
+};
+
+template <int QT, int BM, int BN>
+__device__ __forceinline__ void pf_braw32(const uint8_t* slot, int col, int h, PfBRaw32& r) {
+  using L = PfLayout<QT, BM, BN>;
+  if constexpr (L::BF) {
+    const uint8_t* row = slot + L::OFF_CODE + col * 128;
+    const int x = (col >> 1) & 7;
+    r.mt = *(const uint4*)(row + (((0 + h) ^ x) << 4));
+    r.b1 = *(const uint4*)(row + (((2 + h) ^ x) << 4));
+    r.b2 = *(const uint4*)(row + (((4 + h) ^ x) << 4));
+    r.b3 = *(const uint4*)(row + (((6 + h) ^ x) << 4));
+  } else {
+    r.c0 = *(const uint2*)(slot + L::OFF_CODE + col * 32 + 8 * h);
+    r.c1 = *(const uint2*)(slot + L::OFF_CODE + col * 32 + 16 + 8 * h);
+    r.mt = *(const uint4*)(slot + L::OFF_META + col * 16);
+    if constexpr (L::Q6) {
+      r.scw = *(const uint32_t*)(slot + L::OFF_SC + col * 4);
+      r.dw = *(const uint32_t*)(slot + L::OFF_D + col * 4);
+    }
+  }
+}
+
+template <int QT, int S>
+__device__ __forceinline__ gbf16x8 pf_bdec32(const PfBRaw32& r, int h, int kt, int dpar) {
+  gbf16x8 f;
+  if constexpr (QT == QT_BF16) {
+    const uint4 v = S == 0 ? r.mt : (S == 1 ? r.b1 : (S == 2 ? r.b2 : r.b3));
+    __builtin_memcpy(&f, &v, 16);
+  } else {
+    const uint2 cw = (S & 1) ? r.c1 : r.c0;
+    const uint32_t w0 = (S < 2) ? (cw.x & 0x0f0f0f0fu) : ((cw.x >> 4) & 0x0f0f0f0fu);
+    const uint32_t w1 = (S < 2) ? (cw.y & 0x0f0f0f0fu) : ((cw.y >> 4) & 0x0f0f0f0fu);
+    if constexpr (QT == QT_Q6_K) {
+      // run (S >> 1) of chunk (S & 1): high-bit word and int8 scale
+      constexpr int idx = 2 * (S & 1) + (S >> 1);
+      const uint32_t hv = idx == 0 ? r.mt.x : (idx == 1 ? r.mt.y : (idx == 2 ? r.mt.z : r.mt.w));
+      const float d = h2f((uint16_t)(r.dw >> (16 * dpar)));
+      const float ds = d * (float)(int8_t)((r.scw >> (8 * idx)) & 0xff);
+      const int j0 = 2 * h;  // code words 2h, 2h + 1 of the chunk
+      f = pf_dq8(w0 | (((hv >> (2 * j0)) & 0x03030303u) << 4), w1 | (((hv >> (2 * j0 + 2)) & 0x03030303u) << 4), ds,
+                 32.f * ds);
+    } else {  // Q4_K: sub-block 2g (S < 2) or 2g + 1
+      const float d = h2f((uint16_t)(r.mt.x & 0xffff)), dmin = h2f((uint16_t)(r.mt.x >> 16));
+      const uint32_t fl = kq_field(r.mt.y, r.mt.z, r.mt.w, kt & 3);
+      constexpr int sb = S >> 1;
+      const float ds = d * (float)((fl >> (6 * sb)) & 63), dm = dmin * (float)((fl >> (12 + 6 * sb)) & 63);
+      f = pf_dq8(w0, w1, ds, dm);
+    }
+  }
+  return f;
+}
+
+template <int QT, int BM, int NW, int NS, int EPI, int PROBE = 0>
+__device__ __forceinline__ void pf_body32(const GemmQArgs& a, int m0, int n0, int seg, int kt0, int kt1, int S) {
+  constexpr int BN = NW * 32, MT = BM / 32;
+  using L = PfLayout<QT, BM, BN>;
+  extern __shared__ __attribute__((aligned(16))) uint8_t pf_smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  QWeight w;
+  w.qtype = QT;
+  w.rows = seg == 0 ? a.seg[0].rows : (seg == 1 ? a.seg[1].rows : a.seg[2].rows);
+  w.cols = a.K;
+  w.pad_ = 0;
+  w.p0 = seg == 0 ? a.seg[0].p0 : (seg == 1 ? a.seg[1].p0 : a.seg[2].p0);
+  w.p1 = seg == 0 ? a.seg[0].p1 : (seg == 1 ? a.seg[1].p1 : a.seg[2].p1);
+  w.p2 = seg == 0 ? a.seg[0].p2 : (seg == 1 ? a.seg[1].p2 : a.seg[2].p2);
+  w.p3 = seg == 0 ? a.seg[0].p3 : (seg == 1 ? a.seg[1].p3 : a.seg[2].p3);
+  const int wrow0 = n0 - (seg == 0 ? a.seg_n0[0] : (seg == 1 ? a.seg_n0[1] : a.seg_n0[2]));
+  const int nbk = a.K >> 8;
+  const int r32 = lane & 31, h = lane >> 5;
+  const int col = wv * 32 + r32;  // this lane's tile column
+
+  gf32x16 acc[MT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[i][e] = 0.f;
+
+  constexpr int PH = (L::TI + NW - 1) / NW, PLO = L::TI / NW;
+  const bool many = (L::TI % NW == 0) || wv < L::TI % NW;
+  const int nk = kt1 - kt0;
+  PfDma<QT, BM, BN, NW> dma;
+  const uint32_t lds0 = __builtin_amdgcn_readfirstlane(pf_lds_addr(pf_smem));
+  dma.init(a, wrow0, m0, wv);
+#pragma unroll
+  for (int p = 0; p < NS - 1; ++p)
+    if (p < nk) dma.issue(a, w, kt0 + p, lds0 + p * L::SLOT, wv);
+
+  int cur = 0;
+  for (int t = 0; t < nk; ++t) {
+    if constexpr (PROBE & 1) {
+    } else if constexpr (NS == 3) {
+      if (t + 1 < nk) {
+        if (many) pf_vmcnt<PH>(); else pf_vmcnt<PLO>();
+      } else {
+        pf_vmcnt<0>();
+      }
+    } else {
+      static_assert(NS == 2, "2 or 3 slots");
+      pf_vmcnt<0>();
+    }
+    if constexpr (!(PROBE & 8)) pf_barrier();
+    const bool refill = !(PROBE & 4) && t + NS - 1 < nk;
+    const uint32_t nslot = lds0 + (cur == 0 ? NS - 1 : cur - 1) * L::SLOT;
+    const int knext = kt0 + t + NS - 1;
+    const uint8_t* slot = pf_smem + cur * L::SLOT;
+    const int kt = kt0 + t;
+    const int dpar = L::Q6 ? (int)(((uint32_t)(wrow0 + col) * (uint32_t)nbk + (uint32_t)(kt >> 2)) & 1u) : 0;
+    PfBRaw32 raw;
+    pf_braw32<QT, BM, BN>(slot, col, h, raw);
+    gbf16x8 fa[MT], fb[MT], bf[4];
+    auto ldA = [&](gbf16x8(&f)[MT], int sp) __attribute__((always_inline)) {
+#pragma unroll
+      for (int i = 0; i < MT; ++i) {
+        const int row = 32 * i + r32;
+        const uint4 av = *(const uint4*)(slot + row * 128 + (((2 * sp + h) ^ ((row >> 1) & 7)) << 4));
+        __builtin_memcpy(&f[i], &av, 16);
+      }
+    };
+    ldA(fa, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    bf[0] = pf_bdec32<QT, 0>(raw, h, kt, dpar);
+    __builtin_amdgcn_sched_barrier(0);
+    // phase sp: next substep's A reads, one share of the refill DMA, the next fragment's decode, the MFMAs
+    static_for<4>([&](auto pc) {
+      constexpr int sp = decltype(pc)::value;
+      if constexpr (sp + 1 < 4) {
+        if constexpr (sp % 2 == 0) ldA(fb, sp + 1);
+        else ldA(fa, sp + 1);
+      }
+      if (refill) dma.template issue<sp, 4>(a, w, knext, nslot, wv);
+      if constexpr (sp + 1 < 4) bf[sp + 1] = pf_bdec32<QT, sp + 1>(raw, h, kt, dpar);
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+        acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(sp % 2 == 0 ? fa[i] : fb[i], bf[sp], acc[i], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    });
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    cur = cur == NS - 1 ? 0 : cur + 1;
+  }
+
+  // epilogue -- C/D map of the 32x32 accumulator: col = lane & 31, row = (e & 3) + 8 (e >> 2) + 4 h
+  const int n = n0 + col;
+#pragma unroll
+  for (int i = 0; i < MT; ++i) {
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int m = m0 + 32 * i + (e & 3) + 8 * (e >> 2) + 4 * h;
+      const float v = acc[i][e];
+      if constexpr (EPI == GEPI_SWIGLU_BF16) {
+        const float up = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));
+        if (m < a.M && !(r32 & 1)) a.C16[(size_t)m * a.ldc + (n >> 1)] = f32_to_bf16(v / (1.f + __expf(-v)) * up);
+      } else if (m < a.M) {
+        float* cp = a.C + (size_t)m * a.ldc + n;
+        if (S > 1) unsafeAtomicAdd(cp, v);
+        else if constexpr (EPI == GEPI_ACCUM) *cp += v;
+        else *cp = v;
+      }
+    }
+  }
+}
+
+
+// ==== pf4: 4 waves (one per SIMD) x WC columns each, 32x32x16 MFMA, accumulators in AGPRs ============
+// Round-5 probes (tools/bench_gemm.py --pf-probe + rocprofv3 PMC, gate/up M = 2048): with 8 waves the
+// two waves of a SIMD race for its matrix pipe, the leader then idles at every per-step barrier
+// (SQ_WAIT_ANY 148M vs 55M quad-cycles without the barrier) while the step head -- fragment reads
+// and the B decode -- ran with the pipe idle; the runtime piece selection of the shared DMA added
+// ~68 SALU per wave-step.  Here each wave owns its SIMD, DMAs its OWN weight columns (so it can
+// wait for, read and decode step t+1's B fragments with its own vmcnt, before the barrier, inside
+// step t's last phases) and every DMA piece is compile-time: one vmcnt immediate per wave.
+template <int QT, int BM, int WC>
+struct Pf4Layout {
+  static constexpr bool Q6 = QT == QT_Q6_K, BF = QT == QT_BF16;
+  static constexpr int A_BYTES = BM * 128;
+  static constexpr int CODE = BF ? WC * 128 : WC * 32;       // per wave: bf16 rows / 2 code chunks per column
+  static constexpr int META = BF ? 0 : (WC * 16 > 1024 ? WC * 16 : 1024);  // Q4_K record / Q6_K high bits
+  static constexpr int SC = Q6 ? 256 : 0, DW = Q6 ? 256 : 0;  // Q6_K int8 scales / d dword (4-B pieces)
+  static constexpr int WB = CODE + META + SC + DW;            // one wave's weight bytes per slot
+  static constexpr int OFF_B = A_BYTES;
+  static constexpr int SLOT = (A_BYTES + 4 * WB + 255) / 256 * 256;
+  static constexpr int NS = 3 * SLOT <= 160 * 1024 ? 3 : 2;
+  static constexpr int NA = BM / 32, NCODE = CODE / 1024, NMETA = META / 1024, NSC = SC / 256, ND = DW / 256;
+  static constexpr int PW = NA + NCODE + NMETA + NSC + ND;    // DMA instructions per wave per slot
+  static_assert(CODE % 1024 == 0 && WC * 4 <= 256 && PW <= 31, "pf4 slot");
+};
+
+template <int QT, int BM, int WC>
+struct Pf4Dma {
+  using L = Pf4Layout<QT, BM, WC>;
+  uint32_t off[L::PW];
+
+  __device__ __forceinline__ void init(const GemmQArgs& a, int wcol0, int m0, int wv) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t nbk = (uint32_t)a.K >> 8;
+    static_for<L::PW>([&](auto ic) {
+      constexpr int i = decltype(ic)::value;
+      uint32_t o;
+      if constexpr (i < L::NA) {  // A piece j = 4i + wv: unit p -> row p>>3, logical unit (p&7) ^ ((row>>1)&7)
+        const int p = 64 * (4 * i + wv) + lane, row = p >> 3, c = (p & 7) ^ ((row >> 1) & 7);
+        const int m = min(m0 + row, a.M - 1);
+        o = ((uint32_t)m * (uint32_t)a.lda + (uint32_t)(c * 8)) * 2u;
+      } else if constexpr (i < L::NA + L::NCODE) {
+        const int p = 64 * (i - L::NA) + lane;
+        if constexpr (L::BF) {
+          const int col = p >> 3, c = (p & 7) ^ ((col >> 1) & 7);
+          o = ((uint32_t)(wcol0 + col) * (uint32_t)a.K + (uint32_t)(c * 8)) * 2u;
+        } else {
+          const int col = p >> 1, hh = p & 1;
+          o = (uint32_t)(wcol0 + col) * nbk * 128u + (uint32_t)hh * 16u;
+        }
+      } else if constexpr (i < L::NA + L::NCODE + L::NMETA) {
+        const uint32_t row = (uint32_t)(wcol0 + (lane & (WC - 1)));
+        o = L::Q6 ? row * nbk * 64u : row * nbk * 16u;
+      } else if constexpr (i < L::NA + L::NCODE + L::NMETA + L::NSC) {
+        o = (uint32_t)(wcol0 + (lane & (WC - 1))) * nbk * 16u;
+      } else {
+        o = (uint32_t)(wcol0 + (lane & (WC - 1))) * nbk;
+      }
+      off[i] = o;
+    });
+  }
+
+  // K-step kt into the slot at LDS byte address dst (wave-uniform).  PROBE 16: weight pieces read
+  // contiguous 1 KB (wrong data; coalescing probe), PROBE 32: no weight pieces (timing only)
+  template <int PROBE = 0>
+  __device__ __forceinline__ void issue(const GemmQArgs& a, const QWeight& w, int kt, uint32_t dst, int wv) const {
+    const uint32_t wb = dst + L::OFF_B + (uint32_t)wv * L::WB;
+    static_for<L::PW>([&](auto ic) {
+      constexpr int i = decltype(ic)::value;
+      if constexpr ((PROBE & 32) && i >= L::NA) return;
+      if constexpr ((PROBE & 16) && i >= L::NA) {
+        pf_glds16(w.p0 + kt * 4096 + (i - L::NA) * 1024 + (threadIdx.x & 63) * 16 + wv * 65536, wb + (i - L::NA) * 256);
+        return;
+      }
+      if constexpr (i < L::NA) {
+        pf_glds16((const uint8_t*)a.A + kt * 128 + off[i], dst + (4 * i + wv) * 1024);
+      } else if constexpr (i < L::NA + L::NCODE) {
+        pf_glds16(w.p0 + (L::BF ? kt * 128 : kt * 32) + off[i], wb + (i - L::NA) * 1024);
+      } else if constexpr (i < L::NA + L::NCODE + L::NMETA) {
+        pf_glds16(w.p1 + (L::Q6 ? kt * 16 : (kt >> 2) * 16) + off[i], wb + L::CODE);
+      } else if constexpr (i < L::NA + L::NCODE + L::NMETA + L::NSC) {
+        pf_glds4(w.p2 + kt * 4 + off[i], wb + L::CODE + L::META);
+      } else {
+        pf_glds4(w.p3 + (((off[i] + (uint32_t)(kt >> 2)) >> 1) << 2), wb + L::CODE + L::META + L::SC);
+      }
+    });
+  }
+};
+
+// raw B bytes of tile column cl (0..WC-1 of this wave) for lane half h
+template <int QT, int BM, int WC>
+__device__ __forceinline__ void pf4_braw(const uint8_t* wbase, int cl, int h, PfBRaw32& r) {
+  using L = Pf4Layout<QT, BM, WC>;
+  if constexpr (L::BF) {
+    const uint8_t* row = wbase + cl * 128;
+    const int x = (cl >> 1) & 7;
+    r.mt = *(const uint4*)(row + (((0 + h) ^ x) << 4));
+    r.b1 = *(const uint4*)(row + (((2 + h) ^ x) << 4));
+    r.b2 = *(const uint4*)(row + (((4 + h) ^ x) << 4));
+    r.b3 = *(const uint4*)(row + (((6 + h) ^ x) << 4));
+  } else {
+    r.c0 = *(const uint2*)(wbase + cl * 32 + 8 * h);
+    r.c1 = *(const uint2*)(wbase + cl * 32 + 16 + 8 * h);
+    r.mt = *(const uint4*)(wbase + L::CODE + cl * 16);
+    if constexpr (L::Q6) {
+      r.scw = *(const uint32_t*)(wbase + L::CODE + L::META + cl * 4);
+      r.dw = *(const uint32_t*)(wbase + L::CODE + L::META + L::SC + cl * 4);
+    }
+  }
+}
+
+template <int QT, int BM, int WC, int EPI, int PROBE = 0>
+__device__ __forceinline__ void pf4_body(const GemmQArgs& a, int m0, int n0, int seg, int kt0, int kt1, int S) {
+  using L = Pf4Layout<QT, BM, WC>;
+  constexpr int MT = BM / 32, CT = WC / 32, NS = L::NS, PW = L::PW;
+  extern __shared__ __attribute__((aligned(16))) uint8_t pf_smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  QWeight w;
+  w.qtype = QT;
+  w.rows = seg == 0 ? a.seg[0].rows : (seg == 1 ? a.seg[1].rows : a.seg[2].rows);
+  w.cols = a.K;
+  w.pad_ = 0;
+  w.p0 = seg == 0 ? a.seg[0].p0 : (seg == 1 ? a.seg[1].p0 : a.seg[2].p0);
+  w.p1 = seg == 0 ? a.seg[0].p1 : (seg == 1 ? a.seg[1].p1 : a.seg[2].p1);
+  w.p2 = seg == 0 ? a.seg[0].p2 : (seg == 1 ? a.seg[1].p2 : a.seg[2].p2);
+  w.p3 = seg == 0 ? a.seg[0].p3 : (seg == 1 ? a.seg[1].p3 : a.seg[2].p3);
+  const int wcol0 = n0 - (seg == 0 ? a.seg_n0[0] : (seg == 1 ? a.seg_n0[1] : a.seg_n0[2])) + wv * WC;
+  const uint32_t nbk = (uint32_t)a.K >> 8;
+  const int r32 = lane & 31, h = lane >> 5;
+
+  gf32x16 acc[MT][CT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int c = 0; c < CT; ++c)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][c][e] = 0.f;
+
+  const int nk = kt1 - kt0;
+  Pf4Dma<QT, BM, WC> dma;
+  const uint32_t lds0 = __builtin_amdgcn_readfirstlane(pf_lds_addr(pf_smem));
+  dma.init(a, wcol0, m0, wv);
+  // Pipeline: NS slots, all NS filled ahead.  The barrier B(t+1) sits inside step t's last phase,
+  // between its two MFMA halves: by then every wave has waited for its own step-(t+1) pieces
+  // (phase 1) and holds step t's last fragments in registers, so slot t is free for DMA(t + NS) and
+  // step t+1's first A reads fly under the remaining MFMAs.  The loop is branch-free (a branch splits
+  // the scheduling region and, here, made the allocator shuttle accumulators between AGPRs and
+  // VGPRs): past the last step the DMA re-loads step nk-1 into the free slot and the decode reads a
+  // stale slot, neither ever consumed; every DMA is drained before the epilogue.
+  const int klast = kt1 - 1;
+#pragma unroll
+  for (int p = 0; p < NS; ++p) dma.template issue<PROBE>(a, w, min(kt0 + p, klast), lds0 + p * L::SLOT, wv);
+
+  // B fragments: bf[c][s] is consumed by phase s; the next step's fragment s is decoded into it in
+  // the phase after (s = 0..2 in phases 1..3 of this step, s = 3 in phase 0 of the next), from raw
+  // bytes read once per column in phase 1 -- one fragment per column per phase, no second set.
+  gbf16x8 bf[CT][4], fa[MT], fb[MT];
+  PfBRaw32 raw[CT];
+  int rkt = kt0;  // K-step of raw
+  auto read_raw = [&](const uint8_t* sl, int kt) __attribute__((always_inline)) {
+#pragma unroll
+    for (int c = 0; c < CT; ++c) pf4_braw<QT, BM, WC>(sl + L::OFF_B + wv * L::WB, 32 * c + r32, h, raw[c]);
+    rkt = kt;
+  };
+  auto dec = [&](auto sc) __attribute__((always_inline)) {
+    constexpr int S4 = decltype(sc)::value;
+#pragma unroll
+    for (int c = 0; c < CT; ++c) {
+      const int cl = 32 * c + r32;
+      const int dpar = L::Q6 ? (int)(((uint32_t)(wcol0 + cl) * nbk + (uint32_t)(rkt >> 2)) & 1u) : 0;
+      bf[c][S4] = pf_bdec32<QT, S4>(raw[c], h, rkt, dpar);
+      // pinned here: LLVM otherwise sinks the arithmetic to its first use (the next step, past the
+      // barrier), where it ran serially with the matrix pipe idle
+      asm volatile("" : "+v"(bf[c][S4]));
+    }
+  };
+  auto ldA = [&](const uint8_t* sl, gbf16x8(&f)[MT], int sp) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+      const int row = 32 * i + r32;
+      const uint4 av = *(const uint4*)(sl + row * 128 + (((2 * sp + h) ^ ((row >> 1) & 7)) << 4));
+      __builtin_memcpy(&f[i], &av, 16);
+    }
+  };
+  auto mfma_range = [&](const gbf16x8(&f)[MT], int sp, int k0, int k1) __attribute__((always_inline)) {
+#pragma unroll
+    for (int k = 0; k < MT * CT; ++k) {
+      if (k < k0 || k >= k1) continue;
+      const int c = k / MT, i = k % MT;
+      acc[i][c] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f[i], bf[c][sp], acc[i][c], 0, 0, 0);
+    }
+  };
+  constexpr int NMF = MT * CT, HALF = NMF / 2;
+  // step kt0's own pieces (NS - 1 younger steps in flight)
+  if constexpr (!(PROBE & 1)) {
+    if constexpr (NS == 3) pf_vmcnt<2 * PW>(); else pf_vmcnt<PW>();
+  }
+  read_raw(pf_smem, kt0);
+  dec(std::integral_constant<int, 0>{});
+  dec(std::integral_constant<int, 1>{});
+  dec(std::integral_constant<int, 2>{});
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  pf_barrier();
+  ldA(pf_smem, fa, 0);
+
+  int cur = 0;
+  for (int t = 0; t < nk; ++t) {
+    const uint8_t* slot = pf_smem + cur * L::SLOT;
+    const int nxt = cur == NS - 1 ? 0 : cur + 1;
+    __builtin_amdgcn_sched_barrier(0);
+    // phase 0: step t's fragment 3
+    ldA(slot, fb, 1);
+    dec(std::integral_constant<int, 3>{});
+    mfma_range(fa, 0, 0, NMF);
+    __builtin_amdgcn_sched_barrier(0);
+    // phase 1: own step-(t+1) pieces landed (NS - 2 younger steps in flight) -> raw bytes, fragment 0
+    ldA(slot, fa, 2);
+    if constexpr (!(PROBE & 1)) {
+      if constexpr (NS == 3) pf_vmcnt<PW>(); else pf_vmcnt<0>();
+    }
+    read_raw(pf_smem + nxt * L::SLOT, kt0 + t + 1);
+    dec(std::integral_constant<int, 0>{});
+    mfma_range(fb, 1, 0, NMF);
+    __builtin_amdgcn_sched_barrier(0);
+    // phase 2
+    ldA(slot, fb, 3);
+    dec(std::integral_constant<int, 1>{});
+    mfma_range(fa, 2, 0, NMF);
+    __builtin_amdgcn_sched_barrier(0);
+    // phase 3: half the MFMAs; B(t+1); step t+1's first reads, DMA(t + NS) into slot t, fragment 2
+    // of step t+1, under the other half
+    mfma_range(fb, 3, 0, HALF);
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if constexpr (!(PROBE & 8)) pf_barrier();
+    ldA(pf_smem + nxt * L::SLOT, fa, 0);
+    if constexpr (!(PROBE & 4)) dma.template issue<PROBE>(a, w, min(kt0 + t + NS, klast), lds0 + cur * L::SLOT, wv);
+    dec(std::integral_constant<int, 2>{});
+    mfma_range(fb, 3, HALF, NMF);
+    cur = nxt;
+  }
+  pf_vmcnt<0>();  // no LDS-DMA may land after this workgroup's LDS is released
+
+  // epilogue -- C/D map of the 32x32 accumulator: col = lane & 31, row = (e & 3) + 8 (e >> 2) + 4 h
+#pragma unroll
+  for (int c = 0; c < CT; ++c) {
+    const int n = n0 + wv * WC + 32 * c + r32;
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int m = m0 + 32 * i + (e & 3) + 8 * (e >> 2) + 4 * h;
+        const float v = acc[i][c][e];
+        if constexpr (EPI == GEPI_SWIGLU_BF16) {
+          const float up = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));
+          if (m < a.M && !(r32 & 1)) a.C16[(size_t)m * a.ldc + (n >> 1)] = f32_to_bf16(v / (1.f + __expf(-v)) * up);
+        } else if (m < a.M) {
+          float* cp = a.C + (size_t)m * a.ldc + n;
+          if (S > 1) unsafeAtomicAdd(cp, v);
+          else if constexpr (EPI == GEPI_ACCUM) *cp += v;
+          else *cp = v;
+        }
+      }
+    }
+  }
+}
+
+template <int QT0, int QT1, int BM, int WC, int EPI, int PROBE = 0>
+__global__ void __launch_bounds__(256) gemm_pf4_kernel(GemmQArgs a) {
+  constexpr int BN = 4 * WC;
+  const int nN = a.N / BN, nM = (a.M + BM - 1) / BM, total = nN * nM;
+  const int L = xcd_remap(blockIdx.x, total);
+  const int tn = L % nN, tm = L / nN;
+  const int m0 = tm * BM, n0 = tn * BN;
+  int seg = 0;
+  if (a.nseg > 1 && n0 >= a.seg_n0[1]) seg = 1;
+  if (a.nseg > 2 && n0 >= a.seg_n0[2]) seg = 2;
+  const int S = gridDim.y, nk_all = a.K / 64;
+  const int kt0 = (int)((long)blockIdx.y * nk_all / S), kt1 = (int)((long)(blockIdx.y + 1) * nk_all / S);
+  if constexpr (QT0 != QT1) {
+    if (seg == a.nseg - 1) {
+      pf4_body<QT1, BM, WC, EPI, PROBE>(a, m0, n0, seg, kt0, kt1, S);
+      return;
+    }
+  }
+  pf4_body<QT0, BM, WC, EPI, PROBE>(a, m0, n0, seg, kt0, kt1, S);
+}
+
+template <int QT0, int QT1, int BM, int WC>
+constexpr int pf4_lds_bytes() {
+  using L0 = Pf4Layout<QT0, BM, WC>;
+  using L1 = Pf4Layout<QT1, BM, WC>;
+  return L0::NS * L0::SLOT > L1::NS * L1::SLOT ? L0::NS * L0::SLOT : L1::NS * L1::SLOT;
+}
+
+template <int QT0, int QT1, int BM, int WC>
+void pf4_launch(const GemmQArgs& a, int S, hipStream_t st) {
+  constexpr int lds = pf4_lds_bytes<QT0, QT1, BM, WC>();
+  static_assert(lds <= 160 * 1024, "LDS");
+  const dim3 grid((a.N / (4 * WC)) * ((a.M + BM - 1) / BM), S), block(256);
+  switch (a.epi) {
+    case GEPI_STORE: hipLaunchKernelGGL((gemm_pf4_kernel<QT0, QT1, BM, WC, GEPI_STORE>), grid, block, lds, st, a); break;
+    case GEPI_ACCUM: hipLaunchKernelGGL((gemm_pf4_kernel<QT0, QT1, BM, WC, GEPI_ACCUM>), grid, block, lds, st, a); break;
+    default: hipLaunchKernelGGL((gemm_pf4_kernel<QT0, QT1, BM, WC, GEPI_SWIGLU_BF16>), grid, block, lds, st, a); break;
+  }
+}
+
+// One launch for every tile of a (possibly mixed-format) segment stack: tiles of the last segment
+// run the QT1 body (the Q4_K_M QKV stack: Q|K Q4_K, V Q6_K).  gridDim.y = K slices (atomic adds).
+#ifndef AIOS_PF_MF
+#define AIOS_PF_MF 32  // MFMA shape of the production body (16: the 16x16x32 body)
+#endif
+template <int QT0, int QT1, int BM, int NW, int NS, int EPI, int PROBE = 0, int MF = AIOS_PF_MF>
+__global__ void __launch_bounds__(NW * 64) gemm_pf_kernel(GemmQArgs a) {
+  constexpr int BN = NW * 32;
+  const int nN = a.N / BN, nM = (a.M + BM - 1) / BM, total = nN * nM;
+  const int L = xcd_remap(blockIdx.x, total);
+  const int tn = L % nN, tm = L / nN;
+  const int m0 = tm * BM, n0 = tn * BN;
+  int seg = 0;
+  if (a.nseg > 1 && n0 >= a.seg_n0[1]) seg = 1;
+  if (a.nseg > 2 && n0 >= a.seg_n0[2]) seg = 2;
+  const int S = gridDim.y, nk_all = a.K / 64;
+  const int kt0 = (int)((long)blockIdx.y * nk_all / S), kt1 = (int)((long)(blockIdx.y + 1) * nk_all / S);
+  if constexpr (QT0 != QT1) {
+    if (seg == a.nseg - 1) {
+      if constexpr (MF == 32) pf_body32<QT1, BM, NW, NS, EPI, PROBE>(a, m0, n0, seg, kt0, kt1, S);
+      else pf_body<QT1, BM, NW, NS, EPI, PROBE>(a, m0, n0, seg, kt0, kt1, S);
+      return;
+    }
+  }
+  if constexpr (MF == 32) pf_body32<QT0, BM, NW, NS, EPI, PROBE>(a, m0, n0, seg, kt0, kt1, S);
+  else pf_body<QT0, BM, NW, NS, EPI, PROBE>(a, m0, n0, seg, kt0, kt1, S);
+}
+
+// slot bytes of a launch (the larger format's) and its slot count: 3 where they fit in 160 KB
+template <int QT0, int QT1, int BM, int NW>
+constexpr int pf_slot_bytes() {
+  return PfLayout<QT0, BM, NW * 32>::SLOT > PfLayout<QT1, BM, NW * 32>::SLOT ? PfLayout<QT0, BM, NW * 32>::SLOT
+                                                                             : PfLayout<QT1, BM, NW * 32>::SLOT;
+}
+template <int QT0, int QT1, int BM, int NW>
+constexpr int pf_slots() {
+  return 3 * pf_slot_bytes<QT0, QT1, BM, NW>() <= 160 * 1024 ? 3 : 2;
+}
+
+// host: launch one instantiation (grid = tiles x S)
+template <int QT0, int QT1, int BM, int NW>
+void pf_launch(const GemmQArgs& a, int S, hipStream_t st) {
+  constexpr int BN = NW * 32;
+  constexpr int NS = pf_slots<QT0, QT1, BM, NW>();
+  constexpr int lds = NS * pf_slot_bytes<QT0, QT1, BM, NW>();
+  static_assert(lds <= 160 * 1024, "LDS");
+  const dim3 grid((a.N / BN) * ((a.M + BM - 1) / BM), S), block(NW * 64);
+  switch (a.epi) {
+    case GEPI_STORE: hipLaunchKernelGGL((gemm_pf_kernel<QT0, QT1, BM, NW, NS, GEPI_STORE>), grid, block, lds, st, a); break;
+    case GEPI_ACCUM: hipLaunchKernelGGL((gemm_pf_kernel<QT0, QT1, BM, NW, NS, GEPI_ACCUM>), grid, block, lds, st, a); break;
+    default: hipLaunchKernelGGL((gemm_pf_kernel<QT0, QT1, BM, NW, NS, GEPI_SWIGLU_BF16>), grid, block, lds, st, a); break;
+  }
+}
+
+// the tile set of one format pair (one translation unit each, compiled in parallel): BM x BN tiles,
+// BN = 4 waves x WC columns
+template <int QT0, int QT1>
+bool pf_launch_fmt(const GemmQArgs& a, int BM, int BN, int S, hipStream_t st) {
+#define PF_GO(bm, bn)                             \
+  if (BM == bm && BN == bn) {                     \
+    pf4_launch<QT0, QT1, bm, bn / 4>(a, S, st);   \
+    return true;                                  \
+  }
+  PF_GO(256, 256) PF_GO(128, 256) PF_GO(64, 256) PF_GO(256, 128) PF_GO(128, 128) PF_GO(64, 128)
+#undef PF_GO
+  return false;
+}
+
+}  // namespace aios

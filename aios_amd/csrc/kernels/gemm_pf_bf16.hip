@@ -1,0 +1,7 @@
+// Prefill GEMM instantiations for the (QT_BF16, QT_BF16) weight-format pair (gemm_pf.h); one translation unit
+// per pair so the tile set compiles in parallel.
+#include "gemm_pf.h"
+
+namespace aios {
+template bool pf_launch_fmt<QT_BF16, QT_BF16>(const GemmQArgs&, int, int, int, hipStream_t);
+}  // namespace aios

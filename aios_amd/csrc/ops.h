@@ -231,5 +231,9 @@ int gemm_skinny_cnt_len(int N);
 // output tiles of the skinny kernel for these args (0: not served by the skinny kernel)
 int gemm_skinny_ntile(const GemmQArgs& a);
 void launch_gemm_q(const GemmQArgs& a, hipStream_t st);
+// the prefill GEMM (kernels/gemm_pf.hip): true if it took the launch; its tile / split plan for a shape
+bool launch_gemm_pf(const GemmQArgs& a, hipStream_t st);
+void gemm_pf_plan(const GemmQArgs& a, int& bm, int& bn, int& s);
+bool gemm_pf_probe(const GemmQArgs& a, int probe, hipStream_t st);  // timing anatomy (tools only)
 
 }  // namespace aios

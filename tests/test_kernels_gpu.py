@@ -828,3 +828,96 @@ def test_gemv_lds_batched_qkv(E, mixed, B):
         assert torch.allclose(kc[s, :, p].float().cpu(), kr[0], atol=2e-2, rtol=1e-2)
         assert torch.allclose(vc[s, :, p].float().cpu(), vr[0], atol=2e-2, rtol=1e-2)
     assert int((kc != 0).sum()) == B * Hkv * hd and int((vc != 0).sum()) == B * Hkv * hd
+
+
+# ---- the prefill GEMM (gemm_pf.hip): LDS-DMA slots, weights dequantised once per workgroup tile ------
+PF_TILES = ["256x256", "128x256", "64x256", "256x128", "128x128", "64x128"]
+PF_SEGS = {
+    "q4k": [(GGMLType.Q4_K, 512)],
+    "q6k": [(GGMLType.Q6_K, 512)],
+    "mixed": [(GGMLType.Q4_K, 256), (GGMLType.Q4_K, 256), (GGMLType.Q6_K, 256)],  # Q4_K_M QKV stack
+    "bf16": [(GGMLType.BF16, 512)],
+}
+_pf_cache = {}
+
+
+def pf_mats(E, name, K):
+    key = (name, K)
+    if key not in _pf_cache:
+        mats, refs = zip(*[qmat(E, t, n, K, seed=100 + 7 * i + K, std=0.02) for i, (t, n) in enumerate(PF_SEGS[name])])
+        _pf_cache[key] = (list(mats), torch.cat(refs, 0))
+    return _pf_cache[key]
+
+
+@pytest.mark.parametrize("tile", PF_TILES)
+@pytest.mark.parametrize("fmt", list(PF_SEGS))
+@pytest.mark.parametrize("M", [33, 200, 512])
+@pytest.mark.parametrize("epi", ["store", "accum"])
+def test_gemm_pf_vs_unquantized(E, monkeypatch, tile, fmt, M, epi):
+    """Against the UNQUANTIZED fp32 product (exact dequantised weights x the fp32 activations): every
+    tile shape, partial last row tile (M = 33, 200), mixed-format segment stacks in one launch."""
+    monkeypatch.setenv("AIOS_GEMM_PF_TILE", tile)
+    K = 1024
+    mats, W = pf_mats(E, fmt, K)
+    N = W.shape[0]
+    if N % int(tile.split("x")[1]):
+        pytest.skip("tile does not divide N")
+    assert E.gemm_pf_plan(mats, M, E.GEPI_STORE, 1)[0] == int(tile.split("x")[0])
+    x = torch.randn(M, K, generator=torch.Generator().manual_seed(M))
+    A = x.to(torch.bfloat16).cuda()
+    base = 0.0 if epi == "store" else 2.0
+    C = torch.full((M, N), 5.0 if epi == "store" else 2.0, device="cuda")
+    E.gemm_q(A.data_ptr(), K, mats, M, C.data_ptr(), 0, N, E.GEPI_STORE if epi == "store" else E.GEPI_ACCUM,
+             stream(), 1)
+    torch.cuda.synchronize()
+    ref = x.double() @ W.double().T
+    got = C.cpu().double() - base
+    rel = float((got - ref).norm() / ref.norm())
+    assert rel < 6e-3, rel
+    per_row = ((got - ref).norm(dim=1) / ref.norm(dim=1)).max().item()
+    assert per_row < 1e-2, per_row
+
+
+@pytest.mark.parametrize("fmt", ["q4k", "mixed", "bf16"])
+@pytest.mark.parametrize("M,S", [(64, 2), (100, 3), (300, 4)])
+@pytest.mark.parametrize("epi", ["store", "accum"])
+def test_gemm_pf_split_k(E, monkeypatch, fmt, M, S, epi):
+    """split-K (gridDim.y slices, fp32 atomic adds; STORE zeroes its target first), K = 4096"""
+    monkeypatch.setenv("AIOS_GEMM_PF_TILE", "128x256")
+    K = 4096
+    mats, W = pf_mats(E, fmt, K)
+    N = W.shape[0]
+    assert E.gemm_pf_plan(mats, M, E.GEPI_ACCUM, S)[2] == S
+    x = torch.randn(M, K, generator=torch.Generator().manual_seed(S))
+    A = x.to(torch.bfloat16).cuda()
+    C = torch.full((M, N), 1.0, device="cuda")
+    E.gemm_q(A.data_ptr(), K, mats, M, C.data_ptr(), 0, N, E.GEPI_STORE if epi == "store" else E.GEPI_ACCUM,
+             stream(), S)
+    torch.cuda.synchronize()
+    ref = x.double() @ W.double().T + (0.0 if epi == "store" else 1.0)
+    rel = float((C.cpu().double() - ref).norm() / ref.norm())
+    assert rel < 6e-3, rel
+
+
+@pytest.mark.parametrize("tile", ["256x256", "128x256", "64x128"])
+@pytest.mark.parametrize("M", [40, 300])
+def test_gemm_pf_swiglu(E, monkeypatch, tile, M):
+    monkeypatch.setenv("AIOS_GEMM_PF_TILE", tile)
+    K, N = 1024, 512
+    m, W = qmat(E, GGMLType.Q4_K, N, K, seed=93, std=0.05)
+    A = torch.randn(M, K, device="cuda").to(torch.bfloat16)
+    out = torch.zeros(M, N // 2, dtype=torch.bfloat16, device="cuda")
+    E.gemm_q(A.data_ptr(), K, [m], M, 0, out.data_ptr(), N // 2, E.GEPI_SWIGLU_BF16, stream())
+    torch.cuda.synchronize()
+    y = A.float().cpu() @ W.to(torch.bfloat16).float().T
+    ref = torch.nn.functional.silu(y[:, 0::2]) * y[:, 1::2]
+    assert torch.allclose(out.float().cpu(), ref, atol=2e-2, rtol=2e-2), (out.float().cpu() - ref).abs().max()
+
+
+def test_gemm_pf_serves_prefill_shapes(E):
+    """The default plan takes every prefill launch of the Q4_K_M / bf16 stacks (no fallback kernel)."""
+    for fmt in PF_SEGS:
+        mats, _ = pf_mats(E, fmt, 1024)
+        for M in (33, 64, 128, 512, 2048):
+            bm, bn, s = E.gemm_pf_plan(mats, M, E.GEPI_ACCUM, 0)
+            assert bm in (64, 128, 256) and bn in (128, 256) and s >= 1, (fmt, M, bm, bn, s)

@@ -46,17 +46,54 @@ def main():
     ap.add_argument("--json", default=None)
     ap.add_argument("--no-torch", action="store_true")
     ap.add_argument("--sweep", action="store_true", help="skinny kernel: RB x split-K sweep per shape")
+    ap.add_argument("--pf-sweep", action="store_true", help="prefill GEMM: tile x split-K sweep per shape")
+    ap.add_argument("--pf-probe", action="store_true", help="prefill GEMM 256x256 Q4_K: timing-anatomy probes")
+    ap.add_argument("--shapes", default=None, help="comma list of shape names (default: all)")
     args = ap.parse_args()
     E = native.require()
     st = torch.cuda.current_stream().cuda_stream
     ms = [int(x) for x in args.ms.split(",")]
     out = open(args.json, "w") if args.json else None
     for name, N, K, t, epi in SHAPES:
+        if args.shapes and name not in args.shapes.split(","):
+            continue
         nbytes = N * K // 256 * BLOCK_INFO[t][1]
         raw = np.random.default_rng(0).integers(0, 256, nbytes, dtype=np.uint8)
         m = E.QMatrix(int(t), N, K, raw)
         m.fill_random(1, 0.02)
         wb = torch.randn(N, K, device="cuda", dtype=torch.bfloat16) * 0.02 if not args.no_torch else None
+        if args.pf_probe:
+            if t != GGMLType.Q4_K:
+                continue
+            for M in ms:
+                A = torch.randn(M, K, device="cuda").to(torch.bfloat16)
+                C = torch.zeros(M, N, device="cuda")
+                for probe in (200, 201, 204, 208, 213, 216, 217, 232, 233):
+                    us = time_fn(lambda: E.gemm_pf_probe(A.data_ptr(), K, m, M, C.data_ptr(), probe, st), reps=10)
+                    row = dict(probe=probe, shape=name, M=M, us=round(us, 2), tflops=round(2 * M * N * K / us / 1e6, 1))
+                    print(json.dumps(row), flush=True)
+            continue
+        if args.pf_sweep:
+            for M in ms:
+                A = torch.randn(M, K, device="cuda").to(torch.bfloat16)
+                C = torch.zeros(M, N, device="cuda")
+                C16 = torch.zeros(M, N // 2, device="cuda", dtype=torch.bfloat16)
+                plan = E.gemm_pf_plan([m], M, E.GEPI_ACCUM, 0)
+                for tile in ("256x256", "128x256", "64x256", "256x128", "128x128", "64x128"):
+                    os.environ["AIOS_GEMM_PF_TILE"] = tile
+                    for S in ((1,) if epi == "swiglu" else (1, 2, 4, 8)):
+                        if epi == "swiglu":
+                            fn = lambda: E.gemm_q(A.data_ptr(), K, [m], M, 0, C16.data_ptr(), N // 2, E.GEPI_SWIGLU_BF16, st)
+                        else:
+                            fn = lambda: E.gemm_q(A.data_ptr(), K, [m], M, C.data_ptr(), 0, N, E.GEPI_ACCUM, st, S)
+                        us = time_fn(fn, reps=10)
+                        row = dict(pf=1, shape=name, M=M, tile=tile, S=S, us=round(us, 2),
+                                   tflops=round(2 * M * N * K / us / 1e6, 1), auto=list(plan))
+                        print(json.dumps(row), flush=True)
+                        if out:
+                            out.write(json.dumps(row) + "\n")
+                os.environ.pop("AIOS_GEMM_PF_TILE", None)
+            continue
         if args.sweep:
             for M in ms:
                 A = torch.randn(M, K, device="cuda").to(torch.bfloat16)
