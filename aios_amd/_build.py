@@ -39,7 +39,7 @@ def target_path() -> Path:
 
 def _sources():
     srcs = sorted((CSRC / "kernels").glob("*.hip")) + [CSRC / "engine.hip", CSRC / "grammar.cpp", CSRC / "rccl_comm.cpp",
-                                                      CSRC / "blas.cpp", CSRC / "bindings.cpp"]
+                                                      CSRC / "bindings.cpp"]
     return srcs
 
 
@@ -123,7 +123,7 @@ def build(verbose: bool = True, jobs: int | None = None) -> Path:
     if not out.exists() or out.stat().st_mtime < newest:
         tmp = out.with_suffix(".tmp.so")
         cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(tmp), *map(str, objs),
-               "-L/opt/rocm/lib", "-lrocprofiler-sdk-roctx", "-lhipblaslt", "-Wl,-rpath,/opt/rocm/lib"]
+               "-L/opt/rocm/lib", "-lrocprofiler-sdk-roctx", "-Wl,-rpath,/opt/rocm/lib"]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stderr[-6000:]}")

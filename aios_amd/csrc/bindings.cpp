@@ -242,8 +242,6 @@ PYBIND11_MODULE(_engine, m) {
       .def_property_readonly("kv_blocks_free", &Engine::kv_blocks_free)
       .def_property_readonly("kv_blocks_total", &Engine::kv_blocks_total)
       .def_property_readonly("norm_fused_parts", &Engine::norm_fused_parts)
-      .def_property_readonly("blas_prefill", &Engine::blas_prefill)
-      .def_property_readonly("blas_prefill_min_rows", &Engine::blas_prefill_min_rows)
       .def("capture_graphs", &Engine::capture_graphs, py::arg("max_b"), py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("stream", &Engine::stream_handle)
       .def_property_readonly("k_cache_ptr", &Engine::kv_cache_k)

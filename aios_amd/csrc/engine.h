@@ -16,7 +16,6 @@
 
 #include "common.h"
 #include "ops.h"
-#include "blas.h"
 
 namespace aios {
 
@@ -142,8 +141,6 @@ class Engine {
   int kv_blocks_free() const { return (int)free_blocks_.size(); }
   int kv_blocks_total() const { return kv_nblocks_; }
   int norm_fused_parts() const { return nrm_parts_; }  // 0: batched-decode RMSNorm not split into the GEMMs
-  bool blas_prefill() const { return blas_ != nullptr; }  // long prefill chunks on hipBLASLt (blas.h)
-  int blas_prefill_min_rows() const { return blas_min_rows_; }
   std::vector<int> block_table(int slot) const;
 
   // raw device pointers for tests / custom kernels
@@ -175,6 +172,7 @@ class Engine {
   float* upload_f32(const void* host, size_t n, int qt);
   QMat interleave_rows(const QMat& a, const QMat& b);
   void* dmalloc(size_t bytes);
+  void tune_prefill_gemm();  // measured prefill-GEMM plans for this model's projection shapes
   void allreduce(float* p, size_t n, float* residual);
   void lm_head(int B, const float* x, int ldx);  // logits_[B][V] (vocab-parallel aware)
 
@@ -242,20 +240,9 @@ class Engine {
   bf16_t* gm_xn16_ = nullptr;
   float* gm_npart_ = nullptr;
   int gm_nparts_ = 0;
-  // long prefill chunks (>= blas_min_rows_ tokens) through hipBLASLt against a resident bf16 copy of
-  // the projection weights (blas.h): per layer {QKV stacked [q+2kv][d], O [d][q], gate/up [2ff][d],
-  // down [d][ff]}; gate/up lands in fp32 (gm_gu32_) for the SwiGLU kernel
-  std::unique_ptr<BlasGemm> blas_;
-  std::vector<bf16_t*> w16_;  // 4 per layer
-  float* gm_gu32_ = nullptr;
-  int blas_min_rows_ = 256;
-  int blas_lo_ = 33, blas_hi_ = 128;  // AIOS_PREFILL_BLAS_WINDOW: shorter chunks on the library too
-  bool blas_rows(int n) const { return blas_ && (n >= blas_min_rows_ || (n >= blas_lo_ && n <= blas_hi_)); }
   const ArDevCtx* tp_fuse_ = nullptr;
   int tp_fuse_grid_ = 0;
   bool tp_fuse_gemv(GemvArgs a);  // EPI_TP_RESID launch when the engine serves the shape (else false)
-  size_t w16_bytes_ = 0;
-  void setup_blas_prefill();
   // batched decode through the skinny MFMA GEMM (B >= dec_gemm_min_b_): bf16 activation buffers
   // (MI355X, Mistral-7B Q4_K_M, tools/gpu_batch_ab.sh: B=2 GEMV 2.41 ms vs GEMM 3.25 ms, B=4 3.31 vs 3.26,
   // B=8 5.80 vs 3.37 -- the skinny GEMM's per-step dequant floor lost below 4 rows; after the split

@@ -1,5 +1,7 @@
 // Engine implementation -- see engine.h.
 #include "engine.h"
+
+#include <set>
 #include "comm.h"
 #include <cstdlib>
 #include <map>
@@ -649,66 +651,63 @@ void Engine::finalize() {
       }
     }
   }
-  setup_blas_prefill();
-  if (blas_) ws += w16_bytes_ + (size_t)gm_rows_ * 2 * cfg_.d_ff * 4;
   ws_bytes_ = ws;
   HIP_CHECK(hipDeviceSynchronize());
+  tune_prefill_gemm();
   finalized_ = true;
 }
 
-// Resident bf16 projection weights + hipBLASLt for prefill chunks of >= blas_min_rows_ tokens
-// (blas.h).  AIOS_PREFILL_BLAS=0 turns it off; the copy is made only when it fits comfortably:
-// <= AIOS_PREFILL_BF16_MAX_GB (default 48) and under a quarter of the free HBM at finalize (Mistral-7B
-// 14 GB, Llama-3-70B at TP=8 17.5 GB per rank; the 70B at TP=1 stays on the fused GEMM).
-void Engine::setup_blas_prefill() {
-  if (!gm_ok_) return;
-  if (const char* e = std::getenv("AIOS_PREFILL_BLAS"))
+// Measured prefill-GEMM plans (kernels/gemm_pf.hip): every distinct projection launch of this model
+// -- QKV stack, O, gate/up (SwiGLU), down, per weight-format signature -- timed over its candidate
+// tiles / K splits at M = 64 .. gm_rows_ (powers of two), the fastest kept per M bucket in the
+// process-wide plan cache (one tuning per shape per process; ~0.3 s for Mistral-7B).  Activations
+// are random bf16 (a zero fill clocks the chip differently).  AIOS_GEMM_PF_TUNE=0: model plans only.
+void Engine::tune_prefill_gemm() {
+  if (!gm_ok_ || cfg_.n_layers == 0) return;
+  if (const char* e = std::getenv("AIOS_GEMM_PF_TUNE"))
     if (std::atoi(e) == 0) return;
-  if (const char* e = std::getenv("AIOS_PREFILL_BLAS_MIN")) blas_min_rows_ = std::max(1, std::atoi(e));
-  // "lo,hi": chunks of lo..hi rows take the library too (the fused GEMM's 33..64-row tiles lose to
-  // it: 64 tokens 6.0 vs 4.9 ms, profiles/prefill_blas_r4.txt); "0" turns the window off
-  if (const char* e = std::getenv("AIOS_PREFILL_BLAS_WINDOW")) {
-    blas_lo_ = std::atoi(e);
-    const char* c = std::strchr(e, ',');
-    blas_hi_ = c ? std::atoi(c + 1) : 0;
+  const int d = cfg_.d_model, hd = cfg_.head_dim, qd = cfg_.n_heads * hd, kvd = cfg_.n_kv_heads * hd;
+  const int ff = cfg_.d_ff, G = gm_rows_, ldqkv = qd + 2 * kvd;
+  const bool tp = cfg_.tp_size > 1;
+  const size_t n = (size_t)G * std::max({d, qd, ff});
+  float* tmp = nullptr;
+  HIP_CHECK(hipMalloc(&tmp, n * 4));
+  fill_random_f32(tmp, n, 0x7u, 0.f, 1.f, stream_);
+  launch_f32_to_bf16(tmp, gm_a16_, (size_t)G * d, stream_);
+  launch_f32_to_bf16(tmp, gm_attn16_, (size_t)G * qd, stream_);
+  launch_f32_to_bf16(tmp, gm_ff16_, (size_t)G * ff, stream_);
+  std::set<std::string> seen;
+  for (int M = 64; M <= G; M *= 2) {
+    for (const LayerW& L : layers_) {
+      auto tune = [&](GemmQArgs& g, const char* what) {
+        std::string sig = std::string(what) + ":" + std::to_string(M);
+        for (int s = 0; s < g.nseg; ++s) sig += "," + std::to_string(g.seg[s].qtype);
+        if (!seen.insert(sig).second) return;
+        gemm_pf_autotune(g, stream_);
+      };
+      GemmQArgs g;
+      std::memset(&g, 0, sizeof(g));
+      g.A = gm_a16_; g.lda = d; g.M = M; g.K = d; g.nseg = 3;
+      g.seg[0] = L.wq.w; g.seg[1] = L.wk.w; g.seg[2] = L.wv.w;
+      g.seg_n0[0] = 0; g.seg_n0[1] = qd; g.seg_n0[2] = qd + kvd;
+      g.N = ldqkv; g.C = gm_qkv_; g.ldc = ldqkv; g.epi = GEPI_STORE;
+      tune(g, "qkv");
+      std::memset(&g, 0, sizeof(g));
+      g.A = gm_attn16_; g.lda = qd; g.M = M; g.K = qd; g.nseg = 1; g.seg[0] = L.wo.w; g.N = d; g.ldc = d;
+      if (tp) { g.C = gm_part_; g.epi = GEPI_STORE; } else { g.C = gm_x_; g.epi = GEPI_ACCUM; }
+      tune(g, "o");
+      std::memset(&g, 0, sizeof(g));
+      g.A = gm_a16_; g.lda = d; g.M = M; g.K = d; g.nseg = 1; g.seg[0] = L.wgu.w; g.N = 2 * ff;
+      g.C16 = gm_ff16_; g.ldc = ff; g.epi = GEPI_SWIGLU_BF16;
+      tune(g, "gu");
+      std::memset(&g, 0, sizeof(g));
+      g.A = gm_ff16_; g.lda = ff; g.M = M; g.K = ff; g.nseg = 1; g.seg[0] = L.wdown.w; g.N = d; g.ldc = d;
+      if (tp) { g.C = gm_part_; g.epi = GEPI_STORE; } else { g.C = gm_x_; g.epi = GEPI_ACCUM; }
+      tune(g, "down");
+    }
   }
-  if (gm_rows_ < blas_min_rows_) return;
-  const int d = cfg_.d_model, qd = cfg_.n_heads * cfg_.head_dim, kvd = cfg_.n_kv_heads * cfg_.head_dim;
-  const int ff = cfg_.d_ff;
-  for (const auto& L : layers_) {
-    if (L.wq.w.rows != qd || L.wk.w.rows != kvd || L.wv.w.rows != kvd || L.wq.w.cols != d || L.wk.w.cols != d ||
-        L.wv.w.cols != d || L.wo.w.rows != d || L.wo.w.cols != qd || L.wgu.w.rows != 2 * ff || L.wgu.w.cols != d ||
-        L.wdown.w.rows != d || L.wdown.w.cols != ff)
-      return;
-  }
-  const size_t per = ((size_t)(qd + 2 * kvd) * d + (size_t)d * qd + (size_t)2 * ff * d + (size_t)d * ff) * 2;
-  const size_t bytes = per * cfg_.n_layers;
-  double max_gb = 48.0;
-  if (const char* e = std::getenv("AIOS_PREFILL_BF16_MAX_GB")) max_gb = std::atof(e);
-  size_t fr = 0, tot = 0;
-  HIP_CHECK(hipMemGetInfo(&fr, &tot));
-  if ((double)bytes > max_gb * 1e9 || bytes > fr / 4) return;
-  auto b = std::make_unique<BlasGemm>();
-  if (!b->ok()) return;
-  w16_.assign((size_t)4 * cfg_.n_layers, nullptr);
-  for (int l = 0; l < cfg_.n_layers; ++l) {
-    const LayerW& L = layers_[l];
-    bf16_t* base = (bf16_t*)dmalloc(per);
-    bf16_t* wqkv = base;
-    bf16_t* wo = wqkv + (size_t)(qd + 2 * kvd) * d;
-    bf16_t* wgu = wo + (size_t)d * qd;
-    bf16_t* wdn = wgu + (size_t)2 * ff * d;
-    launch_dequant_bf16(L.wq.w, wqkv, stream_);
-    launch_dequant_bf16(L.wk.w, wqkv + (size_t)qd * d, stream_);
-    launch_dequant_bf16(L.wv.w, wqkv + (size_t)(qd + kvd) * d, stream_);
-    launch_dequant_bf16(L.wo.w, wo, stream_);
-    launch_dequant_bf16(L.wgu.w, wgu, stream_);
-    launch_dequant_bf16(L.wdown.w, wdn, stream_);
-    w16_[4 * l] = wqkv; w16_[4 * l + 1] = wo; w16_[4 * l + 2] = wgu; w16_[4 * l + 3] = wdn;
-  }
-  gm_gu32_ = (float*)dmalloc((size_t)gm_rows_ * 2 * ff * 4);
-  w16_bytes_ = bytes;
-  blas_ = std::move(b);
+  HIP_CHECK(hipStreamSynchronize(stream_));
+  HIP_CHECK(hipFree(tmp));
 }
 
 // TP: sum the row-parallel partials in `p` over the ranks and add the total into `residual`
@@ -1123,7 +1122,9 @@ void Engine::prefill_gemm(int slot, const std::vector<int>& tokens, int start_po
   static const bool short_fuse = !(std::getenv("AIOS_PREFILL_SHORT_FUSE") && std::atoi(std::getenv("AIOS_PREFILL_SHORT_FUSE")) == 0);
   for (int r0 = 0; r0 < T; r0 += gm_rows_) {
     const int n = std::min(gm_rows_, T - r0);
-    const bool sh = short_fuse && !tp && n <= 64 && !blas_rows(n);
+    // (the fused epilogues are the ring GEMM's: chunks of <= 32 rows; longer chunks take the prefill
+    // GEMM, kernels/gemm_pf.hip, with the plain epilogues)
+    const bool sh = short_fuse && !tp && n <= 32;
     const bool fnp = sh && gm_nparts_ > 0;
     for (int i = 0; i < n; ++i) hp[i] = start_pos + r0 + i;
     HIP_CHECK(hipMemcpyAsync(gm_tokens_, tokens.data() + r0, n * 4, hipMemcpyHostToDevice, stream_));
@@ -1158,9 +1159,7 @@ void Engine::prefill_gemm(int slot, const std::vector<int>& tokens, int start_po
         g.rope_cs = rope_cs_; g.pos = gm_pos_; g.slot = gm_slot_; g.block_table = d_bt_;
         g.q_out = gm_q_; g.k_cache = kc; g.v_cache = vc;
       }
-      // long chunks: hipBLASLt on the resident bf16 weights (blas.h); falls back per call
-      const bool lib = blas_rows(n);
-      if (!(lib && blas_->gemm(gm_a16_, d, w16_[4 * l], gm_qkv_, ldqkv, n, ldqkv, d, false, stream_))) gemm(g);
+      gemm(g);
       if (!qepi) {
       QkvPostArgs p;
       p.qkv = gm_qkv_; p.ldqkv = ldqkv; p.T = n;
@@ -1183,7 +1182,7 @@ void Engine::prefill_gemm(int slot, const std::vector<int>& tokens, int start_po
       g.A = gm_attn16_; g.lda = qd; g.M = n; g.K = qd; g.nseg = 1; g.seg[0] = L.wo.w; g.N = d; g.ldc = d;
       if (tp) { g.C = gm_part_; g.epi = GEPI_STORE; } else { g.C = gm_x_; g.epi = GEPI_ACCUM; }
       if (fnp) nrm_out(g, L.ffn_norm);
-      if (!(lib && blas_->gemm(gm_attn16_, qd, w16_[4 * l + 1], g.C, d, n, d, qd, !tp, stream_))) gemm(g);
+      gemm(g);
       if (tp) allreduce(gm_part_, (size_t)n * d, gm_x_);
       // FFN
       if (!fnp) launch_rmsnorm_bf16(gm_x_, d, L.ffn_norm, gm_a16_, d, n, d, cfg_.norm_eps, stream_);
@@ -1191,15 +1190,12 @@ void Engine::prefill_gemm(int slot, const std::vector<int>& tokens, int start_po
       g.A = gm_a16_; g.lda = d; g.M = n; g.K = d; g.nseg = 1; g.seg[0] = L.wgu.w; g.N = 2 * ff;
       g.C16 = gm_ff16_; g.ldc = ff; g.epi = GEPI_SWIGLU_BF16;
       if (fnp) nrm_in(g);
-      if (lib && blas_->gemm(gm_a16_, d, w16_[4 * l + 2], gm_gu32_, 2 * ff, n, 2 * ff, d, false, stream_))
-        launch_swiglu_interleaved_bf16(gm_gu32_, 2 * ff, gm_ff16_, ff, n, ff, stream_);
-      else
-        gemm(g);
+      gemm(g);
       std::memset(&g, 0, sizeof(g));
       g.A = gm_ff16_; g.lda = ff; g.M = n; g.K = ff; g.nseg = 1; g.seg[0] = L.wdown.w; g.N = d; g.ldc = d;
       if (tp) { g.C = gm_part_; g.epi = GEPI_STORE; } else { g.C = gm_x_; g.epi = GEPI_ACCUM; }
       if (fnp && l + 1 < cfg_.n_layers) nrm_out(g, layers_[l + 1].attn_norm);  // (lm_head normalises its row)
-      if (!(lib && blas_->gemm(gm_ff16_, ff, w16_[4 * l + 3], g.C, d, n, d, ff, !tp, stream_))) gemm(g);
+      gemm(g);
       if (tp) allreduce(gm_part_, (size_t)n * d, gm_x_);
     }
     if (r0 + n == T && want_logits) lm_head(1, gm_x_ + (size_t)(n - 1) * d, d);

@@ -546,7 +546,7 @@ __device__ __forceinline__ void pf_body32(const GemmQArgs& a, int m0, int n0, in
 // ~68 SALU per wave-step.  Here each wave owns its SIMD, DMAs its OWN weight columns (so it can
 // wait for, read and decode step t+1's B fragments with its own vmcnt, before the barrier, inside
 // step t's last phases) and every DMA piece is compile-time: one vmcnt immediate per wave.
-template <int QT, int BM, int WC>
+template <int QT, int BM, int WC, int NW = 4>
 struct Pf4Layout {
   static constexpr bool Q6 = QT == QT_Q6_K, BF = QT == QT_BF16;
   static constexpr int A_BYTES = BM * 128;
@@ -555,16 +555,16 @@ struct Pf4Layout {
   static constexpr int SC = Q6 ? 256 : 0, DW = Q6 ? 256 : 0;  // Q6_K int8 scales / d dword (4-B pieces)
   static constexpr int WB = CODE + META + SC + DW;            // one wave's weight bytes per slot
   static constexpr int OFF_B = A_BYTES;
-  static constexpr int SLOT = (A_BYTES + 4 * WB + 255) / 256 * 256;
+  static constexpr int SLOT = (A_BYTES + NW * WB + 255) / 256 * 256;
   static constexpr int NS = 3 * SLOT <= 160 * 1024 ? 3 : 2;
-  static constexpr int NA = BM / 32, NCODE = CODE / 1024, NMETA = META / 1024, NSC = SC / 256, ND = DW / 256;
+  static constexpr int NA = BM / (8 * NW), NCODE = CODE / 1024, NMETA = META / 1024, NSC = SC / 256, ND = DW / 256;
   static constexpr int PW = NA + NCODE + NMETA + NSC + ND;    // DMA instructions per wave per slot
-  static_assert(CODE % 1024 == 0 && WC * 4 <= 256 && PW <= 31, "pf4 slot");
+  static_assert(CODE % 1024 == 0 && WC * 4 <= 256 && PW <= 31 && NA * 8 * NW == BM, "pf4 slot");
 };
 
-template <int QT, int BM, int WC>
+template <int QT, int BM, int WC, int NW = 4>
 struct Pf4Dma {
-  using L = Pf4Layout<QT, BM, WC>;
+  using L = Pf4Layout<QT, BM, WC, NW>;
   uint32_t off[L::PW];
 
   __device__ __forceinline__ void init(const GemmQArgs& a, int wcol0, int m0, int wv) {
@@ -573,8 +573,8 @@ struct Pf4Dma {
     static_for<L::PW>([&](auto ic) {
       constexpr int i = decltype(ic)::value;
       uint32_t o;
-      if constexpr (i < L::NA) {  // A piece j = 4i + wv: unit p -> row p>>3, logical unit (p&7) ^ ((row>>1)&7)
-        const int p = 64 * (4 * i + wv) + lane, row = p >> 3, c = (p & 7) ^ ((row >> 1) & 7);
+      if constexpr (i < L::NA) {  // A piece j = NW i + wv: unit p -> row p>>3, logical unit (p&7) ^ ((row>>1)&7)
+        const int p = 64 * (NW * i + wv) + lane, row = p >> 3, c = (p & 7) ^ ((row >> 1) & 7);
         const int m = min(m0 + row, a.M - 1);
         o = ((uint32_t)m * (uint32_t)a.lda + (uint32_t)(c * 8)) * 2u;
       } else if constexpr (i < L::NA + L::NCODE) {
@@ -611,7 +611,7 @@ struct Pf4Dma {
         return;
       }
       if constexpr (i < L::NA) {
-        pf_glds16((const uint8_t*)a.A + kt * 128 + off[i], dst + (4 * i + wv) * 1024);
+        pf_glds16((const uint8_t*)a.A + kt * 128 + off[i], dst + (NW * i + wv) * 1024);
       } else if constexpr (i < L::NA + L::NCODE) {
         pf_glds16(w.p0 + (L::BF ? kt * 128 : kt * 32) + off[i], wb + (i - L::NA) * 1024);
       } else if constexpr (i < L::NA + L::NCODE + L::NMETA) {
@@ -804,6 +804,702 @@ __device__ __forceinline__ void pf4_body(const GemmQArgs& a, int m0, int n0, int
   }
 }
 
+// ==== pf8: 8 waves (two per SIMD) x 32 columns, 16x16x32 MFMA ======================================
+// The 8-wave 16x16x32 body ran the compute-only probe at 1.33 PF per busy CU against 1.16 for pf4's
+// one wave per SIMD (the SIMD's second wave covers the first's LDS latencies); this is that body
+// with pf4's structure: compile-time own-column DMA pieces, the next step's B decode inside this
+// step's phases, the barrier between the two halves of the last phase, a branch-free loop.
+template <int QT, int BM, int EPI, int PROBE = 0>
+__device__ __forceinline__ void pf8_body(const GemmQArgs& a, int m0, int n0, int seg, int kt0, int kt1, int S) {
+  constexpr int NW = 8, WC = 32;
+  using L = Pf4Layout<QT, BM, WC, NW>;
+  constexpr int MT = BM / 16, GR = MT < 8 ? MT : 8, NG = MT / GR, NPH = 2 * NG, NS = L::NS, PW = L::PW;
+  extern __shared__ __attribute__((aligned(16))) uint8_t pf_smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  QWeight w;
+  w.qtype = QT;
+  w.rows = seg == 0 ? a.seg[0].rows : (seg == 1 ? a.seg[1].rows : a.seg[2].rows);
+  w.cols = a.K;
+  w.pad_ = 0;
+  w.p0 = seg == 0 ? a.seg[0].p0 : (seg == 1 ? a.seg[1].p0 : a.seg[2].p0);
+  w.p1 = seg == 0 ? a.seg[0].p1 : (seg == 1 ? a.seg[1].p1 : a.seg[2].p1);
+  w.p2 = seg == 0 ? a.seg[0].p2 : (seg == 1 ? a.seg[1].p2 : a.seg[2].p2);
+  w.p3 = seg == 0 ? a.seg[0].p3 : (seg == 1 ? a.seg[1].p3 : a.seg[2].p3);
+  const int wcol0 = n0 - (seg == 0 ? a.seg_n0[0] : (seg == 1 ? a.seg_n0[1] : a.seg_n0[2])) + wv * WC;
+  const uint32_t nbk = (uint32_t)a.K >> 8;
+  const int r16 = lane & 15, q = lane >> 4;
+
+  gf32x4 acc[MT][2];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int c = 0; c < 2; ++c) acc[i][c] = gf32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = kt1 - kt0, klast = kt1 - 1;
+  Pf4Dma<QT, BM, WC, NW> dma;
+  const uint32_t lds0 = __builtin_amdgcn_readfirstlane(pf_lds_addr(pf_smem));
+  dma.init(a, wcol0, m0, wv);
+#pragma unroll
+  for (int p = 0; p < NS; ++p) dma.template issue<PROBE>(a, w, min(kt0 + p, klast), lds0 + p * L::SLOT, wv);
+
+  gbf16x8 bf[2][2], fa[GR], fb[GR];
+  PfBRaw raw[2];
+  int rkt = kt0;
+  auto read_raw = [&](const uint8_t* sl, int kt) __attribute__((always_inline)) {
+    const uint8_t* wb = sl + L::OFF_B + wv * L::WB;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int cl = 16 * c + r16;
+      PfBRaw& r = raw[c];
+      if constexpr (L::BF) {
+        r.mt = *(const uint4*)(wb + cl * 128 + (((0 + q) ^ ((cl >> 1) & 7)) << 4));
+        r.b1 = *(const uint4*)(wb + cl * 128 + (((4 + q) ^ ((cl >> 1) & 7)) << 4));
+      } else {
+        r.cw = *(const uint2*)(wb + cl * 32 + 8 * q);
+        if constexpr (L::Q6) {
+          r.hb = *(const uint2*)(wb + L::CODE + cl * 16 + 8 * (q >> 1));
+          r.scw = *(const uint32_t*)(wb + L::CODE + L::META + cl * 4);
+          r.dw = *(const uint32_t*)(wb + L::CODE + L::META + L::SC + cl * 4);
+        } else {
+          r.mt = *(const uint4*)(wb + L::CODE + cl * 16);
+        }
+      }
+    }
+    rkt = kt;
+  };
+  auto dec = [&](auto sc) __attribute__((always_inline)) {
+    constexpr int S2 = decltype(sc)::value;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int cl = 16 * c + r16;
+      const int dpar = L::Q6 ? (int)(((uint32_t)(wcol0 + cl) * nbk + (uint32_t)(rkt >> 2)) & 1u) : 0;
+      bf[c][S2] = pf_bdec<QT, S2>(raw[c], q, rkt, dpar);
+      asm volatile("" : "+v"(bf[c][S2]));  // keep the decode in this phase (else sunk past the barrier)
+    }
+  };
+  auto ldA = [&](const uint8_t* sl, gbf16x8(&f)[GR], int p) __attribute__((always_inline)) {
+    const int sp = p / NG, g = p % NG;
+#pragma unroll
+    for (int i = 0; i < GR; ++i) {
+      const int row = 16 * (g * GR + i) + r16;
+      const uint4 av = *(const uint4*)(sl + row * 128 + (((4 * sp + q) ^ ((row >> 1) & 7)) << 4));
+      __builtin_memcpy(&f[i], &av, 16);
+    }
+  };
+  auto mfma_range = [&](const gbf16x8(&f)[GR], int p, int k0, int k1) __attribute__((always_inline)) {
+    const int sp = p / NG, g = p % NG;
+#pragma unroll
+    for (int k = 0; k < 2 * GR; ++k) {
+      if (k < k0 || k >= k1) continue;
+      const int c = k / GR, i = k % GR;
+      acc[g * GR + i][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f[i], bf[c][sp], acc[g * GR + i][c], 0, 0, 0);
+    }
+  };
+  if constexpr (!(PROBE & 1)) {
+    if constexpr (NS == 3) pf_vmcnt<2 * PW>(); else pf_vmcnt<PW>();
+  }
+  read_raw(pf_smem, kt0);
+  dec(std::integral_constant<int, 0>{});
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  pf_barrier();
+  ldA(pf_smem, fa, 0);
+
+  int cur = 0;
+  for (int t = 0; t < nk; ++t) {
+    const uint8_t* slot = pf_smem + cur * L::SLOT;
+    const int nxt = cur == NS - 1 ? 0 : cur + 1;
+    static_for<NPH>([&](auto pc) {
+      constexpr int p = decltype(pc)::value;
+      __builtin_amdgcn_sched_barrier(0);
+      auto& cf = (p % 2 == 0) ? fa : fb;
+      auto& nf = (p % 2 == 0) ? fb : fa;
+      if constexpr (p + 1 < NPH) ldA(slot, nf, p + 1);
+      if constexpr (p == 0) dec(std::integral_constant<int, 1>{});  // this step's fragment 1
+      if constexpr (p == NG) {
+        // own pieces of step t+1 landed (NS - 2 younger steps in flight): its raw bytes, fragment 0
+        if constexpr (!(PROBE & 1)) {
+          if constexpr (NS == 3) pf_vmcnt<PW>(); else pf_vmcnt<0>();
+        }
+        read_raw(pf_smem + nxt * L::SLOT, kt0 + t + 1);
+        dec(std::integral_constant<int, 0>{});
+      }
+      if constexpr (p + 1 < NPH) {
+        mfma_range(cf, p, 0, 2 * GR);
+      } else {
+        // last phase: half the MFMAs; B(t+1); the next step's first reads and DMA(t + NS) into slot t
+        // under the other half
+        mfma_range(cf, p, 0, GR);
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if constexpr (!(PROBE & 8)) pf_barrier();
+        ldA(pf_smem + nxt * L::SLOT, nf, 0);
+        if constexpr (!(PROBE & 4)) dma.template issue<PROBE>(a, w, min(kt0 + t + NS, klast), lds0 + cur * L::SLOT, wv);
+        mfma_range(cf, p, GR, 2 * GR);
+      }
+    });
+    if constexpr (NPH % 2 == 1) {
+#pragma unroll
+      for (int i = 0; i < GR; ++i) fa[i] = fb[i];
+    }
+    cur = nxt;
+  }
+  pf_vmcnt<0>();  // no LDS-DMA may land after this workgroup's LDS is released
+
+  // epilogue -- C/D map of the 16x16 accumulator: col = lane & 15, row = 4 * (lane >> 4) + e
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const int n = n0 + wv * WC + 16 * c + r16;
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int m = m0 + 16 * i + 4 * q + e;
+        const float v = acc[i][c][e];
+        if constexpr (EPI == GEPI_SWIGLU_BF16) {
+          const float up = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));
+          if (m < a.M && !(r16 & 1)) a.C16[(size_t)m * a.ldc + (n >> 1)] = f32_to_bf16(v / (1.f + __expf(-v)) * up);
+        } else if (m < a.M) {
+          float* cp = a.C + (size_t)m * a.ldc + n;
+          if (S > 1) unsafeAtomicAdd(cp, v);
+          else if constexpr (EPI == GEPI_ACCUM) *cp += v;
+          else *cp = v;
+        }
+      }
+    }
+  }
+}
+
+// ==== pf8c: pf8 with the K-quant weight planes staged coalesced ==================================
+// Round-5 probe (bench_gemm.py --pf-probe 216/316): the per-step weight pieces -- each column's 32 B
+// of codes and its 16-B scale record, i.e. 32-64 separate rows per DMA instruction -- cost 13-18 %
+// of the kernel against contiguous pieces.  Here a wave stages, per HALF block (2 K-steps), 64
+// contiguous bytes of codes per column (16 rows x 64 B per DMA: 4 lanes per row, the 16-B units
+// XOR-swizzled by (row >> 2) & 3 on the source side so the 8-byte fragment reads are conflict-free),
+// per 256-block the scale records (Q4_K meta / Q6_K int8 scales: 16 B per row) and Q6_K d, and the
+// Q6_K high bits per half block (32 B per row); double buffers by half-block / block parity.
+// Every step issues the same group (so one vmcnt immediate): the per-block / per-half-block planes
+// go as partial-lane pieces, one per step (records: 8 rows = 32 lanes x 4 B; Q6_K d: 8 lanes).
+// Group G(s), issued at the end of step s (after the barrier B(s+1)), s relative to the slice:
+//   A(s + 3); code piece (s & 1) [+ Q6_K high-bit piece (s & 1)] of half block (s + 4) / 2;
+//   record piece (s + 6) % 4 [+ Q6_K d piece] of block (s + 6) / 4.
+// Every target buffer is free by then (its previous contents were last decoded during step s); the
+// data is needed by the decode of the first step using it, at least 1.25 steps later.
+template <int QT, int BM>
+struct PfcLayout {
+  static constexpr int NW = 8, WC = 32, NSA = 3;
+  static constexpr bool Q6 = QT == QT_Q6_K;
+  static constexpr int A_BYTES = BM * 128;
+  static constexpr int OFF_CB = NSA * A_BYTES, CB_W = WC * 64;
+  static constexpr int OFF_HB = OFF_CB + 2 * NW * CB_W, HB_W = Q6 ? WC * 32 : 0;  // Q6_K high bits
+  static constexpr int OFF_RB = OFF_HB + 2 * NW * HB_W, RB_W = WC * 16;           // records
+  static constexpr int OFF_D = OFF_RB + 2 * NW * RB_W, D_W = Q6 ? WC * 4 : 0;
+  static constexpr int TOTAL = OFF_D + 2 * NW * D_W;
+  static constexpr int NA = BM / 64;
+  static constexpr int PW = NA + 2 + (Q6 ? 2 : 0);     // DMA instructions per wave per step
+  static constexpr int PRE = NA + 6 + (Q6 ? 6 : 0);    // prologue group: step 0's A, half block 0, block 0
+};
+
+template <int QT, int BM>
+struct PfcDma {
+  using L = PfcLayout<QT, BM>;
+  static constexpr int NW = 8;
+  uint32_t offA[L::NA], offC[2], offR, offH, offD;
+
+  __device__ __forceinline__ void init(const GemmQArgs& a, int wcol0, int m0, int wv) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t nbk = (uint32_t)a.K >> 8;
+#pragma unroll
+    for (int i = 0; i < L::NA; ++i) {
+      const int p = 64 * (NW * i + wv) + lane, row = p >> 3, c = (p & 7) ^ ((row >> 1) & 7);
+      const int m = min(m0 + row, a.M - 1);
+      offA[i] = ((uint32_t)m * (uint32_t)a.lda + (uint32_t)(c * 8)) * 2u;
+    }
+#pragma unroll
+    for (int pc = 0; pc < 2; ++pc) {
+      const int row = 16 * pc + (lane >> 2), u = (lane & 3) ^ ((row >> 2) & 3);
+      offC[pc] = (uint32_t)(wcol0 + row) * nbk * 128u + 16u * (uint32_t)u;
+    }
+    const int l32 = lane & 31;
+    offR = (uint32_t)(wcol0 + (l32 >> 2)) * nbk * 16u + 4u * (uint32_t)(l32 & 3);  // + 8 rows per piece
+    offH = (uint32_t)(wcol0 + (l32 >> 1)) * nbk * 64u + 16u * (uint32_t)(l32 & 1);  // + 16 rows per piece
+    offD = (uint32_t)(wcol0 + (lane & 7)) * nbk;                                      // + 8 rows per piece
+  }
+
+  __device__ __forceinline__ void A(const GemmQArgs& a, int kt, uint32_t dst, int wv) const {
+#pragma unroll
+    for (int i = 0; i < L::NA; ++i) pf_glds16((const uint8_t*)a.A + kt * 128 + offA[i], dst + (NW * i + wv) * 1024);
+  }
+  // the A pieces i with i % NP == P
+  template <int P, int NP>
+  __device__ __forceinline__ void A_part(const GemmQArgs& a, int kt, uint32_t dst, int wv) const {
+#pragma unroll
+    for (int i = 0; i < L::NA; ++i)
+      if (i % NP == P) pf_glds16((const uint8_t*)a.A + kt * 128 + offA[i], dst + (NW * i + wv) * 1024);
+  }
+  // code piece pc of half block hsrc into the wave's half-block buffer at dst
+  __device__ __forceinline__ void code(const QWeight& w, int hsrc, int pc, uint32_t dst) const {
+    // (a register select: offC[pc] with a runtime pc puts the array in scratch, and the scratch
+    // load's vmcnt(0) drained every in-flight DMA)
+    pf_glds16(w.p0 + hsrc * 64 + (pc ? offC[1] : offC[0]), dst + pc * 1024);
+  }
+  // record piece pr (rows 8 pr .. 8 pr + 7) of block bsrc; lanes 0..31
+  __device__ __forceinline__ void rec(const QWeight& w, int bsrc, int pr, uint32_t nbk, uint32_t dst) const {
+    if ((threadIdx.x & 63) < 32) pf_glds4((L::Q6 ? w.p2 : w.p1) + bsrc * 16 + offR + pr * 128 * nbk, dst + pr * 128);
+  }
+  // Q6_K high-bit piece pc (rows 16 pc ..) of half block hsrc; lanes 0..31
+  __device__ __forceinline__ void hi(const QWeight& w, int hsrc, int pc, uint32_t nbk, uint32_t dst) const {
+    if ((threadIdx.x & 63) < 32) pf_glds16(w.p1 + hsrc * 32 + offH + pc * 1024 * nbk, dst + pc * 512);
+  }
+  // Q6_K d piece pr (rows 8 pr ..) of block bsrc: the dword holding each row's f16 d; lanes 0..7
+  __device__ __forceinline__ void dq(const QWeight& w, int bsrc, int pr, uint32_t nbk, uint32_t dst) const {
+    if ((threadIdx.x & 63) < 8) pf_glds4(w.p3 + (((offD + pr * 8 * nbk + (uint32_t)bsrc) * 2u) & ~3u), dst + pr * 32);
+  }
+};
+
+template <int QT, int BM, int EPI, int PROBE = 0>
+__device__ __forceinline__ void pf8c_body(const GemmQArgs& a, int m0, int n0, int seg, int kt0, int kt1, int S) {
+  using L = PfcLayout<QT, BM>;
+  constexpr int NW = 8, WC = 32, NSA = L::NSA, PW = L::PW;
+  // row tiles per phase: 4 at BM = 256 (8 phases; 8 ran out of registers once the DMA is spread)
+  constexpr int MT = BM / 16, GR = MT >= 16 ? 4 : MT, NG = MT / GR, NPH = 2 * NG;
+  extern __shared__ __attribute__((aligned(16))) uint8_t pf_smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  QWeight w;
+  w.qtype = QT;
+  w.rows = seg == 0 ? a.seg[0].rows : (seg == 1 ? a.seg[1].rows : a.seg[2].rows);
+  w.cols = a.K;
+  w.pad_ = 0;
+  w.p0 = seg == 0 ? a.seg[0].p0 : (seg == 1 ? a.seg[1].p0 : a.seg[2].p0);
+  w.p1 = seg == 0 ? a.seg[0].p1 : (seg == 1 ? a.seg[1].p1 : a.seg[2].p1);
+  w.p2 = seg == 0 ? a.seg[0].p2 : (seg == 1 ? a.seg[1].p2 : a.seg[2].p2);
+  w.p3 = seg == 0 ? a.seg[0].p3 : (seg == 1 ? a.seg[1].p3 : a.seg[2].p3);
+  const int wcol0 = n0 - (seg == 0 ? a.seg_n0[0] : (seg == 1 ? a.seg_n0[1] : a.seg_n0[2])) + wv * WC;
+  const uint32_t nbk = (uint32_t)a.K >> 8;
+  const int r16 = lane & 15, q = lane >> 4;
+
+  gf32x4 acc[MT][2];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int c = 0; c < 2; ++c) acc[i][c] = gf32x4{0.f, 0.f, 0.f, 0.f};
+
+  // kt0, kt1 are multiples of 4 (block-aligned slices)
+  const int nk = kt1 - kt0, klast = kt1 - 1, hlast = (kt1 >> 1) - 1, blast = (kt1 >> 2) - 1;
+  PfcDma<QT, BM> dma;
+  const uint32_t lds0 = __builtin_amdgcn_readfirstlane(pf_lds_addr(pf_smem));
+  dma.init(a, wcol0, m0, wv);
+  constexpr uint32_t CBS = NW * L::CB_W, HBS = NW * L::HB_W, RBS = NW * L::RB_W, DBS = NW * L::D_W;
+  const uint32_t cb = lds0 + L::OFF_CB + wv * L::CB_W, hb = lds0 + L::OFF_HB + wv * L::HB_W;
+  const uint32_t rb = lds0 + L::OFF_RB + wv * L::RB_W, db = lds0 + L::OFF_D + wv * L::D_W;
+  // G(s): phase-split -- A pieces in the first phases (longest lead), then code (+ high bits), then
+  // records (+ d); PH_ALL = every phase (prologue)
+  constexpr int PH_ALL = -1;
+  auto group = [&](int s, auto phc) __attribute__((always_inline)) {
+    constexpr int ph = decltype(phc)::value;
+    // A piece i in phase i % NG (all before the decode wait at phase NG)
+    if constexpr (ph == PH_ALL) {
+      dma.A(a, min(kt0 + s + NSA, klast), lds0 + (uint32_t)(((s + 3 * NSA) % NSA) * L::A_BYTES), wv);
+    } else if constexpr (ph < NG) {
+      dma.template A_part<(ph < 0 ? 0 : ph), NG>(a, min(kt0 + s + NSA, klast),
+                                                 lds0 + (uint32_t)(((s + 3 * NSA) % NSA) * L::A_BYTES), wv);
+    }
+    const int H = (kt0 >> 1) + ((s + 4) >> 1), B = (kt0 >> 2) + ((s + 6) >> 2), pr = (s + 6) & 3;
+    if constexpr (ph == PH_ALL || ph == NPH - 2 || (NPH == 2 && ph == 0)) {
+      dma.code(w, min(H, hlast), s & 1, cb + (uint32_t)(H & 1) * CBS);
+      if constexpr (L::Q6) dma.hi(w, min(H, hlast), s & 1, nbk, hb + (uint32_t)(H & 1) * HBS);
+    }
+    if constexpr (ph == PH_ALL || ph == NPH - 1) {
+      dma.rec(w, min(B, blast), pr, nbk, rb + (uint32_t)(B & 1) * RBS);
+      if constexpr (L::Q6) dma.dq(w, min(B, blast), pr, nbk, db + (uint32_t)(B & 1) * DBS);
+    }
+  };
+  // DMA instructions of G(s-1) issued in step s's phases before the decode wait (phase NG)
+  constexpr int NB = 1 + (L::Q6 ? 1 : 0);  // code pieces (+ high bits)
+  constexpr int PRE_WAIT = NPH == 2 ? L::NA + NB : L::NA;
+  {  // prologue: step 0's A, half block 0, block 0 (PRE instructions), then G(-2), G(-1)
+    const int H0 = kt0 >> 1, B0 = kt0 >> 2;
+    dma.A(a, kt0, lds0, wv);
+    dma.code(w, H0, 0, cb + (uint32_t)(H0 & 1) * CBS);
+    dma.code(w, H0, 1, cb + (uint32_t)(H0 & 1) * CBS);
+    if constexpr (L::Q6) {
+      dma.hi(w, H0, 0, nbk, hb + (uint32_t)(H0 & 1) * HBS);
+      dma.hi(w, H0, 1, nbk, hb + (uint32_t)(H0 & 1) * HBS);
+    }
+#pragma unroll
+    for (int pr = 0; pr < 4; ++pr) {
+      dma.rec(w, B0, pr, nbk, rb + (uint32_t)(B0 & 1) * RBS);
+      if constexpr (L::Q6) dma.dq(w, B0, pr, nbk, db + (uint32_t)(B0 & 1) * DBS);
+    }
+    group(-2, std::integral_constant<int, PH_ALL>{});
+  }
+
+  gbf16x8 bf[2][2], fa[GR], fb[GR];
+  PfBRaw raw[2];
+  int rkt = kt0;
+  // raw bytes of (absolute) K-step kt for this lane's two columns
+  auto read_raw = [&](int kt) __attribute__((always_inline)) {
+    const int H = kt >> 1, j = kt & 1, B = kt >> 2;
+    const uint8_t* cbp = pf_smem + L::OFF_CB + (H & 1) * CBS + wv * L::CB_W;
+    const uint8_t* rbp = pf_smem + L::OFF_RB + (B & 1) * RBS + wv * L::RB_W;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int row = 16 * c + r16;
+      PfBRaw& r = raw[c];
+      r.cw = *(const uint2*)(cbp + row * 64 + (((2 * j + (q >> 1)) ^ ((row >> 2) & 3)) << 4) + 8 * (q & 1));
+      if constexpr (L::Q6) {
+        r.hb = *(const uint2*)(pf_smem + L::OFF_HB + (H & 1) * HBS + wv * L::HB_W + row * 32 + (2 * j + (q >> 1)) * 8);
+        r.scw = *(const uint32_t*)(rbp + row * 16 + 4 * (kt & 3));
+        r.dw = *(const uint32_t*)(pf_smem + L::OFF_D + (B & 1) * DBS + wv * L::D_W + row * 4);
+      } else {
+        r.mt = *(const uint4*)(rbp + row * 16);
+      }
+    }
+    rkt = kt;
+  };
+  auto dec = [&](auto sc) __attribute__((always_inline)) {
+    constexpr int S2 = decltype(sc)::value;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int cl = 16 * c + r16;
+      const int dpar = L::Q6 ? (int)(((uint32_t)(wcol0 + cl) * nbk + (uint32_t)(rkt >> 2)) & 1u) : 0;
+      bf[c][S2] = pf_bdec<QT, S2>(raw[c], q, rkt, dpar);
+      asm volatile("" : "+v"(bf[c][S2]));  // keep the decode in this phase (else sunk past the barrier)
+    }
+  };
+  auto ldA = [&](const uint8_t* sl, gbf16x8(&f)[GR], int p) __attribute__((always_inline)) {
+    const int sp = p / NG, g = p % NG;
+#pragma unroll
+    for (int i = 0; i < GR; ++i) {
+      const int row = 16 * (g * GR + i) + r16;
+      const uint4 av = *(const uint4*)(sl + row * 128 + (((4 * sp + q) ^ ((row >> 1) & 7)) << 4));
+      __builtin_memcpy(&f[i], &av, 16);
+    }
+  };
+  auto mfma_range = [&](const gbf16x8(&f)[GR], int p, int k0, int k1) __attribute__((always_inline)) {
+    const int sp = p / NG, g = p % NG;
+#pragma unroll
+    for (int k = 0; k < 2 * GR; ++k) {
+      if (k < k0 || k >= k1) continue;
+      const int c = k / GR, i = k % GR;
+      acc[g * GR + i][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f[i], bf[c][sp], acc[g * GR + i][c], 0, 0, 0);
+    }
+  };
+  if constexpr (!(PROBE & 1)) pf_vmcnt<PW>();  // the prologue group landed (G(-2) in flight)
+  read_raw(kt0);
+  dec(std::integral_constant<int, 0>{});
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  pf_barrier();
+  ldA(pf_smem, fa, 0);
+
+  int cur = 0;
+  for (int s = 0; s < nk; ++s) {
+    const uint8_t* slot = pf_smem + cur * L::A_BYTES;
+    const int nxt = cur == NSA - 1 ? 0 : cur + 1;
+    static_for<NPH>([&](auto pc) {
+      constexpr int p = decltype(pc)::value;
+      __builtin_amdgcn_sched_barrier(0);
+      auto& cf = (p % 2 == 0) ? fa : fb;
+      auto& nf = (p % 2 == 0) ? fb : fa;
+      if constexpr (p + 1 < NPH) ldA(slot, nf, p + 1);
+      if constexpr (p == 0) dec(std::integral_constant<int, 1>{});
+      if constexpr (p == NG) {
+        // G(s-2) landed -- step s+1's codes / records and this wave's A pieces of it -- with only
+        // G(s-1)'s first-phase pieces younger
+        if constexpr (!(PROBE & 1)) pf_vmcnt<PRE_WAIT>();
+        read_raw(kt0 + s + 1);  // (past the last step: stale buffers, unused)
+        dec(std::integral_constant<int, 0>{});
+      }
+      // G(s-1): its slot / buffers were released by B(s) (past the end: clamped re-loads, unused)
+      if constexpr (!(PROBE & 4)) group(s - 1, pc);
+      if constexpr (p + 1 < NPH) {
+        mfma_range(cf, p, 0, 2 * GR);
+      } else {
+        mfma_range(cf, p, 0, GR);
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if constexpr (!(PROBE & 8)) pf_barrier();
+        ldA(pf_smem + nxt * L::A_BYTES, nf, 0);
+        mfma_range(cf, p, GR, 2 * GR);
+      }
+    });
+    if constexpr (NPH % 2 == 1) {
+#pragma unroll
+      for (int i = 0; i < GR; ++i) fa[i] = fb[i];
+    }
+    cur = nxt;
+  }
+  pf_vmcnt<0>();  // no LDS-DMA may land after this workgroup's LDS is released
+
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const int n = n0 + wv * WC + 16 * c + r16;
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int m = m0 + 16 * i + 4 * q + e;
+        const float v = acc[i][c][e];
+        if constexpr (EPI == GEPI_SWIGLU_BF16) {
+          const float up = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));
+          if (m < a.M && !(r16 & 1)) a.C16[(size_t)m * a.ldc + (n >> 1)] = f32_to_bf16(v / (1.f + __expf(-v)) * up);
+        } else if (m < a.M) {
+          float* cp = a.C + (size_t)m * a.ldc + n;
+          if (S > 1) unsafeAtomicAdd(cp, v);
+          else if constexpr (EPI == GEPI_ACCUM) *cp += v;
+          else *cp = v;
+        }
+      }
+    }
+  }
+}
+
+// ==== pf8d: pf8c on v_mfma_f32_32x32x16_bf16 ======================================================
+// PMC (round 5, gate/up M = 2048): with the DMA on, the waves spend +25 % active-instruction cycles
+// (LDS-DMA issue ~55-60 cycles each) and the SIMD's issue port -- MFMA issue + decode VALU + DMA +
+// LDS reads -- exceeds the matrix pipe's 2048 cycles per step.  A 32x32x16 MFMA holds vector issue
+// for 8 of its 32 cycles against 8 of 16 for 16x16x32: half the MFMA issue cost at equal FLOPs.
+// Wave tile BM rows x 32 columns = BM/32 accumulators; per K-step four k16 substeps (k = 16 s + 8 h
+// + j: chunk (s & 1) bytes 8h.., low nibbles for s < 2).  Phase s uses fragment s; the next step's
+// fragment s is decoded in phase s+1 (fragment 3 in the next step's phase 0) from raw bytes read
+// after the phase-1 wait.  The staging is pf8c's (same layout, same DMA groups).
+template <int QT, int BM, int EPI, int PROBE = 0>
+__device__ __forceinline__ void pf8d_body(const GemmQArgs& a, int m0, int n0, int seg, int kt0, int kt1, int S) {
+  using L = PfcLayout<QT, BM>;
+  constexpr int NW = 8, WC = 32, NSA = L::NSA, PW = L::PW;
+  // GD row tiles per phase (4 at BM = 256: two 8-fragment A buffers spill), ND phases per substep
+  constexpr int MT = BM / 32, GD = MT > 4 ? 4 : MT, ND = MT / GD, NPH = 4 * ND;
+  extern __shared__ __attribute__((aligned(16))) uint8_t pf_smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  QWeight w;
+  w.qtype = QT;
+  w.rows = seg == 0 ? a.seg[0].rows : (seg == 1 ? a.seg[1].rows : a.seg[2].rows);
+  w.cols = a.K;
+  w.pad_ = 0;
+  w.p0 = seg == 0 ? a.seg[0].p0 : (seg == 1 ? a.seg[1].p0 : a.seg[2].p0);
+  w.p1 = seg == 0 ? a.seg[0].p1 : (seg == 1 ? a.seg[1].p1 : a.seg[2].p1);
+  w.p2 = seg == 0 ? a.seg[0].p2 : (seg == 1 ? a.seg[1].p2 : a.seg[2].p2);
+  w.p3 = seg == 0 ? a.seg[0].p3 : (seg == 1 ? a.seg[1].p3 : a.seg[2].p3);
+  const int wcol0 = n0 - (seg == 0 ? a.seg_n0[0] : (seg == 1 ? a.seg_n0[1] : a.seg_n0[2])) + wv * WC;
+  const uint32_t nbk = (uint32_t)a.K >> 8;
+  const int r32 = lane & 31, h = lane >> 5;
+
+  gf32x16 acc[MT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[i][e] = 0.f;
+
+  const int nk = kt1 - kt0, klast = kt1 - 1, hlast = (kt1 >> 1) - 1, blast = (kt1 >> 2) - 1;
+  PfcDma<QT, BM> dma;
+  const uint32_t lds0 = __builtin_amdgcn_readfirstlane(pf_lds_addr(pf_smem));
+  dma.init(a, wcol0, m0, wv);
+  constexpr uint32_t CBS = NW * L::CB_W, HBS = NW * L::HB_W, RBS = NW * L::RB_W, DBS = NW * L::D_W;
+  const uint32_t cb = lds0 + L::OFF_CB + wv * L::CB_W, hb = lds0 + L::OFF_HB + wv * L::HB_W;
+  const uint32_t rb = lds0 + L::OFF_RB + wv * L::RB_W, db = lds0 + L::OFF_D + wv * L::D_W;
+  // G(s) during step s+1, after the wait at phase ND: A pieces over phases ND .. ND + NAP - 1, code
+  // (+ high bits) and records (+ d) in phase NPH - 2 (NPH - 1 at ND == 1); PH_ALL = every piece (prologue)
+  constexpr int PH_ALL = -1, NAP = ND == 1 ? 2 : 4, PB = ND == 1 ? 3 : NPH - 2;
+  auto group = [&](int s, auto phc) __attribute__((always_inline)) {
+    constexpr int ph = decltype(phc)::value;
+    const uint32_t adst = lds0 + (uint32_t)(((s + 3 * NSA) % NSA) * L::A_BYTES);
+    const int ka = min(kt0 + s + NSA, klast);
+    if constexpr (ph == PH_ALL) dma.A(a, ka, adst, wv);
+    else if constexpr (ph >= ND && ph < ND + NAP) dma.template A_part<(ph - ND), NAP>(a, ka, adst, wv);
+    const int H = (kt0 >> 1) + ((s + 4) >> 1), B = (kt0 >> 2) + ((s + 6) >> 2), pr = (s + 6) & 3;
+    if constexpr (ph == PH_ALL || ph == PB) {
+      dma.code(w, min(H, hlast), s & 1, cb + (uint32_t)(H & 1) * CBS);
+      if constexpr (L::Q6) dma.hi(w, min(H, hlast), s & 1, nbk, hb + (uint32_t)(H & 1) * HBS);
+      dma.rec(w, min(B, blast), pr, nbk, rb + (uint32_t)(B & 1) * RBS);
+      if constexpr (L::Q6) dma.dq(w, min(B, blast), pr, nbk, db + (uint32_t)(B & 1) * DBS);
+    }
+  };
+  {  // prologue: step 0's A, half block 0, block 0, then G(-2)
+    const int H0 = kt0 >> 1, B0 = kt0 >> 2;
+    dma.A(a, kt0, lds0, wv);
+    dma.code(w, H0, 0, cb + (uint32_t)(H0 & 1) * CBS);
+    dma.code(w, H0, 1, cb + (uint32_t)(H0 & 1) * CBS);
+    if constexpr (L::Q6) {
+      dma.hi(w, H0, 0, nbk, hb + (uint32_t)(H0 & 1) * HBS);
+      dma.hi(w, H0, 1, nbk, hb + (uint32_t)(H0 & 1) * HBS);
+    }
+#pragma unroll
+    for (int pr = 0; pr < 4; ++pr) {
+      dma.rec(w, B0, pr, nbk, rb + (uint32_t)(B0 & 1) * RBS);
+      if constexpr (L::Q6) dma.dq(w, B0, pr, nbk, db + (uint32_t)(B0 & 1) * DBS);
+    }
+    group(-2, std::integral_constant<int, PH_ALL>{});
+  }
+
+  gbf16x8 bf[4], fa[GD], fb[GD];
+  PfBRaw32 raw;
+  int rkt = kt0;
+  auto read_raw = [&](int kt) __attribute__((always_inline)) {
+    const int H = kt >> 1, j = kt & 1, B = kt >> 2;
+    const uint8_t* cbp = pf_smem + L::OFF_CB + (H & 1) * CBS + wv * L::CB_W + r32 * 64;
+    const uint8_t* rbp = pf_smem + L::OFF_RB + (B & 1) * RBS + wv * L::RB_W + r32 * 16;
+    const int x = (r32 >> 2) & 3;
+    raw.c0 = *(const uint2*)(cbp + (((2 * j) ^ x) << 4) + 8 * h);
+    raw.c1 = *(const uint2*)(cbp + (((2 * j + 1) ^ x) << 4) + 8 * h);
+    if constexpr (L::Q6) {
+      // high bits {c0 run0, c0 run1, c1 run0, c1 run1} of this step's two chunks
+      raw.mt = *(const uint4*)(pf_smem + L::OFF_HB + (H & 1) * HBS + wv * L::HB_W + r32 * 32 + 16 * j);
+      // int8 scales {c0 run0, c0 run1, c1 run0, c1 run1}: chunks 2g, 2g + 1 -> bytes 4g .. 4g + 3
+      raw.scw = *(const uint32_t*)(rbp + 4 * (kt & 3));
+      raw.dw = *(const uint32_t*)(pf_smem + L::OFF_D + (B & 1) * DBS + wv * L::D_W + r32 * 4);
+    } else {
+      raw.mt = *(const uint4*)rbp;
+    }
+    rkt = kt;
+  };
+  auto dec = [&](auto sc) __attribute__((always_inline)) {
+    constexpr int S4 = decltype(sc)::value;
+    const int dpar = L::Q6 ? (int)(((uint32_t)(wcol0 + r32) * nbk + (uint32_t)(rkt >> 2)) & 1u) : 0;
+    bf[S4] = pf_bdec32<QT, S4>(raw, h, rkt, dpar);
+    asm volatile("" : "+v"(bf[S4]));  // keep the decode in this phase (else sunk past the barrier)
+  };
+  auto ldA = [&](const uint8_t* sl, gbf16x8(&f)[GD], int p) __attribute__((always_inline)) {
+    const int sp = p / ND, g = p % ND;
+#pragma unroll
+    for (int i = 0; i < GD; ++i) {
+      const int row = 32 * (g * GD + i) + r32;
+      const uint4 av = *(const uint4*)(sl + row * 128 + (((2 * sp + h) ^ ((row >> 1) & 7)) << 4));
+      __builtin_memcpy(&f[i], &av, 16);
+    }
+  };
+  auto mfma_range = [&](const gbf16x8(&f)[GD], int p, int k0, int k1) __attribute__((always_inline)) {
+    const int sp = p / ND, g = p % ND;
+#pragma unroll
+    for (int i = 0; i < GD; ++i)
+      if (i >= k0 && i < k1)
+        acc[g * GD + i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f[i], bf[sp], acc[g * GD + i], 0, 0, 0);
+  };
+  if constexpr (!(PROBE & 1)) pf_vmcnt<PW>();  // the prologue group landed (G(-2) in flight)
+  read_raw(kt0);
+  dec(std::integral_constant<int, 0>{});
+  dec(std::integral_constant<int, 1>{});
+  dec(std::integral_constant<int, 2>{});
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  pf_barrier();
+  ldA(pf_smem, fa, 0);
+
+  int cur = 0;
+  for (int s = 0; s < nk; ++s) {
+    const uint8_t* slot = pf_smem + cur * L::A_BYTES;
+    const int nxt = cur == NSA - 1 ? 0 : cur + 1;
+    static_for<NPH>([&](auto pc) {
+      constexpr int p = decltype(pc)::value;
+      __builtin_amdgcn_sched_barrier(0);
+      auto& cf = (p % 2 == 0) ? fa : fb;
+      auto& nf = (p % 2 == 0) ? fb : fa;
+      if constexpr (p + 1 < NPH) ldA(slot, nf, p + 1);
+      if constexpr (p == 0) dec(std::integral_constant<int, 3>{});  // this step's fragment 3
+      if constexpr (p == ND) {
+        // G(s-2) landed (step s+1's codes / records, this wave's A pieces of it); nothing of G(s-1)
+        // is issued before this point
+        if constexpr (!(PROBE & 1)) pf_vmcnt<0>();
+        read_raw(kt0 + s + 1);  // (past the last step: stale buffers, unused)
+        dec(std::integral_constant<int, 0>{});
+      }
+      if constexpr (p == 2 * ND) dec(std::integral_constant<int, 1>{});
+      if constexpr (ND > 1 && p == 3 * ND) dec(std::integral_constant<int, 2>{});
+      if constexpr (!(PROBE & 4)) {
+        if constexpr (p >= ND) group(s - 1, pc);
+      }
+      if constexpr (p + 1 < NPH) {
+        mfma_range(cf, p, 0, GD);
+      } else {
+        mfma_range(cf, p, 0, GD / 2);
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (ND == 1) dec(std::integral_constant<int, 2>{});
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if constexpr (!(PROBE & 8)) pf_barrier();
+        ldA(pf_smem + nxt * L::A_BYTES, nf, 0);
+        mfma_range(cf, p, GD / 2, GD);
+      }
+    });
+    cur = nxt;
+  }
+  pf_vmcnt<0>();  // no LDS-DMA may land after this workgroup's LDS is released
+
+  // epilogue -- C/D map of the 32x32 accumulator: col = lane & 31, row = (e & 3) + 8 (e >> 2) + 4 h
+  const int n = n0 + wv * WC + r32;
+#pragma unroll
+  for (int i = 0; i < MT; ++i) {
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const int m = m0 + 32 * i + (e & 3) + 8 * (e >> 2) + 4 * h;
+      const float v = acc[i][e];
+      if constexpr (EPI == GEPI_SWIGLU_BF16) {
+        const float up = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));
+        if (m < a.M && !(r32 & 1)) a.C16[(size_t)m * a.ldc + (n >> 1)] = f32_to_bf16(v / (1.f + __expf(-v)) * up);
+      } else if (m < a.M) {
+        float* cp = a.C + (size_t)m * a.ldc + n;
+        if (S > 1) unsafeAtomicAdd(cp, v);
+        else if constexpr (EPI == GEPI_ACCUM) *cp += v;
+        else *cp = v;
+      }
+    }
+  }
+}
+
+template <int QT0, int QT1, int BM, int EPI, int PROBE = 0>
+__global__ void __launch_bounds__(512) gemm_pf8_kernel(GemmQArgs a) {
+  const int nN = a.N / 256, nM = (a.M + BM - 1) / BM, total = nN * nM;
+  const int L = xcd_remap(blockIdx.x, total);
+  const int tn = L % nN, tm = L / nN;
+  const int m0 = tm * BM, n0 = tn * 256;
+  int seg = 0;
+  if (a.nseg > 1 && n0 >= a.seg_n0[1]) seg = 1;
+  if (a.nseg > 2 && n0 >= a.seg_n0[2]) seg = 2;
+  const int S = gridDim.y;
+  if constexpr (QT0 == QT_BF16) {
+    const int nk_all = a.K / 64;
+    const int kt0 = (int)((long)blockIdx.y * nk_all / S), kt1 = (int)((long)(blockIdx.y + 1) * nk_all / S);
+    pf8_body<QT0, BM, EPI, PROBE>(a, m0, n0, seg, kt0, kt1, S);
+  } else {
+    // K-quant stacks: pf8c, slices on 256-block boundaries
+    const int nb = a.K / 256;
+    const int kt0 = 4 * (int)((long)blockIdx.y * nb / S), kt1 = 4 * (int)((long)(blockIdx.y + 1) * nb / S);
+    // PROBE bit 64: the 32x32x16 body (pf8d) instead of pf8c, for A/B timing (measured slower with
+    // the DMA on: gate/up M = 2048 611 vs 484 us, round 5)
+    if constexpr (QT0 != QT1) {
+      if (seg == a.nseg - 1) {
+        if constexpr (PROBE & 64) pf8d_body<QT1, BM, EPI, PROBE>(a, m0, n0, seg, kt0, kt1, S);
+        else pf8c_body<QT1, BM, EPI, PROBE>(a, m0, n0, seg, kt0, kt1, S);
+        return;
+      }
+    }
+    if constexpr (PROBE & 64) pf8d_body<QT0, BM, EPI, PROBE>(a, m0, n0, seg, kt0, kt1, S);
+    else pf8c_body<QT0, BM, EPI, PROBE>(a, m0, n0, seg, kt0, kt1, S);
+  }
+}
+
+template <int QT0, int QT1, int BM>
+constexpr int pf8_lds_bytes() {
+  if constexpr (QT0 == QT_BF16) {
+    using L0 = Pf4Layout<QT0, BM, 32, 8>;
+    return L0::NS * L0::SLOT;
+  } else {
+    return PfcLayout<QT0, BM>::TOTAL > PfcLayout<QT1, BM>::TOTAL ? PfcLayout<QT0, BM>::TOTAL
+                                                                 : PfcLayout<QT1, BM>::TOTAL;
+  }
+}
+
+template <int QT0, int QT1, int BM>
+void pf8_launch(const GemmQArgs& a, int S, hipStream_t st) {
+  constexpr int lds = pf8_lds_bytes<QT0, QT1, BM>();
+  static_assert(lds <= 160 * 1024, "LDS");
+  const dim3 grid((a.N / 256) * ((a.M + BM - 1) / BM), S), block(512);
+  switch (a.epi) {
+    case GEPI_STORE: hipLaunchKernelGGL((gemm_pf8_kernel<QT0, QT1, BM, GEPI_STORE>), grid, block, lds, st, a); break;
+    case GEPI_ACCUM: hipLaunchKernelGGL((gemm_pf8_kernel<QT0, QT1, BM, GEPI_ACCUM>), grid, block, lds, st, a); break;
+    default: hipLaunchKernelGGL((gemm_pf8_kernel<QT0, QT1, BM, GEPI_SWIGLU_BF16>), grid, block, lds, st, a); break;
+  }
+}
+
 template <int QT0, int QT1, int BM, int WC, int EPI, int PROBE = 0>
 __global__ void __launch_bounds__(256) gemm_pf4_kernel(GemmQArgs a) {
   constexpr int BN = 4 * WC;
@@ -902,13 +1598,20 @@ void pf_launch(const GemmQArgs& a, int S, hipStream_t st) {
 // BN = 4 waves x WC columns
 template <int QT0, int QT1>
 bool pf_launch_fmt(const GemmQArgs& a, int BM, int BN, int S, hipStream_t st) {
-#define PF_GO(bm, bn)                             \
-  if (BM == bm && BN == bn) {                     \
-    pf4_launch<QT0, QT1, bm, bn / 4>(a, S, st);   \
-    return true;                                  \
+  // 256-column tiles: the 8-wave body (pf8 / pf8c); 128-column tiles: pf4 with 32 columns per wave
+#define PF_GO8(bm)                      \
+  if (BM == bm && BN == 256) {          \
+    pf8_launch<QT0, QT1, bm>(a, S, st); \
+    return true;                        \
   }
-  PF_GO(256, 256) PF_GO(128, 256) PF_GO(64, 256) PF_GO(256, 128) PF_GO(128, 128) PF_GO(64, 128)
-#undef PF_GO
+#define PF_GO4(bm)                          \
+  if (BM == bm && BN == 128) {              \
+    pf4_launch<QT0, QT1, bm, 32>(a, S, st); \
+    return true;                            \
+  }
+  PF_GO8(256) PF_GO8(128) PF_GO8(64) PF_GO4(256) PF_GO4(128) PF_GO4(64)
+#undef PF_GO8
+#undef PF_GO4
   return false;
 }
 

@@ -3,6 +3,10 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <map>
+#include <mutex>
+#include <tuple>
+#include <vector>
 
 #include "gemm_pf.h"
 
@@ -49,9 +53,51 @@ static bool pf_tile_ok(const GemmQArgs& a, int bn) {
   return true;
 }
 
+// Measured plans: one per (shape, formats, epilogue, M bucket), filled by gemm_pf_autotune (the
+// engine tunes its projection shapes at finalize); the model below is the fallback.
+using PfKey = std::tuple<int, int, int, int, int, int, int, int, int>;
+static int pf_bucket(int M) {
+  int b = 64;
+  while (b < M && b < 2048) b <<= 1;
+  return M > 2048 ? (M + 2047) / 2048 * 2048 : b;
+}
+static PfKey pf_key(const GemmQArgs& a) {
+  return PfKey(a.N, a.K, pf_bucket(a.M), a.epi, a.seg[0].qtype, a.seg[a.nseg - 1].qtype, a.nseg,
+               a.nseg > 1 ? a.seg_n0[1] : 0, a.nseg > 2 ? a.seg_n0[2] : 0);
+}
+static std::mutex pf_mu;
+static std::map<PfKey, PfPlan>& pf_tuned() {
+  static std::map<PfKey, PfPlan> m;
+  return m;
+}
+
+// every plan the launcher could run for these args (ksplit > 0 pins the split)
+static std::vector<PfPlan> pf_candidates(const GemmQArgs& a, bool bf) {
+  std::vector<PfPlan> out;
+  const int nk = a.K / 64;
+  for (int bm : {256, 128, 64})
+    for (int bn : {256, 128}) {
+      if (!pf_tile_ok(a, bn)) continue;
+      for (int S : {1, 2, 3, 4, 6, 8, 12, 16}) {
+        if (a.ksplit > 0 && S != a.ksplit) continue;
+        if (S > 1 && (a.epi == GEPI_SWIGLU_BF16 || nk / S < 2)) continue;
+        if (!bf && bn == 256 && (a.K / 256) / S < 1) continue;
+        PfPlan p;
+        p.bm = bm; p.bn = bn; p.s = S;
+        out.push_back(p);
+      }
+    }
+  return out;
+}
+
 static PfPlan pf_plan(const GemmQArgs& a, bool bf) {
   PfPlan best;
   double bt = 1e30;
+  if (!std::getenv("AIOS_GEMM_PF_TILE") && !std::getenv("AIOS_GEMM_PF_SPLIT") && a.ksplit <= 0) {
+    std::lock_guard<std::mutex> g(pf_mu);
+    auto it = pf_tuned().find(pf_key(a));
+    if (it != pf_tuned().end()) return it->second;
+  }
   // AIOS_GEMM_PF_TILE=BMxBN / AIOS_GEMM_PF_SPLIT=S pin the plan (sweeps: tools/bench_gemm.py --pf-sweep)
   // (read per call: tests and sweeps change them inside one process)
   const char* tile = std::getenv("AIOS_GEMM_PF_TILE");
@@ -67,6 +113,7 @@ static PfPlan pf_plan(const GemmQArgs& a, bool bf) {
         if (a.ksplit > 0 && S != a.ksplit) continue;
         if (a.ksplit <= 0 && split > 0 && S != split) continue;
         if (S > 1 && (a.epi == GEPI_SWIGLU_BF16 || nk / S < 2)) continue;
+        if (!bf && bn == 256 && (a.K / 256) / S < 1) continue;  // pf8c slices whole 256-blocks
         const double t = pf_model(a, bm, bn, S, bf);
         if (t < bt) {
           bt = t;
@@ -81,10 +128,29 @@ static PfPlan pf_plan(const GemmQArgs& a, bool bf) {
 // Serves M >= AIOS_GEMM_PF_MIN_M (default 33: the ring GEMM keeps 5..32) for Q4_K / Q6_K / mixed
 // Q4_K|Q6_K / bf16 weight stacks with the STORE / ACCUM / SWIGLU epilogues; false -> the caller's
 // fallback (formats and fused epilogues this kernel does not do).
+static bool pf_eligible(const GemmQArgs& a);
+static bool pf_run(const GemmQArgs& a, const PfPlan& p, hipStream_t st) {
+  const int qt0 = a.seg[0].qtype, qt1 = a.seg[a.nseg - 1].qtype;
+  if (p.s > 1 && a.epi == GEPI_STORE)
+    HIP_CHECK(hipMemset2DAsync(a.C, (size_t)a.ldc * 4, 0, (size_t)a.N * 4, a.M, st));
+  if (qt0 == QT_Q4_K && qt1 == QT_Q4_K) return pf_launch_fmt<QT_Q4_K, QT_Q4_K>(a, p.bm, p.bn, p.s, st);
+  if (qt0 == QT_Q6_K && qt1 == QT_Q6_K) return pf_launch_fmt<QT_Q6_K, QT_Q6_K>(a, p.bm, p.bn, p.s, st);
+  if (qt0 == QT_Q4_K && qt1 == QT_Q6_K) return pf_launch_fmt<QT_Q4_K, QT_Q6_K>(a, p.bm, p.bn, p.s, st);
+  return pf_launch_fmt<QT_BF16, QT_BF16>(a, p.bm, p.bn, p.s, st);
+}
+
 bool launch_gemm_pf(const GemmQArgs& a, hipStream_t st) {
   const int on = pf_env("AIOS_GEMM_PF", 1);
   const int min_m = pf_env("AIOS_GEMM_PF_MIN_M", 33);
-  if (!on || a.M < min_m || a.nseg < 1) return false;
+  if (!on || a.M < min_m) return false;
+  if (!pf_eligible(a)) return false;
+  const PfPlan p = pf_plan(a, a.seg[0].qtype == QT_BF16);
+  if (!p.bm) return false;
+  return pf_run(a, p, st);
+}
+
+static bool pf_eligible(const GemmQArgs& a) {
+  if (a.nseg < 1 || a.M < 1) return false;
   if (a.epi != GEPI_STORE && a.epi != GEPI_ACCUM && a.epi != GEPI_SWIGLU_BF16) return false;
   if (a.nrm_in || a.lda % 8 || ((uintptr_t)a.A & 15)) return false;
   const int qt0 = a.seg[0].qtype, qt1 = a.seg[a.nseg - 1].qtype;
@@ -96,14 +162,39 @@ bool launch_gemm_pf(const GemmQArgs& a, hipStream_t st) {
   if (qt0 == QT_Q6_K && qt1 == QT_Q4_K) return false;  // not instantiated (no such stack in the GGUF recipes)
   if (a.epi == GEPI_SWIGLU_BF16 && (!a.C16 || a.nseg != 1)) return false;
   if (a.epi != GEPI_SWIGLU_BF16 && !a.C) return false;
-  const PfPlan p = pf_plan(a, bf);
-  if (!p.bm) return false;
-  if (p.s > 1 && a.epi == GEPI_STORE)
-    HIP_CHECK(hipMemset2DAsync(a.C, (size_t)a.ldc * 4, 0, (size_t)a.N * 4, a.M, st));
-  if (qt0 == QT_Q4_K && qt1 == QT_Q4_K) return pf_launch_fmt<QT_Q4_K, QT_Q4_K>(a, p.bm, p.bn, p.s, st);
-  if (qt0 == QT_Q6_K && qt1 == QT_Q6_K) return pf_launch_fmt<QT_Q6_K, QT_Q6_K>(a, p.bm, p.bn, p.s, st);
-  if (qt0 == QT_Q4_K && qt1 == QT_Q6_K) return pf_launch_fmt<QT_Q4_K, QT_Q6_K>(a, p.bm, p.bn, p.s, st);
-  return pf_launch_fmt<QT_BF16, QT_BF16>(a, p.bm, p.bn, p.s, st);
+  return true;
+}
+
+// Time every candidate plan for these args (real buffers; outputs overwritten) and keep the fastest
+// for their M bucket.  Returns the number of candidates timed (0: not a prefill-GEMM launch).
+int gemm_pf_autotune(const GemmQArgs& a, hipStream_t st) {
+  if (!pf_eligible(a)) return 0;
+  const bool bf = a.seg[0].qtype == QT_BF16;
+  const std::vector<PfPlan> cands = pf_candidates(a, bf);
+  if (cands.empty()) return 0;
+  hipEvent_t e0, e1;
+  HIP_CHECK(hipEventCreate(&e0));
+  HIP_CHECK(hipEventCreate(&e1));
+  PfPlan best = cands[0];
+  float bt = 1e30f;
+  for (const PfPlan& p : cands) {
+    pf_run(a, p, st);  // warm (code object load, caches)
+    HIP_CHECK(hipEventRecord(e0, st));
+    for (int r = 0; r < 3; ++r) pf_run(a, p, st);
+    HIP_CHECK(hipEventRecord(e1, st));
+    HIP_CHECK(hipEventSynchronize(e1));
+    float ms = 0.f;
+    HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+    if (ms < bt) {
+      bt = ms;
+      best = p;
+    }
+  }
+  HIP_CHECK(hipEventDestroy(e0));
+  HIP_CHECK(hipEventDestroy(e1));
+  std::lock_guard<std::mutex> g(pf_mu);
+  pf_tuned()[pf_key(a)] = best;
+  return (int)cands.size();
 }
 
 // the plan the launcher would pick (bindings / tools)

@@ -15,7 +15,17 @@ bool gemm_pf_probe(const GemmQArgs& a, int probe, hipStream_t st) {
   case P + 100 * (MF == 16): \
     hipLaunchKernelGGL((gemm_pf_kernel<QT_Q4_K, QT_Q4_K, 256, 8, NS, GEPI_STORE, P, MF>), grid, block, lds, st, a); \
     return true;
-  // probe + 100: the 16x16x32 body; probe + 200: the 4-wave pf4 body (256 x 256)
+  // probe + 100: the 16x16x32 body; probe + 200: the 4-wave pf4 body (256 x 256); + 300: pf8
+  if (probe >= 300) {
+    constexpr int lds8 = pf8_lds_bytes<QT_Q4_K, QT_Q4_K, 256>();
+    const dim3 g8((a.N / 256) * ((a.M + 255) / 256)), b8(512);
+    switch (probe - 300) {
+#define P8_GO(P) case P: hipLaunchKernelGGL((gemm_pf8_kernel<QT_Q4_K, QT_Q4_K, 256, GEPI_STORE, P>), g8, b8, lds8, st, a); return true;
+      P8_GO(0) P8_GO(1) P8_GO(4) P8_GO(8) P8_GO(13) P8_GO(64) P8_GO(68) P8_GO(77)
+#undef P8_GO
+      default: return false;
+    }
+  }
   if (probe >= 200) {
     constexpr int lds4 = pf4_lds_bytes<QT_Q4_K, QT_Q4_K, 256, 64>();
     const dim3 g4((a.N / 256) * ((a.M + 255) / 256)), b4(256);

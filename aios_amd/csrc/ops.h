@@ -235,5 +235,8 @@ void launch_gemm_q(const GemmQArgs& a, hipStream_t st);
 bool launch_gemm_pf(const GemmQArgs& a, hipStream_t st);
 void gemm_pf_plan(const GemmQArgs& a, int& bm, int& bn, int& s);
 bool gemm_pf_probe(const GemmQArgs& a, int probe, hipStream_t st);  // timing anatomy (tools only)
+// time every prefill-GEMM plan for these args (buffers overwritten) and keep the fastest for their M
+// bucket; returns the number of plans timed
+int gemm_pf_autotune(const GemmQArgs& a, hipStream_t st);
 
 }  // namespace aios

@@ -144,15 +144,16 @@ def test_prefill_gemm_chunks_match_reference(model_files, recipe, monkeypatch):
 
 
 @pytest.mark.parametrize("recipe", ["Q4_K_M", "mistral_shape"])
-def test_prefill_blas_chunks_match_reference(model_files, recipe, monkeypatch):
-    """long prefill chunks through hipBLASLt on the resident bf16 weights (blas.h): 64-row chunks of
-    a 150-token prompt with the library threshold at 32 rows -- two chunks on hipBLASLt, the 22-row
-    tail on the fused GEMM -- against the fp32 reference, continued at start_pos > 0 too"""
+@pytest.mark.parametrize("tile", ["", "256x256", "128x256", "64x128"])
+def test_prefill_gemm_pf_chunks_match_reference(model_files, recipe, tile, monkeypatch):
+    """prefill chunks on the hand-written prefill GEMM (kernels/gemm_pf.hip, M >= 33): 64-row chunks of
+    a 150-token prompt -- two 64-row chunks on gemm_pf (each tile shape), the 22-row tail on the ring
+    GEMM -- against the fp32 reference, continued at start_pos > 0 too"""
     monkeypatch.setenv("AIOS_PREFILL_GEMM_ROWS", "64")
-    monkeypatch.setenv("AIOS_PREFILL_BLAS_MIN", "32")
+    if tile:
+        monkeypatch.setenv("AIOS_GEMM_PF_TILE", tile)
     path = model_files[recipe]
     eng, cfg = _load(path)
-    assert eng.blas_prefill and eng.blas_prefill_min_rows == 32
     ref = ReferenceModel.from_gguf(path, kv_bf16=True)
     prompt = [1] + list(np.random.default_rng(5).integers(3, cfg.vocab_size, 149))
     rl = ref.forward(prompt)[-1]

@@ -36,7 +36,7 @@ def main():
             for _ in range(n):
                 eng.prefill(0, p, 0, True)
             dt = (time.perf_counter() - t0) / n
-            r = dict(path=("blas" if getattr(eng, "blas_prefill", False) and T >= 64 else path), model=args.model,
+            r = dict(path=path, model=args.model,
                      recipe=args.recipe, prompt_tokens=T, ms=round(dt * 1e3, 2),
                      tok_per_s=round(T / dt, 1))
             rows.append(r)
