@@ -245,6 +245,7 @@ PYBIND11_MODULE(_engine, m) {
       .def("capture_graphs", &Engine::capture_graphs, py::arg("max_b"), py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("stream", &Engine::stream_handle)
       .def_property_readonly("k_cache_ptr", &Engine::kv_cache_k)
+      .def("attn_o_counters", &Engine::attn_o_counters)
       .def_property_readonly("v_cache_ptr", &Engine::kv_cache_v)
       .def("set_allreduce_ptr", [](Engine& e, uintptr_t fn, uintptr_t ctx) {
         e.set_allreduce(reinterpret_cast<AllReduceFn>(fn), reinterpret_cast<void*>(ctx));
@@ -271,6 +272,9 @@ PYBIND11_MODULE(_engine, m) {
       .def("ipc_handle", [](const XgmiComm& c) { return py::bytes(c.ipc_handle()); })
       .def("set_ranks_per_gpu", &XgmiComm::set_ranks_per_gpu)
       .def_property_readonly("fuse_grid", &XgmiComm::fuse_grid)
+      .def_property_readonly("fuse_eligible", &XgmiComm::fuse_eligible)
+      .def_property_readonly("uncached", &XgmiComm::uncached)
+      .def("disable_fuse", &XgmiComm::disable_fuse)
       .def("connect", [](XgmiComm& c, const std::vector<py::bytes>& hs) {
         std::vector<std::string> v;
         for (auto& h : hs) v.push_back(std::string(h));
@@ -413,6 +417,12 @@ PYBIND11_MODULE(_engine, m) {
         py::arg("ml"), py::arg("out"), py::arg("counters"), py::arg("st"), py::arg("split") = 0,
         py::arg("block_table") = 0, py::arg("bt_rows") = 0, py::arg("ts") = 0);
   m.def("attn_decode_split", &attn_decode_split);
+  // physical identity of a device (PCI bus id): ranks that share a GPU see the same string
+  m.def("device_pci_bus_id", [](int dev) {
+    char buf[64] = {0};
+    HIP_CHECK(hipDeviceGetPCIBusId(buf, (int)sizeof(buf), dev));
+    return std::string(buf);
+  });
   m.def("rmsnorm", [](uintptr_t x, int ldx, uintptr_t w, uintptr_t y, int ldy, int rows, int n, float eps, uintptr_t st) {
     launch_rmsnorm((const float*)x, ldx, (const float*)w, (float*)y, ldy, rows, n, eps, S(st));
   });

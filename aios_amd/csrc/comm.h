@@ -107,6 +107,12 @@ class XgmiComm {
   // world 1 or AIOS_TP_FUSE=0) and the engine-workgroup cap that lets every rank's grid be resident
   // at once when ranks share a GPU (0: one workgroup per CU)
   const ArDevCtx* fuse_ctx() const { return fuse_on_ && uncached_ && h_.world > 1 ? d_ : nullptr; }
+  // this rank's eligibility for the fused epilogue; create_comm all-gathers it and turns the path off
+  // everywhere unless EVERY rank is eligible (a rank on the fused path spins on flags that a rank
+  // running separate all-reduces never raises)
+  bool fuse_eligible() const { return fuse_on_ && uncached_; }
+  void disable_fuse() { fuse_on_ = false; }
+  bool uncached() const { return uncached_; }
   int fuse_grid() const { return fuse_grid_; }
   void set_ranks_per_gpu(int n);
   bool bf16_payload() const { return bf16_; }

@@ -145,6 +145,8 @@ class Engine {
 
   // raw device pointers for tests / custom kernels
   uintptr_t kv_cache_k() const { return (uintptr_t)k_cache_; }
+  // layer l's attention -> O counter block (kernels/attn_o.hip; tests / probes read it)
+  std::vector<int> attn_o_counters(int l) const;
   uintptr_t kv_cache_v() const { return (uintptr_t)v_cache_; }
 
  private:
@@ -220,6 +222,8 @@ class Engine {
   void fill_row_seeds(uint64_t* host_seeds, int B, uint64_t seed, const std::vector<uint64_t>& seeds);
   uint8_t* d_mask_ = nullptr;
   int n_chunks_ = 0;
+  int* attn_o_cnt_ = nullptr;  // [n_layers][ATTN_O_CNT_INTS] attention -> O hand-off counters (batch 1)
+  float* attn_o_x_ = nullptr;  // [8 XCDs][n_heads * head_dim] attention outputs of the XCD-local path
   int* attn_cnt_ = nullptr;  // [max(prefill_rows, max_batch)][n_kv_heads] combine tickets
   float2* rope_cs_ = nullptr;  // [max_ctx][head_dim/2] cos/sin computed in double on the host
   int prefill_rows_ = 64;  // rows of the prefill workspace

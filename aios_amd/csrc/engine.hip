@@ -462,6 +462,10 @@ void Engine::finalize() {
     const size_t nc = (size_t)std::max(prefill_rows_, Bm) * H;  // decode attention tickets [row][head]
     attn_cnt_ = (int*)dmalloc(nc * 4);
     HIP_CHECK(hipMemset(attn_cnt_, 0, nc * 4));
+    // batch-1 attention -> O hand-off counters (kernels/attn_o.hip), one per layer
+    attn_o_cnt_ = (int*)dmalloc((size_t)cfg_.n_layers * ATTN_O_CNT_INTS * 4);
+    HIP_CHECK(hipMemset(attn_o_cnt_, 0, (size_t)cfg_.n_layers * ATTN_O_CNT_INTS * 4));
+    attn_o_x_ = (float*)dmalloc((size_t)8 * H * hd * 4);  // per-XCD attention outputs
   }
   {
     const int half = hd / 2;
@@ -977,6 +981,7 @@ void Engine::layer_decode(int l, int B) {
     }
   }
   // ---- attention (fp32 output: a bf16 hand-off to O measured neutral, 544.0-544.5 vs 545.0-545.7 tok/s)
+  bool attn_o_fused = false;
   {
     AttnDecodeArgs a;
     a.split = 0;
@@ -990,13 +995,24 @@ void Engine::layer_decode(int l, int B) {
     a.n_chunks = n_chunks_;
     a.scale = 1.f / std::sqrt((float)hd);
     a.o_part = opart_; a.ml = ml_; a.out = attn_; a.counters = attn_cnt_;
-    launch_attn_decode(a, stream_);
+    // batch 1 without TP, AIOS_ATTN_O=1: attention and the O GEMV (+ residual) in one launch, the
+    // O weights streaming while attention runs (kernels/attn_o.hip; measured no faster, off by
+    // default); otherwise two launches
+    // (counter re-arm: layer l zeroes layer l-1's, cyclically -- every B = 1 step runs all layers)
+    if (B == 1 && cfg_.tp_size <= 1 && cfg_.n_layers >= 2)
+      attn_o_fused = launch_attn_o(a, gemv_args({&L.wo}, d, qd, B, attn_, qd, nullptr, x_, d, EPI_RESID, l),
+                                   attn_o_cnt_ + (size_t)l * ATTN_O_CNT_INTS,
+                                   attn_o_cnt_ + (size_t)((l + cfg_.n_layers - 1) % cfg_.n_layers) * ATTN_O_CNT_INTS,
+                                   attn_o_x_, stream_);
+    if (!attn_o_fused) launch_attn_decode(a, stream_);
   }
   // ---- O projection (+ residual; TP: partial -> all-reduce -> add, fused into the GEMV epilogue
   // when the comm provides it)
   {
     const bool tp = cfg_.tp_size > 1;
-    if (!(tp && tp_fuse_gemv(gemv_args({&L.wo}, d, qd, B, attn_, qd, nullptr, x_, d, EPI_TP_RESID, l)))) {
+    if (attn_o_fused) {
+      // (launched above, in the attention launch)
+    } else if (!(tp && tp_fuse_gemv(gemv_args({&L.wo}, d, qd, B, attn_, qd, nullptr, x_, d, EPI_TP_RESID, l)))) {
       GemvArgs a = gemv_args({&L.wo}, d, qd, B, attn_, qd, nullptr, tp ? ff_ : x_, d, tp ? EPI_STORE : EPI_RESID, l);
       launch_gemv(a, stream_);
       if (tp) allreduce(ff_, (size_t)B * d, x_);
@@ -1026,6 +1042,14 @@ void Engine::layer_decode(int l, int B) {
   }
 }
 
+std::vector<int> Engine::attn_o_counters(int l) const {
+  std::vector<int> v(ATTN_O_CNT_INTS);
+  if (l < 0 || l >= cfg_.n_layers) throw std::runtime_error("attn_o_counters: bad layer");
+  HIP_CHECK(hipStreamSynchronize(stream_));
+  HIP_CHECK(hipMemcpy(v.data(), attn_o_cnt_ + (size_t)l * ATTN_O_CNT_INTS, v.size() * 4, hipMemcpyDeviceToHost));
+  return v;
+}
+
 // EPI_TP_RESID (the O / down all-reduce in the GEMV epilogue, gemv_q8.h) when the comm provides the
 // fused context
 bool Engine::tp_fuse_gemv(GemvArgs a) {
@@ -1040,8 +1064,9 @@ bool Engine::tp_fuse_gemv(GemvArgs a) {
   a.tune_u = 0;
   a.tune_ksplit = 0;
   a.grid_cap = tp_fuse_grid_;  // ranks sharing a GPU: every rank's workgroups resident together
-  launch_gemv(a, stream_);
-  return true;
+  // (false: the row-pair kernel did not take it -- stage capacity within grid_cap, LDS plan -- and
+  // nothing was launched; the caller runs the plain GEMV + all-reduce)
+  return launch_gemv_tp_fused(a, stream_);
 }
 
 // logits_[B][V] = rmsnorm(x) . output^T.  Vocab-parallel TP: this rank holds V/tp rows of

@@ -66,5 +66,7 @@ struct GemvArgs {
 
 void launch_gemv(const GemvArgs& a, hipStream_t st);
 bool gemv_engine_fits(const GemvArgs& a);  // the B-row LDS-DMA engine serves a (gemv_dispatch.hip)
+// EPI_TP_RESID through the row-pair kernel; false = nothing launched (gemv_dispatch.hip)
+bool launch_gemv_tp_fused(const GemvArgs& a, hipStream_t st);
 
 }  // namespace aios

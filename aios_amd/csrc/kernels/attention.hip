@@ -28,34 +28,7 @@ namespace aios {
 template <int HD, int G>
 __global__ void __launch_bounds__(512) attn_decode_kernel(AttnDecodeArgs a, AttnSplit sp_) {
   kernarg_warm<sizeof(AttnDecodeArgs) + sizeof(AttnSplit)>();
-  const int wg = blockIdx.x;
-  const int len = a.seq_len[blockIdx.z];
-  if (G > 1 && len <= a.short_len) {
-    // XCD-aware roles: workgroups are dealt round-robin over the 8 XCDs (blockIdx % 8), so
-    // workgroup wg takes query head (wg % 8) * (H / 8) + (wg / 8) / P -- the G query heads of a KV
-    // head then run on one XCD and read its K/V from that XCD's L2 after the first miss (the plain
-    // mapping put them on G different XCDs: G MALL/HBM reads of every K/V line)
-    int h, sp;
-    if ((a.n_heads & 7) == 0 && sp_.xcd) {
-      if (wg >= a.n_heads * sp_.p_short) return;
-      const int j = wg >> 3;
-      h = (wg & 7) * (a.n_heads >> 3) + j / sp_.p_short;
-      sp = j % sp_.p_short;
-    } else {
-      h = wg / sp_.p_short;
-      sp = wg % sp_.p_short;
-    }
-    if (h >= a.n_heads) return;
-    attn_core<HD, 1>(a, sp, h / G, h, h, sp_.p_short, sp_.ppw);
-  } else {
-    constexpr int GL = AttnGL<G>::value;
-    const int hsi = wg / sp_.p_long, sp = wg % sp_.p_long;
-    if (hsi >= a.n_kv_heads * (G / GL)) return;
-    const int kvh = hsi / (G / GL), h0 = kvh * G + (hsi % (G / GL)) * GL;
-    // long mode: every K/V line is read by exactly one workgroup -> streaming loads (round 4,
-    // same box: --prompt 4000 546.9 -> 567.0 tok/s, 16000 467.6 -> 487.3)
-    attn_core<HD, GL>(a, sp, kvh, h0, h0, sp_.p_long, sp_.ppw, a.kv_nt != 0);
-  }
+  attn_role<HD, G>(a, sp_, blockIdx.x);
 }
 
 template <int HD>
@@ -92,19 +65,7 @@ void launch_attn_decode(const AttnDecodeArgs& a, hipStream_t st) {
   if (!a.counters) throw std::runtime_error("attn_decode: counters buffer required ([B][n_heads])");
   if (a.max_ctx % 128) throw std::runtime_error("attn_decode: max_ctx must be a multiple of 128");
   const int G = a.n_heads / a.n_kv_heads;
-  AttnDecodeArgs b = a;
-  if (b.split <= 0) b.split = attn_decode_split(a.max_ctx, a.B, a.n_kv_heads);
-  if (b.combine_trips == 0) b.combine_trips = attn_env_int("AIOS_ATTN_COMBINE", 1);
-  if (b.kv_nt < 0) b.kv_nt = attn_env_int("AIOS_ATTN_NT", 1);
-  if (b.kv_tail < 0) b.kv_tail = attn_env_int("AIOS_ATTN_TAIL", 1);
-  // Batched decode fills the chip with (row, KV head) workgroups on its own: from
-  // AIOS_ATTN_GROUPED_MIN such workgroups up, every context length takes the grouped mode (one
-  // K/V read for the G query heads of a KV head) instead of the per-query-head split that buys
-  // batch-1 latency with G x the K/V reads and workgroups
-  if (b.short_len < 0) {
-    const int grouped_min = attn_env_int("AIOS_ATTN_GROUPED_MIN", 128);
-    b.short_len = (grouped_min > 0 && a.B * a.n_kv_heads >= grouped_min) ? 0 : ATTN_SPLIT_LEN;
-  }
+  const AttnDecodeArgs b = attn_resolve(a);
   if (b.split % ATTN_CHUNK) throw std::runtime_error("attn_decode: split must be a multiple of ATTN_CHUNK");
   if (a.head_dim == 128) launch_hd<128>(b, G, st);
   else if (a.head_dim == 64) launch_hd<64>(b, G, st);

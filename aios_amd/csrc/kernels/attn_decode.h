@@ -293,6 +293,7 @@ __device__ __forceinline__ void attn_core(const AttnDecodeArgs& a, int sp, int k
     const int h = h0 + g;
     if (nact == 1) {
       if (a.out16) a.out16[((size_t)b * a.n_heads + h) * HD + d] = f32_to_bf16(acc / L);
+      else if (a.out_wt) st_wt(a.out + ((size_t)b * a.n_heads + h) * HD + d, acc / L);
       else a.out[((size_t)b * a.n_heads + h) * HD + d] = acc / L;
     } else {
       st_wt(a.o_part + (((size_t)b * a.n_heads + h) * a.n_chunks + sp) * HD + d, acc);
@@ -368,6 +369,7 @@ __device__ __forceinline__ void attn_core(const AttnDecodeArgs& a, int sp, int k
         if (j < nact) acc = fmaf(s_pm[g][j], ov[j], acc);
       const int h = h0 + g;
       if (a.out16) a.out16[((size_t)b * a.n_heads + h) * HD + d] = f32_to_bf16(acc);
+      else if (a.out_wt) st_wt(a.out + ((size_t)b * a.n_heads + h) * HD + d, acc);
       else a.out[((size_t)b * a.n_heads + h) * HD + d] = acc;
     }
   };
@@ -415,7 +417,8 @@ __device__ __forceinline__ void attn_core(const AttnDecodeArgs& a, int sp, int k
         if (c + j < nact) acc = fmaf(s_pm[g][c + j], ov[j], acc);
     }
     if (a.out16) a.out16[((size_t)b * a.n_heads + h) * HD + d] = f32_to_bf16(acc);
-    else a.out[((size_t)b * a.n_heads + h) * HD + d] = acc;
+    else if (a.out_wt) st_wt(a.out + ((size_t)b * a.n_heads + h) * HD + d, acc);
+      else a.out[((size_t)b * a.n_heads + h) * HD + d] = acc;
   }
   if (threadIdx.x == 0) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
   stamp(6);
@@ -442,9 +445,61 @@ struct AttnSplit {
 };
 
 
+// workgroup wg's role in the flat grid (see attn_decode_kernel, attention.hip); returns with the
+// whole workgroup (every early exit inside is workgroup-uniform)
+template <int HD, int G>
+__device__ __forceinline__ void attn_role(const AttnDecodeArgs& a, const AttnSplit& sp_, int wg) {
+  const int len = a.seq_len[blockIdx.z];
+  if (G > 1 && len <= a.short_len) {
+    // XCD-aware roles: workgroups are dealt round-robin over the 8 XCDs (blockIdx % 8), so
+    // workgroup wg takes query head (wg % 8) * (H / 8) + (wg / 8) / P -- the G query heads of a KV
+    // head then run on one XCD and read its K/V from that XCD's L2 after the first miss (the plain
+    // mapping put them on G different XCDs: G MALL/HBM reads of every K/V line)
+    int h, sp;
+    if ((a.n_heads & 7) == 0 && sp_.xcd) {
+      if (wg >= a.n_heads * sp_.p_short) return;
+      const int j = wg >> 3;
+      h = (wg & 7) * (a.n_heads >> 3) + j / sp_.p_short;
+      sp = j % sp_.p_short;
+    } else {
+      h = wg / sp_.p_short;
+      sp = wg % sp_.p_short;
+    }
+    if (h >= a.n_heads) return;
+    attn_core<HD, 1>(a, sp, h / G, h, h, sp_.p_short, sp_.ppw);
+  } else {
+    constexpr int GL = AttnGL<G>::value;
+    const int hsi = wg / sp_.p_long, sp = wg % sp_.p_long;
+    if (hsi >= a.n_kv_heads * (G / GL)) return;
+    const int kvh = hsi / (G / GL), h0 = kvh * G + (hsi % (G / GL)) * GL;
+    // long mode: every K/V line is read by exactly one workgroup -> streaming loads (round 4,
+    // same box: --prompt 4000 546.9 -> 567.0 tok/s, 16000 467.6 -> 487.3)
+    attn_core<HD, GL>(a, sp, kvh, h0, h0, sp_.p_long, sp_.ppw, a.kv_nt != 0);
+  }
+}
+
 inline int attn_env_int(const char* k, int dflt) {
   const char* e = std::getenv(k);
   return e ? std::atoi(e) : dflt;
+}
+
+int attn_decode_split(int max_ctx, int B, int n_kv_heads);
+// the launcher's defaults filled in (split, combine, K/V load policy, short-mode length)
+inline AttnDecodeArgs attn_resolve(const AttnDecodeArgs& a) {
+  AttnDecodeArgs b = a;
+  if (b.split <= 0) b.split = attn_decode_split(a.max_ctx, a.B, a.n_kv_heads);
+  if (b.combine_trips == 0) b.combine_trips = attn_env_int("AIOS_ATTN_COMBINE", 1);
+  if (b.kv_nt < 0) b.kv_nt = attn_env_int("AIOS_ATTN_NT", 1);
+  if (b.kv_tail < 0) b.kv_tail = attn_env_int("AIOS_ATTN_TAIL", 1);
+  // Batched decode fills the chip with (row, KV head) workgroups on its own: from
+  // AIOS_ATTN_GROUPED_MIN such workgroups up, every context length takes the grouped mode (one
+  // K/V read for the G query heads of a KV head) instead of the per-query-head split that buys
+  // batch-1 latency with G x the K/V reads and workgroups
+  if (b.short_len < 0) {
+    const int grouped_min = attn_env_int("AIOS_ATTN_GROUPED_MIN", 128);
+    b.short_len = (grouped_min > 0 && a.B * a.n_kv_heads >= grouped_min) ? 0 : ATTN_SPLIT_LEN;
+  }
+  return b;
 }
 
 // the launch shape for AttnDecodeArgs a (split already resolved): fills the split and returns the

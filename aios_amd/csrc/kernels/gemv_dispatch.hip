@@ -44,6 +44,27 @@ bool gemv_engine_fits(const GemvArgs& a) {
   return false;
 }
 
+bool gemv_tpf_q4k(const GemvArgs&, hipStream_t);
+bool gemv_tpf_q6k(const GemvArgs&, hipStream_t);
+bool gemv_tpf_q5k(const GemvArgs&, hipStream_t);
+bool gemv_tpf_q4_0(const GemvArgs&, hipStream_t);
+bool gemv_tpf_q8_0(const GemvArgs&, hipStream_t);
+
+// EPI_TP_RESID (the TP all-reduce in the GEMV epilogue): launched by the row-pair kernel, or false
+// with nothing launched (format, shape or stage capacity outside it) -- the caller then runs the
+// plain GEMV and a separate all-reduce
+bool launch_gemv_tp_fused(const GemvArgs& a, hipStream_t st) {
+  if (a.nseg != 1 || a.epi != EPI_TP_RESID) return false;
+  switch (a.seg[0].qtype) {
+    case QT_Q4_K: return gemv_tpf_q4k(a, st);
+    case QT_Q6_K: return gemv_tpf_q6k(a, st);
+    case QT_Q5_K: return gemv_tpf_q5k(a, st);
+    case QT_Q4_0: return gemv_tpf_q4_0(a, st);
+    case QT_Q8_0: return gemv_tpf_q8_0(a, st);
+  }
+  return false;
+}
+
 bool gemv_supports(int qt0, int qt1) {
   if (qt0 == qt1)
     return qt0 == QT_Q4_K || qt0 == QT_Q6_K || qt0 == QT_Q5_K || qt0 == QT_Q4_0 || qt0 == QT_Q8_0 ||

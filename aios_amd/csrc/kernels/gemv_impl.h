@@ -238,6 +238,8 @@ __device__ __forceinline__ void gemv_epilogue(const GemvArgs& a, int grow, int b
         cache[base + db] = f32_to_bf16(v1);
       }
     } break;
+    default:
+      __builtin_trap();  // an epilogue these kernels do not do (EPI_TP_RESID: row-pair kernel only)
   }
 }
 
@@ -550,6 +552,17 @@ void launch_gemv_t(GemvArgs a, hipStream_t st) {
   hipLaunchKernelGGL((gemv_kernel<QT0, QT1, B, U>), dim3(blocks), dim3(GEMV_THREADS), lds, st, a);
 }
 
+// the fused TP all-reduce epilogue (EPI_TP_RESID, batch 1): the row-pair kernel or nothing
+template <int QT0>
+bool launch_gemv_tpf(const GemvArgs& a, hipStream_t st) {
+  if constexpr (QT0 == QT_F16 || QT0 == QT_BF16) {
+    return false;
+  } else {
+    if (a.B != 1 || !a.act_q8 || a.nseg != 1 || a.epi != EPI_TP_RESID) return false;
+    return launch_gemv_q8<QT0, QT0, 1>(a, st);
+  }
+}
+
 template <int QT0, int QT1>
 void launch_gemv_pair(const GemvArgs& a, hipStream_t st) {
   constexpr int W = QFmt<QT0>::W;
@@ -565,6 +578,8 @@ void launch_gemv_pair(const GemvArgs& a, hipStream_t st) {
       if (a.B > 4 && launch_gemv_q8<QT0, QT1, 8>(a, st)) return;
     }
   }
+  if (a.epi == EPI_TP_RESID)  // only the row-pair int8 kernel does the fused all-reduce epilogue
+    throw std::runtime_error("gemv: EPI_TP_RESID launch not taken by the row-pair kernel (use launch_gemv_tp_fused)");
   if (a.x16 || a.y16) throw std::runtime_error("bf16 GEMV input / SwiGLU output: int8-activation kernels only");
   if (!a.force_v1) {
     if (a.B == 1 && launch_gemv_persistent<QT0, QT1, 1, 2>(a, st)) return;

@@ -516,6 +516,8 @@ __device__ __forceinline__ void gemv_epilogue1(const GemvArgs& a, int grow, floa
         }
       }
     } break;
+    default:
+      __builtin_trap();  // an epilogue this kernel does not do (EPI_TP_RESID runs in the tpf path)
   }
 }
 
@@ -906,8 +908,10 @@ inline size_t q8_lds_bytes(int K) {
   return 64 * 4 + (size_t)B * (K / W) * R * 8 + (size_t)B * K + 2048 + 16;
 }
 
+// false (nothing launched): an EPI_TP_RESID launch whose rows do not fit the fused stage within the
+// co-residency cap -- the caller takes the separate all-reduce instead
 template <int QT0, int QT1, int B, int U, int PIPE>
-void launch_q8_rows(const GemvArgs& a, size_t lds, hipStream_t st) {
+bool launch_q8_rows(const GemvArgs& a, size_t lds, hipStream_t st) {
   static int occ = -1;
   if (occ < 0) {
     int o = 0;
@@ -965,15 +969,17 @@ void launch_q8_rows(const GemvArgs& a, size_t lds, hipStream_t st) {
   }
   if (!blocks) blocks = std::min((npairs + nw - 1) / nw, cus * per_cu);
   if (a.epi == EPI_TP_RESID) {
-    // fused all-reduce: at most grid_cap workgroups (every rank sharing a GPU resident at once),
-    // at most TPF_SLOTS, and each workgroup's pairs inside its stage slot (TPF_CAP values)
-    if (a.grid_cap > 0) blocks = std::min(blocks, a.grid_cap);
-    blocks = std::min(blocks, TPF_SLOTS);
+    // fused all-reduce: at most grid_cap workgroups (every rank sharing a GPU resident at once --
+    // spinning workgroups past it could wait on peers that cannot be scheduled), at most
+    // TPF_SLOTS, and each workgroup's pairs inside its stage slot (TPF_CAP values)
+    const int cap = a.grid_cap > 0 ? std::min(a.grid_cap, TPF_SLOTS) : TPF_SLOTS;
+    blocks = std::min(blocks, cap);
     auto per_wg = [&](int g) { return 2 * nw * ((npairs + g * nw - 1) / (g * nw)); };
-    while (per_wg(blocks) > TPF_CAP && blocks < TPF_SLOTS) ++blocks;
-    if (per_wg(blocks) > TPF_CAP) throw std::runtime_error("EPI_TP_RESID: output rows above the fused stage capacity");
+    while (per_wg(blocks) > TPF_CAP && blocks < cap) ++blocks;
+    if (per_wg(blocks) > TPF_CAP) return false;
   }
   hipLaunchKernelGGL((gemv_q8_rows<QT0, QT1, B, U, PIPE>), dim3(blocks), dim3(nw * 64), lds, st, a);
+  return true;
 }
 
 template <int QT0, int QT1, int B>
@@ -1009,26 +1015,26 @@ bool launch_gemv_q8(GemvArgs a, hipStream_t st) {
           u = nch <= 64 ? 11 : 12;
       }
       switch (u) {
-        case 11: launch_q8_rows<QT0, QT1, 1, 1, 1>(a, lds, st); break;  // one pair per wave: the K slice in
-        case 12: launch_q8_rows<QT0, QT1, 1, 2, 1>(a, lds, st); break;  // one single-buffered item
-        case 13: launch_q8_rows<QT0, QT1, 1, 3, 2>(a, lds, st); break;  // tuning: U = 3/4 double-buffered
-        case 14: launch_q8_rows<QT0, QT1, 1, 4, 2>(a, lds, st); break;
-        case 21: launch_q8_rows<QT0, QT1, 1, 1, 3>(a, lds, st); break;  // tuning: triple / quad buffers
-        case 22: launch_q8_rows<QT0, QT1, 1, 2, 3>(a, lds, st); break;
-        case 31: launch_q8_rows<QT0, QT1, 1, 1, 4>(a, lds, st); break;
-        case 1: launch_q8_rows<QT0, QT1, 1, 1, 2>(a, lds, st); break;
-        case 2: launch_q8_rows<QT0, QT1, 1, 2, 2>(a, lds, st); break;
-        case 3: launch_q8_rows<QT0, QT1, 1, 3, 1>(a, lds, st); break;
-        case 4: launch_q8_rows<QT0, QT1, 1, 4, 1>(a, lds, st); break;
-        case 5: launch_q8_rows<QT0, QT1, 1, 5, 1>(a, lds, st); break;
-        case 6: launch_q8_rows<QT0, QT1, 1, 6, 1>(a, lds, st); break;
-        case 7: launch_q8_rows<QT0, QT1, 1, 7, 1>(a, lds, st); break;
-        default: launch_q8_rows<QT0, QT1, 1, 8, 1>(a, lds, st); break;
+        case 11: return launch_q8_rows<QT0, QT1, 1, 1, 1>(a, lds, st);  // one pair per wave: the K slice in
+        case 12: return launch_q8_rows<QT0, QT1, 1, 2, 1>(a, lds, st);  // one single-buffered item
+        case 13: return launch_q8_rows<QT0, QT1, 1, 3, 2>(a, lds, st);  // tuning: U = 3/4 double-buffered
+        case 14: return launch_q8_rows<QT0, QT1, 1, 4, 2>(a, lds, st);
+        case 21: return launch_q8_rows<QT0, QT1, 1, 1, 3>(a, lds, st);  // tuning: triple / quad buffers
+        case 22: return launch_q8_rows<QT0, QT1, 1, 2, 3>(a, lds, st);
+        case 31: return launch_q8_rows<QT0, QT1, 1, 1, 4>(a, lds, st);
+        case 1: return launch_q8_rows<QT0, QT1, 1, 1, 2>(a, lds, st);
+        case 2: return launch_q8_rows<QT0, QT1, 1, 2, 2>(a, lds, st);
+        case 3: return launch_q8_rows<QT0, QT1, 1, 3, 1>(a, lds, st);
+        case 4: return launch_q8_rows<QT0, QT1, 1, 4, 1>(a, lds, st);
+        case 5: return launch_q8_rows<QT0, QT1, 1, 5, 1>(a, lds, st);
+        case 6: return launch_q8_rows<QT0, QT1, 1, 6, 1>(a, lds, st);
+        case 7: return launch_q8_rows<QT0, QT1, 1, 7, 1>(a, lds, st);
+        default: return launch_q8_rows<QT0, QT1, 1, 8, 1>(a, lds, st);
       }
     } else if constexpr (B == 8) {
-      launch_q8_rows<QT0, QT1, 8, 1, 2>(a, lds, st);
+      return launch_q8_rows<QT0, QT1, 8, 1, 2>(a, lds, st);
     } else {
-      launch_q8_rows<QT0, QT1, B, 2, 2>(a, lds, st);
+      return launch_q8_rows<QT0, QT1, B, 2, 2>(a, lds, st);
     }
     return true;
   }

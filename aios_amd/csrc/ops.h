@@ -4,6 +4,7 @@
 // into a hipGraph.
 #pragma once
 #include "common.h"
+#include <vector>
 #include "gemv.h"
 #include "qweight.h"
 
@@ -110,9 +111,17 @@ struct AttnDecodeArgs {
   int kv_nt = -1;          // long mode: K/V loads with the streaming (nt) policy (-1: AIOS_ATTN_NT, default 1)
   int kv_tail = -1;        // last partial block: loads only for live keys (-1: AIOS_ATTN_TAIL, default 1)
   int combine_trips = 0;   // split-K combine: 0 = launcher (AIOS_ATTN_COMBINE, default one round trip), 2 = two
+  int out_wt = 0;          // fp32 out with write-through (agent-scope) stores: read in the same launch (attn_o.hip)
 };
 constexpr int ATTN_CHUNK = 64;
 void launch_attn_decode(const AttnDecodeArgs& a, hipStream_t st);
+struct GemvArgs;
+// batch 1: attention then the O GEMV reading its output, as one launch (kernels/attn_o.hip); false
+// (nothing launched) outside the shapes it serves.  cnt: this launch's counter block
+// (ATTN_O_CNT_INTS ints, zero on entry); rearm: the block of the launch before it in a fixed cycle,
+// zeroed here; xloc: per-XCD copies of the attention output (8 x n_heads x head_dim floats).
+constexpr int ATTN_O_CSTRIDE = 32, ATTN_O_CNT_INTS = 1024;
+bool launch_attn_o(const AttnDecodeArgs& a, const GemvArgs& g, int* cnt, int* rearm, float* xloc, hipStream_t st);
 int attn_decode_split(int max_ctx, int B, int n_kv_heads);
 
 // causal flash attention for a prefill chunk of T tokens at positions [start, start+T) of one

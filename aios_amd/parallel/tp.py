@@ -44,8 +44,16 @@ def comm_kind() -> str:
     return k
 
 
-def ranks_per_gpu(world: int) -> int:
-    """TP ranks that share one GPU on this node (1 on a node with a GPU per rank)."""
+def ranks_per_gpu(world: int, identities: Optional[List[str]] = None) -> int:
+    """TP ranks that share one GPU (1 on a node with a GPU per rank).  With `identities` (every
+    rank's physical device identity, all-gathered: host + PCI bus id) it counts the ranks on the
+    most shared device -- the same answer on every rank, and right when each rank sees only its own
+    GPU (HIP_VISIBLE_DEVICES per rank makes device_count() 1 everywhere).  Without them: inferred
+    from the visible device count (single-process tools)."""
+    if identities:
+        from collections import Counter
+
+        return max(Counter(identities).values())
     try:
         import torch
 
@@ -55,30 +63,108 @@ def ranks_per_gpu(world: int) -> int:
     return max(1, -(-world // n)) if n > 0 else 1
 
 
+def device_identity(device: int) -> str:
+    """host + PCI bus id of `device` (ranks that share a GPU report the same string)."""
+    import socket
+
+    from ..runtime import native
+
+    try:
+        bus = native.require().device_pci_bus_id(device)
+    except Exception:  # noqa: BLE001
+        bus = f"device{device}"
+    return f"{socket.gethostname()}/{bus}"
+
+
+def comm_self_test(comm, rank: int, world: int, device: int) -> bool:
+    """All-reduce (one-shot and two-shot sizes) and column all-gather through `comm`, checked on the
+    host against the values every rank contributed.  Run once at TP init: a peer mapping that
+    silently misbehaves (wrong IPC memory type, a stale mapping) shows up here, not as a wrong token."""
+    import torch
+
+    dev = torch.device("cuda", device)
+    st = torch.cuda.current_stream(dev).cuda_stream
+    ok = True
+    for n in (4096, 16384, 1 << 20):
+        if n > comm.capacity:
+            continue
+        base = torch.arange(n, dtype=torch.float32, device=dev) * 1e-3
+        t = base + (rank + 1)
+        comm.allreduce(t.data_ptr(), n, 0, st)
+        torch.cuda.synchronize(dev)
+        want = base * world + world * (world + 1) / 2
+        ok &= bool(torch.allclose(t, want, rtol=1e-2, atol=1e-2))  # (two-shot stages bf16)
+    rows, sl = 2, 64
+    if rows * sl * world <= comm.capacity:
+        ld = sl * world
+        g = torch.full((rows, ld), -7.0, dtype=torch.float32, device=dev)
+        g[:, rank * sl:(rank + 1) * sl] = rank + 0.25
+        comm.allgather_cols(g.data_ptr(), rows, sl, ld, st)
+        torch.cuda.synchronize(dev)
+        want = torch.arange(world, dtype=torch.float32, device=dev).repeat_interleave(sl) + 0.25
+        ok &= bool(torch.equal(g, want.expand(rows, ld)))
+    ok &= not comm.error()
+    return ok
+
+
 def create_comm(rank: int, world: int, device: int, cap_floats: int, group=None, kind: Optional[str] = None):
     """XgmiComm (or RcclComm, see comm_kind) connected to every rank of `group` (default: the
-    default process group)."""
+    default process group).
+
+    The xGMI comm is checked before use: every rank's fused-epilogue eligibility (uncached peer
+    memory, AIOS_TP_FUSE) is all-gathered and the fused path stays on only if ALL agree, then
+    `comm_self_test` runs on every rank (AIOS_TP_SELFTEST=0 skips it).  A failed self-test or a rank
+    without uncached peer memory falls back to RCCL when each rank has its own GPU, and is an error
+    when ranks share one (RCCL refuses that)."""
     import torch.distributed as dist
 
     from ..runtime import native
 
     m = native.require()
-    if (kind or comm_kind()) == "rccl":
+
+    def rccl():
         uid: List[Any] = [m.RcclComm.unique_id() if rank == 0 else None]
         if world > 1:
             dist.broadcast_object_list(uid, src=0, group=group)
         return m.RcclComm(rank, world, device, uid[0])
+
+    if (kind or comm_kind()) == "rccl":
+        return rccl()
+    ids: List[Any] = [device_identity(device)]
+    if world > 1:
+        ids = [None] * world
+        dist.all_gather_object(ids, device_identity(device), group=group)
+    per_gpu = ranks_per_gpu(world, ids)
     comm = m.XgmiComm(rank, world, device, cap_floats)
-    per_gpu = ranks_per_gpu(world)
     if per_gpu > 1:  # every spinning workgroup of every rank must be resident on the shared GPU at once
         comm.call_wg = max(1, min(512, 1024 // per_gpu))
         # ... including the O / down GEMV engines whose epilogue runs the all-reduce (EPI_TP_RESID)
         comm.set_ranks_per_gpu(per_gpu)
-    if world > 1:
-        handles: List[Any] = [None] * world
-        dist.all_gather_object(handles, comm.ipc_handle(), group=group)
-        comm.connect(handles)
-    return comm
+    if world == 1:
+        return comm
+    handles: List[Any] = [None] * world
+    dist.all_gather_object(handles, comm.ipc_handle(), group=group)
+    comm.connect(handles)
+    flags: List[Any] = [None] * world
+    dist.all_gather_object(flags, (bool(comm.fuse_eligible), bool(comm.uncached)), group=group)
+    if not all(f[0] for f in flags):
+        comm.disable_fuse()
+    ok = True
+    if os.environ.get("AIOS_TP_SELFTEST", "1") != "0":
+        oks: List[Any] = [None] * world
+        dist.all_gather_object(oks, comm_self_test(comm, rank, world, device), group=group)
+        ok = all(oks)
+    if ok and all(f[1] for f in flags):
+        return comm
+    why = "self-test mismatch" if not ok else "a rank without uncached peer memory"
+    if per_gpu > 1:
+        if not ok:
+            raise RuntimeError(f"xGMI comm: {why} (ranks share a GPU, no RCCL fallback)")
+        log.warning("xGMI comm: %s; fused all-reduce epilogue off", why)
+        return comm
+    log.warning("xGMI comm: %s; falling back to RCCL", why)
+    del comm
+    return rccl()
 
 
 class TPEngine:

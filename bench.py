@@ -178,6 +178,8 @@ def main():
     import torch
 
     n_dev = max(1, torch.cuda.device_count())  # counting devices does not initialise the GPU
+    if args.dry_run and os.environ.get("AIOS_BENCH_DEVICES"):  # (launcher tests: a node's device count)
+        n_dev = int(os.environ["AIOS_BENCH_DEVICES"])
     share = world > n_dev                      # more ranks than GPUs: ranks share (not a scaling run)
     device = local % n_dev
     dist = gloo = None

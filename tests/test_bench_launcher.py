@@ -50,3 +50,27 @@ def test_gpus_8_through_torchrun_dry_run():
     lines = [json.loads(m) for m in re.findall(r"\{[^{}]*\}", r.stdout)]
     assert sorted(d["rank"] for d in lines) == list(range(8))
     assert all(d["world"] == 8 for d in lines)
+
+
+def test_gpus_8_one_device_per_rank():
+    """the 8-GPU node shape: with 8 devices visible every rank gets its own (share False -> RCCL
+    process group, the XgmiComm / self-test path, the persistent kernels on), device = LOCAL_RANK"""
+    env = _env()
+    env["AIOS_BENCH_DEVICES"] = "8"
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8", "--dry-run"],
+                       capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [json.loads(m) for m in re.findall(r"\{[^{}]*\}", r.stdout)]
+    assert sorted(d["rank"] for d in lines) == list(range(8))
+    assert not any(d["ranks_share_gpu"] for d in lines)
+    assert sorted(d["device"] for d in lines) == list(range(8))
+
+
+def test_ranks_per_gpu_from_device_identity():
+    """sharing is counted from the physical device identity, not device_count() (each
+    rank may see only its own GPU)"""
+    from aios_amd.parallel.tp import ranks_per_gpu
+
+    assert ranks_per_gpu(8, [f"node/0000:{i:02x}:00.0" for i in range(8)]) == 1
+    assert ranks_per_gpu(4, ["node/0000:05:00.0"] * 4) == 4
+    assert ranks_per_gpu(4, ["n/a", "n/a", "n/b", "n/b"]) == 2

@@ -1,4 +1,6 @@
 """GPU end-to-end: native engine vs the fp32 reference model on synthetic GGUF checkpoints."""
+import time
+
 import numpy as np
 import pytest
 import torch
@@ -396,3 +398,47 @@ def test_sample_first_on_device(model_files):
     x = eng.sample_first(3, 1.0, 0, 1.0, 1234)
     assert x == eng.sample_first(3, 1.0, 0, 1.0, 1234)
     assert len({eng.sample_first(3, 1.0, 0, 1.0, s) for s in range(1, 30)}) > 1
+
+
+@pytest.mark.parametrize("preset,ctx", [("test-mistral-shape", 40), ("mistral-7b", 40), ("mistral-7b", 700),
+                                        ("tinyllama-1.1b", 40), ("llama3-8b", 150)])
+def test_attention_o_one_launch_matches_two_launches(monkeypatch, preset, ctx):
+    """Batch-1 decode with attention and the O GEMV in ONE launch (kernels/attn_o.hip: the O
+    workgroups stream their weights while attention runs and wait on its arrival count) gives the
+    same logits as the two-launch path -- short (per-query-head) and long (split-K + combine)
+    attention modes, eager steps and the captured graph loop."""
+    import dataclasses
+
+    from aios_amd.runtime.loader import random_engine
+
+    monkeypatch.setenv("AIOS_GEMM_PF_TUNE", "0")
+    try:
+        cfg = dataclasses.replace(get_preset(preset), n_layers=2)
+    except KeyError:
+        pytest.skip(f"no preset {preset}")
+    res = {}
+    for on in ("0", "1"):
+        monkeypatch.setenv("AIOS_ATTN_O", on)  # (off by default: measured no faster)
+        eng = random_engine(cfg, "Q4_K_M", seed=3, max_ctx=1024, max_slots=2, max_batch=1)
+        prompt = [1] + [(7 * i) % (cfg.vocab_size - 3) + 3 for i in range(ctx - 1)]
+        tok = int(np.argmax(eng.prefill(0, prompt, 0, True)))
+        eng.prefill(1, prompt, 0, False)
+        first, pos, logs = tok, len(prompt), []
+        t0 = time.perf_counter()
+        for _ in range(5):
+            tok = eng.decode([0], [tok], [pos])[0]
+            logs.append(np.asarray(eng.last_logits(1))[0].copy())
+            pos += 1
+        # a hand-off that never completes shows as the 1 s wait bound per launch, not as wrong numbers
+        assert (time.perf_counter() - t0) / 5 < 0.5, "fused attention -> O waits ran into their bound"
+        eng.decode_loop_prepare([1], [first], [len(prompt)])
+        eng.decode_loop_run(1, 6, True)
+        hist = list(eng.decode_loop_history(1, len(prompt) + 1, 6))
+        res[on] = (np.stack(logs), hist)
+        del eng
+    l0, h0 = res["0"]
+    l1, h1 = res["1"]
+    assert np.isfinite(l1).all()
+    err = np.abs(l0 - l1).max()
+    assert err <= 1e-4 * max(np.abs(l0).max(), 1.0), err
+    assert h0 == h1

@@ -156,6 +156,41 @@ def test_tp_xgmi_allreduce_and_sharded_model(tmp_path, world, gemm_prefill, prom
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_tp_fused_epilogue_int8_activations(tmp_path, world):
+    """the production TP decode path -- int8 GEMV activations, the batch-1 O / down
+    all-reduces in the row-pair GEMV epilogue (EPI_TP_RESID: per-slot epochs, double-buffered stage
+    halves, peer flags) -- against AIOS_TP_FUSE=0 (separate all-reduce launches) and against TP=1,
+    over 24 decode steps (each stage half reused a dozen times per layer) plus the graph loop."""
+    outs = {}
+    for fuse in ("1", "0"):
+        out = tmp_path / f"tpq{world}_{fuse}.json"
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(world),
+               "--master-addr", "127.0.0.1", "--master-port", str(29700 + 2 * world + int(fuse)),
+               os.path.join(ROOT, "tools", "tp_check.py"), "--out", str(out), "--model", "test-tp8-shape",
+               "--prompt-len", "21", "--steps", "24", "--act-q8", "--dump-logits"]
+        env = dict(os.environ, AIOS_TP_FUSE=fuse, AIOS_PREFILL_GEMM="0")
+        r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=600, env=env)
+        assert r.returncode == 0, r.stderr[-3000:]
+        outs[fuse] = json.loads(out.read_text())
+    on, off = outs["1"], outs["0"]
+    assert on["tp_fused"] and not off["tp_fused"]
+    for res in (on, off):
+        assert not res["comm_error_flag"] and not res["comm_error_flag_model"]
+        m = res["model"]
+        assert m["act_q8"] and m["graph_tokens_match"]
+        # the int8 path quantises the sharded activations per shard (norm-scaled x, the SwiGLU output of
+        # each shard): ~1e-2 of the logit scale against TP=1 by design; a sharding bug is O(1)
+        tol = 5e-2 * max(1.0, m["logit_scale"])
+        assert max(m["decode_logit_max_abs_diff_per_step"]) < tol, m["decode_logit_max_abs_diff_per_step"]
+    import numpy as np
+
+    a, b = np.asarray(on["model"]["step_logits"]), np.asarray(off["model"]["step_logits"])
+    assert on["model"]["tp_tokens"] == off["model"]["tp_tokens"]
+    assert np.abs(a - b).max() < 1e-3 * max(1.0, np.abs(b).max())
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("norm_fuse", [1, 0])
 def test_tp_batched_decode_fused_norm(tmp_path, norm_fuse):
     """Batched TP decode (B = 6: the skinny-GEMM path) with C1 / C2 fused with the next RMSNorm: the

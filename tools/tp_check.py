@@ -35,6 +35,10 @@ def main():
     ap.add_argument("--batch", type=int, default=0,
                     help="also decode B >= 5 rows (the skinny-GEMM path, C1 / C2 fused with the next RMSNorm) "
                          "and compare every row's logits against the unsharded engine at the same batch")
+    ap.add_argument("--act-q8", action="store_true",
+                    help="int8 GEMV activations on both sides (the production decode path: with TP the batch-1 O / "
+                         "down all-reduces then run in the GEMV epilogue, EPI_TP_RESID, unless AIOS_TP_FUSE=0)")
+    ap.add_argument("--dump-logits", action="store_true", help="store every decode step's logits in the JSON")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -152,13 +156,13 @@ def main():
 
         write_synthetic_gguf(path, cfg, args.recipe, seed=7)
     dist.barrier()
-    # fp32 activations on both sides (the int8-activation path quantises per shard, so its
-    # rounding differs from TP=1 by design); greedy stream from TP, then TP=1 teacher-forced on
-    # the same tokens, comparing logits at every step
+    # the same activation precision on both sides (fp32 by default; --act-q8: int8 per 32-block,
+    # whose blocks a K-sharded GEMV quantises exactly as TP=1 does); greedy stream from TP, then
+    # TP=1 teacher-forced on the same tokens, comparing logits at every step
     max_ctx = (args.prompt_len + args.steps + 64 + 127) // 128 * 128
     nb = max(2, args.batch)
     eng, comm = build_tp_engine(cfg, rank, world, dev, path=path, max_ctx=max_ctx, max_slots=nb, max_batch=nb,
-                                act_q8=False)
+                                act_q8=args.act_q8)
     res["vocab_parallel"] = bool(eng.vocab_parallel)
     res["tp_fused"] = bool(getattr(eng, "tp_fused", False))  # C1 / C2 in the GEMV engine's epilogue
     prompt = [cfg.bos_id] + [(11 * i + 5) % (cfg.vocab_size - 3) + 3 for i in range(args.prompt_len - 1)]
@@ -193,7 +197,7 @@ def main():
         tp.close()
         from aios_amd.runtime.loader import load_engine
 
-        ref, _, _ = load_engine(path, max_ctx=max_ctx, max_slots=nb, max_batch=nb, device=dev, act_q8=False)
+        ref, _, _ = load_engine(path, max_ctx=max_ctx, max_slots=nb, max_batch=nb, device=dev, act_q8=args.act_q8)
         rl = np.asarray(ref.prefill(0, prompt, 0, True))
         pos = len(prompt)
         diffs = []
@@ -207,7 +211,10 @@ def main():
             "prefill_logit_max_abs_diff": float(np.abs(logits - rl).max()),
             "decode_logit_max_abs_diff_per_step": diffs, "logit_scale": float(np.abs(rl).max()),
             "graph_tokens_match": [toks[0]] + hist == toks[:len(hist) + 1],
+            "act_q8": bool(args.act_q8),
         }
+        if args.dump_logits:
+            res["model"]["step_logits"] = [[float(v) for v in l] for l in step_logits]
         if B > 1:
             for b in range(B):
                 ref.prefill(b, prompts[b], 0, False)
