@@ -53,6 +53,8 @@ def parse():
     ap.add_argument("--fp32-act", action="store_true",
                     help="headline with fp32 activations in the GEMVs instead of int8 (q8_1-style) ones")
     ap.add_argument("--no-tp", action="store_true", help="skip the strategic-tier TP secondary")
+    ap.add_argument("--no-serving", action="store_true",
+                    help="skip the gRPC operational-tier (config 2) and co-resident tiers (config 4) secondaries")
     ap.add_argument("--no-goal-plan", action="store_true",
                     help="skip the goal->plan latency secondary (BASELINE.json's agent metric)")
     ap.add_argument("--tp-model", default="llama3-70b")
@@ -126,8 +128,35 @@ def measure_goal_plan(goals: int = 16, timeout_s: float = 60.0):
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "tools"))
     from bench_goal_plan import main_async
 
-    ns = _ap.Namespace(model="mistral-7b", goals=goals, warmup=2, burst=0, plan_tokens=160)
+    # + goal_plan_burst: 3 tactical goals submitted at once with a 300-token plan cap
+    ns = _ap.Namespace(model="mistral-7b", goals=goals, warmup=2, burst=3, plan_tokens=160, burst_plan_tokens=300)
     return asyncio.run(asyncio.wait_for(main_async(ns), timeout_s))
+
+
+def measure_grpc(timeout_s: float = 120.0):
+    """BASELINE.json config 2: TinyLlama-1.1B BF16, the operational tier, tokens/s through
+    AIRuntime.StreamInfer / Infer on loopback gRPC (tools/bench_grpc.py; reference path
+    runtime/src/grpc_service.rs:33-177).  Bounded: a run past timeout_s reports an error."""
+    import argparse as _ap
+    import asyncio
+
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "tools"))
+    from bench_grpc import main_async
+
+    ns = _ap.Namespace(tokens=256, reps=3, recipe="BF16")
+    return asyncio.run(asyncio.wait_for(main_async(ns), timeout_s))
+
+
+def measure_coresident(steps: int = 256, prompt: int = 128):
+    """BASELINE.json config 4: TinyLlama-1.1B and Mistral-7B resident together on one GPU, each
+    replaying its decode graph on its own stream, dispatched concurrently from two host threads
+    (tools/bench_coresident.py): per-tier tok/s alone and concurrent, the aggregate, HBM per tier."""
+    import argparse as _ap
+
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "tools"))
+    from bench_coresident import run
+
+    return run(_ap.Namespace(steps=steps, prompt=prompt))
 
 
 def measure_tp(args, rank: int, world: int, device: int, gloo):
@@ -235,6 +264,22 @@ def main():
             goal_plan = {"error": f"{type(e).__name__}: {e}"[:300]}
             print(f"goal_plan failed: {goal_plan['error']}", file=sys.stderr, flush=True)
 
+    # BASELINE configs 2 and 4 (rank 0; each bounded, a failure is reported, never costs the headline)
+    grpc_res = coresident = None
+    if not args.no_secondary and not args.no_serving and rank == 0:
+        try:
+            edt, _ = measure("tinyllama-1.1b", "BF16", 1, args.prompt, 256, 16, not args.no_graph, None, device)
+            grpc_res = measure_grpc()
+            grpc_res["engine_tok_s"] = round(256 / edt, 1)
+        except Exception as e:  # noqa: BLE001
+            grpc_res = {"error": f"{type(e).__name__}: {e}"[:300]}
+            print(f"tinyllama_bf16_grpc failed: {grpc_res['error']}", file=sys.stderr, flush=True)
+        try:
+            coresident = measure_coresident()
+        except Exception as e:  # noqa: BLE001
+            coresident = {"error": f"{type(e).__name__}: {e}"[:300]}
+            print(f"coresident failed: {coresident['error']}", file=sys.stderr, flush=True)
+
     # max over ranks
     if dist is not None:
         t = torch.tensor([dt, secondary or 0.0, other_act or 0.0], dtype=torch.float64)
@@ -321,6 +366,15 @@ def main():
                 out["goal_plan"] = {k: goal_plan[k] for k in ("metric", "p90_ms", "goals", "tasks_per_goal",
                                                               "reactive_p50_ms", "plan_tokens_cap", "model",
                                                               "baseline_ms")}
+                b = goal_plan.get("burst", {})
+                out["goal_plan_burst"] = {"metric": "goal->plan latency, 3 tactical goals submitted at once",
+                                          "p50_ms": b.get("p50_ms"), "p90_ms": b.get("p90_ms"),
+                                          "goals": b.get("concurrent_goals"), "plan_tokens_cap": b.get("plan_tokens_cap"),
+                                          "wall_s": b.get("wall_s")}
+        if grpc_res is not None:
+            out["tinyllama_bf16_grpc"] = grpc_res
+        if coresident is not None:
+            out["coresident"] = coresident
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.barrier()

@@ -21,7 +21,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=512)
     ap.add_argument("--prompt", type=int, default=128)
-    args = ap.parse_args()
+    print(json.dumps(run(ap.parse_args())), flush=True)
+
+
+def run(args):
+    """the measurement (bench.py's `coresident` secondary calls this); returns the summary dict"""
     import torch  # noqa: F401  (HIP runtime init order as in bench.py)
 
     from aios_amd.models.config import get_preset
@@ -55,7 +59,9 @@ def main():
 
     out = {"bench": "co-resident tiers, B=1 decode on one GPU", "steps": args.steps, "prompt": args.prompt,
            "data": "synthetic (random-init Q4_K_M weights, synthetic prompts)",
-           "hbm_weights_gb": round(sum(e.weight_bytes for _, e in models.values()) / 1e9, 3)}
+           "hbm_weights_gb": round(sum(e.weight_bytes for _, e in models.values()) / 1e9, 3),
+           "hbm_gb_per_tier": {n: {"weights": round(e.weight_bytes / 1e9, 3), "kv": round(e.kv_bytes / 1e9, 3),
+                                   "workspace": round(e.workspace_bytes / 1e9, 3)} for n, (_, e) in models.items()}}
     for name in models:
         prep(name)
         r = {}
@@ -81,7 +87,9 @@ def main():
     # the same token counts run one model after the other (a single decode stream time-sharing the GPU)
     out["time_shared_aggregate_tok_s"] = round(
         sum(steps.values()) / sum(steps[n] / out[f"{n}_alone_tok_s"] for n in models), 1)
-    print(json.dumps(out), flush=True)
+    for name in list(models):
+        del models[name]
+    return out
 
 
 if __name__ == "__main__":

@@ -87,7 +87,11 @@ async def main_async(args):
         await submit(d)
     tac = [await submit(TACTICAL[i % len(TACTICAL)] + f" #{i}") for i in range(args.goals)]
     rea = [await submit(REACTIVE[i % len(REACTIVE)]) for i in range(args.goals)]
-    # concurrent burst: the runtime batches the decomposition calls
+    # concurrent burst: the runtime batches the decomposition calls (its own plan-token cap:
+    # bench.py's goal_plan_burst secondary runs 3 goals at 300 tokens)
+    import aios_amd.orchestrator.state as orch_state
+
+    orch_state.PLAN_MAX_TOKENS = getattr(args, "burst_plan_tokens", 0) or args.plan_tokens
     t = time.perf_counter()
     burst = await asyncio.gather(*(submit(TACTICAL[i % len(TACTICAL)] + f" burst {i}") for i in range(args.burst)))
     burst_s = time.perf_counter() - t
@@ -105,7 +109,8 @@ async def main_async(args):
            "p90_ms": round(q(lat, 0.9), 1), "mean_ms": round(statistics.mean(lat), 1), "goals": len(lat),
            "tasks_per_goal": round(statistics.mean(x[1] for x in tac), 2),
            "reactive_p50_ms": round(statistics.median(rlat), 2),
-           "burst": {"concurrent_goals": n_burst, "wall_s": round(burst_s, 3), "p50_ms": round(statistics.median(blat), 1)},
+           "burst": {"concurrent_goals": n_burst, "wall_s": round(burst_s, 3), "p50_ms": round(statistics.median(blat), 1),
+                     "p90_ms": round(q(blat, 0.9), 1), "plan_tokens_cap": orch_state.PLAN_MAX_TOKENS},
            "plan_tokens_cap": args.plan_tokens, "model": f"{args.model} Q4_K_M (random-init, synthetic vocab)",
            "baseline_ms": "200-500 (tactical tier, docs/VISION.md:45)", "model_load_s": round(load_s, 1),
            "data": "synthetic goals; decomposition output length fixed by plan_tokens_cap (random weights)"}
@@ -123,6 +128,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--burst", type=int, default=8)
     ap.add_argument("--plan-tokens", type=int, default=160)
+    ap.add_argument("--burst-plan-tokens", type=int, default=0, help="plan-token cap of the burst (0: --plan-tokens)")
     print(json.dumps(asyncio.run(main_async(ap.parse_args()))), flush=True)
 
 
