@@ -41,7 +41,7 @@ __device__ __forceinline__ float raw_exp2(float x) { return __builtin_amdgcn_exp
 constexpr int FP_KT = 64;  // keys per tile
 
 template <int HD, int G>
-__global__ void __launch_bounds__(256) attn_prefill_kernel(AttnPrefillArgs a) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) attn_prefill_kernel(AttnPrefillArgs a) {
   constexpr int BQ = 128 / G;          // query positions per workgroup
   constexpr int KS = HD / 16;          // k-steps of the S MFMA
   constexpr int OT = HD / 32;          // O^T accumulator tiles (32 dims each)
@@ -50,13 +50,32 @@ __global__ void __launch_bounds__(256) attn_prefill_kernel(AttnPrefillArgs a) {
   // 8-byte column chunks and its 32-lane half two such groups 16 dims apart; rows HD + 32 elements
   // apart put the 4 rows 16 banks apart (mod 64) and the two groups 8 banks apart: conflict-free
   constexpr int VROW = HD + 32;
-  __shared__ __attribute__((aligned(16))) bf16_t sK[FP_KT * KROW];
-  __shared__ __attribute__((aligned(16))) bf16_t sV[FP_KT * VROW];
+  // two LDS tile buffers (dynamic: 2 x 37 KB for HD 128), K then V in each
+  constexpr int TILE_ELEMS = FP_KT * (KROW + VROW);
+  extern __shared__ __attribute__((aligned(16))) bf16_t fp_smem[];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int l32 = lane & 31, half = lane >> 5;
-  // heaviest (latest) query blocks first
-  const int qb = gridDim.x - 1 - blockIdx.x, kvh = blockIdx.y;
+  // Causal balance: workgroup L (dispatch order, x fastest) and L + W/2 share a CU once the grid
+  // fills every CU twice (the second pass lands on the CUs in the same order), so the first half
+  // takes query blocks heaviest-first and the second half lightest-first: every CU gets blocks qb and
+  // nx-1-qb, nx + 1 key tiles in all.  (Before, both of a CU's workgroups had the same qb: at 2k
+  // tokens one CU did 64 tiles while the average was 33.)  Odd KV-head counts keep heaviest-first.
+  const int nx = gridDim.x, ny = gridDim.y;
+  int qb, kvh;
+  if ((ny & 1) == 0) {
+    const int L = blockIdx.y * nx + blockIdx.x, W2 = nx * ny / 2;
+    if (L < W2) {
+      qb = nx - 1 - L % nx;
+      kvh = L / nx;
+    } else {
+      qb = (L - W2) % nx;
+      kvh = ny / 2 + (L - W2) / nx;
+    }
+  } else {
+    qb = nx - 1 - blockIdx.x;
+    kvh = blockIdx.y;
+  }
   const int T = a.T, start = a.start;
   const int t0 = qb * BQ;
   // this lane's query row (column of S^T / O^T)
@@ -97,36 +116,42 @@ __global__ void __launch_bounds__(256) attn_prefill_kernel(AttnPrefillArgs a) {
   const int last_pos = start + min(T, t0 + BQ) - 1;  // highest query position of the block
   const int ntiles = last_pos / FP_KT + 1;
 
-  // tile loader: 64 keys x HD dims of K and of V, 16 B per piece
+  // tile loader: 64 keys x HD dims of K and of V, 16 B per piece, into register buffer r (2 of
+  // them: tile kt + 2 is requested while tile kt is computed, so two tiles of math cover the
+  // memory latency); stage() writes one buffer to an LDS tile buffer
   constexpr int PIECES = FP_KT * HD / 8;  // 16-B pieces per tensor per tile
   constexpr int PPT = PIECES / 256;        // per thread
-  u32x4_t kreg[PPT], vreg[PPT];
-  auto load = [&](int kt) {
+  struct Regs {
+    u32x4_t k[PPT], v[PPT];
+  };
+  const int nt_last = ntiles - 1;
+  auto load = [&](Regs& r, int kt) {
+    kt = min(kt, nt_last);  // (clamped: the pipeline's tail requests are re-reads, never unmapped blocks)
     const size_t tbase = (size_t)kv_block(a.block_table, maxb, a.slot, kt * FP_KT) * blk_stride +
                          (size_t)(kt & 1) * FP_KT * HD;
     static_for<PPT>([&](auto I) {
       constexpr int i = decltype(I)::value;
       const int idx = tid + 256 * i, key = idx / (HD / 8), c = idx % (HD / 8);
       const size_t off = tbase + (size_t)key * HD + c * 8;
-      kreg[i] = *(const u32x4_t*)(kc + off);
-      vreg[i] = *(const u32x4_t*)(vc + off);
+      r.k[i] = *(const u32x4_t*)(kc + off);
+      r.v[i] = *(const u32x4_t*)(vc + off);
     });
   };
-  auto stage = [&]() {
+  auto stage = [&](const Regs& r, bf16_t* buf) {
+    bf16_t* sK = buf;
+    bf16_t* sV = buf + FP_KT * KROW;
     static_for<PPT>([&](auto I) {
       constexpr int i = decltype(I)::value;
       const int idx = tid + 256 * i, key = idx / (HD / 8), c = idx % (HD / 8);
-      *(u32x4_t*)(sK + key * KROW + c * 8) = kreg[i];
-      *(u32x4_t*)(sV + key * VROW + c * 8) = vreg[i];
+      *(u32x4_t*)(sK + key * KROW + c * 8) = r.k[i];
+      *(u32x4_t*)(sV + key * VROW + c * 8) = r.v[i];
     });
   };
-
-  load(0);
-  for (int kt = 0; kt < ntiles; ++kt) {
-    __syncthreads();  // previous tile's LDS reads done
-    stage();
-    __syncthreads();
-    if (kt + 1 < ntiles) load(kt + 1);  // next tile in flight during this tile's math
+  // one 64-key tile of math on LDS buffer buf (a tile past the last one -- the odd count's pad --
+  // is fully masked: p = 0, alpha = 1)
+  auto math = [&](const bf16_t* buf, int kt) {
+    const bf16_t* sK = buf;
+    const bf16_t* sV = buf + FP_KT * KROW;
     // ---- S^T = K Q^T for the tile's two 32-key halves
     f32x16_t st[2];
 #pragma unroll
@@ -200,6 +225,30 @@ __global__ void __launch_bounds__(256) attn_prefill_kernel(AttnPrefillArgs a) {
         o[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf, o[i], 0, 0, 0);
       }
     }
+  };
+
+  // Pipeline (round 5; was: one register buffer, stage + two barriers per tile, 130-150 us per
+  // 2k-token layer): two register buffers A / B and two LDS tile buffers L0 / L1, ONE barrier per
+  // tile.  Iteration kt computes tile kt from L[kt & 1] while tile kt + 2 is requested into the
+  // register buffer just staged, then stages tile kt + 1 into the other LDS buffer (last read two
+  // iterations ago, before the previous barrier) and barriers.  Branch-free: tiles run in pairs, an
+  // odd count computes one fully masked pad tile.
+  bf16_t* L0 = fp_smem;
+  bf16_t* L1 = fp_smem + TILE_ELEMS;
+  Regs A, B;
+  load(A, 0);
+  load(B, 1);
+  stage(A, L0);
+  __syncthreads();
+  for (int kt = 0; kt < ntiles; kt += 2) {
+    load(A, kt + 2);
+    math(L0, kt);
+    stage(B, L1);
+    __syncthreads();
+    load(B, kt + 3);
+    math(L1, kt + 1);
+    stage(A, L0);
+    __syncthreads();
   }
   // ---- normalise and store bf16: O^T[dim][row], dim = 32 i + (r&3) + 8 (r>>2) + 4 half
   if (qvalid) {
@@ -226,11 +275,12 @@ template <int HD>
 static void prefill_hd(const AttnPrefillArgs& a, int G, hipStream_t st) {
   const int BQ = 128 / G;
   dim3 grid((a.T + BQ - 1) / BQ, a.n_kv_heads);
+  const size_t lds = (size_t)2 * FP_KT * ((HD + 8) + (HD + 32)) * sizeof(bf16_t);  // two K|V tile buffers
   switch (G) {
-    case 1: hipLaunchKernelGGL((attn_prefill_kernel<HD, 1>), grid, dim3(256), 0, st, a); break;
-    case 2: hipLaunchKernelGGL((attn_prefill_kernel<HD, 2>), grid, dim3(256), 0, st, a); break;
-    case 4: hipLaunchKernelGGL((attn_prefill_kernel<HD, 4>), grid, dim3(256), 0, st, a); break;
-    case 8: hipLaunchKernelGGL((attn_prefill_kernel<HD, 8>), grid, dim3(256), 0, st, a); break;
+    case 1: hipLaunchKernelGGL((attn_prefill_kernel<HD, 1>), grid, dim3(256), lds, st, a); break;
+    case 2: hipLaunchKernelGGL((attn_prefill_kernel<HD, 2>), grid, dim3(256), lds, st, a); break;
+    case 4: hipLaunchKernelGGL((attn_prefill_kernel<HD, 4>), grid, dim3(256), lds, st, a); break;
+    case 8: hipLaunchKernelGGL((attn_prefill_kernel<HD, 8>), grid, dim3(256), lds, st, a); break;
     default: throw std::runtime_error("attn_prefill: unsupported GQA group size");
   }
 }
