@@ -195,6 +195,42 @@ def measure_tp(args, rank: int, world: int, device: int, gloo):
     return dt, info
 
 
+def measure_collectives(rank: int, world: int, device: int, gloo):
+    """All-reduce latency of the two TP data planes at the decode / prefill message sizes the
+    engine issues: 16 KB (B=1 d=4096), 64 KB (B=4 or d=16384) and 32 MB (a 2k-token prefill chunk's
+    partial), xGMI one-shot / two-shot kernels (XgmiComm) vs librccl (RcclComm); max over ranks."""
+    import torch
+    import torch.distributed as td
+
+    from aios_amd.parallel.tp import create_comm
+
+    res = {}
+    dev = torch.device("cuda", device)
+    for kind in ("xgmi", "rccl"):
+        try:
+            comm = create_comm(rank, world, device, 8 << 20, gloo, kind=kind)
+        except Exception as e:  # noqa: BLE001
+            res[f"{kind}_error"] = f"{type(e).__name__}: {e}"[:200]
+            continue
+        st = torch.cuda.current_stream(dev).cuda_stream
+        for n, key in ((4096, "16KB"), (16384, "64KB"), (8 << 20, "32MB")):
+            x = torch.randn(n, device=dev)
+            for _ in range(5):
+                comm.allreduce(x.data_ptr(), n, 0, st)
+            torch.cuda.synchronize(dev)
+            td.barrier(group=gloo)
+            reps = 200 if n < (1 << 20) else 20
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                comm.allreduce(x.data_ptr(), n, 0, st)
+            torch.cuda.synchronize(dev)
+            t = torch.tensor([(time.perf_counter() - t0) / reps * 1e6])
+            td.all_reduce(t, op=td.ReduceOp.MAX, group=gloo)
+            res[f"{kind}_allreduce_us_{key}"] = round(float(t[0]), 2)
+        del comm
+    return res
+
+
 def main():
     args = parse()
     if os.environ.get("WORLD_SIZE") is None and args.gpus > 1:
@@ -255,6 +291,14 @@ def main():
             except Exception as e:  # noqa: BLE001
                 tp_dt, tp_info = None, {"error": f"{type(e).__name__}: {e}"[:300]}
                 print(f"[rank {rank}] tp_strategic failed: {tp_info['error']}", file=sys.stderr, flush=True)
+
+    collectives = None
+    if world > 1 and not share and not args.no_secondary and not args.no_tp:
+        try:
+            collectives = measure_collectives(rank, world, device, gloo)
+        except Exception as e:  # noqa: BLE001
+            collectives = {"error": f"{type(e).__name__}: {e}"[:300]}
+            print(f"[rank {rank}] collectives failed: {collectives['error']}", file=sys.stderr, flush=True)
 
     goal_plan = None
     if not args.no_secondary and not args.no_goal_plan and rank == 0:
@@ -371,6 +415,8 @@ def main():
                                           "p50_ms": b.get("p50_ms"), "p90_ms": b.get("p90_ms"),
                                           "goals": b.get("concurrent_goals"), "plan_tokens_cap": b.get("plan_tokens_cap"),
                                           "wall_s": b.get("wall_s")}
+        if collectives is not None:
+            out["collectives"] = collectives
         if grpc_res is not None:
             out["tinyllama_bf16_grpc"] = grpc_res
         if coresident is not None:

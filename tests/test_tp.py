@@ -4,6 +4,7 @@ TP=2/4/8 sharded model against TP=1 (several ranks sharing one GPU; tools/tp_che
 the strategic tier's target degree and AR_MAX_RANKS: its IPC mesh, one-shot pull over 7 peers and
 vocab-parallel all-gather run here with 8 processes on one GPU (not a scaling measurement)."""
 import json
+import time
 import os
 import subprocess
 import sys
@@ -188,6 +189,56 @@ def test_tp_fused_epilogue_int8_activations(tmp_path, world):
     a, b = np.asarray(on["model"]["step_logits"]), np.asarray(off["model"]["step_logits"])
     assert on["model"]["tp_tokens"] == off["model"]["tp_tokens"]
     assert np.abs(a - b).max() < 1e-3 * max(1.0, np.abs(b).max())
+
+
+@pytest.mark.gpu
+def test_tp_shared_gpu_with_cotenant_decode(tmp_path):
+    """TP=2 with both ranks sharing this GPU WHILE a third process runs a TinyLlama
+    decode loop on the same GPU (the co-resident operational tier): the spinning all-reduce / fused
+    epilogue workgroups must still meet (no comm.error(), numerics as without the co-tenant); the
+    slowdown of both is recorded."""
+    def tp_run(tag):
+        out = tmp_path / f"tpc_{tag}.json"
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
+               "--master-addr", "127.0.0.1", "--master-port", str(29760 + (tag == "cotenant")),
+               os.path.join(ROOT, "tools", "tp_check.py"), "--out", str(out), "--model", "test-tp8-shape",
+               "--prompt-len", "21", "--steps", "16", "--act-q8"]
+        r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=600,
+                           env=dict(os.environ, AIOS_PREFILL_GEMM="0"))
+        assert r.returncode == 0, r.stderr[-3000:]
+        return json.loads(out.read_text())
+
+    alone = tp_run("alone")
+    stop = tmp_path / "stop"
+    co = subprocess.Popen([sys.executable, os.path.join(ROOT, "tools", "cotenant_decode.py"), "--seconds", "240",
+                           "--stop-file", str(stop)], cwd=ROOT, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    try:
+        line = ""
+        t0 = time.time()
+        while "ready" not in line and time.time() - t0 < 180:
+            line = co.stdout.readline()
+            if not line and co.poll() is not None:
+                break
+        assert "ready" in line, co.stderr.read()[-2000:]
+        shared = tp_run("cotenant")
+    finally:
+        stop.write_text("1")
+        try:
+            outs, errs = co.communicate(timeout=60)
+        except subprocess.TimeoutExpired:
+            co.kill()
+            outs, errs = co.communicate()
+    assert co.returncode == 0, errs[-2000:]
+    cot = json.loads([l for l in outs.splitlines() if l.startswith("{")][-1])
+    for res in (alone, shared):
+        assert not res["comm_error_flag"] and not res["comm_error_flag_model"]
+        m = res["model"]
+        assert m["graph_tokens_match"]
+        assert max(m["decode_logit_max_abs_diff_per_step"]) < 5e-2 * max(1.0, m["logit_scale"])
+    assert shared["model"]["tp_tokens"] == alone["model"]["tp_tokens"]
+    print(json.dumps({"allreduce_us_8192_alone": alone["allreduce_us_8192"],
+                      "allreduce_us_8192_with_cotenant": shared["allreduce_us_8192"],
+                      "cotenant_tok_s": cot["tok_s"]}))
 
 
 @pytest.mark.gpu
