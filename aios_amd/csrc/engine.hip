@@ -1160,7 +1160,6 @@ void Engine::prefill_gemm(int slot, const std::vector<int>& tokens, int start_po
       const LayerW& L = layers_[l];
       bf16_t* kc = k_cache_ + (size_t)l * layer_kv_elems_;
       bf16_t* vc = v_cache_ + (size_t)l * layer_kv_elems_;
-      const bool qepi = sh && !cfg_.qk_norm && !cfg_.rope_neox && !L.bqkv && rope_cs_;
       // split-RMSNorm consumer / producer (as in layer_decode_gemm, on this chunk's rows)
       auto nrm_in = [&](GemmQArgs& g) {
         g.A = gm_xn16_; g.nrm_in = gm_npart_; g.nrm_parts = gm_nparts_; g.nrm_eps = cfg_.norm_eps;
@@ -1178,11 +1177,21 @@ void Engine::prefill_gemm(int slot, const std::vector<int>& tokens, int start_po
       g.seg[0] = L.wq.w; g.seg[1] = L.wk.w; g.seg[2] = L.wv.w;
       g.seg_n0[0] = 0; g.seg_n0[1] = qd; g.seg_n0[2] = qd + kvd;
       g.N = ldqkv; g.C = gm_qkv_; g.ldc = ldqkv; g.epi = GEPI_STORE;
-      if (qepi) {
-        g.epi = GEPI_QKV; g.col0 = 0;
-        g.head_dim = hd; g.q_dim = qd; g.kv_dim = kvd; g.n_kv_heads = Hkv; g.max_ctx = cfg_.max_ctx;
-        g.rope_cs = rope_cs_; g.pos = gm_pos_; g.slot = gm_slot_; g.block_table = d_bt_;
-        g.q_out = gm_q_; g.k_cache = kc; g.v_cache = vc;
+      // the RoPE / KV-cache epilogue: short chunks (ring / skinny GEMMs); the prefill GEMM's chunks
+      // (>= 33 rows) only with AIOS_PREFILL_QKV_EPI=1 -- it needs S = 1 plans, and at 2048 tokens
+      // the QKV GEMM then took 212.7 us against 115.7 (split-K) + 32 us of qkv_post (64 tokens:
+      // 5.77 vs 4.6 ms per prompt), profiles/prefill_r5.txt
+      const bool qepi_ok = !cfg_.qk_norm && !cfg_.rope_neox && !L.bqkv && rope_cs_ && !tp;
+      bool qepi = false;
+      if (qepi_ok) {
+        GemmQArgs q = g;
+        q.epi = GEPI_QKV; q.col0 = 0;
+        q.head_dim = hd; q.q_dim = qd; q.kv_dim = kvd; q.n_kv_heads = Hkv; q.max_ctx = cfg_.max_ctx;
+        q.rope_cs = rope_cs_; q.pos = gm_pos_; q.slot = gm_slot_; q.block_table = d_bt_;
+        q.q_out = gm_q_; q.k_cache = kc; q.v_cache = vc;
+        static const int pf_qkv = [] { const char* e = std::getenv("AIOS_PREFILL_QKV_EPI"); return e ? std::atoi(e) : 0; }();
+        qepi = sh || (pf_qkv && gemm_pf_serves(q));
+        if (qepi) g = q;
       }
       gemm(g);
       if (!qepi) {

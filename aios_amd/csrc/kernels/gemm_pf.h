@@ -30,6 +30,35 @@
 
 namespace aios {
 
+// GEPI_QKV (prefill chunks, non-NeoX RoPE, no QK-norm / bias, S = 1): the accumulator element
+// (m, n) of this lane goes to the attention inputs directly -- RoPE'd q fp32 to q_out[m][q_dim], RoPE'd
+// k and v as bf16 into the paged KV cache at (slot[m], pos[m]) -- the qkv_post launch and the fp32
+// QKV round trip folded into the epilogue.  The RoPE partner (column n ^ 1) is the lane ^ 1 in both
+// accumulator layouts (column = lane mod 16 / 32); every lane runs the DPP, the even one stores the pair.
+__device__ __forceinline__ void pf_qkv_out(const GemmQArgs& a, int m, int n, float v, bool even) {
+  const float w = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));
+  if (!even || m >= a.M) return;
+  const int hd = a.head_dim, pos = a.pos[m], slot = a.slot ? a.slot[m] : 0;
+  float v0 = v, v1 = w;
+  const int part = n < a.q_dim ? 0 : (n < a.q_dim + a.kv_dim ? 1 : 2);
+  const int r = n - (part == 0 ? 0 : (part == 1 ? a.q_dim : a.q_dim + a.kv_dim));
+  const int head = r / hd, lr = r - head * hd;
+  if (part < 2) {
+    const float2 t = a.rope_cs[(size_t)pos * (hd >> 1) + (lr >> 1)];
+    const float o0 = v0 * t.x - v1 * t.y, o1 = v0 * t.y + v1 * t.x;
+    v0 = o0;
+    v1 = o1;
+  }
+  if (part == 0) {
+    *(float2*)(a.q_out + (size_t)m * a.q_dim + n) = make_float2(v0, v1);
+  } else {
+    bf16_t* cache = part == 1 ? a.k_cache : a.v_cache;
+    const size_t base = kv_offset(a.block_table, a.max_ctx / KV_BLOCK, slot, a.n_kv_heads, head, pos, hd);
+    *(uint32_t*)(cache + base + lr) = pk_bf16(v0, v1);
+  }
+}
+
+
 // slot layout for one K-step: A, then the weight planes of BN columns
 template <int QT, int BM, int BN>
 struct PfLayout {
@@ -348,6 +377,8 @@ __device__ __forceinline__ void pf_body(const GemmQArgs& a, int m0, int n0, int 
           // interleaved gate/up columns: even lane = gate, odd lane = its up partner
           const float up = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));
           if (m < a.M && !(r16 & 1)) a.C16[(size_t)m * a.ldc + (n >> 1)] = f32_to_bf16(v / (1.f + __expf(-v)) * up);
+        } else if constexpr (EPI == GEPI_QKV) {
+          pf_qkv_out(a, m, n, v, !(r16 & 1));
         } else if (m < a.M) {
           float* cp = a.C + (size_t)m * a.ldc + n;
           if (S > 1) unsafeAtomicAdd(cp, v);
@@ -793,6 +824,8 @@ __device__ __forceinline__ void pf4_body(const GemmQArgs& a, int m0, int n0, int
         if constexpr (EPI == GEPI_SWIGLU_BF16) {
           const float up = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));
           if (m < a.M && !(r32 & 1)) a.C16[(size_t)m * a.ldc + (n >> 1)] = f32_to_bf16(v / (1.f + __expf(-v)) * up);
+        } else if constexpr (EPI == GEPI_QKV) {
+          pf_qkv_out(a, m, n, v, !(r32 & 1));
         } else if (m < a.M) {
           float* cp = a.C + (size_t)m * a.ldc + n;
           if (S > 1) unsafeAtomicAdd(cp, v);
@@ -959,6 +992,8 @@ __device__ __forceinline__ void pf8_body(const GemmQArgs& a, int m0, int n0, int
         if constexpr (EPI == GEPI_SWIGLU_BF16) {
           const float up = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));
           if (m < a.M && !(r16 & 1)) a.C16[(size_t)m * a.ldc + (n >> 1)] = f32_to_bf16(v / (1.f + __expf(-v)) * up);
+        } else if constexpr (EPI == GEPI_QKV) {
+          pf_qkv_out(a, m, n, v, !(r16 & 1));
         } else if (m < a.M) {
           float* cp = a.C + (size_t)m * a.ldc + n;
           if (S > 1) unsafeAtomicAdd(cp, v);
@@ -1244,6 +1279,8 @@ __device__ __forceinline__ void pf8c_body(const GemmQArgs& a, int m0, int n0, in
         if constexpr (EPI == GEPI_SWIGLU_BF16) {
           const float up = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));
           if (m < a.M && !(r16 & 1)) a.C16[(size_t)m * a.ldc + (n >> 1)] = f32_to_bf16(v / (1.f + __expf(-v)) * up);
+        } else if constexpr (EPI == GEPI_QKV) {
+          pf_qkv_out(a, m, n, v, !(r16 & 1));
         } else if (m < a.M) {
           float* cp = a.C + (size_t)m * a.ldc + n;
           if (S > 1) unsafeAtomicAdd(cp, v);
@@ -1496,6 +1533,7 @@ void pf8_launch(const GemmQArgs& a, int S, hipStream_t st) {
   switch (a.epi) {
     case GEPI_STORE: hipLaunchKernelGGL((gemm_pf8_kernel<QT0, QT1, BM, GEPI_STORE>), grid, block, lds, st, a); break;
     case GEPI_ACCUM: hipLaunchKernelGGL((gemm_pf8_kernel<QT0, QT1, BM, GEPI_ACCUM>), grid, block, lds, st, a); break;
+    case GEPI_QKV: hipLaunchKernelGGL((gemm_pf8_kernel<QT0, QT1, BM, GEPI_QKV>), grid, block, lds, st, a); break;
     default: hipLaunchKernelGGL((gemm_pf8_kernel<QT0, QT1, BM, GEPI_SWIGLU_BF16>), grid, block, lds, st, a); break;
   }
 }
@@ -1536,6 +1574,7 @@ void pf4_launch(const GemmQArgs& a, int S, hipStream_t st) {
   switch (a.epi) {
     case GEPI_STORE: hipLaunchKernelGGL((gemm_pf4_kernel<QT0, QT1, BM, WC, GEPI_STORE>), grid, block, lds, st, a); break;
     case GEPI_ACCUM: hipLaunchKernelGGL((gemm_pf4_kernel<QT0, QT1, BM, WC, GEPI_ACCUM>), grid, block, lds, st, a); break;
+    case GEPI_QKV: hipLaunchKernelGGL((gemm_pf4_kernel<QT0, QT1, BM, WC, GEPI_QKV>), grid, block, lds, st, a); break;
     default: hipLaunchKernelGGL((gemm_pf4_kernel<QT0, QT1, BM, WC, GEPI_SWIGLU_BF16>), grid, block, lds, st, a); break;
   }
 }

@@ -70,6 +70,14 @@ static std::map<PfKey, PfPlan>& pf_tuned() {
   static std::map<PfKey, PfPlan> m;
   return m;
 }
+// the best plan without split-K per key (GEPI_QKV launches: the RoPE / KV-cache epilogue cannot
+// take split partials; they use the STORE shape's tuned S = 1 plan -- tuning them for real would
+// write the KV cache)
+static std::map<PfKey, PfPlan>& pf_tuned_s1() {
+  static std::map<PfKey, PfPlan> m;
+  return m;
+}
+static bool pf_no_split(const GemmQArgs& a) { return a.epi == GEPI_SWIGLU_BF16 || a.epi == GEPI_QKV; }
 
 // every plan the launcher could run for these args (ksplit > 0 pins the split)
 static std::vector<PfPlan> pf_candidates(const GemmQArgs& a, bool bf) {
@@ -80,7 +88,7 @@ static std::vector<PfPlan> pf_candidates(const GemmQArgs& a, bool bf) {
       if (!pf_tile_ok(a, bn)) continue;
       for (int S : {1, 2, 3, 4, 6, 8, 12, 16}) {
         if (a.ksplit > 0 && S != a.ksplit) continue;
-        if (S > 1 && (a.epi == GEPI_SWIGLU_BF16 || nk / S < 2)) continue;
+        if (S > 1 && (pf_no_split(a) || nk / S < 2)) continue;
         if (!bf && bn == 256 && (a.K / 256) / S < 1) continue;
         PfPlan p;
         p.bm = bm; p.bn = bn; p.s = S;
@@ -95,8 +103,15 @@ static PfPlan pf_plan(const GemmQArgs& a, bool bf) {
   double bt = 1e30;
   if (!std::getenv("AIOS_GEMM_PF_TILE") && !std::getenv("AIOS_GEMM_PF_SPLIT") && a.ksplit <= 0) {
     std::lock_guard<std::mutex> g(pf_mu);
-    auto it = pf_tuned().find(pf_key(a));
-    if (it != pf_tuned().end()) return it->second;
+    if (a.epi == GEPI_QKV) {
+      GemmQArgs b = a;
+      b.epi = GEPI_STORE;
+      auto it = pf_tuned_s1().find(pf_key(b));
+      if (it != pf_tuned_s1().end()) return it->second;
+    } else {
+      auto it = pf_tuned().find(pf_key(a));
+      if (it != pf_tuned().end()) return it->second;
+    }
   }
   // AIOS_GEMM_PF_TILE=BMxBN / AIOS_GEMM_PF_SPLIT=S pin the plan (sweeps: tools/bench_gemm.py --pf-sweep)
   // (read per call: tests and sweeps change them inside one process)
@@ -112,7 +127,7 @@ static PfPlan pf_plan(const GemmQArgs& a, bool bf) {
       for (int S : {1, 2, 3, 4, 6, 8, 12, 16}) {
         if (a.ksplit > 0 && S != a.ksplit) continue;
         if (a.ksplit <= 0 && split > 0 && S != split) continue;
-        if (S > 1 && (a.epi == GEPI_SWIGLU_BF16 || nk / S < 2)) continue;
+        if (S > 1 && (pf_no_split(a) || nk / S < 2)) continue;
         if (!bf && bn == 256 && (a.K / 256) / S < 1) continue;  // pf8c slices whole 256-blocks
         const double t = pf_model(a, bm, bn, S, bf);
         if (t < bt) {
@@ -131,6 +146,7 @@ static PfPlan pf_plan(const GemmQArgs& a, bool bf) {
 static bool pf_eligible(const GemmQArgs& a);
 static bool pf_run(const GemmQArgs& a, const PfPlan& p, hipStream_t st) {
   const int qt0 = a.seg[0].qtype, qt1 = a.seg[a.nseg - 1].qtype;
+  if (p.s > 1 && a.epi == GEPI_QKV) return false;  // (plans keep S = 1 for it; a pinned split declines)
   if (p.s > 1 && a.epi == GEPI_STORE)
     HIP_CHECK(hipMemset2DAsync(a.C, (size_t)a.ldc * 4, 0, (size_t)a.N * 4, a.M, st));
   if (qt0 == QT_Q4_K && qt1 == QT_Q4_K) return pf_launch_fmt<QT_Q4_K, QT_Q4_K>(a, p.bm, p.bn, p.s, st);
@@ -151,7 +167,10 @@ bool launch_gemm_pf(const GemmQArgs& a, hipStream_t st) {
 
 static bool pf_eligible(const GemmQArgs& a) {
   if (a.nseg < 1 || a.M < 1) return false;
-  if (a.epi != GEPI_STORE && a.epi != GEPI_ACCUM && a.epi != GEPI_SWIGLU_BF16) return false;
+  if (a.epi != GEPI_STORE && a.epi != GEPI_ACCUM && a.epi != GEPI_SWIGLU_BF16 && a.epi != GEPI_QKV) return false;
+  if (a.epi == GEPI_QKV && (a.col0 != 0 || !a.q_out || !a.k_cache || !a.v_cache || !a.pos || !a.rope_cs ||
+                            a.head_dim % 2 || a.N != a.q_dim + 2 * a.kv_dim))
+    return false;
   if (a.nrm_in || a.lda % 8 || ((uintptr_t)a.A & 15)) return false;
   const int qt0 = a.seg[0].qtype, qt1 = a.seg[a.nseg - 1].qtype;
   for (int s = 0; s + 1 < a.nseg; ++s)
@@ -161,7 +180,7 @@ static bool pf_eligible(const GemmQArgs& a) {
   if (!bf && !((qt0 == QT_Q4_K || qt0 == QT_Q6_K) && (qt1 == QT_Q4_K || qt1 == QT_Q6_K))) return false;
   if (qt0 == QT_Q6_K && qt1 == QT_Q4_K) return false;  // not instantiated (no such stack in the GGUF recipes)
   if (a.epi == GEPI_SWIGLU_BF16 && (!a.C16 || a.nseg != 1)) return false;
-  if (a.epi != GEPI_SWIGLU_BF16 && !a.C) return false;
+  if (a.epi != GEPI_SWIGLU_BF16 && a.epi != GEPI_QKV && !a.C) return false;
   return true;
 }
 
@@ -175,8 +194,8 @@ int gemm_pf_autotune(const GemmQArgs& a, hipStream_t st) {
   hipEvent_t e0, e1;
   HIP_CHECK(hipEventCreate(&e0));
   HIP_CHECK(hipEventCreate(&e1));
-  PfPlan best = cands[0];
-  float bt = 1e30f;
+  PfPlan best = cands[0], best1 = cands[0];
+  float bt = 1e30f, bt1 = 1e30f;
   for (const PfPlan& p : cands) {
     pf_run(a, p, st);  // warm (code object load, caches)
     HIP_CHECK(hipEventRecord(e0, st));
@@ -189,12 +208,25 @@ int gemm_pf_autotune(const GemmQArgs& a, hipStream_t st) {
       bt = ms;
       best = p;
     }
+    if (p.s == 1 && ms < bt1) {
+      bt1 = ms;
+      best1 = p;
+    }
   }
   HIP_CHECK(hipEventDestroy(e0));
   HIP_CHECK(hipEventDestroy(e1));
   std::lock_guard<std::mutex> g(pf_mu);
   pf_tuned()[pf_key(a)] = best;
+  if (bt1 < 1e30f) pf_tuned_s1()[pf_key(a)] = best1;
   return (int)cands.size();
+}
+
+// whether launch_gemm_pf takes these args (the engine asks before choosing the GEPI_QKV epilogue
+// for a prefill chunk, which only this kernel and the small-M ones implement)
+bool gemm_pf_serves(const GemmQArgs& a) {
+  if (!pf_env("AIOS_GEMM_PF", 1) || a.M < pf_env("AIOS_GEMM_PF_MIN_M", 33) || !pf_eligible(a)) return false;
+  const PfPlan p = pf_plan(a, a.seg[0].qtype == QT_BF16);
+  return p.bm != 0 && !(p.s > 1 && a.epi == GEPI_QKV);
 }
 
 // the plan the launcher would pick (bindings / tools)

@@ -242,6 +242,7 @@ int gemm_skinny_ntile(const GemmQArgs& a);
 void launch_gemm_q(const GemmQArgs& a, hipStream_t st);
 // the prefill GEMM (kernels/gemm_pf.hip): true if it took the launch; its tile / split plan for a shape
 bool launch_gemm_pf(const GemmQArgs& a, hipStream_t st);
+bool gemm_pf_serves(const GemmQArgs& a);  // launch_gemm_pf would take a (gemm_pf.hip)
 void gemm_pf_plan(const GemmQArgs& a, int& bm, int& bn, int& s);
 bool gemm_pf_probe(const GemmQArgs& a, int probe, hipStream_t st);  // timing anatomy (tools only)
 // time every prefill-GEMM plan for these args (buffers overwritten) and keep the fastest for their M
