@@ -36,13 +36,60 @@ __global__ void rmsnorm_kernel(const float* __restrict__ x, int ldx, const float
   }
 }
 
+// rows of up to 256 * 4 * NV floats: the row stays in registers between the sum of squares and the
+// scaled store (one HBM read per element; the two-pass kernel above re-read it: 12.5 us for a
+// 2048 x 4096 prefill chunk, ~3.8 TB/s)
+template <typename OutT, int NV>
+__global__ void __launch_bounds__(256) rmsnorm_reg_kernel(const float* __restrict__ x, int ldx, const float* __restrict__ w,
+                                                          OutT* __restrict__ y, int ldy, int n, float eps) {
+  __shared__ float red[32];
+  const float* xr = x + (size_t)blockIdx.x * ldx;
+  float4 v[NV];
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int i = (threadIdx.x + 256 * k) * 4;
+    v[k] = i < n ? *(const float4*)(xr + i) : make_float4(0.f, 0.f, 0.f, 0.f);
+    s += v[k].x * v[k].x + v[k].y * v[k].y + v[k].z * v[k].z + v[k].w * v[k].w;
+  }
+  s = block_sum(s, red);
+  const float ir = rsqrtf(s / (float)n + eps);
+  OutT* yr = y + (size_t)blockIdx.x * ldy;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int i = (threadIdx.x + 256 * k) * 4;
+    if (i >= n) break;
+    const float4 g = *(const float4*)(w + i);
+    const float o0 = v[k].x * ir * g.x, o1 = v[k].y * ir * g.y, o2 = v[k].z * ir * g.z, o3 = v[k].w * ir * g.w;
+    if constexpr (sizeof(OutT) == 4) {
+      *(float4*)((float*)yr + i) = make_float4(o0, o1, o2, o3);
+    } else {
+      const uint32_t lo = f32_to_bf16(o0) | ((uint32_t)f32_to_bf16(o1) << 16);
+      const uint32_t hi = f32_to_bf16(o2) | ((uint32_t)f32_to_bf16(o3) << 16);
+      *(uint2*)((bf16_t*)yr + i) = make_uint2(lo, hi);
+    }
+  }
+}
+
+template <typename OutT>
+static void rmsnorm_go(const float* x, int ldx, const float* w, OutT* y, int ldy, int rows, int n, float eps,
+                       hipStream_t st) {
+  const bool al = n % 4 == 0 && ldx % 4 == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)w & 15) == 0;
+  if (al && n <= 1024 * 4)
+    hipLaunchKernelGGL((rmsnorm_reg_kernel<OutT, 4>), dim3(rows), dim3(256), 0, st, x, ldx, w, y, ldy, n, eps);
+  else if (al && n <= 1024 * 8)
+    hipLaunchKernelGGL((rmsnorm_reg_kernel<OutT, 8>), dim3(rows), dim3(256), 0, st, x, ldx, w, y, ldy, n, eps);
+  else
+    hipLaunchKernelGGL(rmsnorm_kernel<OutT>, dim3(rows), dim3(256), 0, st, x, ldx, w, y, ldy, n, eps);
+}
+
 void launch_rmsnorm(const float* x, int ldx, const float* w, float* y, int ldy, int rows, int n, float eps,
                     hipStream_t st) {
-  hipLaunchKernelGGL(rmsnorm_kernel<float>, dim3(rows), dim3(256), 0, st, x, ldx, w, y, ldy, n, eps);
+  rmsnorm_go<float>(x, ldx, w, y, ldy, rows, n, eps, st);
 }
 void launch_rmsnorm_bf16(const float* x, int ldx, const float* w, bf16_t* y, int ldy, int rows, int n, float eps,
                          hipStream_t st) {
-  hipLaunchKernelGGL(rmsnorm_kernel<bf16_t>, dim3(rows), dim3(256), 0, st, x, ldx, w, y, ldy, n, eps);
+  rmsnorm_go<bf16_t>(x, ldx, w, y, ldy, rows, n, eps, st);
 }
 
 __global__ void f32_to_bf16_kernel(const float* __restrict__ x, bf16_t* __restrict__ y, size_t n) {
@@ -164,7 +211,61 @@ __global__ void __launch_bounds__(256) qkv_post_kernel(QkvPostArgs a) {
     }
   }
 }
+// The common case -- non-NeoX RoPE, no QK-norm, no bias (Llama / Mistral / TinyLlama) -- one
+// workgroup per token row: pos, slot and the KV block are looked up ONCE per row (the per-(token,
+// head) kernel above ran a pos -> block-table -> store chain per wave and was latency bound: 30.8
+// us for a 2048-token Mistral chunk, ~3 TB/s of its 90 MB), then every thread walks row pairs
+// (2 floats in, RoPE, fp32 pair / bf16 pair out) with 8 in flight.
+__global__ void __launch_bounds__(256) qkv_post_row_kernel(QkvPostArgs a) {
+  const int t = blockIdx.x;
+  const int hd = a.head_dim, half = hd >> 1;
+  const int qd = a.n_heads * hd, kvd = a.n_kv_heads * hd;
+  const int npair = (qd + 2 * kvd) >> 1;
+  const int pos = a.pos[t];
+  const int slot = a.slot ? a.slot[t] : 0;
+  const size_t kvbase = (((size_t)kv_block(a.block_table, a.max_ctx / KV_BLOCK, slot, pos) * a.n_kv_heads) * KV_BLOCK +
+                         (pos % KV_BLOCK)) * hd;  // + head * KV_BLOCK * hd
+  const float2* src = (const float2*)(a.qkv + (size_t)t * a.ldqkv);
+  const float2* cs = a.rope_cs + (size_t)pos * half;
+  constexpr int UNR = 8;
+  for (int j0 = threadIdx.x; j0 < npair; j0 += 256 * UNR) {
+    float2 v[UNR];
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      const int j = j0 + 256 * u;
+      v[u] = j < npair ? src[j] : make_float2(0.f, 0.f);
+    }
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      const int j = j0 + 256 * u;
+      if (j >= npair) break;
+      const int c = 2 * j;
+      const int part = c < qd ? 0 : (c < qd + kvd ? 1 : 2);
+      const int r = c - (part == 0 ? 0 : (part == 1 ? qd : qd + kvd));
+      const int head = r / hd, lr = r - head * hd;
+      float v0 = v[u].x, v1 = v[u].y;
+      if (part < 2) {
+        const float2 tt = cs[lr >> 1];
+        const float o0 = v0 * tt.x - v1 * tt.y, o1 = v0 * tt.y + v1 * tt.x;
+        v0 = o0;
+        v1 = o1;
+      }
+      if (part == 0) {
+        *(float2*)(a.q_out + (size_t)t * qd + c) = make_float2(v0, v1);
+      } else {
+        bf16_t* cache = part == 1 ? a.k_cache : a.v_cache;
+        *(uint32_t*)(cache + kvbase + (size_t)head * KV_BLOCK * hd + lr) =
+            (uint32_t)f32_to_bf16(v0) | ((uint32_t)f32_to_bf16(v1) << 16);
+      }
+    }
+  }
+}
+
 void launch_qkv_post(const QkvPostArgs& a, hipStream_t st) {
+  if (!a.rope_neox && !a.q_norm && !a.k_norm && !a.bias && a.rope_cs && a.head_dim % 2 == 0) {
+    hipLaunchKernelGGL(qkv_post_row_kernel, dim3(a.T), dim3(256), 0, st, a);
+    return;
+  }
   const int items = a.T * (a.n_heads + 2 * a.n_kv_heads);
   hipLaunchKernelGGL(qkv_post_kernel, dim3((items + 3) / 4), dim3(256), 0, st, a);
 }
