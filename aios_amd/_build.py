@@ -96,8 +96,8 @@ def _deps(src: Path, seen=None) -> set:
     return seen
 
 
-def _compile(src: Path, flags, hipcc) -> Path:
-    obj = BUILD / (src.stem + ".o")
+def _compile(src: Path, flags, hipcc, build_dir: Path = None) -> Path:
+    obj = (build_dir or BUILD) / (src.stem + ".o")
     newest_dep = max(d.stat().st_mtime for d in _deps(src))
     if obj.exists() and obj.stat().st_mtime >= newest_dep:
         return obj
@@ -110,15 +110,19 @@ def _compile(src: Path, flags, hipcc) -> Path:
     return obj
 
 
-def build(verbose: bool = True, jobs: int | None = None) -> Path:
-    BUILD.mkdir(parents=True, exist_ok=True)
+def build(verbose: bool = True, jobs: int | None = None, build_dir: Path | None = None, out: Path | None = None) -> Path:
+    """Compile every HIP / C++ source of the engine for gfx950 (incrementally: an object is rebuilt when
+    its source or a header it includes is newer) and link the extension.  build_dir / out: a clean
+    build elsewhere (tests/test_build.py), leaving the in-tree objects and .so alone."""
+    build_dir = Path(build_dir) if build_dir else BUILD
+    build_dir.mkdir(parents=True, exist_ok=True)
     hipcc = _hipcc()
     flags = _flags()
     srcs = _sources()
     jobs = jobs or min(len(srcs), max(1, (os.cpu_count() or 4)), 16)
     with cf.ThreadPoolExecutor(jobs) as ex:
-        objs = list(ex.map(lambda s: _compile(s, flags, hipcc), srcs))
-    out = target_path()
+        objs = list(ex.map(lambda s: _compile(s, flags, hipcc, build_dir), srcs))
+    out = Path(out) if out else target_path()
     newest = max(o.stat().st_mtime for o in objs)
     if not out.exists() or out.stat().st_mtime < newest:
         tmp = out.with_suffix(".tmp.so")
