@@ -1,10 +1,12 @@
-# refresh the serving / co-resident records: 8 and 16 concurrent JSON-mode Mistral streams with
-# 3k prompts sharing a 2k prefix, and the co-resident TinyLlama + Mistral bench
-set -u
-cd $GRAFT_REPO_ROOT
+#!/bin/bash
+# serving record: 2 / 3 / 4 / 8 concurrent JSON-mode Mistral streams, 3k prompts sharing a 2k prefix
+# (the autonomy loop's pattern); one JSON line each into gpurun_out/serving.jsonl
+set -o pipefail
 mkdir -p gpurun_out
 export HSA_ENABLE_IPC_MODE_LEGACY=0
-run() { local name=$1 t=$2; shift 2; timeout -k 10 $t "$@" > gpurun_out/$name.log 2>&1; local rc=$?; grep -v amdgpu.ids gpurun_out/$name.log | tail -${TAILN:-1} | cut -c1-600; [ $rc -eq 0 ] || { echo "[$name] rc=$rc"; tail -30 gpurun_out/$name.log; exit 1; }; }
-run serve8 400 python tools/bench_serving.py --streams 8 --json gpurun_out/serving8.json
-run serve16 400 python tools/bench_serving.py --streams 16 --json gpurun_out/serving16.json
-run cores 300 python tools/bench_coresident.py
+: > gpurun_out/serving.jsonl
+for n in 2 3 4 8; do
+  timeout -k 10 400 python tools/bench_serving.py --streams $n --json gpurun_out/serving$n.json > gpurun_out/serve$n.log 2>&1 || { tail -30 gpurun_out/serve$n.log; exit 1; }
+  cat gpurun_out/serving$n.json >> gpurun_out/serving.jsonl; echo >> gpurun_out/serving.jsonl
+  python -c "import json;d=json.load(open('gpurun_out/serving$n.json'));print($n, {k:d[k] for k in d if 'itl' in k or 'step' in k or 'ttft' in k or 'tok_s' in k})"
+done
