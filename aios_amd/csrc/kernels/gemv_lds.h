@@ -796,7 +796,7 @@ bool launch_gemv_lds(const GemvArgs& a, hipStream_t st, bool dry = false) {
       const int most = std::max(rup(np0, g0), rup(npairs - np0, G - g0));
       pl = CuPlan{g0, np0, (2 * most + 3) & ~3};
     }
-    // small projections (QKV, O: <= ~60 KB per CU) stay on the row-pair kernel: the engine's fixed
+    // small projections (O: <= ~40 KB per CU) stay on the row-pair kernel: the engine's fixed
     // start-up (first slot lands ~3-4 us after issue, behind the CU's whole prologue burst) and its
     // barrier steps cost more than the row kernel's x-staging stall there (tools/gemv_cu_probe.py:
     // O 6.96 vs 5.60 us, QKV 8.73 vs 8.38; gate_up 17.35 vs 19.39, down 13.8 vs 15.2, lm_head 24.8
@@ -804,10 +804,13 @@ bool launch_gemv_lds(const GemvArgs& a, hipStream_t st, bool dry = false) {
     // batched launches (B >= 2) take the engine for every shape: the row-pair kernels re-read the
     // B x vectors per wave and measured 2-3x slower there (B = 2 QKV 26 us vs 9.6 at B = 1)
     if (mode != 2 && a.kernel_sel != 3 && a.B == 1) {
-      // AIOS_GEMV_LDS_MIN_KB: per-CU weight bytes from which the engine serves a shape (default 96)
+      // AIOS_GEMV_LDS_MIN_KB: per-CU weight bytes from which the engine serves a shape.  Round 5
+      // (same box, tools/ab.sh): 40 instead of 96 -- the Mistral QKV (59 KB per CU) and the
+      // TinyLlama gate/up (50 KB) move to the engine: Mistral 668.2 / 668.1 -> 672.6 / 671.5 tok/s,
+      // TinyLlama 1500.7 / 1500.5 -> 1530.8 / 1535.3 (O, 37 KB, stays on the row kernel)
       static const double min_kb = [] {
         const char* e = std::getenv("AIOS_GEMV_LDS_MIN_KB");
-        return e ? std::atof(e) : 96.0;
+        return e ? std::atof(e) : 40.0;
       }();
       double bytes = 0;
       for (int sg = 0; sg < a.nseg; ++sg)
