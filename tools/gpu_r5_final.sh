@@ -7,3 +7,5 @@ timeout -k 10 1500 python -u -m pytest -x -q --timeout 900 --timeout-method thre
 tail -n 1 gpurun_out/t_final.log
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/smoke.log 2>&1 || { tail -20 gpurun_out/smoke.log; exit 1; }
 tail -n 1 gpurun_out/smoke.log
+timeout -k 10 1100 python bench.py > gpurun_out/bench_final.log 2>&1 || { tail -20 gpurun_out/bench_final.log; exit 1; }
+grep '^{"metric"' gpurun_out/bench_final.log | tail -1 | cut -c1-300
