@@ -26,6 +26,8 @@
 // fragments are plain 16-B row reads at unit 4s + q.  Q6_K is repacked into the same chunk order
 // (qweight.h), its 2 high bits and int8 sub-block scales riding beside the codes.
 #pragma once
+#include <cstdlib>
+
 #include "gemm_common.h"
 
 namespace aios {
@@ -1514,6 +1516,48 @@ __global__ void __launch_bounds__(512) gemm_pf8_kernel(GemmQArgs a) {
   }
 }
 
+// Tail split (round 5).  A 256x256-tile launch of T tiles runs one workgroup per CU (LDS), so it
+// takes ceil(T / CUs) rounds; when the last round is at most half full (R = T mod CUs <= CUs / 2)
+// the other CUs idle through it -- Mistral's gate/up at 2048 rows is 896 tiles = 3.5 rounds of 256
+// that cost 4.  Here the first T - R tiles run as usual and each of the last R runs as TWO 128-row
+// workgroups (the BM = 128 body on its half), dispatched last: the final round puts half-size work
+// on every CU.  K-quant stacks, S = 1 (plans with split-K fill the chip their own way).
+template <int QT0, int QT1, int EPI>
+__global__ void __launch_bounds__(512) gemm_pf8t_kernel(GemmQArgs a, int F) {
+  const int nN = a.N / 256;
+  int L, half = -1;
+  if ((int)blockIdx.x < F) {
+    L = xcd_remap(blockIdx.x, F);
+  } else {
+    const int j = xcd_remap(blockIdx.x - F, gridDim.x - F);
+    L = F + (j >> 1);
+    half = j & 1;
+  }
+  const int tn = L % nN, tm = L / nN;
+  const int m0 = tm * 256 + (half > 0 ? 128 : 0), n0 = tn * 256;
+  int seg = 0;
+  if (a.nseg > 1 && n0 >= a.seg_n0[1]) seg = 1;
+  if (a.nseg > 2 && n0 >= a.seg_n0[2]) seg = 2;
+  const int kt1 = 4 * (a.K / 256);
+  if constexpr (QT0 != QT1) {
+    if (seg == a.nseg - 1) {
+      if (half < 0) pf8c_body<QT1, 256, EPI>(a, m0, n0, seg, 0, kt1, 1);
+      else pf8c_body<QT1, 128, EPI>(a, m0, n0, seg, 0, kt1, 1);
+      return;
+    }
+  }
+  if (half < 0) pf8c_body<QT0, 256, EPI>(a, m0, n0, seg, 0, kt1, 1);
+  else pf8c_body<QT0, 128, EPI>(a, m0, n0, seg, 0, kt1, 1);
+}
+
+// full tiles before the tail of a 256x256 launch, or -1 (no tail split for this shape / plan)
+inline int pf8_tail_full(const GemmQArgs& a, int S) {
+  const char* e = std::getenv("AIOS_GEMM_PF_TAIL");  // (read per call: tests compare both)
+  if ((e && std::atoi(e) == 0) || S != 1 || a.epi == GEPI_QKV) return -1;
+  const int T = (a.N / 256) * ((a.M + 255) / 256), C = device_cu_count(), R = T % C;
+  return (T > C && R > 0 && 2 * R <= C) ? T - R : -1;
+}
+
 template <int QT0, int QT1, int BM>
 constexpr int pf8_lds_bytes() {
   if constexpr (QT0 == QT_BF16) {
@@ -1529,6 +1573,21 @@ template <int QT0, int QT1, int BM>
 void pf8_launch(const GemmQArgs& a, int S, hipStream_t st) {
   constexpr int lds = pf8_lds_bytes<QT0, QT1, BM>();
   static_assert(lds <= 160 * 1024, "LDS");
+  if constexpr (BM == 256 && QT0 != QT_BF16) {
+    const int F = pf8_tail_full(a, S);
+    if (F >= 0) {
+      constexpr int l128 = pf8_lds_bytes<QT0, QT1, 128>();
+      constexpr int ldst = lds > l128 ? lds : l128;
+      const int T = (a.N / 256) * ((a.M + 255) / 256);
+      const dim3 grid(F + 2 * (T - F)), block(512);
+      switch (a.epi) {
+        case GEPI_STORE: hipLaunchKernelGGL((gemm_pf8t_kernel<QT0, QT1, GEPI_STORE>), grid, block, ldst, st, a, F); break;
+        case GEPI_ACCUM: hipLaunchKernelGGL((gemm_pf8t_kernel<QT0, QT1, GEPI_ACCUM>), grid, block, ldst, st, a, F); break;
+        default: hipLaunchKernelGGL((gemm_pf8t_kernel<QT0, QT1, GEPI_SWIGLU_BF16>), grid, block, ldst, st, a, F); break;
+      }
+      return;
+    }
+  }
   const dim3 grid((a.N / 256) * ((a.M + BM - 1) / BM), S), block(512);
   switch (a.epi) {
     case GEPI_STORE: hipLaunchKernelGGL((gemm_pf8_kernel<QT0, QT1, BM, GEPI_STORE>), grid, block, lds, st, a); break;

@@ -899,6 +899,40 @@ def test_gemm_pf_split_k(E, monkeypatch, fmt, M, S, epi):
     assert rel < 6e-3, rel
 
 
+@pytest.mark.parametrize("epi", ["store", "accum", "swiglu"])
+def test_gemm_pf_tail_split(E, monkeypatch, epi):
+    """256x256 plan whose last round is at most half full (M = 1280, N = 16384: 320 tiles on 256 CUs):
+    the last 64 tiles run as two 128-row workgroups each (gemm_pf8t_kernel).  Against the unquantized
+    product and bit-identical to the plain launch (same per-element accumulation order)."""
+    monkeypatch.setenv("AIOS_GEMM_PF_TILE", "256x256")
+    M, N, K = 1280, 16384, 512
+    m, W = qmat(E, GGMLType.Q4_K, N, K, seed=131, std=0.02)
+    assert E.gemm_pf_plan([m], M, E.GEPI_ACCUM, 1)[:2] == (256, 256)
+    x = torch.randn(M, K, generator=torch.Generator().manual_seed(9))
+    A = x.to(torch.bfloat16).cuda()
+    outs = []
+    for tail in ("1", "0"):
+        monkeypatch.setenv("AIOS_GEMM_PF_TAIL", tail)
+        if epi == "swiglu":
+            C = torch.zeros(M, N // 2, dtype=torch.bfloat16, device="cuda")
+            E.gemm_q(A.data_ptr(), K, [m], M, 0, C.data_ptr(), N // 2, E.GEPI_SWIGLU_BF16, stream(), 1)
+        else:
+            C = torch.full((M, N), 0.5, device="cuda")
+            E.gemm_q(A.data_ptr(), K, [m], M, C.data_ptr(), 0, N, E.GEPI_STORE if epi == "store" else E.GEPI_ACCUM,
+                     stream(), 1)
+        torch.cuda.synchronize()
+        outs.append(C.float().cpu())
+    assert torch.equal(outs[0], outs[1])
+    y = x.double() @ W.double().T
+    if epi == "swiglu":
+        ref = torch.nn.functional.silu(y[:, 0::2]) * y[:, 1::2]
+        assert torch.allclose(outs[0].double(), ref, atol=2e-2, rtol=2e-2), (outs[0].double() - ref).abs().max()
+    else:
+        ref = y + (0.0 if epi == "store" else 0.5)
+        rel = float((outs[0].double() - ref).norm() / ref.norm())
+        assert rel < 6e-3, rel
+
+
 @pytest.mark.parametrize("tile", ["256x256", "128x256", "64x128"])
 @pytest.mark.parametrize("M", [40, 300])
 def test_gemm_pf_swiglu(E, monkeypatch, tile, M):
