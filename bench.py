@@ -408,13 +408,14 @@ def main():
             else:
                 out["goal_plan_p50_ms"] = goal_plan["value"]
                 out["goal_plan"] = {k: goal_plan[k] for k in ("metric", "p90_ms", "goals", "tasks_per_goal",
-                                                              "reactive_p50_ms", "plan_tokens_cap", "model",
+                                                              "reactive_p50_ms", "plan_tokens_cap", "plan_tokens_p50",
+                                                              "plan_tokens_min_max", "ms_per_token", "model",
                                                               "baseline_ms")}
                 b = goal_plan.get("burst", {})
                 out["goal_plan_burst"] = {"metric": "goal->plan latency, 3 tactical goals submitted at once",
                                           "p50_ms": b.get("p50_ms"), "p90_ms": b.get("p90_ms"),
                                           "goals": b.get("concurrent_goals"), "plan_tokens_cap": b.get("plan_tokens_cap"),
-                                          "wall_s": b.get("wall_s")}
+                                          "plan_tokens_total": b.get("plan_tokens_total"), "wall_s": b.get("wall_s")}
         if collectives is not None:
             out["collectives"] = collectives
         if grpc_res is not None:

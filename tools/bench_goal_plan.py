@@ -9,10 +9,13 @@ a tactical/strategic description; latency = the SubmitGoal RPC round trip, which
 classification, the decomposition LLM call (gateway attempt -> runtime JSON-mode generation),
 parsing, and persisting the tasks (exactly the reference's SubmitGoal path, main.rs:142-175).
 
-Random weights never stop on their own, so the decomposition output length is fixed by the token
-cap: --plan-tokens (default 160 ~ a 2-5 step JSON plan; the reference's cap is 1024, which a real
-model does not reach).  Reported alongside: the same measurement for reactive/operational goals
-(planned heuristically, no LLM).
+The decomposition output length is capped by --plan-tokens (default 160 ~ a 2-5 step JSON plan; the
+reference's cap is 1024, which a real model does not reach).  Random weights mostly run to the cap,
+but the JSON-mode grammar lets them close the object early now and then (which goals do shifts with
+the kernels' rounding), so the tokens each plan generated are counted (the runtime scheduler's
+token counter around each goal) and reported with the latencies: plan_tokens_p50, and ms_per_token
+= latency / tokens over the goals.  Reported alongside: the same measurement for reactive /
+operational goals (planned heuristically, no LLM).
 """
 import argparse
 import asyncio
@@ -76,12 +79,16 @@ async def main_async(args):
                                                              OrchestratorService(st)}).start()
     orch = Stub(channel(f"127.0.0.1:{servers['orchestrator'].port}"), "aios.orchestrator.Orchestrator", timeout=120)
 
+    sched_stats = m.scheduler.stats
+
     async def submit(desc):
+        n0 = sched_stats["tokens"]
         t = time.perf_counter()
         gid = (await orch.SubmitGoal(pb.orchestrator.SubmitGoalRequest(description=desc, priority=5))).id
         ms = (time.perf_counter() - t) * 1000
+        ntok = sched_stats["tokens"] - n0  # decoded tokens of this goal's plan (0: heuristic plan)
         s = await orch.GetGoalStatus(pb.common.GoalId(id=gid))
-        return ms, len(s.tasks), s.tasks[0].intelligence_level if s.tasks else ""
+        return ms, len(s.tasks), s.tasks[0].intelligence_level if s.tasks else "", ntok
 
     for d in TACTICAL[:args.warmup]:
         await submit(d)
@@ -92,9 +99,11 @@ async def main_async(args):
     import aios_amd.orchestrator.state as orch_state
 
     orch_state.PLAN_MAX_TOKENS = getattr(args, "burst_plan_tokens", 0) or args.plan_tokens
+    nb0 = sched_stats["tokens"]
     t = time.perf_counter()
     burst = await asyncio.gather(*(submit(TACTICAL[i % len(TACTICAL)] + f" burst {i}") for i in range(args.burst)))
     burst_s = time.perf_counter() - t
+    burst_tokens = sched_stats["tokens"] - nb0  # (the goals decode together: one total)
     n_burst = len(burst)
     # every measured goal must have gone through the LLM decomposition (tactical / strategic
     # classification) -- a goal the classifier routes to the heuristic planner is not a sample
@@ -104,16 +113,20 @@ async def main_async(args):
     rlat = sorted(x[0] for x in rea)
     blat = sorted(x[0] for x in burst) or [0.0]
     q = lambda v, p: v[min(len(v) - 1, int(p * len(v)))]
+    toks = [x[3] for x in tac]
     out = {"metric": "p50 agent goal->plan latency (tactical goals, LLM decomposition)",
            "value": round(statistics.median(lat), 1), "unit": "ms", "higher_is_better": False,
            "p90_ms": round(q(lat, 0.9), 1), "mean_ms": round(statistics.mean(lat), 1), "goals": len(lat),
+           "plan_tokens_p50": statistics.median(toks), "plan_tokens_min_max": [min(toks), max(toks)],
+           "ms_per_token": round(sum(x[0] for x in tac) / max(1, sum(toks)), 3),
            "tasks_per_goal": round(statistics.mean(x[1] for x in tac), 2),
            "reactive_p50_ms": round(statistics.median(rlat), 2),
            "burst": {"concurrent_goals": n_burst, "wall_s": round(burst_s, 3), "p50_ms": round(statistics.median(blat), 1),
-                     "p90_ms": round(q(blat, 0.9), 1), "plan_tokens_cap": orch_state.PLAN_MAX_TOKENS},
+                     "p90_ms": round(q(blat, 0.9), 1), "plan_tokens_cap": orch_state.PLAN_MAX_TOKENS,
+                     "plan_tokens_total": burst_tokens},
            "plan_tokens_cap": args.plan_tokens, "model": f"{args.model} Q4_K_M (random-init, synthetic vocab)",
            "baseline_ms": "200-500 (tactical tier, docs/VISION.md:45)", "model_load_s": round(load_s, 1),
-           "data": "synthetic goals; decomposition output length fixed by plan_tokens_cap (random weights)"}
+           "data": "synthetic goals; decomposition output length capped by plan_tokens_cap (random weights)"}
     for s in servers.values():
         await s.stop(0)
     await close_all()

@@ -5,9 +5,9 @@ AIRuntime.StreamInfer and AIRuntime.Infer with intelligence_level="operational" 
 ModelManager like the reference's runtime, grpc_service.rs:33-177), next to the bare engine's decode
 rate that bench.py measures on the same weights.
 
-Random weights never emit EOS, so every streamed request generates exactly --tokens tokens (the cap);
-stream rate = (chunks - 1) / (last chunk - first chunk) (one chunk per decoded token), TTFT = request
--> first chunk.  (The unary Infer is JSON-mode -- grammar-constrained like the reference's -- and with
+Random weights mostly run to the --tokens cap, but may sample EOS early; stream rate = (chunks - 1) /
+(last chunk - first chunk) (one chunk per decoded token) over however many tokens the request
+produced (stream_chunks), TTFT = request -> first chunk.  (The unary Infer is JSON-mode -- grammar-constrained like the reference's -- and with
 random weights closes its object after a few tokens, so it is only the routing check here.)
 
 python tools/bench_grpc.py [--tokens 256] [--reps 3] [--recipe BF16]"""
@@ -43,7 +43,6 @@ async def main_async(args):
     r = await stub.Infer(req)  # warm-up (graph capture, first prefill)
     assert r.model_used.startswith("tinyllama"), r.model_used
     stream, ttft, chunks = [], [], []
-    n_tok = args.tokens  # (random weights: every streamed request runs to the cap)
     for _ in range(args.reps):
         t = time.perf_counter()
         first = last = None
@@ -62,7 +61,7 @@ async def main_async(args):
     out = {"metric": "operational tier tokens/s over gRPC (TinyLlama-1.1B " + args.recipe + ", loopback)",
            "service_stream_tok_s": round(statistics.median(stream), 1),
            "stream_ttft_ms": round(statistics.median(ttft), 2),
-           "tokens_per_request": n_tok, "stream_chunks": chunks[-1], "reps": args.reps,
+           "max_tokens": args.tokens, "stream_chunks": chunks, "reps": args.reps,
            "intelligence_level": "operational", "model_used": r.model_used, "model_load_s": round(load_s, 1),
            "data": f"synthetic (random-init {args.recipe} weights of the TinyLlama-1.1B architecture)"}
     await server.stop(0)
