@@ -25,9 +25,17 @@ import logging
 import os
 import threading
 import time
+import zlib
 from typing import Dict, List, Optional
 
 from .faults import FaultSpec, FaultyEngine
+
+
+def _synth_seed(name: str) -> int:
+    """Weight seed of a synthetic (random-init) model: stable across processes (str hash() is
+    salted per process, which made every bench run draw different weights -- and, with JSON-mode
+    plans that random weights close at arbitrary points, different plan lengths)."""
+    return zlib.crc32(name.encode()) % 1000
 
 log = logging.getLogger("aios.runtime.models")
 
@@ -200,7 +208,7 @@ class ModelManager:
                     context_length = context_for_size(os.path.getsize(base)) if os.path.exists(base) else 8192
             ctx = context_length
             eng, cfg = launch_tp(base, tp, self.tp_devices(), ctx, self.max_slots, self.max_batch,
-                                 seed=abs(hash(m.name)) % 1000, act_q8=act_q8)
+                                 seed=_synth_seed(m.name), act_q8=act_q8)
             if base.startswith("synthetic:"):
                 toks, scores, types = synthetic_vocab(cfg.vocab_size)
                 tok = SpmTokenizer(toks, scores, types, cfg.bos_id, cfg.eos_id)
@@ -215,7 +223,7 @@ class ModelManager:
             cfg = get_preset(parts[1])
             recipe = parts[2] if len(parts) > 2 else "Q4_K_M"
             ctx = context_length or tier_context(cfg)
-            eng = random_engine(cfg, recipe, seed=abs(hash(m.group or m.name)) % 1000, max_ctx=ctx,
+            eng = random_engine(cfg, recipe, seed=_synth_seed(m.group or m.name), max_ctx=ctx,
                                 max_slots=self.max_slots, max_batch=self.max_batch, device=device, act_q8=act_q8)
             toks, scores, types = synthetic_vocab(cfg.vocab_size)
             tok = SpmTokenizer(toks, scores, types, cfg.bos_id, cfg.eos_id)
@@ -361,7 +369,7 @@ class ModelManager:
 
             path = os.path.join(tempfile.gettempdir(), f"aios-cpu-{parts[1]}-{recipe}.gguf")
             if not os.path.exists(path):
-                write_synthetic_gguf(path, cfg, recipe, seed=abs(hash(m.name)) % 1000)
+                write_synthetic_gguf(path, cfg, recipe, seed=_synth_seed(m.name))
             ctx = context_length or min(cfg.max_ctx, 2048)
             eng = CpuEngine.from_gguf(path, max_ctx=ctx, max_slots=slots, max_batch=min(self.max_batch, slots))
             toks, scores, types = synthetic_vocab(cfg.vocab_size)
