@@ -1550,11 +1550,11 @@ __global__ void __launch_bounds__(512) gemm_pf8t_kernel(GemmQArgs a, int F) {
   else pf8c_body<QT0, 128, EPI>(a, m0, n0, seg, 0, kt1, 1);
 }
 
-// full tiles before the tail of a 256x256 launch, or -1 (no tail split for this shape / plan)
-inline int pf8_tail_full(const GemmQArgs& a, int S) {
+// full tiles before the tail of a 256 x BN launch, or -1 (no tail split for this shape / plan)
+inline int pf_tail_full(const GemmQArgs& a, int BN, int S) {
   const char* e = std::getenv("AIOS_GEMM_PF_TAIL");  // (read per call: tests compare both)
   if ((e && std::atoi(e) == 0) || S != 1 || a.epi == GEPI_QKV) return -1;
-  const int T = (a.N / 256) * ((a.M + 255) / 256), C = device_cu_count(), R = T % C;
+  const int T = (a.N / BN) * ((a.M + 255) / 256), C = device_cu_count(), R = T % C;
   return (T > C && R > 0 && 2 * R <= C) ? T - R : -1;
 }
 
@@ -1574,7 +1574,7 @@ void pf8_launch(const GemmQArgs& a, int S, hipStream_t st) {
   constexpr int lds = pf8_lds_bytes<QT0, QT1, BM>();
   static_assert(lds <= 160 * 1024, "LDS");
   if constexpr (BM == 256 && QT0 != QT_BF16) {
-    const int F = pf8_tail_full(a, S);
+    const int F = pf_tail_full(a, 256, S);
     if (F >= 0) {
       constexpr int l128 = pf8_lds_bytes<QT0, QT1, 128>();
       constexpr int ldst = lds > l128 ? lds : l128;
@@ -1618,6 +1618,36 @@ __global__ void __launch_bounds__(256) gemm_pf4_kernel(GemmQArgs a) {
   pf4_body<QT0, BM, WC, EPI, PROBE>(a, m0, n0, seg, kt0, kt1, S);
 }
 
+// pf4's tail split (256 x 4 WC tiles): as gemm_pf8t_kernel, the last R tiles as two 128-row halves
+template <int QT0, int QT1, int WC, int EPI>
+__global__ void __launch_bounds__(256) gemm_pf4t_kernel(GemmQArgs a, int F) {
+  constexpr int BN = 4 * WC;
+  const int nN = a.N / BN;
+  int L, half = -1;
+  if ((int)blockIdx.x < F) {
+    L = xcd_remap(blockIdx.x, F);
+  } else {
+    const int j = xcd_remap(blockIdx.x - F, gridDim.x - F);
+    L = F + (j >> 1);
+    half = j & 1;
+  }
+  const int tn = L % nN, tm = L / nN;
+  const int m0 = tm * 256 + (half > 0 ? 128 : 0), n0 = tn * BN;
+  int seg = 0;
+  if (a.nseg > 1 && n0 >= a.seg_n0[1]) seg = 1;
+  if (a.nseg > 2 && n0 >= a.seg_n0[2]) seg = 2;
+  const int kt1 = a.K / 64;
+  if constexpr (QT0 != QT1) {
+    if (seg == a.nseg - 1) {
+      if (half < 0) pf4_body<QT1, 256, WC, EPI>(a, m0, n0, seg, 0, kt1, 1);
+      else pf4_body<QT1, 128, WC, EPI>(a, m0, n0, seg, 0, kt1, 1);
+      return;
+    }
+  }
+  if (half < 0) pf4_body<QT0, 256, WC, EPI>(a, m0, n0, seg, 0, kt1, 1);
+  else pf4_body<QT0, 128, WC, EPI>(a, m0, n0, seg, 0, kt1, 1);
+}
+
 template <int QT0, int QT1, int BM, int WC>
 constexpr int pf4_lds_bytes() {
   using L0 = Pf4Layout<QT0, BM, WC>;
@@ -1629,6 +1659,21 @@ template <int QT0, int QT1, int BM, int WC>
 void pf4_launch(const GemmQArgs& a, int S, hipStream_t st) {
   constexpr int lds = pf4_lds_bytes<QT0, QT1, BM, WC>();
   static_assert(lds <= 160 * 1024, "LDS");
+  if constexpr (BM == 256) {
+    const int F = pf_tail_full(a, 4 * WC, S);
+    if (F >= 0) {
+      constexpr int l128 = pf4_lds_bytes<QT0, QT1, 128, WC>();
+      constexpr int ldst = lds > l128 ? lds : l128;
+      const int T = (a.N / (4 * WC)) * ((a.M + 255) / 256);
+      const dim3 grid(F + 2 * (T - F)), block(256);
+      switch (a.epi) {
+        case GEPI_STORE: hipLaunchKernelGGL((gemm_pf4t_kernel<QT0, QT1, WC, GEPI_STORE>), grid, block, ldst, st, a, F); break;
+        case GEPI_ACCUM: hipLaunchKernelGGL((gemm_pf4t_kernel<QT0, QT1, WC, GEPI_ACCUM>), grid, block, ldst, st, a, F); break;
+        default: hipLaunchKernelGGL((gemm_pf4t_kernel<QT0, QT1, WC, GEPI_SWIGLU_BF16>), grid, block, ldst, st, a, F); break;
+      }
+      return;
+    }
+  }
   const dim3 grid((a.N / (4 * WC)) * ((a.M + BM - 1) / BM), S), block(256);
   switch (a.epi) {
     case GEPI_STORE: hipLaunchKernelGGL((gemm_pf4_kernel<QT0, QT1, BM, WC, GEPI_STORE>), grid, block, lds, st, a); break;

@@ -43,7 +43,7 @@ static double pf_model(const GemmQArgs& a, int bm, int bn, int S, bool bf) {
   const double t_wg = std::max(t_mfma, t_mem) + 2.5e-6;
   double t = std::ceil(tiles * S / cus) * t_wg;
   const double R = std::fmod(tiles, cus);
-  if (bm == 256 && S == 1 && !bf && tiles > cus && R > 0 && 2 * R <= cus)  // tail split (pf8t)
+  if (bm == 256 && S == 1 && (bn == 128 || !bf) && tiles > cus && R > 0 && 2 * R <= cus)  // tail split
     t = (std::floor(tiles / cus) + 0.6) * t_wg;
   if (S > 1) t += (double)a.M * a.N * 4 * S / 1.2e12 + (a.epi == GEPI_STORE ? (double)a.M * a.N * 4 / 4e12 : 0.0);
   return t;

@@ -903,14 +903,15 @@ def test_gemm_pf_split_k(E, monkeypatch, fmt, M, S, epi):
 
 
 @pytest.mark.parametrize("epi", ["store", "accum", "swiglu"])
-def test_gemm_pf_tail_split(E, monkeypatch, epi):
-    """256x256 plan whose last round is at most half full (M = 1280, N = 16384: 320 tiles on 256 CUs):
-    the last 64 tiles run as two 128-row workgroups each (gemm_pf8t_kernel).  Against the unquantized
-    product and bit-identical to the plain launch (same per-element accumulation order)."""
-    monkeypatch.setenv("AIOS_GEMM_PF_TILE", "256x256")
-    M, N, K = 1280, 16384, 512
+@pytest.mark.parametrize("tile,N", [("256x256", 16384), ("256x128", 8192)])
+def test_gemm_pf_tail_split(E, monkeypatch, epi, tile, N):
+    """256-row plan whose last round is at most half full (M = 1280: 320 tiles on 256 CUs): the last
+    64 tiles run as two 128-row workgroups each (gemm_pf8t_kernel / gemm_pf4t_kernel).  Against the
+    unquantized product and bit-identical to the plain launch (same per-element accumulation order)."""
+    monkeypatch.setenv("AIOS_GEMM_PF_TILE", tile)
+    M, K = 1280, 512
     m, W = qmat(E, GGMLType.Q4_K, N, K, seed=131, std=0.02)
-    assert E.gemm_pf_plan([m], M, E.GEPI_ACCUM, 1)[:2] == (256, 256)
+    assert E.gemm_pf_plan([m], M, E.GEPI_ACCUM, 1)[:2] == tuple(int(v) for v in tile.split("x"))
     x = torch.randn(M, K, generator=torch.Generator().manual_seed(9))
     A = x.to(torch.bfloat16).cuda()
     outs = []
