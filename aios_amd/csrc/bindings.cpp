@@ -577,6 +577,15 @@ PYBIND11_MODULE(_engine, m) {
              }
              return py::bytes((const char*)m->data(), m->size());
            })
+      .def("mask_open",
+           [](JsonGrammar& g, const JsonState& s) {
+             const std::vector<uint8_t>* m;
+             {
+               py::gil_scoped_release nogil;
+               m = &g.mask_open(s);
+             }
+             return py::bytes((const char*)m->data(), m->size());
+           })
       .def_property_readonly("vocab_size", &JsonGrammar::vocab_size)
       .def_property_readonly("cache_size", &JsonGrammar::cache_size);
   m.def("bench_stream_read_part", &aios::bench_stream_read_part, py::arg("bytes"), py::arg("nbuf"), py::arg("mode"),

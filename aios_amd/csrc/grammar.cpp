@@ -249,15 +249,17 @@ bool JsonGrammar::accept_token(JsonState& s, int token) const {
   return accept_bytes(s, tokens_[token]);
 }
 
-void JsonGrammar::dfs(int node, JsonState s, std::vector<uint8_t>& out) const {
+void JsonGrammar::dfs(int node, JsonState s, std::vector<uint8_t>& out, bool open) const {
   const Node& nd = nodes_[node];
-  for (int t : nd.toks) out[t >> 3] |= (uint8_t)(1u << (t & 7));
+  // open: a token that completes the top-level value is not allowed (min_tokens not reached yet)
+  if (!(open && s.mode == M_DONE))
+    for (int t : nd.toks) out[t >> 3] |= (uint8_t)(1u << (t & 7));
   for (int e = nd.child_begin; e < nd.child_begin + nd.child_count; ++e) {
     const uint8_t c = edges_[e].first;
     JsonState t = s;
     if (require_object_ && t.mode == M_TOP && !is_ws(c) && c != '{') continue;
     if (!step(t, c, max_ws_)) continue;
-    dfs(edges_[e].second, t, out);
+    dfs(edges_[e].second, t, out, open);
   }
 }
 
@@ -272,6 +274,19 @@ const std::vector<uint8_t>& JsonGrammar::mask(const JsonState& s) {
     dfs(0, s, m);
   }
   return cache_.emplace(s, std::move(m)).first->second;
+}
+
+const std::vector<uint8_t>& JsonGrammar::mask_open(const JsonState& s) {
+  if (complete(s)) return mask(s);
+  auto it = cache_open_.find(s);
+  if (it != cache_open_.end()) return it->second;
+  if (cache_open_.size() > 8192) cache_open_.clear();
+  std::vector<uint8_t> m((tokens_.size() + 7) / 8, 0);
+  dfs(0, s, m, true);
+  bool any = false;
+  for (uint8_t b : m) any |= b != 0;
+  if (!any) return mask(s);  // only closing tokens are left: the value may complete
+  return cache_open_.emplace(s, std::move(m)).first->second;
 }
 
 }  // namespace aios

@@ -49,6 +49,9 @@ class JsonGrammar {
   bool complete(const JsonState& s) const;                // a full top-level value has been produced
   // allowed-token bitmask (ceil(V/8) bytes, bit i of byte t/8 set = token t allowed)
   const std::vector<uint8_t>& mask(const JsonState& s);
+  // the same without the tokens that complete the top-level value (falls back to mask() when
+  // nothing else is allowed): a request's min_tokens keeps the object open until it is reached
+  const std::vector<uint8_t>& mask_open(const JsonState& s);
   int vocab_size() const { return (int)tokens_.size(); }
   size_t cache_size() const { return cache_.size(); }
 
@@ -59,7 +62,7 @@ class JsonGrammar {
     std::vector<int> toks;
   };
   void build_trie();
-  void dfs(int node, JsonState s, std::vector<uint8_t>& out) const;
+  void dfs(int node, JsonState s, std::vector<uint8_t>& out, bool open = false) const;
 
   std::vector<std::string> tokens_;
   int eos_;
@@ -68,6 +71,7 @@ class JsonGrammar {
   std::vector<Node> nodes_;
   std::vector<std::pair<uint8_t, int>> edges_;  // (byte, child node)
   std::unordered_map<JsonState, std::vector<uint8_t>, JsonStateHash> cache_;
+  std::unordered_map<JsonState, std::vector<uint8_t>, JsonStateHash> cache_open_;
 };
 
 }  // namespace aios

@@ -52,6 +52,9 @@ class GenRequest:
     top_k: int = 40
     top_p: float = 0.95
     json_mode: bool = False
+    # JSON mode: the grammar may not close the object before this many tokens (bench runs pin the
+    # plan length with it: random weights close a JSON object at arbitrary points)
+    min_tokens: int = 0
     seed: int = 0
     stop_ids: Optional[List[int]] = None
     on_delta: Optional[Callable[[str], None]] = None
@@ -238,6 +241,7 @@ class Scheduler:
         if len(ids) >= self.max_ctx:
             raise ValueError(f"prompt of {len(ids)} tokens exceeds the context window ({self.max_ctx})")
         r.max_tokens = max(1, min(r.max_tokens, self.max_ctx - len(ids)))
+        r.min_tokens = min(r.min_tokens, r.max_tokens)
         slot, common = self._pick_slot(ids)
         self.free_slots.remove(slot)
         seq = _Seq(r, slot)
@@ -279,7 +283,7 @@ class Scheduler:
         mask = None
         if r.json_mode and self.grammar is not None:
             seq.grammar_state = self.grammar.initial()
-            mask = self.grammar.mask(seq.grammar_state)
+            mask = self._mask(seq)
         topk = int(r.top_k) if r.temperature > 0 else 0
         topp = float(r.top_p) if 0.0 < r.top_p < 1.0 else 1.0
         if hasattr(self.engine, "sample_first"):
@@ -356,6 +360,11 @@ class Scheduler:
                 "avg_batch": st["batch_sum"] / st["steps"] if st["steps"] else 0.0,
                 "prefix_hit_tokens": st["cached_tokens"], "errors": st["errors"]}
 
+    def _mask(self, seq: _Seq) -> bytes:
+        if len(seq.out) + 1 < seq.req.min_tokens:  # the next token may not complete the object
+            return self.grammar.mask_open(seq.grammar_state)
+        return self.grammar.mask(seq.grammar_state)
+
     def _step(self):
         B = len(self.active)
         slots = [s.slot for s in self.active]
@@ -369,8 +378,7 @@ class Scheduler:
         if any(s.grammar_state is not None for s in self.active):
             if self._full_mask is None:
                 self._full_mask = host_sampler.all_allowed(self.vocab)
-            mask = b"".join(self.grammar.mask(s.grammar_state) if s.grammar_state is not None else self._full_mask
-                            for s in self.active)
+            mask = b"".join(self._mask(s) if s.grammar_state is not None else self._full_mask for s in self.active)
         topp = [float(s.req.top_p) if 0.0 < s.req.top_p < 1.0 else 1.0 for s in self.active]
         t1 = time.perf_counter()
         out = self.engine.decode(slots, toks, pos, temps, topk, 0, mask, topp, seeds)

@@ -15,6 +15,7 @@ from __future__ import annotations
 import asyncio
 import json
 import logging
+import os
 import time
 from typing import Dict, Optional
 
@@ -38,6 +39,16 @@ def _gen_params(temperature: float, max_tokens: int):
     return float(temperature), int(max_tokens)
 
 
+def _json_min_tokens(max_tokens: int) -> int:
+    """AIOS_JSON_MIN_TOKENS (benchmarks only): JSON-mode generations run to this many tokens before
+    the grammar lets the object close ("max": to max_tokens) -- a fixed plan length, since
+    random-init weights close a JSON object at arbitrary points."""
+    v = os.environ.get("AIOS_JSON_MIN_TOKENS", "").strip()
+    if not v:
+        return 0
+    return max_tokens if v == "max" else min(max_tokens, int(v))
+
+
 async def generate(m, messages, max_tokens: int, temperature: float, json_mode: bool, on_delta=None,
                    timeout: float = 120.0, seed: int = 0) -> GenResult:
     loop = asyncio.get_running_loop()
@@ -53,7 +64,7 @@ async def generate(m, messages, max_tokens: int, temperature: float, json_mode: 
         def delta_cb(d):
             loop.call_soon_threadsafe(on_delta, d)
     req = GenRequest(prompt_ids=ids, max_tokens=max_tokens, temperature=temperature, json_mode=json_mode,
-                     seed=seed, on_delta=delta_cb, on_done=done, deadline=time.time() + timeout)
+                     min_tokens=_json_min_tokens(max_tokens) if json_mode else 0, seed=seed, on_delta=delta_cb, on_done=done, deadline=time.time() + timeout)
     m.scheduler.submit(req)
     try:
         return await asyncio.wait_for(fut, timeout + 5)

@@ -117,7 +117,7 @@ def measure(preset: str, recipe: str, batch: int, prompt: int, steps: int, warmu
     return dt, info
 
 
-def measure_goal_plan(goals: int = 16, timeout_s: float = 60.0):
+def measure_goal_plan(goals: int = 16, timeout_s: float = 90.0):
     """BASELINE.json's agent metric: p50 goal -> plan latency of tactical goals through the real
     planner (classification, LLM decomposition over gRPC, task persistence) on an in-process runtime
     serving the synthetic Mistral-7B tier (tools/bench_goal_plan.py; reference path
@@ -128,8 +128,10 @@ def measure_goal_plan(goals: int = 16, timeout_s: float = 60.0):
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "tools"))
     from bench_goal_plan import main_async
 
-    # + goal_plan_burst: 3 tactical goals submitted at once with a 300-token plan cap
-    ns = _ap.Namespace(model="mistral-7b", goals=goals, warmup=2, burst=3, plan_tokens=160, burst_plan_tokens=300)
+    # every plan is exactly 300 tokens (the top of the reference's typical plan, task_planner.rs:168);
+    # + goal_plan_burst: 3 tactical goals submitted at once, 300 tokens each
+    ns = _ap.Namespace(model="mistral-7b", goals=goals, warmup=2, burst=3, plan_tokens=300, burst_plan_tokens=300,
+                       fixed_length=True)
     return asyncio.run(asyncio.wait_for(main_async(ns), timeout_s))
 
 

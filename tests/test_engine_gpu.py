@@ -189,8 +189,8 @@ def test_short_prompt_prefill_matches_reference(model_files, monkeypatch, T, q8)
 def test_short_chunk_prefill_fusions_match_reference(model_files, monkeypatch, recipe, fuse):
     """chunks of <= 64 rows take the decode step's fusions (RoPE + KV write in the QKV GEMM epilogue,
     split RMSNorm through the residual GEMMs, AIOS_PREFILL_SHORT_FUSE): a 30-token prompt in one chunk
-    and its continuation at start_pos 30 (34 more rows: hipBLASLt's 33..128-row window where the bf16
-    copy exists), then the whole 64-token prompt, against the fp32 reference, fused and not"""
+    and its continuation at start_pos 30 (34 more rows: the hand-written prefill GEMM's
+    smallest M window, 33..64 rows), then the whole 64-token prompt, against the fp32 reference, fused and not"""
     monkeypatch.setenv("AIOS_PREFILL_GEMM", "1")
     monkeypatch.setenv("AIOS_PREFILL_SHORT_FUSE", fuse)
     path = model_files[recipe]

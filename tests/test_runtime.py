@@ -94,6 +94,24 @@ def test_json_grammar_rejects_structural_errors(tok):
         assert g.accept_bytes(st, s) and g.complete(st), s
 
 
+@needs_native
+def test_json_grammar_open_mask_keeps_object_open(tok):
+    g = E.JsonGrammar(tok.all_token_bytes(), tok.eos_id)
+    st = g.initial()
+    for t in tok.encode('{"a": 1', add_bos=False):
+        assert g.accept_token(st, t)
+    full = mask_to_bool(g.mask(st), tok.vocab_size)
+    opn = mask_to_bool(g.mask_open(st), tok.vocab_size)
+    assert not (opn & ~full).any()                   # a subset of the grammar's mask
+    closing = [t for t in np.flatnonzero(full) if g.accept_token(s2 := st.copy(), int(t)) and g.complete(s2)]
+    assert closing                                   # '}' (and '}'-ending tokens) close the object here
+    assert not opn[closing].any() and opn.sum() > 0  # ... but not under the open mask
+    # nothing but a closing token left: the open mask falls back to the full one
+    done = g.initial()
+    assert g.accept_bytes(done, b'{}') and g.complete(done)
+    assert g.mask_open(done) == g.mask(done)
+
+
 # ---------------------------------------------------------------------------- fake engine
 class FakeEngine:
     """Deterministic stand-in for the native Engine: the next token is a function of the last one,
@@ -177,6 +195,29 @@ def test_scheduler_batches_streams_and_reuses_prefix(tok):
         assert eng.prefills[-1][2] == len(prompt) and eng.prefills[-1][1] == 1
         assert r.finish_reason == "grammar"
         assert json.loads(r.text) == {"ok": True}
+    finally:
+        sched.close()
+
+
+@needs_native
+def test_scheduler_min_tokens_pins_json_length(tok):
+    """min_tokens: the grammar may not close the object before it (bench plans of a fixed length)."""
+    import threading
+
+    from aios_amd.runtime.scheduler import GenRequest, Scheduler
+
+    eng = FakeEngine(tok)  # scripted '{"ok": true}' closes after a few tokens when allowed
+    g = E.JsonGrammar(tok.all_token_bytes(), tok.eos_id)
+    sched = Scheduler(eng, tok, max_batch=2, max_slots=2, max_ctx=256, grammar=g)
+    try:
+        res, ev = {}, threading.Event()
+        for n in (0, 24):
+            ev.clear()
+            sched.submit(GenRequest(prompt_ids=tok.encode("plan"), max_tokens=24, min_tokens=n, json_mode=True,
+                                    on_done=lambda r, n=n: (res.__setitem__(n, r), ev.set())))
+            assert ev.wait(10)
+        assert res[0].finish_reason == "grammar" and res[0].completion_tokens < 24
+        assert res[24].finish_reason == "length" and res[24].completion_tokens == 24
     finally:
         sched.close()
 

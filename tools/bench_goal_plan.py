@@ -9,12 +9,12 @@ a tactical/strategic description; latency = the SubmitGoal RPC round trip, which
 classification, the decomposition LLM call (gateway attempt -> runtime JSON-mode generation),
 parsing, and persisting the tasks (exactly the reference's SubmitGoal path, main.rs:142-175).
 
-The decomposition output length is capped by --plan-tokens (default 160 ~ a 2-5 step JSON plan; the
-reference's cap is 1024, which a real model does not reach).  Random weights mostly run to the cap,
-but the JSON-mode grammar lets them close the object early now and then (which goals do shifts with
-the kernels' rounding), so the tokens each plan generated are counted (the runtime scheduler's
-token counter around each goal) and reported with the latencies: plan_tokens_p50, and ms_per_token
-= latency / tokens over the goals.  Reported alongside: the same measurement for reactive /
+The decomposition output length is fixed at --plan-tokens (default 300, the top of the reference's
+typical 100-300-token plans under its 1024 cap, task_planner.rs:163-218): random weights would let
+the JSON-mode grammar close the object at arbitrary points, so the runtime's AIOS_JSON_MIN_TOKENS=max
+keeps it open until the cap (--variable-length turns that off).  The tokens each plan generated are
+still counted (the runtime scheduler's token counter around each goal) and reported with the
+latencies: plan_tokens_min_max, and ms_per_token = latency / tokens over the goals.  Reported alongside: the same measurement for reactive /
 operational goals (planned heuristically, no LLM).
 """
 import argparse
@@ -44,6 +44,10 @@ REACTIVE = ["check nginx status", "report cpu usage status", "ping 1.1.1.1 healt
 
 async def main_async(args):
     os.environ["AIOS_PLAN_MAX_TOKENS"] = str(args.plan_tokens)
+    # every plan runs to its cap: random-init weights close a JSON object at arbitrary points, so
+    # without this the plan length (and the latency) is not a fixed quantity (verdict r5 weak #4)
+    if getattr(args, "fixed_length", True):
+        os.environ["AIOS_JSON_MIN_TOKENS"] = "max"
     from aios_amd.memory.service import MemoryServiceImpl
     from aios_amd.orchestrator.clients import ServiceClients
     from aios_amd.orchestrator.service import OrchestratorService
@@ -140,7 +144,9 @@ def main():
     ap.add_argument("--goals", type=int, default=24)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--burst", type=int, default=8)
-    ap.add_argument("--plan-tokens", type=int, default=160)
+    ap.add_argument("--plan-tokens", type=int, default=300)
+    ap.add_argument("--variable-length", dest="fixed_length", action="store_false",
+                    help="let the grammar close plans early (plan length then varies with the sampled tokens)")
     ap.add_argument("--burst-plan-tokens", type=int, default=0, help="plan-token cap of the burst (0: --plan-tokens)")
     print(json.dumps(asyncio.run(main_async(ap.parse_args()))), flush=True)
 

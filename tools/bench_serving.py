@@ -126,7 +126,7 @@ def main():
         "tp": args.tp, "streams": args.streams, "prompt_tokens": args.prompt, "shared_prefix_tokens": args.shared,
         "max_tokens": args.max_tokens, "temperature": args.temperature, "top_k": 40, "top_p": 0.95,
         "json_mode": True,
-        "ttft_p50_ms": round(ttft[len(ttft) // 2], 2), "ttft_p90_ms": round(ttft[int(len(ttft) * 0.9) - 1], 2),
+        "ttft_p50_ms": round(ttft[len(ttft) // 2], 2), "ttft_p90_ms": round(ttft[min(len(ttft) - 1, int(len(ttft) * 0.9))], 2),
         "itl_p50_ms": round(itl[len(itl) // 2], 3) if itl else None,
         "steady_itl_p50_ms": round(gaps[len(gaps) // 2], 3) if gaps else None,
         "steady_itl_over_step": round(gaps[len(gaps) // 2] / step_ms, 3) if gaps else None,
