@@ -200,6 +200,25 @@ PYBIND11_MODULE(_engine, m) {
            py::arg("slots"), py::arg("tokens"), py::arg("pos"), py::arg("temperature") = std::vector<float>{},
            py::arg("top_k") = std::vector<int>{}, py::arg("seed") = 0, py::arg("mask") = py::bytes(),
            py::arg("top_p") = std::vector<float>{}, py::arg("seeds") = std::vector<uint64_t>{})
+      .def("decode_submit",
+           [](Engine& e, const std::vector<int>& slots, const std::vector<int>& tokens, const std::vector<int>& pos,
+              const std::vector<float>& temperature, const std::vector<int>& top_k, uint64_t seed,
+              const std::vector<float>& top_p, const std::vector<uint64_t>& seeds) {
+             py::gil_scoped_release nogil;
+             e.decode_submit(slots, tokens, pos, temperature, top_k, seed, top_p, seeds);
+           },
+           py::arg("slots"), py::arg("tokens"), py::arg("pos"), py::arg("temperature") = std::vector<float>{},
+           py::arg("top_k") = std::vector<int>{}, py::arg("seed") = 0, py::arg("top_p") = std::vector<float>{},
+           py::arg("seeds") = std::vector<uint64_t>{})
+      .def("decode_sample",
+           [](Engine& e, py::bytes mask) {
+             std::string m = mask;
+             std::vector<uint8_t> mv(m.begin(), m.end());
+             py::gil_scoped_release nogil;
+             e.decode_sample(mv);
+           },
+           py::arg("mask") = py::bytes())
+      .def("decode_collect", &Engine::decode_collect, py::call_guard<py::gil_scoped_release>())
       .def("sample_first",
            [](Engine& e, int pos, float temperature, int top_k, float top_p, uint64_t seed, py::bytes mask) {
              std::string m = mask;
@@ -263,7 +282,9 @@ PYBIND11_MODULE(_engine, m) {
         e.set_allreduce_norm(&RcclComm::norm_hook, &c);
       })
       .def_property_readonly("vocab_parallel", &Engine::vocab_parallel)
-      .def_property_readonly("tp_fused", &Engine::tp_fused);
+      .def_property_readonly("tp_fused", &Engine::tp_fused)
+      .def("tp_fuse_fits", &Engine::tp_fuse_fits)
+      .def("disable_tp_fuse", &Engine::disable_tp_fuse);
 
   // ------------------------------------------------------------------ TP collectives (xGMI)
   py::class_<XgmiComm>(m, "XgmiComm")
@@ -275,6 +296,22 @@ PYBIND11_MODULE(_engine, m) {
       .def_property_readonly("fuse_eligible", &XgmiComm::fuse_eligible)
       .def_property_readonly("uncached", &XgmiComm::uncached)
       .def("disable_fuse", &XgmiComm::disable_fuse)
+      .def_property_readonly("fused", [](const XgmiComm& c) { return c.fuse_ctx() != nullptr; })
+      // one batch-1 EPI_TP_RESID GEMV through this comm's fused context (the TP init self-test of the
+      // O / down all-reduce epilogue): y[n] += sum over ranks of (W x)[n]; false = not launched (no
+      // fused context, or the shape does not fit the stage) -- dry: only whether it would launch
+      .def("fused_gemv",
+           [](XgmiComm& c, PyQMatrix& w, uintptr_t x, uintptr_t y, uintptr_t st, bool dry) {
+             if (!c.fuse_ctx()) return false;
+             GemvArgs a;
+             std::memset(&a, 0, sizeof(a));
+             a.nseg = 1; a.seg[0] = w.w; a.N = w.w.rows; a.K = w.w.cols; a.B = 1;
+             a.x = (const float*)x; a.ldx = a.K; a.y = (float*)y; a.ldy = a.N;
+             a.epi = EPI_TP_RESID; a.act_q8 = 1; a.tp = c.fuse_ctx(); a.kernel_sel = 1; a.grid_cap = c.fuse_grid();
+             a.dry = dry ? 1 : 0;
+             return launch_gemv_tp_fused(a, S(st));
+           },
+           py::arg("w"), py::arg("x"), py::arg("y"), py::arg("stream") = 0, py::arg("dry") = false)
       .def("connect", [](XgmiComm& c, const std::vector<py::bytes>& hs) {
         std::vector<std::string> v;
         for (auto& h : hs) v.push_back(std::string(h));
@@ -353,7 +390,7 @@ PYBIND11_MODULE(_engine, m) {
   m.def("gemv",
         [](std::vector<PyQMatrix*> segs, int B, uintptr_t x, int ldx, uintptr_t norm_w, float eps, uintptr_t y,
            int ldy, int epi, uintptr_t st, int force_v1, int act_q8, int tune_grid, int tune_u, int tune_ksplit, int tune_dbg,
-           int kernel_sel, uintptr_t dbg_ts) {
+           int kernel_sel, uintptr_t dbg_ts, uintptr_t x16, uintptr_t y16) {
           GemvArgs a;
           std::memset(&a, 0, sizeof(a));
           a.nseg = (int)segs.size();
@@ -364,12 +401,24 @@ PYBIND11_MODULE(_engine, m) {
           a.y = (float*)y; a.ldy = ldy; a.epi = epi; a.force_v1 = force_v1; a.act_q8 = act_q8;
           a.tune_grid = tune_grid; a.tune_u = tune_u; a.tune_ksplit = tune_ksplit; a.tune_dbg = tune_dbg;
           a.kernel_sel = kernel_sel; a.dbg_ts = (unsigned long long*)dbg_ts;
+          a.x16 = (const bf16_t*)x16; a.y16 = (bf16_t*)y16;  // bf16 input / SwiGLU output (hand-off kernels)
           launch_gemv(a, S(st));
         },
         py::arg("segs"), py::arg("B"), py::arg("x"), py::arg("ldx"), py::arg("norm_w"), py::arg("eps"), py::arg("y"),
         py::arg("ldy"), py::arg("epi"), py::arg("stream"), py::arg("force_v1") = 0, py::arg("act_q8") = 0,
         py::arg("tune_grid") = 0, py::arg("tune_u") = 0, py::arg("tune_ksplit") = 0, py::arg("tune_dbg") = 0,
-        py::arg("kernel_sel") = 0, py::arg("dbg_ts") = 0);
+        py::arg("kernel_sel") = 0, py::arg("dbg_ts") = 0, py::arg("x16") = 0, py::arg("y16") = 0);
+  m.def("gemv_bf16_engine_fits",
+        [](std::vector<PyQMatrix*> segs, int B, int epi) {
+          GemvArgs a;
+          std::memset(&a, 0, sizeof(a));
+          a.nseg = (int)segs.size();
+          int r = 0;
+          for (int s = 0; s < a.nseg; ++s) { a.seg[s] = segs[s]->w; a.seg_row0[s] = r; r += segs[s]->w.rows; }
+          a.N = r; a.K = segs[0]->w.cols; a.B = B; a.epi = epi;
+          return gemv_bf16_engine_fits(a);
+        },
+        py::arg("segs"), py::arg("B"), py::arg("epi") = 0);
   m.def("gemv_qkv",
         [](std::vector<PyQMatrix*> segs, int B, uintptr_t x, int ldx, uintptr_t norm_w, float eps, uintptr_t q_out,
            uintptr_t bias, int head_dim, int n_heads, int n_kv_heads, int max_ctx, int rope_neox, float rope_base,
@@ -588,6 +637,8 @@ PYBIND11_MODULE(_engine, m) {
            })
       .def_property_readonly("vocab_size", &JsonGrammar::vocab_size)
       .def_property_readonly("cache_size", &JsonGrammar::cache_size);
+  m.def("gemm_pf_export", &gemm_pf_export);
+  m.def("gemm_pf_import", &gemm_pf_import, py::arg("plans"));
   m.def("bench_stream_read_part", &aios::bench_stream_read_part, py::arg("bytes"), py::arg("nbuf"), py::arg("mode"),
         py::arg("threads") = 512, py::arg("reps") = 20);
   m.def("bench_stream_read", &aios::bench_stream_read, py::arg("bytes"), py::arg("nbuf"), py::arg("wg_per_cu"),

@@ -151,8 +151,23 @@ struct TraceRange {
   bool on;
 };
 
-// CUs of the current device (host; cached per process)
+// Per-thread CU budget: an engine whose stream is CU-masked (co-resident tiers, EngineConfig::cu_mask)
+// sizes its one-workgroup-per-CU grids to its mask while it enqueues (CuScope); 0 = the whole device
+inline int& cu_budget() {
+  static thread_local int v = 0;
+  return v;
+}
+struct CuScope {
+  int saved;
+  explicit CuScope(int n) : saved(cu_budget()) {
+    if (n > 0) cu_budget() = n;
+  }
+  ~CuScope() { cu_budget() = saved; }
+};
+
+// CUs of the current device (host; cached per process), or the enqueuing engine's CU budget
 inline int device_cu_count() {
+  if (cu_budget() > 0) return cu_budget();
   static int cus = 0;
   if (!cus) {
     int dev = 0;

@@ -45,6 +45,9 @@ struct EngineConfig {
   // logits are completed by the all-gather hook (ignored for tp_size 1 / tied embeddings)
   int vocab_parallel = 0;
   int device = 0;
+  // CU mask of the engine's stream (hipExtStreamCreateWithCUMask; 32 CUs per word, empty = every CU):
+  // co-resident tiers each get their own CUs, and the engine sizes its grids to the mask's CU count
+  std::vector<uint32_t> cu_mask;
 };
 
 // device matrix in repacked layout (owns its buffer)
@@ -114,6 +117,20 @@ class Engine {
   // logits of the last decode (B x V) -- host copy
   std::vector<float> last_logits(int B);
 
+  // Pipelined decode (the serving scheduler's fast path): decode() split so that the forward of step
+  // t+1 is enqueued before the host has seen step t's token -- the rows' tokens are the ones step t's
+  // sampler left on the device -- and only the sampler waits for the host's grammar mask:
+  //   decode_submit(..., tokens = {})   forward graph of the next step (tokens from the device)
+  //   decode_sample(mask)               mask upload + sampler + token copy, one event
+  //   decode_collect()                  waits for that event: the sampled tokens
+  // The stream holds sample(t), forward(t+1) while the host turns token t into mask t+1.
+  // decode_submit with tokens: the host's tokens (a batch's first step).
+  void decode_submit(const std::vector<int>& slots, const std::vector<int>& tokens, const std::vector<int>& pos,
+                     const std::vector<float>& temperature, const std::vector<int>& top_k, uint64_t seed,
+                     const std::vector<float>& top_p = {}, const std::vector<uint64_t>& seeds = {});
+  void decode_sample(const std::vector<uint8_t>& mask);
+  std::vector<int> decode_collect();
+
   // Device-resident greedy generation for benchmarking: runs n_steps decode steps for B
   // sequences without host synchronisation (tokens fed back on device, graph replay when
   // use_graph).  Sequences must already be prefilled to positions pos[b].
@@ -130,6 +147,12 @@ class Engine {
   // ctx null = separate all-reduce launches; grid = engine workgroups per launch (0: one per CU)
   void set_tp_fuse(const ArDevCtx* ctx, int grid) { tp_fuse_ = ctx; tp_fuse_grid_ = grid; }
   bool tp_fused() const { return tp_fuse_ != nullptr; }
+  // TP init: for every layer's O and down projection at batch 1, whether the fused all-reduce
+  // epilogue would launch on THIS rank (row kernel stage fit under the co-residency cap, which
+  // depends on the device's CU count); the ranks all-gather it and turn fusion off everywhere unless
+  // every rank fits every shape (a rank falling back alone would leave its peers waiting on flags)
+  std::vector<int> tp_fuse_fits();
+  void disable_tp_fuse() { tp_fuse_ = nullptr; }
   bool vocab_parallel() const { return cfg_.vocab_parallel != 0; }
   void reset_graphs();
   int capture_graphs(int max_b);  // pre-capture the decode-step graphs of B = 1..max_b (masked + unmasked)
@@ -151,6 +174,14 @@ class Engine {
 
  private:
   void enqueue_decode_step(int B);       // uses device arrays d_tokens_/d_pos_/d_seqlen_/d_slot_
+  void enqueue_decode_forward(int B);    // ... up to the logits (no sampler)
+  void enqueue_sample(int B);            // the step's sampler (sample_mask_: with d_mask_)
+  hipGraphExec_t forward_graph(int B);
+  int cus_ = 0;                          // CUs of the stream's mask (0: the whole device)
+  int pipe_B_ = 0;                       // rows of the submitted, not yet sampled step
+  int par_buf_ = 0;                      // which half of the double-buffered pinned parameter block
+  uint8_t* h_mask_ = nullptr;            // pinned staging of the pipelined sampler's masks
+  hipEvent_t pipe_ev_ = nullptr;         // the pipelined sampler's token copy
   bool gemm_prefill_ok(int T) const;
   void prefill_gemm(int slot, const std::vector<int>& tokens, int start_pos, bool want_logits);
   void layer_decode(int l, int B);

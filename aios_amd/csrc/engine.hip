@@ -1,5 +1,6 @@
 // Engine implementation -- see engine.h.
 #include "engine.h"
+#include <hip/hip_ext.h>
 
 #include <set>
 #include "comm.h"
@@ -62,7 +63,16 @@ static bool native_qtype(int qt) {
 
 Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
   HIP_CHECK(hipSetDevice(cfg_.device));
-  HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+  if (!cfg_.cu_mask.empty()) {
+    int n = 0, dev_cus = 0;
+    for (uint32_t w : cfg_.cu_mask) n += __builtin_popcount(w);
+    HIP_CHECK(hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, cfg_.device));
+    if (n <= 0) throw std::runtime_error("cu_mask selects no CU");
+    HIP_CHECK(hipExtStreamCreateWithCUMask(&stream_, (uint32_t)cfg_.cu_mask.size(), cfg_.cu_mask.data()));
+    cus_ = std::min(n, dev_cus);
+  } else {
+    HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+  }
 
   layers_.resize(cfg_.n_layers);
   // B <= 8 decodes through the fused GEMVs; larger batches (up to 64) through the MFMA GEMM path
@@ -82,6 +92,8 @@ Engine::~Engine() {
   for (void* p : allocs_) hipFree(p);
   if (h_par_) hipHostFree(h_par_);
   if (h_tok_out_) hipHostFree(h_tok_out_);
+  if (h_mask_) hipHostFree(h_mask_);
+  if (pipe_ev_) hipEventDestroy(pipe_ev_);
   if (stream_) hipStreamDestroy(stream_);
 }
 
@@ -264,6 +276,7 @@ QMat Engine::interleave_rows(const QMat& a, const QMat& b) {
 }
 
 void Engine::set_tensor(const std::string& name, int qt, int rows, int cols, const void* host, size_t nbytes) {
+  const CuScope cu_scope(cus_);  // (grids sized to this engine's CU mask)
   if (finalized_) throw std::runtime_error("set_tensor after finalize");
   HIP_CHECK(hipSetDevice(cfg_.device));
   static const std::regex blk_re(R"(blk\.(\d+)\.(.+))");
@@ -333,6 +346,7 @@ void Engine::set_tensor(const std::string& name, int qt, int rows, int cols, con
 }
 
 void Engine::init_random(const std::string& recipe_in, uint64_t seed) {
+  const CuScope cu_scope(cus_);  // (grids sized to this engine's CU mask)
   TraceRange tr("aios.init_random");
   HIP_CHECK(hipSetDevice(cfg_.device));
   std::string r = recipe_in;
@@ -428,6 +442,7 @@ std::string Engine::weight_type_summary() const {
 static std::vector<std::vector<const QMat*>> qkv_groups(const LayerW& L);
 
 void Engine::finalize() {
+  const CuScope cu_scope(cus_);  // (grids sized to this engine's CU mask)
   TraceRange tr("aios.finalize");
   HIP_CHECK(hipSetDevice(cfg_.device));
   stage_release();  // weights are in place: drop the load-time staging buffers
@@ -488,7 +503,9 @@ void Engine::finalize() {
   qkv_ = fbuf((size_t)Bm * (qd + 2 * kvd));
   attn_ = fbuf((size_t)Bm * std::max(qd, d));
   ff_ = fbuf((size_t)Bm * std::max(cfg_.d_ff, d));
-  if (cfg_.act_q8 && cfg_.d_ff % 8 == 0 && !(std::getenv("AIOS_FF16") && std::atoi(std::getenv("AIOS_FF16")) == 0)) {
+  // (the BF16 engine stages its x as bf16 whatever act_q8 says: the hand-off serves it too)
+  if ((cfg_.act_q8 || layers_[0].wgu.w.qtype == QT_BF16) && cfg_.d_ff % 8 == 0 &&
+      !(std::getenv("AIOS_FF16") && std::atoi(std::getenv("AIOS_FF16")) == 0)) {
     gv_ff16_ = (bf16_t*)dmalloc((size_t)Bm * cfg_.d_ff * 2);
     ws += (size_t)Bm * cfg_.d_ff * 2;
   }
@@ -505,9 +522,13 @@ void Engine::finalize() {
     par_bytes_ = par_mask_off_ + mb;
     d_par_ = (char*)dmalloc(par_bytes_);
     ws += par_bytes_;
-    HIP_CHECK(hipHostMalloc(&h_par_, par_bytes_, hipHostMallocDefault));
+    // two halves: the pipelined decode writes step t+1's parameters while step t's copy may still be
+    // queued (decode_submit); the other paths use the first half
+    HIP_CHECK(hipHostMalloc(&h_par_, 2 * par_bytes_, hipHostMallocDefault));
+    HIP_CHECK(hipHostMalloc((void**)&h_mask_, mb, hipHostMallocDefault));
+    HIP_CHECK(hipEventCreateWithFlags(&pipe_ev_, hipEventDisableTiming));
     HIP_CHECK(hipHostMalloc((void**)&h_tok_out_, (size_t)Bm * 4, hipHostMallocDefault));
-    std::memset(h_par_, 0, par_bytes_);
+    std::memset(h_par_, 0, 2 * par_bytes_);
     d_seed_ = (uint64_t*)d_par_;
     d_slot_ = (int*)(d_par_ + 8);
     d_tokens_ = d_slot_ + Bm;
@@ -1022,6 +1043,10 @@ void Engine::layer_decode(int l, int B) {
   // matrices take the int8-activation kernels: quantised formats, not F16 / BF16)
   auto q8k = [](int qt) { return qt != QT_F16 && qt != QT_BF16 && qt != QT_F32; };
   bf16_t* ff16 = (gv_ff16_ && q8k(L.wgu.w.qtype) && q8k(L.wdown.w.qtype)) ? gv_ff16_ : nullptr;
+  if (gv_ff16_ && L.wgu.w.qtype == QT_BF16 && L.wdown.w.qtype == QT_BF16 &&
+      gemv_bf16_engine_fits(gemv_args({&L.wgu}, 2 * cfg_.d_ff, d, B, x_, d, L.ffn_norm, ff_, cfg_.d_ff, EPI_SWIGLU, l)) &&
+      gemv_bf16_engine_fits(gemv_args({&L.wdown}, d, cfg_.d_ff, B, ff_, cfg_.d_ff, nullptr, x_, d, EPI_RESID, l)))
+    ff16 = gv_ff16_;  // BF16 weights: both GEMVs on the BF16 engine, which reads / writes the bf16 hand-off
   {
     GemvArgs a = gemv_args({&L.wgu}, 2 * cfg_.d_ff, d, B, x_, d, L.ffn_norm, ff_, cfg_.d_ff, EPI_SWIGLU, l);
     a.y16 = ff16;
@@ -1069,6 +1094,23 @@ bool Engine::tp_fuse_gemv(GemvArgs a) {
   return launch_gemv_tp_fused(a, stream_);
 }
 
+std::vector<int> Engine::tp_fuse_fits() {
+  const CuScope cu_scope(cus_);  // (grids sized to this engine's CU mask)
+  std::vector<int> out;
+  if (!tp_fuse_) return out;
+  HIP_CHECK(hipSetDevice(cfg_.device));
+  const int d = cfg_.d_model, qd = cfg_.n_heads * cfg_.head_dim;
+  for (int l = 0; l < cfg_.n_layers; ++l) {
+    const LayerW& L = layers_[l];
+    GemvArgs o = gemv_args({&L.wo}, d, qd, 1, attn_, qd, nullptr, x_, d, EPI_TP_RESID, l);
+    GemvArgs f = gemv_args({&L.wdown}, d, cfg_.d_ff, 1, ff_, cfg_.d_ff, nullptr, x_, d, EPI_TP_RESID, l);
+    o.dry = f.dry = 1;
+    out.push_back(tp_fuse_gemv(o) ? 1 : 0);
+    out.push_back(tp_fuse_gemv(f) ? 1 : 0);
+  }
+  return out;
+}
+
 // logits_[B][V] = rmsnorm(x) . output^T.  Vocab-parallel TP: this rank holds V/tp rows of
 // output.weight, writes its column slice of every logits row, and the xGMI all-gather completes the
 // rows on every rank, so the sampler and the grammar mask run identically everywhere -- 1/tp of
@@ -1099,7 +1141,12 @@ void Engine::lm_head(int B, const float* x, int ldx) {
 }
 
 void Engine::enqueue_decode_step(int B) {
-  const int d = cfg_.d_model, V = cfg_.vocab_size;
+  enqueue_decode_forward(B);
+  enqueue_sample(B);
+}
+
+void Engine::enqueue_decode_forward(int B) {
+  const int d = cfg_.d_model;
   {
     StepPrep sp{d_pos_, d_slot_, d_bt_, kv_maxb_, rope_cs_, cfg_.head_dim / 2, d_step_kv_, d_step_rope_};
     launch_get_rows_step(tok_embd_.w, d_tokens_, B, x_, d, 1.f, sp, stream_);
@@ -1111,6 +1158,10 @@ void Engine::enqueue_decode_step(int B) {
   step_prep_on_ = false;
   lm_head(B, x_, d);
   nrm_lm_ = false;
+}
+
+void Engine::enqueue_sample(int B) {
+  const int V = cfg_.vocab_size;
   SampleArgs s;
   std::memset(&s, 0, sizeof(s));
   s.logits = logits_; s.ldl = V; s.B = B; s.V = V;
@@ -1237,6 +1288,7 @@ void Engine::prefill_gemm(int slot, const std::vector<int>& tokens, int start_po
 }
 
 std::vector<float> Engine::prefill(int slot, const std::vector<int>& tokens, int start_pos, bool want_logits) {
+  const CuScope cu_scope(cus_);  // (grids sized to this engine's CU mask)
   TraceRange tr("aios.prefill");
   if (!finalized_) throw std::runtime_error("engine not finalized");
   HIP_CHECK(hipSetDevice(cfg_.device));
@@ -1404,6 +1456,7 @@ std::vector<int> Engine::decode(const std::vector<int>& slots, const std::vector
                                 const std::vector<int>& pos, const std::vector<float>& temperature,
                                 const std::vector<int>& top_k, uint64_t seed, const std::vector<uint8_t>& mask,
                                 const std::vector<float>& top_p, const std::vector<uint64_t>& seeds) {
+  const CuScope cu_scope(cus_);  // (grids sized to this engine's CU mask)
   if (!finalized_) throw std::runtime_error("engine not finalized");
   HIP_CHECK(hipSetDevice(cfg_.device));
   const int B = (int)slots.size();
@@ -1451,6 +1504,7 @@ std::vector<int> Engine::decode(const std::vector<int>& slots, const std::vector
 
 std::vector<int> Engine::resample(int B, const std::vector<float>& temperature, const std::vector<int>& top_k,
                                   uint64_t seed, const std::vector<uint8_t>& mask, const std::vector<float>& top_p) {
+  const CuScope cu_scope(cus_);  // (grids sized to this engine's CU mask)
   // re-run only the sampler on the logits of the last step (grammar fast path: the unmasked
   // sample was rejected on the host)
   HIP_CHECK(hipSetDevice(cfg_.device));
@@ -1495,6 +1549,7 @@ void Engine::fill_row_seeds(uint64_t* hs, int B, uint64_t seed, const std::vecto
 
 int Engine::sample_first(int pos, float temperature, int top_k, float top_p, uint64_t seed,
                          const std::vector<uint8_t>& mask) {
+  const CuScope cu_scope(cus_);  // (grids sized to this engine's CU mask)
   if (!finalized_) throw std::runtime_error("engine not finalized");
   HIP_CHECK(hipSetDevice(cfg_.device));
   const size_t mbytes = (size_t)((cfg_.vocab_size + 7) / 8);
@@ -1557,6 +1612,7 @@ void Engine::decode_loop_prepare(const std::vector<int>& slots, const std::vecto
 }
 
 void Engine::decode_loop_run(int B, int n_steps, bool use_graph) {
+  const CuScope cu_scope(cus_);  // (grids sized to this engine's CU mask)
   TraceRange tr(use_graph ? "aios.decode_graph_replay" : "aios.decode_eager");
   HIP_CHECK(hipSetDevice(cfg_.device));
   if ((int)row_slots_.size() < B) throw std::runtime_error("decode_loop_run: rows not prepared");
@@ -1577,7 +1633,7 @@ void Engine::decode_loop_run(int B, int n_steps, bool use_graph) {
 // the captured decode step for (B, sample_mask_): captured once, replayed for every request --
 // the kernels read tokens / positions / slots / sampling parameters from device arrays
 hipGraphExec_t Engine::step_graph(int B) {
-  const int key = B * 2 + (sample_mask_ ? 1 : 0);
+  const int key = B * 4 + (sample_mask_ ? 1 : 0);
   auto it = graphs_.find(key);
   if (it == graphs_.end()) {
     hipGraph_t g;
@@ -1597,10 +1653,112 @@ hipGraphExec_t Engine::step_graph(int B) {
   return it->second;
 }
 
+// the forward of a decode step without its sampler (the pipelined decode's graph)
+hipGraphExec_t Engine::forward_graph(int B) {
+  const int key = B * 4 + 2;
+  auto it = graphs_.find(key);
+  if (it == graphs_.end()) {
+    hipGraph_t g;
+    HIP_CHECK(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal));
+    try {
+      enqueue_decode_forward(B);
+    } catch (...) {
+      hipStreamEndCapture(stream_, &g);
+      throw;
+    }
+    HIP_CHECK(hipStreamEndCapture(stream_, &g));
+    hipGraphExec_t ge;
+    HIP_CHECK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+    HIP_CHECK(hipGraphDestroy(g));
+    it = graphs_.emplace(key, ge).first;
+  }
+  return it->second;
+}
+
+void Engine::decode_submit(const std::vector<int>& slots, const std::vector<int>& tokens, const std::vector<int>& pos,
+                           const std::vector<float>& temperature, const std::vector<int>& top_k, uint64_t seed,
+                           const std::vector<float>& top_p, const std::vector<uint64_t>& seeds) {
+  const CuScope cu_scope(cus_);  // (grids sized to this engine's CU mask)
+  if (!finalized_) throw std::runtime_error("engine not finalized");
+  HIP_CHECK(hipSetDevice(cfg_.device));
+  const int B = (int)slots.size();
+  if (B < 1 || B > cfg_.max_batch) throw std::runtime_error("decode_submit: batch out of range");
+  if ((int)pos.size() != B || (!tokens.empty() && (int)tokens.size() != B) || (!seeds.empty() && (int)seeds.size() != B))
+    throw std::runtime_error("decode_submit: size mismatch");
+  for (int b = 0; b < B; ++b) {
+    if (pos[b] < 0 || pos[b] >= cfg_.max_ctx) throw std::runtime_error("decode_submit: position out of range");
+    if (slots[b] < 0 || slots[b] >= cfg_.max_slots) throw std::runtime_error("decode_submit: bad slot");
+    if (!tokens.empty() && (tokens[b] < 0 || tokens[b] >= cfg_.vocab_size))
+      throw std::runtime_error("decode_submit: token out of range");
+  }
+  const int Bm = cfg_.max_batch;
+  par_buf_ ^= 1;  // the other half: the previous submit's copy may not have run yet
+  char* hpar = h_par_ + (size_t)par_buf_ * par_bytes_;
+  *(uint64_t*)hpar = seed;
+  int* hs = (int*)(hpar + 8);
+  int *ht = hs + Bm, *hp = ht + Bm, *hl = hp + Bm, *hk = hl + Bm;
+  float* hT = (float*)(hk + Bm);
+  float* hP = hT + Bm;
+  for (int b = 0; b < B; ++b) {
+    hs[b] = slots[b]; hp[b] = pos[b]; hl[b] = pos[b] + 1;
+    if (!tokens.empty()) ht[b] = tokens[b];
+    hk[b] = b < (int)top_k.size() ? top_k[b] : 0;
+    hT[b] = b < (int)temperature.size() ? temperature[b] : 0.f;
+    hP[b] = b < (int)top_p.size() ? top_p[b] : 1.f;
+  }
+  const size_t seeds_off = (size_t)((char*)d_seeds_ - d_par_);
+  fill_row_seeds((uint64_t*)(hpar + seeds_off), B, seed, seeds);
+  const size_t tok_off = (size_t)((char*)d_tokens_ - d_par_), end = seeds_off + (size_t)Bm * 8;
+  if (tokens.empty()) {  // every row array but the tokens the previous sampler left on the device
+    const size_t after = tok_off + (size_t)Bm * 4;
+    HIP_CHECK(hipMemcpyAsync(d_par_, hpar, tok_off, hipMemcpyHostToDevice, stream_));
+    HIP_CHECK(hipMemcpyAsync(d_par_ + after, hpar + after, end - after, hipMemcpyHostToDevice, stream_));
+  } else {
+    HIP_CHECK(hipMemcpyAsync(d_par_, hpar, end, hipMemcpyHostToDevice, stream_));
+  }
+  row_slots_ = slots;
+  row_pos_ = pos;
+  for (int b = 0; b < B; ++b) {
+    kv_prepare_write(slots[b], pos[b], pos[b] + 1);
+    row_pos_[b] = pos[b] + 1;
+  }
+  kv_sync(B);
+  HIP_CHECK(hipGraphLaunch(forward_graph(B), stream_));
+  pipe_B_ = B;
+}
+
+void Engine::decode_sample(const std::vector<uint8_t>& mask) {
+  const CuScope cu_scope(cus_);  // (grids sized to this engine's CU mask)
+  const int B = pipe_B_;
+  if (B < 1) throw std::runtime_error("decode_sample: no submitted step");
+  HIP_CHECK(hipSetDevice(cfg_.device));
+  const size_t mbytes = (size_t)B * ((cfg_.vocab_size + 7) / 8);
+  if (!mask.empty()) {
+    if (mask.size() != mbytes) throw std::runtime_error("decode_sample: mask size mismatch");
+    // (one pinned buffer: the previous mask's copy ran before the sampler whose token the host
+    // already collected)
+    std::memcpy(h_mask_, mask.data(), mbytes);
+    HIP_CHECK(hipMemcpyAsync(d_mask_, h_mask_, mbytes, hipMemcpyHostToDevice, stream_));
+  }
+  sample_mask_ = !mask.empty();
+  enqueue_sample(B);
+  sample_mask_ = false;
+  HIP_CHECK(hipMemcpyAsync(h_tok_out_, d_tokens_, B * 4, hipMemcpyDeviceToHost, stream_));
+  HIP_CHECK(hipEventRecord(pipe_ev_, stream_));
+}
+
+std::vector<int> Engine::decode_collect() {
+  const int B = pipe_B_;
+  if (B < 1) throw std::runtime_error("decode_collect: no sampled step");
+  HIP_CHECK(hipEventSynchronize(pipe_ev_));
+  return std::vector<int>(h_tok_out_, h_tok_out_ + B);
+}
+
 // capture (without running) the decode-step graphs of every batch size up to max_b, masked and
 // unmasked, so a serving scheduler whose batch grows and shrinks never stalls a step on a capture
 // (a 160-launch capture + instantiate costs milliseconds); returns the graphs held
 int Engine::capture_graphs(int max_b) {
+  const CuScope cu_scope(cus_);  // (grids sized to this engine's CU mask)
   if (!finalized_) throw std::runtime_error("engine not finalized");
   HIP_CHECK(hipSetDevice(cfg_.device));
   const bool saved = sample_mask_;
@@ -1608,6 +1766,7 @@ int Engine::capture_graphs(int max_b) {
     for (int m = 0; m < 2; ++m) {
       sample_mask_ = m != 0;
       step_graph(B);
+      if (m == 0) forward_graph(B);  // (the pipelined decode's forward)
     }
   sample_mask_ = saved;
   return (int)graphs_.size();
@@ -1691,16 +1850,21 @@ void Engine::kv_sync(int B) {
   if (bt_dirty_) {
     std::vector<int> dev(bt_.size());
     for (size_t i = 0; i < bt_.size(); ++i) dev[i] = bt_[i] < 0 ? kv_nblocks_ : bt_[i];
-    HIP_CHECK(hipMemcpy(d_bt_, dev.data(), dev.size() * 4, hipMemcpyHostToDevice));
+    // (on the engine's stream, not the null stream: a co-resident tier's CU-masked stream is a
+    // blocking stream, and a null-stream copy would wait for the other tier's queued steps)
+    HIP_CHECK(hipMemcpyAsync(d_bt_, dev.data(), dev.size() * 4, hipMemcpyHostToDevice, stream_));
+    HIP_CHECK(hipStreamSynchronize(stream_));
     bt_dirty_ = false;
   }
   if (rows_changed) {
     std::copy(rows.begin(), rows.end(), row_bt_host_.begin());
-    HIP_CHECK(hipMemcpy(d_row_bt_, rows.data(), rows.size() * 4, hipMemcpyHostToDevice));
+    HIP_CHECK(hipMemcpyAsync(d_row_bt_, rows.data(), rows.size() * 4, hipMemcpyHostToDevice, stream_));
+    HIP_CHECK(hipStreamSynchronize(stream_));
   }
 }
 
 void Engine::copy_slot(int src, int dst, int n) {
+  const CuScope cu_scope(cus_);  // (grids sized to this engine's CU mask)
   if (!finalized_) throw std::runtime_error("engine not finalized");
   if (src < 0 || src >= cfg_.max_slots || dst < 0 || dst >= cfg_.max_slots) throw std::runtime_error("copy_slot: bad slot");
   if (src == dst) return;

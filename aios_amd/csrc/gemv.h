@@ -62,10 +62,12 @@ struct GemvArgs {
   const float2* step_rope;
   const ArDevCtx* tp;           // EPI_TP_RESID: the XgmiComm device context (XgmiComm::fuse_ctx)
   int grid_cap;                 // EPI_TP_RESID row kernel: workgroups at most (0: no cap; ranks sharing a GPU)
+  int dry;                      // EPI_TP_RESID (launch_gemv_tp_fused): only report whether it would launch
 };
 
 void launch_gemv(const GemvArgs& a, hipStream_t st);
 bool gemv_engine_fits(const GemvArgs& a);  // the B-row LDS-DMA engine serves a (gemv_dispatch.hip)
+bool gemv_bf16_engine_fits(const GemvArgs& a);  // the BF16 LDS-DMA engine serves a (gemv_lds16.h)
 // EPI_TP_RESID through the row-pair kernel; false = nothing launched (gemv_dispatch.hip)
 bool launch_gemv_tp_fused(const GemvArgs& a, hipStream_t st);
 

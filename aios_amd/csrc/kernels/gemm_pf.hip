@@ -4,6 +4,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <map>
+#include <stdexcept>
 #include <mutex>
 #include <tuple>
 #include <vector>
@@ -58,15 +59,16 @@ static bool pf_tile_ok(const GemmQArgs& a, int bn) {
 
 // Measured plans: one per (shape, formats, epilogue, M bucket), filled by gemm_pf_autotune (the
 // engine tunes its projection shapes at finalize); the model below is the fallback.
-using PfKey = std::tuple<int, int, int, int, int, int, int, int, int>;
+using PfKey = std::tuple<int, int, int, int, int, int, int, int, int, int>;
 static int pf_bucket(int M) {
   int b = 64;
   while (b < M && b < 2048) b <<= 1;
   return M > 2048 ? (M + 2047) / 2048 * 2048 : b;
 }
 static PfKey pf_key(const GemmQArgs& a) {
+  // (+ the CU budget: a CU-masked co-resident engine plans for its own CUs)
   return PfKey(a.N, a.K, pf_bucket(a.M), a.epi, a.seg[0].qtype, a.seg[a.nseg - 1].qtype, a.nseg,
-               a.nseg > 1 ? a.seg_n0[1] : 0, a.nseg > 2 ? a.seg_n0[2] : 0);
+               a.nseg > 1 ? a.seg_n0[1] : 0, a.nseg > 2 ? a.seg_n0[2] : 0, device_cu_count());
 }
 static std::mutex pf_mu;
 static std::map<PfKey, PfPlan>& pf_tuned() {
@@ -101,9 +103,8 @@ static std::vector<PfPlan> pf_candidates(const GemmQArgs& a, bool bf) {
   return out;
 }
 
+static PfPlan pf_model_plan(const GemmQArgs& a, bool bf, bool s1_only);
 static PfPlan pf_plan(const GemmQArgs& a, bool bf) {
-  PfPlan best;
-  double bt = 1e30;
   if (!std::getenv("AIOS_GEMM_PF_TILE") && !std::getenv("AIOS_GEMM_PF_SPLIT") && a.ksplit <= 0) {
     std::lock_guard<std::mutex> g(pf_mu);
     if (a.epi == GEPI_QKV) {
@@ -116,6 +117,13 @@ static PfPlan pf_plan(const GemmQArgs& a, bool bf) {
       if (it != pf_tuned().end()) return it->second;
     }
   }
+  return pf_model_plan(a, bf, false);
+}
+
+// the modelled plan (pf_model), or the one AIOS_GEMM_PF_TILE / _SPLIT / a.ksplit pin
+static PfPlan pf_model_plan(const GemmQArgs& a, bool bf, bool s1_only) {
+  PfPlan best;
+  double bt = 1e30;
   // AIOS_GEMM_PF_TILE=BMxBN / AIOS_GEMM_PF_SPLIT=S pin the plan (sweeps: tools/bench_gemm.py --pf-sweep)
   // (read per call: tests and sweeps change them inside one process)
   const char* tile = std::getenv("AIOS_GEMM_PF_TILE");
@@ -130,7 +138,7 @@ static PfPlan pf_plan(const GemmQArgs& a, bool bf) {
       for (int S : {1, 2, 3, 4, 6, 8, 12, 16}) {
         if (a.ksplit > 0 && S != a.ksplit) continue;
         if (a.ksplit <= 0 && split > 0 && S != split) continue;
-        if (S > 1 && (pf_no_split(a) || nk / S < 2)) continue;
+        if (S > 1 && (s1_only || pf_no_split(a) || nk / S < 2)) continue;
         if (!bf && bn == 256 && (a.K / 256) / S < 1) continue;  // pf8c slices whole 256-blocks
         const double t = pf_model(a, bm, bn, S, bf);
         if (t < bt) {
@@ -188,12 +196,25 @@ static bool pf_eligible(const GemmQArgs& a) {
 }
 
 // Time every candidate plan for these args (real buffers; outputs overwritten) and keep the fastest
-// for their M bucket.  Returns the number of candidates timed (0: not a prefill-GEMM launch).
+// for their M bucket.  Returns the number of candidates timed (0: not a prefill-GEMM launch, or a
+// key already planned in this process -- tuned by an earlier engine or imported, gemm_pf_import: a
+// second engine never changes the plans a first one runs).
+//
+// Stable choice: a measured plan replaces the modelled one only when it is > 5 % faster,
+// so timing noise (a co-tenant, TP ranks sharing the GPU) does not pick a different tile / split in
+// each process; ties keep the earlier candidate (a fixed order).  TP ranks then take rank 0's plans
+// (tp.py broadcasts gemm_pf_export), and AIOS_GEMM_PF_PLANS persists them across processes.
 int gemm_pf_autotune(const GemmQArgs& a, hipStream_t st) {
   if (!pf_eligible(a)) return 0;
+  {
+    std::lock_guard<std::mutex> g(pf_mu);
+    if (pf_tuned().count(pf_key(a))) return 0;
+  }
   const bool bf = a.seg[0].qtype == QT_BF16;
   const std::vector<PfPlan> cands = pf_candidates(a, bf);
   if (cands.empty()) return 0;
+  const PfPlan mp = pf_model_plan(a, bf, false), mp1 = pf_model_plan(a, bf, true);
+  float tm = -1.f, tm1 = -1.f;  // the modelled plans' measured times
   hipEvent_t e0, e1;
   HIP_CHECK(hipEventCreate(&e0));
   HIP_CHECK(hipEventCreate(&e1));
@@ -215,13 +236,46 @@ int gemm_pf_autotune(const GemmQArgs& a, hipStream_t st) {
       bt1 = ms;
       best1 = p;
     }
+    auto same = [](const PfPlan& x, const PfPlan& y) { return x.bm == y.bm && x.bn == y.bn && x.s == y.s; };
+    if (same(p, mp)) tm = ms;
+    if (same(p, mp1)) tm1 = ms;
   }
   HIP_CHECK(hipEventDestroy(e0));
   HIP_CHECK(hipEventDestroy(e1));
+  if (tm > 0.f && bt > 0.95f * tm) best = mp;
+  if (tm1 > 0.f && bt1 > 0.95f * tm1) best1 = mp1;
   std::lock_guard<std::mutex> g(pf_mu);
   pf_tuned()[pf_key(a)] = best;
   if (bt1 < 1e30f) pf_tuned_s1()[pf_key(a)] = best1;
   return (int)cands.size();
+}
+
+// every tuned plan as flat ints: 10 key fields, bm, bn, s, map (0: best, 1: best without split-K)
+std::vector<int> gemm_pf_export() {
+  std::lock_guard<std::mutex> g(pf_mu);
+  std::vector<int> v;
+  for (int m = 0; m < 2; ++m)
+    for (const auto& kv : (m ? pf_tuned_s1() : pf_tuned())) {
+      const PfKey& k = kv.first;
+      for (int x : {std::get<0>(k), std::get<1>(k), std::get<2>(k), std::get<3>(k), std::get<4>(k), std::get<5>(k),
+                    std::get<6>(k), std::get<7>(k), std::get<8>(k), std::get<9>(k)})
+        v.push_back(x);
+      v.push_back(kv.second.bm); v.push_back(kv.second.bn); v.push_back(kv.second.s); v.push_back(m);
+    }
+  return v;
+}
+
+// install plans (replacing any tuned for the same keys): TP workers take the leader's, a process
+// takes a persisted set; later autotune calls skip these keys
+void gemm_pf_import(const std::vector<int>& v) {
+  if (v.size() % 14) throw std::runtime_error("gemm_pf_import: bad plan list");
+  std::lock_guard<std::mutex> g(pf_mu);
+  for (size_t i = 0; i < v.size(); i += 14) {
+    const PfKey k(v[i], v[i + 1], v[i + 2], v[i + 3], v[i + 4], v[i + 5], v[i + 6], v[i + 7], v[i + 8], v[i + 9]);
+    PfPlan p;
+    p.bm = v[i + 10]; p.bn = v[i + 11]; p.s = v[i + 12];
+    (v[i + 13] ? pf_tuned_s1() : pf_tuned())[k] = p;
+  }
 }
 
 // whether launch_gemm_pf takes these args (the engine asks before choosing the GEPI_QKV epilogue

@@ -534,6 +534,7 @@ bool launch_gemv_persistent(GemvArgs a, hipStream_t st) {
 #include "gemv_q8.h"
 #include "gemv_cu.h"
 #include "gemv_lds.h"
+#include "gemv_lds16.h"
 
 inline int qtype_block(int qt) {
   return (qt == QT_Q4_K || qt == QT_Q5_K || qt == QT_Q6_K) ? 256 : (qt == QT_F16 || qt == QT_BF16 ? 8 : 32);
@@ -577,6 +578,9 @@ void launch_gemv_pair(const GemvArgs& a, hipStream_t st) {
       if (a.B > 2 && a.B <= 4 && launch_gemv_q8<QT0, QT1, 4>(a, st)) return;
       if (a.B > 4 && launch_gemv_q8<QT0, QT1, 8>(a, st)) return;
     }
+  }
+  if constexpr (QT0 == QT_BF16 && QT1 == QT_BF16) {
+    if (!a.force_v1 && launch_gemv_lds16(a, st)) return;  // B = 1..4: the BF16 LDS-DMA engine
   }
   if (a.epi == EPI_TP_RESID)  // only the row-pair int8 kernel does the fused all-reduce epilogue
     throw std::runtime_error("gemv: EPI_TP_RESID launch not taken by the row-pair kernel (use launch_gemv_tp_fused)");

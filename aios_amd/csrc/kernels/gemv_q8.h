@@ -977,6 +977,7 @@ bool launch_q8_rows(const GemvArgs& a, size_t lds, hipStream_t st) {
     auto per_wg = [&](int g) { return 2 * nw * ((npairs + g * nw - 1) / (g * nw)); };
     while (per_wg(blocks) > TPF_CAP && blocks < cap) ++blocks;
     if (per_wg(blocks) > TPF_CAP) return false;
+    if (a.dry) return true;  // (TP init: every rank's fit for this shape is all-gathered first)
   }
   hipLaunchKernelGGL((gemv_q8_rows<QT0, QT1, B, U, PIPE>), dim3(blocks), dim3(nw * 64), lds, st, a);
   return true;

@@ -248,5 +248,7 @@ bool gemm_pf_probe(const GemmQArgs& a, int probe, hipStream_t st);  // timing an
 // time every prefill-GEMM plan for these args (buffers overwritten) and keep the fastest for their M
 // bucket; returns the number of plans timed
 int gemm_pf_autotune(const GemmQArgs& a, hipStream_t st);
+std::vector<int> gemm_pf_export();              // the process's tuned prefill plans (flat ints)
+void gemm_pf_import(const std::vector<int>& v);  // ... installed (TP: the leader's; persisted sets)
 
 }  // namespace aios

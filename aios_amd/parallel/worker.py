@@ -24,7 +24,8 @@ def main(argv=None):
 
     from ..runtime import native
     from .channel import WorkerChannel
-    from .tp import _shard, comm_capacity, comm_kind, worker_loop
+    from .tp import (_shard, channel_allgather, comm_capacity, comm_kind, reconcile_tp_fuse, share_prefill_plans,
+                     worker_loop, xgmi_handshake)
 
     ch = WorkerChannel(a.leader, a.rank, os.environ.pop("AIOS_TP_TOKEN", ""))
     eng, cfg = _shard(a.spec, a.rank, a.world, a.device, a.max_ctx, a.max_slots, a.max_batch, a.seed, bool(a.q8))
@@ -34,7 +35,11 @@ def main(argv=None):
         comm = native.require().XgmiComm(a.rank, a.world, a.device, comm_capacity(cfg.d_model, a.max_batch))
         ch.send(comm.ipc_handle())
         comm.connect(ch.recv())
+        xgmi_handshake(comm, a.rank, a.world, a.device, channel_allgather(ch, False))
     eng.set_comm(comm)
+    share_prefill_plans(channel_allgather(ch, False))
+    if comm_kind() != "rccl":
+        reconcile_tp_fuse(eng, channel_allgather(ch, False))
     # per-step commands arrive through the leader's shared-memory ring (ring.py); the TCP channel
     # only carried the authenticated setup
     from .ring import CommandRing

@@ -77,4 +77,10 @@ class FaultyEngine:
         return self._engine.decode(*a, **k)
 
     def __getattr__(self, name):
-        return getattr(self._engine, name)
+        attr = getattr(self._engine, name)
+        if name == "decode_submit":  # the pipelined decode's step (present iff the engine has it)
+            def submit(*a, **k):
+                self._spec.check("decode")
+                return attr(*a, **k)
+            return submit
+        return attr

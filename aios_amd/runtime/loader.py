@@ -10,6 +10,8 @@ rows), row-parallel attn_output/ffn_down (whole quant blocks along K), vocab-par
 """
 from __future__ import annotations
 
+import logging
+import os
 import time
 from typing import Optional
 
@@ -19,6 +21,8 @@ from ..gguf.quants import BLOCK_INFO, GGMLType
 from ..gguf.reader import GGUFReader
 from ..models.config import ModelConfig
 from . import native
+
+log = logging.getLogger("aios.runtime.loader")
 
 COLUMN_PARALLEL = ("attn_q.weight", "attn_k.weight", "attn_v.weight", "ffn_gate.weight", "ffn_up.weight",
                    "attn_q.bias", "attn_k.bias", "attn_v.bias")
@@ -69,11 +73,37 @@ def load_engine(path: str, max_ctx: Optional[int] = None, max_slots: int = 4, ma
         rows, cols = ti.rows, ti.cols
         raw, rows, cols = shard_tensor(tname, raw, int(ti.ggml_type), rows, cols, tp_rank, tp_size, vp)
         eng.set_tensor(tname, int(ti.ggml_type), rows, cols, raw)
-    eng.finalize()
+    finalize(eng)
     if verbose:
         print(f"[loader] {cfg.name}: {eng.weight_bytes / 1e9:.2f} GB weights, {eng.kv_bytes / 1e9:.2f} GB KV, "
               f"{time.time() - t0:.1f}s")
     return eng, cfg, r
+
+
+def finalize(eng):
+    """Engine.finalize with the prefill-GEMM plans persisted when AIOS_GEMM_PF_PLANS names a file:
+    plans saved by an earlier process are installed first (finalize then times only shapes it does
+    not hold), and the process's plans are written back -- every process serving a model runs the
+    same tile / split plans (per-process tuning noise changed prefill numerics)."""
+    import json
+
+    m = native.require()
+    path = os.environ.get("AIOS_GEMM_PF_PLANS", "")
+    if path and os.path.exists(path):
+        try:
+            with open(path) as f:
+                m.gemm_pf_import([int(v) for v in json.load(f)])
+        except (OSError, ValueError, RuntimeError) as e:
+            log.warning("ignoring prefill plan file %s: %s", path, e)
+    eng.finalize()
+    if path:
+        tmp = f"{path}.{os.getpid()}.tmp"
+        try:
+            with open(tmp, "w") as f:
+                json.dump(list(m.gemm_pf_export()), f)
+            os.replace(tmp, path)
+        except OSError as e:
+            log.warning("cannot persist prefill plans to %s: %s", path, e)
 
 
 def random_engine(cfg: ModelConfig, recipe: str = "Q4_K_M", seed: int = 0, max_ctx: Optional[int] = None,
@@ -86,5 +116,5 @@ def random_engine(cfg: ModelConfig, recipe: str = "Q4_K_M", seed: int = 0, max_c
                               act_q8=act_q8)
     eng = m.Engine(ec)
     eng.init_random(recipe, seed)
-    eng.finalize()
+    finalize(eng)
     return eng

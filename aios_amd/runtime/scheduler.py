@@ -134,6 +134,11 @@ class Scheduler:
         self._ttft = collections.deque(maxlen=256)
         self._step_ms = collections.deque(maxlen=256)
         self._tok_times = collections.deque(maxlen=4096)
+        # pipelined decode (Engine.decode_submit / decode_sample / decode_collect): the forward of step
+        # t+1 is queued before the host has seen step t's token, so the host's per-token work (grammar
+        # mask, accept, detokenize, callbacks) overlaps the device step instead of adding to it
+        self.pipeline = hasattr(engine, "decode_submit") and os.environ.get("AIOS_DECODE_PIPELINE", "1") != "0"
+        self._pending: Optional[List[_Seq]] = None  # rows whose sampled step is in flight
         self.thread = threading.Thread(target=self._run, name=f"sched-{name}", daemon=True)
         self.thread.start()
 
@@ -161,6 +166,7 @@ class Scheduler:
                 while not self.stop_flag and not self.queue and not self.active and not self.prefilling:
                     self.cv.wait(timeout=1.0)
                 if self.stop_flag:
+                    self._discard_pending()
                     for s in list(self.active) + list(self.prefilling):
                         self._finish(s, "cancelled")
                     while self.queue:
@@ -171,6 +177,8 @@ class Scheduler:
                 while (self.queue and self.free_slots and
                        len(self.active) + len(self.prefilling) + len(admit) < self.max_batch):
                     admit.append(self.queue.popleft())
+            if admit or self.prefilling:
+                self._drain()  # (no other engine call while a pipelined step is in flight)
             for r in admit:
                 try:
                     self._admit(r)
@@ -201,6 +209,7 @@ class Scheduler:
                 except Exception as e:  # noqa: BLE001
                     log.exception("decode step failed")
                     self._engine_failed(e)
+                    self._pending = None
                     for s in list(self.active):
                         self._finish(s, "error", str(e))
 
@@ -365,7 +374,102 @@ class Scheduler:
             return self.grammar.mask_open(seq.grammar_state)
         return self.grammar.mask(seq.grammar_state)
 
+    def _drain(self):
+        """Collect and accept a pipelined step still in flight (before any other engine call)."""
+        rows = self._pending
+        if rows is None:
+            return
+        self._pending = None
+        try:
+            out = self.engine.decode_collect()
+        except Exception as e:  # noqa: BLE001
+            log.exception("decode step failed")
+            self._engine_failed(e)
+            for s in list(self.active):
+                self._finish(s, "error", str(e))
+            return
+        self._take(rows, out)
+
+    def _discard_pending(self):
+        if self._pending is not None:
+            self._pending = None
+            try:
+                self.engine.decode_collect()
+            except Exception:  # noqa: BLE001
+                pass
+
+    def _take(self, rows, out):
+        self.stats["steps"] += 1
+        self.stats["batch_sum"] += len(rows)
+        for s, t in zip(rows, out):
+            s.pos += 1
+            self.slot_cache[s.slot].append(s.last)
+            self._accept(s, int(t))
+
+    def _can_speculate(self, rows) -> bool:
+        """Whether step t+1 of the same rows can be queued before step t's tokens are known: no
+        admission or prefill will interleave, and no row is certain to finish at step t."""
+        if self.prefilling or (self.queue and self.free_slots and
+                               len(self.active) + len(self.prefilling) < self.max_batch):
+            return False
+        now = time.time()
+        for s in rows:
+            r = s.req
+            if r.cancelled or len(s.out) + 1 >= r.max_tokens or s.pos + 2 >= self.max_ctx:
+                return False
+            if r.deadline and now > r.deadline:
+                return False
+        return True
+
+    def _submit(self, rows, first: bool):
+        """Queue the forward of the rows' next step: `first` with the host's tokens at s.pos, else
+        with the tokens the in-flight sampler leaves on the device, at s.pos + 1."""
+        self.engine.decode_submit([s.slot for s in rows], [s.last for s in rows] if first else [],
+                                  [s.pos + (0 if first else 1) for s in rows],
+                                  [float(s.req.temperature) for s in rows],
+                                  [int(s.req.top_k) if s.req.temperature > 0 else 0 for s in rows], 0,
+                                  [float(s.req.top_p) if 0.0 < s.req.top_p < 1.0 else 1.0 for s in rows],
+                                  [s.seed for s in rows])
+
+    def _masks(self, rows) -> bytes:
+        if not any(s.grammar_state is not None for s in rows):
+            return b""
+        if self._full_mask is None:
+            self._full_mask = host_sampler.all_allowed(self.vocab)
+        return b"".join(self._mask(s) if s.grammar_state is not None else self._full_mask for s in rows)
+
+    def _step_pipelined(self):
+        t0 = time.perf_counter()
+        rows = self._pending
+        if rows is None:  # a batch's first step (or after an admission / finish): host tokens
+            rows = list(self.active)
+            self._submit(rows, True)
+            self.engine.decode_sample(self._masks(rows))
+        self._pending = None
+        spec = self._can_speculate(rows)
+        if spec:
+            self._submit(rows, False)
+        t1 = time.perf_counter()
+        out = self.engine.decode_collect()
+        t2 = time.perf_counter()
+        self._take(rows, out)
+        t2b = time.perf_counter()
+        if spec and self.active == rows:
+            # nobody finished or joined: sample the queued forward with the masks of the new tokens
+            self.engine.decode_sample(self._masks(rows))
+            self._pending = rows
+        # (spec and a row finished: the queued forward is dropped -- its KV writes at the next
+        # position are rewritten by whatever runs there next)
+        t3 = time.perf_counter()
+        tm = self.timing
+        tm["mask_s"] += (t3 - t2b) + (t1 - t0)   # masks + submit / sampler enqueue
+        tm["engine_decode_s"] += t2 - t1          # waiting for the device
+        tm["accept_s"] += t2b - t2
+        self.step_log.append((t3, len(rows)))
+
     def _step(self):
+        if self.pipeline:
+            return self._step_pipelined()
         B = len(self.active)
         slots = [s.slot for s in self.active]
         toks = [s.last for s in self.active]

@@ -49,6 +49,28 @@ def test_batched_equals_sequential(model):
         assert a.token_ids == b.token_ids
 
 
+@pytest.mark.parametrize("json_mode", [False, True])
+def test_pipelined_decode_matches_sync(model, json_mode):
+    """The scheduler's pipelined decode on the native engine (Engine.decode_submit / decode_sample /
+    decode_collect: step t+1's forward queued from the device-resident token before step t's token
+    reaches the host) against the synchronous decode() path: the same greedy tokens for one and for
+    three concurrent requests (rows finishing at different lengths), JSON mode with the masks."""
+    tok, sched = model.tokenizer, model.scheduler
+    prompts = [tok.encode(p) for p in ["alpha beta gamma", "the quick brown fox jumps", "aiOS goal"]]
+    kw = [dict(max_tokens=n, temperature=0.0, json_mode=json_mode) for n in (20, 9, 31)]
+    res = {}
+    try:
+        for pipe in (False, True):
+            sched.pipeline = pipe
+            one = [_run_all(sched, [(p, k)])[0] for p, k in zip(prompts, kw)]
+            many = _run_all(sched, list(zip(prompts, kw)))
+            res[pipe] = [(r.token_ids, r.finish_reason) for r in one + many]
+    finally:
+        sched.pipeline = True
+    assert res[False] == res[True]
+    assert all(len(t) > 0 for t, _ in res[True])
+
+
 def test_prefix_reuse_is_exact(model):
     tok, sched = model.tokenizer, model.scheduler
     base = tok.encode("system: you are the aiOS planner. tools: fs.read fs.write net.ping " * 2)

@@ -87,6 +87,80 @@ def test_tp_command_channel_gloo(tmp_path):
     assert c0 == c1 and [c[0] for c in c0] == ["prefill", "decode", "decode_loop_run"]
 
 
+FUSE_WORKER = r"""
+import os, sys, json
+sys.path.insert(0, sys.argv[1])
+import torch.distributed as dist
+import aios_amd.parallel.tp as tp
+
+rank = int(sys.argv[2]); out = sys.argv[3]
+dist.init_process_group("gloo", init_method="tcp://127.0.0.1:" + sys.argv[4], rank=rank, world_size=2)
+
+class FakeComm:
+    fused = True
+    disabled = False
+    def disable_fuse(self): self.disabled = True; self.fused = False
+
+class FakeEngine:
+    tp_fused = True
+    disabled = False
+    def tp_fuse_fits(self): return [1, 1, 1, 0] if rank == 1 else [1, 1, 1, 1]  # rank 1 misses one shape
+    def disable_tp_fuse(self): self.disabled = True; self.tp_fused = False
+
+ag = tp.gloo_allgather(None, 2)
+res = {}
+# 1. the fused self-test fails on rank 1 only: every rank disables the fused epilogue
+tp.fused_self_test = lambda comm, r, w, d, g: r != 1
+c = FakeComm()
+res["fail_on"] = tp.check_fused_comm(c, rank, 2, 0, ag)
+res["fail_disabled"] = c.disabled
+# 2. it passes everywhere: fused stays on
+tp.fused_self_test = lambda comm, r, w, d, g: True
+c2 = FakeComm()
+res["pass_on"] = tp.check_fused_comm(c2, rank, 2, 0, ag)
+res["pass_disabled"] = c2.disabled
+# 3. the self-test raises on rank 0: a failed check, not a hang
+def boom(*a):
+    if rank == 0:
+        raise RuntimeError("peer mapping refused")
+    return True
+tp.fused_self_test = boom
+c3 = FakeComm()
+res["raise_on"] = tp.check_fused_comm(c3, rank, 2, 0, ag)
+# 4. per-layer launch fits differ: every rank's engine turns fusion off
+e = FakeEngine()
+res["fits_on"] = tp.reconcile_tp_fuse(e, ag)
+res["fits_disabled"] = e.disabled
+json.dump(res, open(out + str(rank), "w"))
+dist.destroy_process_group()
+"""
+
+
+def test_tp_fused_check_fails_safe_on_every_rank(tmp_path):
+    """a fused-epilogue self-test failing on ONE rank (or raising there), and per-layer
+    fused-launch fits that differ between ranks, turn the fused all-reduce epilogue off on EVERY rank
+    (GEMV + separate all-reduce everywhere), over a real gloo world of 2 with mocked comms."""
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = str(s.getsockname()[1])
+    s.close()
+    script = tmp_path / "f.py"
+    script.write_text(FUSE_WORKER)
+    out = str(tmp_path / "res")
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    procs = [subprocess.Popen([sys.executable, str(script), ROOT, str(r), out, port], env=env) for r in range(2)]
+    for p in procs:
+        assert p.wait(timeout=120) == 0
+    for r in range(2):
+        res = json.load(open(out + str(r)))
+        assert res["fail_on"] is False and res["fail_disabled"] is True, res
+        assert res["pass_on"] is True and res["pass_disabled"] is False, res
+        assert res["raise_on"] is False, res
+        assert res["fits_on"] is False and res["fits_disabled"] is True, res
+
+
 def test_shard_tensor_vocab_parallel_output():
     from aios_amd.gguf.quants import BLOCK_INFO, GGMLType
     from aios_amd.runtime.loader import shard_tensor
