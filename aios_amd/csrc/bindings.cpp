@@ -158,7 +158,9 @@ PYBIND11_MODULE(_engine, m) {
       .def_readwrite("tp_rank", &EngineConfig::tp_rank)
       .def_readwrite("tp_size", &EngineConfig::tp_size)
       .def_readwrite("vocab_parallel", &EngineConfig::vocab_parallel)
-      .def_readwrite("device", &EngineConfig::device);
+      .def_readwrite("device", &EngineConfig::device)
+      .def_readwrite("cu_mask", &EngineConfig::cu_mask)
+      .def_readwrite("kv_fp8", &EngineConfig::kv_fp8);
 
   py::class_<Engine>(m, "Engine")
       .def(py::init<const EngineConfig&>())
@@ -264,7 +266,6 @@ PYBIND11_MODULE(_engine, m) {
       .def("capture_graphs", &Engine::capture_graphs, py::arg("max_b"), py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("stream", &Engine::stream_handle)
       .def_property_readonly("k_cache_ptr", &Engine::kv_cache_k)
-      .def("attn_o_counters", &Engine::attn_o_counters)
       .def_property_readonly("v_cache_ptr", &Engine::kv_cache_v)
       .def("set_allreduce_ptr", [](Engine& e, uintptr_t fn, uintptr_t ctx) {
         e.set_allreduce(reinterpret_cast<AllReduceFn>(fn), reinterpret_cast<void*>(ctx));
@@ -284,6 +285,9 @@ PYBIND11_MODULE(_engine, m) {
       .def_property_readonly("vocab_parallel", &Engine::vocab_parallel)
       .def_property_readonly("tp_fused", &Engine::tp_fused)
       .def("tp_fuse_fits", &Engine::tp_fuse_fits)
+      .def("set_kv_scales", &Engine::set_kv_scales)
+      .def_property_readonly("kv_scales", &Engine::kv_scales)
+      .def_property_readonly("kv_fp8", &Engine::kv_fp8)
       .def("disable_tp_fuse", &Engine::disable_tp_fuse);
 
   // ------------------------------------------------------------------ TP collectives (xGMI)
@@ -449,9 +453,11 @@ PYBIND11_MODULE(_engine, m) {
   m.def("attn_decode",
         [](uintptr_t q, uintptr_t k, uintptr_t v, uintptr_t seq_len, uintptr_t slot, int B, int H, int Hkv, int hd,
            int max_ctx, int n_chunks, float scale, uintptr_t opart, uintptr_t ml, uintptr_t out, uintptr_t counters,
-           uintptr_t st, int split, uintptr_t block_table, int bt_rows, uintptr_t ts) {
+           uintptr_t st, int split, uintptr_t block_table, int bt_rows, uintptr_t ts, int kv_fp8, float k_scale,
+           float v_scale) {
           AttnDecodeArgs a;
           a.split = split;
+          a.kv_fp8 = kv_fp8; a.kv_scale_k = k_scale; a.kv_scale_v = v_scale;
           a.ts = (unsigned long long*)ts;
           a.block_table = (const int*)block_table; a.bt_rows = bt_rows;
           a.q = (const float*)q; a.k_cache = (const bf16_t*)k; a.v_cache = (const bf16_t*)v;
@@ -464,9 +470,15 @@ PYBIND11_MODULE(_engine, m) {
         py::arg("q"), py::arg("k"), py::arg("v"), py::arg("seq_len"), py::arg("slot"), py::arg("B"), py::arg("H"),
         py::arg("Hkv"), py::arg("hd"), py::arg("max_ctx"), py::arg("n_chunks"), py::arg("scale"), py::arg("opart"),
         py::arg("ml"), py::arg("out"), py::arg("counters"), py::arg("st"), py::arg("split") = 0,
-        py::arg("block_table") = 0, py::arg("bt_rows") = 0, py::arg("ts") = 0);
+        py::arg("block_table") = 0, py::arg("bt_rows") = 0, py::arg("ts") = 0, py::arg("kv_fp8") = 0,
+        py::arg("k_scale") = 1.f, py::arg("v_scale") = 1.f);
   m.def("attn_decode_split", &attn_decode_split);
   // physical identity of a device (PCI bus id): ranks that share a GPU see the same string
+  m.def("device_cu_count", [](int dev) {
+    int n = 0;
+    HIP_CHECK(hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev));
+    return n;
+  }, py::arg("device") = 0);
   m.def("device_pci_bus_id", [](int dev) {
     char buf[64] = {0};
     HIP_CHECK(hipDeviceGetPCIBusId(buf, (int)sizeof(buf), dev));
@@ -586,8 +598,10 @@ PYBIND11_MODULE(_engine, m) {
   m.def(
       "attn_prefill",
       [](uintptr_t q, uintptr_t k, uintptr_t v, int slot, int start, int T, int H, int Hkv, int hd, int max_ctx,
-         float scale, uintptr_t out, int ldo, uintptr_t st, uintptr_t block_table) {
+         float scale, uintptr_t out, int ldo, uintptr_t st, uintptr_t block_table, int kv_fp8, float k_scale,
+         float v_scale) {
         AttnPrefillArgs a;
+        a.kv_fp8 = kv_fp8; a.kv_scale_k = k_scale; a.kv_scale_v = v_scale;
         a.block_table = (const int*)block_table;
         a.q = (const float*)q; a.k_cache = (const bf16_t*)k; a.v_cache = (const bf16_t*)v;
         a.slot = slot; a.start = start; a.T = T; a.n_heads = H; a.n_kv_heads = Hkv; a.head_dim = hd;
@@ -596,7 +610,8 @@ PYBIND11_MODULE(_engine, m) {
       },
       py::arg("q"), py::arg("k"), py::arg("v"), py::arg("slot"), py::arg("start"), py::arg("T"), py::arg("H"),
       py::arg("Hkv"), py::arg("hd"), py::arg("max_ctx"), py::arg("scale"), py::arg("out"), py::arg("ldo"),
-      py::arg("st"), py::arg("block_table") = 0);
+      py::arg("st"), py::arg("block_table") = 0, py::arg("kv_fp8") = 0, py::arg("k_scale") = 1.f,
+      py::arg("v_scale") = 1.f);
   m.def("attn_prefill_supports", &attn_prefill_supports);
 
   // ------------------------------------------------------------------ JSON-mode grammar (K10)

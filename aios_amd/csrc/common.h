@@ -69,6 +69,35 @@ __device__ __forceinline__ uint16_t f32_to_bf16(float f) {
 }
 __device__ __forceinline__ float h2f(uint16_t h) { return __half2float(__ushort_as_half(h)); }
 
+// ---- KV cache element formats: bf16, or OCP fp8 e4m3 (gfx950's e4m3fn, max 448) with a per-layer
+// K / V scale (EngineConfig::kv_fp8; value = code * scale).  Element indices are the same for both;
+// an fp8 pool is addressed in bytes.
+__device__ __forceinline__ uint32_t f32x2_to_fp8x2(float a, float b) {
+  a = fminf(fmaxf(a, -448.f), 448.f);  // (saturate: e4m3fn has no infinity, an overflow is NaN)
+  b = fminf(fmaxf(b, -448.f), 448.f);
+  return (uint32_t)__builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false) & 0xffffu;
+}
+// K or V pair (v0 -> element i0, v1 -> element i1) of one token: one 4-B (bf16) / 2-B (fp8) store when
+// adjacent; inv = 1 / the layer's scale (fp8 only)
+__device__ __forceinline__ void kv_store_pair(bf16_t* cache, size_t i0, size_t i1, float v0, float v1, int fp8,
+                                              float inv) {
+  if (fp8) {
+    uint8_t* c = (uint8_t*)cache;
+    const uint32_t p = f32x2_to_fp8x2(v0 * inv, v1 * inv);
+    if (i1 == i0 + 1 && !(i0 & 1)) {
+      *(uint16_t*)(c + i0) = (uint16_t)p;
+    } else {
+      c[i0] = (uint8_t)(p & 0xff);
+      c[i1] = (uint8_t)(p >> 8);
+    }
+  } else if (i1 == i0 + 1 && !(i0 & 1)) {
+    *(uint32_t*)(cache + i0) = (uint32_t)f32_to_bf16(v0) | ((uint32_t)f32_to_bf16(v1) << 16);
+  } else {
+    cache[i0] = f32_to_bf16(v0);
+    cache[i1] = f32_to_bf16(v1);
+  }
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

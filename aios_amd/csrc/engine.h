@@ -45,6 +45,10 @@ struct EngineConfig {
   // logits are completed by the all-gather hook (ignored for tp_size 1 / tied embeddings)
   int vocab_parallel = 0;
   int device = 0;
+  // KV cache element type: 0 = bf16, 1 = fp8 e4m3 (OCP) with a per-layer K / V scale (value = code x
+  // scale, Engine::set_kv_scales; 1.0 until set) -- half the cache bytes and the decode attention's
+  // K / V reads (bf16 or fp8 on MI355X)
+  int kv_fp8 = 0;
   // CU mask of the engine's stream (hipExtStreamCreateWithCUMask; 32 CUs per word, empty = every CU):
   // co-resident tiers each get their own CUs, and the engine sizes its grids to the mask's CU count
   std::vector<uint32_t> cu_mask;
@@ -153,6 +157,13 @@ class Engine {
   // every rank fits every shape (a rank falling back alone would leave its peers waiting on flags)
   std::vector<int> tp_fuse_fits();
   void disable_tp_fuse() { tp_fuse_ = nullptr; }
+  // fp8 KV: the per-layer (K, V) scales, 2 x n_layers values (value = code x scale; captured decode
+  // graphs are dropped, they hold the old ones).  1.0 until set: e4m3 spans 2^-9 .. 448, the range of
+  // post-RoPE keys and values, as serving stacks' uncalibrated fp8 KV caches do; a calibrated model
+  // (per-layer K / V absolute maxima / 448) sets them here
+  void set_kv_scales(const std::vector<float>& s);
+  std::vector<float> kv_scales() const { return kv_scale_; }
+  int kv_fp8() const { return cfg_.kv_fp8; }
   bool vocab_parallel() const { return cfg_.vocab_parallel != 0; }
   void reset_graphs();
   int capture_graphs(int max_b);  // pre-capture the decode-step graphs of B = 1..max_b (masked + unmasked)
@@ -168,8 +179,6 @@ class Engine {
 
   // raw device pointers for tests / custom kernels
   uintptr_t kv_cache_k() const { return (uintptr_t)k_cache_; }
-  // layer l's attention -> O counter block (kernels/attn_o.hip; tests / probes read it)
-  std::vector<int> attn_o_counters(int l) const;
   uintptr_t kv_cache_v() const { return (uintptr_t)v_cache_; }
 
  private:
@@ -178,6 +187,23 @@ class Engine {
   void enqueue_sample(int B);            // the step's sampler (sample_mask_: with d_mask_)
   hipGraphExec_t forward_graph(int B);
   int cus_ = 0;                          // CUs of the stream's mask (0: the whole device)
+  int kv_es_ = 2;                        // bytes per KV element (2 bf16, 1 fp8)
+  std::vector<float> kv_scale_;          // [n_layers][K, V] fp8 scales (value = code * scale)
+  bf16_t* kv_layer(bf16_t* base, int l) const {  // layer l's pool (element indices as bf16, bytes as kv_es_)
+    return (bf16_t*)((char*)base + (size_t)l * layer_kv_elems_ * kv_es_);
+  }
+  template <typename T>
+  void kv_write_args(T& a, int l) const {
+    a.kv_fp8 = cfg_.kv_fp8;
+    a.kv_inv_k = 1.f / kv_scale_[2 * l];
+    a.kv_inv_v = 1.f / kv_scale_[2 * l + 1];
+  }
+  template <typename T>
+  void kv_read_args(T& a, int l) const {
+    a.kv_fp8 = cfg_.kv_fp8;
+    a.kv_scale_k = kv_scale_[2 * l];
+    a.kv_scale_v = kv_scale_[2 * l + 1];
+  }
   int pipe_B_ = 0;                       // rows of the submitted, not yet sampled step
   int par_buf_ = 0;                      // which half of the double-buffered pinned parameter block
   uint8_t* h_mask_ = nullptr;            // pinned staging of the pipelined sampler's masks
@@ -253,8 +279,6 @@ class Engine {
   void fill_row_seeds(uint64_t* host_seeds, int B, uint64_t seed, const std::vector<uint64_t>& seeds);
   uint8_t* d_mask_ = nullptr;
   int n_chunks_ = 0;
-  int* attn_o_cnt_ = nullptr;  // [n_layers][ATTN_O_CNT_INTS] attention -> O hand-off counters (batch 1)
-  float* attn_o_x_ = nullptr;  // [8 XCDs][n_heads * head_dim] attention outputs of the XCD-local path
   int* attn_cnt_ = nullptr;  // [max(prefill_rows, max_batch)][n_kv_heads] combine tickets
   float2* rope_cs_ = nullptr;  // [max_ctx][head_dim/2] cos/sin computed in double on the host
   int prefill_rows_ = 64;  // rows of the prefill workspace

@@ -467,7 +467,9 @@ void Engine::finalize() {
   for (int b = kv_nblocks_ - 1; b >= 0; --b) free_blocks_.push_back(b);
   row_bt_host_.assign((size_t)Bm * kv_maxb_, kv_nblocks_);
   layer_kv_elems_ = (size_t)(kv_nblocks_ + 1) * Hkv * KV_BLOCK * hd;
-  kv_bytes_ = 2 * layer_kv_elems_ * cfg_.n_layers * sizeof(bf16_t);
+  kv_es_ = cfg_.kv_fp8 ? 1 : 2;  // bytes per cached element (fp8 e4m3 or bf16)
+  kv_bytes_ = 2 * layer_kv_elems_ * cfg_.n_layers * kv_es_;
+  if (kv_scale_.size() != (size_t)2 * cfg_.n_layers) kv_scale_.assign((size_t)2 * cfg_.n_layers, 1.f);
   k_cache_ = (bf16_t*)dmalloc(kv_bytes_ / 2);
   v_cache_ = (bf16_t*)dmalloc(kv_bytes_ / 2);
   HIP_CHECK(hipMemset(k_cache_, 0, kv_bytes_ / 2));
@@ -477,10 +479,6 @@ void Engine::finalize() {
     const size_t nc = (size_t)std::max(prefill_rows_, Bm) * H;  // decode attention tickets [row][head]
     attn_cnt_ = (int*)dmalloc(nc * 4);
     HIP_CHECK(hipMemset(attn_cnt_, 0, nc * 4));
-    // batch-1 attention -> O hand-off counters (kernels/attn_o.hip), one per layer
-    attn_o_cnt_ = (int*)dmalloc((size_t)cfg_.n_layers * ATTN_O_CNT_INTS * 4);
-    HIP_CHECK(hipMemset(attn_o_cnt_, 0, (size_t)cfg_.n_layers * ATTN_O_CNT_INTS * 4));
-    attn_o_x_ = (float*)dmalloc((size_t)8 * H * hd * 4);  // per-XCD attention outputs
   }
   {
     const int half = hd / 2;
@@ -801,8 +799,9 @@ GemvArgs Engine::gemv_args(const std::vector<const QMat*>& segs, int N, int K, i
     a.rope_neox = cfg_.rope_neox;
     a.rope_base = cfg_.rope_theta;
     a.rope_cs = rope_cs_;
-    a.k_cache = k_cache_ + (size_t)layer * layer_kv_elems_;
-    a.v_cache = v_cache_ + (size_t)layer * layer_kv_elems_;
+    a.k_cache = kv_layer(k_cache_, layer);
+    a.v_cache = kv_layer(v_cache_, layer);
+    kv_write_args(a, layer);
   }
   apply_knobs(a, K == cfg_.d_ff ? "DOWN" : (N == 2 * cfg_.d_ff ? "GU" : (N == cfg_.vocab_size ? "LM" : "O")));
   return a;
@@ -845,8 +844,8 @@ void Engine::layer_decode_gemm(int l, int B) {
   const bool tp = cfg_.tp_size > 1;
   const bool fn = nrm_on(B);
   const bool tpn = tp && tpn_on(B);  // (fn and tpn are exclusive: fn needs tp_size 1)
-  bf16_t* kc = k_cache_ + (size_t)l * layer_kv_elems_;
-  bf16_t* vc = v_cache_ + (size_t)l * layer_kv_elems_;
+  bf16_t* kc = kv_layer(k_cache_, l);
+  bf16_t* vc = kv_layer(v_cache_, l);
   // consumer side of the split RMSNorm: A = bf16(x * g) from the previous residual GEMM
   auto nrm_in = [&](GemmQArgs& g) {
     g.A = dec_xn16_; g.nrm_in = nrm_part_; g.nrm_parts = nrm_parts_; g.nrm_eps = cfg_.norm_eps;
@@ -886,6 +885,7 @@ void Engine::layer_decode_gemm(int l, int B) {
     g.head_dim = hd; g.q_dim = qd; g.kv_dim = kvd; g.n_kv_heads = Hkv; g.max_ctx = cfg_.max_ctx;
     g.rope_cs = rope_cs_; g.pos = d_pos_; g.slot = d_slot_; g.block_table = d_bt_;
     g.q_out = q_; g.k_cache = kc; g.v_cache = vc;
+    kv_write_args(g, l);
   }
   gemm(g);
   static const bool attn_out16 = !(std::getenv("AIOS_ATTN_OUT16") && std::atoi(std::getenv("AIOS_ATTN_OUT16")) == 0);
@@ -897,12 +897,14 @@ void Engine::layer_decode_gemm(int l, int B) {
   p.rope_neox = cfg_.rope_neox; p.rope_base = cfg_.rope_theta; p.rope_cs = rope_cs_;
   p.pos = d_pos_; p.slot = d_slot_; p.q_out = q_;
   p.k_cache = kc; p.v_cache = vc; p.max_ctx = cfg_.max_ctx; p.block_table = d_bt_;
+  kv_write_args(p, l);
   launch_qkv_post(p, stream_);
   }
   {
     AttnDecodeArgs a;
     a.split = 0;
     a.q = q_; a.k_cache = kc; a.v_cache = vc; a.seq_len = d_seqlen_; a.slot = d_slot_;
+    kv_read_args(a, l);
     a.block_table = attn_bt_; a.bt_rows = attn_bt_rows_;
     a.B = B; a.n_heads = H; a.n_kv_heads = Hkv; a.head_dim = hd; a.max_ctx = cfg_.max_ctx;
     a.n_chunks = n_chunks_; a.scale = 1.f / std::sqrt((float)hd);
@@ -963,8 +965,9 @@ void Engine::layer_decode(int l, int B) {
       a.head_dim = hd; a.q_dim = qd; a.kv_dim = kvd; a.n_kv_heads = cfg_.n_kv_heads; a.max_ctx = cfg_.max_ctx;
       a.rope_neox = cfg_.rope_neox; a.rope_base = cfg_.rope_theta; a.rope_cs = rope_cs_;
       a.pos = d_pos_; a.slot = d_slot_;
-      a.k_cache = k_cache_ + (size_t)l * layer_kv_elems_;
-      a.v_cache = v_cache_ + (size_t)l * layer_kv_elems_;
+      a.k_cache = kv_layer(k_cache_, l);
+      a.v_cache = kv_layer(v_cache_, l);
+      kv_write_args(a, l);
       a.block_table = d_bt_;
       if (step_prep_on_ && B == 1) { a.step_kv = d_step_kv_; a.step_rope = d_step_rope_; }
     } else {
@@ -994,21 +997,22 @@ void Engine::layer_decode(int l, int B) {
       p.q_norm = L.q_norm; p.k_norm = L.k_norm; p.eps = cfg_.norm_eps;
       p.rope_neox = cfg_.rope_neox; p.rope_base = cfg_.rope_theta; p.rope_cs = rope_cs_;
       p.pos = d_pos_; p.slot = d_slot_; p.q_out = q_;
-      p.k_cache = k_cache_ + (size_t)l * layer_kv_elems_;
-      p.v_cache = v_cache_ + (size_t)l * layer_kv_elems_;
+      p.k_cache = kv_layer(k_cache_, l);
+      p.v_cache = kv_layer(v_cache_, l);
+      kv_write_args(p, l);
       p.max_ctx = cfg_.max_ctx;
       p.block_table = d_bt_;
       launch_qkv_post(p, stream_);
     }
   }
   // ---- attention (fp32 output: a bf16 hand-off to O measured neutral, 544.0-544.5 vs 545.0-545.7 tok/s)
-  bool attn_o_fused = false;
   {
     AttnDecodeArgs a;
     a.split = 0;
     a.q = q_;
-    a.k_cache = k_cache_ + (size_t)l * layer_kv_elems_;
-    a.v_cache = v_cache_ + (size_t)l * layer_kv_elems_;
+    a.k_cache = kv_layer(k_cache_, l);
+    a.v_cache = kv_layer(v_cache_, l);
+    kv_read_args(a, l);
     a.seq_len = d_seqlen_;
     a.slot = d_slot_;
     a.block_table = attn_bt_; a.bt_rows = attn_bt_rows_;
@@ -1016,24 +1020,13 @@ void Engine::layer_decode(int l, int B) {
     a.n_chunks = n_chunks_;
     a.scale = 1.f / std::sqrt((float)hd);
     a.o_part = opart_; a.ml = ml_; a.out = attn_; a.counters = attn_cnt_;
-    // batch 1 without TP, AIOS_ATTN_O=1: attention and the O GEMV (+ residual) in one launch, the
-    // O weights streaming while attention runs (kernels/attn_o.hip; measured no faster, off by
-    // default); otherwise two launches
-    // (counter re-arm: layer l zeroes layer l-1's, cyclically -- every B = 1 step runs all layers)
-    if (B == 1 && cfg_.tp_size <= 1 && cfg_.n_layers >= 2)
-      attn_o_fused = launch_attn_o(a, gemv_args({&L.wo}, d, qd, B, attn_, qd, nullptr, x_, d, EPI_RESID, l),
-                                   attn_o_cnt_ + (size_t)l * ATTN_O_CNT_INTS,
-                                   attn_o_cnt_ + (size_t)((l + cfg_.n_layers - 1) % cfg_.n_layers) * ATTN_O_CNT_INTS,
-                                   attn_o_x_, stream_);
-    if (!attn_o_fused) launch_attn_decode(a, stream_);
+    launch_attn_decode(a, stream_);
   }
   // ---- O projection (+ residual; TP: partial -> all-reduce -> add, fused into the GEMV epilogue
   // when the comm provides it)
   {
     const bool tp = cfg_.tp_size > 1;
-    if (attn_o_fused) {
-      // (launched above, in the attention launch)
-    } else if (!(tp && tp_fuse_gemv(gemv_args({&L.wo}, d, qd, B, attn_, qd, nullptr, x_, d, EPI_TP_RESID, l)))) {
+    if (!(tp && tp_fuse_gemv(gemv_args({&L.wo}, d, qd, B, attn_, qd, nullptr, x_, d, EPI_TP_RESID, l)))) {
       GemvArgs a = gemv_args({&L.wo}, d, qd, B, attn_, qd, nullptr, tp ? ff_ : x_, d, tp ? EPI_STORE : EPI_RESID, l);
       launch_gemv(a, stream_);
       if (tp) allreduce(ff_, (size_t)B * d, x_);
@@ -1067,13 +1060,6 @@ void Engine::layer_decode(int l, int B) {
   }
 }
 
-std::vector<int> Engine::attn_o_counters(int l) const {
-  std::vector<int> v(ATTN_O_CNT_INTS);
-  if (l < 0 || l >= cfg_.n_layers) throw std::runtime_error("attn_o_counters: bad layer");
-  HIP_CHECK(hipStreamSynchronize(stream_));
-  HIP_CHECK(hipMemcpy(v.data(), attn_o_cnt_ + (size_t)l * ATTN_O_CNT_INTS, v.size() * 4, hipMemcpyDeviceToHost));
-  return v;
-}
 
 // EPI_TP_RESID (the O / down all-reduce in the GEMV epilogue, gemv_q8.h) when the comm provides the
 // fused context
@@ -1209,8 +1195,8 @@ void Engine::prefill_gemm(int slot, const std::vector<int>& tokens, int start_po
     launch_get_rows(tok_embd_.w, gm_tokens_, n, gm_x_, d, 1.f, stream_);
     for (int l = 0; l < cfg_.n_layers; ++l) {
       const LayerW& L = layers_[l];
-      bf16_t* kc = k_cache_ + (size_t)l * layer_kv_elems_;
-      bf16_t* vc = v_cache_ + (size_t)l * layer_kv_elems_;
+      bf16_t* kc = kv_layer(k_cache_, l);
+      bf16_t* vc = kv_layer(v_cache_, l);
       // split-RMSNorm consumer / producer (as in layer_decode_gemm, on this chunk's rows)
       auto nrm_in = [&](GemmQArgs& g) {
         g.A = gm_xn16_; g.nrm_in = gm_npart_; g.nrm_parts = gm_nparts_; g.nrm_eps = cfg_.norm_eps;
@@ -1240,6 +1226,7 @@ void Engine::prefill_gemm(int slot, const std::vector<int>& tokens, int start_po
         q.head_dim = hd; q.q_dim = qd; q.kv_dim = kvd; q.n_kv_heads = Hkv; q.max_ctx = cfg_.max_ctx;
         q.rope_cs = rope_cs_; q.pos = gm_pos_; q.slot = gm_slot_; q.block_table = d_bt_;
         q.q_out = gm_q_; q.k_cache = kc; q.v_cache = vc;
+        kv_write_args(q, l);
         static const int pf_qkv = [] { const char* e = std::getenv("AIOS_PREFILL_QKV_EPI"); return e ? std::atoi(e) : 0; }();
         qepi = sh || (pf_qkv && gemm_pf_serves(q));
         if (qepi) g = q;
@@ -1253,10 +1240,12 @@ void Engine::prefill_gemm(int slot, const std::vector<int>& tokens, int start_po
       p.rope_neox = cfg_.rope_neox; p.rope_base = cfg_.rope_theta; p.rope_cs = rope_cs_;
       p.pos = gm_pos_; p.slot = gm_slot_; p.q_out = gm_q_;
       p.k_cache = kc; p.v_cache = vc; p.max_ctx = cfg_.max_ctx; p.block_table = d_bt_;
+      kv_write_args(p, l);
       launch_qkv_post(p, stream_);
       }
       AttnPrefillArgs at;
       at.q = gm_q_; at.k_cache = kc; at.v_cache = vc; at.block_table = d_bt_;
+      kv_read_args(at, l);
       at.slot = slot; at.start = start_pos + r0; at.T = n;
       at.n_heads = H; at.n_kv_heads = Hkv; at.head_dim = hd; at.max_ctx = cfg_.max_ctx;
       at.scale = 1.f / std::sqrt((float)hd);
@@ -1357,8 +1346,9 @@ std::vector<float> Engine::prefill(int slot, const std::vector<int>& tokens, int
               a.head_dim = hd; a.q_dim = qd; a.kv_dim = kvd; a.n_kv_heads = cfg_.n_kv_heads; a.max_ctx = cfg_.max_ctx;
               a.rope_neox = cfg_.rope_neox; a.rope_base = cfg_.rope_theta; a.rope_cs = rope_cs_;
               a.pos = d_pos_; a.slot = d_slot_;
-              a.k_cache = k_cache_ + (size_t)l * layer_kv_elems_;
-              a.v_cache = v_cache_ + (size_t)l * layer_kv_elems_;
+              a.k_cache = kv_layer(k_cache_, l);
+              a.v_cache = kv_layer(v_cache_, l);
+              kv_write_args(a, l);
               a.block_table = d_bt_;
             } else {
               a.epi = EPI_STORE; a.y = qkv_; a.ldy = qd + 2 * kvd;
@@ -1373,8 +1363,9 @@ std::vector<float> Engine::prefill(int slot, const std::vector<int>& tokens, int
             p.q_norm = L.q_norm; p.k_norm = L.k_norm; p.eps = cfg_.norm_eps;
             p.rope_neox = cfg_.rope_neox; p.rope_base = cfg_.rope_theta; p.rope_cs = rope_cs_;
             p.pos = d_pos_; p.slot = d_slot_; p.q_out = q_;
-            p.k_cache = k_cache_ + (size_t)l * layer_kv_elems_;
-            p.v_cache = v_cache_ + (size_t)l * layer_kv_elems_;
+            p.k_cache = kv_layer(k_cache_, l);
+            p.v_cache = kv_layer(v_cache_, l);
+            kv_write_args(p, l);
             p.max_ctx = cfg_.max_ctx;
             p.block_table = d_bt_;
             launch_qkv_post(p, stream_);
@@ -1385,8 +1376,9 @@ std::vector<float> Engine::prefill(int slot, const std::vector<int>& tokens, int
           AttnDecodeArgs a;
           a.split = 0;
           a.q = qb;
-          a.k_cache = k_cache_ + (size_t)l * layer_kv_elems_;
-          a.v_cache = v_cache_ + (size_t)l * layer_kv_elems_;
+          a.k_cache = kv_layer(k_cache_, l);
+          a.v_cache = kv_layer(v_cache_, l);
+          kv_read_args(a, l);
           a.seq_len = pf_seqlen_; a.slot = pf_slot_;
           a.block_table = d_bt_; a.bt_rows = 0;  // prefill rows: one slot, slot-indexed table
           a.B = n; a.n_heads = cfg_.n_heads; a.n_kv_heads = cfg_.n_kv_heads; a.head_dim = cfg_.head_dim;
@@ -1785,6 +1777,15 @@ void Engine::synchronize() {
   HIP_CHECK(hipStreamSynchronize(stream_));
 }
 
+void Engine::set_kv_scales(const std::vector<float>& s) {
+  if (s.size() != (size_t)2 * cfg_.n_layers) throw std::runtime_error("set_kv_scales: need 2 x n_layers values");
+  for (float v : s)
+    if (!(v > 0.f) || !std::isfinite(v)) throw std::runtime_error("set_kv_scales: scales must be positive");
+  if (finalized_) HIP_CHECK(hipStreamSynchronize(stream_));  // (no replay of the old graphs in flight)
+  kv_scale_ = s;
+  reset_graphs();
+}
+
 void Engine::reset_graphs() {
   for (auto& kv : graphs_) hipGraphExecDestroy(kv.second);
   graphs_.clear();
@@ -1806,12 +1807,11 @@ void Engine::kv_unref(int blk) {
 
 // one block of every layer's K and V pool: [n_kv_heads][KV_BLOCK][hd] contiguous
 void Engine::kv_copy_block(int src, int dst) {
-  const size_t blk = (size_t)cfg_.n_kv_heads * KV_BLOCK * cfg_.head_dim;
+  const size_t blk = (size_t)cfg_.n_kv_heads * KV_BLOCK * cfg_.head_dim * kv_es_;  // bytes
   for (int l = 0; l < cfg_.n_layers; ++l)
     for (bf16_t* base : {k_cache_, v_cache_}) {
-      bf16_t* lb = base + (size_t)l * layer_kv_elems_;
-      HIP_CHECK(hipMemcpyAsync(lb + (size_t)dst * blk, lb + (size_t)src * blk, blk * sizeof(bf16_t),
-                               hipMemcpyDeviceToDevice, stream_));
+      char* lb = (char*)kv_layer(base, l);
+      HIP_CHECK(hipMemcpyAsync(lb + (size_t)dst * blk, lb + (size_t)src * blk, blk, hipMemcpyDeviceToDevice, stream_));
     }
 }
 

@@ -55,6 +55,8 @@ struct GemvArgs {
   bf16_t* k_cache;              // layer base of the paged pool [blocks][n_kv][KV_BLOCK][hd]
   const int* block_table;       // [slots][max_ctx / KV_BLOCK] or null (identity)
   bf16_t* v_cache;
+  int kv_fp8;                   // KV pool in fp8 e4m3: stores code = value * kv_inv_{k,v}
+  float kv_inv_k, kv_inv_v;
   // batch-1 decode: {pos, physical KV block} and the RoPE (cos, sin) row of this step's position,
   // prepared by the step's embedding launch (StepPrep, ops.h) -- no pos -> block table / rope chain
   // in the QKV kernel (null: looked up from pos / slot / block_table)

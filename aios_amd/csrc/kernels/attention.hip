@@ -25,13 +25,13 @@
 
 namespace aios {
 
-template <int HD, int G>
+template <int HD, int G, bool F8>
 __global__ void __launch_bounds__(512) attn_decode_kernel(AttnDecodeArgs a, AttnSplit sp_) {
   kernarg_warm<sizeof(AttnDecodeArgs) + sizeof(AttnSplit)>();
-  attn_role<HD, G>(a, sp_, blockIdx.x);
+  attn_role<HD, G, F8>(a, sp_, blockIdx.x);
 }
 
-template <int HD>
+template <int HD, bool F8>
 static void launch_hd(const AttnDecodeArgs& a, int G, hipStream_t st) {
   AttnSplit sp;
   const int nwg = attn_plan(a, G, sp);
@@ -39,11 +39,11 @@ static void launch_hd(const AttnDecodeArgs& a, int G, hipStream_t st) {
   sp.n_attn = nwg;
   dim3 grid(nwg, 1, a.B);
   switch (G) {
-    case 1: hipLaunchKernelGGL((attn_decode_kernel<HD, 1>), grid, dim3(512), 0, st, a, sp); break;
-    case 2: hipLaunchKernelGGL((attn_decode_kernel<HD, 2>), grid, dim3(512), 0, st, a, sp); break;
-    case 4: hipLaunchKernelGGL((attn_decode_kernel<HD, 4>), grid, dim3(512), 0, st, a, sp); break;
-    case 5: hipLaunchKernelGGL((attn_decode_kernel<HD, 5>), grid, dim3(512), 0, st, a, sp); break;
-    case 8: hipLaunchKernelGGL((attn_decode_kernel<HD, 8>), grid, dim3(512), 0, st, a, sp); break;
+    case 1: hipLaunchKernelGGL((attn_decode_kernel<HD, 1, F8>), grid, dim3(512), 0, st, a, sp); break;
+    case 2: hipLaunchKernelGGL((attn_decode_kernel<HD, 2, F8>), grid, dim3(512), 0, st, a, sp); break;
+    case 4: hipLaunchKernelGGL((attn_decode_kernel<HD, 4, F8>), grid, dim3(512), 0, st, a, sp); break;
+    case 5: hipLaunchKernelGGL((attn_decode_kernel<HD, 5, F8>), grid, dim3(512), 0, st, a, sp); break;
+    case 8: hipLaunchKernelGGL((attn_decode_kernel<HD, 8, F8>), grid, dim3(512), 0, st, a, sp); break;
     default: throw std::runtime_error("attn_decode: unsupported GQA group size " + std::to_string(G));
   }
 }
@@ -67,9 +67,15 @@ void launch_attn_decode(const AttnDecodeArgs& a, hipStream_t st) {
   const int G = a.n_heads / a.n_kv_heads;
   const AttnDecodeArgs b = attn_resolve(a);
   if (b.split % ATTN_CHUNK) throw std::runtime_error("attn_decode: split must be a multiple of ATTN_CHUNK");
-  if (a.head_dim == 128) launch_hd<128>(b, G, st);
-  else if (a.head_dim == 64) launch_hd<64>(b, G, st);
-  else throw std::runtime_error("attn_decode: head_dim must be 64 or 128");
+  if (a.head_dim == 128) {
+    if (a.kv_fp8) launch_hd<128, true>(b, G, st);
+    else launch_hd<128, false>(b, G, st);
+  } else if (a.head_dim == 64) {
+    if (a.kv_fp8) launch_hd<64, true>(b, G, st);
+    else launch_hd<64, false>(b, G, st);
+  } else {
+    throw std::runtime_error("attn_decode: head_dim must be 64 or 128");
+  }
 }
 
 }  // namespace aios

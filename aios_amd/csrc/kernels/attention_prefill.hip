@@ -40,7 +40,12 @@ __device__ __forceinline__ float raw_exp2(float x) { return __builtin_amdgcn_exp
 
 constexpr int FP_KT = 64;  // keys per tile
 
-template <int HD, int G>
+typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
+
+// F8: the pool holds fp8 e4m3 codes (EngineConfig::kv_fp8): the tile loads move half the bytes and
+// staging converts them to bf16 with the layer's K / V scale (v_cvt_scalef32_pk_bf16_fp8) -- the LDS
+// tiles and the MFMA math are the bf16 kernel's
+template <int HD, int G, bool F8 = false>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) attn_prefill_kernel(AttnPrefillArgs a) {
   constexpr int BQ = 128 / G;          // query positions per workgroup
   constexpr int KS = HD / 16;          // k-steps of the S MFMA
@@ -111,8 +116,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
   static_assert(KV_BLOCK == 2 * FP_KT, "two prefill key tiles per paged KV block");
   const int maxb = a.max_ctx / KV_BLOCK;
   const size_t blk_stride = (size_t)a.n_kv_heads * KV_BLOCK * HD;
-  const bf16_t* kc = a.k_cache + (size_t)kvh * KV_BLOCK * HD;
-  const bf16_t* vc = a.v_cache + (size_t)kvh * KV_BLOCK * HD;
+  constexpr int ES = F8 ? 1 : 2;  // bytes per cached element
+  const uint8_t* kc = (const uint8_t*)a.k_cache + (size_t)kvh * KV_BLOCK * HD * ES;
+  const uint8_t* vc = (const uint8_t*)a.v_cache + (size_t)kvh * KV_BLOCK * HD * ES;
   const int last_pos = start + min(T, t0 + BQ) - 1;  // highest query position of the block
   const int ntiles = last_pos / FP_KT + 1;
 
@@ -121,8 +127,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
   // memory latency); stage() writes one buffer to an LDS tile buffer
   constexpr int PIECES = FP_KT * HD / 8;  // 16-B pieces per tensor per tile
   constexpr int PPT = PIECES / 256;        // per thread
+  using PT = typename std::conditional<F8, u32x2_t, u32x4_t>::type;  // one 8-element piece
   struct Regs {
-    u32x4_t k[PPT], v[PPT];
+    PT k[PPT], v[PPT];
   };
   const int nt_last = ntiles - 1;
   auto load = [&](Regs& r, int kt) {
@@ -132,9 +139,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
     static_for<PPT>([&](auto I) {
       constexpr int i = decltype(I)::value;
       const int idx = tid + 256 * i, key = idx / (HD / 8), c = idx % (HD / 8);
-      const size_t off = tbase + (size_t)key * HD + c * 8;
-      r.k[i] = *(const u32x4_t*)(kc + off);
-      r.v[i] = *(const u32x4_t*)(vc + off);
+      const size_t off = (tbase + (size_t)key * HD + c * 8) * ES;
+      r.k[i] = *(const PT*)(kc + off);
+      r.v[i] = *(const PT*)(vc + off);
     });
   };
   auto stage = [&](const Regs& r, bf16_t* buf) {
@@ -143,8 +150,21 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
     static_for<PPT>([&](auto I) {
       constexpr int i = decltype(I)::value;
       const int idx = tid + 256 * i, key = idx / (HD / 8), c = idx % (HD / 8);
-      *(u32x4_t*)(sK + key * KROW + c * 8) = r.k[i];
-      *(u32x4_t*)(sV + key * VROW + c * 8) = r.v[i];
+      if constexpr (F8) {
+        auto cv = [](u32x2_t w, float s) {
+          u32x4_t o;
+          o[0] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w[0], s, false));
+          o[1] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w[0], s, true));
+          o[2] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w[1], s, false));
+          o[3] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w[1], s, true));
+          return o;
+        };
+        *(u32x4_t*)(sK + key * KROW + c * 8) = cv(r.k[i], a.kv_scale_k);
+        *(u32x4_t*)(sV + key * VROW + c * 8) = cv(r.v[i], a.kv_scale_v);
+      } else {
+        *(u32x4_t*)(sK + key * KROW + c * 8) = r.k[i];
+        *(u32x4_t*)(sV + key * VROW + c * 8) = r.v[i];
+      }
     });
   };
   // one 64-key tile of math on LDS buffer buf (a tile past the last one -- the odd count's pad --
@@ -271,16 +291,16 @@ bool attn_prefill_supports(int n_heads, int n_kv_heads, int head_dim) {
   return (head_dim == 64 || head_dim == 128) && (G == 1 || G == 2 || G == 4 || G == 8);
 }
 
-template <int HD>
+template <int HD, bool F8>
 static void prefill_hd(const AttnPrefillArgs& a, int G, hipStream_t st) {
   const int BQ = 128 / G;
   dim3 grid((a.T + BQ - 1) / BQ, a.n_kv_heads);
   const size_t lds = (size_t)2 * FP_KT * ((HD + 8) + (HD + 32)) * sizeof(bf16_t);  // two K|V tile buffers
   switch (G) {
-    case 1: hipLaunchKernelGGL((attn_prefill_kernel<HD, 1>), grid, dim3(256), lds, st, a); break;
-    case 2: hipLaunchKernelGGL((attn_prefill_kernel<HD, 2>), grid, dim3(256), lds, st, a); break;
-    case 4: hipLaunchKernelGGL((attn_prefill_kernel<HD, 4>), grid, dim3(256), lds, st, a); break;
-    case 8: hipLaunchKernelGGL((attn_prefill_kernel<HD, 8>), grid, dim3(256), lds, st, a); break;
+    case 1: hipLaunchKernelGGL((attn_prefill_kernel<HD, 1, F8>), grid, dim3(256), lds, st, a); break;
+    case 2: hipLaunchKernelGGL((attn_prefill_kernel<HD, 2, F8>), grid, dim3(256), lds, st, a); break;
+    case 4: hipLaunchKernelGGL((attn_prefill_kernel<HD, 4, F8>), grid, dim3(256), lds, st, a); break;
+    case 8: hipLaunchKernelGGL((attn_prefill_kernel<HD, 8, F8>), grid, dim3(256), lds, st, a); break;
     default: throw std::runtime_error("attn_prefill: unsupported GQA group size");
   }
 }
@@ -291,8 +311,13 @@ void launch_attn_prefill(const AttnPrefillArgs& a, hipStream_t st) {
   if (a.T <= 0) return;
   if (a.start + a.T > a.max_ctx) throw std::runtime_error("attn_prefill: context overflow");
   const int G = a.n_heads / a.n_kv_heads;
-  if (a.head_dim == 128) prefill_hd<128>(a, G, st);
-  else prefill_hd<64>(a, G, st);
+  if (a.head_dim == 128) {
+    if (a.kv_fp8) prefill_hd<128, true>(a, G, st);
+    else prefill_hd<128, false>(a, G, st);
+  } else {
+    if (a.kv_fp8) prefill_hd<64, true>(a, G, st);
+    else prefill_hd<64, false>(a, G, st);
+  }
 }
 
 }  // namespace aios

@@ -82,6 +82,22 @@ __device__ __forceinline__ float dot2_bf16(uint32_t a, uint32_t b, float c) {
   return __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(gbf16x2, a), __builtin_bit_cast(gbf16x2, b), c, false);
 }
 
+typedef unsigned int gu32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint2 ld_nt8(const uint8_t* p) {
+  const gu32x2 v = __builtin_nontemporal_load((const gu32x2*)p);
+  return make_uint2(v[0], v[1]);
+}
+// fp8 KV (OCP e4m3): 2 codes (bytes 2*hi, 2*hi+1 of w) -> a bf16 pair (one v_cvt_scalef32_pk_bf16_fp8)
+template <bool HI>
+__device__ __forceinline__ uint32_t fp8x2_bf16x2(uint32_t w) {
+  return __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w, 1.f, HI));
+}
+// ... -> an fp32 pair (v_cvt_pk_f32_fp8)
+template <bool HI>
+__device__ __forceinline__ gf32x2 fp8x2_f32x2(uint32_t w) {
+  return __builtin_amdgcn_cvt_pk_f32_fp8((int)w, HI);
+}
+
 // One workgroup's share: heads [h0, h0 + G) of KV head kvh, keys of the passes sp, sp + P, ...
 // (P active workgroups per (row, head set); counters indexed by `ci`).  `ppw` = passes per
 // workgroup the split aims for (1: more workgroups, each one 128-key pass; 2: both buffers).
@@ -89,9 +105,14 @@ __device__ __forceinline__ float dot2_bf16(uint32_t a, uint32_t b, float c) {
 // VALU diet (the kernel is VALU-bound per CU once its loads are in flight): q . k runs on
 // v_dot2_f32_bf16 against q pre-rounded to bf16 pairs (4 instructions per 8 dims and head, as the
 // MFMA prefill path rounds q), P . V on packed v_pk_fma_f32 with the probabilities in fp32.
-template <int HD, int G>
+// F8: the pool holds fp8 e4m3 codes (EngineConfig::kv_fp8): half the K / V bytes per pass; a lane's 8
+// dims are 8 bytes, K converted to bf16 pairs for the same v_dot2 (the layer's K scale folded into q),
+// V to fp32 pairs for the P.V FMAs (its V scale applied to the output)
+template <int HD, int G, bool F8 = false>
 __device__ __forceinline__ void attn_core(const AttnDecodeArgs& a, int sp, int kvh, int h0, int ci, int P_max,
                                           int ppw, bool nt = false) {
+  using KVT = typename std::conditional<F8, uint2, uint4>::type;
+  constexpr int ES = F8 ? 1 : 2;  // bytes per cached element
   constexpr int NW = 8;                // waves per workgroup
   constexpr int LPK = HD / 8;          // lanes per key (8 dims per lane)
   constexpr int KPS = 64 / LPK;        // keys per wave-instruction
@@ -124,8 +145,8 @@ __device__ __forceinline__ void attn_core(const AttnDecodeArgs& a, int sp, int k
   const int* btr = a.block_table ? a.block_table + (size_t)(a.bt_rows ? b : slot) * maxb : nullptr;
   const size_t blk_stride = (size_t)a.n_kv_heads * KV_BLOCK * HD;
   const int koff = wave * KPW + ksub;  // this lane's key within a pass (+ s * KPS)
-  const bf16_t* kc = a.k_cache + (size_t)kvh * KV_BLOCK * HD + (size_t)koff * HD + dsl * 8;
-  const bf16_t* vc = a.v_cache + (size_t)kvh * KV_BLOCK * HD + (size_t)koff * HD + dsl * 8;
+  const uint8_t* kc = (const uint8_t*)a.k_cache + ((size_t)kvh * KV_BLOCK * HD + (size_t)koff * HD + dsl * 8) * ES;
+  const uint8_t* vc = (const uint8_t*)a.v_cache + ((size_t)kvh * KV_BLOCK * HD + (size_t)koff * HD + dsl * 8) * ES;
   const int cmax = maxb - 1;           // last chunk with valid memory
 
   const int len = a.seq_len[b];
@@ -135,39 +156,45 @@ __device__ __forceinline__ void attn_core(const AttnDecodeArgs& a, int sp, int k
   stamp(1);
 
   // two passes in flight per workgroup: buffers A and B (static, so they stay in VGPRs)
-  uint4 kA[STEPS], vA[STEPS], kB[STEPS], vB[STEPS];
+  KVT kA[STEPS], vA[STEPS], kB[STEPS], vB[STEPS];
   const bool tail = a.kv_tail != 0;
-  auto issue = [&](uint4 (&kr)[STEPS], uint4 (&vr)[STEPS], int chunk) __attribute__((always_inline)) {
+  auto ld = [&](const uint8_t* p) __attribute__((always_inline)) { return *(const KVT*)p; };
+  auto ld_nt = [&](const uint8_t* p) __attribute__((always_inline)) {
+    if constexpr (F8) return ld_nt8(p);
+    else return ld_nt16((const bf16_t*)p);
+  };
+  auto issue = [&](KVT (&kr)[STEPS], KVT (&vr)[STEPS], int chunk) __attribute__((always_inline)) {
     const int c = min(chunk, cmax);  // clamped: always a mapped block
-    const size_t base = (size_t)(btr ? btr[c] : slot * maxb + c) * blk_stride;
+    const size_t base = (size_t)(btr ? btr[c] : slot * maxb + c) * blk_stride * ES;  // (bytes)
     if (tail && (chunk + 1) * CH > len) {
       // the context's last, partly filled block: only the lanes of live keys load (a 153-key context
       // fetched 2 x 64 KB for 25 keys of its second block); dead keys hold zeros (scores masked, V x 0)
       const int k0 = chunk * CH + koff;
 #pragma unroll
       for (int s = 0; s < STEPS; ++s) {
-        kr[s] = make_uint4(0u, 0u, 0u, 0u);
-        vr[s] = make_uint4(0u, 0u, 0u, 0u);
+        kr[s] = KVT{};
+        vr[s] = KVT{};
         if (k0 + s * KPS < len) {
-          kr[s] = *(const uint4*)(kc + base + (size_t)s * KPS * HD);
-          vr[s] = *(const uint4*)(vc + base + (size_t)s * KPS * HD);
+          kr[s] = ld(kc + base + (size_t)s * KPS * HD * ES);
+          vr[s] = ld(vc + base + (size_t)s * KPS * HD * ES);
         }
       }
     } else if (nt) {  // streaming (nt) policy: K/V lines read once per launch (long mode)
 #pragma unroll
-      for (int s = 0; s < STEPS; ++s) kr[s] = ld_nt16(kc + base + (size_t)s * KPS * HD);
+      for (int s = 0; s < STEPS; ++s) kr[s] = ld_nt(kc + base + (size_t)s * KPS * HD * ES);
 #pragma unroll
-      for (int s = 0; s < STEPS; ++s) vr[s] = ld_nt16(vc + base + (size_t)s * KPS * HD);
+      for (int s = 0; s < STEPS; ++s) vr[s] = ld_nt(vc + base + (size_t)s * KPS * HD * ES);
     } else {
 #pragma unroll
-      for (int s = 0; s < STEPS; ++s) kr[s] = *(const uint4*)(kc + base + (size_t)s * KPS * HD);
+      for (int s = 0; s < STEPS; ++s) kr[s] = ld(kc + base + (size_t)s * KPS * HD * ES);
 #pragma unroll
-      for (int s = 0; s < STEPS; ++s) vr[s] = *(const uint4*)(vc + base + (size_t)s * KPS * HD);
+      for (int s = 0; s < STEPS; ++s) vr[s] = ld(vc + base + (size_t)s * KPS * HD * ES);
     }
   };
   issue(kA, vA, sp);
   if (sp + P < nchunk) issue(kB, vB, sp + P);
-  const float qs = a.scale * kLog2e;  // scores in the log2 domain: exp2 below
+  const float qs = a.scale * kLog2e * (F8 ? a.kv_scale_k : 1.f);  // scores in the log2 domain: exp2 below
+  const float vs = F8 ? a.kv_scale_v : 1.f;                         // (fp8: V's scale, on the output)
   uint32_t q2[G][4];                  // q * scale as bf16 pairs
 #pragma unroll
   for (int g = 0; g < G; ++g) {
@@ -188,18 +215,25 @@ __device__ __forceinline__ void attn_core(const AttnDecodeArgs& a, int sp, int k
 #pragma unroll
     for (int i = 0; i < 4; ++i) o[g][i] = gf32x2{0.f, 0.f};
   }
-  auto pass = [&](const uint4 (&kr)[STEPS], const uint4 (&vr)[STEPS], int c) __attribute__((always_inline)) {
+  auto pass = [&](const KVT (&kr)[STEPS], const KVT (&vr)[STEPS], int c) __attribute__((always_inline)) {
     // ---- scores of this lane's STEPS keys for the G heads (reduced over the key's LPK lanes)
     float sc[STEPS][G];
 #pragma unroll
     for (int s = 0; s < STEPS; ++s) {
       const bool valid = c * CH + koff + s * KPS < len;
+      uint32_t kb[4];
+      if constexpr (F8) {
+        kb[0] = fp8x2_bf16x2<false>(kr[s].x); kb[1] = fp8x2_bf16x2<true>(kr[s].x);
+        kb[2] = fp8x2_bf16x2<false>(kr[s].y); kb[3] = fp8x2_bf16x2<true>(kr[s].y);
+      } else {
+        kb[0] = kr[s].x; kb[1] = kr[s].y; kb[2] = kr[s].z; kb[3] = kr[s].w;
+      }
 #pragma unroll
       for (int g = 0; g < G; ++g) {
-        float d = dot2_bf16(kr[s].x, q2[g][0], 0.f);
-        d = dot2_bf16(kr[s].y, q2[g][1], d);
-        d = dot2_bf16(kr[s].z, q2[g][2], d);
-        d = dot2_bf16(kr[s].w, q2[g][3], d);
+        float d = dot2_bf16(kb[0], q2[g][0], 0.f);
+        d = dot2_bf16(kb[1], q2[g][1], d);
+        d = dot2_bf16(kb[2], q2[g][2], d);
+        d = dot2_bf16(kb[3], q2[g][3], d);
         d = group_sum<LPK>(d);
         sc[s][g] = valid ? d : kNeg;
       }
@@ -228,10 +262,15 @@ __device__ __forceinline__ void attn_core(const AttnDecodeArgs& a, int sp, int k
     // ---- P.V (lane-local over its keys; merged across key groups and waves at the end)
 #pragma unroll
     for (int s = 0; s < STEPS; ++s) {
-      const uint32_t w[4] = {vr[s].x, vr[s].y, vr[s].z, vr[s].w};
       gf32x2 vf[4];
+      if constexpr (F8) {
+        vf[0] = fp8x2_f32x2<false>(vr[s].x); vf[1] = fp8x2_f32x2<true>(vr[s].x);
+        vf[2] = fp8x2_f32x2<false>(vr[s].y); vf[3] = fp8x2_f32x2<true>(vr[s].y);
+      } else {
+        const uint32_t w[4] = {vr[s].x, vr[s].y, vr[s].z, vr[s].w};
 #pragma unroll
-      for (int i = 0; i < 4; ++i) vf[i] = gf32x2{__uint_as_float(w[i] << 16), __uint_as_float(w[i] & 0xffff0000u)};
+        for (int i = 0; i < 4; ++i) vf[i] = gf32x2{__uint_as_float(w[i] << 16), __uint_as_float(w[i] & 0xffff0000u)};
+      }
 #pragma unroll
       for (int g = 0; g < G; ++g) {
         const gf32x2 pp = gf32x2{sc[s][g], sc[s][g]};
@@ -291,6 +330,7 @@ __device__ __forceinline__ void attn_core(const AttnDecodeArgs& a, int sp, int k
       acc += sw * s_o[w][g][d];
     }
     const int h = h0 + g;
+    if (F8) acc *= vs;
     if (nact == 1) {
       if (a.out16) a.out16[((size_t)b * a.n_heads + h) * HD + d] = f32_to_bf16(acc / L);
       else if (a.out_wt) st_wt(a.out + ((size_t)b * a.n_heads + h) * HD + d, acc / L);
@@ -447,7 +487,7 @@ struct AttnSplit {
 
 // workgroup wg's role in the flat grid (see attn_decode_kernel, attention.hip); returns with the
 // whole workgroup (every early exit inside is workgroup-uniform)
-template <int HD, int G>
+template <int HD, int G, bool F8 = false>
 __device__ __forceinline__ void attn_role(const AttnDecodeArgs& a, const AttnSplit& sp_, int wg) {
   const int len = a.seq_len[blockIdx.z];
   if (G > 1 && len <= a.short_len) {
@@ -466,7 +506,7 @@ __device__ __forceinline__ void attn_role(const AttnDecodeArgs& a, const AttnSpl
       sp = wg % sp_.p_short;
     }
     if (h >= a.n_heads) return;
-    attn_core<HD, 1>(a, sp, h / G, h, h, sp_.p_short, sp_.ppw);
+    attn_core<HD, 1, F8>(a, sp, h / G, h, h, sp_.p_short, sp_.ppw);
   } else {
     constexpr int GL = AttnGL<G>::value;
     const int hsi = wg / sp_.p_long, sp = wg % sp_.p_long;
@@ -474,7 +514,7 @@ __device__ __forceinline__ void attn_role(const AttnDecodeArgs& a, const AttnSpl
     const int kvh = hsi / (G / GL), h0 = kvh * G + (hsi % (G / GL)) * GL;
     // long mode: every K/V line is read by exactly one workgroup -> streaming loads (round 4,
     // same box: --prompt 4000 546.9 -> 567.0 tok/s, 16000 467.6 -> 487.3)
-    attn_core<HD, GL>(a, sp, kvh, h0, h0, sp_.p_long, sp_.ppw, a.kv_nt != 0);
+    attn_core<HD, GL, F8>(a, sp, kvh, h0, h0, sp_.p_long, sp_.ppw, a.kv_nt != 0);
   }
 }
 

@@ -202,12 +202,7 @@ __global__ void __launch_bounds__(256) qkv_post_kernel(QkvPostArgs a) {
     } else {
       bf16_t* cache = part == 1 ? a.k_cache : a.v_cache;
       const size_t base = kv_offset(a.block_table, a.max_ctx / KV_BLOCK, slot, a.n_kv_heads, head, pos, hd);
-      if (ib == ia + 1) {
-        *(uint32_t*)(cache + base + ia) = (uint32_t)f32_to_bf16(v0) | ((uint32_t)f32_to_bf16(v1) << 16);
-      } else {
-        cache[base + ia] = f32_to_bf16(v0);
-        cache[base + ib] = f32_to_bf16(v1);
-      }
+      kv_store_pair(cache, base + ia, base + ib, v0, v1, a.kv_fp8, part == 1 ? a.kv_inv_k : a.kv_inv_v);
     }
   }
 }
@@ -254,8 +249,8 @@ __global__ void __launch_bounds__(256) qkv_post_row_kernel(QkvPostArgs a) {
         *(float2*)(a.q_out + (size_t)t * qd + c) = make_float2(v0, v1);
       } else {
         bf16_t* cache = part == 1 ? a.k_cache : a.v_cache;
-        *(uint32_t*)(cache + kvbase + (size_t)head * KV_BLOCK * hd + lr) =
-            (uint32_t)f32_to_bf16(v0) | ((uint32_t)f32_to_bf16(v1) << 16);
+        const size_t i0 = kvbase + (size_t)head * KV_BLOCK * hd + lr;
+        kv_store_pair(cache, i0, i0 + 1, v0, v1, a.kv_fp8, part == 1 ? a.kv_inv_k : a.kv_inv_v);
       }
     }
   }

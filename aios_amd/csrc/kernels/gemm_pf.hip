@@ -179,7 +179,7 @@ bool launch_gemm_pf(const GemmQArgs& a, hipStream_t st) {
 static bool pf_eligible(const GemmQArgs& a) {
   if (a.nseg < 1 || a.M < 1) return false;
   if (a.epi != GEPI_STORE && a.epi != GEPI_ACCUM && a.epi != GEPI_SWIGLU_BF16 && a.epi != GEPI_QKV) return false;
-  if (a.epi == GEPI_QKV && (a.col0 != 0 || !a.q_out || !a.k_cache || !a.v_cache || !a.pos || !a.rope_cs ||
+  if (a.epi == GEPI_QKV && (a.kv_fp8 || a.col0 != 0 || !a.q_out || !a.k_cache || !a.v_cache || !a.pos || !a.rope_cs ||
                             a.head_dim % 2 || a.N != a.q_dim + 2 * a.kv_dim))
     return false;
   if (a.nrm_in || a.lda % 8 || ((uintptr_t)a.A & 15)) return false;

@@ -183,8 +183,7 @@ __device__ __forceinline__ void cu_qkv_epilogue(const GemvArgs& a, int grow, flo
   } else {
     bf16_t* cache = pick_ptr(part == 1, a.k_cache, a.v_cache);
     const size_t base = (((size_t)kv_blk0 * a.n_kv_heads + head) * KV_BLOCK + (pos0 % KV_BLOCK)) * hd;
-    cache[base + da] = f32_to_bf16(v0);
-    cache[base + db] = f32_to_bf16(v1);
+    kv_store_pair(cache, base + da, base + db, v0, v1, a.kv_fp8, part == 1 ? a.kv_inv_k : a.kv_inv_v);
   }
 }
 

@@ -16,11 +16,15 @@
 #pragma once
 // (included inside namespace aios by gemv_impl.h)
 
-constexpr int LB_GPW = 2;                   // groups per consumer wave per step (one per half-wave)
-constexpr int LB_NGS = LG_NG * LB_GPW;      // groups per slot
-constexpr int LB_SLOT = LB_NGS * 1024;      // 28 KB
-constexpr int LB_PL = LB_NGS / LG_NL;       // DMA instructions per loader wave per slot
-static_assert(LB_NGS % LG_NL == 0, "every loader issues the same count per slot");
+// slot geometry: GPW groups per consumer wave per step (2: one per half-wave, 28 KB slots; 1: one
+// per wave, 14 KB slots -- a smaller prologue burst, a deeper ring for the same LDS)
+template <int GPW>
+struct LbSlot {
+  static constexpr int NGS = LG_NG * GPW;   // groups per slot
+  static constexpr int BYTES = NGS * 1024;
+  static constexpr int PL = NGS / LG_NL;    // DMA instructions per loader wave per slot
+  static_assert(NGS % LG_NL == 0, "every loader issues the same count per slot");
+};
 
 typedef __bf16 lb_bf16x2 __attribute__((ext_vector_type(2)));
 
@@ -42,8 +46,10 @@ __device__ __forceinline__ uint32_t lb_pk(float a, float b) {
 // group gw0 + s * NGS + i (clamped to the last one: the tail slot re-reads it into unused space);
 // loader lw issues i = lw, lw + NL, ...  The group index is wave-uniform, so the segment select is
 // scalar and the only per-lane address term is lane * 16.
+template <int GPW>
 __device__ __forceinline__ void lb_dma_slot(const GemvArgs& a, uint8_t* dst, int s, int lw, int gw0, int glast,
                                             int nit) {
+  constexpr int LB_NGS = LbSlot<GPW>::NGS, LB_PL = LbSlot<GPW>::PL;
   const int lane = threadIdx.x & 63;
   const int G1 = a.nseg > 1 ? a.seg_row0[1] * nit : 0x7fffffff;
   const int G2 = a.nseg > 2 ? a.seg_row0[2] * nit : 0x7fffffff;
@@ -106,9 +112,10 @@ __device__ __forceinline__ void lb_stage(const GemvArgs& a, uint16_t* xs, float*
   }
 }
 
-template <int B, int R>
+template <int B, int R, int GPW = 2>
 __global__ void __launch_bounds__(LG_THREADS) gemv_lds16(GemvArgs a, CuPlan pl) {
   kernarg_warm<sizeof(GemvArgs) + sizeof(CuPlan)>();
+  constexpr int LB_NGS = LbSlot<GPW>::NGS, LB_SLOT = LbSlot<GPW>::BYTES, LB_PL = LbSlot<GPW>::PL, LB_GPW = GPW;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int nit = a.K >> 9;  // 1 KB groups per row
   const int npairs = a.N >> 1;
@@ -136,13 +143,13 @@ __global__ void __launch_bounds__(LG_THREADS) gemv_lds16(GemvArgs a, CuPlan pl) 
     const int lw = wave - LG_NG;
     const int gw0 = r0 * nit, glast = gw0 + ngroups - 1;
     const int npro = min(T, R - 1);
-    for (int s = 0; s < npro; ++s) lb_dma_slot(a, ring + (size_t)s * LB_SLOT, s, lw, gw0, glast, nit);
+    for (int s = 0; s < npro; ++s) lb_dma_slot<GPW>(a, ring + (size_t)s * LB_SLOT, s, lw, gw0, glast, nit);
     if (npro == R - 1) lg_vmcnt<(R - 2) * LB_PL>();
     else lg_vmcnt<0>();
     lg_barrier();  // B1: slot 0 landed, x staged
     for (int t = 0; t < T; ++t) {
       if (t + R - 1 < T) {
-        lb_dma_slot(a, ring + (size_t)((t + R - 1) % R) * LB_SLOT, t + R - 1, lw, gw0, glast, nit);
+        lb_dma_slot<GPW>(a, ring + (size_t)((t + R - 1) % R) * LB_SLOT, t + R - 1, lw, gw0, glast, nit);
         lg_vmcnt<(R - 2) * LB_PL>();  // slot t + 1 landed
       } else {
         lg_vmcnt<0>();
@@ -168,7 +175,37 @@ __global__ void __launch_bounds__(LG_THREADS) gemv_lds16(GemvArgs a, CuPlan pl) 
   lb_stage<B>(a, xs, red);
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   lg_barrier();  // B1
-  {
+  if constexpr (GPW == 1) {
+    // one group per wave: lane p takes 16 B (cols p * 8 of the group's 512), a full-wave row sum
+    const int kk = wave;
+    const int dq = LB_NGS / nit, dr = LB_NGS - dq * nit;
+    int row = kk / nit, it = kk - row * nit;
+    for (int t = 0; t < T; ++t) {
+      const int gg = t * LB_NGS + kk;
+      if (gg < ngroups) {
+        const uint4 w0 = *(const uint4*)(ring + (size_t)(t % R) * LB_SLOT + kk * 1024 + lane * 16);
+        const int col = it * 512 + lane * 8;
+        float v[B];
+#pragma unroll
+        for (int b = 0; b < B; ++b) v[b] = lb_dot8(w0, *(const uint4*)(xs + (size_t)b * a.K + col), 0.f);
+        if constexpr (B == 1) {
+          const float r = cu_wave_sum(v[0]);
+          if (lane == 0) __hip_atomic_fetch_add(&rowacc[row], r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        } else {
+          float r = lg_half_sum_rows<B>(v, lane & 31);
+          const auto h = __builtin_amdgcn_permlane32_swap(__float_as_uint(r), __float_as_uint(r), false, false);
+          r = __uint_as_float(h[0]) + __uint_as_float(h[1]);  // both 32-lane halves
+          const int rb = lg_half_row<B>(lane & 31);
+          if (lane < (B > 2 ? 4 : 2) && rb < B)
+            __hip_atomic_fetch_add(&rowacc[rb * pl.racc_n + row], r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+      }
+      row += dq;
+      it += dr;
+      if (it >= nit) { it -= nit; ++row; }
+      lg_barrier();
+    }
+  } else {
     const int half = lane >> 5, p = lane & 31;
     const int kk = wave * LB_GPW + half;  // this half-wave's group within a slot
     // (row, column group) of group t * NGS + kk, advanced by NGS per step without a division
@@ -267,10 +304,10 @@ __global__ void __launch_bounds__(LG_THREADS) gemv_lds16(GemvArgs a, CuPlan pl) 
   }
 }
 
-template <int B, int R>
+template <int B, int R, int GPW = 2>
 size_t lb_lds_bytes(const GemvArgs& a, const CuPlan& pl) {
   const size_t head = (64 + (size_t)B * pl.racc_n) * 4 + (size_t)B * a.K * 2;
-  return (head + 255) / 256 * 256 + (size_t)R * LB_SLOT;
+  return (head + 255) / 256 * 256 + (size_t)R * LbSlot<GPW>::BYTES;
 }
 
 // The BF16 engine for B = 1..4, or false (shape / epilogue outside it: the register kernels run).
@@ -289,6 +326,26 @@ inline bool launch_gemv_lds16(const GemvArgs& a, hipStream_t st, bool dry = fals
   constexpr size_t LDS_MAX = 160 * 1024;
   // R = 3 (two 28 KB slots in flight per CU, the quantised engine's batch-1 depth), R = 2 where the
   // staged x rows leave no room (long K at B = 3..4)
+  // AIOS_LB_CFG (batch 1 only): slot geometry x ring depth -- 23 = 28 KB slots x 3 (default),
+  // 24 = 28 KB x 4, 14 = 14 KB x 4, 16 = 14 KB x 6 (profiles/decode_tinyllama_bf16_rocprof_r6.txt)
+  static const int cfg = [] {
+    const char* e = std::getenv("AIOS_LB_CFG");
+    return e ? std::atoi(e) : 23;
+  }();
+  if (a.B == 1 && cfg != 23) {
+    auto b1 = [&](auto gp, auto rr) -> bool {
+      constexpr int GP = decltype(gp)::value, RR = decltype(rr)::value;
+      const size_t lds = lb_lds_bytes<1, RR, GP>(a, pl);
+      if (lds > LDS_MAX) return false;
+      if (!dry) hipLaunchKernelGGL((gemv_lds16<1, RR, GP>), dim3(G), dim3(LG_THREADS), lds, st, a, pl);
+      return true;
+    };
+    using I = std::integral_constant<int, 1>;
+    using II = std::integral_constant<int, 2>;
+    if (cfg == 24 && b1(II{}, std::integral_constant<int, 4>{})) return true;
+    if (cfg == 14 && b1(I{}, std::integral_constant<int, 4>{})) return true;
+    if (cfg == 16 && b1(I{}, std::integral_constant<int, 6>{})) return true;
+  }
   auto go = [&](auto bt) -> bool {
     constexpr int BB = decltype(bt)::value;
     size_t lds = lb_lds_bytes<BB, 3>(a, pl);

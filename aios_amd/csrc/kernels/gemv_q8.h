@@ -508,12 +508,8 @@ __device__ __forceinline__ void gemv_epilogue1(const GemvArgs& a, int grow, floa
         bf16_t* cache = pick_ptr(part == 1, a.k_cache, a.v_cache);
         // kv_blk0: the physical block of (slot, pos), looked up once behind the first weight loads
         const size_t base = (((size_t)kv_blk0 * a.n_kv_heads + head) * KV_BLOCK + (pos0 % KV_BLOCK)) * hd;
-        if (db == da + 1) {  // adjacent pair (V rows, non-NeoX RoPE): one 4-byte store
-          *(uint32_t*)(cache + base + da) = (uint32_t)f32_to_bf16(v0) | ((uint32_t)f32_to_bf16(v1) << 16);
-        } else {
-          cache[base + da] = f32_to_bf16(v0);
-          cache[base + db] = f32_to_bf16(v1);
-        }
+        // (adjacent pair -- V rows, non-NeoX RoPE: one store)
+        kv_store_pair(cache, base + da, base + db, v0, v1, a.kv_fp8, part == 1 ? a.kv_inv_k : a.kv_inv_v);
       }
     } break;
     default:

@@ -53,7 +53,8 @@ __device__ __forceinline__ bool sk_epilogue(const GemmQArgs& a, gf32x4 (&acc)[MT
         } else {
           bf16_t* cache = part == 1 ? a.k_cache : a.v_cache;
           const size_t base = kv_offset(a.block_table, a.max_ctx / KV_BLOCK, slot, a.n_kv_heads, head, pos, hd);
-          *(uint32_t*)(cache + base + lr) = pk_bf16(v0, v1);
+          if (a.kv_fp8) kv_store_pair(cache, base + lr, base + lr + 1, v0, v1, 1, part == 1 ? a.kv_inv_k : a.kv_inv_v);
+          else *(uint32_t*)(cache + base + lr) = pk_bf16(v0, v1);
         }
       }
     } else {

@@ -85,6 +85,8 @@ struct QkvPostArgs {
   bf16_t* v_cache;
   int max_ctx;
   const int* block_table = nullptr;  // [slots][max_ctx / KV_BLOCK] or null (identity)
+  int kv_fp8 = 0;    // fp8 e4m3 pool: code = value * kv_inv_{k,v}
+  float kv_inv_k = 1.f, kv_inv_v = 1.f;
 };
 void launch_qkv_post(const QkvPostArgs& a, hipStream_t st);
 
@@ -111,17 +113,13 @@ struct AttnDecodeArgs {
   int kv_nt = -1;          // long mode: K/V loads with the streaming (nt) policy (-1: AIOS_ATTN_NT, default 1)
   int kv_tail = -1;        // last partial block: loads only for live keys (-1: AIOS_ATTN_TAIL, default 1)
   int combine_trips = 0;   // split-K combine: 0 = launcher (AIOS_ATTN_COMBINE, default one round trip), 2 = two
-  int out_wt = 0;          // fp32 out with write-through (agent-scope) stores: read in the same launch (attn_o.hip)
+  int out_wt = 0;          // fp32 out with write-through (agent-scope) stores
+  int kv_fp8 = 0;          // fp8 e4m3 pool: value = code * kv_scale_{k,v}
+  float kv_scale_k = 1.f, kv_scale_v = 1.f;
 };
 constexpr int ATTN_CHUNK = 64;
 void launch_attn_decode(const AttnDecodeArgs& a, hipStream_t st);
 struct GemvArgs;
-// batch 1: attention then the O GEMV reading its output, as one launch (kernels/attn_o.hip); false
-// (nothing launched) outside the shapes it serves.  cnt: this launch's counter block
-// (ATTN_O_CNT_INTS ints, zero on entry); rearm: the block of the launch before it in a fixed cycle,
-// zeroed here; xloc: per-XCD copies of the attention output (8 x n_heads x head_dim floats).
-constexpr int ATTN_O_CSTRIDE = 32, ATTN_O_CNT_INTS = 1024;
-bool launch_attn_o(const AttnDecodeArgs& a, const GemvArgs& g, int* cnt, int* rearm, float* xloc, hipStream_t st);
 int attn_decode_split(int max_ctx, int B, int n_kv_heads);
 
 // causal flash attention for a prefill chunk of T tokens at positions [start, start+T) of one
@@ -136,6 +134,8 @@ struct AttnPrefillArgs {
   float scale;
   bf16_t* out;             // [T][ldo] bf16
   int ldo;
+  int kv_fp8 = 0;          // fp8 e4m3 pool: value = code * kv_scale_{k,v}
+  float kv_scale_k = 1.f, kv_scale_v = 1.f;
 };
 void launch_attn_prefill(const AttnPrefillArgs& a, hipStream_t st);
 bool attn_prefill_supports(int n_heads, int n_kv_heads, int head_dim);  // keys per workgroup the launcher picks
@@ -220,6 +220,8 @@ struct GemmQArgs {
   float* q_out;
   bf16_t* k_cache;
   bf16_t* v_cache;
+  int kv_fp8;        // fp8 e4m3 pool: code = value * kv_inv_{k,v}
+  float kv_inv_k, kv_inv_v;
   // RMSNorm split across two skinny GEMMs (batched decode: no normalisation launch).
   //  producer (GEPI_ACCUM_NORM = residual add): also writes bf16(x_new * nrm_g) to nrm_out16
   //    [M][ldc] and, per output tile t, sum_n x_new[m][n]^2 to nrm_part[m * nrm_parts + t]

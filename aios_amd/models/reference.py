@@ -20,16 +20,22 @@ from .config import ROPE_NEOX, ModelConfig
 
 class ReferenceModel:
     def __init__(self, cfg: ModelConfig, weights: Dict[str, torch.Tensor], kv_bf16: bool = False,
-                 device: str = "cpu", act_q8: bool = False, quantized: Optional[set] = None):
+                 device: str = "cpu", act_q8: bool = False, quantized: Optional[set] = None, kv_fp8: bool = False,
+                 kv_scales: Optional[list] = None):
         self.cfg = cfg
         self.w = weights
         self.kv_bf16 = kv_bf16
+        # the engine's fp8 KV cache (EngineConfig::kv_fp8): K / V rounded to OCP e4m3 (saturating at
+        # 448) after division by the layer's scale (kv_scales: [K0, V0, K1, V1, ...], default 1)
+        self.kv_fp8 = kv_fp8
+        self.kv_scales = kv_scales
         self.device = device
         self.act_q8 = act_q8                     # emulate the engine's int8 activation path
         self.quantized = quantized or set()      # weight names stored in a block-quant format
 
     @classmethod
-    def from_gguf(cls, path: str, kv_bf16: bool = False, device: str = "cpu", act_q8: bool = False) -> "ReferenceModel":
+    def from_gguf(cls, path: str, kv_bf16: bool = False, device: str = "cpu", act_q8: bool = False,
+                  kv_fp8: bool = False, kv_scales: Optional[list] = None) -> "ReferenceModel":
         from ..gguf.quants import GGMLType
 
         r = GGUFReader(path)
@@ -41,7 +47,13 @@ class ReferenceModel:
             if ti.ggml_type not in (GGMLType.F32, GGMLType.F16, GGMLType.BF16):
                 quant.add(name)
         r.close()
-        return cls(cfg, w, kv_bf16=kv_bf16, device=device, act_q8=act_q8, quantized=quant)
+        return cls(cfg, w, kv_bf16=kv_bf16, device=device, act_q8=act_q8, quantized=quant, kv_fp8=kv_fp8,
+                   kv_scales=kv_scales)
+
+    @staticmethod
+    def fp8(x: torch.Tensor, scale: float = 1.0) -> torch.Tensor:
+        """OCP e4m3 round trip (round-to-nearest-even, saturating at +-448) of x / scale, times scale."""
+        return (x / scale).clamp(-448.0, 448.0).to(torch.float8_e4m3fn).to(torch.float32) * scale
 
     @staticmethod
     def q8(x: torch.Tensor) -> torch.Tensor:
@@ -112,7 +124,11 @@ class ReferenceModel:
                 k = self._rms(k, self.w[p + "attn_k_norm.weight"])
             q = self._rope(q, pos)
             k = self._rope(k, pos)
-            if self.kv_bf16:
+            if self.kv_fp8:
+                sk, sv = (self.kv_scales[2 * l], self.kv_scales[2 * l + 1]) if self.kv_scales else (1.0, 1.0)
+                k = self.fp8(k, sk)
+                v = self.fp8(v, sv)
+            elif self.kv_bf16:
                 k = k.to(torch.bfloat16).to(torch.float32)
                 v = v.to(torch.bfloat16).to(torch.float32)
             if cache["k"][l] is not None:

@@ -424,9 +424,19 @@ def env_rank_world():
 
 
 # ------------------------------------------------------------------------------ runtime launcher
+def spec_kv_dtype(path: str) -> str:
+    """the '#...&kv=fp8_e4m3' fragment of a model spec (default: AIOS_KV_DTYPE, else bf16)"""
+    for kv in filter(None, path.partition("#")[2].split("&")):
+        k, _, v = kv.partition("=")
+        if k == "kv":
+            return v
+    return os.environ.get("AIOS_KV_DTYPE", "bf16")
+
+
 def parse_spec(path: str):
     """'synthetic:<preset>[:<recipe>]#tp=N&q8=0' or '<file.gguf>#tp=N' -> (base, tp, act_q8).
-    q8=0 selects fp32 activations in the GEMVs (int8 activations are the default)."""
+    q8=0 selects fp32 activations in the GEMVs (int8 activations are the default); kv=fp8_e4m3 the
+    fp8 KV cache (spec_kv_dtype)."""
     base, _, frag = path.partition("#")
     tp, q8 = 1, True
     for kv in filter(None, frag.split("&")):
@@ -439,7 +449,7 @@ def parse_spec(path: str):
 
 
 def _shard(spec: str, rank: int, world: int, device: int, max_ctx: int, max_slots: int, max_batch: int, seed: int,
-           act_q8: bool = True):
+           act_q8: bool = True, kv_dtype: str = "bf16"):
     from ..models.config import get_preset
     from ..runtime.loader import load_engine, random_engine
 
@@ -448,15 +458,15 @@ def _shard(spec: str, rank: int, world: int, device: int, max_ctx: int, max_slot
         cfg = get_preset(parts[1])
         eng = random_engine(cfg, parts[2] if len(parts) > 2 else "Q4_K_M", seed=seed, max_ctx=max_ctx,
                             max_slots=max_slots, max_batch=max_batch, device=device, tp_rank=rank, tp_size=world,
-                            act_q8=act_q8)
+                            act_q8=act_q8, kv_dtype=kv_dtype)
         return eng, cfg
     eng, cfg, _ = load_engine(spec, max_ctx=max_ctx, max_slots=max_slots, max_batch=max_batch, device=device,
-                              tp_rank=rank, tp_size=world, act_q8=act_q8)
+                              tp_rank=rank, tp_size=world, act_q8=act_q8, kv_dtype=kv_dtype)
     return eng, cfg
 
 
 def launch_tp(spec: str, world: int, devices, max_ctx: int, max_slots: int, max_batch: int, seed: int = 0,
-              act_q8: bool = True):
+              act_q8: bool = True, kv_dtype: str = "bf16"):
     """Runtime-side TP model: spawn ranks 1..N-1 as worker processes (python -m
     aios_amd.parallel.worker), build rank 0 here, exchange IPC handles over the channel.
     Returns (TPEngine, cfg)."""
@@ -477,10 +487,11 @@ def launch_tp(spec: str, world: int, devices, max_ctx: int, max_slots: int, max_
                                        "--rank", str(r), "--world", str(world), "--device",
                                        str(devices[r % len(devices)]), "--spec", spec, "--max-ctx", str(max_ctx),
                                        "--max-slots", str(max_slots), "--max-batch", str(max_batch),
-                                       "--seed", str(seed), "--q8", "1" if act_q8 else "0"], env=env))
+                                       "--seed", str(seed), "--q8", "1" if act_q8 else "0", "--kv", kv_dtype],
+                                      env=env))
     try:
         ch.accept_all()
-        eng, cfg = _shard(spec, 0, world, devices[0], max_ctx, max_slots, max_batch, seed, act_q8)
+        eng, cfg = _shard(spec, 0, world, devices[0], max_ctx, max_slots, max_batch, seed, act_q8, kv_dtype)
         if comm_kind() == "rccl":
             uid = native.require().RcclComm.unique_id()
             ch.broadcast(uid)

@@ -18,6 +18,7 @@ def main(argv=None):
     ap.add_argument("--max-batch", type=int, default=8)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--q8", type=int, default=1)
+    ap.add_argument("--kv", default="bf16")
     a = ap.parse_args(argv)
     logging.basicConfig(level=os.environ.get("AIOS_LOG", "INFO"))
     import torch  # noqa: F401  (loads the HIP runtime the extension links against)
@@ -28,7 +29,8 @@ def main(argv=None):
                      worker_loop, xgmi_handshake)
 
     ch = WorkerChannel(a.leader, a.rank, os.environ.pop("AIOS_TP_TOKEN", ""))
-    eng, cfg = _shard(a.spec, a.rank, a.world, a.device, a.max_ctx, a.max_slots, a.max_batch, a.seed, bool(a.q8))
+    eng, cfg = _shard(a.spec, a.rank, a.world, a.device, a.max_ctx, a.max_slots, a.max_batch, a.seed, bool(a.q8),
+                      a.kv)
     if comm_kind() == "rccl":  # the leader broadcasts the ncclUniqueId; the init is collective
         comm = native.require().RcclComm(a.rank, a.world, a.device, ch.recv())
     else:

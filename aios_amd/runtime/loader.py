@@ -57,7 +57,7 @@ def shard_tensor(name: str, raw: np.ndarray, ggml_type: int, rows: int, cols: in
 
 def load_engine(path: str, max_ctx: Optional[int] = None, max_slots: int = 4, max_batch: int = 8, device: int = 0,
                 tp_rank: int = 0, tp_size: int = 1, name: Optional[str] = None, verbose: bool = False,
-                act_q8: bool = True):
+                act_q8: bool = True, cu_mask: Optional[list] = None, kv_dtype: str = "bf16"):
     """Load a GGUF file into a native Engine on `device`. Returns (engine, ModelConfig, reader)."""
     m = native.require()
     t0 = time.time()
@@ -65,7 +65,7 @@ def load_engine(path: str, max_ctx: Optional[int] = None, max_slots: int = 4, ma
     cfg = ModelConfig.from_gguf(r, name=name)
     ec = native.engine_config(cfg, max_ctx=max_ctx or min(cfg.max_ctx, 4096), max_slots=max_slots,
                               max_batch=max_batch, device=device, tp_rank=tp_rank, tp_size=tp_size,
-                              act_q8=act_q8)
+                              act_q8=act_q8, cu_mask=cu_mask, kv_dtype=kv_dtype)
     eng = m.Engine(ec)
     vp = bool(ec.vocab_parallel)
     for tname, ti in r.tensors.items():
@@ -108,12 +108,13 @@ def finalize(eng):
 
 def random_engine(cfg: ModelConfig, recipe: str = "Q4_K_M", seed: int = 0, max_ctx: Optional[int] = None,
                   max_slots: int = 4, max_batch: int = 8, device: int = 0, tp_rank: int = 0, tp_size: int = 1,
-                  act_q8: bool = True):
-    """Engine with random-init weights of `cfg`'s architecture generated directly in HBM."""
+                  act_q8: bool = True, cu_mask: Optional[list] = None, kv_dtype: str = "bf16"):
+    """Engine with random-init weights of `cfg`'s architecture generated directly in HBM (cu_mask: the
+    CUs its stream may use, native.cu_mask_words)."""
     m = native.require()
     ec = native.engine_config(cfg, max_ctx=max_ctx or min(cfg.max_ctx, 4096), max_slots=max_slots,
                               max_batch=max_batch, device=device, tp_rank=tp_rank, tp_size=tp_size,
-                              act_q8=act_q8)
+                              act_q8=act_q8, cu_mask=cu_mask, kv_dtype=kv_dtype)
     eng = m.Engine(ec)
     eng.init_random(recipe, seed)
     finalize(eng)

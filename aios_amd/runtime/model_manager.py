@@ -187,11 +187,12 @@ class ModelManager:
         from .tokenizer import SpmTokenizer, from_gguf
 
         E = native.require()
-        from ..parallel.tp import launch_tp, parse_spec
+        from ..parallel.tp import launch_tp, parse_spec, spec_kv_dtype
 
         device = self.device if m.device < 0 else m.device
 
         base, tp, act_q8 = parse_spec(m.path)
+        kv_dtype = spec_kv_dtype(m.path)
         faults = FaultSpec.from_env(m.name)
         if faults is not None:
             faults.check("load")
@@ -208,7 +209,7 @@ class ModelManager:
                     context_length = context_for_size(os.path.getsize(base)) if os.path.exists(base) else 8192
             ctx = context_length
             eng, cfg = launch_tp(base, tp, self.tp_devices(), ctx, self.max_slots, self.max_batch,
-                                 seed=_synth_seed(m.name), act_q8=act_q8)
+                                 seed=_synth_seed(m.name), act_q8=act_q8, kv_dtype=kv_dtype)
             if base.startswith("synthetic:"):
                 toks, scores, types = synthetic_vocab(cfg.vocab_size)
                 tok = SpmTokenizer(toks, scores, types, cfg.bos_id, cfg.eos_id)
@@ -224,7 +225,8 @@ class ModelManager:
             recipe = parts[2] if len(parts) > 2 else "Q4_K_M"
             ctx = context_length or tier_context(cfg)
             eng = random_engine(cfg, recipe, seed=_synth_seed(m.group or m.name), max_ctx=ctx,
-                                max_slots=self.max_slots, max_batch=self.max_batch, device=device, act_q8=act_q8)
+                                max_slots=self.max_slots, max_batch=self.max_batch, device=device, act_q8=act_q8,
+                                kv_dtype=kv_dtype)
             toks, scores, types = synthetic_vocab(cfg.vocab_size)
             tok = SpmTokenizer(toks, scores, types, cfg.bos_id, cfg.eos_id)
             tmpl = chat_template.for_model(cfg.chat_template if cfg.chat_template in chat_template.BUILTIN else "zephyr",
@@ -234,7 +236,7 @@ class ModelManager:
                 raise FileNotFoundError(base)
             ctx = context_length or context_for_size(os.path.getsize(base))
             eng, cfg, reader = load_engine(base, max_ctx=ctx, max_slots=self.max_slots, max_batch=self.max_batch,
-                                           device=device, name=m.name, act_q8=act_q8)
+                                           device=device, name=m.name, act_q8=act_q8, kv_dtype=kv_dtype)
             tok = from_gguf(reader)
             tmpl = chat_template.for_model(reader, tok)
         if not cpu:

@@ -62,8 +62,39 @@ def require():
     return load(build_if_missing=True)
 
 
+KV_DTYPES = ("bf16", "fp8", "fp8_e4m3")
+
+
+def kv_fp8_flag(kv_dtype: str) -> int:
+    """KV cache dtype name -> EngineConfig.kv_fp8: 'bf16' (default) or 'fp8' / 'fp8_e4m3' (OCP e4m3
+    with per-layer K / V scales, half the cache bytes)."""
+    k = (kv_dtype or "bf16").strip().lower()
+    if k not in KV_DTYPES:
+        raise ValueError(f"kv_dtype must be one of {KV_DTYPES}, not {kv_dtype!r}")
+    return 0 if k == "bf16" else 1
+
+
+def cu_mask_words(n: int, first: int = 0, total: int = 256) -> list:
+    """A CU mask (32 CUs per word) of n CUs for one co-resident tier: CU slots [first, first + n/8) of
+    every aligned group of 32 CU ids.  Whether the driver numbers CUs XCD-major (32 per XCD) or
+    XCD-minor (id % 8), every XCD then keeps CUs of the tier (no XCD left without any -- each XCD has
+    its own L2 and dispatcher) and two tiers with disjoint [first, first + n/8) ranges never share a CU.
+    n must be a multiple of 8 between 64 and total."""
+    if n % 8 or not (64 <= n <= total) or total % 32:
+        raise ValueError(f"cu mask: {n} CUs (multiple of 8, 64..{total})")
+    per = n // (total // 32)
+    if first < 0 or first + per > 32:
+        raise ValueError("cu mask: slot range outside the 32-CU group")
+    words = [0] * (total // 32)
+    for i in range(total):
+        if first <= i % 32 < first + per:
+            words[i // 32] |= 1 << (i % 32)
+    return words
+
+
 def engine_config(cfg, max_ctx: Optional[int] = None, max_slots: int = 4, max_batch: int = 8, device: int = 0,
-                  tp_rank: int = 0, tp_size: int = 1, act_q8: bool = True, vocab_parallel: bool = True):
+                  tp_rank: int = 0, tp_size: int = 1, act_q8: bool = True, vocab_parallel: bool = True,
+                  cu_mask: Optional[list] = None, kv_dtype: str = "bf16"):
     """aios_amd.models.config.ModelConfig -> native EngineConfig (per-rank shapes under TP).
     Under TP the lm_head is vocab-parallel (V/tp rows per rank + logits all-gather) unless the
     embeddings are tied or V is not divisible by tp."""
@@ -93,5 +124,8 @@ def engine_config(cfg, max_ctx: Optional[int] = None, max_slots: int = 4, max_ba
     ec.vocab_parallel = int(bool(vocab_parallel) and tp_size > 1 and not cfg.tie_embeddings
                             and cfg.vocab_size % tp_size == 0)
     ec.device = device
+    if cu_mask:
+        ec.cu_mask = [int(w) & 0xFFFFFFFF for w in cu_mask]
+    ec.kv_fp8 = kv_fp8_flag(kv_dtype)
     ec.act_q8 = int(act_q8)
     return ec

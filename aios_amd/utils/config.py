@@ -45,6 +45,7 @@ class ModelTier:
     device: str = ""            # "" = GPU when present, "cpu" = the CPU engine
     replicas: int = 1           # engines of this tier, one per GPU (request-level data parallelism)
     devices: List[int] = dataclasses.field(default_factory=list)  # GPUs of the replicas ([] = first `replicas` of models.devices)
+    kv_dtype: str = "bf16"      # KV cache: "bf16" or "fp8_e4m3" (half the cache bytes; long contexts)
 
 
 @dataclasses.dataclass
@@ -129,6 +130,8 @@ class NodeConfig:
                 frag.append(f"tp={t.tensor_parallel}")
             if t.device == "cpu":
                 frag.append("cpu")
+            if t.kv_dtype and t.kv_dtype != "bf16":
+                frag.append(f"kv={t.kv_dtype}")
             devs = list(t.devices)
             if not devs and t.replicas > 1:
                 devs = list(self.models.devices[:t.replicas]) or list(range(t.replicas))
@@ -163,6 +166,8 @@ class NodeConfig:
                 frag.append(f"tp={t.tensor_parallel}")
             if t.device == "cpu":
                 frag.append("cpu")
+            if t.kv_dtype and t.kv_dtype != "bf16":
+                frag.append(f"kv={t.kv_dtype}")
             out.append((name, path + ("#" + "&".join(frag) if frag else ""), t.context_length))
         return out
 

@@ -48,6 +48,7 @@ def parse():
     ap.add_argument("--model", default="mistral-7b")
     ap.add_argument("--recipe", default="Q4_K_M")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--kv-dtype", default="bf16", help="KV cache dtype: bf16 (default) or fp8_e4m3")
     ap.add_argument("--no-secondary", action="store_true",
                     help="skip the secondary measurements (TinyLlama, fp32-activation Mistral)")
     ap.add_argument("--fp32-act", action="store_true",
@@ -81,7 +82,7 @@ def spawn(args) -> int:
 
 
 def measure(preset: str, recipe: str, batch: int, prompt: int, steps: int, warmup: int, use_graph: bool, dist,
-            device: int, act_q8: bool = True):
+            device: int, act_q8: bool = True, kv_dtype: str = "bf16"):
     import torch
 
     from aios_amd.models.config import get_preset
@@ -90,7 +91,7 @@ def measure(preset: str, recipe: str, batch: int, prompt: int, steps: int, warmu
     cfg = get_preset(preset)
     max_ctx = ((prompt + warmup + steps + 2 + 63) // 64) * 64
     eng = random_engine(cfg, recipe, seed=1234, max_ctx=max_ctx, max_slots=max(batch, 1), max_batch=batch,
-                        device=device, act_q8=act_q8)
+                        device=device, act_q8=act_q8, kv_dtype=kv_dtype)
     slots = list(range(batch))
     toks = []
     for s in slots:
@@ -275,7 +276,7 @@ def main():
 
     act_q8 = not args.fp32_act
     dt, info = measure(args.model, args.recipe, args.batch, args.prompt, args.steps, args.warmup,
-                       not args.no_graph, dist, device, act_q8)
+                       not args.no_graph, dist, device, act_q8, args.kv_dtype)
     secondary = other_act = tp_dt = tp_info = None
     if not args.no_secondary:
         secondary, _ = measure("tinyllama-1.1b", "Q4_K_M", 1, args.prompt, args.steps, args.warmup,
@@ -368,7 +369,9 @@ def main():
                 "activations": ("int8 per-32-block activations with fp32 scales in the quantised GEMVs "
                                 "(q8_1 as llama.cpp), fp32 residual stream, fp32 accumulate" if act_q8 else
                                 "fp32 activations in the GEMVs, fp32 accumulate") +
-                               "; int8 GEMV engine up to B = 4, bf16 MFMA operands for B >= 5; attention: bf16 KV cache, bf16-rounded q, fp32 softmax",
+                               "; int8 GEMV engine up to B = 4, bf16 MFMA operands for B >= 5; attention: " +
+                               ("fp8 e4m3 KV cache (per-layer scales)" if args.kv_dtype != "bf16" else "bf16 KV cache") +
+                               ", bf16-rounded q, fp32 softmax",
                 "per_gpu_batch": args.batch,
                 "prompt_tokens": args.prompt,
                 "hipgraph": not args.no_graph,

@@ -63,3 +63,24 @@ load_on_demand = true
     assert specs["strategic"][0] == "synthetic:llama3-70b#tp=8"
     assert "tactical" not in specs and "lazy" not in specs
     assert c.models.devices == [0, 1]
+
+
+def test_cu_mask_words_balanced_and_disjoint():
+    """co-resident tier CU masks: every aligned 32-CU group keeps CUs of both tiers (XCD-major or
+    XCD-minor numbering alike), the two tiers never share a CU, sizes are exact"""
+    from aios_amd.runtime.native import cu_mask_words
+
+    a = cu_mask_words(64, 0, 256)
+    b = cu_mask_words(192, 8, 256)
+    bits = lambda w: {32 * i + j for i, x in enumerate(w) for j in range(32) if x >> j & 1}  # noqa: E731
+    A, Bs = bits(a), bits(b)
+    assert len(A) == 64 and len(Bs) == 192 and not (A & Bs) and len(A | Bs) == 256
+    for xcd in range(8):
+        assert any(i // 32 == xcd for i in A) and any(i % 8 == xcd for i in A)
+        assert any(i // 32 == xcd for i in Bs) and any(i % 8 == xcd for i in Bs)
+    import pytest
+
+    with pytest.raises(ValueError):
+        cu_mask_words(60, 0, 256)
+    with pytest.raises(ValueError):
+        cu_mask_words(192, 16, 256)

@@ -45,3 +45,34 @@ def test_coresident_engines_decode_concurrently_and_match_alone():
     for t in ts:
         t.join(timeout=120)
     assert out[0] == alone[0] and out[1] == alone[1]
+
+
+@pytest.mark.parametrize("split", [64, 128])
+def test_cu_masked_tiers_match_unmasked(split):
+    """each tier on its own CUs (CU-masked stream, grids sized to the mask) decodes
+    exactly the tokens of the unmasked engine, alone and concurrently with the other tier."""
+    from aios_amd.runtime.loader import random_engine
+    from aios_amd.runtime.native import cu_mask_words, require
+
+    total = require().device_cu_count()
+    small_cfg, big_cfg = get_preset("test-small"), get_preset("test-mistral-shape")
+    ref_small, ref_big = _engine("test-small", 5)[1], _engine("test-mistral-shape", 6)[1]
+    want = (_decode(ref_small, small_cfg, 48), _decode(ref_big, big_cfg, 48))
+    del ref_small, ref_big
+    small = random_engine(small_cfg, "Q4_K_M", seed=5, max_ctx=256, max_slots=1, max_batch=1,
+                          cu_mask=cu_mask_words(split, 0, total))
+    big = random_engine(big_cfg, "Q4_K_M", seed=6, max_ctx=256, max_slots=1, max_batch=1,
+                        cu_mask=cu_mask_words(total - split, split // 8, total))
+    assert (_decode(small, small_cfg, 48), _decode(big, big_cfg, 48)) == want
+    out = [None, None]
+
+    def run(i, eng, cfg):
+        for _ in range(3):
+            out[i] = _decode(eng, cfg, 48)
+
+    ts = [threading.Thread(target=run, args=(0, small, small_cfg)), threading.Thread(target=run, args=(1, big, big_cfg))]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=120)
+    assert tuple(out) == want

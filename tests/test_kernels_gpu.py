@@ -484,6 +484,91 @@ def test_attention_decode(E, hd, H, Hkv, lens, max_ctx, split, paging, grouped, 
         assert (out[b].cpu() - ref32).abs().max() < 1e-2
 
 
+def fp8_codes(x, scale):
+    """logical values -> (OCP e4m3 codes as uint8, their dequantised fp32 values) at one scale"""
+    c = (x.float() / scale).clamp(-448, 448).to(torch.float8_e4m3fn)
+    return c.view(torch.uint8), c.float() * scale
+
+
+@pytest.mark.parametrize("hd,H,Hkv", [(128, 32, 8), (64, 32, 4)])
+@pytest.mark.parametrize("lens,max_ctx", [([1], 256), ([37, 200], 256), ([700], 1024), ([3000, 129], 4096)])
+@pytest.mark.parametrize("grouped", ["", "1"])
+def test_attention_decode_fp8_kv(E, hd, H, Hkv, lens, max_ctx, grouped, monkeypatch):
+    """fp8 e4m3 KV pool (EngineConfig::kv_fp8): the decode attention reads 1-byte codes, K converted to
+    bf16 pairs for v_dot2 with the layer's K scale folded into q, V to fp32 with its scale on the output
+    -- against fp32 attention over the dequantised codes (the op as defined), short / long / grouped
+    modes with a shuffled block table"""
+    if grouped:
+        monkeypatch.setenv("AIOS_ATTN_GROUPED_MIN", grouped)
+    B = len(lens)
+    slots = B + 1
+    sk, sv = 0.02, 0.05  # per-layer scales (value = code x scale)
+    kc = torch.randn(slots, Hkv, max_ctx, hd) * 0.5
+    vc = torch.randn(slots, Hkv, max_ctx, hd)
+    k8, kdq = fp8_codes(kc, sk)
+    v8, vdq = fp8_codes(vc, sv)
+    kp, bt = paged_cache(k8, shuffle=True, seed=12)
+    vp, _ = paged_cache(v8, shuffle=True, seed=12)
+    kp, vp, bt_dev = kp.cuda(), vp.cuda(), bt.cuda()
+    q = torch.randn(B, H, hd, device="cuda")
+    seq = torch.tensor(lens, dtype=torch.int32, device="cuda")
+    slot = torch.tensor(list(range(1, B + 1)), dtype=torch.int32, device="cuda")
+    nch = max_ctx // E.ATTN_CHUNK
+    opart = torch.empty(B, H, nch, hd, device="cuda")
+    ml = torch.empty(B, H, nch, 2, device="cuda")
+    out = torch.empty(B, H * hd, device="cuda")
+    cnt = torch.zeros(B, H, dtype=torch.int32, device="cuda")
+    scale = 1 / math.sqrt(hd)
+    E.attn_decode(q.data_ptr(), kp.data_ptr(), vp.data_ptr(), seq.data_ptr(), slot.data_ptr(), B, H, Hkv, hd,
+                  max_ctx, nch, scale, opart.data_ptr(), ml.data_ptr(), out.data_ptr(), cnt.data_ptr(), stream(),
+                  0, bt_dev.data_ptr(), 0, kv_fp8=1, k_scale=sk, v_scale=sv)
+    torch.cuda.synchronize()
+    assert int(cnt.abs().sum()) == 0
+    G = H // Hkv
+    log2e = 1.4426950408889634
+    for b in range(B):
+        L, s_ = lens[b], b + 1
+        k = kdq[s_, :, :L].repeat_interleave(G, 0)
+        v = vdq[s_, :, :L].repeat_interleave(G, 0)
+        # q * scale * log2(e) * k_scale rounded to bf16, dot with the codes (exact in bf16), fp32 softmax
+        qs = (q[b].cpu() * (scale * log2e * sk)).to(torch.bfloat16).float()
+        att = torch.softmax(torch.einsum("hd,hsd->hs", qs, k / sk) * math.log(2.0), -1)
+        ref = torch.einsum("hs,hsd->hd", att, v).reshape(-1)
+        assert torch.allclose(out[b].cpu(), ref, atol=5e-4, rtol=5e-3), (b, (out[b].cpu() - ref).abs().max())
+
+
+@pytest.mark.parametrize("H,Hkv,hd", [(32, 8, 128), (32, 4, 64)])
+@pytest.mark.parametrize("start,T", [(0, 37), (70, 130), (0, 300)])
+def test_attention_prefill_fp8_kv(E, H, Hkv, hd, start, T):
+    """the prefill flash attention over an fp8 e4m3 KV pool: tiles converted to bf16 with the layer's
+    scales while staging, then the bf16 MFMA math -- against fp32 attention over the dequantised codes"""
+    max_ctx = 512
+    slot, slots = 1, 2
+    G = H // Hkv
+    sk, sv = 0.03, 0.04
+    k8, kdq = fp8_codes(torch.randn(slots, Hkv, max_ctx, hd) * 0.5, sk)
+    v8, vdq = fp8_codes(torch.randn(slots, Hkv, max_ctx, hd), sv)
+    kp, bt = paged_cache(k8, True, seed=6)
+    vp, _ = paged_cache(v8, True, seed=6)
+    kp, vp, bt_dev = kp.cuda(), vp.cuda(), bt.cuda()
+    q = torch.randn(T, H, hd, device="cuda")
+    out = torch.zeros(T, H * hd, dtype=torch.bfloat16, device="cuda")
+    scale = 1 / math.sqrt(hd)
+    E.attn_prefill(q.data_ptr(), kp.data_ptr(), vp.data_ptr(), slot, start, T, H, Hkv, hd, max_ctx, scale,
+                   out.data_ptr(), H * hd, stream(), bt_dev.data_ptr(), kv_fp8=1, k_scale=sk, v_scale=sv)
+    torch.cuda.synchronize()
+    L = start + T
+    k = kdq[slot, :, :L].to(torch.bfloat16).float().repeat_interleave(G, 0)
+    v = vdq[slot, :, :L].to(torch.bfloat16).float().repeat_interleave(G, 0)
+    qq = q.cpu().to(torch.bfloat16).float()
+    s_ = torch.einsum("thd,hld->htl", qq, k) * scale
+    pos = torch.arange(start, L)[:, None]
+    s_ = s_.masked_fill(torch.arange(L)[None, :] > pos, float("-inf"))
+    ref = torch.einsum("htl,hld->thd", torch.softmax(s_, -1), v).reshape(T, H * hd)
+    err = (out.float().cpu() - ref).abs().max().item()
+    assert err < 3e-2, err
+
+
 def test_rmsnorm(E):
     x = torch.randn(5, 4096, device="cuda") * 2
     w = torch.rand(4096, device="cuda")

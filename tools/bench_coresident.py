@@ -21,6 +21,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=512)
     ap.add_argument("--prompt", type=int, default=128)
+    ap.add_argument("--cu-split", type=int, default=0,
+                    help="CUs for the TinyLlama tier's stream (the rest for Mistral; 0: both tiers on every CU)")
     print(json.dumps(run(ap.parse_args())), flush=True)
 
 
@@ -30,12 +32,20 @@ def run(args):
 
     from aios_amd.models.config import get_preset
     from aios_amd.runtime.loader import random_engine
+    from aios_amd.runtime.native import cu_mask_words, require
 
+    # CU partition: each tier's stream gets its own CUs (hipExtStreamCreateWithCUMask)
+    # and the engine sizes its one-workgroup-per-CU grids to them, so the tiers stop trampling each
+    # other's dispatch rounds
+    split = int(getattr(args, "cu_split", 0) or 0)
+    total = require().device_cu_count() if split else 0
+    masks = {"tinyllama": cu_mask_words(split, 0, total), "mistral": cu_mask_words(total - split, split // 8, total)} \
+        if split else {}
     models = {}
     for name, preset, seed in (("tinyllama", "tinyllama-1.1b", 1), ("mistral", "mistral-7b", 2)):
         cfg = get_preset(preset)
         eng = random_engine(cfg, "Q4_K_M", seed=seed, max_ctx=((args.prompt + 3 * args.steps + 64) // 128 + 1) * 128,
-                            max_slots=1, max_batch=1)
+                            max_slots=1, max_batch=1, cu_mask=masks.get(name))
         models[name] = (cfg, eng)
 
     pos = {}
@@ -58,6 +68,7 @@ def run(args):
         res[name] = time.perf_counter() - t0
 
     out = {"bench": "co-resident tiers, B=1 decode on one GPU", "steps": args.steps, "prompt": args.prompt,
+           "cu_split": {"tinyllama": split, "mistral": total - split} if split else None,
            "data": "synthetic (random-init Q4_K_M weights, synthetic prompts)",
            "hbm_weights_gb": round(sum(e.weight_bytes for _, e in models.values()) / 1e9, 3),
            "hbm_gb_per_tier": {n: {"weights": round(e.weight_bytes / 1e9, 3), "kv": round(e.kv_bytes / 1e9, 3),
