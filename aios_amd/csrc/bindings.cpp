@@ -160,7 +160,8 @@ PYBIND11_MODULE(_engine, m) {
       .def_readwrite("vocab_parallel", &EngineConfig::vocab_parallel)
       .def_readwrite("device", &EngineConfig::device)
       .def_readwrite("cu_mask", &EngineConfig::cu_mask)
-      .def_readwrite("kv_fp8", &EngineConfig::kv_fp8);
+      .def_readwrite("kv_fp8", &EngineConfig::kv_fp8)
+      .def_readwrite("stream_priority", &EngineConfig::stream_priority);
 
   py::class_<Engine>(m, "Engine")
       .def(py::init<const EngineConfig&>())

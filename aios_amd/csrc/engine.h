@@ -52,6 +52,9 @@ struct EngineConfig {
   // CU mask of the engine's stream (hipExtStreamCreateWithCUMask; 32 CUs per word, empty = every CU):
   // co-resident tiers each get their own CUs, and the engine sizes its grids to the mask's CU count
   std::vector<uint32_t> cu_mask;
+  // stream priority (co-resident tiers, unmasked streams): 0 = normal, < 0 = higher (the range of
+  // hipDeviceGetStreamPriorityRange; the hardware queue's dispatcher serves it first)
+  int stream_priority = 0;
 };
 
 // device matrix in repacked layout (owns its buffer)

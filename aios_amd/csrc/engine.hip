@@ -70,6 +70,11 @@ Engine::Engine(const EngineConfig& cfg) : cfg_(cfg) {
     if (n <= 0) throw std::runtime_error("cu_mask selects no CU");
     HIP_CHECK(hipExtStreamCreateWithCUMask(&stream_, (uint32_t)cfg_.cu_mask.size(), cfg_.cu_mask.data()));
     cus_ = std::min(n, dev_cus);
+  } else if (cfg_.stream_priority != 0) {
+    int least = 0, greatest = 0;
+    HIP_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
+    const int pr = std::max(greatest, std::min(least, cfg_.stream_priority));
+    HIP_CHECK(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, pr));
   } else {
     HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
   }

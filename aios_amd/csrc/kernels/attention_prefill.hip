@@ -43,8 +43,9 @@ constexpr int FP_KT = 64;  // keys per tile
 typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
 
 // F8: the pool holds fp8 e4m3 codes (EngineConfig::kv_fp8): the tile loads move half the bytes and
-// staging converts them to bf16 with the layer's K / V scale (v_cvt_scalef32_pk_bf16_fp8) -- the LDS
-// tiles and the MFMA math are the bf16 kernel's
+// staging converts the codes to bf16 (exact; v_cvt_scalef32_pk_bf16_fp8 at scale 1 -- its scale
+// operand is applied as a power of two, so the layer's K scale is folded into q and its V scale into
+// the output instead) -- the LDS tiles and the MFMA math are the bf16 kernel's
 template <int HD, int G, bool F8 = false>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) attn_prefill_kernel(AttnPrefillArgs a) {
   constexpr int BQ = 128 / G;          // query positions per workgroup
@@ -95,7 +96,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
   bf16x8_t qf[KS];
   {
     const float* qp = a.q + ((size_t)tql * a.n_heads + h) * HD + 8 * half;
-    const float sc = a.scale * 1.4426950408889634f;
+    const float sc = a.scale * 1.4426950408889634f * (F8 ? a.kv_scale_k : 1.f);
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
       const float4 x0 = *(const float4*)(qp + 16 * s), x1 = *(const float4*)(qp + 16 * s + 4);
@@ -151,16 +152,16 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
       constexpr int i = decltype(I)::value;
       const int idx = tid + 256 * i, key = idx / (HD / 8), c = idx % (HD / 8);
       if constexpr (F8) {
-        auto cv = [](u32x2_t w, float s) {
+        auto cv = [](u32x2_t w) {
           u32x4_t o;
-          o[0] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w[0], s, false));
-          o[1] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w[0], s, true));
-          o[2] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w[1], s, false));
-          o[3] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w[1], s, true));
+          o[0] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w[0], 1.f, false));
+          o[1] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w[0], 1.f, true));
+          o[2] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w[1], 1.f, false));
+          o[3] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w[1], 1.f, true));
           return o;
         };
-        *(u32x4_t*)(sK + key * KROW + c * 8) = cv(r.k[i], a.kv_scale_k);
-        *(u32x4_t*)(sV + key * VROW + c * 8) = cv(r.v[i], a.kv_scale_v);
+        *(u32x4_t*)(sK + key * KROW + c * 8) = cv(r.k[i]);
+        *(u32x4_t*)(sV + key * VROW + c * 8) = cv(r.v[i]);
       } else {
         *(u32x4_t*)(sK + key * KROW + c * 8) = r.k[i];
         *(u32x4_t*)(sV + key * VROW + c * 8) = r.v[i];
@@ -272,7 +273,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
   }
   // ---- normalise and store bf16: O^T[dim][row], dim = 32 i + (r&3) + 8 (r>>2) + 4 half
   if (qvalid) {
-    const float inv = 1.f / l_run;
+    const float inv = (F8 ? a.kv_scale_v : 1.f) / l_run;
     bf16_t* op = a.out + (size_t)tq * a.ldo + (size_t)h * HD;
 #pragma unroll
     for (int i = 0; i < OT; ++i)

@@ -105,16 +105,20 @@ __device__ __forceinline__ gf32x2 fp8x2_f32x2(uint32_t w) {
 // VALU diet (the kernel is VALU-bound per CU once its loads are in flight): q . k runs on
 // v_dot2_f32_bf16 against q pre-rounded to bf16 pairs (4 instructions per 8 dims and head, as the
 // MFMA prefill path rounds q), P . V on packed v_pk_fma_f32 with the probabilities in fp32.
-// F8: the pool holds fp8 e4m3 codes (EngineConfig::kv_fp8): half the K / V bytes per pass; a lane's 8
-// dims are 8 bytes, K converted to bf16 pairs for the same v_dot2 (the layer's K scale folded into q),
-// V to fp32 pairs for the P.V FMAs (its V scale applied to the output)
+// F8: the pool holds fp8 e4m3 codes (EngineConfig::kv_fp8): K converted to bf16 pairs for the same
+// v_dot2 (the layer's K scale folded into q), V to fp32 pairs for the P.V FMAs (its V scale applied to
+// the output).  At head_dim 128 a lane takes 16 dims (16 bytes: the bf16 path's load width -- with 8
+// dims per lane the fp8 kernel issued as many load instructions for half the bytes and measured only
+// 3 % faster than bf16 at 32k keys, latency- not byte-bound); head_dim 64 keeps 8 dims (8 bytes).
 template <int HD, int G, bool F8 = false>
 __device__ __forceinline__ void attn_core(const AttnDecodeArgs& a, int sp, int kvh, int h0, int ci, int P_max,
                                           int ppw, bool nt = false) {
-  using KVT = typename std::conditional<F8, uint2, uint4>::type;
+  constexpr int DPL = (F8 && HD == 128) ? 16 : 8;  // dims per lane
+  using KVT = typename std::conditional<F8 && DPL == 8, uint2, uint4>::type;
   constexpr int ES = F8 ? 1 : 2;  // bytes per cached element
+  constexpr int NP = DPL / 2;     // bf16 / fp32 pairs per lane
   constexpr int NW = 8;                // waves per workgroup
-  constexpr int LPK = HD / 8;          // lanes per key (8 dims per lane)
+  constexpr int LPK = HD / DPL;        // lanes per key
   constexpr int KPS = 64 / LPK;        // keys per wave-instruction
   constexpr int CH = 128;              // keys per workgroup pass
   constexpr int KPW = CH / NW;         // keys per wave per pass
@@ -145,8 +149,8 @@ __device__ __forceinline__ void attn_core(const AttnDecodeArgs& a, int sp, int k
   const int* btr = a.block_table ? a.block_table + (size_t)(a.bt_rows ? b : slot) * maxb : nullptr;
   const size_t blk_stride = (size_t)a.n_kv_heads * KV_BLOCK * HD;
   const int koff = wave * KPW + ksub;  // this lane's key within a pass (+ s * KPS)
-  const uint8_t* kc = (const uint8_t*)a.k_cache + ((size_t)kvh * KV_BLOCK * HD + (size_t)koff * HD + dsl * 8) * ES;
-  const uint8_t* vc = (const uint8_t*)a.v_cache + ((size_t)kvh * KV_BLOCK * HD + (size_t)koff * HD + dsl * 8) * ES;
+  const uint8_t* kc = (const uint8_t*)a.k_cache + ((size_t)kvh * KV_BLOCK * HD + (size_t)koff * HD + dsl * DPL) * ES;
+  const uint8_t* vc = (const uint8_t*)a.v_cache + ((size_t)kvh * KV_BLOCK * HD + (size_t)koff * HD + dsl * DPL) * ES;
   const int cmax = maxb - 1;           // last chunk with valid memory
 
   const int len = a.seq_len[b];
@@ -160,7 +164,7 @@ __device__ __forceinline__ void attn_core(const AttnDecodeArgs& a, int sp, int k
   const bool tail = a.kv_tail != 0;
   auto ld = [&](const uint8_t* p) __attribute__((always_inline)) { return *(const KVT*)p; };
   auto ld_nt = [&](const uint8_t* p) __attribute__((always_inline)) {
-    if constexpr (F8) return ld_nt8(p);
+    if constexpr (F8 && DPL == 8) return ld_nt8(p);
     else return ld_nt16((const bf16_t*)p);
   };
   auto issue = [&](KVT (&kr)[STEPS], KVT (&vr)[STEPS], int chunk) __attribute__((always_inline)) {
@@ -195,25 +199,25 @@ __device__ __forceinline__ void attn_core(const AttnDecodeArgs& a, int sp, int k
   if (sp + P < nchunk) issue(kB, vB, sp + P);
   const float qs = a.scale * kLog2e * (F8 ? a.kv_scale_k : 1.f);  // scores in the log2 domain: exp2 below
   const float vs = F8 ? a.kv_scale_v : 1.f;                         // (fp8: V's scale, on the output)
-  uint32_t q2[G][4];                  // q * scale as bf16 pairs
+  uint32_t q2[G][NP];                 // q * scale as bf16 pairs
 #pragma unroll
   for (int g = 0; g < G; ++g) {
-    const float* qp = a.q + ((size_t)b * a.n_heads + h0 + g) * HD + dsl * 8;
-    const float4 q0 = *(const float4*)qp;
-    const float4 q1 = *(const float4*)(qp + 4);
-    q2[g][0] = pk_bf16(q0.x * qs, q0.y * qs);
-    q2[g][1] = pk_bf16(q0.z * qs, q0.w * qs);
-    q2[g][2] = pk_bf16(q1.x * qs, q1.y * qs);
-    q2[g][3] = pk_bf16(q1.z * qs, q1.w * qs);
+    const float* qp = a.q + ((size_t)b * a.n_heads + h0 + g) * HD + dsl * DPL;
+#pragma unroll
+    for (int j = 0; j < DPL / 4; ++j) {
+      const float4 q0 = *(const float4*)(qp + 4 * j);
+      q2[g][2 * j] = pk_bf16(q0.x * qs, q0.y * qs);
+      q2[g][2 * j + 1] = pk_bf16(q0.z * qs, q0.w * qs);
+    }
   }
   float m[G], l[G];
-  gf32x2 o[G][4];
+  gf32x2 o[G][NP];
 #pragma unroll
   for (int g = 0; g < G; ++g) {
     m[g] = kNeg;
     l[g] = 0.f;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) o[g][i] = gf32x2{0.f, 0.f};
+    for (int i = 0; i < NP; ++i) o[g][i] = gf32x2{0.f, 0.f};
   }
   auto pass = [&](const KVT (&kr)[STEPS], const KVT (&vr)[STEPS], int c) __attribute__((always_inline)) {
     // ---- scores of this lane's STEPS keys for the G heads (reduced over the key's LPK lanes)
@@ -221,8 +225,12 @@ __device__ __forceinline__ void attn_core(const AttnDecodeArgs& a, int sp, int k
 #pragma unroll
     for (int s = 0; s < STEPS; ++s) {
       const bool valid = c * CH + koff + s * KPS < len;
-      uint32_t kb[4];
-      if constexpr (F8) {
+      uint32_t kb[NP];
+      if constexpr (F8 && DPL == 16) {
+        const uint32_t w4[4] = {kr[s].x, kr[s].y, kr[s].z, kr[s].w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) { kb[2 * i] = fp8x2_bf16x2<false>(w4[i]); kb[2 * i + 1] = fp8x2_bf16x2<true>(w4[i]); }
+      } else if constexpr (F8) {
         kb[0] = fp8x2_bf16x2<false>(kr[s].x); kb[1] = fp8x2_bf16x2<true>(kr[s].x);
         kb[2] = fp8x2_bf16x2<false>(kr[s].y); kb[3] = fp8x2_bf16x2<true>(kr[s].y);
       } else {
@@ -231,9 +239,8 @@ __device__ __forceinline__ void attn_core(const AttnDecodeArgs& a, int sp, int k
 #pragma unroll
       for (int g = 0; g < G; ++g) {
         float d = dot2_bf16(kb[0], q2[g][0], 0.f);
-        d = dot2_bf16(kb[1], q2[g][1], d);
-        d = dot2_bf16(kb[2], q2[g][2], d);
-        d = dot2_bf16(kb[3], q2[g][3], d);
+#pragma unroll
+        for (int i = 1; i < NP; ++i) d = dot2_bf16(kb[i], q2[g][i], d);
         d = group_sum<LPK>(d);
         sc[s][g] = valid ? d : kNeg;
       }
@@ -257,13 +264,17 @@ __device__ __forceinline__ void attn_core(const AttnDecodeArgs& a, int sp, int k
       l[g] = l[g] * alpha + keys_sum<LPK>(ps);
       m[g] = mn;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) o[g][i] *= alpha;
+      for (int i = 0; i < NP; ++i) o[g][i] *= alpha;
     }
     // ---- P.V (lane-local over its keys; merged across key groups and waves at the end)
 #pragma unroll
     for (int s = 0; s < STEPS; ++s) {
-      gf32x2 vf[4];
-      if constexpr (F8) {
+      gf32x2 vf[NP];
+      if constexpr (F8 && DPL == 16) {
+        const uint32_t w4[4] = {vr[s].x, vr[s].y, vr[s].z, vr[s].w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) { vf[2 * i] = fp8x2_f32x2<false>(w4[i]); vf[2 * i + 1] = fp8x2_f32x2<true>(w4[i]); }
+      } else if constexpr (F8) {
         vf[0] = fp8x2_f32x2<false>(vr[s].x); vf[1] = fp8x2_f32x2<true>(vr[s].x);
         vf[2] = fp8x2_f32x2<false>(vr[s].y); vf[3] = fp8x2_f32x2<true>(vr[s].y);
       } else {
@@ -275,7 +286,7 @@ __device__ __forceinline__ void attn_core(const AttnDecodeArgs& a, int sp, int k
       for (int g = 0; g < G; ++g) {
         const gf32x2 pp = gf32x2{sc[s][g], sc[s][g]};
 #pragma unroll
-        for (int i = 0; i < 4; ++i) o[g][i] = __builtin_elementwise_fma(pp, vf[i], o[g][i]);
+        for (int i = 0; i < NP; ++i) o[g][i] = __builtin_elementwise_fma(pp, vf[i], o[g][i]);
       }
     }
   };
@@ -289,20 +300,20 @@ __device__ __forceinline__ void attn_core(const AttnDecodeArgs& a, int sp, int k
     }
   }
   // ---- merge the key groups of a wave (shuffles), then the 8 waves in LDS (one barrier)
-  float of[G][8];
+  float of[G][DPL];
 #pragma unroll
   for (int g = 0; g < G; ++g)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < NP; ++i) {
       of[g][2 * i] = keys_sum<LPK>(o[g][i].x);
       of[g][2 * i + 1] = keys_sum<LPK>(o[g][i].y);
     }
   if (ksub == 0) {
 #pragma unroll
     for (int g = 0; g < G; ++g) {
-      float4* dst = (float4*)&s_o[wave][g][dsl * 8];
-      dst[0] = make_float4(of[g][0], of[g][1], of[g][2], of[g][3]);
-      dst[1] = make_float4(of[g][4], of[g][5], of[g][6], of[g][7]);
+      float4* dst = (float4*)&s_o[wave][g][dsl * DPL];
+#pragma unroll
+      for (int j = 0; j < DPL / 4; ++j) dst[j] = make_float4(of[g][4 * j], of[g][4 * j + 1], of[g][4 * j + 2], of[g][4 * j + 3]);
     }
   }
   if (lane < G) {

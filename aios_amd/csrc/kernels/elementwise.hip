@@ -74,7 +74,11 @@ __global__ void __launch_bounds__(256) rmsnorm_reg_kernel(const float* __restric
 template <typename OutT>
 static void rmsnorm_go(const float* x, int ldx, const float* w, OutT* y, int ldy, int rows, int n, float eps,
                        hipStream_t st) {
-  const bool al = n % 4 == 0 && ldx % 4 == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)w & 15) == 0;
+  // (the register kernel's vector stores: float4 / 4 x bf16 at y + row * ldy + 4i -- ADVICE r5: y and
+  // ldy are checked too, a misaligned output takes the scalar kernel)
+  constexpr uintptr_t ymask = sizeof(OutT) == 4 ? 15 : 7;
+  const bool al = n % 4 == 0 && ldx % 4 == 0 && ldy % 4 == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)w & 15) == 0 &&
+                  ((uintptr_t)y & ymask) == 0;
   if (al && n <= 1024 * 4)
     hipLaunchKernelGGL((rmsnorm_reg_kernel<OutT, 4>), dim3(rows), dim3(256), 0, st, x, ldx, w, y, ldy, n, eps);
   else if (al && n <= 1024 * 8)

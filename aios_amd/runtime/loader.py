@@ -108,13 +108,14 @@ def finalize(eng):
 
 def random_engine(cfg: ModelConfig, recipe: str = "Q4_K_M", seed: int = 0, max_ctx: Optional[int] = None,
                   max_slots: int = 4, max_batch: int = 8, device: int = 0, tp_rank: int = 0, tp_size: int = 1,
-                  act_q8: bool = True, cu_mask: Optional[list] = None, kv_dtype: str = "bf16"):
+                  act_q8: bool = True, cu_mask: Optional[list] = None, kv_dtype: str = "bf16",
+                  stream_priority: int = 0):
     """Engine with random-init weights of `cfg`'s architecture generated directly in HBM (cu_mask: the
     CUs its stream may use, native.cu_mask_words)."""
     m = native.require()
     ec = native.engine_config(cfg, max_ctx=max_ctx or min(cfg.max_ctx, 4096), max_slots=max_slots,
                               max_batch=max_batch, device=device, tp_rank=tp_rank, tp_size=tp_size,
-                              act_q8=act_q8, cu_mask=cu_mask, kv_dtype=kv_dtype)
+                              act_q8=act_q8, cu_mask=cu_mask, kv_dtype=kv_dtype, stream_priority=stream_priority)
     eng = m.Engine(ec)
     eng.init_random(recipe, seed)
     finalize(eng)

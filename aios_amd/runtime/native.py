@@ -94,7 +94,7 @@ def cu_mask_words(n: int, first: int = 0, total: int = 256) -> list:
 
 def engine_config(cfg, max_ctx: Optional[int] = None, max_slots: int = 4, max_batch: int = 8, device: int = 0,
                   tp_rank: int = 0, tp_size: int = 1, act_q8: bool = True, vocab_parallel: bool = True,
-                  cu_mask: Optional[list] = None, kv_dtype: str = "bf16"):
+                  cu_mask: Optional[list] = None, kv_dtype: str = "bf16", stream_priority: int = 0):
     """aios_amd.models.config.ModelConfig -> native EngineConfig (per-rank shapes under TP).
     Under TP the lm_head is vocab-parallel (V/tp rows per rank + logits all-gather) unless the
     embeddings are tied or V is not divisible by tp."""
@@ -127,5 +127,6 @@ def engine_config(cfg, max_ctx: Optional[int] = None, max_slots: int = 4, max_ba
     if cu_mask:
         ec.cu_mask = [int(w) & 0xFFFFFFFF for w in cu_mask]
     ec.kv_fp8 = kv_fp8_flag(kv_dtype)
+    ec.stream_priority = int(stream_priority)
     ec.act_q8 = int(act_q8)
     return ec

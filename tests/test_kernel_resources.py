@@ -29,8 +29,8 @@ def test_hot_kernels_use_no_scratch():
     assert len(rows) > 100  # the whole kernel set was read
     names = {r["name"] for r in rows}
     # the decode path's kernels are all present ...
-    for must in ("gemv_lds_b1<12, 12, 1, 1>", "gemv_q8_rows<12, 14, 1, 2, 1>", "attn_decode_kernel<128, 4>",
-                 "gemm_ring_kernel<12, 12, 1, 2, true>"):
+    for must in ("gemv_lds_b1<12, 12, 1, 1>", "gemv_q8_rows<12, 14, 1, 2, 1>", "attn_decode_kernel<128, 4, false>",
+                 "attn_decode_kernel<128, 4, true>", "gemv_lds16<1, 3, 2>", "gemm_ring_kernel<12, 12, 1, 2, true>"):
         assert any(must in n for n in names), must
     # ... and none of them spills to scratch
     bad = kr.hot_with_scratch(rows)

@@ -558,10 +558,11 @@ def test_attention_prefill_fp8_kv(E, H, Hkv, hd, start, T):
                    out.data_ptr(), H * hd, stream(), bt_dev.data_ptr(), kv_fp8=1, k_scale=sk, v_scale=sv)
     torch.cuda.synchronize()
     L = start + T
-    k = kdq[slot, :, :L].to(torch.bfloat16).float().repeat_interleave(G, 0)
-    v = vdq[slot, :, :L].to(torch.bfloat16).float().repeat_interleave(G, 0)
-    qq = q.cpu().to(torch.bfloat16).float()
-    s_ = torch.einsum("thd,hld->htl", qq, k) * scale
+    k = kdq[slot, :, :L].repeat_interleave(G, 0)
+    v = vdq[slot, :, :L].repeat_interleave(G, 0)
+    # q * scale * log2(e) * k_scale rounded to bf16 against the codes (exact in bf16)
+    qq = (q.cpu() * (scale * 1.4426950408889634 * sk)).to(torch.bfloat16).float() / (1.4426950408889634 * sk)
+    s_ = torch.einsum("thd,hld->htl", qq, k)
     pos = torch.arange(start, L)[:, None]
     s_ = s_.masked_fill(torch.arange(L)[None, :] > pos, float("-inf"))
     ref = torch.einsum("htl,hld->thd", torch.softmax(s_, -1), v).reshape(T, H * hd)
@@ -569,17 +570,25 @@ def test_attention_prefill_fp8_kv(E, H, Hkv, hd, start, T):
     assert err < 3e-2, err
 
 
-def test_rmsnorm(E):
-    x = torch.randn(5, 4096, device="cuda") * 2
-    w = torch.rand(4096, device="cuda")
-    y = torch.empty_like(x)
-    E.rmsnorm(x.data_ptr(), 4096, w.data_ptr(), y.data_ptr(), 4096, 5, 4096, 1e-5, stream())
-    yb = torch.empty(5, 4096, dtype=torch.bfloat16, device="cuda")
-    E.rmsnorm_bf16(x.data_ptr(), 4096, w.data_ptr(), yb.data_ptr(), 4096, 5, 4096, 1e-5, stream())
+@pytest.mark.parametrize("n", [2048, 4096, 8192, 6000])
+@pytest.mark.parametrize("y_off", [0, 1])
+def test_rmsnorm(E, n, y_off):
+    """register kernel (n <= 4096: NV = 4; <= 8192: NV = 8 -- Llama-3-70B's d 8192) and the scalar
+    kernel (n % 4 != 0 or a misaligned output: y_off shifts y by one element)"""
+    x = torch.randn(5, n, device="cuda") * 2
+    w = torch.rand(n, device="cuda")
+    ld = n + 4
+    ybuf = torch.zeros(5 * ld + 8, device="cuda")
+    y = ybuf[y_off:y_off + 5 * ld].view(5, ld)
+    E.rmsnorm(x.data_ptr(), n, w.data_ptr(), y.data_ptr(), ld, 5, n, 1e-5, stream())
+    ybb = torch.zeros(5 * ld + 8, dtype=torch.bfloat16, device="cuda")
+    yb = ybb[y_off:y_off + 5 * ld].view(5, ld)
+    E.rmsnorm_bf16(x.data_ptr(), n, w.data_ptr(), yb.data_ptr(), ld, 5, n, 1e-5, stream())
     torch.cuda.synchronize()
     ref = x * torch.rsqrt((x * x).mean(-1, keepdim=True) + 1e-5) * w
-    assert torch.allclose(y, ref, atol=1e-5, rtol=1e-5)
-    assert torch.allclose(yb.float(), ref, atol=2e-2, rtol=1e-2)
+    assert torch.allclose(y[:, :n], ref, atol=1e-5, rtol=1e-5)
+    assert torch.allclose(yb[:, :n].float(), ref, atol=2e-2, rtol=1e-2)
+    assert not y[:, n:].any() and not yb[:, n:].float().any()  # nothing past each row
 
 
 @pytest.mark.parametrize("neox", [0, 1])
@@ -1119,6 +1128,60 @@ def test_gemm_pf_tail_split(E, monkeypatch, epi, tile, N):
         ref = y + (0.0 if epi == "store" else 0.5)
         rel = float((outs[0].double() - ref).norm() / ref.norm())
         assert rel < 6e-3, rel
+
+
+@pytest.mark.parametrize("segs,M", [([(GGMLType.Q4_K, 8192)], 2100),
+                                    ([(GGMLType.Q4_K, 4096), (GGMLType.Q4_K, 1024), (GGMLType.Q6_K, 1024)], 2800)])
+@pytest.mark.parametrize("epi", ["store", "accum"])
+def test_gemm_pf_tail_split_ragged(E, monkeypatch, segs, M, epi):
+    """the tail split with M NOT a multiple of 256 (the last row tile partial, its second
+    128-row half entirely past M) and on the mixed Q4_K|Q6_K QKV stack (Mistral's 4096 + 1024 + 1024
+    rows: the segment branch runs per half): bit-identical to the plain launch, and against the
+    unquantized product"""
+    monkeypatch.setenv("AIOS_GEMM_PF_TILE", "256x256")
+    K = 512
+    mats, refs = zip(*[qmat(E, t, n, K, seed=140 + i, std=0.02) for i, (t, n) in enumerate(segs)])
+    mats, W = list(mats), torch.cat(refs, 0)
+    N = W.shape[0]
+    tiles = -(-M // 256) * (N // 256)
+    assert tiles % E.device_cu_count() <= E.device_cu_count() // 2 < tiles  # (a half-full last round)
+    x = torch.randn(M, K, generator=torch.Generator().manual_seed(M))
+    A = x.to(torch.bfloat16).cuda()
+    outs = []
+    for tail in ("1", "0"):
+        monkeypatch.setenv("AIOS_GEMM_PF_TAIL", tail)
+        C = torch.full((M, N), 0.25, device="cuda")
+        E.gemm_q(A.data_ptr(), K, mats, M, C.data_ptr(), 0, N, E.GEPI_STORE if epi == "store" else E.GEPI_ACCUM,
+                 stream(), 1)
+        torch.cuda.synchronize()
+        outs.append(C.cpu())
+    assert torch.equal(outs[0], outs[1])
+    ref = x.double() @ W.double().T + (0.0 if epi == "store" else 0.25)
+    rel = float((outs[0].double() - ref).norm() / ref.norm())
+    assert rel < 6e-3, rel
+
+
+@pytest.mark.parametrize("fmt,N,K", [(GGMLType.Q4_K, 512, 4096), (GGMLType.Q6_K, 256, 14336), (GGMLType.BF16, 256, 4096)])
+@pytest.mark.parametrize("split", [0, 4])
+def test_gemm_pf_production_shapes_vs_unquantized(E, monkeypatch, fmt, N, K, split):
+    """a 2048-token prefill chunk (M = 2048) at the production K of the Mistral
+    projections -- K = 4096 (QKV / O / gate-up) and K = 14336 (the Q6_K down) -- through the
+    launcher's own plan and a split-K plan, against the unquantized fp64 product"""
+    if split:
+        monkeypatch.setenv("AIOS_GEMM_PF_SPLIT", str(split))
+    M = 2048
+    m, W = qmat(E, fmt, N, K, seed=150 + K, std=0.02)
+    x = torch.randn(M, K, generator=torch.Generator().manual_seed(K))
+    A = x.to(torch.bfloat16).cuda()
+    C = torch.zeros(M, N, device="cuda")
+    E.gemm_q(A.data_ptr(), K, [m], M, C.data_ptr(), 0, N, E.GEPI_ACCUM, stream(), split or 0)
+    torch.cuda.synchronize()
+    ref = x.double() @ W.double().T
+    got = C.cpu().double()
+    rel = float((got - ref).norm() / ref.norm())
+    assert rel < 6e-3, rel
+    per_row = ((got - ref).norm(dim=1) / ref.norm(dim=1)).max().item()
+    assert per_row < 1e-2, per_row
 
 
 @pytest.mark.parametrize("tile", ["256x256", "128x256", "64x128"])

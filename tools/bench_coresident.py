@@ -23,6 +23,8 @@ def main():
     ap.add_argument("--prompt", type=int, default=128)
     ap.add_argument("--cu-split", type=int, default=0,
                     help="CUs for the TinyLlama tier's stream (the rest for Mistral; 0: both tiers on every CU)")
+    ap.add_argument("--priority", default="",
+                    help="tier whose stream gets the high priority (unmasked streams only): tinyllama | mistral")
     print(json.dumps(run(ap.parse_args())), flush=True)
 
 
@@ -44,8 +46,9 @@ def run(args):
     models = {}
     for name, preset, seed in (("tinyllama", "tinyllama-1.1b", 1), ("mistral", "mistral-7b", 2)):
         cfg = get_preset(preset)
+        prio = -1 if (not split and getattr(args, "priority", "") == name) else 0
         eng = random_engine(cfg, "Q4_K_M", seed=seed, max_ctx=((args.prompt + 3 * args.steps + 64) // 128 + 1) * 128,
-                            max_slots=1, max_batch=1, cu_mask=masks.get(name))
+                            max_slots=1, max_batch=1, cu_mask=masks.get(name), stream_priority=prio)
         models[name] = (cfg, eng)
 
     pos = {}
@@ -69,6 +72,7 @@ def run(args):
 
     out = {"bench": "co-resident tiers, B=1 decode on one GPU", "steps": args.steps, "prompt": args.prompt,
            "cu_split": {"tinyllama": split, "mistral": total - split} if split else None,
+           "high_priority_tier": (getattr(args, "priority", "") or None) if not split else None,
            "data": "synthetic (random-init Q4_K_M weights, synthetic prompts)",
            "hbm_weights_gb": round(sum(e.weight_bytes for _, e in models.values()) / 1e9, 3),
            "hbm_gb_per_tier": {n: {"weights": round(e.weight_bytes / 1e9, 3), "kv": round(e.kv_bytes / 1e9, 3),

@@ -25,6 +25,7 @@ SO = os.path.join(ROOT, "aios_amd")
 # demangled text); the batch>1 row-pair GEMV variants are fallbacks and are reported, not enforced
 HOT = [
     "aios::gemv_lds_b1<*, *, 1, *>*",
+    "aios::gemv_lds16<*",
     "aios::gemv_q8_rows<*, *, 1, 2, 1>*",
     "aios::gemv_q8_rows<*, *, 1, 1, *>*",
     "aios::gemv_q8_rows<*, *, 1, 2, 2>*",
