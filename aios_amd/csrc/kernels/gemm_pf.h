@@ -1558,6 +1558,78 @@ inline int pf_tail_full(const GemmQArgs& a, int BN, int S) {
   return (T > C && R > 0 && 2 * R <= C) ? T - R : -1;
 }
 
+// Stream-K (round 6, verdict r5 #6): a launch whose output tiles do not fill the chip -- the N = 4096-6144
+// projections of a 512-token chunk have 32-192 tiles for 256 CUs -- runs one workgroup per CU over an
+// equal share of the flattened (tile, K-step) iteration space instead of split-K's equal slices of
+// every tile: workgroup w takes iterations [w * ipw, (w + 1) * ipw), i.e. the tail of one tile and the
+// head of the next, and adds each partial tile into C with the split-K atomics (STORE targets zeroed
+// first).  KG: K-steps per unit (4 for the K-quant pf8c body, which slices on 256-blocks).  A workgroup
+// that runs a second segment barriers first: the previous body's last LDS reads against its prologue DMA.
+template <int QT0, int QT1, int BM, int EPI, int KG, typename Body>
+__device__ __forceinline__ void pf_stream_k(const GemmQArgs& a, int BN, int ipw, Body body) {
+  const int nN = a.N / BN, nM = (a.M + BM - 1) / BM;
+  const int nk = a.K / (64 * KG);
+  const long total = (long)nN * nM * nk;
+  long it = (long)blockIdx.x * ipw;
+  const long end = it + ipw < total ? it + ipw : total;
+  bool first = true;
+  while (it < end) {
+    const int L = (int)(it / nk), k0 = (int)(it - (long)L * nk);
+    const int k1 = (int)(k0 + (end - it) < nk ? k0 + (end - it) : nk);
+    const int tn = L % nN, tm = L / nN;
+    const int m0 = tm * BM, n0 = tn * BN;
+    int seg = 0;
+    if (a.nseg > 1 && n0 >= a.seg_n0[1]) seg = 1;
+    if (a.nseg > 2 && n0 >= a.seg_n0[2]) seg = 2;
+    if (!first) __syncthreads();
+    // S: 1 when this workgroup owns the whole tile (plain epilogue), else atomic partials
+    body(m0, n0, seg, k0 * KG, k1 * KG, (k0 == 0 && k1 == nk) ? 1 : 2);
+    it += k1 - k0;
+    first = false;
+  }
+}
+
+template <int QT0, int QT1, int BM, int WC, int EPI>
+__global__ void __launch_bounds__(256) gemm_pf4sk_kernel(GemmQArgs a, int ipw) {
+  pf_stream_k<QT0, QT1, BM, EPI, 1>(a, 4 * WC, ipw, [&](int m0, int n0, int seg, int kt0, int kt1, int S) {
+    if constexpr (QT0 != QT1) {
+      if (seg == a.nseg - 1) {
+        pf4_body<QT1, BM, WC, EPI>(a, m0, n0, seg, kt0, kt1, S);
+        return;
+      }
+    }
+    pf4_body<QT0, BM, WC, EPI>(a, m0, n0, seg, kt0, kt1, S);
+  });
+}
+
+template <int QT0, int QT1, int BM, int EPI>
+__global__ void __launch_bounds__(512) gemm_pf8sk_kernel(GemmQArgs a, int ipw) {
+  constexpr int KG = QT0 == QT_BF16 ? 1 : 4;
+  pf_stream_k<QT0, QT1, BM, EPI, KG>(a, 256, ipw, [&](int m0, int n0, int seg, int kt0, int kt1, int S) {
+    if constexpr (QT0 == QT_BF16) {
+      pf8_body<QT0, BM, EPI>(a, m0, n0, seg, kt0, kt1, S);
+    } else {
+      if constexpr (QT0 != QT1) {
+        if (seg == a.nseg - 1) {
+          pf8c_body<QT1, BM, EPI>(a, m0, n0, seg, kt0, kt1, S);
+          return;
+        }
+      }
+      pf8c_body<QT0, BM, EPI>(a, m0, n0, seg, kt0, kt1, S);
+    }
+  });
+}
+
+// iterations per workgroup of a stream-K launch over the device's CUs (workgroups = its grid)
+inline int pf_sk_ipw(const GemmQArgs& a, int BM, int BN, int KG, int& grid) {
+  const long total = (long)(a.N / BN) * ((a.M + BM - 1) / BM) * (a.K / (64 * KG));
+  const int cus = device_cu_count();
+  // (even: with an even K-step count per tile every segment is >= 2 units, as the split-K slices)
+  const int ipw = (int)(((total + cus - 1) / cus + 1) & ~1L);
+  grid = (int)((total + ipw - 1) / ipw);
+  return ipw;
+}
+
 template <int QT0, int QT1, int BM>
 constexpr int pf8_lds_bytes() {
   if constexpr (QT0 == QT_BF16) {
@@ -1573,6 +1645,15 @@ template <int QT0, int QT1, int BM>
 void pf8_launch(const GemmQArgs& a, int S, hipStream_t st) {
   constexpr int lds = pf8_lds_bytes<QT0, QT1, BM>();
   static_assert(lds <= 160 * 1024, "LDS");
+  if (S < 0) {  // stream-K (STORE / ACCUM only: partial tiles are atomic adds)
+    int grid = 0;
+    const int ipw = pf_sk_ipw(a, BM, 256, QT0 == QT_BF16 ? 1 : 4, grid);
+    if (a.epi == GEPI_STORE)
+      hipLaunchKernelGGL((gemm_pf8sk_kernel<QT0, QT1, BM, GEPI_STORE>), dim3(grid), dim3(512), lds, st, a, ipw);
+    else
+      hipLaunchKernelGGL((gemm_pf8sk_kernel<QT0, QT1, BM, GEPI_ACCUM>), dim3(grid), dim3(512), lds, st, a, ipw);
+    return;
+  }
   if constexpr (BM == 256 && QT0 != QT_BF16) {
     const int F = pf_tail_full(a, 256, S);
     if (F >= 0) {
@@ -1659,6 +1740,15 @@ template <int QT0, int QT1, int BM, int WC>
 void pf4_launch(const GemmQArgs& a, int S, hipStream_t st) {
   constexpr int lds = pf4_lds_bytes<QT0, QT1, BM, WC>();
   static_assert(lds <= 160 * 1024, "LDS");
+  if (S < 0) {  // stream-K (STORE / ACCUM only)
+    int grid = 0;
+    const int ipw = pf_sk_ipw(a, BM, 4 * WC, 1, grid);
+    if (a.epi == GEPI_STORE)
+      hipLaunchKernelGGL((gemm_pf4sk_kernel<QT0, QT1, BM, WC, GEPI_STORE>), dim3(grid), dim3(256), lds, st, a, ipw);
+    else
+      hipLaunchKernelGGL((gemm_pf4sk_kernel<QT0, QT1, BM, WC, GEPI_ACCUM>), dim3(grid), dim3(256), lds, st, a, ipw);
+    return;
+  }
   if constexpr (BM == 256) {
     const int F = pf_tail_full(a, 4 * WC, S);
     if (F >= 0) {

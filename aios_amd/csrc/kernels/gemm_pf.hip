@@ -24,7 +24,7 @@ static int pf_env(const char* name, int dflt) {
 }
 
 struct PfPlan {
-  int bm = 0, bn = 0, s = 1;
+  int bm = 0, bn = 0, s = 1;  // s < 0: stream-K over the CUs (gemm_pf.h pf_stream_k)
 };
 
 // Modelled time of one launch.  Per workgroup: max(MFMA time at the tile's sustained fraction of the
@@ -42,6 +42,12 @@ static double pf_model(const GemmQArgs& a, int bm, int bn, int S, bool bf) {
   const double slot = bm * 128.0 + bn * (bf ? 128.0 : 48.0);
   const double t_mem = slot * ksteps / 55e9;
   const double t_wg = std::max(t_mfma, t_mem) + 2.5e-6;
+  if (S < 0) {  // stream-K: every CU the same share of the tile x K-step iterations, ~2 partial tiles each
+    const double iters = tiles * (a.K / 64.0), per = std::ceil(iters / cus);
+    const double t_it = std::max(t_mfma, t_mem) / ksteps;
+    return per * t_it + 2 * 2.5e-6 + (double)cus * 2 * bm * bn * 4 / 1.2e12 +
+           (a.epi == GEPI_STORE ? (double)a.M * a.N * 4 / 4e12 : 0.0);
+  }
   double t = std::ceil(tiles * S / cus) * t_wg;
   const double R = std::fmod(tiles, cus);
   if (bm == 256 && S == 1 && (bn == 128 || !bf) && tiles > cus && R > 0 && 2 * R <= cus)  // tail split
@@ -83,6 +89,14 @@ static std::map<PfKey, PfPlan>& pf_tuned_s1() {
   return m;
 }
 static bool pf_no_split(const GemmQArgs& a) { return a.epi == GEPI_SWIGLU_BF16 || a.epi == GEPI_QKV; }
+// stream-K: STORE / ACCUM launches whose tiles leave CUs idle, with an even K-step count per tile
+// (every stream-K segment then spans >= 2 steps / 256-blocks); AIOS_GEMM_PF_SK=0 keeps it out of plans
+static bool pf_sk_ok(const GemmQArgs& a, int bm, int bn, bool bf) {
+  if (pf_no_split(a) || !pf_env("AIOS_GEMM_PF_SK", 1)) return false;
+  const int units = bn == 256 && !bf ? a.K / 256 : a.K / 64;
+  const double tiles = (double)((a.M + bm - 1) / bm) * (a.N / bn);
+  return units % 2 == 0 && units >= 4 && tiles < 2.0 * device_cu_count();
+}
 
 // every plan the launcher could run for these args (ksplit > 0 pins the split)
 static std::vector<PfPlan> pf_candidates(const GemmQArgs& a, bool bf) {
@@ -91,8 +105,9 @@ static std::vector<PfPlan> pf_candidates(const GemmQArgs& a, bool bf) {
   for (int bm : {256, 128, 64})
     for (int bn : {256, 128}) {
       if (!pf_tile_ok(a, bn)) continue;
-      for (int S : {1, 2, 3, 4, 6, 8, 12, 16}) {
+      for (int S : {1, 2, 3, 4, 6, 8, 12, 16, -1}) {
         if (a.ksplit > 0 && S != a.ksplit) continue;
+        if (S < 0 && !pf_sk_ok(a, bm, bn, bf)) continue;
         if (S > 1 && (pf_no_split(a) || nk / S < 2)) continue;
         if (!bf && bn == 256 && (a.K / 256) / S < 1) continue;
         PfPlan p;
@@ -135,9 +150,10 @@ static PfPlan pf_model_plan(const GemmQArgs& a, bool bf, bool s1_only) {
     for (int bn : {256, 128}) {
       if (fbm && (bm != fbm || bn != fbn)) continue;
       if (!pf_tile_ok(a, bn)) continue;
-      for (int S : {1, 2, 3, 4, 6, 8, 12, 16}) {
+      for (int S : {1, 2, 3, 4, 6, 8, 12, 16, -1}) {
         if (a.ksplit > 0 && S != a.ksplit) continue;
-        if (a.ksplit <= 0 && split > 0 && S != split) continue;
+        if (a.ksplit <= 0 && split != 0 && S != split) continue;  // (AIOS_GEMM_PF_SPLIT=-1: stream-K)
+        if (S < 0 && (s1_only || !pf_sk_ok(a, bm, bn, bf))) continue;
         if (S > 1 && (s1_only || pf_no_split(a) || nk / S < 2)) continue;
         if (!bf && bn == 256 && (a.K / 256) / S < 1) continue;  // pf8c slices whole 256-blocks
         const double t = pf_model(a, bm, bn, S, bf);
@@ -157,8 +173,8 @@ static PfPlan pf_model_plan(const GemmQArgs& a, bool bf, bool s1_only) {
 static bool pf_eligible(const GemmQArgs& a);
 static bool pf_run(const GemmQArgs& a, const PfPlan& p, hipStream_t st) {
   const int qt0 = a.seg[0].qtype, qt1 = a.seg[a.nseg - 1].qtype;
-  if (p.s > 1 && a.epi == GEPI_QKV) return false;  // (plans keep S = 1 for it; a pinned split declines)
-  if (p.s > 1 && a.epi == GEPI_STORE)
+  if (p.s != 1 && a.epi == GEPI_QKV) return false;  // (plans keep S = 1 for it; a pinned split declines)
+  if (p.s != 1 && a.epi == GEPI_STORE)
     HIP_CHECK(hipMemset2DAsync(a.C, (size_t)a.ldc * 4, 0, (size_t)a.N * 4, a.M, st));
   if (qt0 == QT_Q4_K && qt1 == QT_Q4_K) return pf_launch_fmt<QT_Q4_K, QT_Q4_K>(a, p.bm, p.bn, p.s, st);
   if (qt0 == QT_Q6_K && qt1 == QT_Q6_K) return pf_launch_fmt<QT_Q6_K, QT_Q6_K>(a, p.bm, p.bn, p.s, st);
@@ -232,7 +248,7 @@ int gemm_pf_autotune(const GemmQArgs& a, hipStream_t st) {
       bt = ms;
       best = p;
     }
-    if (p.s == 1 && ms < bt1) {
+    if (p.s == 1 && ms < bt1) {  // (stream-K is not an S = 1 plan either)
       bt1 = ms;
       best1 = p;
     }
@@ -283,7 +299,7 @@ void gemm_pf_import(const std::vector<int>& v) {
 bool gemm_pf_serves(const GemmQArgs& a) {
   if (!pf_env("AIOS_GEMM_PF", 1) || a.M < pf_env("AIOS_GEMM_PF_MIN_M", 33) || !pf_eligible(a)) return false;
   const PfPlan p = pf_plan(a, a.seg[0].qtype == QT_BF16);
-  return p.bm != 0 && !(p.s > 1 && a.epi == GEPI_QKV);
+  return p.bm != 0 && !(p.s != 1 && a.epi == GEPI_QKV);
 }
 
 // the plan the launcher would pick (bindings / tools)

@@ -67,15 +67,16 @@ def test_greedy_decode_token_exact(model_files, recipe, q8):
 @pytest.mark.parametrize("gemm_prefill", ["0", "1"])
 def test_fp8_kv_cache_matches_reference(model_files, monkeypatch, recipe, gemm_prefill):
     """the fp8 e4m3 KV cache (kv_dtype='fp8_e4m3', per-layer K / V scales) against the
-    fp32 reference model with the same fp8 rounding of K / V -- prefill logits (GEMV and MFMA prefill
-    paths, 70-token prompt) within the bf16-KV tolerance, and against the bf16-KV engine: the fp8
-    cache's own error stays within 5 % of the logit scale and greedy decoding agrees with the
-    fp8-emulating reference over 64 tokens."""
+    fp32 reference model with the same fp8 rounding of K / V (fp32 GEMV activations on both sides, so
+    the KV cache is the only approximation): prefill logits (GEMV and MFMA prefill paths, 70-token
+    prompt) within the bf16-KV tolerance; the fp8 cache's own error against the bf16-KV engine within 5 %
+    of the logit scale; 64 teacher-forced decode steps (the reference's greedy tokens fed back, so one
+    near-tie does not cascade) with every step's logits within tolerance and >= 62 of 63 argmaxes equal."""
     from aios_amd.runtime.loader import load_engine
 
     monkeypatch.setenv("AIOS_PREFILL_GEMM", gemm_prefill)
     path = model_files[recipe]
-    eng, cfg, _ = load_engine(path, max_ctx=256, kv_dtype="fp8_e4m3")
+    eng, cfg, _ = load_engine(path, max_ctx=256, kv_dtype="fp8_e4m3", act_q8=False)
     assert eng.kv_fp8 == 1 and len(eng.kv_scales) == 2 * cfg.n_layers
     scales = [0.05 if i % 2 == 0 else 0.02 for i in range(2 * cfg.n_layers)]
     eng.set_kv_scales(scales)
@@ -85,19 +86,22 @@ def test_fp8_kv_cache_matches_reference(model_files, monkeypatch, recipe, gemm_p
     rl = ref.forward(prompt)[-1]
     sc = rl.abs().max().item()
     assert (logits - rl).abs().max().item() < 2e-2 * max(sc, 1.0)
-    bf, _, _ = load_engine(path, max_ctx=256)
+    bf, _, _ = load_engine(path, max_ctx=256, act_q8=False)
     lb = torch.from_numpy(np.asarray(bf.prefill(0, prompt, 0, True)))
     assert (logits - lb).abs().max().item() < 5e-2 * max(sc, 1.0)
-    # greedy decode over 64 tokens vs the fp8-emulating reference
+    # 64 decode steps, teacher-forced with the fp8-emulating reference's greedy tokens
     want = ref.greedy(prompt[:8], 64)
-    tok = int(np.argmax(np.asarray(eng.prefill(1, prompt[:8], 0, True))))
-    got, pos = [tok], 8
-    for _ in range(63):
-        tok = eng.decode([1], [tok], [pos])[0]
-        pos += 1
-        got.append(tok)
-    agree = sum(a == b for a, b in zip(got, want))
-    assert agree >= 60, (agree, got, want)
+    assert int(np.argmax(np.asarray(eng.prefill(1, prompt[:8], 0, True)))) == want[0]
+    ctx = list(prompt[:8])
+    agree, worst = 0, 0.0
+    for i in range(63):
+        eng.decode([1], [want[i]], [8 + i])
+        el = torch.from_numpy(np.asarray(eng.last_logits(1))[0])
+        ctx.append(want[i])
+        rl = ref.forward(ctx)[-1]
+        worst = max(worst, (el - rl).abs().max().item() / max(rl.abs().max().item(), 1.0))
+        agree += int(el.argmax()) == want[i + 1]
+    assert worst < 2e-2 and agree >= 62, (worst, agree)
 
 
 def test_batched_decode_matches_single(model_files):

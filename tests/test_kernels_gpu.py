@@ -1184,6 +1184,40 @@ def test_gemm_pf_production_shapes_vs_unquantized(E, monkeypatch, fmt, N, K, spl
     assert per_row < 1e-2, per_row
 
 
+@pytest.mark.parametrize("fmt,N,K", [("mixed6144", 6144, 4096), ("q4k", 4096, 4096), ("q6k", 4096, 14336),
+                                     ("bf16", 2048, 2048)])
+@pytest.mark.parametrize("tile", ["128x128", "128x256", "256x256"])
+@pytest.mark.parametrize("epi", ["store", "accum"])
+def test_gemm_pf_stream_k(E, monkeypatch, fmt, N, K, tile, epi):
+    """Stream-K (AIOS_GEMM_PF_SPLIT=-1): one workgroup per CU over an equal share of the (tile, K-step)
+    iterations, partial tiles added atomically -- the 512-token shapes of Mistral's QKV stack, O and
+    Q6_K down, and a bf16 matrix, every body (pf4 128-column, pf8c 256-column K-quant, pf8 bf16),
+    against the unquantized fp64 product"""
+    monkeypatch.setenv("AIOS_GEMM_PF_TILE", tile)
+    monkeypatch.setenv("AIOS_GEMM_PF_SPLIT", "-1")
+    segs = {"mixed6144": [(GGMLType.Q4_K, 4096), (GGMLType.Q4_K, 1024), (GGMLType.Q6_K, 1024)],
+            "q4k": [(GGMLType.Q4_K, N)], "q6k": [(GGMLType.Q6_K, N)], "bf16": [(GGMLType.BF16, N)]}[fmt]
+    key = ("sk", fmt, K)
+    if key not in _pf_cache:
+        mats, refs = zip(*[qmat(E, t, n, K, seed=170 + i, std=0.02) for i, (t, n) in enumerate(segs)])
+        _pf_cache[key] = (list(mats), torch.cat(refs, 0))
+    mats, W = _pf_cache[key]
+    M = 512
+    if E.gemm_pf_plan(mats, M, E.GEPI_ACCUM, 0)[2] != -1:
+        pytest.skip("stream-K not eligible for this tile / shape")
+    x = torch.randn(M, K, generator=torch.Generator().manual_seed(K + N))
+    A = x.to(torch.bfloat16).cuda()
+    C = torch.full((M, N), 0.5, device="cuda")
+    E.gemm_q(A.data_ptr(), K, mats, M, C.data_ptr(), 0, N, E.GEPI_STORE if epi == "store" else E.GEPI_ACCUM, stream(), 0)
+    torch.cuda.synchronize()
+    ref = x.double() @ W.double().T + (0.0 if epi == "store" else 0.5)
+    got = C.cpu().double()
+    rel = float((got - ref).norm() / ref.norm())
+    assert rel < 6e-3, rel
+    per_row = ((got - ref).norm(dim=1) / ref.norm(dim=1)).max().item()
+    assert per_row < 1e-2, per_row
+
+
 @pytest.mark.parametrize("tile", ["256x256", "128x256", "64x128"])
 @pytest.mark.parametrize("M", [40, 300])
 def test_gemm_pf_swiglu(E, monkeypatch, tile, M):
@@ -1205,4 +1239,4 @@ def test_gemm_pf_serves_prefill_shapes(E):
         mats, _ = pf_mats(E, fmt, 1024)
         for M in (33, 64, 128, 512, 2048):
             bm, bn, s = E.gemm_pf_plan(mats, M, E.GEPI_ACCUM, 0)
-            assert bm in (64, 128, 256) and bn in (128, 256) and s >= 1, (fmt, M, bm, bn, s)
+            assert bm in (64, 128, 256) and bn in (128, 256) and (s >= 1 or s == -1), (fmt, M, bm, bn, s)
