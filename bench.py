@@ -150,16 +150,17 @@ def measure_grpc(timeout_s: float = 120.0):
     return asyncio.run(asyncio.wait_for(main_async(ns), timeout_s))
 
 
-def measure_coresident(steps: int = 256, prompt: int = 128):
+def measure_coresident(steps: int = 256, prompt: int = 128, cu_split: int = 0):
     """BASELINE.json config 4: TinyLlama-1.1B and Mistral-7B resident together on one GPU, each
     replaying its decode graph on its own stream, dispatched concurrently from two host threads
-    (tools/bench_coresident.py): per-tier tok/s alone and concurrent, the aggregate, HBM per tier."""
+    (tools/bench_coresident.py): per-tier tok/s alone and concurrent, the aggregate, HBM per tier.
+    cu_split > 0: each tier on its own CUs (CU-masked streams, grids sized to them)."""
     import argparse as _ap
 
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "tools"))
     from bench_coresident import run
 
-    return run(_ap.Namespace(steps=steps, prompt=prompt))
+    return run(_ap.Namespace(steps=steps, prompt=prompt, cu_split=cu_split, priority=""))
 
 
 def measure_tp(args, rank: int, world: int, device: int, gloo):
@@ -323,6 +324,13 @@ def main():
             print(f"tinyllama_bf16_grpc failed: {grpc_res['error']}", file=sys.stderr, flush=True)
         try:
             coresident = measure_coresident()
+            # the same with each tier on its own CUs (TinyLlama 128 / Mistral 128: the split with the
+            # highest aggregate of 64 / 96 / 128 measured, profiles/coresident_r6.txt)
+            try:
+                part = measure_coresident(cu_split=128)
+                coresident["cu_partitioned"] = {k: part[k] for k in part if k.endswith("_tok_s") or k == "cu_split"}
+            except Exception as e:  # noqa: BLE001
+                coresident["cu_partitioned"] = {"error": f"{type(e).__name__}: {e}"[:300]}
         except Exception as e:  # noqa: BLE001
             coresident = {"error": f"{type(e).__name__}: {e}"[:300]}
             print(f"coresident failed: {coresident['error']}", file=sys.stderr, flush=True)
