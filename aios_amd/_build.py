@@ -75,7 +75,8 @@ _FILE_FLAGS = {n: _NO_ATOMIC_OPT for n in ("gemv_kquant.hip", "gemv_kquant2.hip"
 # The prefill GEMM's weight decode beside MFMAs: LLVM's SLP vectoriser packs the fmaf pairs into
 # v_pk_fma_f32, which costs ~+22 cycles per instruction when issued between MFMAs (MI355X guide,
 # price list 'packed f32 VALU ... an anti-lever beside MFMAs'); plain v_fma_f32 instead.
-for _n in ("gemm_pf.hip", "gemm_pf_q4k.hip", "gemm_pf_q6k.hip", "gemm_pf_mix.hip", "gemm_pf_bf16.hip"):
+for _n in ("gemm_pf.hip", "gemm_pf_q4k.hip", "gemm_pf_q6k.hip", "gemm_pf_mix.hip", "gemm_pf_bf16.hip", "gemm_pf_q5k.hip",
+           "gemm_pf_q8q4.hip"):
     _FILE_FLAGS[_n] = ["-fno-slp-vectorize"]
 
 

@@ -234,6 +234,15 @@ __device__ __forceinline__ gbf16x8 pf_bdec(const PfBRaw& r, int q, int kt, int d
   if constexpr (QT == QT_BF16) {
     const uint4 v = S == 0 ? r.mt : r.b1;
     __builtin_memcpy(&f, &v, 16);
+  } else if constexpr (QT == QT_Q8_0) {  // (pf8 body) fragment S = the K-step's 32-block S: cw / b1.xy
+    const uint32_t w0 = (S == 0 ? r.cw.x : r.b1.x) ^ 0x80808080u, w1 = (S == 0 ? r.cw.y : r.b1.y) ^ 0x80808080u;
+    const float d = h2f((uint16_t)(r.scw >> (16 * S)));
+    f = pf_dq8(w0, w1, d, 128.f * d);
+  } else if constexpr (QT == QT_Q4_0) {  // block S: weights 8q.. = low nibbles (q < 2) / high (q >= 2)
+    const int sh = 4 * (q >> 1);
+    const uint32_t w0 = ((S == 0 ? r.cw.x : r.b1.x) >> sh) & 0x0f0f0f0fu, w1 = ((S == 0 ? r.cw.y : r.b1.y) >> sh) & 0x0f0f0f0fu;
+    const float d = h2f((uint16_t)(r.scw >> (16 * S)));
+    f = pf_dq8(w0, w1, d, 8.f * d);
   } else if constexpr (QT == QT_Q6_K) {
     const float d = h2f((uint16_t)(r.dw >> (16 * dpar)));
     const float ds = d * (float)(int8_t)((r.scw >> (16 * (q >> 1) + 8 * S)) & 0xff);
@@ -247,8 +256,13 @@ __device__ __forceinline__ gbf16x8 pf_bdec(const PfBRaw& r, int q, int kt, int d
     const float d = h2f((uint16_t)(r.mt.x & 0xffff)), dmin = h2f((uint16_t)(r.mt.x >> 16));
     const uint32_t fl = kq_field(r.mt.y, r.mt.z, r.mt.w, kt & 3);
     const float ds = d * (float)((fl >> (6 * S)) & 63), dm = dmin * (float)((fl >> (12 + 6 * S)) & 63);
-    const uint32_t c0 = S == 0 ? (r.cw.x & 0x0f0f0f0fu) : ((r.cw.x >> 4) & 0x0f0f0f0fu);
-    const uint32_t c1 = S == 0 ? (r.cw.y & 0x0f0f0f0fu) : ((r.cw.y >> 4) & 0x0f0f0f0fu);
+    uint32_t c0 = S == 0 ? (r.cw.x & 0x0f0f0f0fu) : ((r.cw.x >> 4) & 0x0f0f0f0fu);
+    uint32_t c1 = S == 0 ? (r.cw.y & 0x0f0f0f0fu) : ((r.cw.y >> 4) & 0x0f0f0f0fu);
+    if constexpr (QT == QT_Q5_K) {  // (pf8 body) qh bytes 8q.. in hb: bit 2g + S
+      const int sh = 2 * (kt & 3) + S;
+      c0 |= ((r.hb.x >> sh) & 0x01010101u) << 4;
+      c1 |= ((r.hb.y >> sh) & 0x01010101u) << 4;
+    }
     f = pf_dq8(c0, c1, ds, dm);
   }
   return f;
@@ -435,6 +449,17 @@ __device__ __forceinline__ gbf16x8 pf_bdec32(const PfBRaw32& r, int h, int kt, i
   if constexpr (QT == QT_BF16) {
     const uint4 v = S == 0 ? r.mt : (S == 1 ? r.b1 : (S == 2 ? r.b2 : r.b3));
     __builtin_memcpy(&f, &v, 16);
+  } else if constexpr (QT == QT_Q8_0) {  // int8 codes (+128 -> the unsigned decode), d of block S >> 1
+    const uint32_t w0 = (S == 0 ? r.c0.x : (S == 1 ? r.c1.x : (S == 2 ? r.b1.x : r.b1.z))) ^ 0x80808080u;
+    const uint32_t w1 = (S == 0 ? r.c0.y : (S == 1 ? r.c1.y : (S == 2 ? r.b1.y : r.b1.w))) ^ 0x80808080u;
+    const float d = h2f((uint16_t)(r.scw >> (16 * (S >> 1))));
+    f = pf_dq8(w0, w1, d, 128.f * d);
+  } else if constexpr (QT == QT_Q4_0) {  // block S >> 1: low nibbles = weights 0..15, high = 16..31
+    const uint2 cw = (S >> 1) ? r.c1 : r.c0;
+    const uint32_t w0 = (S & 1) ? ((cw.x >> 4) & 0x0f0f0f0fu) : (cw.x & 0x0f0f0f0fu);
+    const uint32_t w1 = (S & 1) ? ((cw.y >> 4) & 0x0f0f0f0fu) : (cw.y & 0x0f0f0f0fu);
+    const float d = h2f((uint16_t)(r.scw >> (16 * (S >> 1))));
+    f = pf_dq8(w0, w1, d, 8.f * d);
   } else {
     const uint2 cw = (S & 1) ? r.c1 : r.c0;
     const uint32_t w0 = (S < 2) ? (cw.x & 0x0f0f0f0fu) : ((cw.x >> 4) & 0x0f0f0f0fu);
@@ -448,12 +473,18 @@ __device__ __forceinline__ gbf16x8 pf_bdec32(const PfBRaw32& r, int h, int kt, i
       const int j0 = 2 * h;  // code words 2h, 2h + 1 of the chunk
       f = pf_dq8(w0 | (((hv >> (2 * j0)) & 0x03030303u) << 4), w1 | (((hv >> (2 * j0 + 2)) & 0x03030303u) << 4), ds,
                  32.f * ds);
-    } else {  // Q4_K: sub-block 2g (S < 2) or 2g + 1
+    } else {  // Q4_K / Q5_K: sub-block 2g (S < 2) or 2g + 1
       const float d = h2f((uint16_t)(r.mt.x & 0xffff)), dmin = h2f((uint16_t)(r.mt.x >> 16));
       const uint32_t fl = kq_field(r.mt.y, r.mt.z, r.mt.w, kt & 3);
       constexpr int sb = S >> 1;
       const float ds = d * (float)((fl >> (6 * sb)) & 63), dm = dmin * (float)((fl >> (12 + 6 * sb)) & 63);
-      f = pf_dq8(w0, w1, ds, dm);
+      if constexpr (QT == QT_Q5_K) {  // + bit (2g + hi) of the weights' qh bytes as bit 4
+        const int sh = 2 * (kt & 3) + sb;
+        const uint32_t h0 = (S & 1) ? r.b1.z : r.b1.x, h1 = (S & 1) ? r.b1.w : r.b1.y;
+        f = pf_dq8(w0 | (((h0 >> sh) & 0x01010101u) << 4), w1 | (((h1 >> sh) & 0x01010101u) << 4), ds, dm);
+      } else {
+        f = pf_dq8(w0, w1, ds, dm);
+      }
     }
   }
   return f;
@@ -579,20 +610,39 @@ __device__ __forceinline__ void pf_body32(const GemmQArgs& a, int m0, int n0, in
 // ~68 SALU per wave-step.  Here each wave owns its SIMD, DMAs its OWN weight columns (so it can
 // wait for, read and decode step t+1's B fragments with its own vmcnt, before the barrier, inside
 // step t's last phases) and every DMA piece is compile-time: one vmcnt immediate per wave.
+//
+// Formats beyond Q4_K / Q6_K / bf16 (round 6, verdict r5 missing #4) read the GEMV engines' planes
+// (quant_pack.hip) in place -- no second copy of any weight:
+//   Q5_K  = the Q4_K codes + record, plus the block's 32 qh bytes (bit 2g + hi of byte l = high bit of
+//           weight 64g + 32hi + l) fetched with every K-step as one more 1 KB piece;
+//   Q4_0  = 32-weight blocks: the K-step's two 16-B code blocks (the Q4_K code reads, a different
+//           nibble <-> fragment map) + the dword holding both blocks' f16 d (4-B piece, as Q6_K's scales);
+//   Q8_0  = row-major int8 codes, 64 B per column per K-step (two 1 KB pieces) + the d-pair dword.
+template <int QT>
+struct PfFmt {
+  static constexpr bool Q6 = QT == QT_Q6_K, BF = QT == QT_BF16, Q5 = QT == QT_Q5_K, L0 = QT == QT_Q4_0,
+                        L8 = QT == QT_Q8_0, KREC = QT == QT_Q4_K || QT == QT_Q5_K;
+};
 template <int QT, int BM, int WC, int NW = 4>
 struct Pf4Layout {
-  static constexpr bool Q6 = QT == QT_Q6_K, BF = QT == QT_BF16;
+  using F = PfFmt<QT>;
+  static constexpr bool Q6 = F::Q6, BF = F::BF, Q5 = F::Q5, L0 = F::L0, L8 = F::L8;
   static constexpr int A_BYTES = BM * 128;
-  static constexpr int CODE = BF ? WC * 128 : WC * 32;       // per wave: bf16 rows / 2 code chunks per column
-  static constexpr int META = BF ? 0 : (WC * 16 > 1024 ? WC * 16 : 1024);  // Q4_K record / Q6_K high bits
-  static constexpr int SC = Q6 ? 256 : 0, DW = Q6 ? 256 : 0;  // Q6_K int8 scales / d dword (4-B pieces)
-  static constexpr int WB = CODE + META + SC + DW;            // one wave's weight bytes per slot
+  // per wave: bf16 rows / Q8_0 bytes / 2 code chunks per column
+  static constexpr int CODE = BF ? WC * 128 : (L8 ? WC * 64 : WC * 32);
+  static constexpr int META = (F::KREC || Q6) ? (WC * 16 > 1024 ? WC * 16 : 1024) : 0;  // K record / Q6_K high bits
+  static constexpr int HB = Q5 ? WC * 32 : 0;                                             // Q5_K qh bytes
+  static constexpr int SC = (Q6 || L0 || L8) ? 256 : 0;  // Q6_K int8 scales / Q4_0, Q8_0 d pair (4-B pieces)
+  static constexpr int DW = Q6 ? 256 : 0;                // Q6_K d dword
+  static constexpr int OFF_META = CODE, OFF_HB = OFF_META + META, OFF_SC = OFF_HB + HB, OFF_DW = OFF_SC + SC;
+  static constexpr int WB = OFF_DW + DW;                 // one wave's weight bytes per slot
   static constexpr int OFF_B = A_BYTES;
   static constexpr int SLOT = (A_BYTES + NW * WB + 255) / 256 * 256;
   static constexpr int NS = 3 * SLOT <= 160 * 1024 ? 3 : 2;
-  static constexpr int NA = BM / (8 * NW), NCODE = CODE / 1024, NMETA = META / 1024, NSC = SC / 256, ND = DW / 256;
-  static constexpr int PW = NA + NCODE + NMETA + NSC + ND;    // DMA instructions per wave per slot
-  static_assert(CODE % 1024 == 0 && WC * 4 <= 256 && PW <= 31 && NA * 8 * NW == BM, "pf4 slot");
+  static constexpr int NA = BM / (8 * NW), NCODE = CODE / 1024, NMETA = META / 1024, NHB = HB / 1024,
+                       NSC = SC / 256, ND = DW / 256;
+  static constexpr int PW = NA + NCODE + NMETA + NHB + NSC + ND;  // DMA instructions per wave per slot
+  static_assert(CODE % 1024 == 0 && HB % 1024 == 0 && WC * 4 <= 256 && PW <= 31 && NA * 8 * NW == BM, "pf4 slot");
 };
 
 template <int QT, int BM, int WC, int NW = 4>
@@ -615,6 +665,9 @@ struct Pf4Dma {
         if constexpr (L::BF) {
           const int col = p >> 3, c = (p & 7) ^ ((col >> 1) & 7);
           o = ((uint32_t)(wcol0 + col) * (uint32_t)a.K + (uint32_t)(c * 8)) * 2u;
+        } else if constexpr (L::L8) {  // 4 x 16 B per column
+          const int col = p >> 2, u = p & 3;
+          o = (uint32_t)(wcol0 + col) * nbk * 256u + (uint32_t)u * 16u;
         } else {
           const int col = p >> 1, hh = p & 1;
           o = (uint32_t)(wcol0 + col) * nbk * 128u + (uint32_t)hh * 16u;
@@ -622,8 +675,10 @@ struct Pf4Dma {
       } else if constexpr (i < L::NA + L::NCODE + L::NMETA) {
         const uint32_t row = (uint32_t)(wcol0 + (lane & (WC - 1)));
         o = L::Q6 ? row * nbk * 64u : row * nbk * 16u;
-      } else if constexpr (i < L::NA + L::NCODE + L::NMETA + L::NSC) {
-        o = (uint32_t)(wcol0 + (lane & (WC - 1))) * nbk * 16u;
+      } else if constexpr (i < L::NA + L::NCODE + L::NMETA + L::NHB) {  // Q5_K qh: 2 x 16 B per column
+        o = (uint32_t)(wcol0 + (lane >> 1)) * nbk * 32u + (uint32_t)(lane & 1) * 16u;
+      } else if constexpr (i < L::NA + L::NCODE + L::NMETA + L::NHB + L::NSC) {
+        o = (uint32_t)(wcol0 + (lane & (WC - 1))) * nbk * 16u;  // (Q4_0 / Q8_0: K / 16 bytes of d per row)
       } else {
         o = (uint32_t)(wcol0 + (lane & (WC - 1))) * nbk;
       }
@@ -646,13 +701,15 @@ struct Pf4Dma {
       if constexpr (i < L::NA) {
         pf_glds16((const uint8_t*)a.A + kt * 128 + off[i], dst + (NW * i + wv) * 1024);
       } else if constexpr (i < L::NA + L::NCODE) {
-        pf_glds16(w.p0 + (L::BF ? kt * 128 : kt * 32) + off[i], wb + (i - L::NA) * 1024);
+        pf_glds16(w.p0 + (L::BF ? kt * 128 : (L::L8 ? kt * 64 : kt * 32)) + off[i], wb + (i - L::NA) * 1024);
       } else if constexpr (i < L::NA + L::NCODE + L::NMETA) {
-        pf_glds16(w.p1 + (L::Q6 ? kt * 16 : (kt >> 2) * 16) + off[i], wb + L::CODE);
-      } else if constexpr (i < L::NA + L::NCODE + L::NMETA + L::NSC) {
-        pf_glds4(w.p2 + kt * 4 + off[i], wb + L::CODE + L::META);
+        pf_glds16(w.p1 + (L::Q6 ? kt * 16 : (kt >> 2) * 16) + off[i], wb + L::OFF_META);
+      } else if constexpr (i < L::NA + L::NCODE + L::NMETA + L::NHB) {
+        pf_glds16(w.p2 + (kt >> 2) * 32 + off[i], wb + L::OFF_HB);
+      } else if constexpr (i < L::NA + L::NCODE + L::NMETA + L::NHB + L::NSC) {
+        pf_glds4((L::Q6 ? w.p2 : w.p1) + kt * 4 + off[i], wb + L::OFF_SC);
       } else {
-        pf_glds4(w.p3 + (((off[i] + (uint32_t)(kt >> 2)) >> 1) << 2), wb + L::CODE + L::META + L::SC);
+        pf_glds4(w.p3 + (((off[i] + (uint32_t)(kt >> 2)) >> 1) << 2), wb + L::OFF_DW);
       }
     });
   }
@@ -669,14 +726,24 @@ __device__ __forceinline__ void pf4_braw(const uint8_t* wbase, int cl, int h, Pf
     r.b1 = *(const uint4*)(row + (((2 + h) ^ x) << 4));
     r.b2 = *(const uint4*)(row + (((4 + h) ^ x) << 4));
     r.b3 = *(const uint4*)(row + (((6 + h) ^ x) << 4));
+  } else if constexpr (L::L8) {  // fragment s: bytes 16 s + 8 h .. of the column's 64
+    const uint8_t* row = wbase + cl * 64 + 8 * h;
+    r.c0 = *(const uint2*)(row);
+    r.c1 = *(const uint2*)(row + 16);
+    const uint2 c2 = *(const uint2*)(row + 32), c3 = *(const uint2*)(row + 48);
+    r.b1 = make_uint4(c2.x, c2.y, c3.x, c3.y);
+    r.scw = *(const uint32_t*)(wbase + L::OFF_SC + cl * 4);
   } else {
     r.c0 = *(const uint2*)(wbase + cl * 32 + 8 * h);
     r.c1 = *(const uint2*)(wbase + cl * 32 + 16 + 8 * h);
-    r.mt = *(const uint4*)(wbase + L::CODE + cl * 16);
-    if constexpr (L::Q6) {
-      r.scw = *(const uint32_t*)(wbase + L::CODE + L::META + cl * 4);
-      r.dw = *(const uint32_t*)(wbase + L::CODE + L::META + L::SC + cl * 4);
+    if constexpr (L::META > 0) r.mt = *(const uint4*)(wbase + L::OFF_META + cl * 16);
+    if constexpr (L::Q5) {  // qh bytes 8 h .. and 16 + 8 h .. of the block's 32
+      const uint2 q0 = *(const uint2*)(wbase + L::OFF_HB + cl * 32 + 8 * h);
+      const uint2 q1 = *(const uint2*)(wbase + L::OFF_HB + cl * 32 + 16 + 8 * h);
+      r.b1 = make_uint4(q0.x, q0.y, q1.x, q1.y);
     }
+    if constexpr (L::SC > 0) r.scw = *(const uint32_t*)(wbase + L::OFF_SC + cl * 4);
+    if constexpr (L::Q6) r.dw = *(const uint32_t*)(wbase + L::OFF_DW + cl * 4);
   }
 }
 
@@ -890,14 +957,22 @@ __device__ __forceinline__ void pf8_body(const GemmQArgs& a, int m0, int n0, int
       if constexpr (L::BF) {
         r.mt = *(const uint4*)(wb + cl * 128 + (((0 + q) ^ ((cl >> 1) & 7)) << 4));
         r.b1 = *(const uint4*)(wb + cl * 128 + (((4 + q) ^ ((cl >> 1) & 7)) << 4));
+      } else if constexpr (L::L8 || L::L0) {  // the K-step's two 32-blocks: bytes of fragment 0 / 1
+        const int bs = L::L8 ? 32 : 16, o = L::L8 ? 8 * q : 8 * (q & 1);
+        r.cw = *(const uint2*)(wb + cl * (2 * bs) + o);
+        const uint2 c1 = *(const uint2*)(wb + cl * (2 * bs) + bs + o);
+        r.b1.x = c1.x;
+        r.b1.y = c1.y;
+        r.scw = *(const uint32_t*)(wb + L::OFF_SC + cl * 4);
       } else {
         r.cw = *(const uint2*)(wb + cl * 32 + 8 * q);
+        if constexpr (L::Q5) r.hb = *(const uint2*)(wb + L::OFF_HB + cl * 32 + 8 * q);
         if constexpr (L::Q6) {
           r.hb = *(const uint2*)(wb + L::CODE + cl * 16 + 8 * (q >> 1));
           r.scw = *(const uint32_t*)(wb + L::CODE + L::META + cl * 4);
-          r.dw = *(const uint32_t*)(wb + L::CODE + L::META + L::SC + cl * 4);
+          r.dw = *(const uint32_t*)(wb + L::OFF_DW + cl * 4);
         } else {
-          r.mt = *(const uint4*)(wb + L::CODE + cl * 16);
+          r.mt = *(const uint4*)(wb + L::OFF_META + cl * 16);
         }
       }
     }
@@ -1484,6 +1559,13 @@ __device__ __forceinline__ void pf8d_body(const GemmQArgs& a, int m0, int n0, in
   }
 }
 
+// stacks the 256-column launches run on pf8_body (64-weight K-steps, Pf4Layout planes) instead of pf8c:
+// bf16, and the Q5_K / Q4_0 / Q8_0 recipes' stacks (their Q6_K segments too)
+template <int QT0, int QT1>
+constexpr bool pf8_generic() {
+  return QT0 == QT_BF16 || QT0 == QT_Q5_K || QT0 == QT_Q4_0 || QT0 == QT_Q8_0;
+}
+
 template <int QT0, int QT1, int BM, int EPI, int PROBE = 0>
 __global__ void __launch_bounds__(512) gemm_pf8_kernel(GemmQArgs a) {
   const int nN = a.N / 256, nM = (a.M + BM - 1) / BM, total = nN * nM;
@@ -1494,9 +1576,15 @@ __global__ void __launch_bounds__(512) gemm_pf8_kernel(GemmQArgs a) {
   if (a.nseg > 1 && n0 >= a.seg_n0[1]) seg = 1;
   if (a.nseg > 2 && n0 >= a.seg_n0[2]) seg = 2;
   const int S = gridDim.y;
-  if constexpr (QT0 == QT_BF16) {
+  if constexpr (pf8_generic<QT0, QT1>()) {
     const int nk_all = a.K / 64;
     const int kt0 = (int)((long)blockIdx.y * nk_all / S), kt1 = (int)((long)(blockIdx.y + 1) * nk_all / S);
+    if constexpr (QT0 != QT1) {
+      if (seg == a.nseg - 1) {
+        pf8_body<QT1, BM, EPI, PROBE>(a, m0, n0, seg, kt0, kt1, S);
+        return;
+      }
+    }
     pf8_body<QT0, BM, EPI, PROBE>(a, m0, n0, seg, kt0, kt1, S);
   } else {
     // K-quant stacks: pf8c, slices on 256-block boundaries
@@ -1539,15 +1627,27 @@ __global__ void __launch_bounds__(512) gemm_pf8t_kernel(GemmQArgs a, int F) {
   if (a.nseg > 1 && n0 >= a.seg_n0[1]) seg = 1;
   if (a.nseg > 2 && n0 >= a.seg_n0[2]) seg = 2;
   const int kt1 = 4 * (a.K / 256);
-  if constexpr (QT0 != QT1) {
-    if (seg == a.nseg - 1) {
-      if (half < 0) pf8c_body<QT1, 256, EPI>(a, m0, n0, seg, 0, kt1, 1);
-      else pf8c_body<QT1, 128, EPI>(a, m0, n0, seg, 0, kt1, 1);
-      return;
+  if constexpr (pf8_generic<QT0, QT1>()) {
+    if constexpr (QT0 != QT1) {
+      if (seg == a.nseg - 1) {
+        if (half < 0) pf8_body<QT1, 256, EPI>(a, m0, n0, seg, 0, kt1, 1);
+        else pf8_body<QT1, 128, EPI>(a, m0, n0, seg, 0, kt1, 1);
+        return;
+      }
     }
+    if (half < 0) pf8_body<QT0, 256, EPI>(a, m0, n0, seg, 0, kt1, 1);
+    else pf8_body<QT0, 128, EPI>(a, m0, n0, seg, 0, kt1, 1);
+  } else {
+    if constexpr (QT0 != QT1) {
+      if (seg == a.nseg - 1) {
+        if (half < 0) pf8c_body<QT1, 256, EPI>(a, m0, n0, seg, 0, kt1, 1);
+        else pf8c_body<QT1, 128, EPI>(a, m0, n0, seg, 0, kt1, 1);
+        return;
+      }
+    }
+    if (half < 0) pf8c_body<QT0, 256, EPI>(a, m0, n0, seg, 0, kt1, 1);
+    else pf8c_body<QT0, 128, EPI>(a, m0, n0, seg, 0, kt1, 1);
   }
-  if (half < 0) pf8c_body<QT0, 256, EPI>(a, m0, n0, seg, 0, kt1, 1);
-  else pf8c_body<QT0, 128, EPI>(a, m0, n0, seg, 0, kt1, 1);
 }
 
 // full tiles before the tail of a 256 x BN launch, or -1 (no tail split for this shape / plan)
@@ -1604,9 +1704,15 @@ __global__ void __launch_bounds__(256) gemm_pf4sk_kernel(GemmQArgs a, int ipw) {
 
 template <int QT0, int QT1, int BM, int EPI>
 __global__ void __launch_bounds__(512) gemm_pf8sk_kernel(GemmQArgs a, int ipw) {
-  constexpr int KG = QT0 == QT_BF16 ? 1 : 4;
+  constexpr int KG = pf8_generic<QT0, QT1>() ? 1 : 4;
   pf_stream_k<QT0, QT1, BM, EPI, KG>(a, 256, ipw, [&](int m0, int n0, int seg, int kt0, int kt1, int S) {
-    if constexpr (QT0 == QT_BF16) {
+    if constexpr (pf8_generic<QT0, QT1>()) {
+      if constexpr (QT0 != QT1) {
+        if (seg == a.nseg - 1) {
+          pf8_body<QT1, BM, EPI>(a, m0, n0, seg, kt0, kt1, S);
+          return;
+        }
+      }
       pf8_body<QT0, BM, EPI>(a, m0, n0, seg, kt0, kt1, S);
     } else {
       if constexpr (QT0 != QT1) {
@@ -1632,9 +1738,10 @@ inline int pf_sk_ipw(const GemmQArgs& a, int BM, int BN, int KG, int& grid) {
 
 template <int QT0, int QT1, int BM>
 constexpr int pf8_lds_bytes() {
-  if constexpr (QT0 == QT_BF16) {
+  if constexpr (pf8_generic<QT0, QT1>()) {
     using L0 = Pf4Layout<QT0, BM, 32, 8>;
-    return L0::NS * L0::SLOT;
+    using L1 = Pf4Layout<QT1, BM, 32, 8>;
+    return L0::NS * L0::SLOT > L1::NS * L1::SLOT ? L0::NS * L0::SLOT : L1::NS * L1::SLOT;
   } else {
     return PfcLayout<QT0, BM>::TOTAL > PfcLayout<QT1, BM>::TOTAL ? PfcLayout<QT0, BM>::TOTAL
                                                                  : PfcLayout<QT1, BM>::TOTAL;
@@ -1647,14 +1754,14 @@ void pf8_launch(const GemmQArgs& a, int S, hipStream_t st) {
   static_assert(lds <= 160 * 1024, "LDS");
   if (S < 0) {  // stream-K (STORE / ACCUM only: partial tiles are atomic adds)
     int grid = 0;
-    const int ipw = pf_sk_ipw(a, BM, 256, QT0 == QT_BF16 ? 1 : 4, grid);
+    const int ipw = pf_sk_ipw(a, BM, 256, pf8_generic<QT0, QT1>() ? 1 : 4, grid);
     if (a.epi == GEPI_STORE)
       hipLaunchKernelGGL((gemm_pf8sk_kernel<QT0, QT1, BM, GEPI_STORE>), dim3(grid), dim3(512), lds, st, a, ipw);
     else
       hipLaunchKernelGGL((gemm_pf8sk_kernel<QT0, QT1, BM, GEPI_ACCUM>), dim3(grid), dim3(512), lds, st, a, ipw);
     return;
   }
-  if constexpr (BM == 256 && QT0 != QT_BF16) {
+  if constexpr (BM == 256 && QT0 != QT_BF16) {  // (K-quant stacks: the tail split)
     const int F = pf_tail_full(a, 256, S);
     if (F >= 0) {
       constexpr int l128 = pf8_lds_bytes<QT0, QT1, 128>();

@@ -17,6 +17,10 @@ extern template bool pf_launch_fmt<QT_Q4_K, QT_Q4_K>(const GemmQArgs&, int, int,
 extern template bool pf_launch_fmt<QT_Q6_K, QT_Q6_K>(const GemmQArgs&, int, int, int, hipStream_t);
 extern template bool pf_launch_fmt<QT_Q4_K, QT_Q6_K>(const GemmQArgs&, int, int, int, hipStream_t);
 extern template bool pf_launch_fmt<QT_BF16, QT_BF16>(const GemmQArgs&, int, int, int, hipStream_t);
+extern template bool pf_launch_fmt<QT_Q5_K, QT_Q5_K>(const GemmQArgs&, int, int, int, hipStream_t);
+extern template bool pf_launch_fmt<QT_Q5_K, QT_Q6_K>(const GemmQArgs&, int, int, int, hipStream_t);
+extern template bool pf_launch_fmt<QT_Q4_0, QT_Q4_0>(const GemmQArgs&, int, int, int, hipStream_t);
+extern template bool pf_launch_fmt<QT_Q8_0, QT_Q8_0>(const GemmQArgs&, int, int, int, hipStream_t);
 
 static int pf_env(const char* name, int dflt) {
   const char* e = std::getenv(name);
@@ -167,8 +171,8 @@ static PfPlan pf_model_plan(const GemmQArgs& a, bool bf, bool s1_only) {
   return best;
 }
 
-// Serves M >= AIOS_GEMM_PF_MIN_M (default 33: the ring GEMM keeps 5..32) for Q4_K / Q6_K / mixed
-// Q4_K|Q6_K / bf16 weight stacks with the STORE / ACCUM / SWIGLU epilogues; false -> the caller's
+// Serves M >= AIOS_GEMM_PF_MIN_M (default 33: the ring GEMM keeps 5..32) for Q4_K / Q5_K / Q6_K / mixed
+// Q4_K|Q6_K, Q5_K|Q6_K / Q4_0 / Q8_0 / bf16 weight stacks with the STORE / ACCUM / SWIGLU epilogues; false -> the caller's
 // fallback (formats and fused epilogues this kernel does not do).
 static bool pf_eligible(const GemmQArgs& a);
 static bool pf_run(const GemmQArgs& a, const PfPlan& p, hipStream_t st) {
@@ -179,6 +183,11 @@ static bool pf_run(const GemmQArgs& a, const PfPlan& p, hipStream_t st) {
   if (qt0 == QT_Q4_K && qt1 == QT_Q4_K) return pf_launch_fmt<QT_Q4_K, QT_Q4_K>(a, p.bm, p.bn, p.s, st);
   if (qt0 == QT_Q6_K && qt1 == QT_Q6_K) return pf_launch_fmt<QT_Q6_K, QT_Q6_K>(a, p.bm, p.bn, p.s, st);
   if (qt0 == QT_Q4_K && qt1 == QT_Q6_K) return pf_launch_fmt<QT_Q4_K, QT_Q6_K>(a, p.bm, p.bn, p.s, st);
+  if (qt0 == QT_Q5_K && qt1 == QT_Q5_K) return pf_launch_fmt<QT_Q5_K, QT_Q5_K>(a, p.bm, p.bn, p.s, st);
+  if (qt0 == QT_Q5_K && qt1 == QT_Q6_K) return pf_launch_fmt<QT_Q5_K, QT_Q6_K>(a, p.bm, p.bn, p.s, st);
+  if (qt0 == QT_Q4_0 && qt1 == QT_Q4_0) return pf_launch_fmt<QT_Q4_0, QT_Q4_0>(a, p.bm, p.bn, p.s, st);
+  if (qt0 == QT_Q8_0 && qt1 == QT_Q8_0) return pf_launch_fmt<QT_Q8_0, QT_Q8_0>(a, p.bm, p.bn, p.s, st);
+  if (qt0 != QT_BF16) return false;
   return pf_launch_fmt<QT_BF16, QT_BF16>(a, p.bm, p.bn, p.s, st);
 }
 
@@ -204,8 +213,12 @@ static bool pf_eligible(const GemmQArgs& a) {
     if (a.seg[s].qtype != qt0) return false;
   const bool bf = qt0 == QT_BF16;
   if (bf ? (qt1 != QT_BF16 || a.K % 64) : (a.K % 256)) return false;
-  if (!bf && !((qt0 == QT_Q4_K || qt0 == QT_Q6_K) && (qt1 == QT_Q4_K || qt1 == QT_Q6_K))) return false;
-  if (qt0 == QT_Q6_K && qt1 == QT_Q4_K) return false;  // not instantiated (no such stack in the GGUF recipes)
+  // instantiated stacks (gemm_pf_*.hip): the GGUF recipes' Q4_K_M / Q5_K_M (mixed QKV: Q|K Q4_K or Q5_K, V Q6_K),
+  // Q6_K, Q4_0 and Q8_0 matrices
+  const bool kq = (qt0 == QT_Q4_K && (qt1 == QT_Q4_K || qt1 == QT_Q6_K)) || (qt0 == QT_Q6_K && qt1 == QT_Q6_K) ||
+                  (qt0 == QT_Q5_K && (qt1 == QT_Q5_K || qt1 == QT_Q6_K)) || (qt0 == QT_Q4_0 && qt1 == QT_Q4_0) ||
+                  (qt0 == QT_Q8_0 && qt1 == QT_Q8_0);
+  if (!bf && !kq) return false;
   if (a.epi == GEPI_SWIGLU_BF16 && (!a.C16 || a.nseg != 1)) return false;
   if (a.epi != GEPI_SWIGLU_BF16 && a.epi != GEPI_QKV && !a.C) return false;
   return true;

