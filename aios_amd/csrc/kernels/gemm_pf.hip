@@ -92,7 +92,12 @@ static std::map<PfKey, PfPlan>& pf_tuned_s1() {
   static std::map<PfKey, PfPlan> m;
   return m;
 }
-static bool pf_no_split(const GemmQArgs& a) { return a.epi == GEPI_SWIGLU_BF16 || a.epi == GEPI_QKV; }
+// AIOS_GEMM_PF_DETERMINISTIC=1: no split-K / stream-K plans (their fp32 atomics add partial tiles in
+// arrival order, so the low bits of a prefill could differ run to run even with the same plan)
+static bool pf_deterministic() { return pf_env("AIOS_GEMM_PF_DETERMINISTIC", 0) != 0; }
+static bool pf_no_split(const GemmQArgs& a) {
+  return a.epi == GEPI_SWIGLU_BF16 || a.epi == GEPI_QKV || pf_deterministic();
+}
 // stream-K: STORE / ACCUM launches whose tiles leave CUs idle, with an even K-step count per tile
 // (every stream-K segment then spans >= 2 steps / 256-blocks); AIOS_GEMM_PF_SK=0 keeps it out of plans
 static bool pf_sk_ok(const GemmQArgs& a, int bm, int bn, bool bf) {
@@ -126,9 +131,9 @@ static PfPlan pf_model_plan(const GemmQArgs& a, bool bf, bool s1_only);
 static PfPlan pf_plan(const GemmQArgs& a, bool bf) {
   if (!std::getenv("AIOS_GEMM_PF_TILE") && !std::getenv("AIOS_GEMM_PF_SPLIT") && a.ksplit <= 0) {
     std::lock_guard<std::mutex> g(pf_mu);
-    if (a.epi == GEPI_QKV) {
+    if (a.epi == GEPI_QKV || pf_deterministic()) {  // (the best plan without split partials)
       GemmQArgs b = a;
-      b.epi = GEPI_STORE;
+      if (a.epi == GEPI_QKV) b.epi = GEPI_STORE;
       auto it = pf_tuned_s1().find(pf_key(b));
       if (it != pf_tuned_s1().end()) return it->second;
     } else {

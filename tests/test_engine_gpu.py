@@ -16,7 +16,7 @@ pytestmark = pytest.mark.gpu
 def model_files(tmp_path_factory):
     d = tmp_path_factory.mktemp("eng")
     out = {}
-    for recipe in ("Q4_K_M", "Q4_0", "Q8_0", "BF16"):
+    for recipe in ("Q4_K_M", "Q4_0", "Q8_0", "BF16", "Q5_K_M"):
         out[recipe] = write_synthetic_gguf(str(d / f"small_{recipe}.gguf"), get_preset("test-small"), recipe, seed=7)
     out["mistral_shape"] = write_synthetic_gguf(str(d / "ms.gguf"), get_preset("test-mistral-shape"), "Q4_K_M", seed=9)
     return out
@@ -147,8 +147,9 @@ def test_capture_graphs_precaptures_every_batch_size(model_files):
     for pre in (False, True):
         eng, cfg = _load(path, max_slots=4, max_batch=4)
         if pre:
-            assert eng.capture_graphs(4) == 8
-            assert eng.capture_graphs(4) == 8  # idempotent
+            # 4 B x (masked, unmasked) step graphs + the pipelined decode's 4 forward graphs
+            assert eng.capture_graphs(4) == 12
+            assert eng.capture_graphs(4) == 12  # idempotent
         firsts = [int(np.argmax(eng.prefill(s, p, 0, True))) for s, p in enumerate(prompts)]
         outs.append(eng.decode([0, 1, 2], firsts, [len(p) for p in prompts]))
         del eng
@@ -186,12 +187,13 @@ def test_prefill_gemm_chunks_match_reference(model_files, recipe, monkeypatch):
     assert (logits2 - rl).abs().max().item() < 2e-2 * scale
 
 
-@pytest.mark.parametrize("recipe", ["Q4_K_M", "mistral_shape"])
+@pytest.mark.parametrize("recipe", ["Q4_K_M", "mistral_shape", "Q5_K_M", "Q4_0", "Q8_0"])
 @pytest.mark.parametrize("tile", ["", "256x256", "128x256", "64x128"])
 def test_prefill_gemm_pf_chunks_match_reference(model_files, recipe, tile, monkeypatch):
     """prefill chunks on the hand-written prefill GEMM (kernels/gemm_pf.hip, M >= 33): 64-row chunks of
     a 150-token prompt -- two 64-row chunks on gemm_pf (each tile shape), the 22-row tail on the ring
-    GEMM -- against the fp32 reference, continued at start_pos > 0 too"""
+    GEMM -- against the fp32 reference, continued at start_pos > 0 too (round 6: the Q5_K_M / Q4_0 / Q8_0
+    recipes' stacks as well, on the pf4 / pf8 bodies)"""
     monkeypatch.setenv("AIOS_PREFILL_GEMM_ROWS", "64")
     if tile:
         monkeypatch.setenv("AIOS_GEMM_PF_TILE", tile)
@@ -441,3 +443,46 @@ def test_sample_first_on_device(model_files):
     assert len({eng.sample_first(3, 1.0, 0, 1.0, s) for s in range(1, 30)}) > 1
 
 
+
+
+_PLAN_PROC = r"""
+import json, sys, numpy as np
+from aios_amd.models.config import get_preset
+from aios_amd.runtime import native
+from aios_amd.runtime.loader import random_engine
+eng = random_engine(get_preset("test-mistral-shape"), "Q4_K_M", seed=3, max_ctx=512, max_batch=2)
+prompt = [1] + list(np.random.default_rng(5).integers(3, 1024, 299))
+np.save(sys.argv[1], np.asarray(eng.prefill(0, [int(t) for t in prompt], 0, True), dtype=np.float32))
+print(json.dumps(sorted(native.require().gemm_pf_export())))
+"""
+
+
+@pytest.mark.parametrize("deterministic", [False, True])
+def test_prefill_plans_persist_across_processes(tmp_path, deterministic):
+    """with AIOS_GEMM_PF_PLANS naming a file, a second process installs the first's
+    tuned prefill-GEMM plans instead of timing its own (the same plan list in both).  Split-K / stream-K
+    plans add partial tiles with fp32 atomics in arrival order, so their last bits may still differ:
+    the logits agree to float rounding and on the argmax; AIOS_GEMM_PF_DETERMINISTIC=1 keeps those plans
+    out, and the two processes' prefill logits are then bit-identical."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    env = dict(os.environ, AIOS_GEMM_PF_PLANS=str(tmp_path / "plans.json"))
+    if deterministic:
+        env["AIOS_GEMM_PF_DETERMINISTIC"] = "1"
+    outs, plans = [], []
+    for i in range(2):
+        out = tmp_path / f"logits{i}.npy"
+        r = subprocess.run([sys.executable, "-c", _PLAN_PROC, str(out)], env=env, capture_output=True, text=True,
+                           timeout=240, cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        assert r.returncode == 0, r.stderr[-2000:]
+        plans.append(json.loads(r.stdout.strip().splitlines()[-1]))
+        outs.append(np.load(out))
+    assert (tmp_path / "plans.json").exists() and plans[0] and plans[1] == plans[0]
+    assert np.isfinite(outs[0]).all() and int(np.argmax(outs[0])) == int(np.argmax(outs[1]))
+    if deterministic:
+        assert np.array_equal(outs[0], outs[1])
+    else:
+        assert np.allclose(outs[0], outs[1], rtol=1e-4, atol=1e-5)

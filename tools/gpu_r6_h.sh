@@ -1,0 +1,9 @@
+#!/bin/bash
+# engine-level checks of this round's prefill formats + plan persistence, then every GPU test and smoke()
+set -o pipefail
+mkdir -p gpurun_out
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+timeout -k 10 1500 python -u -m pytest -x -q --timeout 900 --timeout-method thread -m gpu tests > gpurun_out/t_all.log 2>&1 || { tail -40 gpurun_out/t_all.log; exit 1; }
+tail -n 1 gpurun_out/t_all.log
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/smoke.log 2>&1 || { tail -20 gpurun_out/smoke.log; exit 1; }
+tail -n 1 gpurun_out/smoke.log
