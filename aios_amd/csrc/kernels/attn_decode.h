@@ -110,6 +110,9 @@ __device__ __forceinline__ gf32x2 fp8x2_f32x2(uint32_t w) {
 // the output).  At head_dim 128 a lane takes 16 dims (16 bytes: the bf16 path's load width -- with 8
 // dims per lane the fp8 kernel issued as many load instructions for half the bytes and measured only
 // 3 % faster than bf16 at 32k keys, latency- not byte-bound); head_dim 64 keeps 8 dims (8 bytes).
+#ifndef AIOS_ATTN_RESCALE_SKIP
+#define AIOS_ATTN_RESCALE_SKIP 1
+#endif
 template <int HD, int G, bool F8 = false>
 __device__ __forceinline__ void attn_core(const AttnDecodeArgs& a, int sp, int kvh, int h0, int ci, int P_max,
                                           int ppw, bool nt = false) {
@@ -245,15 +248,16 @@ __device__ __forceinline__ void attn_core(const AttnDecodeArgs& a, int sp, int k
         sc[s][g] = valid ? d : kNeg;
       }
     }
-    // ---- per-wave online softmax over this pass's KPW keys
+    // ---- online softmax over this lane's keys (round 6: per key group -- the LPK lanes of a key share
+    // its score, so (m, l) are uniform over them; the cross-key-group max / sum, two 3-stage lane
+    // reductions per head and pass, move to the end of the pass loop: the fp8 long mode's passes are
+    // bound by their own VALU chain, profiles/long_context_r6.txt)
 #pragma unroll
     for (int g = 0; g < G; ++g) {
       float mx = sc[0][g];
 #pragma unroll
       for (int s = 1; s < STEPS; ++s) mx = fmaxf(mx, sc[s][g]);
-      mx = keys_max<LPK>(mx);
       const float mn = fmaxf(m[g], mx);
-      const float alpha = fast_exp2(m[g] - mn);
       float ps = 0.f;
 #pragma unroll
       for (int s = 0; s < STEPS; ++s) {
@@ -261,10 +265,16 @@ __device__ __forceinline__ void attn_core(const AttnDecodeArgs& a, int sp, int k
         sc[s][g] = p;
         ps += p;
       }
-      l[g] = l[g] * alpha + keys_sum<LPK>(ps);
-      m[g] = mn;
+      // rescale only when some lane's max grew (a wave-uniform branch: past the first passes of a long
+      // context the running max rarely moves, and the NP packed multiplies + exp2 per head were per pass)
+      if (AIOS_ATTN_RESCALE_SKIP == 0 || __builtin_amdgcn_ballot_w64(mn > m[g])) {
+        const float alpha = fast_exp2(m[g] - mn);
+        l[g] *= alpha;
 #pragma unroll
-      for (int i = 0; i < NP; ++i) o[g][i] *= alpha;
+        for (int i = 0; i < NP; ++i) o[g][i] *= alpha;
+      }
+      l[g] += ps;
+      m[g] = mn;
     }
     // ---- P.V (lane-local over its keys; merged across key groups and waves at the end)
 #pragma unroll
@@ -299,15 +309,21 @@ __device__ __forceinline__ void attn_core(const AttnDecodeArgs& a, int sp, int k
       if (c + 3 * P < nchunk) issue(kB, vB, c + 3 * P);
     }
   }
-  // ---- merge the key groups of a wave (shuffles), then the 8 waves in LDS (one barrier)
+  // ---- merge the key groups of a wave (shuffles: their (m, l, o) rescaled to the wave's max), then the 8
+  // waves in LDS (one barrier)
   float of[G][DPL];
 #pragma unroll
-  for (int g = 0; g < G; ++g)
+  for (int g = 0; g < G; ++g) {
+    const float M = keys_max<LPK>(m[g]);
+    const float w = fast_exp2(m[g] - M);
+    l[g] = keys_sum<LPK>(l[g] * w);
+    m[g] = M;
 #pragma unroll
     for (int i = 0; i < NP; ++i) {
-      of[g][2 * i] = keys_sum<LPK>(o[g][i].x);
-      of[g][2 * i + 1] = keys_sum<LPK>(o[g][i].y);
+      of[g][2 * i] = keys_sum<LPK>(o[g][i].x * w);
+      of[g][2 * i + 1] = keys_sum<LPK>(o[g][i].y * w);
     }
+  }
   if (ksub == 0) {
 #pragma unroll
     for (int g = 0; g < G; ++g) {

@@ -491,13 +491,14 @@ def fp8_codes(x, scale):
 
 
 @pytest.mark.parametrize("hd,H,Hkv", [(128, 32, 8), (64, 32, 4)])
-@pytest.mark.parametrize("lens,max_ctx", [([1], 256), ([37, 200], 256), ([700], 1024), ([3000, 129], 4096)])
+@pytest.mark.parametrize("lens,max_ctx", [([1], 256), ([37, 200], 256), ([700], 1024), ([3000, 129], 4096),
+                                          ([20000, 9000], 32768)])
 @pytest.mark.parametrize("grouped", ["", "1"])
 def test_attention_decode_fp8_kv(E, hd, H, Hkv, lens, max_ctx, grouped, monkeypatch):
     """fp8 e4m3 KV pool (EngineConfig::kv_fp8): the decode attention reads 1-byte codes, K converted to
     bf16 pairs for v_dot2 with the layer's K scale folded into q, V to fp32 with its scale on the output
     -- against fp32 attention over the dequantised codes (the op as defined), short / long / grouped
-    modes with a shuffled block table"""
+    modes with a shuffled block table; 32k keys: several passes per long-mode workgroup"""
     if grouped:
         monkeypatch.setenv("AIOS_ATTN_GROUPED_MIN", grouped)
     B = len(lens)
