@@ -61,7 +61,7 @@ def _flags():
         f"-I{CSRC}",
         f"-I{pybind11.get_include()}",
         f"-I{sysconfig.get_paths()['include']}",
-    ] + (["-DAIOS_GEMV_PROBES=1", "-DAIOS_ATTN_PROBES=1"] if os.environ.get("AIOS_BUILD_PROBES") == "1" else [])
+    ] + (["-DAIOS_GEMV_PROBES=1", "-DAIOS_ATTN_PROBES=1", "-DAIOS_SAMPLE_PROBES=1"] if os.environ.get("AIOS_BUILD_PROBES") == "1" else [])
     # (AIOS_BUILD_PROBES=1: the microbenchmark / phase-stamp hooks the probe tools use -- tools/attn_probe.py
     # --stamps, tools/gemv_cu_probe.py ring mode; compiled out of production builds)
 

@@ -512,7 +512,7 @@ PYBIND11_MODULE(_engine, m) {
         py::arg("block_table") = 0);
   m.def("sample",
         [](uintptr_t logits, int ldl, int B, int V, uintptr_t temperature, uintptr_t top_k, uint64_t seed,
-           uintptr_t tokens, uintptr_t pos, uintptr_t mask, uintptr_t st, uintptr_t top_p) {
+           uintptr_t tokens, uintptr_t pos, uintptr_t mask, uintptr_t st, uintptr_t top_p, uintptr_t ts) {
           // grow-on-demand scratch for the raw-op binding (the engine owns its own)
           static void* ws = nullptr;
           static size_t ws_bytes = 0;
@@ -536,10 +536,12 @@ PYBIND11_MODULE(_engine, m) {
           a.temperature = (const float*)temperature; a.top_k = (const int*)top_k; a.seed = seed;
           a.tokens = (int*)tokens; a.pos = (int*)pos; a.mask = (const uint8_t*)mask;
           a.top_p = (const float*)top_p; a.ws = ws; a.ws_bytes = ws_bytes; a.counters = cnt;
+          a.ts = (long long*)ts;
           launch_sample(a, S(st));
         },
         py::arg("logits"), py::arg("ldl"), py::arg("B"), py::arg("V"), py::arg("temperature"), py::arg("top_k"),
-        py::arg("seed"), py::arg("tokens"), py::arg("pos"), py::arg("mask"), py::arg("st"), py::arg("top_p") = 0);
+        py::arg("seed"), py::arg("tokens"), py::arg("pos"), py::arg("mask"), py::arg("st"), py::arg("top_p") = 0,
+        py::arg("ts") = 0);
   m.def("gemm",
         [](uintptr_t A, int lda, PyQMatrix* w, int M, uintptr_t C, int ldc, int accumulate, uintptr_t st) {
           GemmArgs a;

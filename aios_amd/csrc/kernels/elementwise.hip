@@ -319,6 +319,9 @@ __device__ ArgMax block_argmax(ArgMax m, float* sv, int* si) {
 // Round 1 ran one 1024-thread workgroup per row over the whole vocabulary: 13-15 us per greedy
 // step, and 24 bisection passes re-reading the logits when sampling; top-p was ignored.
 // ----------------------------------------------------------------------------------------------
+#ifndef AIOS_SAMPLE_PROBES
+#define AIOS_SAMPLE_PROBES 0
+#endif
 constexpr int SAMPLE_THREADS = 256;
 constexpr int SAMPLE_PER_THREAD = 16;
 constexpr int SAMPLE_SLICE = SAMPLE_THREADS * SAMPLE_PER_THREAD;
@@ -353,61 +356,82 @@ __device__ __forceinline__ float gumbel(uint64_t seed, uint32_t step, int b, int
   return -__logf(-__logf(u));
 }
 
-// 7 block-wide counts at once (one LDS round): c[q] = #{register values >= t[q]}
+// threshold thr <= hi such that #{v >= thr} >= K and (within ~span / 2^24) as high as possible; values below
+// hi - span are treated as absent (probability < e^-30 relative at the temperatures served).  Round 6: a radix
+// select on a 24-bit quantisation of (v - (hi - span)), 8 bits per pass (an LDS histogram of the digit under
+// the prefix found so far, a block suffix scan, the digit where the count from the top reaches K) -- 3
+// passes of 5 barriers instead of the 8 bisection passes' ~2.5 us each (profiles/sampler_r6.txt).
+__device__ __forceinline__ int block_excl_scan(int c, int* s_w, int& total);
 template <int N>
-__device__ __forceinline__ void block_count7(const float (&v)[N], const float (&t)[7], float (&c)[7], float* red) {
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+__device__ float topk_threshold(const float (&v)[N], float hi, float span, int K, float* /*red*/) {
+  __shared__ int s_hist[SAMPLE_THREADS];
+  __shared__ int s_w2[16], s_sel[2];
+  static_assert(SAMPLE_THREADS == 256, "one histogram bin per thread");
+  const int tid = threadIdx.x;
+  const float lo = hi - span, scale = 16777216.f / span;
+  int u[N];
 #pragma unroll
-  for (int q = 0; q < 7; ++q) {
-    float x = 0.f;
+  for (int j = 0; j < N; ++j) u[j] = v[j] >= lo ? min((int)((v[j] - lo) * scale), 16777215) : -1;
+  int prefix = 0, above = 0;
+#pragma unroll 1
+  for (int pass = 0; pass < 3; ++pass) {
+    const int shift = 16 - 8 * pass;
+    s_hist[tid] = 0;
+    __syncthreads();
 #pragma unroll
-    for (int j = 0; j < N; ++j) x += v[j] >= t[q] ? 1.f : 0.f;
-    c[q] = wave_sum(x);
+    for (int j = 0; j < N; ++j)
+      if (u[j] >= 0 && (u[j] >> (shift + 8)) == prefix) atomicAdd(&s_hist[(u[j] >> shift) & 255], 1);
+    __syncthreads();
+    const int c = s_hist[255 - tid];  // thread t: digit 255 - t (the scan runs from the top digit down)
+    int tot;
+    const int cum = block_excl_scan(c, s_w2, tot) + c;
+    if (tid == 0) s_sel[0] = -1;
+    __syncthreads();
+    if (cum + above >= K && cum - c + above < K) {
+      s_sel[0] = 255 - tid;
+      s_sel[1] = above + cum - c;
+    }
+    __syncthreads();
+    const int d = s_sel[0];
+    if (d < 0) return lo;  // fewer than K values within the span: all of them
+    prefix = (prefix << 8) | d;
+    above = s_sel[1];
+    __syncthreads();  // (s_sel / s_hist rewritten by the next pass)
   }
-  __syncthreads();
-  if (lane == 0)
-#pragma unroll
-    for (int q = 0; q < 7; ++q) red[q * 16 + wid] = c[q];
-  __syncthreads();
-#pragma unroll
-  for (int q = 0; q < 7; ++q) {
-    float x = 0.f;
-    for (int w = 0; w < nw; ++w) x += red[q * 16 + w];
-    c[q] = x;
-  }
+  return lo + (float)prefix / scale - span * 1e-7f;
 }
 
-// threshold thr <= hi such that #{v >= thr} >= K and (within the search precision) as high as
-// possible; values below hi - span are treated as absent (probability < e^-30 relative at the
-// temperatures served).  8 passes of 8-way bisection.
-template <int N>
-__device__ float topk_threshold(const float (&v)[N], float hi, float span, int K, float* red) {
-  float lo = hi - span;
-  float t[7], c[7];
-#pragma unroll 1
-  for (int pass = 0; pass < 8; ++pass) {
-    const float step = (hi - lo) * 0.125f;
+// exclusive prefix sum of one int per thread over the block (wave scans + wave offsets); `total` = the sum
+__device__ __forceinline__ int block_excl_scan(int c, int* s_w, int& total) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  int x = c;
 #pragma unroll
-    for (int q = 0; q < 7; ++q) t[q] = lo + step * (q + 1);
-    block_count7(v, t, c, red);
-    float nlo = lo, nhi = hi;
-#pragma unroll
-    for (int q = 0; q < 7; ++q)
-      if (c[q] >= (float)K) { nlo = t[q]; nhi = (q < 6) ? t[q + 1] : hi; }
-    if (nlo == lo) nhi = t[0];
-    lo = nlo;
-    hi = nhi;
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o);
+    if (lane >= o) x += y;
   }
-  return lo;
+  __syncthreads();  // (s_w may still be read from a previous scan)
+  if (lane == 63) s_w[wid] = x;
+  __syncthreads();
+  int off = 0, tot = 0;
+  for (int w = 0; w < nw; ++w) {
+    off += w < wid ? s_w[w] : 0;
+    tot += s_w[w];
+  }
+  total = tot;
+  return off + x - c;
 }
 
 __global__ void __launch_bounds__(SAMPLE_THREADS) sample_kernel(SampleArgs a) {
   __shared__ float sv[16];
   __shared__ int si[16];
-  __shared__ float red[7 * 16];
-  __shared__ int s_cnt, s_last;
+  __shared__ __attribute__((aligned(16))) float red[7 * 16];
+  __shared__ int s_cnt, s_last, s_w[16], s_off[65];
   __shared__ float s_kv[SAMPLE_MAX_CAND];
   __shared__ int s_ki[SAMPLE_MAX_CAND];
+  __shared__ __attribute__((aligned(16))) float s_sv[SAMPLE_MAX_CAND + 4];
+  __shared__ __attribute__((aligned(16))) float s_se[SAMPLE_MAX_CAND + 4];
+  __shared__ __attribute__((aligned(16))) int s_si[SAMPLE_MAX_CAND + 4];
   const int b = blockIdx.y, slice = blockIdx.x, NS = gridDim.x, tid = threadIdx.x;
   const float* l = a.logits + (size_t)b * a.ldl;
   const uint8_t* mask = a.mask ? a.mask + (size_t)b * ((a.V + 7) / 8) : nullptr;
@@ -415,11 +439,22 @@ __global__ void __launch_bounds__(SAMPLE_THREADS) sample_kernel(SampleArgs a) {
   const int topk = a.top_k ? a.top_k[b] : 0;
   const float topp = a.top_p ? a.top_p[b] : 1.f;
   const uint32_t step = a.pos ? (uint32_t)a.pos[b] : 0u;  // RNG stream (seed, row, position)
-  const uint64_t seed = a.seeds ? a.seeds[b] : (a.seed_dev ? *a.seed_dev : a.seed);
+  // (not `c ? *p : a.seed`: a select between pointers made the compiler copy the kernel argument to scratch
+  // to load it through a pointer)
+  // (relaxed atomic loads: plain ones were sunk into one load through a select of the two pointers)
+  uint64_t seed = a.seed;
+  if (a.seeds) seed = __hip_atomic_load(a.seeds + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else if (a.seed_dev) seed = __hip_atomic_load(a.seed_dev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const int rkey = a.seeds ? 0 : b;  // per-row seeds: row-independent streams
   const bool filt = temp > 0.f && (topk > 0 || topp < 1.f);
   const int K = topk > 0 ? min(topk, SAMPLE_KCAP) : SAMPLE_TOPP_K;
   SampleWs w = sample_ws(a.ws, a.B, NS);
+  // probe stamps (tools/sample_probe.py; compiled into probe builds only, AIOS_BUILD_PROBES=1: the sites'
+  // pointer checks pushed the kernel into SGPR spills)
+  auto stamp = [&](int k) __attribute__((always_inline)) {
+    if (AIOS_SAMPLE_PROBES && a.ts && tid == 0) a.ts[((size_t)b * NS + slice) * 16 + k] = __builtin_amdgcn_s_memrealtime();
+  };
+  stamp(0);
 
   // ---- A) this slice in registers
   float v[SAMPLE_PER_THREAD];
@@ -433,6 +468,7 @@ __global__ void __launch_bounds__(SAMPLE_THREADS) sample_kernel(SampleArgs a) {
     m = am_better(m, ArgMax{x, i});
   }
   m = block_argmax(m, sv, si);
+  stamp(1);
   ArgMax pub = m;
   if (temp > 0.f && !filt) {  // plain temperature sampling: this slice's Gumbel-max
     ArgMax g{-INFINITY, 0x7fffffff};
@@ -446,20 +482,27 @@ __global__ void __launch_bounds__(SAMPLE_THREADS) sample_kernel(SampleArgs a) {
   }
   if (filt) {  // local top-K candidates (the global top-K is a subset of their union)
     const float thr = m.v > -INFINITY ? topk_threshold(v, m.v, 30.f * temp + 1.f, K, red) : INFINITY;
-    if (tid == 0) s_cnt = 0;
-    __syncthreads();
+    stamp(2);
+    // (slots by a block prefix sum in (thread, j) order: the candidate order -- and so every float sum over
+    // candidates below -- is the same on every run)
+    int c = 0;
+#pragma unroll
+    for (int j = 0; j < SAMPLE_PER_THREAD; ++j) c += (v[j] >= thr && v[j] > -INFINITY) ? 1 : 0;
+    int total;
+    int k = block_excl_scan(c, s_w, total);
 #pragma unroll
     for (int j = 0; j < SAMPLE_PER_THREAD; ++j) {
       if (v[j] >= thr && v[j] > -INFINITY) {
-        const int k = atomicAdd(&s_cnt, 1);
         if (k < SAMPLE_KCAP) {
           const size_t o = ((size_t)b * NS + slice) * SAMPLE_KCAP + k;
           __hip_atomic_store(w.cand_v + o, v[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           __hip_atomic_store(w.cand_i + o, slice * SAMPLE_SLICE + j * SAMPLE_THREADS + tid, __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_AGENT);
         }
+        ++k;
       }
     }
+    if (tid == 0) s_cnt = total;
     __syncthreads();
   }
   if (tid == 0) {
@@ -475,8 +518,10 @@ __global__ void __launch_bounds__(SAMPLE_THREADS) sample_kernel(SampleArgs a) {
     s_last = (t == NS - 1);
   }
   __syncthreads();
+  stamp(3);
   if (!s_last) return;
   __atomic_thread_fence(__ATOMIC_ACQUIRE);
+  stamp(4);
 
   // ---- B) the row's last arriver merges
   auto ldf = [](const float* p) { return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
@@ -485,57 +530,95 @@ __global__ void __launch_bounds__(SAMPLE_THREADS) sample_kernel(SampleArgs a) {
   for (int s = tid; s < NS; s += SAMPLE_THREADS)
     r = am_better(r, ArgMax{ldf(w.part_v + (size_t)b * NS + s), ldi(w.part_i + (size_t)b * NS + s)});
   r = block_argmax(r, sv, si);
+  stamp(5);
   int tok = r.i;
   if (filt) {
-    // gather every slice's candidates: up to 16 per thread in registers
-    if (tid == 0) s_cnt = 0;
+    // gather every slice's candidates (slice-major, in their published order), all loads in flight at
+    // once: the counts first (one round trip), then every candidate at its prefix offset (round 6: the
+    // slice-serial gather cost a round trip per slice)
+    if (tid < NS) s_off[tid + 1] = min(ldi(w.cand_n + (size_t)b * NS + tid), SAMPLE_KCAP);
     __syncthreads();
-    for (int s = 0; s < NS; ++s) {
-      const int n = ldi(w.cand_n + (size_t)b * NS + s);
-      for (int k = tid; k < n; k += SAMPLE_THREADS) {
-        const int o = atomicAdd(&s_cnt, 1);
-        if (o < SAMPLE_MAX_CAND) {
-          const size_t g = ((size_t)b * NS + s) * SAMPLE_KCAP + k;
-          s_kv[o] = ldf(w.cand_v + g);
-          s_ki[o] = ldi(w.cand_i + g);
-        }
-      }
+    if (tid == 0) {
+      s_off[0] = 0;
+      for (int s = 0; s < NS; ++s) s_off[s + 1] += s_off[s];
     }
     __syncthreads();
-    const int nc = min(s_cnt, SAMPLE_MAX_CAND);
+    const int nc = min(s_off[NS], SAMPLE_MAX_CAND);
+    for (int o = tid; o < nc; o += SAMPLE_THREADS) {
+      int s = 0;
+      while (s + 1 < NS && s_off[s + 1] <= o) ++s;
+      const size_t g = ((size_t)b * NS + s) * SAMPLE_KCAP + (o - s_off[s]);
+      s_kv[o] = ldf(w.cand_v + g);
+      s_ki[o] = ldi(w.cand_i + g);
+    }
+    __syncthreads();
     float cv[SAMPLE_MAX_CAND / SAMPLE_THREADS];
 #pragma unroll
     for (int j = 0; j < SAMPLE_MAX_CAND / SAMPLE_THREADS; ++j) {
       const int o = j * SAMPLE_THREADS + tid;
       cv[j] = o < nc ? s_kv[o] : -INFINITY;
     }
+    stamp(6);
     const float M = r.v;  // the global max is a candidate of its slice
     const float thr = topk_threshold(cv, M, 30.f * temp + 1.f, K, red);
-    // survivors: top-K (ties kept), then the nucleus over them
+    stamp(7);
+    // survivors: top-K (ties kept), then the nucleus over them.  Round 6: the survivors are compacted
+    // (block prefix sum, deterministic order) with their weights e = exp((v - M) / T) computed once, and
+    // each survivor's rank-ordered mass before it sums over the S survivors only -- the old loop re-ran
+    // exp over all nc candidates per survivor (~100 us per sampled token at nc ~ 2k, profiles/)
     const float it = 1.f / temp;
+    int c = 0;
+#pragma unroll
+    for (int j = 0; j < SAMPLE_MAX_CAND / SAMPLE_THREADS; ++j) c += (cv[j] >= thr && cv[j] > -INFINITY) ? 1 : 0;
+    int S;
+    int k = block_excl_scan(c, s_w, S);
     float zs = 0.f;
 #pragma unroll
-    for (int j = 0; j < SAMPLE_MAX_CAND / SAMPLE_THREADS; ++j)
-      if (cv[j] >= thr && cv[j] > -INFINITY) zs += __expf((cv[j] - M) * it);
-    const float Z = block_sum(zs, red);
-    ArgMax g{-INFINITY, 0x7fffffff};
-#pragma unroll
     for (int j = 0; j < SAMPLE_MAX_CAND / SAMPLE_THREADS; ++j) {
-      const int o = j * SAMPLE_THREADS + tid;
-      if (!(cv[j] >= thr && cv[j] > -INFINITY)) continue;
-      const int idx = s_ki[o];
+      if (cv[j] >= thr && cv[j] > -INFINITY) {
+        const float e = __expf((cv[j] - M) * it);
+        zs += e;
+        s_sv[k] = cv[j];
+        s_si[k] = s_ki[j * SAMPLE_THREADS + tid];
+        s_se[k] = e;
+        ++k;
+      }
+    }
+    if (tid < 4) {  // pad to a multiple of 4 (the float4 sweep below): never ranked before a survivor
+      s_sv[S + tid] = -INFINITY;
+      s_si[S + tid] = 0x7fffffff;
+      s_se[S + tid] = 0.f;
+    }
+    const float Z = block_sum(zs, red);  // (its internal barriers also publish the survivor arrays)
+    __syncthreads();
+    stamp(8);
+    if (AIOS_SAMPLE_PROBES && a.ts && tid == 0) {  // (probe: candidate / survivor counts)
+      a.ts[((size_t)b * NS + slice) * 16 + 12] = nc;
+      a.ts[((size_t)b * NS + slice) * 16 + 13] = S;
+    }
+    ArgMax g{-INFINITY, 0x7fffffff};
+    for (int u = tid; u < S; u += SAMPLE_THREADS) {
+      const float vu = s_sv[u];
+      const int idx = s_si[u];
       bool keep = true;
       if (topp < 1.f) {  // mass of the survivors ranked before this one (value desc, index asc)
-        float before = 0.f;
-        for (int q = 0; q < nc; ++q) {
-          const float u = s_kv[q];
-          if (u >= thr && (u > cv[j] || (u == cv[j] && s_ki[q] < idx))) before += __expf((u - M) * it);
+        // (float4 sweeps, four partial sums: the scalar loop waited one LDS round trip per survivor)
+        float b0 = 0.f, b1 = 0.f, b2 = 0.f, b3 = 0.f;
+        for (int q = 0; q < S; q += 4) {
+          const float4 x = *(const float4*)(s_sv + q);
+          const int4 xi = *(const int4*)(s_si + q);
+          const float4 e = *(const float4*)(s_se + q);
+          b0 += (x.x > vu || (x.x == vu && xi.x < idx)) ? e.x : 0.f;
+          b1 += (x.y > vu || (x.y == vu && xi.y < idx)) ? e.y : 0.f;
+          b2 += (x.z > vu || (x.z == vu && xi.z < idx)) ? e.z : 0.f;
+          b3 += (x.w > vu || (x.w == vu && xi.w < idx)) ? e.w : 0.f;
         }
-        keep = before < topp * Z;
+        keep = (b0 + b1) + (b2 + b3) < topp * Z;
       }
-      if (keep) g = am_better(g, ArgMax{cv[j] * it + gumbel(seed, step, rkey, idx), idx});
+      if (keep) g = am_better(g, ArgMax{vu * it + gumbel(seed, step, rkey, idx), idx});
     }
     g = block_argmax(g, sv, si);
+    stamp(9);
     if (g.i >= 0 && g.i < a.V) tok = g.i;
   } else if (temp > 0.f) {
     tok = r.i;  // r already holds the Gumbel winners' max
@@ -551,6 +634,7 @@ __global__ void __launch_bounds__(SAMPLE_THREADS) sample_kernel(SampleArgs a) {
     }
     __hip_atomic_store(a.counters + b, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
   }
+  stamp(10);
 }
 
 void launch_sample(const SampleArgs& a, hipStream_t st) {

@@ -166,6 +166,7 @@ struct SampleArgs {
   void* ws;                  // sample_ws_bytes(B, V) scratch (slice partials + candidates)
   size_t ws_bytes;
   int* counters;             // [B] arrival tickets, zero-initialised, self re-arming
+  long long* ts;             // probe stamps [B][slices][16] (tools/sample_probe.py --stamps) or null
 };
 void launch_sample(const SampleArgs& a, hipStream_t st);
 size_t sample_ws_bytes(int B, int V);
