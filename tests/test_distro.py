@@ -77,3 +77,83 @@ def test_first_boot_initialises_a_node(tmp_path):
     r2 = subprocess.run(["bash", os.path.join(ROOT, "scripts", "first-boot.sh"), "--no-network"], env=env,
                         capture_output=True, text=True, timeout=120)
     assert r2.returncode == 0 and (data / "node_id").read_text() == node_id
+
+
+def test_cpio_newc_roundtrip(tmp_path):
+    """aios_amd.utils.cpio: a tree (dirs, files with modes, a symlink) -> newc -> the same entries back,
+    root-owned, deterministic (two writes are byte-identical), /dev/console declared"""
+    from aios_amd.utils.cpio import read_newc, write_newc
+
+    root = tmp_path / "t"
+    (root / "a" / "b").mkdir(parents=True)
+    (root / "a" / "b" / "x.txt").write_text("hello")
+    (root / "run.sh").write_text("#!/bin/sh\n")
+    os.chmod(root / "run.sh", 0o755)
+    os.symlink("a/b/x.txt", root / "link")
+    data = write_newc(str(root))
+    assert data == write_newc(str(root)) and len(data) % 4 == 0
+    ents = {n: (m, b) for n, m, _, b in read_newc(data)}
+    assert ents["a/b/x.txt"][1] == b"hello" and ents["run.sh"][0] == 0o100755
+    assert ents["link"] == (0o120777, b"a/b/x.txt") and ents["a"][0] == 0o40755
+    assert ents["dev/console"][0] == 0o20600
+
+
+def test_initramfs_builds_offline(tmp_path):
+    """scripts/build-initramfs.sh without busybox, cpio or root: a static /init (distro/initramfs/init.c)
+    in a gzip newc image; the packed /init, run with --plan on the build host, prints the boot plan ending in
+    switch_root into aios-init"""
+    import shutil
+    import stat
+
+    from aios_amd.utils.cpio import read_newc
+
+    if not shutil.which("gcc"):
+        pytest.skip("no C compiler")
+    r = subprocess.run(["bash", os.path.join(ROOT, "scripts", "build-initramfs.sh"), "--out", str(tmp_path)],
+                       capture_output=True, text=True, timeout=300)
+    if r.returncode != 0 and "cannot find -lc" in r.stderr:
+        pytest.skip("no static libc")
+    assert r.returncode == 0, r.stderr
+    ents = {n: (m, b) for n, m, _, b in read_newc((tmp_path / "initramfs.img").read_bytes())}
+    for d in ("proc", "sys", "dev", "mnt/medium", "mnt/ro", "mnt/rw", "newroot", "lib/modules"):
+        assert stat.S_ISDIR(ents[d][0]), d
+    mode, init = ents["init"]
+    assert stat.S_ISREG(mode) and mode & 0o111 and init[:4] == b"\x7fELF"
+    import struct
+
+    phoff, = struct.unpack_from("<Q", init, 0x20)
+    phentsize, phnum = struct.unpack_from("<HH", init, 0x36)
+    ptypes = [struct.unpack_from("<I", init, phoff + i * phentsize)[0] for i in range(phnum)]
+    assert 3 not in ptypes  # static: no PT_INTERP program header
+    exe = tmp_path / "init_plan"
+    exe.write_bytes(init)
+    exe.chmod(0o755)
+    plan = subprocess.run([str(exe), "--plan"], capture_output=True, text=True, timeout=30)
+    assert plan.returncode == 0, plan.stderr
+    lines = plan.stdout.splitlines()
+    assert lines[0] == "mount -t proc proc /proc" and "squashfs" in plan.stdout and "overlay" in plan.stdout
+    assert lines[-1] == "switch_root /newroot /usr/sbin/aios-init"
+
+
+def test_overlay_rootfs_builds_offline(tmp_path):
+    """scripts/build-rootfs.sh --overlay-only: the aiOS layer (package with its built extensions, aios-init,
+    configs, environment) as an ext4 image built without root (mkfs.ext4 -d)"""
+    import shutil
+
+    mkfs = shutil.which("mkfs.ext4") or ("/usr/sbin/mkfs.ext4" if os.path.exists("/usr/sbin/mkfs.ext4") else None)
+    if not mkfs:
+        pytest.skip("no mkfs.ext4")
+    env = dict(os.environ, PATH=os.environ.get("PATH", "") + ":/usr/sbin:/sbin")
+    r = subprocess.run(["bash", os.path.join(ROOT, "scripts", "build-rootfs.sh"), "--out", str(tmp_path),
+                        "--overlay-only"], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr
+    img = tmp_path / "aios-overlay.ext4"
+    assert img.exists() and img.stat().st_size > 1 << 20
+    o = tmp_path / "overlay"
+    assert (o / "usr/lib/aios/aios_amd/__init__.py").exists() and (o / "etc/aios/config.toml").exists()
+    assert "PYTHONPATH=/usr/lib/aios" in (o / "etc/aios/environment").read_text()
+    assert not list(o.rglob("__pycache__"))
+    debugfs = shutil.which("debugfs", path=env["PATH"])
+    if debugfs:
+        ls = subprocess.run([debugfs, "-R", "ls /usr/lib/aios/aios_amd", str(img)], capture_output=True, text=True)
+        assert "__init__.py" in ls.stdout
