@@ -623,6 +623,9 @@ struct PfFmt {
   static constexpr bool Q6 = QT == QT_Q6_K, BF = QT == QT_BF16, Q5 = QT == QT_Q5_K, L0 = QT == QT_Q4_0,
                         L8 = QT == QT_Q8_0, KREC = QT == QT_Q4_K || QT == QT_Q5_K;
 };
+#ifndef AIOS_PF4_NS
+#define AIOS_PF4_NS 3
+#endif
 template <int QT, int BM, int WC, int NW = 4>
 struct Pf4Layout {
   using F = PfFmt<QT>;
@@ -638,11 +641,15 @@ struct Pf4Layout {
   static constexpr int WB = OFF_DW + DW;                 // one wave's weight bytes per slot
   static constexpr int OFF_B = A_BYTES;
   static constexpr int SLOT = (A_BYTES + NW * WB + 255) / 256 * 256;
-  static constexpr int NS = 3 * SLOT <= 160 * 1024 ? 3 : 2;
+  // ring depth: as many slots as 160 KB of LDS holds, up to AIOS_PF4_NS (deeper rings keep more K-steps of
+  // DMA in flight for the one workgroup per CU; the counted waits are (NS - 1) / (NS - 2) x PW)
+  static constexpr int NS_FIT = (160 * 1024) / SLOT;
+  static constexpr int NS = NS_FIT < AIOS_PF4_NS ? NS_FIT : AIOS_PF4_NS;
   static constexpr int NA = BM / (8 * NW), NCODE = CODE / 1024, NMETA = META / 1024, NHB = HB / 1024,
                        NSC = SC / 256, ND = DW / 256;
   static constexpr int PW = NA + NCODE + NMETA + NHB + NSC + ND;  // DMA instructions per wave per slot
   static_assert(CODE % 1024 == 0 && HB % 1024 == 0 && WC * 4 <= 256 && PW <= 31 && NA * 8 * NW == BM, "pf4 slot");
+  static_assert(NS >= 2 && (NS - 1) * PW <= 63, "pf4 ring depth / vmcnt immediate");
 };
 
 template <int QT, int BM, int WC, int NW = 4>
@@ -832,7 +839,7 @@ __device__ __forceinline__ void pf4_body(const GemmQArgs& a, int m0, int n0, int
   constexpr int NMF = MT * CT, HALF = NMF / 2;
   // step kt0's own pieces (NS - 1 younger steps in flight)
   if constexpr (!(PROBE & 1)) {
-    if constexpr (NS == 3) pf_vmcnt<2 * PW>(); else pf_vmcnt<PW>();
+    pf_vmcnt<(NS - 1) * PW>();
   }
   read_raw(pf_smem, kt0);
   dec(std::integral_constant<int, 0>{});
@@ -855,7 +862,7 @@ __device__ __forceinline__ void pf4_body(const GemmQArgs& a, int m0, int n0, int
     // phase 1: own step-(t+1) pieces landed (NS - 2 younger steps in flight) -> raw bytes, fragment 0
     ldA(slot, fa, 2);
     if constexpr (!(PROBE & 1)) {
-      if constexpr (NS == 3) pf_vmcnt<PW>(); else pf_vmcnt<0>();
+      pf_vmcnt<(NS - 2) * PW>();
     }
     read_raw(pf_smem + nxt * L::SLOT, kt0 + t + 1);
     dec(std::integral_constant<int, 0>{});
@@ -1007,7 +1014,7 @@ __device__ __forceinline__ void pf8_body(const GemmQArgs& a, int m0, int n0, int
     }
   };
   if constexpr (!(PROBE & 1)) {
-    if constexpr (NS == 3) pf_vmcnt<2 * PW>(); else pf_vmcnt<PW>();
+    pf_vmcnt<(NS - 1) * PW>();
   }
   read_raw(pf_smem, kt0);
   dec(std::integral_constant<int, 0>{});
@@ -1029,7 +1036,7 @@ __device__ __forceinline__ void pf8_body(const GemmQArgs& a, int m0, int n0, int
       if constexpr (p == NG) {
         // own pieces of step t+1 landed (NS - 2 younger steps in flight): its raw bytes, fragment 0
         if constexpr (!(PROBE & 1)) {
-          if constexpr (NS == 3) pf_vmcnt<PW>(); else pf_vmcnt<0>();
+          pf_vmcnt<(NS - 2) * PW>();
         }
         read_raw(pf_smem + nxt * L::SLOT, kt0 + t + 1);
         dec(std::integral_constant<int, 0>{});
