@@ -828,9 +828,11 @@ bool launch_gemv_lds(const GemvArgs& a, hipStream_t st, bool dry = false) {
         const char* e = std::getenv("AIOS_LDS_B1_RSUB");
         return e ? std::atoi(e) : 1;
       }();
-      static const int rsub_q6 = [] {  // AIOS_LDS_B1_RSUB_Q6: Q6_K matrices' own value (default: the same)
+      // AIOS_LDS_B1_RSUB_Q6: Q6_K matrices' own value (default 2: their 23.5 KB slots cover the latency with
+      // one slot fewer still -- Mistral B=1 670.7 / 670.9 -> 672.6 / 672.0 tok/s, profiles/decode_b1_experiments_r6.txt)
+      static const int rsub_q6 = [] {
         const char* e = std::getenv("AIOS_LDS_B1_RSUB_Q6");
-        return e ? std::atoi(e) : -1;
+        return e ? std::atoi(e) : 2;
       }();
       const int rsub = (QT0 == QT_Q6_K && rsub_q6 >= 0) ? rsub_q6 : rsub_all;
       if (rsub == 1 || rsub == 2) {
