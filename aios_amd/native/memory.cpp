@@ -4,6 +4,7 @@
 #include <cctype>
 #include <cmath>
 #include <cstring>
+#include <queue>
 #include <set>
 #include <unordered_map>
 
@@ -61,6 +62,77 @@ double keyword_relevance(const std::vector<std::string>& kws, const std::string&
 }
 
 int estimate_tokens(const std::string& s) { return (int)((s.size() + 3) / 4); }
+
+// ---- collection scans: the query side is prepared once, every row is scored without allocating, and only
+// the top-n rows are materialised as records (a scan used to build a record for every row, then sort them all)
+namespace {
+struct Scorer {
+  std::vector<std::string> kws;  // lower-cased once
+  std::vector<float> qe;
+  explicit Scorer(const std::string& query) : qe(hashed_embedding(query)) {
+    for (auto& k : split_ws(query)) kws.push_back(lower(k));
+  }
+  // 0.4 * keyword overlap + 0.6 * cosine(query, stored embedding blob)   (longterm.rs:186)
+  double operator()(const std::string& text, const std::string& emb) const {
+    double kw = 0.5;
+    if (!kws.empty()) {
+      const std::string t = lower(text);
+      int m = 0;
+      for (auto& k : kws)
+        if (t.find(k) != std::string::npos) ++m;
+      kw = (double)m / (double)kws.size();
+    }
+    double cos = 0;
+    const size_t n = emb.size() / 4;
+    if (n == qe.size() && n) {
+      double d = 0, na = 0, nb = 0;
+      for (size_t i = 0; i < n; ++i) {
+        float b;
+        std::memcpy(&b, emb.data() + 4 * i, 4);
+        d += (double)qe[i] * b;
+        na += (double)qe[i] * qe[i];
+        nb += (double)b * b;
+      }
+      cos = (na > 0 && nb > 0) ? d / std::sqrt(na * nb) : 0;
+    }
+    return 0.4 * kw + 0.6 * cos;
+  }
+};
+
+// the n best (relevance desc, scan order on ties -- what a stable sort of every row gave)
+class TopN {
+ public:
+  explicit TopN(int n) : n_((size_t)std::max(n, 0)) {}
+  bool wants(double r) const { return n_ && (heap_.size() < n_ || r > heap_.top().r); }
+  void push(double r, Json rec) {
+    heap_.push({r, seq_++, std::move(rec)});
+    if (heap_.size() > n_) heap_.pop();
+  }
+  void skip() { ++seq_; }
+  Json take() {
+    std::vector<Hit> v;
+    while (!heap_.empty()) {
+      v.push_back(std::move(const_cast<Hit&>(heap_.top())));
+      heap_.pop();
+    }
+    Json out = Json::array();
+    for (auto it = v.rbegin(); it != v.rend(); ++it) out.push(std::move(it->rec));
+    return out;
+  }
+
+ private:
+  struct Hit {
+    double r;
+    size_t seq;
+    Json rec;
+  };
+  struct Worse {  // heap top = the current worst kept hit
+    bool operator()(const Hit& a, const Hit& b) const { return a.r != b.r ? a.r > b.r : a.seq < b.seq; }
+  };
+  size_t n_, seq_ = 0;
+  std::priority_queue<Hit, std::vector<Hit>, Worse> heap_;
+};
+}  // namespace
 
 static std::string emb_blob(const std::vector<float>& v) { return std::string((const char*)v.data(), v.size() * 4); }
 static std::vector<float> blob_emb(const std::string& b) {
@@ -335,12 +407,10 @@ Json MemoryStore::semantic_search(const std::string& query, const std::vector<st
                                   double min_rel) {
   // hybrid relevance = 0.4 * keyword overlap + 0.6 * cosine(hashed embeddings)  (longterm.rs:186)
   // scored over the whole collection (the reference scored only the N most recent rows)
-  const int limit = n <= 0 ? 10 : n;
-  const auto kws = split_ws(query);
-  const auto qe = hashed_embedding(query);
+  const Scorer score(query);
   std::vector<std::string> cols = cols_in;
   if (cols.empty()) cols = {"procedures", "incidents", "config_changes"};
-  std::vector<std::pair<double, Json>> res;
+  TopN top(n <= 0 ? 10 : n);
   std::lock_guard<std::recursive_mutex> l(lt_.mutex());
   std::set<std::string> done;
   for (auto& c : cols) {
@@ -350,36 +420,42 @@ Json MemoryStore::semantic_search(const std::string& query, const std::vector<st
       Stmt s(lt_, "SELECT id, name, description, embedding, steps_json FROM procedures ORDER BY last_used DESC LIMIT 5000");
       while (s.step()) {
         const std::string content = s.col_text(1) + ": " + s.col_text(2);
-        const double r = 0.4 * keyword_relevance(kws, content) + 0.6 * cosine(qe, blob_emb(s.col_blob(3)));
-        if (r >= min_rel)
-          res.push_back({r, Json::object({{"id", s.col_text(0)}, {"content", content},
-                                          {"metadata_json", Json::object({{"steps", s.col_text(4)}}).dump()},
-                                          {"relevance", r}, {"collection", "procedures"}})});
+        const double r = score(content, s.col_blob(3));
+        if (r < min_rel || !top.wants(r)) {
+          top.skip();
+          continue;
+        }
+        top.push(r, Json::object({{"id", s.col_text(0)}, {"content", content},
+                                  {"metadata_json", Json::object({{"steps", s.col_text(4)}}).dump()},
+                                  {"relevance", r}, {"collection", "procedures"}}));
       }
     } else if (coll == "incidents") {
       Stmt s(lt_, "SELECT id, description, root_cause, resolution, embedding FROM incidents ORDER BY timestamp DESC LIMIT 5000");
       while (s.step()) {
         const std::string content = s.col_text(1) + " | cause: " + s.col_text(2) + " | fix: " + s.col_text(3);
-        const double r = 0.4 * keyword_relevance(kws, content) + 0.6 * cosine(qe, blob_emb(s.col_blob(4)));
-        if (r >= min_rel)
-          res.push_back({r, Json::object({{"id", s.col_text(0)}, {"content", content}, {"metadata_json", ""},
-                                          {"relevance", r}, {"collection", "incidents"}})});
+        const double r = score(content, s.col_blob(4));
+        if (r < min_rel || !top.wants(r)) {
+          top.skip();
+          continue;
+        }
+        top.push(r, Json::object({{"id", s.col_text(0)}, {"content", content}, {"metadata_json", ""},
+                                  {"relevance", r}, {"collection", "incidents"}}));
       }
     } else if (coll == "config_changes") {
       Stmt s(lt_, "SELECT id, file_path, reason, changed_by FROM config_changes ORDER BY timestamp DESC LIMIT 5000");
       while (s.step()) {
         const std::string content = s.col_text(1) + ": " + s.col_text(2) + " (by " + s.col_text(3) + ")";
-        const double r = 0.4 * keyword_relevance(kws, content) + 0.6 * cosine(qe, hashed_embedding(content));
-        if (r >= min_rel)
-          res.push_back({r, Json::object({{"id", s.col_text(0)}, {"content", content}, {"metadata_json", ""},
-                                          {"relevance", r}, {"collection", "config_changes"}})});
+        const double r = score(content, emb_blob(hashed_embedding(content)));
+        if (r < min_rel || !top.wants(r)) {
+          top.skip();
+          continue;
+        }
+        top.push(r, Json::object({{"id", s.col_text(0)}, {"content", content}, {"metadata_json", ""},
+                                  {"relevance", r}, {"collection", "config_changes"}}));
       }
     }
   }
-  std::stable_sort(res.begin(), res.end(), [](auto& a, auto& b) { return a.first > b.first; });
-  Json out = Json::array();
-  for (size_t i = 0; i < res.size() && (int)i < limit; ++i) out.push(res[i].second);
-  return out;
+  return top.take();
 }
 
 // ---- knowledge
@@ -395,24 +471,22 @@ void MemoryStore::add_knowledge(const Json& k) {
   s.bind_blob(7, b.data(), b.size()).exec();
 }
 Json MemoryStore::search_knowledge(const std::string& query, int n, double min_rel) {
-  const int limit = n <= 0 ? 5 : n;
-  const auto kws = split_ws(query);
-  const auto qe = hashed_embedding(query);
-  std::vector<std::pair<double, Json>> res;
+  const Scorer score(query);
+  TopN top(n <= 0 ? 5 : n);
   std::lock_guard<std::recursive_mutex> l(kn_.mutex());
   Stmt s(kn_, "SELECT id, title, content, source, tags, embedding FROM knowledge LIMIT 20000");
   while (s.step()) {
-    const std::string content = s.col_text(1) + ": " + s.col_text(2);
-    const double r = 0.4 * keyword_relevance(kws, content + " " + s.col_text(4)) + 0.6 * cosine(qe, blob_emb(s.col_blob(5)));
-    if (r >= min_rel)
-      res.push_back({r, Json::object({{"id", s.col_text(0)}, {"content", content},
-                                      {"metadata_json", Json::object({{"source", s.col_text(3)}, {"tags", s.col_text(4)}}).dump()},
-                                      {"relevance", r}, {"collection", "knowledge"}})});
+    const std::string content = s.col_text(1) + ": " + s.col_text(2), tags = s.col_text(4);
+    const double r = score(content + " " + tags, s.col_blob(5));
+    if (r < min_rel || !top.wants(r)) {
+      top.skip();
+      continue;
+    }
+    top.push(r, Json::object({{"id", s.col_text(0)}, {"content", content},
+                              {"metadata_json", Json::object({{"source", s.col_text(3)}, {"tags", tags}}).dump()},
+                              {"relevance", r}, {"collection", "knowledge"}}));
   }
-  std::stable_sort(res.begin(), res.end(), [](auto& a, auto& b) { return a.first > b.first; });
-  Json out = Json::array();
-  for (size_t i = 0; i < res.size() && (int)i < limit; ++i) out.push(res[i].second);
-  return out;
+  return top.take();
 }
 
 // ---- context assembly

@@ -232,6 +232,28 @@ def test_longterm_semantic_search_and_migration(mem):
     assert st["procedures"] >= 2
 
 
+def test_search_top_n_matches_full_sort(mem):
+    """The scans keep only the n best rows; that must equal scoring every row (hybrid relevance from the
+    exported helpers) and stable-sorting them -- ties (the duplicated texts) keep scan order."""
+    texts = [f"{w} service on node {i % 7}" for i, w in enumerate(["nginx", "disk", "backup", "nginx logs"] * 12)]
+    for i, t in enumerate(texts):
+        mem.add_knowledge({"id": f"k{i:03d}", "title": t, "content": "runbook entry", "tags": []})
+    q = "nginx logs on node 3"
+    kws = q.split()
+    qe = c.hashed_embedding(q)
+    scored = []
+    for i, t in enumerate(texts):
+        content = f"{t}: runbook entry"
+        r = 0.4 * c.keyword_relevance(kws, content + " ") + 0.6 * c.cosine(qe, c.hashed_embedding(t + " runbook entry "))
+        scored.append((r, f"k{i:03d}"))
+    scored.sort(key=lambda x: -x[0])  # stable
+    for n in (1, 5, 13):
+        hits = mem.search_knowledge(q, n, 0.0)
+        assert [h["id"] for h in hits] == [k for _, k in scored[:n]]
+        assert all(abs(h["relevance"] - r) < 1e-6 for h, (r, _) in zip(hits, scored))
+    assert len(mem.search_knowledge(q, 5, 0.99)) == 0
+
+
 def test_memory_persists_across_reopen(tmp_path):
     paths = [str(tmp_path / n) for n in ("w.db", "lt.db", "kn.db")]
     m1 = c.MemoryStore(*paths)
