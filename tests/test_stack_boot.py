@@ -32,3 +32,18 @@ def test_stack_boots_and_accepts_a_goal():
     assert set(out["service_ready_s"]) == {"orchestrator", "tools", "memory", "api_gateway", "runtime"}
     assert out["boot_to_autonomy_s"] < 30 and out.get("tasks"), out
     assert _ports_free()  # the stack's process group was stopped
+
+
+def test_memory_tier_bench_runs():
+    """tools/bench_memory.py end to end at a small size: the daemon process over gRPC and the in-process
+    handlers both answer every RPC of the three tiers (latencies are the GPU box's record,
+    profiles/memory_tiers_r6.json; this machine's loopback is too noisy for the targets)."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "bench_memory.py"), "--calls", "5", "--entries", "20"],
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    for mode in ("rpc", "service"):
+        assert set(out[mode]) == {"operational", "working", "long-term"}
+        for tier in out[mode].values():
+            assert all(c["p50_ms"] > 0 for c in tier["calls"].values())
+    assert out["service"]["long-term"]["meets_target"]

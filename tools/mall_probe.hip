@@ -8,6 +8,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 
 #define CK(x)                                                                 \
   do {                                                                        \
@@ -51,7 +52,37 @@ static float run(bool nt, const f4* p, size_t bytes, float* out, hipEvent_t a, h
   return ms;
 }
 
-int main() {
+// --sol MB...: cold-cache single launches of the given sizes (flush, default-policy read, flush, nt read;
+// 5 reps), for a kernel trace to time: the one-launch streaming-read speed of light at the decode
+// matrices' sizes (rocprofv3 --kernel-trace; tools/sol_trace.py reads the trace)
+static int sol(int argc, char** argv) {
+  const size_t flush_bytes = (size_t)1 << 30;
+  f4 *buf, *flush;
+  float* out;
+  CK(hipMalloc(&buf, (size_t)320 << 20));
+  CK(hipMalloc(&flush, flush_bytes));
+  CK(hipMalloc(&out, 4096 * sizeof(float)));
+  CK(hipMemset(buf, 0, (size_t)320 << 20));
+  CK(hipMemset(flush, 0, flush_bytes));
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a));
+  CK(hipEventCreate(&b));
+  for (int i = 2; i < argc; ++i) {
+    const size_t bytes = ((size_t)(std::atof(argv[i]) * 1048576.0) + 4095) & ~(size_t)4095;
+    if (bytes > ((size_t)320 << 20)) return 2;
+    for (int rep = 0; rep < 5; ++rep) {
+      run(false, flush, flush_bytes, out, a, b);
+      run(false, buf, bytes, out, a, b);
+      run(false, flush, flush_bytes, out, a, b);
+      run(true, buf, bytes, out, a, b);
+    }
+    std::printf("%s MB: %zu bytes\n", argv[i], bytes);
+  }
+  return 0;
+}
+
+int main(int argc, char** argv) {
+  if (argc > 1 && std::string(argv[1]) == "--sol") return sol(argc, argv);
   const size_t flush_bytes = (size_t)1 << 30;
   const size_t sizes_mb[] = {8, 16, 32, 64, 96, 128, 192, 320};
   f4 *buf, *flush;
