@@ -18,6 +18,7 @@ import argparse
 import asyncio
 import json
 import os
+import shutil
 import socket
 import statistics
 import subprocess
@@ -155,7 +156,9 @@ async def over_rpc(args):
             proc.wait(timeout=20)
         except subprocess.TimeoutExpired:
             proc.kill()
+            proc.wait()
         await client.close_all()
+        shutil.rmtree(d, ignore_errors=True)
 
 
 async def in_process(args):
@@ -165,6 +168,8 @@ async def in_process(args):
         return await exercise(lambda name, req: getattr(svc, name)(req, None), args)
     finally:
         svc.pool.shutdown()
+        del svc
+        shutil.rmtree(d, ignore_errors=True)
 
 
 async def run(args):
