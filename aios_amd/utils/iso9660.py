@@ -89,7 +89,10 @@ def _scan(root: str):
                 sub = _Dir(e.path, name, d)
                 d.dirs.append(sub)
             elif e.is_file():
-                d.files.append((name, e.path, e.stat().st_size))
+                size = e.stat().st_size
+                if size >= 1 << 32:  # one extent per file (no level-3 multi-extent files)
+                    raise ValueError(f"{e.path}: {size} bytes does not fit one ISO 9660 extent (< 4 GiB)")
+                d.files.append((name, e.path, size))
         d.dirs.sort(key=lambda x: x.name)
         todo.extend(d.dirs)
     for i, d in enumerate(order):
