@@ -5,7 +5,7 @@
 //   2. load the boot-path modules shipped in /lib/modules (finit_module)
 //   3. find the boot medium: the block device whose filesystem label is AIOS (ISO 9660 volume id or ext4
 //      label), else the first NVMe partition; mount it read-only
-//   4. loop-mount /rootfs.squashfs from it, a tmpfs upper layer, overlay both at /newroot
+//   4. loop-mount /rootfs.squashfs (or /rootfs.ext4) from it, a tmpfs upper layer, overlay both at /newroot
 //   5. aios.<key>=<value> kernel parameters -> AIOS_<KEY>=<value> in the environment
 //   6. switch_root: move /newroot to /, chroot, exec /usr/sbin/aios-init (PID 1 stays PID 1)
 // aios.debug_shell=1 or any failure execs /bin/sh when the image has one, else powers off after a delay.
@@ -185,8 +185,15 @@ int main(int argc, char** argv) {
   if (do_mount(medium, "/mnt/medium", "iso9660", MS_RDONLY, NULL) != 0 &&
       do_mount(medium, "/mnt/medium", "ext4", MS_RDONLY, NULL) != 0)
     rescue();
-  if (loop_attach("/mnt/medium/rootfs.squashfs", loop, sizeof loop) != 0) rescue();
-  if (do_mount(loop, "/mnt/ro", "squashfs", MS_RDONLY, NULL) != 0) rescue();
+  // the root image: rootfs.squashfs, else an ext4 image (rootfs.ext4: what mkfs.ext4 -d packs on a
+  // build host without squashfs tools), mounted read-only either way
+  const char *img = "/mnt/medium/rootfs.squashfs", *img_fs = "squashfs";
+  if (!plan_only && access(img, F_OK) != 0) {
+    img = "/mnt/medium/rootfs.ext4";
+    img_fs = "ext4";
+  }
+  if (loop_attach(img, loop, sizeof loop) != 0) rescue();
+  if (do_mount(loop, "/mnt/ro", img_fs, MS_RDONLY, NULL) != 0) rescue();
   if (do_mount("tmpfs", "/mnt/rw", "tmpfs", 0, "mode=0755") != 0) rescue();
   if (!plan_only) {
     mkdir("/mnt/rw/upper", 0755);

@@ -43,7 +43,11 @@ for i in $(seq 1 30); do
 done
 [ -n "$dev" ] || dev=/dev/nvme0n1p1
 mount -o ro "$dev" /mnt/medium || exec sh
-mount -t squashfs -o loop,ro /mnt/medium/rootfs.squashfs /mnt/ro || exec sh
+if [ -f /mnt/medium/rootfs.squashfs ]; then
+  mount -t squashfs -o loop,ro /mnt/medium/rootfs.squashfs /mnt/ro || exec sh
+else
+  mount -t ext4 -o loop,ro /mnt/medium/rootfs.ext4 /mnt/ro || exec sh
+fi
 mount -t tmpfs tmpfs /mnt/rw; mkdir -p /mnt/rw/upper /mnt/rw/work
 mount -t overlay overlay -o lowerdir=/mnt/ro,upperdir=/mnt/rw/upper,workdir=/mnt/rw/work /newroot || exec sh
 grep -q aios.debug_shell=1 /proc/cmdline && exec sh

@@ -3,7 +3,7 @@
 #   scripts/build-iso.sh [--out build/distro] [--iso build/aios-mi355x.iso] [--data] [--dry-run]
 # Runs the kernel / rootfs / initramfs builds first when their outputs are missing.
 # --data (or no grub-mkrescue on PATH): a non-bootable data medium written by aios_amd.utils.iso9660 --
-# no root, no ISO tools -- holding whatever of vmlinuz / initramfs.img / rootfs.squashfs /
+# no root, no ISO tools -- holding whatever of vmlinuz / initramfs.img / rootfs.squashfs / rootfs.ext4 /
 # aios-overlay.ext4 exists (the initramfs is built offline when missing); volume id AIOS, so the early
 # init finds it; the kernel and initramfs are then started by an external loader (qemu -kernel/-initrd).
 set -euo pipefail
@@ -24,7 +24,7 @@ if [ "$DATA" = 1 ]; then
   run rm -rf "$S"
   run mkdir -p "$S/boot"
   for f in vmlinuz initramfs.img; do if [ -f "$OUT/$f" ]; then run cp "$OUT/$f" "$S/boot/$f"; fi; done
-  for f in rootfs.squashfs aios-overlay.ext4; do if [ -f "$OUT/$f" ]; then run cp "$OUT/$f" "$S/$f"; fi; done
+  for f in rootfs.squashfs rootfs.ext4 aios-overlay.ext4; do if [ -f "$OUT/$f" ]; then run cp "$OUT/$f" "$S/$f"; fi; done
   run env PYTHONPATH="$ROOT" "${PYTHON:-python3}" -m aios_amd.utils.iso9660 --root "$S" --out "$ISO" --volid AIOS
   echo "data iso -> $ISO"
   exit 0

@@ -4,17 +4,23 @@
 # aios_amd package and its prebuilt gfx950 extensions, aios-init as /usr/sbin/aios-init, the
 # node config, agent TOMLs, security policy, AppArmor profile and systemd-free boot.
 #   scripts/build-rootfs.sh [--out build/distro] [--rocm /opt/rocm] [--suite jammy] [--dry-run] [--overlay-only]
+#                           [--base DIR]
 # --overlay-only: only the aiOS layer (framework + built extensions, aios-init, configs, environment), no
 # debootstrap / chroot / root needed: staged under OUT/overlay and packed as an ext4 image (mkfs.ext4 -d,
 # label AIOS-OVL) to lay over any Ubuntu 22.04 + ROCm userland.
+# --base DIR: an existing userland tree (e.g. an exported Ubuntu 22.04 + ROCm-runtime container rootfs)
+# with the aiOS layer laid over it, packed as OUT/rootfs.ext4 (label AIOS-ROOT) -- the root image the
+# early init mounts when the medium has no squashfs; no debootstrap, chroot or root (files keep the
+# owners they have in DIR).
 set -euo pipefail
 ROOT="$(cd "$(dirname "$0")/.." && pwd)"
-OUT="$ROOT/build/distro"; ROCM="${ROCM_PATH:-/opt/rocm}"; SUITE="jammy"; DRY=0; OVL=0
+OUT="$ROOT/build/distro"; ROCM="${ROCM_PATH:-/opt/rocm}"; SUITE="jammy"; DRY=0; OVL=0; BASE=""
 MIRROR="${AIOS_APT_MIRROR:-http://archive.ubuntu.com/ubuntu}"
 while [ $# -gt 0 ]; do
   case "$1" in
     --out) OUT="$2"; shift ;; --rocm) ROCM="$2"; shift ;; --suite) SUITE="$2"; shift ;;
-    --dry-run) DRY=1 ;; --overlay-only) OVL=1 ;; *) echo "unknown option $1" >&2; exit 2 ;;
+    --dry-run) DRY=1 ;; --overlay-only) OVL=1 ;; --base) BASE="$2"; OVL=1; shift ;;
+    *) echo "unknown option $1" >&2; exit 2 ;;
   esac
   shift
 done
@@ -42,6 +48,20 @@ if [ "$OVL" = 1 ]; then
   run cp -a "$ROOT/deploy/etc/aios/." "$O/etc/aios/"
   run cp -a "$ROOT/deploy/etc/apparmor.d/." "$O/etc/apparmor.d/"
   if [ "$DRY" = 1 ]; then echo "+ write $O/etc/aios/environment"; else cat_env > "$O/etc/aios/environment"; fi
+  if [ -n "$BASE" ]; then
+    [ "$DRY" = 1 ] || [ -d "$BASE" ] || { echo "--base: $BASE is not a directory" >&2; exit 1; }
+    S="$OUT/rootfs-stage"
+    run rm -rf "$S"
+    run mkdir -p "$S"
+    run cp -a "$BASE/." "$S/"
+    run cp -a "$O/." "$S/"
+    SZ=$(( $(du -sm "$S" 2>/dev/null | cut -f1 || echo 64) * 5 / 4 + 64 ))
+    run rm -f "$OUT/rootfs.ext4"
+    run mkfs.ext4 -q -F -L AIOS-ROOT -d "$S" "$OUT/rootfs.ext4" "${SZ}M"
+    run rm -rf "$S"
+    echo "rootfs -> $OUT/rootfs.ext4"
+    exit 0
+  fi
   SZ=$(( $(du -sm "$O" 2>/dev/null | cut -f1 || echo 64) * 5 / 4 + 32 ))
   run rm -f "$OUT/aios-overlay.ext4"
   run mkfs.ext4 -q -F -L AIOS-OVL -d "$O" "$OUT/aios-overlay.ext4" "${SZ}M"

@@ -206,3 +206,40 @@ def test_data_medium_builds_offline(tmp_path):
     assert r.returncode == 0, r.stderr
     volid, files = read_iso(str(iso))
     assert volid == "AIOS" and files["boot/initramfs.img"] == (tmp_path / "initramfs.img").read_bytes()
+
+
+def test_root_image_from_base_tree_offline(tmp_path):
+    """scripts/build-rootfs.sh --base DIR: a userland tree with the aiOS layer over it, packed as rootfs.ext4
+    (the early init's root image when the medium has no squashfs), then put on the data medium"""
+    import shutil
+
+    from aios_amd.utils.iso9660 import read_iso
+
+    mkfs = shutil.which("mkfs.ext4") or ("/usr/sbin/mkfs.ext4" if os.path.exists("/usr/sbin/mkfs.ext4") else None)
+    if not mkfs or not shutil.which("gcc"):
+        pytest.skip("no mkfs.ext4 / C compiler")
+    base = tmp_path / "base"
+    (base / "bin").mkdir(parents=True)
+    (base / "etc").mkdir()
+    (base / "bin" / "sh").write_text("#!/bin/false\n")
+    (base / "etc" / "os-release").write_text('NAME="Ubuntu"\nVERSION_ID="22.04"\n')
+    env = dict(os.environ, PATH=os.environ.get("PATH", "") + ":/usr/sbin:/sbin")
+    out = tmp_path / "out"
+    r = subprocess.run(["bash", os.path.join(ROOT, "scripts", "build-rootfs.sh"), "--out", str(out), "--base", str(base)],
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr
+    img = out / "rootfs.ext4"
+    assert img.exists() and not (out / "rootfs-stage").exists()
+    debugfs = shutil.which("debugfs", path=env["PATH"])
+    if debugfs:
+        for path, want in (("/etc", "os-release"), ("/usr/sbin", "aios-init"), ("/etc/aios", "config.toml")):
+            ls = subprocess.run([debugfs, "-R", f"ls {path}", str(img)], capture_output=True, text=True)
+            assert want in ls.stdout, (path, ls.stdout)
+    iso = tmp_path / "aios.iso"
+    r = subprocess.run(["bash", os.path.join(ROOT, "scripts", "build-iso.sh"), "--data", "--out", str(out), "--iso", str(iso)],
+                       capture_output=True, text=True, timeout=300, env=env)
+    if r.returncode != 0 and "cannot find -lc" in r.stderr:
+        pytest.skip("no static libc")
+    assert r.returncode == 0, r.stderr
+    _, files = read_iso(str(iso))
+    assert files["rootfs.ext4"] == img.read_bytes() and "boot/initramfs.img" in files
