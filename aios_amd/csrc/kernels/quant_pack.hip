@@ -204,14 +204,33 @@ void launch_dequant_bf16(const QWeight& w, void* out, hipStream_t st) {
   hipLaunchKernelGGL(dequant_bf16_kernel, dim3(2048), dim3(256), 0, st, w, (bf16_t*)out);
 }
 
-// Raw (not repacked) legacy 32-blocks -> bf16 (Q4_1 / Q5_0 / Q5_1 / F32 matrices are expanded at
-// load time; they are not on any hot path of the named models).
+// Raw (not repacked) formats -> bf16 at load time: the legacy 32-blocks (Q4_1 / Q5_0 / Q5_1), F32, and the
+// 2- / 3-bit K-quants (Q2_K / Q3_K: Q2_K / Q3_K_M GGUFs run on the bf16 engines); none is on a hot path of
+// the named models.  Q2_K / Q3_K element j of a 256-block: its 2-bit field is at bits 2 ((j >> 5) & 3) of
+// quant byte 32 (j >> 7) + (j & 31), its scale is sub-block j >> 4, and (Q3_K) its high bit is bit j >> 5
+// of byte j & 31 (aios_amd/gguf/quants.py dequant_q2_k / dequant_q3_k are the host references).
 __global__ void legacy_to_bf16_kernel(int qt, const uint8_t* __restrict__ raw, size_t n, bf16_t* __restrict__ out) {
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
     const size_t b = i >> 5;
     const int j = (int)(i & 31);
     float v = 0.f;
-    if (qt == QT_F32) {
+    if (qt == QT_Q2_K || qt == QT_Q3_K) {
+      const int e = (int)(i & 255), sub = e >> 4;
+      const int q2 = (int)((qt == QT_Q2_K ? raw + (i >> 8) * 84 + 16 : raw + (i >> 8) * 110 + 32)[32 * (e >> 7) + (e & 31)] >>
+                           (2 * ((e >> 5) & 3))) & 3;
+      if (qt == QT_Q2_K) {
+        const uint8_t* s = raw + (i >> 8) * 84;
+        const float d = h2f(*(const uint16_t*)(s + 80)), dmin = h2f(*(const uint16_t*)(s + 82));
+        v = d * (float)(s[sub] & 0xF) * (float)q2 - dmin * (float)(s[sub] >> 4);
+      } else {
+        const uint8_t* s = raw + (i >> 8) * 110;
+        const int g = sub >> 2, k = sub & 3;
+        const int lo4 = (s[96 + ((g & 1) ? 4 : 0) + k] >> ((g & 2) ? 4 : 0)) & 0xF;
+        const int sc = (lo4 | (((s[104 + k] >> (2 * g)) & 3) << 4)) - 32;
+        const int hb = (s[e & 31] >> (e >> 5)) & 1;
+        v = h2f(*(const uint16_t*)(s + 108)) * (float)sc * (float)(q2 - (hb ? 0 : 4));
+      }
+    } else if (qt == QT_F32) {
       v = ((const float*)raw)[i];
     } else if (qt == QT_Q4_1) {
       const uint8_t* s = raw + b * 20;

@@ -47,6 +47,8 @@ BLOCK_INFO = {
     GGMLType.Q5_0: (32, 22),
     GGMLType.Q5_1: (32, 24),
     GGMLType.Q8_0: (32, 34),
+    GGMLType.Q2_K: (256, 84),
+    GGMLType.Q3_K: (256, 110),
     GGMLType.Q4_K: (256, 144),
     GGMLType.Q5_K: (256, 176),
     GGMLType.Q6_K: (256, 210),
@@ -128,6 +130,50 @@ def dequant_q8_0(raw) -> np.ndarray:
     d = _f16(b[:, 0:2]).reshape(-1, 1)
     q = b[:, 2:34].view(np.int8).astype(np.float32)
     return (q * d).astype(np.float32).ravel()
+
+
+def _kq_low2(qs: np.ndarray) -> np.ndarray:
+    """2-bit fields of the Q2_K / Q3_K quant bytes [nb, 64] -> [nb, 256] in element order: element
+    j = 128 n + 32 g + t sits in byte 32 n + t at bits 2 g."""
+    g = (2 * np.arange(4, dtype=np.uint8)).reshape(1, 1, 4, 1)
+    return ((qs.reshape(-1, 2, 1, 32) >> g) & 3).reshape(-1, 256).astype(np.int32)
+
+
+def dequant_q2_k(raw) -> np.ndarray:
+    """Q2_K: 16 (4-bit scale, 4-bit min) bytes, 64 bytes of 2-bit quants, f16 d, f16 dmin;
+    y = d * scale(j >> 4) * q - dmin * min(j >> 4)."""
+    b = _blocks(raw, GGMLType.Q2_K)
+    sc = b[:, :16].astype(np.int32)
+    d = _f16(b[:, 80:82]).reshape(-1, 1)
+    dmin = _f16(b[:, 82:84]).reshape(-1, 1)
+    q = _kq_low2(b[:, 16:80])
+    return (d * np.repeat(sc & 0xF, 16, axis=1) * q - dmin * np.repeat(sc >> 4, 16, axis=1)).astype(np.float32).ravel()
+
+
+def q3k_scales(scb: np.ndarray) -> np.ndarray:
+    """The 12-byte table of sixteen 6-bit Q3_K scales -> [nb, 16] signed (stored value - 32): scale s
+    (g = s >> 2, k = s & 3) has its low 4 bits in byte k (g even) or 4 + k (g odd), low or high nibble
+    for g < 2 / g >= 2, and its top 2 bits at bits 2 g of byte 8 + k."""
+    scb = scb.astype(np.int32)
+    out = np.empty((scb.shape[0], 16), np.int32)
+    for s_ in range(16):
+        g, k = s_ >> 2, s_ & 3
+        low = (scb[:, (4 if g & 1 else 0) + k] >> (4 if g & 2 else 0)) & 0xF
+        out[:, s_] = (low | (((scb[:, 8 + k] >> (2 * g)) & 3) << 4)) - 32
+    return out
+
+
+def dequant_q3_k(raw) -> np.ndarray:
+    """Q3_K: 32 bytes of high bits, 64 bytes of 2-bit quants, 12 bytes of 6-bit scales, f16 d;
+    y = d * scale(j >> 4) * (low2 - (high bit ? 0 : 4)), the high bit of element j at bit j >> 5 of
+    byte j & 31."""
+    b = _blocks(raw, GGMLType.Q3_K)
+    hm = b[:, :32]
+    low = _kq_low2(b[:, 32:96])
+    hb = ((hm.reshape(-1, 1, 32) >> np.arange(8, dtype=np.uint8).reshape(1, 8, 1)) & 1).reshape(-1, 256).astype(np.int32)
+    sc = np.repeat(q3k_scales(b[:, 96:108]), 16, axis=1)
+    d = _f16(b[:, 108:110]).reshape(-1, 1)
+    return (d * sc * (low - 4 * (1 - hb))).astype(np.float32).ravel()
 
 
 def kquant_scale_min(scales: np.ndarray):
@@ -244,6 +290,8 @@ DEQUANT = {
     GGMLType.Q5_0: dequant_q5_0,
     GGMLType.Q5_1: dequant_q5_1,
     GGMLType.Q8_0: dequant_q8_0,
+    GGMLType.Q2_K: dequant_q2_k,
+    GGMLType.Q3_K: dequant_q3_k,
     GGMLType.Q4_K: dequant_q4_k,
     GGMLType.Q5_K: dequant_q5_k,
     GGMLType.Q6_K: dequant_q6_k,
@@ -282,6 +330,93 @@ def quant_q8_0(x: np.ndarray) -> np.ndarray:
     inv = np.where(d != 0, 1.0 / np.where(d == 0, 1, d), 0.0).reshape(-1, 1)
     q = np.clip(np.round(x * inv), -127, 127).astype(np.int8)
     return np.concatenate([_to_f16_bytes(d), q.view(np.uint8)], axis=1).ravel()
+
+
+def _affine32(x: np.ndarray, nmax: int):
+    """x [nb, 32] -> (d, m f16-rounded [nb, 1], q [nb, 32] in 0..nmax): y = d * q + m."""
+    mn, mx = x.min(axis=1, keepdims=True), x.max(axis=1, keepdims=True)
+    d = ((mx - mn) / nmax).astype(np.float16).astype(np.float32)
+    m = mn.astype(np.float16).astype(np.float32)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        q = np.where(d > 0, np.round((x - m) / d), 0)
+    return d, m, q.clip(0, nmax).astype(np.int32)
+
+
+def _q5_pack(q: np.ndarray) -> np.ndarray:
+    """5-bit q [nb, 32] -> qh (bit i = high bit of element i, 4 bytes) + 16 nibble-pair bytes."""
+    qh = np.zeros(q.shape[0], np.uint32)
+    for i in range(32):
+        qh |= ((q[:, i] >> 4) & 1).astype(np.uint32) << np.uint32(i)
+    qs = ((q[:, :16] & 0xF) | ((q[:, 16:] & 0xF) << 4)).astype(np.uint8)
+    return np.concatenate([qh.reshape(-1, 1).view(np.uint8), qs], axis=1)
+
+
+def quant_q4_1(x: np.ndarray) -> np.ndarray:
+    d, m, q = _affine32(x.astype(np.float32).reshape(-1, 32), 15)
+    qs = (q[:, :16] | (q[:, 16:] << 4)).astype(np.uint8)
+    return np.concatenate([_to_f16_bytes(d), _to_f16_bytes(m), qs], axis=1).ravel()
+
+
+def quant_q5_0(x: np.ndarray) -> np.ndarray:
+    x = x.astype(np.float32).reshape(-1, 32)
+    mx = x[np.arange(x.shape[0]), np.argmax(np.abs(x), axis=1)]
+    d = (mx / -16.0).astype(np.float16).astype(np.float32)
+    inv = np.where(d != 0, 1.0 / np.where(d == 0, 1, d), 0.0).reshape(-1, 1)
+    q = np.clip(np.floor(x * inv + 16.5), 0, 31).astype(np.int32)
+    return np.concatenate([_to_f16_bytes(d), _q5_pack(q)], axis=1).ravel()
+
+
+def quant_q5_1(x: np.ndarray) -> np.ndarray:
+    d, m, q = _affine32(x.astype(np.float32).reshape(-1, 32), 31)
+    return np.concatenate([_to_f16_bytes(d), _to_f16_bytes(m), _q5_pack(q)], axis=1).ravel()
+
+
+def _kq_pack_low2(q: np.ndarray) -> np.ndarray:
+    """[nb, 256] values 0..3 -> the 64 quant bytes (inverse of _kq_low2)."""
+    q4 = q.reshape(-1, 2, 4, 32).astype(np.uint8)
+    out = np.zeros((q.shape[0], 2, 32), np.uint8)
+    for g in range(4):
+        out |= q4[:, :, g, :] << np.uint8(2 * g)
+    return out.reshape(-1, 64)
+
+
+def quant_q2_k(x: np.ndarray) -> np.ndarray:
+    x = x.astype(np.float32).reshape(-1, 16, 16)
+    lo = np.minimum(x.min(axis=2), 0.0)
+    scale, mins = (x.max(axis=2) - lo) / 3.0, -lo
+    d = (scale.max(axis=1) / 15.0).astype(np.float16).astype(np.float32)
+    dmin = (mins.max(axis=1) / 15.0).astype(np.float16).astype(np.float32)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        sc = np.where(d[:, None] > 0, np.round(scale / d[:, None]), 0).clip(0, 15).astype(np.int32)
+        mn = np.where(dmin[:, None] > 0, np.round(mins / dmin[:, None]), 0).clip(0, 15).astype(np.int32)
+        eff_d, eff_m = d[:, None] * sc, dmin[:, None] * mn
+        q = np.where(eff_d[..., None] > 0, np.round((x + eff_m[..., None]) / eff_d[..., None]), 0)
+    q = q.clip(0, 3).astype(np.int32).reshape(-1, 256)
+    return np.concatenate([(sc | (mn << 4)).astype(np.uint8), _kq_pack_low2(q), _to_f16_bytes(d),
+                           _to_f16_bytes(dmin)], axis=1).ravel()
+
+
+def quant_q3_k(x: np.ndarray) -> np.ndarray:
+    x = x.astype(np.float32).reshape(-1, 16, 16)
+    s_f = np.abs(x).max(axis=2) / 4.0
+    d = (s_f.max(axis=1) / 31.0).astype(np.float16).astype(np.float32)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        sc = np.where(d[:, None] > 0, np.round(s_f / d[:, None]), 0).clip(0, 31).astype(np.int32)
+        eff = d[:, None] * sc
+        q = np.where(eff[..., None] > 0, np.round(x / eff[..., None]), 0)
+    u = (q.clip(-4, 3) + 4).astype(np.int32).reshape(-1, 256)
+    nb = u.shape[0]
+    hm = np.zeros((nb, 32), np.uint8)
+    hbit = (u >> 2).reshape(nb, 8, 32).astype(np.uint8)
+    for bit in range(8):
+        hm |= hbit[:, bit, :] << np.uint8(bit)
+    v = sc + 32  # stored 6-bit scales
+    scb = np.zeros((nb, 12), np.int32)
+    for s_ in range(16):
+        g, k = s_ >> 2, s_ & 3
+        scb[:, (4 if g & 1 else 0) + k] |= (v[:, s_] & 0xF) << (4 if g & 2 else 0)
+        scb[:, 8 + k] |= (v[:, s_] >> 4) << (2 * g)
+    return np.concatenate([hm, _kq_pack_low2(u & 3), scb.astype(np.uint8), _to_f16_bytes(d)], axis=1).ravel()
 
 
 def _kquant_affine(x: np.ndarray, nmax: int):
@@ -376,7 +511,12 @@ QUANT = {
     GGMLType.F16: quant_f16,
     GGMLType.BF16: quant_bf16,
     GGMLType.Q4_0: quant_q4_0,
+    GGMLType.Q4_1: quant_q4_1,
+    GGMLType.Q5_0: quant_q5_0,
+    GGMLType.Q5_1: quant_q5_1,
     GGMLType.Q8_0: quant_q8_0,
+    GGMLType.Q2_K: quant_q2_k,
+    GGMLType.Q3_K: quant_q3_k,
     GGMLType.Q4_K: quant_q4_k,
     GGMLType.Q5_K: quant_q5_k,
     GGMLType.Q6_K: quant_q6_k,

@@ -16,7 +16,7 @@ pytestmark = pytest.mark.gpu
 def model_files(tmp_path_factory):
     d = tmp_path_factory.mktemp("eng")
     out = {}
-    for recipe in ("Q4_K_M", "Q4_0", "Q8_0", "BF16", "Q5_K_M"):
+    for recipe in ("Q4_K_M", "Q4_0", "Q8_0", "BF16", "Q5_K_M", "Q3_K_M", "Q2_K", "Q4_1", "Q5_0", "Q5_1"):
         out[recipe] = write_synthetic_gguf(str(d / f"small_{recipe}.gguf"), get_preset("test-small"), recipe, seed=7)
     out["mistral_shape"] = write_synthetic_gguf(str(d / "ms.gguf"), get_preset("test-mistral-shape"), "Q4_K_M", seed=9)
     return out
@@ -41,6 +41,27 @@ def test_prefill_logits_match_reference(model_files, recipe, q8):
     err = (logits - rl).abs().max().item()
     scale = rl.abs().max().item()
     assert err < 2e-2 * max(scale, 1.0), (err, scale)
+
+
+@pytest.mark.parametrize("recipe", ["Q3_K_M", "Q2_K", "Q4_1", "Q5_0", "Q5_1"])
+def test_load_time_expanded_formats_match_reference(model_files, recipe):
+    """Q2_K / Q3_K (and the legacy Q4_1 / Q5_0 / Q5_1) matrices are expanded to bf16 on the GPU at load
+    (quant_pack.hip legacy_to_bf16_kernel): prefill logits against the fp32 reference over the host
+    dequantisation of the same blocks (quants.py; the engine's copy is that, rounded to bf16), then a few
+    decode steps with finite logits"""
+    path = model_files[recipe]
+    eng, cfg = _load(path, act_q8=False)
+    ref = ReferenceModel.from_gguf(path, kv_bf16=True, act_q8=False)
+    prompt = [1] + list(np.random.default_rng(0).integers(3, cfg.vocab_size, 40))
+    logits = torch.from_numpy(np.asarray(eng.prefill(0, prompt, 0, True)))
+    rl = ref.forward(prompt)[-1]
+    err, scale = (logits - rl).abs().max().item(), rl.abs().max().item()
+    assert err < 2e-2 * max(scale, 1.0), (err, scale)
+    tok, pos = int(torch.argmax(logits)), len(prompt)
+    for _ in range(4):
+        tok = eng.decode([0], [tok], [pos])[0]
+        pos += 1
+        assert 0 <= tok < cfg.vocab_size
 
 
 @pytest.mark.parametrize("recipe", ["Q4_K_M", "BF16"])

@@ -5,9 +5,11 @@ import pytest
 from aios_amd.gguf.quants import (BLOCK_INFO, GGMLType, dequantize, kquant_pack_scale_min, kquant_scale_min,
                                   quantize, type_size)
 
-FORMATS = [GGMLType.Q4_0, GGMLType.Q8_0, GGMLType.Q4_K, GGMLType.Q5_K, GGMLType.Q6_K, GGMLType.F16, GGMLType.BF16]
+FORMATS = [GGMLType.Q4_0, GGMLType.Q8_0, GGMLType.Q4_K, GGMLType.Q5_K, GGMLType.Q6_K, GGMLType.F16, GGMLType.BF16,
+           GGMLType.Q4_1, GGMLType.Q5_0, GGMLType.Q5_1, GGMLType.Q2_K, GGMLType.Q3_K]
 TOL = {GGMLType.Q4_0: 0.2, GGMLType.Q8_0: 0.01, GGMLType.Q4_K: 0.12, GGMLType.Q5_K: 0.06, GGMLType.Q6_K: 0.03,
-       GGMLType.F16: 1e-3, GGMLType.BF16: 1e-2}
+       GGMLType.F16: 1e-3, GGMLType.BF16: 1e-2, GGMLType.Q4_1: 0.12, GGMLType.Q5_0: 0.06, GGMLType.Q5_1: 0.06,
+       GGMLType.Q2_K: 0.4, GGMLType.Q3_K: 0.22}
 
 
 @pytest.mark.parametrize("t", FORMATS)
@@ -73,3 +75,45 @@ def test_block_info_sizes():
     assert BLOCK_INFO[GGMLType.Q5_K] == (256, 176)
     assert BLOCK_INFO[GGMLType.Q8_0] == (32, 34)
     assert BLOCK_INFO[GGMLType.Q4_0] == (32, 18)
+
+
+def test_q2k_hand_block():
+    """Q2_K layout: 16 (scale | min << 4) bytes, 64 quant bytes (element j = 128 n + 32 g + t at bits 2 g of
+    byte 32 n + t), f16 d, f16 dmin; y = d * scale(j >> 4) * q - dmin * min(j >> 4).  (Parity with llama.cpp's
+    own files unpinned: no Q2_K fixture or independent decoder is available offline.)"""
+    sc = np.arange(16, dtype=np.uint8) % 15 + 1
+    mn = (np.arange(16, dtype=np.uint8) * 3) % 16
+    q = (np.arange(256) * 7 + 3) % 4
+    qs = np.zeros(64, np.uint8)
+    for j in range(256):
+        n, g, t = j >> 7, (j >> 5) & 3, j & 31
+        qs[32 * n + t] |= q[j] << (2 * g)
+    blk = np.concatenate([sc | (mn << 4), qs, np.array([0.5], np.float16).view(np.uint8),
+                          np.array([0.25], np.float16).view(np.uint8)])
+    y = dequantize(blk, GGMLType.Q2_K)
+    want = np.array([0.5 * sc[j >> 4] * q[j] - 0.25 * mn[j >> 4] for j in range(256)], np.float32)
+    np.testing.assert_array_equal(y, want)
+
+
+def test_q3k_hand_block():
+    """Q3_K layout: 32 high-bit bytes (bit j >> 5 of byte j & 31), 64 quant bytes (as Q2_K), twelve bytes of
+    sixteen 6-bit scales stored + 32 (low nibbles in bytes 0-7, top 2 bits in bytes 8-11), f16 d;
+    y = d * (scale - 32) * (low2 - (high ? 0 : 4)).  (Parity with llama.cpp's own files unpinned.)"""
+    from aios_amd.gguf.quants import q3k_scales
+
+    v = (np.arange(16) * 5 + 1) % 64  # stored 6-bit scales
+    scb = np.zeros(12, np.int64)
+    for s_ in range(16):
+        g, k = s_ >> 2, s_ & 3
+        scb[(4 if g & 1 else 0) + k] |= (v[s_] & 0xF) << (4 if g & 2 else 0)
+        scb[8 + k] |= (v[s_] >> 4) << (2 * g)
+    np.testing.assert_array_equal(q3k_scales(scb.astype(np.uint8).reshape(1, 12))[0], v - 32)
+    u = (np.arange(256) * 5 + 1) % 8  # value + 4
+    hm, qs = np.zeros(32, np.uint8), np.zeros(64, np.uint8)
+    for j in range(256):
+        hm[j & 31] |= (u[j] >> 2) << (j >> 5)
+        qs[32 * (j >> 7) + (j & 31)] |= (u[j] & 3) << (2 * ((j >> 5) & 3))
+    blk = np.concatenate([hm, qs, scb.astype(np.uint8), np.array([0.125], np.float16).view(np.uint8)])
+    y = dequantize(blk, GGMLType.Q3_K)
+    want = np.array([0.125 * (v[j >> 4] - 32) * (u[j] - 4) for j in range(256)], np.float32)
+    np.testing.assert_array_equal(y, want)
