@@ -40,6 +40,8 @@ enum QType : int {
   QT_Q4_K = 12,
   QT_Q5_K = 13,
   QT_Q6_K = 14,
+  QT_IQ4_NL = 20,  // load-time only, like Q2_K / Q3_K
+  QT_IQ4_XS = 23,
   QT_BF16 = 30,
 };
 

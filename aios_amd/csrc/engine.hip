@@ -35,7 +35,7 @@ static size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
 static bool is_kquant(int qt) { return qt == QT_Q4_K || qt == QT_Q5_K || qt == QT_Q6_K; }
 static int block_elems(int qt) {
-  if (is_kquant(qt) || qt == QT_Q2_K || qt == QT_Q3_K) return 256;
+  if (is_kquant(qt) || qt == QT_Q2_K || qt == QT_Q3_K || qt == QT_IQ4_XS) return 256;
   if (qt == QT_F32 || qt == QT_F16 || qt == QT_BF16) return 1;
   return 32;
 }
@@ -51,6 +51,8 @@ static int block_bytes(int qt) {
     case QT_Q8_0: return 34;
     case QT_Q2_K: return 84;
     case QT_Q3_K: return 110;
+    case QT_IQ4_NL: return 18;
+    case QT_IQ4_XS: return 136;
     case QT_F16:
     case QT_BF16: return 2;
     case QT_F32: return 4;

@@ -209,12 +209,27 @@ void launch_dequant_bf16(const QWeight& w, void* out, hipStream_t st) {
 // the named models.  Q2_K / Q3_K element j of a 256-block: its 2-bit field is at bits 2 ((j >> 5) & 3) of
 // quant byte 32 (j >> 7) + (j & 31), its scale is sub-block j >> 4, and (Q3_K) its high bit is bit j >> 5
 // of byte j & 31 (aios_amd/gguf/quants.py dequant_q2_k / dequant_q3_k are the host references).
+// IQ4_NL / IQ4_XS: 4-bit indices into these 16 levels, scaled by the block (IQ4_NL) or sub-block (IQ4_XS:
+// d x (6-bit scale - 32), low 4 bits in nibble ib & 1 of byte 4 + ib / 2, top 2 at bits 2 ib of the u16 at
+// byte 2) scale; the nibble order of a 32-element run is Q4_0's (quants.py dequant_iq4_nl / _xs)
+__constant__ int8_t kIq4Levels[16] = {-127, -104, -83, -65, -49, -35, -22, -10, 1, 13, 25, 38, 53, 69, 89, 113};
+
 __global__ void legacy_to_bf16_kernel(int qt, const uint8_t* __restrict__ raw, size_t n, bf16_t* __restrict__ out) {
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
     const size_t b = i >> 5;
     const int j = (int)(i & 31);
     float v = 0.f;
-    if (qt == QT_Q2_K || qt == QT_Q3_K) {
+    if (qt == QT_IQ4_NL) {
+      const uint8_t* s = raw + b * 18;
+      const uint8_t byte = s[2 + (j & 15)];
+      v = h2f(*(const uint16_t*)s) * (float)kIq4Levels[j < 16 ? (byte & 0xF) : (byte >> 4)];
+    } else if (qt == QT_IQ4_XS) {
+      const uint8_t* s = raw + (i >> 8) * 136;
+      const int e = (int)(i & 255), ib = e >> 5, t = e & 31;
+      const int ls = ((s[4 + (ib >> 1)] >> (4 * (ib & 1))) & 0xF) | (((*(const uint16_t*)(s + 2) >> (2 * ib)) & 3) << 4);
+      const uint8_t byte = s[8 + 16 * ib + (t & 15)];
+      v = h2f(*(const uint16_t*)s) * (float)(ls - 32) * (float)kIq4Levels[t < 16 ? (byte & 0xF) : (byte >> 4)];
+    } else if (qt == QT_Q2_K || qt == QT_Q3_K) {
       const int e = (int)(i & 255), sub = e >> 4;
       const int q2 = (int)((qt == QT_Q2_K ? raw + (i >> 8) * 84 + 16 : raw + (i >> 8) * 110 + 32)[32 * (e >> 7) + (e & 31)] >>
                            (2 * ((e >> 5) & 3))) & 3;

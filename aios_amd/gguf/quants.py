@@ -32,6 +32,8 @@ class GGMLType(enum.IntEnum):
     Q5_K = 13
     Q6_K = 14
     Q8_K = 15
+    IQ4_NL = 20
+    IQ4_XS = 23
     BF16 = 30
 
 
@@ -47,6 +49,8 @@ BLOCK_INFO = {
     GGMLType.Q5_0: (32, 22),
     GGMLType.Q5_1: (32, 24),
     GGMLType.Q8_0: (32, 34),
+    GGMLType.IQ4_NL: (32, 18),
+    GGMLType.IQ4_XS: (256, 136),
     GGMLType.Q2_K: (256, 84),
     GGMLType.Q3_K: (256, 110),
     GGMLType.Q4_K: (256, 144),
@@ -130,6 +134,38 @@ def dequant_q8_0(raw) -> np.ndarray:
     d = _f16(b[:, 0:2]).reshape(-1, 1)
     q = b[:, 2:34].view(np.int8).astype(np.float32)
     return (q * d).astype(np.float32).ravel()
+
+
+# the IQ4 formats' 16 non-linear levels (the public GGUF definition), scaled by the block's d
+IQ4_LEVELS = np.array([-127, -104, -83, -65, -49, -35, -22, -10, 1, 13, 25, 38, 53, 69, 89, 113], np.float32)
+
+
+def dequant_iq4_nl(raw) -> np.ndarray:
+    """IQ4_NL: f16 d, 16 bytes of 4-bit level indices (element j < 16: low nibble of byte j, j >= 16: high
+    nibble of byte j - 16, as Q4_0); y = d * level."""
+    b = _blocks(raw, GGMLType.IQ4_NL)
+    d = _f16(b[:, 0:2]).reshape(-1, 1)
+    qs = b[:, 2:18]
+    return (d * IQ4_LEVELS[np.concatenate([qs & 0xF, qs >> 4], axis=1)]).astype(np.float32).ravel()
+
+
+def iq4xs_scales(b: np.ndarray) -> np.ndarray:
+    """[nb, 136] IQ4_XS blocks -> [nb, 8] signed sub-block scales: 4 low bits from nibble (i & 1) of byte
+    4 + i // 2, 2 high bits at bits 2 i of the u16 at byte 2; stored value - 32."""
+    sh = np.ascontiguousarray(b[:, 2:4]).view(np.uint16).astype(np.int32).reshape(-1, 1)
+    i = np.arange(8)
+    lo = (b[:, 4 + i // 2].astype(np.int32) >> (4 * (i % 2))) & 0xF
+    return (lo | (((sh >> (2 * i)) & 3) << 4)) - 32
+
+
+def dequant_iq4_xs(raw) -> np.ndarray:
+    """IQ4_XS: f16 d, u16 high scale bits, 4 bytes of low scale nibbles, 128 bytes of level indices (eight
+    32-element sub-blocks, each laid out as an IQ4_NL block's nibbles); y = d * scale(j >> 5) * level."""
+    b = _blocks(raw, GGMLType.IQ4_XS)
+    d = _f16(b[:, 0:2]).reshape(-1, 1)
+    qs = b[:, 8:136].reshape(-1, 8, 16)
+    idx = np.concatenate([qs & 0xF, qs >> 4], axis=2).reshape(-1, 256)
+    return (d * np.repeat(iq4xs_scales(b), 32, axis=1) * IQ4_LEVELS[idx]).astype(np.float32).ravel()
 
 
 def _kq_low2(qs: np.ndarray) -> np.ndarray:
@@ -292,6 +328,8 @@ DEQUANT = {
     GGMLType.Q8_0: dequant_q8_0,
     GGMLType.Q2_K: dequant_q2_k,
     GGMLType.Q3_K: dequant_q3_k,
+    GGMLType.IQ4_NL: dequant_iq4_nl,
+    GGMLType.IQ4_XS: dequant_iq4_xs,
     GGMLType.Q4_K: dequant_q4_k,
     GGMLType.Q5_K: dequant_q5_k,
     GGMLType.Q6_K: dequant_q6_k,
@@ -369,6 +407,37 @@ def quant_q5_0(x: np.ndarray) -> np.ndarray:
 def quant_q5_1(x: np.ndarray) -> np.ndarray:
     d, m, q = _affine32(x.astype(np.float32).reshape(-1, 32), 31)
     return np.concatenate([_to_f16_bytes(d), _to_f16_bytes(m), _q5_pack(q)], axis=1).ravel()
+
+
+def _iq4_index(v: np.ndarray) -> np.ndarray:
+    """Nearest IQ4 level index of each value (in level units)."""
+    return np.abs(v[..., None] - IQ4_LEVELS).argmin(axis=-1).astype(np.uint8)
+
+
+def quant_iq4_nl(x: np.ndarray) -> np.ndarray:
+    x = x.astype(np.float32).reshape(-1, 32)
+    d = (np.abs(x).max(axis=1) / 127.0).astype(np.float16).astype(np.float32)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        q = _iq4_index(np.where(d[:, None] > 0, x / d[:, None], 0.0))
+    return np.concatenate([_to_f16_bytes(d), q[:, :16] | (q[:, 16:] << 4)], axis=1).ravel()
+
+
+def quant_iq4_xs(x: np.ndarray) -> np.ndarray:
+    x = x.astype(np.float32).reshape(-1, 8, 32)
+    s_f = np.abs(x).max(axis=2) / 127.0
+    d = (s_f.max(axis=1) / 31.0).astype(np.float16).astype(np.float32)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        ls = np.where(d[:, None] > 0, np.round(s_f / d[:, None]), 0).clip(0, 31).astype(np.int32)
+        dl = d[:, None] * ls
+        q = _iq4_index(np.where(dl[..., None] > 0, x / dl[..., None], 0.0))
+    v = ls + 32  # stored 6-bit scales
+    sh = np.zeros(x.shape[0], np.uint16)
+    sl = np.zeros((x.shape[0], 4), np.uint8)
+    for i in range(8):
+        sh |= ((v[:, i] >> 4) & 3).astype(np.uint16) << np.uint16(2 * i)
+        sl[:, i // 2] |= ((v[:, i] & 0xF) << (4 * (i % 2))).astype(np.uint8)
+    qs = (q[:, :, :16] | (q[:, :, 16:] << 4)).reshape(-1, 128)
+    return np.concatenate([_to_f16_bytes(d), sh.reshape(-1, 1).view(np.uint8), sl, qs], axis=1).ravel()
 
 
 def _kq_pack_low2(q: np.ndarray) -> np.ndarray:
@@ -517,6 +586,8 @@ QUANT = {
     GGMLType.Q8_0: quant_q8_0,
     GGMLType.Q2_K: quant_q2_k,
     GGMLType.Q3_K: quant_q3_k,
+    GGMLType.IQ4_NL: quant_iq4_nl,
+    GGMLType.IQ4_XS: quant_iq4_xs,
     GGMLType.Q4_K: quant_q4_k,
     GGMLType.Q5_K: quant_q5_k,
     GGMLType.Q6_K: quant_q6_k,

@@ -196,6 +196,8 @@ def tensor_type(recipe: str, name: str, layer: int, n_layers: int) -> GGMLType:
         if name.endswith("attn_v.weight") or name.endswith("ffn_down.weight"):
             return GGMLType.Q6_K if _use_more_bits(layer, n_layers) else GGMLType.Q5_K
         return GGMLType.Q5_K
+    if r in ("IQ4_NL", "IQ4_XS"):  # non-linear 4-bit levels (expanded to bf16 at load)
+        return GGMLType.Q6_K if name == "output.weight" else GGMLType[r]
     if r in ("Q4_1", "Q5_0", "Q5_1"):  # legacy 32-block files: expanded to bf16 at load
         return GGMLType.Q6_K if name == "output.weight" else GGMLType[r]
     if r == "Q3_K_M":  # 3-bit K-quant mix (expanded to bf16 at load, like Q2_K)

@@ -16,7 +16,7 @@ pytestmark = pytest.mark.gpu
 def model_files(tmp_path_factory):
     d = tmp_path_factory.mktemp("eng")
     out = {}
-    for recipe in ("Q4_K_M", "Q4_0", "Q8_0", "BF16", "Q5_K_M", "Q3_K_M", "Q2_K", "Q4_1", "Q5_0", "Q5_1"):
+    for recipe in ("Q4_K_M", "Q4_0", "Q8_0", "BF16", "Q5_K_M", "Q3_K_M", "Q2_K", "Q4_1", "Q5_0", "Q5_1", "IQ4_NL", "IQ4_XS"):
         out[recipe] = write_synthetic_gguf(str(d / f"small_{recipe}.gguf"), get_preset("test-small"), recipe, seed=7)
     out["mistral_shape"] = write_synthetic_gguf(str(d / "ms.gguf"), get_preset("test-mistral-shape"), "Q4_K_M", seed=9)
     return out
@@ -43,7 +43,7 @@ def test_prefill_logits_match_reference(model_files, recipe, q8):
     assert err < 2e-2 * max(scale, 1.0), (err, scale)
 
 
-@pytest.mark.parametrize("recipe", ["Q3_K_M", "Q2_K", "Q4_1", "Q5_0", "Q5_1"])
+@pytest.mark.parametrize("recipe", ["Q3_K_M", "Q2_K", "Q4_1", "Q5_0", "Q5_1", "IQ4_NL", "IQ4_XS"])
 def test_load_time_expanded_formats_match_reference(model_files, recipe):
     """Q2_K / Q3_K (and the legacy Q4_1 / Q5_0 / Q5_1) matrices are expanded to bf16 on the GPU at load
     (quant_pack.hip legacy_to_bf16_kernel): prefill logits against the fp32 reference over the host

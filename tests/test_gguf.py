@@ -54,7 +54,8 @@ def test_vocab_has_bytes_and_ascii():
     assert "{" in toks and '"' in toks and "▁the" in toks
 
 
-@pytest.mark.parametrize("recipe,tol", [("Q5_1", 0.08), ("Q5_0", 0.1), ("Q4_1", 0.15), ("Q3_K_M", 0.3), ("Q2_K", 0.5)])
+@pytest.mark.parametrize("recipe,tol", [("Q5_1", 0.08), ("Q5_0", 0.1), ("Q4_1", 0.15), ("Q3_K_M", 0.3), ("Q2_K", 0.5),
+                                        ("IQ4_NL", 0.15), ("IQ4_XS", 0.15)])
 def test_low_bit_and_legacy_recipes_run(tmp_path, recipe, tol):
     """GGUF files in the legacy 32-block formats and the 2- / 3-bit K-quant mixes (expanded to bf16 by the
     GPU loader; dequantised exactly by the CPU engine's reference forward): the same random weights as an

@@ -6,10 +6,11 @@ from aios_amd.gguf.quants import (BLOCK_INFO, GGMLType, dequantize, kquant_pack_
                                   quantize, type_size)
 
 FORMATS = [GGMLType.Q4_0, GGMLType.Q8_0, GGMLType.Q4_K, GGMLType.Q5_K, GGMLType.Q6_K, GGMLType.F16, GGMLType.BF16,
-           GGMLType.Q4_1, GGMLType.Q5_0, GGMLType.Q5_1, GGMLType.Q2_K, GGMLType.Q3_K]
+           GGMLType.Q4_1, GGMLType.Q5_0, GGMLType.Q5_1, GGMLType.Q2_K, GGMLType.Q3_K, GGMLType.IQ4_NL,
+           GGMLType.IQ4_XS]
 TOL = {GGMLType.Q4_0: 0.2, GGMLType.Q8_0: 0.01, GGMLType.Q4_K: 0.12, GGMLType.Q5_K: 0.06, GGMLType.Q6_K: 0.03,
        GGMLType.F16: 1e-3, GGMLType.BF16: 1e-2, GGMLType.Q4_1: 0.12, GGMLType.Q5_0: 0.06, GGMLType.Q5_1: 0.06,
-       GGMLType.Q2_K: 0.4, GGMLType.Q3_K: 0.22}
+       GGMLType.Q2_K: 0.4, GGMLType.Q3_K: 0.22, GGMLType.IQ4_NL: 0.12, GGMLType.IQ4_XS: 0.12}
 
 
 @pytest.mark.parametrize("t", FORMATS)
@@ -117,3 +118,26 @@ def test_q3k_hand_block():
     y = dequantize(blk, GGMLType.Q3_K)
     want = np.array([0.125 * (v[j >> 4] - 32) * (u[j] - 4) for j in range(256)], np.float32)
     np.testing.assert_array_equal(y, want)
+
+
+def test_iq4_hand_blocks():
+    """IQ4_NL (f16 d + Q4_0-ordered nibbles indexing 16 fixed levels) and IQ4_XS (eight 32-element runs of the
+    same, each scaled by d x (6-bit scale - 32): low nibbles in bytes 4-7, top bits in the u16 at byte 2).
+    (Parity with llama.cpp's own files unpinned.)"""
+    from aios_amd.gguf.quants import IQ4_LEVELS
+
+    idx = (np.arange(32) * 5 + 3) % 16
+    qs = (idx[:16] | (idx[16:] << 4)).astype(np.uint8)
+    y = dequantize(np.concatenate([np.array([0.5], np.float16).view(np.uint8), qs]), GGMLType.IQ4_NL)
+    np.testing.assert_array_equal(y, 0.5 * IQ4_LEVELS[idx])
+    v = (np.arange(8) * 9 + 5) % 64
+    sh = sum(int((v[i] >> 4) & 3) << (2 * i) for i in range(8))
+    sl = np.zeros(4, np.uint8)
+    for i in range(8):
+        sl[i // 2] |= (v[i] & 0xF) << (4 * (i % 2))
+    idx = (np.arange(256) * 7 + 1) % 16
+    q = idx.reshape(8, 32)
+    qs = (q[:, :16] | (q[:, 16:] << 4)).astype(np.uint8).ravel()
+    blk = np.concatenate([np.array([0.25], np.float16).view(np.uint8), np.array([sh], np.uint16).view(np.uint8), sl, qs])
+    y = dequantize(blk, GGMLType.IQ4_XS)
+    np.testing.assert_array_equal(y, (0.25 * np.repeat(v - 32, 32) * IQ4_LEVELS[idx]).astype(np.float32))
