@@ -380,6 +380,18 @@ void Engine::init_random(const std::string& recipe_in, uint64_t seed) {
     if (r == "Q8_0") return QT_Q8_0;
     if (r == "F16") return QT_F16;
     if (r == "BF16") return QT_BF16;
+    // recipes whose formats the loader expands to bf16 (Q2_K / Q3_K / IQ4 / legacy 32-blocks): in HBM
+    // their matrices ARE bf16, next to the native K-quants the mix keeps (models/config.py tensor_type)
+    if (r == "Q3_K_M") {
+      if (t == "output") return QT_Q6_K;
+      if (t == "attn_v" || t == "ffn_down") return more_bits(layer) ? QT_Q5_K : QT_Q4_K;
+      return t == "attn_output" ? QT_Q4_K : QT_BF16;
+    }
+    if (r == "Q2_K") {
+      if (t == "output") return QT_Q6_K;
+      return (t == "attn_v" || t == "ffn_down") && more_bits(layer) ? QT_Q4_K : QT_BF16;
+    }
+    if (r == "IQ4_NL" || r == "IQ4_XS" || r == "Q4_1" || r == "Q5_0" || r == "Q5_1") return t == "output" ? QT_Q6_K : QT_BF16;
     throw std::runtime_error("unknown recipe " + recipe_in);
   };
   uint64_t s = seed * 1000003ULL;
